@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Bench: edges aggregated/sec of the metapath-RGCN relational stack on MI355X.
+
+Workload (BASELINE.json configs[2]): FB15K-237-shaped graph, N = 14,541,
+R = 237, E = 310,116, 128-d features; the RGCN stack of model.py:Net (main_rgcn.py:547,
+L = 3: conv1 then the shared conv2 twice, ReLU after each) with 128-d hidden/output.
+
+One timed STEP = one forward pass of the 3 relational layers over the whole graph, inputs
+resident in HBM.  value = edges aggregated per second = 3 · E · steps / time (an edge
+aggregated = one (node_1, rel, node_2) edge folded into its (node_1, rel) segment in one
+layer).  With --gpus N (torchrun, one process per GPU) the graph is sharded by
+node_2 range (edge-balanced) and each layer's partial outputs are summed by an RCCL
+all-reduce over xGMI: total work is fixed, so "scaling" is "strong".
+
+Also reported (separate loops, outside the timed step): the training epoch of
+main_rgcn.py:458-461 — train step (forward + NLL + backward + Adam) + validation forward.
+
+roofline: the dominant kernel (seg_tile_kernel, forward) timed live with HIP events on its
+launch stream over the timed region; algorithmic FLOPs = 2·S·F_in·F_out per launch
+(segment contraction) against the dense fp32 MFMA peak (157.3 TFLOP/s); algorithmic bytes
+reported beside it.  traffic: HBM bytes per launch from rocprofv3 PMC counters
+(profiles/pmc_seg_fwd.json when present, else null).
+cpu_baseline: the CPU oracle (PyG-2.3.1 loop semantics, same ATen ops) timed on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import mpgnn_amd  # noqa: E402
+from mpgnn_amd import _lib, data  # noqa: E402
+from mpgnn_amd.distributed import shard_ranges  # noqa: E402
+
+METRIC = "edges aggregated/sec + epoch time, FB15K-237 128-d at 1/2/4/8 MI355X"
+PEAK_FP32_MFMA = 157.3  # TFLOP/s dense (MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32)
+PEAK_HBM = 8000.0       # GB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--layers", type=int, default=3)
+    ap.add_argument("--feat", type=int, default=128)
+    ap.add_argument("--epoch-steps", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-reps", type=int, default=2)
+    return ap.parse_args()
+
+
+def setup_dist(n):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n:
+        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        group = dist.group.WORLD
+    return rank, world, local, group
+
+
+def cpu_baseline(g, net_cpu, layers, reps):
+    """Oracle (CPU, all host threads torch uses) on the same graph: `reps` timed forwards of
+    the relational stack after one warm-up; edges/s = layers·E / median time."""
+    from oracle import rgcn_oracle as orc
+    params = {k: v.detach() for k, v in net_cpu.state_dict().items()}
+    x, ei, et = g.x, g.edge_index, g.edge_type
+
+    def fwd():
+        h = x
+        for layer in range(layers):
+            p = "conv1." if layer == 0 else "conv2."
+            h = torch.relu(orc.rgcn_forward(h, ei, et, params[p + "weight"], params[p + "root"],
+                                            params[p + "bias"]))
+        return h
+
+    with torch.no_grad():
+        fwd()
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fwd()
+            times.append(time.perf_counter() - t0)
+    times.sort()
+    med = times[len(times) // 2]
+    return {"value": layers * g.num_edges / med, "unit": "edges/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{reps} timed + 1 warm-up forward passes of the {layers}-layer RGCN stack on the full "
+                      f"FB15K-shaped graph (oracle/rgcn_oracle.py, PyG-2.3.1 loop: index_select/scatter_add_/"
+                      f"div/mm per relation); median {med * 1e3:.1f} ms"}
+
+
+def main():
+    args = parse()
+    rank, world, local, group = setup_dist(args.gpus)
+    dev = torch.device("cuda", local)
+    g = data.fb15k237_graph(feat_dim=args.feat, seed=0)
+    F = args.feat
+    torch.manual_seed(10)  # main_rgcn.py:31
+    net_cpu = mpgnn_amd.Net(F, F, g.num_relations, F, 2, args.layers)
+    net = mpgnn_amd.Net(F, F, g.num_relations, F, 2, args.layers)
+    net.load_state_dict(net_cpu.state_dict())
+    net = net.to(dev)
+    x, ei, et = g.x.to(dev), g.edge_index.to(dev), g.edge_type.to(dev)
+    shard = None
+    if world > 1:
+        shard = shard_ranges(g.edge_index, g.num_nodes, world)[rank]
+    convs = [net.conv1] + [net.conv2] * (args.layers - 1)
+
+    def step():
+        h = x
+        for conv in convs:
+            h = torch.relu(conv(h, ei, et, shard=shard, group=group))
+        return h
+
+    # plan (built once per graph, cached) + warm-up
+    with torch.no_grad():
+        for _ in range(max(args.warmup, 1)):
+            step()
+    torch.cuda.synchronize()
+    plan = mpgnn_amd.get_plan(ei, et, g.num_nodes, shard=shard, device=dev)
+
+    # ---- timed region: K forward steps --------------------------------------------------
+    _lib.lib.mpgnn_timing_reset()
+    _lib.lib.mpgnn_timing_enable(1)
+    if group is not None:
+        dist.barrier(group=group)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        for _ in range(args.steps):
+            step()
+    torch.cuda.synchronize()
+    if group is not None:
+        dist.barrier(group=group)
+    elapsed = time.perf_counter() - t0
+    _lib.lib.mpgnn_timing_enable(0)
+    seg_ms, seg_n = _lib.kernel_timing("seg_fwd")
+    row_ms, row_n = _lib.kernel_timing("row_fwd")
+    if group is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    edges_per_step = args.layers * g.num_edges
+    value = edges_per_step * args.steps / elapsed
+
+    # ---- epoch (main_rgcn.py:458-461): train fwd+bwd+Adam + validation forward ------------
+    opt = torch.optim.Adam(net.parameters(), lr=0.01, weight_decay=0.0005)
+    y = torch.randint(0, 2, (g.num_nodes,), generator=torch.Generator().manual_seed(0)).to(dev)
+    train_idx = torch.arange(0, g.num_nodes, 3, device=dev)
+
+    def epoch():
+        net.train()
+        opt.zero_grad()
+        out = net(x, ei, et, shard=shard, group=group)
+        loss = torch.nn.functional.nll_loss(out[train_idx], y[train_idx])
+        loss.backward()
+        opt.step()
+        net.eval()
+        with torch.no_grad():
+            net(x, ei, et, shard=shard, group=group)
+
+    for _ in range(2):
+        epoch()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.epoch_steps):
+        epoch()
+    torch.cuda.synchronize()
+    epoch_ms = (time.perf_counter() - t1) * 1e3 / args.epoch_steps
+
+    # ---- roofline of the dominant kernel (per launch, this rank) --------------------------
+    S = plan.num_segments
+    E_loc = plan.num_edges
+    seg_avg_ms = seg_ms / max(seg_n, 1)
+    flops = 2.0 * S * F * F
+    alg_bytes = E_loc * (4 * F + 4) + S * (16 + 4 * F)   # gathered rows + col idx; seg meta + Y write
+    achieved_tf = flops / (seg_avg_ms * 1e-3) / 1e12 if seg_n else None
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_seg_fwd.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("workload") == "fb15k237" and pmc.get("feat") == F and world == 1:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {
+        "bound": "mfma", "achieved": round(achieved_tf, 3) if achieved_tf else None, "peak": PEAK_FP32_MFMA,
+        "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_MFMA, 4) if achieved_tf else None,
+        "traffic": traffic, "kernel": "seg_tile_kernel (gather-mean + v_mfma_f32_32x32x2_f32)",
+        "avg_launch_us": round(seg_avg_ms * 1e3, 2), "launches": seg_n,
+        "alg_flops_per_launch": flops, "alg_bytes_per_launch": alg_bytes,
+        "alg_GBps": round(alg_bytes / (seg_avg_ms * 1e-3) / 1e9, 1) if seg_n else None,
+        "hbm_frac_if_streamed": round(alg_bytes / (seg_avg_ms * 1e-3) / 1e9 / PEAK_HBM, 4) if seg_n else None,
+        "row_kernel_avg_us": round(row_ms / max(row_n, 1) * 1e3, 2),
+    }
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(g, net_cpu, args.layers, args.cpu_reps)
+        result = {
+            "metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: FB15K-237-shaped graph (38,000 real dev+test triples + relation-conditional "
+                    "samples to E=310,116), U[0,1) features, seed-10 random-init weights",
+            "config": {"workload": "C3 FB15K-237 (N=14541, R=237, E=310116): RGCN Net stack forward, "
+                                   f"L={args.layers}, F_in=F_hidden=F_out={F}",
+                       "graph": {"nodes": g.num_nodes, "relations": g.num_relations, "edges": g.num_edges,
+                                 "segments": S if world == 1 else None},
+                       "parallelism": "single GPU" if world == 1 else f"dst-range shards x{world} + RCCL all-reduce"},
+            "epoch_ms": round(epoch_ms, 3),
+            "epoch_def": "main_rgcn.py:458-461 train (fwd+NLL+bwd+Adam) + validation forward",
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    if group is not None:
+        dist.barrier(group=group)
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,176 @@
+/*
+ * mpgnn_rgcn.h — C ABI of the MI355X (gfx950) relation-typed aggregation library.
+ *
+ * This is the drop-in boundary for the hot path of the reference
+ * (francescoferrini/MPGNN-Metapath-Graph-Neural-Network): the relation-masked
+ * mean aggregation + per-relation dense transform of
+ *   - CustomRGCNConv.forward      mp_rgcn_layer.py:158-271  ("mode SINGLE": one
+ *     relation per call, 2-D weight [F_in, F_out], used by MPNetm model.py:190,192)
+ *   - PyG RGCNConv.forward loop   ≙ mp_rgcn_layer.py:249-258 with weight [R, F_in, F_out]
+ *     ("mode ALL": relations 0..R-1, used by Net model.py:137-138)
+ * plus their autograd backward (implicit at main.py:1078 / main_rgcn.py:392).
+ *
+ * Conventions
+ *   - Every function returns int32_t status: 0 = ok, < 0 = mpgnn_status. No exception
+ *     crosses the ABI; mpgnn_last_error() returns a thread-local message.
+ *   - Graph tensors follow the reference loader (main.py:366-372):
+ *     edge_index int64 [2, E] row-major (row 0 = node_1, row 1 = node_2), edge_type int64 [E].
+ *     The plan is always built for flow='target_to_source' (model.py:137,190): rows of the
+ *     output are edge_index[0]; the gathered side is edge_index[1]. A caller that wants PyG's
+ *     default 'source_to_target' passes the two rows swapped.
+ *   - Feature/weight buffers are fp32, row-major, contiguous, 16-byte aligned DEVICE pointers
+ *     owned by the caller (PyTorch caching allocator). All kernels are enqueued on `stream`
+ *     (a hipStream_t passed as void*); no call synchronises the device except
+ *     mpgnn_plan_upload().
+ *   - Multi-GPU (dst-range sharding): a plan built with [shard_lo, shard_hi)
+ *     keeps only edges whose node_2 lies in the range, while per-(node_1, relation) counts
+ *     stay GLOBAL, so forward outputs of all shards sum (all-reduce) to the unsharded result.
+ *     The root/bias term is added only for output rows in [row_lo, row_hi).
+ */
+#ifndef MPGNN_RGCN_H
+#define MPGNN_RGCN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mpgnn_plan mpgnn_plan; /* opaque graph plan (segment tables) */
+
+enum mpgnn_status {
+    MPGNN_OK = 0,
+    MPGNN_ERR_ARG = -1,         /* bad shape / null pointer / bad mode */
+    MPGNN_ERR_INDEX = -2,       /* node index out of range (reference: index_select raises) */
+    MPGNN_ERR_HIP = -3,         /* HIP runtime error */
+    MPGNN_ERR_NOT_ON_DEVICE = -4, /* kernel called before mpgnn_plan_upload */
+    MPGNN_ERR_ALLOC = -5,       /* host or device allocation failed */
+    MPGNN_ERR_UNSUPPORTED = -6  /* feature width outside the compiled kernel range (1..256) */
+};
+
+enum mpgnn_mode {
+    MPGNN_MODE_SINGLE = 0, /* CustomRGCNConv: edges with edge_type == relation; weight [F_in, F_out] */
+    MPGNN_MODE_ALL = 1     /* RGCNConv: relations 0..num_relations-1; weight [R, F_in, F_out] */
+};
+
+/* Host tables exported by mpgnn_plan_export (tests compare them bit-exactly with the oracle). */
+enum mpgnn_table {
+    MPGNN_T_REL_VALUES = 0,  /* int64 [nrel]   sorted distinct relation ids                        */
+    MPGNN_T_REL_SEG_PTR = 1, /* int32 [nrel+1] segment range of each relation                      */
+    MPGNN_T_REL_EDGE_PTR = 2,/* int32 [nrel+1] edge range of each relation                         */
+    MPGNN_T_E_COL = 3,       /* int32 [E]      node_2 of each edge, relation-major order            */
+    MPGNN_T_E_ID = 4,        /* int32 [E]      original edge id of each edge, relation-major order  */
+    MPGNN_T_S_PTR = 5,       /* int32 [S+1]    edge range of each segment                           */
+    MPGNN_T_S_ROW = 6,       /* int32 [S]      node_1 of each segment                               */
+    MPGNN_T_S_REL = 7,       /* int32 [S]      relation id of each segment                          */
+    MPGNN_T_S_CNT = 8,       /* int32 [S]      GLOBAL edge count of (node_1, relation)              */
+    MPGNN_T_S_POS = 9,       /* int32 [S]      position of the segment in (node_1, relation) order  */
+    MPGNN_T_RW_PTR = 10,     /* int32 [N+1]    row-major segment range of each node_1               */
+    MPGNN_T_RW_SEG = 11,     /* int32 [S]      segment id at each row-major position                */
+    MPGNN_T_T_PTR = 12,      /* int32 [N+1]    edge range of each node_2 in (node_2, rel) order     */
+    MPGNN_T_T_SEG = 13,      /* int32 [E]      segment id of each edge in (node_2, rel) order       */
+    MPGNN_T_TA_COL = 14,     /* int32 [E]      node_2 of each edge in (rel, node_2) order           */
+    MPGNN_T_TA_SEG = 15,     /* int32 [E]      segment id of each edge in (rel, node_2) order       */
+    MPGNN_T_REL_INVALID = 16,/* uint8 [nrel]   1 if an edge of this relation had a bad node index   */
+    MPGNN_T_COUNT = 17
+};
+
+typedef struct mpgnn_plan_info {
+    int64_t num_nodes;      /* N                                         */
+    int64_t num_edges_in;   /* E given to plan_create                    */
+    int64_t num_edges;      /* local (shard) edges kept                  */
+    int64_t num_segments;   /* S = distinct local (node_1, relation)     */
+    int64_t num_relations;  /* distinct relation ids in edge_type        */
+    int64_t num_tiles;      /* 64-segment relation-pure tiles            */
+    int64_t num_chunks;     /* relation-pure reduction chunks (dW)       */
+    int64_t shard_lo, shard_hi;
+    int32_t device;         /* -1 until mpgnn_plan_upload                */
+    int32_t reserved;
+} mpgnn_plan_info;
+
+/* Build the segment tables on the host (O(E + N + R) counting sorts).
+ * Replaces the per-call `edge_type == r` compaction mp_rgcn_layer.py:29-35,231,251 and
+ * the index bookkeeping of PyG propagate (mp_rgcn_layer.py:236 / RGCNConv loop).
+ * edge_index/edge_type are HOST pointers. Edges whose node ids fall outside [0, N) are
+ * dropped and their relation is flagged invalid; kernels touching a flagged relation return
+ * MPGNN_ERR_INDEX (mirrors IndexError of x.index_select). */
+int32_t mpgnn_plan_create(const int64_t* edge_index, const int64_t* edge_type,
+                          int64_t num_edges, int64_t num_nodes,
+                          int64_t shard_lo, int64_t shard_hi, mpgnn_plan** out);
+int32_t mpgnn_plan_destroy(mpgnn_plan* plan);
+int32_t mpgnn_plan_get_info(const mpgnn_plan* plan, mpgnn_plan_info* info);
+/* Element count of an exported table, and a copy of it into host memory. */
+int32_t mpgnn_plan_table_size(const mpgnn_plan* plan, int32_t table, int64_t* elems, int32_t* elem_bytes);
+int32_t mpgnn_plan_export(const mpgnn_plan* plan, int32_t table, void* dst, int64_t capacity_bytes);
+/* Copy the tables to device `device` (synchronous; call once per graph). */
+int32_t mpgnn_plan_upload(mpgnn_plan* plan, int32_t device);
+
+/* Rows (segments) a mode/relation selects: [seg_begin, seg_end) in relation-major order. */
+int32_t mpgnn_plan_select(const mpgnn_plan* plan, int32_t mode, int64_t relation,
+                          int32_t num_relations, int64_t* seg_begin, int64_t* seg_end);
+
+const char* mpgnn_last_error(void);
+const char* mpgnn_status_string(int32_t status);
+int32_t mpgnn_abi_version(void);
+
+/* --- device entry points ------------------------------------------------------------ */
+
+/* Segment means h[s - seg_begin, :] = (Σ_{e in s} x[node_2(e), :]) / count(s), summed in
+ * original edge order from 0.0f: bit-identical to PyG 2.3.1 scatter(reduce='mean') as
+ * called by propagate at mp_rgcn_layer.py:236. h is [seg_end - seg_begin, F]. */
+int32_t mpgnn_rel_mean_fwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
+                           int32_t num_relations, const float* x, int32_t F, float* h,
+                           void* stream);
+
+/* Bytes of scratch the fwd/bwd calls need (caller allocates, e.g. torch.empty(uint8)). */
+int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* plan, int32_t mode, int64_t relation,
+                                   int32_t num_relations, int32_t F_in, int32_t F_out,
+                                   int64_t row_lo, int64_t row_hi, int64_t* bytes);
+
+/* Layer forward:  out = Σ_{r} mean_r(x) @ W_r  + x @ root + bias
+ *   (mode SINGLE: the single relation `relation`, W = weight [F_in, F_out];
+ *    mode ALL: r = 0..num_relations-1, W_r = weight[r] of [R, F_in, F_out]).
+ * root / bias may be NULL (root_weight=False / bias=False). out is [N, F_out].
+ * h_save (nullable) receives the segment means [seg_end - seg_begin, F_in] for backward. */
+int32_t mpgnn_rgcn_fwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
+                       int32_t num_relations, const float* x, int32_t F_in,
+                       const float* weight, const float* root, const float* bias,
+                       int32_t F_out, int64_t row_lo, int64_t row_hi, float* out,
+                       float* h_save, void* workspace, void* stream);
+
+/* Layer backward given grad_out [N, F_out] and the h_save of the forward.
+ * Any grad_* pointer may be NULL to skip that gradient.
+ *   grad_x      [N, F_in]           (= Σ_r A_rᵀ (grad_out W_rᵀ) + grad_out rootᵀ)
+ *   grad_weight [F_in, F_out] or [R, F_in, F_out]
+ *   grad_root   [F_in, F_out], grad_bias [F_out]  (rows [row_lo, row_hi) only) */
+int32_t mpgnn_rgcn_bwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
+                       int32_t num_relations, const float* x, int32_t F_in,
+                       const float* weight, const float* root, int32_t F_out,
+                       const float* h_save, const float* grad_out,
+                       int64_t row_lo, int64_t row_hi,
+                       float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
+                       void* workspace, void* stream);
+
+/* --- kernel timing (bench / profiling) ----------------------------------------------
+ * When enabled, every kernel launch of the entry points above is bracketed by a pair of
+ * hipEvents recorded on the launch stream; mpgnn_timing_query synchronises those events and
+ * returns the summed duration and the launch count of one kernel kind. */
+enum mpgnn_kernel_kind {
+    MPGNN_K_SEG_FWD = 0,   /* seg_tile_kernel: gather-mean + MFMA with W_r (forward)      */
+    MPGNN_K_ROW_FWD = 1,   /* row_tile_kernel: Σ_r Y + x@root + bias (forward)            */
+    MPGNN_K_SEG_DGRAD = 2, /* seg_tile_kernel: (dout @ W_rᵀ) / cnt (backward)             */
+    MPGNN_K_ROW_DX = 3,    /* row_tile_kernel: transposed gather-sum + dout @ rootᵀ       */
+    MPGNN_K_OUTER = 4,     /* outer_accum_kernel: dW / droot / dbias partial slabs        */
+    MPGNN_K_REDUCE = 5,    /* reduce_slabs_kernel                                         */
+    MPGNN_K_MEAN = 6,      /* seg_tile_kernel: segment means only (mpgnn_rel_mean_fwd)    */
+    MPGNN_K_COUNT = 7
+};
+int32_t mpgnn_timing_enable(int32_t on);
+int32_t mpgnn_timing_reset(void);
+int32_t mpgnn_timing_query(int32_t kernel_kind, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MPGNN_RGCN_H */

@@ -1,0 +1,109 @@
+"""ctypes binding of libmpgnn_rgcn.so (the C ABI declared in include/mpgnn_rgcn.h).
+
+The library is built in-tree by ``csrc/Makefile`` (``__graft_entry__.build()``). Importing
+this module without the library raises ImportError: there is no CPU fallback anywhere on the
+product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmpgnn_rgcn.so")
+
+MPGNN_OK = 0
+MPGNN_ERR_ARG = -1
+MPGNN_ERR_INDEX = -2
+MPGNN_ERR_HIP = -3
+MPGNN_ERR_NOT_ON_DEVICE = -4
+MPGNN_ERR_ALLOC = -5
+MPGNN_ERR_UNSUPPORTED = -6
+
+MODE_SINGLE = 0
+MODE_ALL = 1
+
+TABLES = {
+    "rel_values": (0, "int64"), "rel_seg_ptr": (1, "int32"), "rel_edge_ptr": (2, "int32"),
+    "e_col": (3, "int32"), "e_id": (4, "int32"), "s_ptr": (5, "int32"), "s_row": (6, "int32"),
+    "s_rel": (7, "int32"), "s_cnt": (8, "int32"), "s_pos": (9, "int32"), "rw_ptr": (10, "int32"),
+    "rw_seg": (11, "int32"), "t_ptr": (12, "int32"), "t_seg": (13, "int32"),
+    "ta_col": (14, "int32"), "ta_seg": (15, "int32"), "rel_invalid": (16, "uint8"),
+}
+
+
+class PlanInfo(ctypes.Structure):
+    _fields_ = [
+        ("num_nodes", ctypes.c_int64), ("num_edges_in", ctypes.c_int64),
+        ("num_edges", ctypes.c_int64), ("num_segments", ctypes.c_int64),
+        ("num_relations", ctypes.c_int64), ("num_tiles", ctypes.c_int64),
+        ("num_chunks", ctypes.c_int64), ("shard_lo", ctypes.c_int64),
+        ("shard_hi", ctypes.c_int64), ("device", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    ]
+
+
+# (name, restype, argtypes) — exactly the symbols of include/mpgnn_rgcn.h
+_P = ctypes.c_void_p
+_I32, _I64 = ctypes.c_int32, ctypes.c_int64
+_PI64 = ctypes.POINTER(ctypes.c_int64)
+SIGNATURES = [
+    ("mpgnn_plan_create", _I32, [_P, _P, _I64, _I64, _I64, _I64, ctypes.POINTER(_P)]),
+    ("mpgnn_plan_destroy", _I32, [_P]),
+    ("mpgnn_plan_get_info", _I32, [_P, ctypes.POINTER(PlanInfo)]),
+    ("mpgnn_plan_table_size", _I32, [_P, _I32, _PI64, ctypes.POINTER(_I32)]),
+    ("mpgnn_plan_export", _I32, [_P, _I32, _P, _I64]),
+    ("mpgnn_plan_upload", _I32, [_P, _I32]),
+    ("mpgnn_plan_select", _I32, [_P, _I32, _I64, _I32, _PI64, _PI64]),
+    ("mpgnn_last_error", ctypes.c_char_p, []),
+    ("mpgnn_status_string", ctypes.c_char_p, [_I32]),
+    ("mpgnn_abi_version", _I32, []),
+    ("mpgnn_rel_mean_fwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P]),
+    ("mpgnn_rgcn_workspace_bytes", _I32, [_P, _I32, _I64, _I32, _I32, _I32, _I64, _I64, _PI64]),
+    ("mpgnn_rgcn_fwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _I64, _I64,
+                              _P, _P, _P, _P]),
+    ("mpgnn_rgcn_bwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _I32, _P, _P, _I64, _I64,
+                              _P, _P, _P, _P, _P, _P]),
+    ("mpgnn_timing_enable", _I32, [_I32]),
+    ("mpgnn_timing_reset", _I32, []),
+    ("mpgnn_timing_query", _I32, [_I32, ctypes.POINTER(ctypes.c_double), _PI64]),
+]
+
+KERNEL_KINDS = {"seg_fwd": 0, "row_fwd": 1, "seg_dgrad": 2, "row_dx": 3, "outer": 4, "reduce": 5, "mean": 6}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `make -C csrc` or __graft_entry__.build(). "
+            "mpgnn_amd has no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def kernel_timing(kind: str) -> tuple[float, int]:
+    """(total ms, launches) of one kernel kind since mpgnn_timing_reset (syncs its events)."""
+    ms, n = ctypes.c_double(), ctypes.c_int64()
+    check(lib.mpgnn_timing_query(KERNEL_KINDS[kind], ctypes.byref(ms), ctypes.byref(n)), "mpgnn_timing_query")
+    return float(ms.value), int(n.value)
+
+
+def check(status: int, what: str = "") -> None:
+    """Map a C status to the exception the reference raises for the same condition."""
+    if status == MPGNN_OK:
+        return
+    msg = lib.mpgnn_last_error().decode(errors="replace")
+    text = f"{what}: {msg}" if what else msg
+    if status == MPGNN_ERR_INDEX:
+        raise IndexError(text)  # reference: x.index_select / scatter_add_ with a bad index
+    if status == MPGNN_ERR_ARG:
+        raise ValueError(text)
+    if status == MPGNN_ERR_UNSUPPORTED:
+        raise NotImplementedError(text)
+    raise RuntimeError(text)

@@ -1,0 +1,424 @@
+// plan.cpp — host-side graph plan builder (segment tables) for the relation-typed SpMM.
+//
+// The reference recomputes, on every call and for every relation, the boolean compaction
+// `edge_index[:, edge_type == r]` (mp_rgcn_layer.py:29-35, called at :231 for one relation
+// and once per relation in the RGCNConv loop ≙ :250-251), then lets PyG gather
+// x[edge_index[1]] and scatter-add into edge_index[0] (flow='target_to_source',
+// model.py:137,190). Here the graph is sorted ONCE into tables that make every later pass a
+// contiguous, order-preserving walk:
+//
+//   relation-major edges   stable sort by (relation, node_1)    -> segments (node_1, relation)
+//   row-major segments     stable sort of segments by node_1    -> combine pass (sum over r)
+//   col-major edges        stable sort by (node_2, relation)    -> grad_x (transposed SpMM)
+//   relation/col edges     stable sort by (relation, node_2)    -> grad_x for one relation
+//
+// All sorts are stable counting sorts, O(E + N + R). Within a segment the edges keep their
+// original order, which is what makes the GPU segment sums bit-identical to ATen's
+// sequential scatter_add_ (SURVEY §8c "Determinism facts").
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstring>
+#include <limits>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "plan_internal.h"
+
+namespace mpgnn {
+
+static thread_local std::string g_last_error;
+
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+static int32_t fail(int32_t code, const std::string& msg) {
+    set_last_error(msg);
+    return code;
+}
+
+int32_t select_relations(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R,
+                         int64_t* d_lo, int64_t* d_hi) {
+    const auto& rv = p->rel_values;
+    if (mode == MPGNN_MODE_SINGLE) {
+        auto it = std::lower_bound(rv.begin(), rv.end(), relation);
+        int64_t d = it - rv.begin();
+        if (it == rv.end() || *it != relation) {  // relation absent: empty mask (no error)
+            *d_lo = *d_hi = d;
+            return MPGNN_OK;
+        }
+        if (p->rel_invalid[d])
+            return fail(MPGNN_ERR_INDEX, "edge of relation " + std::to_string(relation) +
+                                             " has a node index out of range [0, N)");
+        *d_lo = d;
+        *d_hi = d + 1;
+        return MPGNN_OK;
+    }
+    if (mode == MPGNN_MODE_ALL) {
+        if (R < 0) return fail(MPGNN_ERR_ARG, "num_relations must be >= 0");
+        int64_t lo = std::lower_bound(rv.begin(), rv.end(), (int64_t)0) - rv.begin();
+        int64_t hi = std::lower_bound(rv.begin(), rv.end(), (int64_t)R) - rv.begin();
+        for (int64_t d = lo; d < hi; ++d)
+            if (p->rel_invalid[d])
+                return fail(MPGNN_ERR_INDEX, "edge of relation " + std::to_string(rv[d]) +
+                                                 " has a node index out of range [0, N)");
+        *d_lo = lo;
+        *d_hi = hi;
+        return MPGNN_OK;
+    }
+    return fail(MPGNN_ERR_ARG, "unknown mode " + std::to_string(mode));
+}
+
+// Stable counting sort of `items` by key(item) in [0, nkeys). Returns the bucket pointers.
+template <class KeyFn>
+static void counting_sort(const std::vector<int32_t>& items, int64_t nkeys, KeyFn key,
+                          std::vector<int32_t>& out, std::vector<int32_t>* ptr_out) {
+    std::vector<int32_t> ptr(nkeys + 1, 0);
+    for (int32_t it : items) ptr[key(it) + 1]++;
+    for (int64_t k = 0; k < nkeys; ++k) ptr[k + 1] += ptr[k];
+    out.assign(items.size(), 0);
+    std::vector<int32_t> cur(ptr.begin(), ptr.end() - 1);
+    for (int32_t it : items) out[cur[key(it)]++] = it;
+    if (ptr_out) ptr_out->swap(ptr);
+}
+
+static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N, int64_t lo,
+                     int64_t hi, mpgnn_plan* p) {
+    const int64_t* n1 = ei;
+    const int64_t* n2 = ei + E;
+    p->N = N;
+    p->E_in = E;
+    p->shard_lo = lo;
+    p->shard_hi = hi;
+
+    // ---- dense relation ids (sorted distinct values of edge_type) ----------------------
+    std::vector<int32_t> rel_d(E);
+    if (E > 0) {
+        int64_t mn = et[0], mx = et[0];
+        for (int64_t e = 1; e < E; ++e) {
+            mn = std::min(mn, et[e]);
+            mx = std::max(mx, et[e]);
+        }
+        const unsigned long long span = (unsigned long long)mx - (unsigned long long)mn;
+        if (span < (unsigned long long)(4 * E + 4096)) {
+            std::vector<int32_t> map(span + 1, -1);
+            for (int64_t e = 0; e < E; ++e) map[et[e] - mn] = 0;
+            int32_t nd = 0;
+            for (size_t v = 0; v <= span; ++v)
+                if (map[v] == 0) {
+                    map[v] = nd++;
+                    p->rel_values.push_back(mn + (int64_t)v);
+                }
+            for (int64_t e = 0; e < E; ++e) rel_d[e] = map[et[e] - mn];
+        } else {
+            std::vector<int64_t> vals(et, et + E);
+            std::sort(vals.begin(), vals.end());
+            vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+            p->rel_values = vals;
+            for (int64_t e = 0; e < E; ++e)
+                rel_d[e] = (int32_t)(std::lower_bound(vals.begin(), vals.end(), et[e]) - vals.begin());
+        }
+    }
+    const int64_t R = (int64_t)p->rel_values.size();
+    p->nrel = R;
+    p->rel_invalid.assign(R, 0);
+    p->rel_val32.resize(R);
+    for (int64_t d = 0; d < R; ++d) {
+        int64_t v = p->rel_values[d];
+        p->rel_val32[d] = (v >= 0 && v <= std::numeric_limits<int32_t>::max()) ? (int32_t)v : -1;
+    }
+
+    // ---- valid edges, global (relation, node_1, edge) order ------------------------------
+    std::vector<int32_t> valid;
+    valid.reserve(E);
+    for (int64_t e = 0; e < E; ++e) {
+        if (n1[e] < 0 || n1[e] >= N || n2[e] < 0 || n2[e] >= N) {
+            p->rel_invalid[rel_d[e]] = 1;
+            continue;
+        }
+        valid.push_back((int32_t)e);
+    }
+    std::vector<int32_t> by_row, by_rel_row;
+    counting_sort(valid, N, [&](int32_t e) { return (int64_t)n1[e]; }, by_row, nullptr);
+    counting_sort(by_row, R, [&](int32_t e) { return (int64_t)rel_d[e]; }, by_rel_row, nullptr);
+
+    // ---- segments: runs of equal (relation, node_1); keep those with a local edge --------
+    p->rel_seg_ptr.assign(R + 1, 0);
+    p->rel_edge_ptr.assign(R + 1, 0);
+    p->s_ptr.push_back(0);
+    const int64_t V = (int64_t)by_rel_row.size();
+    std::vector<int32_t> seg_of_edge;  // segment id of each local edge (relation-major order)
+    for (int64_t a = 0; a < V;) {
+        const int32_t e0 = by_rel_row[a];
+        const int32_t d = rel_d[e0];
+        const int64_t row = n1[e0];
+        int64_t b = a + 1;
+        while (b < V && rel_d[by_rel_row[b]] == d && n1[by_rel_row[b]] == row) ++b;
+        const int32_t cnt = (int32_t)(b - a);  // GLOBAL count of (row, relation)
+        bool any_local = false;
+        for (int64_t k = a; k < b; ++k) {
+            const int32_t e = by_rel_row[k];
+            if (n2[e] >= lo && n2[e] < hi) {
+                p->e_col.push_back((int32_t)n2[e]);
+                p->e_id.push_back(e);
+                seg_of_edge.push_back((int32_t)p->s_row.size());
+                any_local = true;
+            }
+        }
+        if (any_local) {
+            p->s_row.push_back((int32_t)row);
+            p->s_rel.push_back(p->rel_val32[d]);
+            p->s_cnt.push_back(cnt);
+            p->s_ptr.push_back((int32_t)p->e_col.size());
+            p->rel_seg_ptr[d + 1]++;
+        }
+        a = b;
+    }
+    p->E = (int64_t)p->e_col.size();
+    p->S = (int64_t)p->s_row.size();
+    for (int64_t d = 0; d < R; ++d) p->rel_seg_ptr[d + 1] += p->rel_seg_ptr[d];
+    for (int64_t d = 0; d < R; ++d)
+        p->rel_edge_ptr[d + 1] = p->s_ptr[p->rel_seg_ptr[d + 1]];
+
+    // dense relation of each segment (segments are relation-major)
+    std::vector<int32_t> seg_d(p->S);
+    for (int64_t d = 0; d < R; ++d)
+        for (int32_t s = p->rel_seg_ptr[d]; s < p->rel_seg_ptr[d + 1]; ++s) seg_d[s] = (int32_t)d;
+
+    // ---- row-major segment order (node_1, relation) -------------------------------------
+    {
+        std::vector<int32_t> segs(p->S);
+        for (int64_t s = 0; s < p->S; ++s) segs[s] = (int32_t)s;
+        counting_sort(segs, N, [&](int32_t s) { return (int64_t)p->s_row[s]; }, p->rw_seg, &p->rw_ptr);
+        p->s_pos.assign(p->S, 0);
+        for (int64_t q = 0; q < p->S; ++q) p->s_pos[p->rw_seg[q]] = (int32_t)q;
+    }
+
+    // ---- transposed orders for grad_x ---------------------------------------------------
+    {
+        std::vector<int32_t> edges(p->E);
+        for (int64_t k = 0; k < p->E; ++k) edges[k] = (int32_t)k;
+        std::vector<int32_t> by_col;  // (node_2, relation, node_1, edge)
+        counting_sort(edges, N, [&](int32_t k) { return (int64_t)p->e_col[k]; }, by_col, &p->t_ptr);
+        p->t_seg.resize(p->E);
+        for (int64_t q = 0; q < p->E; ++q) p->t_seg[q] = seg_of_edge[by_col[q]];
+        std::vector<int32_t> by_rel_col;  // (relation, node_2, node_1, edge)
+        counting_sort(by_col, R, [&](int32_t k) { return (int64_t)seg_d[seg_of_edge[k]]; }, by_rel_col, nullptr);
+        p->ta_col.resize(p->E);
+        p->ta_seg.resize(p->E);
+        for (int64_t q = 0; q < p->E; ++q) {
+            p->ta_col[q] = p->e_col[by_rel_col[q]];
+            p->ta_seg[q] = seg_of_edge[by_rel_col[q]];
+        }
+    }
+
+    // ---- relation-pure tiles and reduction chunks --------------------------------------
+    p->rel_tile_ptr.assign(R + 1, 0);
+    p->rel_chunk_ptr.assign(R + 1, 0);
+    for (int64_t d = 0; d < R; ++d) {
+        for (int32_t s = p->rel_seg_ptr[d]; s < p->rel_seg_ptr[d + 1]; s += kTileRows) {
+            p->tile_begin.push_back(s);
+            p->tile_end.push_back(std::min<int32_t>(s + kTileRows, p->rel_seg_ptr[d + 1]));
+        }
+        p->rel_tile_ptr[d + 1] = (int32_t)p->tile_begin.size();
+        for (int32_t s = p->rel_seg_ptr[d]; s < p->rel_seg_ptr[d + 1]; s += kChunkRows) {
+            p->chunk_begin.push_back(s);
+            p->chunk_end.push_back(std::min<int32_t>(s + kChunkRows, p->rel_seg_ptr[d + 1]));
+        }
+        p->rel_chunk_ptr[d + 1] = (int32_t)p->chunk_begin.size();
+    }
+    return MPGNN_OK;
+}
+
+}  // namespace mpgnn
+
+using namespace mpgnn;
+
+extern "C" {
+
+int32_t mpgnn_abi_version(void) { return 1; }
+
+const char* mpgnn_last_error(void) { return g_last_error.c_str(); }
+
+const char* mpgnn_status_string(int32_t s) {
+    switch (s) {
+        case MPGNN_OK: return "ok";
+        case MPGNN_ERR_ARG: return "invalid argument";
+        case MPGNN_ERR_INDEX: return "index out of range";
+        case MPGNN_ERR_HIP: return "HIP runtime error";
+        case MPGNN_ERR_NOT_ON_DEVICE: return "plan not uploaded to a device";
+        case MPGNN_ERR_ALLOC: return "allocation failed";
+        case MPGNN_ERR_UNSUPPORTED: return "unsupported feature width";
+        default: return "unknown status";
+    }
+}
+
+int32_t mpgnn_plan_create(const int64_t* edge_index, const int64_t* edge_type, int64_t num_edges,
+                          int64_t num_nodes, int64_t shard_lo, int64_t shard_hi, mpgnn_plan** out) {
+    if (!out) return fail(MPGNN_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (num_edges < 0 || num_nodes < 0) return fail(MPGNN_ERR_ARG, "negative size");
+    if (num_edges > 0 && (!edge_index || !edge_type)) return fail(MPGNN_ERR_ARG, "edge arrays are NULL");
+    if (num_edges >= (int64_t)std::numeric_limits<int32_t>::max() ||
+        num_nodes >= (int64_t)std::numeric_limits<int32_t>::max())
+        return fail(MPGNN_ERR_UNSUPPORTED, "graph exceeds int32 index range");
+    shard_lo = std::max<int64_t>(0, shard_lo);
+    shard_hi = std::min<int64_t>(num_nodes, shard_hi);
+    if (shard_hi < shard_lo) shard_hi = shard_lo;
+    mpgnn_plan* p = new (std::nothrow) mpgnn_plan();
+    if (!p) return fail(MPGNN_ERR_ALLOC, "plan allocation failed");
+    try {
+        int32_t st = build(edge_index, edge_type, num_edges, num_nodes, shard_lo, shard_hi, p);
+        if (st != MPGNN_OK) {
+            delete p;
+            return st;
+        }
+    } catch (const std::bad_alloc&) {
+        delete p;
+        return fail(MPGNN_ERR_ALLOC, "host allocation failed while building the plan");
+    }
+    *out = p;
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_plan_destroy(mpgnn_plan* p) {
+    if (!p) return MPGNN_OK;
+    if (p->d.block) {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(p->device);
+        (void)hipFree(p->d.block);
+        (void)hipSetDevice(prev);
+    }
+    delete p;
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_plan_get_info(const mpgnn_plan* p, mpgnn_plan_info* info) {
+    if (!p || !info) return fail(MPGNN_ERR_ARG, "NULL argument");
+    std::memset(info, 0, sizeof(*info));
+    info->num_nodes = p->N;
+    info->num_edges_in = p->E_in;
+    info->num_edges = p->E;
+    info->num_segments = p->S;
+    info->num_relations = p->nrel;
+    info->num_tiles = (int64_t)p->tile_begin.size();
+    info->num_chunks = (int64_t)p->chunk_begin.size();
+    info->shard_lo = p->shard_lo;
+    info->shard_hi = p->shard_hi;
+    info->device = p->device;
+    return MPGNN_OK;
+}
+
+static const void* table_ptr(const mpgnn_plan* p, int32_t t, int64_t* n, int32_t* eb) {
+    *eb = 4;
+    switch (t) {
+        case MPGNN_T_REL_VALUES: *eb = 8; *n = (int64_t)p->rel_values.size(); return p->rel_values.data();
+        case MPGNN_T_REL_SEG_PTR: *n = (int64_t)p->rel_seg_ptr.size(); return p->rel_seg_ptr.data();
+        case MPGNN_T_REL_EDGE_PTR: *n = (int64_t)p->rel_edge_ptr.size(); return p->rel_edge_ptr.data();
+        case MPGNN_T_E_COL: *n = (int64_t)p->e_col.size(); return p->e_col.data();
+        case MPGNN_T_E_ID: *n = (int64_t)p->e_id.size(); return p->e_id.data();
+        case MPGNN_T_S_PTR: *n = (int64_t)p->s_ptr.size(); return p->s_ptr.data();
+        case MPGNN_T_S_ROW: *n = (int64_t)p->s_row.size(); return p->s_row.data();
+        case MPGNN_T_S_REL: *n = (int64_t)p->s_rel.size(); return p->s_rel.data();
+        case MPGNN_T_S_CNT: *n = (int64_t)p->s_cnt.size(); return p->s_cnt.data();
+        case MPGNN_T_S_POS: *n = (int64_t)p->s_pos.size(); return p->s_pos.data();
+        case MPGNN_T_RW_PTR: *n = (int64_t)p->rw_ptr.size(); return p->rw_ptr.data();
+        case MPGNN_T_RW_SEG: *n = (int64_t)p->rw_seg.size(); return p->rw_seg.data();
+        case MPGNN_T_T_PTR: *n = (int64_t)p->t_ptr.size(); return p->t_ptr.data();
+        case MPGNN_T_T_SEG: *n = (int64_t)p->t_seg.size(); return p->t_seg.data();
+        case MPGNN_T_TA_COL: *n = (int64_t)p->ta_col.size(); return p->ta_col.data();
+        case MPGNN_T_TA_SEG: *n = (int64_t)p->ta_seg.size(); return p->ta_seg.data();
+        case MPGNN_T_REL_INVALID: *eb = 1; *n = (int64_t)p->rel_invalid.size(); return p->rel_invalid.data();
+        default: *n = -1; return nullptr;
+    }
+}
+
+int32_t mpgnn_plan_table_size(const mpgnn_plan* p, int32_t table, int64_t* elems, int32_t* elem_bytes) {
+    if (!p || !elems || !elem_bytes) return fail(MPGNN_ERR_ARG, "NULL argument");
+    table_ptr(p, table, elems, elem_bytes);
+    if (*elems < 0) return fail(MPGNN_ERR_ARG, "unknown table id " + std::to_string(table));
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_plan_export(const mpgnn_plan* p, int32_t table, void* dst, int64_t capacity) {
+    if (!p) return fail(MPGNN_ERR_ARG, "NULL plan");
+    int64_t n = 0;
+    int32_t eb = 0;
+    const void* src = table_ptr(p, table, &n, &eb);
+    if (n < 0) return fail(MPGNN_ERR_ARG, "unknown table id " + std::to_string(table));
+    if (n * eb > capacity) return fail(MPGNN_ERR_ARG, "destination too small");
+    if (n > 0) {
+        if (!dst) return fail(MPGNN_ERR_ARG, "NULL destination");
+        std::memcpy(dst, src, (size_t)(n * eb));
+    }
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_plan_select(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R,
+                          int64_t* seg_begin, int64_t* seg_end) {
+    if (!p || !seg_begin || !seg_end) return fail(MPGNN_ERR_ARG, "NULL argument");
+    int64_t lo = 0, hi = 0;
+    int32_t st = select_relations(p, mode, relation, R, &lo, &hi);
+    if (st != MPGNN_OK) return st;
+    *seg_begin = p->rel_seg_ptr.empty() ? 0 : p->rel_seg_ptr[lo];
+    *seg_end = p->rel_seg_ptr.empty() ? 0 : p->rel_seg_ptr[hi];
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
+    if (!p) return fail(MPGNN_ERR_ARG, "NULL plan");
+    if (p->d.block) {
+        if (p->device == device) return MPGNN_OK;
+        return fail(MPGNN_ERR_ARG, "plan already uploaded to another device");
+    }
+    struct Item {
+        int32_t** dst;
+        const std::vector<int32_t>* src;
+    };
+    Item items[] = {
+        {&p->d.e_col, &p->e_col},       {&p->d.s_ptr, &p->s_ptr},
+        {&p->d.s_row, &p->s_row},       {&p->d.s_rel, &p->s_rel},
+        {&p->d.s_cnt, &p->s_cnt},       {&p->d.s_pos, &p->s_pos},
+        {&p->d.rw_ptr, &p->rw_ptr},     {&p->d.rw_seg, &p->rw_seg},
+        {&p->d.t_ptr, &p->t_ptr},       {&p->d.t_seg, &p->t_seg},
+        {&p->d.ta_col, &p->ta_col},     {&p->d.ta_seg, &p->ta_seg},
+        {&p->d.tile_begin, &p->tile_begin}, {&p->d.tile_end, &p->tile_end},
+        {&p->d.chunk_begin, &p->chunk_begin}, {&p->d.chunk_end, &p->chunk_end},
+        {&p->d.rel_chunk_ptr, &p->rel_chunk_ptr}, {&p->d.rel_val32, &p->rel_val32},
+    };
+    size_t total = 0;
+    std::vector<size_t> offs;
+    for (auto& it : items) {
+        offs.push_back(total);
+        total += ((it.src->size() * sizeof(int32_t) + 255) / 256) * 256;
+    }
+    total = std::max<size_t>(total, 256);
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess) return fail(MPGNN_ERR_HIP, "hipGetDevice failed");
+    if (hipSetDevice(device) != hipSuccess) return fail(MPGNN_ERR_HIP, "hipSetDevice failed");
+    void* block = nullptr;
+    hipError_t err = hipMalloc(&block, total);
+    if (err != hipSuccess) {
+        (void)hipSetDevice(prev);
+        return fail(MPGNN_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(err));
+    }
+    std::vector<char> staging(total, 0);
+    for (size_t i = 0; i < sizeof(items) / sizeof(items[0]); ++i) {
+        if (!items[i].src->empty())
+            std::memcpy(staging.data() + offs[i], items[i].src->data(), items[i].src->size() * sizeof(int32_t));
+        *items[i].dst = reinterpret_cast<int32_t*>(static_cast<char*>(block) + offs[i]);
+    }
+    err = hipMemcpy(block, staging.data(), total, hipMemcpyHostToDevice);
+    (void)hipSetDevice(prev);
+    if (err != hipSuccess) {
+        (void)hipFree(block);
+        return fail(MPGNN_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(err));
+    }
+    p->d.block = block;
+    p->d.block_bytes = total;
+    p->device = device;
+    return MPGNN_OK;
+}
+
+}  // extern "C"

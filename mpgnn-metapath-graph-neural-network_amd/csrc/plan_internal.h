@@ -1,0 +1,84 @@
+// plan_internal.h — the graph plan shared by the host builder (plan.cpp) and the HIP
+// launchers (rgcn_kernels.hip). Not part of the public ABI (include/mpgnn_rgcn.h).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mpgnn_rgcn.h"
+
+namespace mpgnn {
+
+// Segments are packed into relation-pure tiles of this many rows: one workgroup of the
+// segment-transform kernel owns one tile (rgcn_kernels.hip, seg_tile_kernel).
+constexpr int kTileRows = 64;
+// Relation-pure reduction chunks for the weight gradient (outer_accum_kernel).
+constexpr int kChunkRows = 256;
+
+struct DeviceTables {
+    int32_t* e_col = nullptr;
+    int32_t* s_ptr = nullptr;
+    int32_t* s_row = nullptr;
+    int32_t* s_rel = nullptr;
+    int32_t* s_cnt = nullptr;
+    int32_t* s_pos = nullptr;
+    int32_t* rw_ptr = nullptr;
+    int32_t* rw_seg = nullptr;
+    int32_t* t_ptr = nullptr;
+    int32_t* t_seg = nullptr;
+    int32_t* ta_col = nullptr;
+    int32_t* ta_seg = nullptr;
+    int32_t* tile_begin = nullptr;  // [num_tiles] first segment of the tile
+    int32_t* tile_end = nullptr;    // [num_tiles] one past the last segment
+    int32_t* chunk_begin = nullptr; // [num_chunks]
+    int32_t* chunk_end = nullptr;   // [num_chunks]
+    int32_t* rel_chunk_ptr = nullptr; // [nrel+1]
+    int32_t* rel_val32 = nullptr;   // [nrel] relation id clamped to int32 (-1 when it does not fit)
+    void* block = nullptr;          // single hipMalloc holding every table above
+    size_t block_bytes = 0;
+};
+
+}  // namespace mpgnn
+
+struct mpgnn_plan {
+    int64_t N = 0;
+    int64_t E_in = 0;
+    int64_t E = 0;  // local edges kept
+    int64_t S = 0;
+    int64_t nrel = 0;
+    int64_t shard_lo = 0, shard_hi = 0;
+
+    std::vector<int64_t> rel_values;   // [nrel]
+    std::vector<uint8_t> rel_invalid;  // [nrel]
+    std::vector<int32_t> rel_seg_ptr;  // [nrel+1]
+    std::vector<int32_t> rel_edge_ptr; // [nrel+1]
+    std::vector<int32_t> rel_tile_ptr; // [nrel+1]
+    std::vector<int32_t> rel_chunk_ptr;// [nrel+1]
+
+    std::vector<int32_t> e_col, e_id;          // [E]
+    std::vector<int32_t> s_ptr;                // [S+1]
+    std::vector<int32_t> s_row, s_rel, s_cnt, s_pos;  // [S]
+    std::vector<int32_t> rw_ptr;               // [N+1]
+    std::vector<int32_t> rw_seg;               // [S]
+    std::vector<int32_t> t_ptr;                // [N+1]
+    std::vector<int32_t> t_seg;                // [E]
+    std::vector<int32_t> ta_col, ta_seg;       // [E]
+    std::vector<int32_t> tile_begin, tile_end; // [num_tiles]
+    std::vector<int32_t> chunk_begin, chunk_end; // [num_chunks]
+    std::vector<int32_t> rel_val32;            // [nrel]
+
+    int device = -1;
+    mpgnn::DeviceTables d;
+};
+
+namespace mpgnn {
+
+void set_last_error(const std::string& msg);
+
+// Resolve (mode, relation, R) to a contiguous dense-relation range [d_lo, d_hi).
+// Returns MPGNN_ERR_INDEX if a selected relation is flagged invalid.
+int32_t select_relations(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R,
+                         int64_t* d_lo, int64_t* d_hi);
+
+}  // namespace mpgnn

@@ -1,0 +1,149 @@
+"""Graph inputs for the relational layers: the reference's file formats and the seeded
+synthetic workloads of SURVEY §8d (C1-C5).
+
+File formats (reference loaders, main.py:138-195, 347-372):
+  link.dat   ``node_1 \\t relation \\t node_2`` → edge_index int64 [2, E] (row 0 = node_1,
+             row 1 = node_2), edge_type int64 [E], file order kept (main.py:366-372)
+  node.dat   ``id \\t f0 \\t f1 …`` → x float32 [N, F] = the feature columns
+             (get_node_features main.py:347-355: get_dummies leaves numeric columns as is)
+  label.dat  ``id \\t label``
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+FB15K_TRIPLES = os.path.join(_HERE, "data", "fb15k237_devtest.npz")
+FB15K_NUM_EDGES = 310_116  # train + dev + test triples of FB15K-237
+
+
+@dataclass
+class Graph:
+    edge_index: torch.Tensor  # int64 [2, E]
+    edge_type: torch.Tensor   # int64 [E]
+    num_nodes: int
+    num_relations: int
+    x: torch.Tensor | None = None
+
+    @property
+    def num_edges(self) -> int:
+        return int(self.edge_type.numel())
+
+    def to(self, device) -> "Graph":
+        return Graph(self.edge_index.to(device), self.edge_type.to(device), self.num_nodes,
+                     self.num_relations, None if self.x is None else self.x.to(device))
+
+
+# ---------------------------------------------------------------------------------------
+# reference file formats
+# ---------------------------------------------------------------------------------------
+def _read_tsv_numeric(path: str, dtype) -> np.ndarray:
+    rows = []
+    with open(path) as f:
+        for line in f:
+            parts = line.split()
+            if parts:
+                rows.append(parts)
+    width = max(len(r) for r in rows) if rows else 0
+    out = np.zeros((len(rows), width), dtype=dtype)
+    for i, r in enumerate(rows):
+        out[i, :len(r)] = np.asarray(r, dtype=np.float64).astype(dtype)
+    return out
+
+
+def load_links(link_file: str) -> tuple[torch.Tensor, torch.Tensor]:
+    """link.dat → (edge_index, edge_type) — main.py:150-151 + get_edge_index_and_type_no_reverse
+    (main.py:366-372)."""
+    a = _read_tsv_numeric(link_file, np.int64)
+    edge_index = torch.from_numpy(np.ascontiguousarray(np.stack([a[:, 0], a[:, 2]])))
+    edge_type = torch.from_numpy(np.ascontiguousarray(a[:, 1]))
+    return edge_index, edge_type
+
+
+def load_node_features(node_file: str) -> torch.Tensor:
+    """node.dat → x float32 [N, F] (main.py:140-142, 347-355)."""
+    a = _read_tsv_numeric(node_file, np.float64)
+    return torch.from_numpy(a[:, 1:].astype(np.float32))
+
+
+def load_labels(label_file: str) -> tuple[torch.Tensor, torch.Tensor]:
+    a = _read_tsv_numeric(label_file, np.int64)
+    return torch.from_numpy(a[:, 0]), torch.from_numpy(a[:, 1])
+
+
+# ---------------------------------------------------------------------------------------
+# seeded synthetic graphs
+# ---------------------------------------------------------------------------------------
+def synthetic_graph(num_nodes: int, num_relations: int, max_degree: int, feat_dim: int | None = None,
+                    seed: int = 0, one_hot_colors: bool = False) -> Graph:
+    """Mirror of the reference generator's edge distribution (create_graph…:233,245,249):
+    out-degree U{1..max_degree}, node_2 uniform over [0, N) \\ {node_1}, relation uniform.
+    Features: U[0,1) float32 (seed+1), or the 2-colour one-hot of the planted graphs."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    deg = rng.integers(1, max_degree + 1, size=num_nodes)
+    n1 = np.repeat(np.arange(num_nodes, dtype=np.int64), deg)
+    n2 = rng.integers(0, max(num_nodes - 1, 1), size=n1.size)
+    n2 = np.where(n2 >= n1, n2 + 1, n2) % max(num_nodes, 1)
+    rel = rng.integers(0, num_relations, size=n1.size)
+    x = None
+    if feat_dim is not None or one_hot_colors:
+        frng = np.random.Generator(np.random.PCG64(seed + 1))
+        if one_hot_colors:
+            x = np.eye(2, dtype=np.float32)[frng.integers(0, 2, size=num_nodes)]
+        else:
+            x = frng.random((num_nodes, feat_dim), dtype=np.float32)
+        x = torch.from_numpy(x)
+    return Graph(torch.from_numpy(np.stack([n1, n2])), torch.from_numpy(rel.astype(np.int64)),
+                 num_nodes, num_relations, x)
+
+
+def fb15k237_graph(feat_dim: int = 128, seed: int = 0, num_edges: int = FB15K_NUM_EDGES,
+                   smoothing: float = 0.1) -> Graph:
+    """FB15K-237-shaped graph: N = 14,541 entities, R = 237 relations,
+    E = 310,116 edges. train.tsv is absent from the reference, so the 38,000 real dev+test
+    triples are kept and the remaining edges are sampled relation-conditionally from them:
+    relation ~ dev+test relation histogram; node_1 / node_2 ~ the heads / tails observed with
+    that relation, replaced by a uniform entity with probability ``smoothing`` (keeps the hub
+    skew and the relation↔entity correlation). Edge order is shuffled (file order is arbitrary)."""
+    d = np.load(FB15K_TRIPLES)
+    head, rel, tail = d["head"].astype(np.int64), d["rel"].astype(np.int64), d["tail"].astype(np.int64)
+    N, R = int(d["num_entities"]), int(d["num_relations"])
+    rng = np.random.Generator(np.random.PCG64(seed))
+    extra = max(num_edges - rel.size, 0)
+    order = np.argsort(rel, kind="stable")
+    rel_sorted = rel[order]
+    counts = np.bincount(rel, minlength=R)
+    start = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    r_new = rng.choice(R, size=extra, p=counts / counts.sum())
+    pick_h = start[r_new] + (rng.random(extra) * counts[r_new]).astype(np.int64)
+    pick_t = start[r_new] + (rng.random(extra) * counts[r_new]).astype(np.int64)
+    h_new = head[order][pick_h]
+    t_new = tail[order][pick_t]
+    h_new = np.where(rng.random(extra) < smoothing, rng.integers(0, N, extra), h_new)
+    t_new = np.where(rng.random(extra) < smoothing, rng.integers(0, N, extra), t_new)
+    assert (rel_sorted[pick_h] == r_new).all()
+    n1 = np.concatenate([head, h_new])
+    n2 = np.concatenate([tail, t_new])
+    et = np.concatenate([rel, r_new])
+    perm = rng.permutation(n1.size)
+    n1, n2, et = n1[perm], n2[perm], et[perm]
+    frng = np.random.Generator(np.random.PCG64(seed + 1))
+    x = torch.from_numpy(frng.random((N, feat_dim), dtype=np.float32)) if feat_dim else None
+    return Graph(torch.from_numpy(np.stack([n1, n2])), torch.from_numpy(et), N, R, x)
+
+
+# named workloads of BASELINE.json / SURVEY §8d
+def config_graph(name: str, seed: int = 0) -> Graph:
+    if name == "C1":
+        return synthetic_graph(1000, 3, 10, feat_dim=128, seed=seed)
+    if name == "C2":
+        return synthetic_graph(100_000, 16, 32, feat_dim=128, seed=seed)
+    if name in ("C3", "C4", "fb15k237"):
+        return fb15k237_graph(feat_dim=128, seed=seed)
+    if name == "C5":
+        return synthetic_graph(2_000_000, 64, 31, feat_dim=256, seed=seed)
+    raise KeyError(name)

@@ -1,0 +1,129 @@
+"""Autograd functions over the HIP kernels (C ABI calls on torch's current HIP stream).
+
+``rgcn_conv``  — one relational conv layer, forward + backward:
+    out = Σ_r mean_r(x) @ W_r + x @ root + bias
+  mode SINGLE: CustomRGCNConv (mp_rgcn_layer.py:225-246, 260-271), W 2-D, one relation.
+  mode ALL:    PyG RGCNConv loop (≙ mp_rgcn_layer.py:249-258), W [R, F_in, F_out].
+  Backward replaces the autograd graph the reference builds implicitly (main.py:1078):
+  MmBackward (dW, droot, dh = dout·Wᵀ), DivBackward (/count), ScatterAddBackward (gather),
+  IndexSelectBackward (index_add_ into node_2) — SURVEY §3 CS-4.
+
+``segment_means`` — the mean aggregation alone (bit-exact vs PyG propagate, no grad).
+
+With ``group`` set (dst-range sharding) the partial outputs of the ranks are
+summed by an all-reduce (RCCL over xGMI for the "nccl" backend) and so are the gradients.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ._lib import MODE_ALL, MODE_SINGLE, check, lib
+from .plan import GraphPlan
+
+__all__ = ["rgcn_conv", "segment_means", "MODE_SINGLE", "MODE_ALL"]
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _dev(t: torch.Tensor, name: str) -> torch.Tensor:
+    if not t.is_cuda:
+        raise RuntimeError(
+            f"mpgnn_amd: `{name}` is on {t.device}; the relational aggregation runs only as HIP "
+            "kernels on a ROCm GPU (there is no CPU fallback). Move the model and data to 'cuda'.")
+    if t.dtype != torch.float32:
+        raise TypeError(f"mpgnn_amd: `{name}` must be float32 (the reference computes in fp32), got {t.dtype}")
+    t = t.contiguous()
+    if t.data_ptr() % 16:
+        t = t.clone()
+    return t
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+class _RGCNConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, root, bias, plan: GraphPlan, mode: int, relation: int,
+                num_relations: int, row_lo: int, row_hi: int, group):
+        x = _dev(x, "x")
+        weight = _dev(weight, "weight")
+        root = _dev(root, "root") if root is not None else None
+        bias = _dev(bias, "bias") if bias is not None else None
+        plan.to_device(x.device)
+        N, f_in = x.shape
+        f_out = weight.shape[-1]
+        if N != plan.num_nodes:
+            raise ValueError(f"x has {N} rows, the graph plan was built for {plan.num_nodes} nodes")
+        if weight.shape[-2] != f_in:
+            raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({N}x{f_in} and "
+                               f"{weight.shape[-2]}x{f_out})")
+        seg_b, seg_e = plan.select(mode, relation, num_relations)
+        ws = torch.empty(plan.workspace_bytes(mode, relation, num_relations, f_in, f_out, row_lo, row_hi),
+                         dtype=torch.uint8, device=x.device)
+        out = torch.empty(N, f_out, dtype=torch.float32, device=x.device)
+        h_save = None  # segment means, kept for grad_weight (dW_r = Σ h_segᵀ dout[node_1])
+        if ctx.needs_input_grad[1]:
+            h_save = torch.empty(seg_e - seg_b, f_in, dtype=torch.float32, device=x.device)
+        check(lib.mpgnn_rgcn_fwd(plan.handle, mode, int(relation), int(num_relations), x.data_ptr(), f_in,
+                                 weight.data_ptr(), _ptr(root), _ptr(bias), f_out, row_lo, row_hi,
+                                 out.data_ptr(), _ptr(h_save), ws.data_ptr(), _stream(x)),
+              "mpgnn_rgcn_fwd")
+        if group is not None:
+            dist.all_reduce(out, group=group)
+        ctx.plan = plan
+        ctx.mode, ctx.relation, ctx.num_relations = mode, relation, num_relations
+        ctx.rows = (row_lo, row_hi)
+        ctx.group = group
+        ctx.has_root, ctx.has_bias = root is not None, bias is not None
+        ctx.save_for_backward(x, weight, root, h_save)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        x, weight, root, h_save = ctx.saved_tensors
+        plan = ctx.plan
+        grad_out = grad_out.contiguous()
+        if grad_out.data_ptr() % 16:
+            grad_out = grad_out.clone()
+        N, f_in = x.shape
+        f_out = weight.shape[-1]
+        nx, nw, nr, nb = ctx.needs_input_grad[:4]
+        gx = torch.empty_like(x) if nx else None
+        gw = torch.empty_like(weight) if nw else None
+        gr = torch.empty_like(root) if (nr and root is not None) else None
+        gb = torch.empty(f_out, dtype=torch.float32, device=x.device) if (nb and ctx.has_bias) else None
+        ws = torch.empty(plan.workspace_bytes(ctx.mode, ctx.relation, ctx.num_relations, f_in, f_out,
+                                              *ctx.rows), dtype=torch.uint8, device=x.device)
+        check(lib.mpgnn_rgcn_bwd(plan.handle, ctx.mode, int(ctx.relation), int(ctx.num_relations),
+                                 x.data_ptr(), f_in, weight.data_ptr(), _ptr(root), f_out, _ptr(h_save),
+                                 grad_out.data_ptr(), ctx.rows[0], ctx.rows[1], _ptr(gx), _ptr(gw),
+                                 _ptr(gr), _ptr(gb), ws.data_ptr(), _stream(x)), "mpgnn_rgcn_bwd")
+        if ctx.group is not None:
+            for g in (gx, gw, gr, gb):
+                if g is not None:
+                    dist.all_reduce(g, group=ctx.group)
+        return gx, gw, gr, gb, None, None, None, None, None, None, None
+
+
+def rgcn_conv(x: torch.Tensor, weight: torch.Tensor, root, bias, plan: GraphPlan, mode: int,
+              relation: int = -1, num_relations: int = 0, row_range=None, group=None) -> torch.Tensor:
+    """One relational conv layer on the GPU (see module docstring)."""
+    lo, hi = row_range if row_range is not None else (0, plan.num_nodes)
+    return _RGCNConvFn.apply(x, weight, root, bias, plan, int(mode), int(relation),
+                             int(num_relations), int(lo), int(hi), group)
+
+
+def segment_means(x: torch.Tensor, plan: GraphPlan, mode: int, relation: int = -1,
+                  num_relations: int = 0) -> torch.Tensor:
+    """Segment means [S_sel, F] in relation-major segment order (PyG propagate's mean, bit-exact)."""
+    x = _dev(x, "x")
+    plan.to_device(x.device)
+    b, e = plan.select(mode, relation, num_relations)
+    h = torch.empty(e - b, x.shape[1], dtype=torch.float32, device=x.device)
+    check(lib.mpgnn_rel_mean_fwd(plan.handle, int(mode), int(relation), int(num_relations), x.data_ptr(),
+                                 x.shape[1], h.data_ptr(), _stream(x)), "mpgnn_rel_mean_fwd")
+    return h

@@ -1,0 +1,153 @@
+"""GraphPlan — the sorted segment tables of one (edge_index, edge_type) graph.
+
+Replaces the per-call, per-relation compaction ``edge_index[:, edge_type == r]``
+(mp_rgcn_layer.py:29-35, :231, and the RGCNConv loop ≙ :250-251) with a one-time build
+(csrc/plan.cpp) that is uploaded to the GPU and cached across the 999 training epochs of
+``mpgnn_parallel_multiple`` (main.py:1121) keyed by tensor identity and ``_version``.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+import weakref
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+FLOWS = ("target_to_source", "source_to_target")
+
+
+class GraphPlan:
+    """Host + device segment tables for one graph (optionally one dst-range shard)."""
+
+    def __init__(self, edge_index: torch.Tensor, edge_type: torch.Tensor, num_nodes: int,
+                 shard: tuple[int, int] | None = None, flow: str = "target_to_source"):
+        if flow not in FLOWS:
+            raise ValueError(f"Expected 'flow' to be either {FLOWS} (got '{flow}')")
+        if edge_index.dim() != 2 or edge_index.size(0) != 2:
+            raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
+        if edge_type.dim() != 1 or edge_type.numel() != edge_index.size(1):
+            raise ValueError("edge_type must be [E] matching edge_index")
+        ei = edge_index.detach().to("cpu", torch.int64)
+        if flow == "source_to_target":  # aggregate into edge_index[1]: swap the roles
+            ei = ei.flip(0)
+        ei = ei.contiguous()
+        et = edge_type.detach().to("cpu", torch.int64).contiguous()
+        self.num_nodes = int(num_nodes)
+        self.flow = flow
+        lo, hi = shard if shard is not None else (0, self.num_nodes)
+        self.shard = (int(lo), int(hi))
+        handle = ctypes.c_void_p()
+        check(lib.mpgnn_plan_create(ei.data_ptr() if ei.numel() else None,
+                                    et.data_ptr() if et.numel() else None,
+                                    et.numel(), self.num_nodes, self.shard[0], self.shard[1],
+                                    ctypes.byref(handle)), "mpgnn_plan_create")
+        self._h = handle
+        self._device = None
+        self._lock = threading.Lock()
+        info = _lib.PlanInfo()
+        check(lib.mpgnn_plan_get_info(self._h, ctypes.byref(info)))
+        self.num_edges = int(info.num_edges)
+        self.num_segments = int(info.num_segments)
+        self.num_relations_present = int(info.num_relations)
+        self.num_tiles = int(info.num_tiles)
+        self.num_chunks = int(info.num_chunks)
+
+    # -- lifetime -------------------------------------------------------------------------
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib.mpgnn_plan_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def to_device(self, device: torch.device) -> "GraphPlan":
+        if torch.device(device).type != "cuda":
+            raise RuntimeError(
+                f"mpgnn_amd: tensors are on {device}; the relational aggregation runs only as HIP "
+                "kernels on a ROCm GPU (there is no CPU fallback). Move the model and data to 'cuda'.")
+        idx = torch.device(device).index
+        if idx is None:
+            idx = torch.cuda.current_device()
+        with self._lock:
+            if self._device is None:
+                check(lib.mpgnn_plan_upload(self._h, idx), "mpgnn_plan_upload")
+                self._device = idx
+            elif self._device != idx:
+                raise RuntimeError(f"plan lives on cuda:{self._device}, tensor on cuda:{idx}")
+        return self
+
+    # -- queries ---------------------------------------------------------------------------
+    def select(self, mode: int, relation: int, num_relations: int) -> tuple[int, int]:
+        b, e = ctypes.c_int64(), ctypes.c_int64()
+        check(lib.mpgnn_plan_select(self._h, mode, int(relation), int(num_relations),
+                                    ctypes.byref(b), ctypes.byref(e)), "mpgnn_plan_select")
+        return int(b.value), int(e.value)
+
+    def table(self, name: str) -> np.ndarray:
+        tid, dtype = _lib.TABLES[name]
+        n, eb = ctypes.c_int64(), ctypes.c_int32()
+        check(lib.mpgnn_plan_table_size(self._h, tid, ctypes.byref(n), ctypes.byref(eb)))
+        out = np.empty(int(n.value), dtype=dtype)
+        check(lib.mpgnn_plan_export(self._h, tid, out.ctypes.data if out.size else None,
+                                    out.nbytes), "mpgnn_plan_export")
+        return out
+
+    def workspace_bytes(self, mode, relation, num_relations, f_in, f_out, row_lo, row_hi) -> int:
+        b = ctypes.c_int64()
+        check(lib.mpgnn_rgcn_workspace_bytes(self._h, mode, int(relation), int(num_relations),
+                                             f_in, f_out, row_lo, row_hi, ctypes.byref(b)),
+              "mpgnn_rgcn_workspace_bytes")
+        return int(b.value)
+
+
+class _PlanCache:
+    """LRU of plans keyed by the identity/version of the graph tensors."""
+
+    def __init__(self, capacity: int = 16):
+        self.capacity = capacity
+        self._d: OrderedDict = OrderedDict()
+        self._lock = threading.Lock()
+
+    def get(self, edge_index, edge_type, num_nodes, flow="target_to_source", shard=None,
+            device=None) -> GraphPlan:
+        key = (id(edge_index), edge_index._version, tuple(edge_index.shape), edge_index.data_ptr(),
+               id(edge_type), edge_type._version, edge_type.data_ptr(), int(num_nodes), flow,
+               tuple(shard) if shard is not None else None)
+        with self._lock:
+            hit = self._d.get(key)
+            if hit is not None:
+                ref_ei, ref_et, plan = hit
+                if ref_ei() is edge_index and ref_et() is edge_type:
+                    self._d.move_to_end(key)
+                    return plan.to_device(device) if device is not None else plan
+                del self._d[key]
+        plan = GraphPlan(edge_index, edge_type, num_nodes, shard=shard, flow=flow)
+        if device is not None:
+            plan.to_device(device)
+        with self._lock:
+            self._d[key] = (weakref.ref(edge_index), weakref.ref(edge_type), plan)
+            while len(self._d) > self.capacity:
+                self._d.popitem(last=False)
+        return plan
+
+    def clear(self):
+        with self._lock:
+            self._d.clear()
+
+
+plan_cache = _PlanCache()
+
+
+def get_plan(edge_index, edge_type, num_nodes, flow="target_to_source", shard=None, device=None):
+    return plan_cache.get(edge_index, edge_type, num_nodes, flow=flow, shard=shard, device=device)

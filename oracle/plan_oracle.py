@@ -1,0 +1,92 @@
+"""numpy ORACLE for the integer graph plan — TEST INFRASTRUCTURE ONLY.
+
+Restates, with ``np.lexsort`` (stable), the index bookkeeping the reference performs on every
+call: the order-preserving compaction ``edge_index[:, edge_type == r]`` (mp_rgcn_layer.py:29-35,
+called at :231 / per relation in the RGCNConv loop ≙ :250-251) and the (node_1 → rows,
+node_2 → gathered) roles of PyG propagate under flow='target_to_source' (model.py:137,190).
+
+``build_plan`` returns the same tables the C++ builder exports (include/mpgnn_rgcn.h
+``mpgnn_table``), so tests compare them bit-for-bit. Only tests/ may import this module.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+TILE_ROWS = 64
+
+
+def build_plan(edge_index: np.ndarray, edge_type: np.ndarray, num_nodes: int,
+               shard_lo: int = 0, shard_hi: int | None = None) -> dict:
+    n1 = np.asarray(edge_index[0], dtype=np.int64)
+    n2 = np.asarray(edge_index[1], dtype=np.int64)
+    et = np.asarray(edge_type, dtype=np.int64)
+    N = int(num_nodes)
+    shard_hi = N if shard_hi is None else min(int(shard_hi), N)
+    shard_lo = max(int(shard_lo), 0)
+    E = n1.shape[0]
+    rel_values = np.unique(et)
+    rel_d = np.searchsorted(rel_values, et)
+    valid = (n1 >= 0) & (n1 < N) & (n2 >= 0) & (n2 < N)
+    rel_invalid = np.zeros(len(rel_values), dtype=np.uint8)
+    rel_invalid[np.unique(rel_d[~valid])] = 1
+
+    ids = np.nonzero(valid)[0]
+    order = ids[np.lexsort((ids, n1[ids], rel_d[ids]))]          # (rel, node_1, edge)
+    key_d, key_r = rel_d[order], n1[order]
+    new_run = np.ones(len(order), dtype=bool)
+    new_run[1:] = (key_d[1:] != key_d[:-1]) | (key_r[1:] != key_r[:-1])
+    run_id = np.cumsum(new_run) - 1
+    run_cnt = np.bincount(run_id, minlength=run_id.max() + 1 if len(run_id) else 0)
+    local = (n2[order] >= shard_lo) & (n2[order] < shard_hi)
+    loc = order[local]
+    loc_run = run_id[local]
+    # segments = runs with >= 1 local edge, in run order
+    seg_new = np.ones(len(loc), dtype=bool)
+    seg_new[1:] = loc_run[1:] != loc_run[:-1]
+    seg_of_edge = np.cumsum(seg_new) - 1
+    seg_first = np.nonzero(seg_new)[0]
+    S = len(seg_first)
+    s_ptr = np.append(seg_first, len(loc)).astype(np.int32)
+    s_row = n1[loc[seg_first]].astype(np.int32)
+    s_reld = rel_d[loc[seg_first]]
+    s_rel = rel_values[s_reld].astype(np.int64)
+    s_rel = np.where((s_rel >= 0) & (s_rel <= np.iinfo(np.int32).max), s_rel, -1).astype(np.int32)
+    s_cnt = run_cnt[loc_run[seg_first]].astype(np.int32)
+    R = len(rel_values)
+    rel_seg_ptr = np.zeros(R + 1, dtype=np.int32)
+    np.add.at(rel_seg_ptr, s_reld + 1, 1)
+    rel_seg_ptr = np.cumsum(rel_seg_ptr).astype(np.int32)
+    rel_edge_ptr = s_ptr[rel_seg_ptr].astype(np.int32)
+
+    seg_ids = np.arange(S)
+    rw_seg = seg_ids[np.lexsort((seg_ids, s_row))].astype(np.int32)   # (node_1, rel)
+    s_pos = np.empty(S, dtype=np.int32)
+    s_pos[rw_seg] = np.arange(S, dtype=np.int32)
+    rw_ptr = np.zeros(N + 1, dtype=np.int32)
+    np.add.at(rw_ptr, s_row.astype(np.int64) + 1, 1)
+    rw_ptr = np.cumsum(rw_ptr).astype(np.int32)
+
+    e_col = n2[loc].astype(np.int32)
+    k = np.arange(len(loc))
+    by_col = k[np.lexsort((k, e_col))]                  # (node_2, rel, node_1, edge)
+    t_seg = seg_of_edge[by_col].astype(np.int32)
+    t_ptr = np.zeros(N + 1, dtype=np.int32)
+    np.add.at(t_ptr, e_col.astype(np.int64) + 1, 1)
+    t_ptr = np.cumsum(t_ptr).astype(np.int32)
+    edge_reld = s_reld[seg_of_edge]
+    pos = np.arange(len(by_col))
+    by_rel_col = by_col[np.lexsort((pos, edge_reld[by_col]))]   # stable by rel over col-major
+    ta_col = e_col[by_rel_col].astype(np.int32)
+    ta_seg = seg_of_edge[by_rel_col].astype(np.int32)
+
+    return dict(
+        rel_values=rel_values.astype(np.int64), rel_seg_ptr=rel_seg_ptr, rel_edge_ptr=rel_edge_ptr,
+        e_col=e_col, e_id=loc.astype(np.int32), s_ptr=s_ptr, s_row=s_row, s_rel=s_rel,
+        s_cnt=s_cnt, s_pos=s_pos, rw_ptr=rw_ptr, rw_seg=rw_seg, t_ptr=t_ptr, t_seg=t_seg,
+        ta_col=ta_col, ta_seg=ta_seg, rel_invalid=rel_invalid,
+    )
+
+
+def masked_edges(edge_index: np.ndarray, edge_type: np.ndarray, relation: int) -> np.ndarray:
+    """``edge_index[:, edge_type == relation]`` — mp_rgcn_layer.py:35 — as int64 [2, E_r]."""
+    return np.asarray(edge_index)[:, np.asarray(edge_type) == relation]

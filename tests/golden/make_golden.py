@@ -1,0 +1,296 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ from the REFERENCE's own code.
+
+Runs only where /root/reference exists (the survey container); the outputs are committed as
+data (.npz) and travel to the GPU box — the reference never does.
+
+The reference layer (mp_rgcn_layer.py) and model (model.py) import torch_geometric /
+torch_scatter / torch_sparse (requirements.txt:7), which are not installed and cannot be
+(no network). A minimal stand-in package tree is written to a temporary directory with:
+  * torch_geometric.nn.conv.MessagePassing — PyG 2.3.1 propagate semantics for the one code
+    path the reference uses (flow handling, x_j = x.index_select(node_dim, edge_index[j]),
+    identity message, aggr='mean' via scatter_add_ / count.clamp(min=1), dim_size = size[i])
+  * torch_geometric.nn.inits.glorot / zeros (PyG 2.3.1 formulas)
+  * torch_geometric.typing / data / nn.RGCNConv names (RGCNConv raises if instantiated)
+  * torch_scatter.scatter / torch_sparse names (only imported, never called on this path)
+Everything else — the masking (:29-35,:231), h @ W (:245), squeeze (:246), root (:265),
+bias (:268), parameter shapes and glorot init order (:120-155), MPNetm wiring (model.py:179-228)
+— is the reference's code, executed as is. The PyG arithmetic itself (third-party) is therefore
+restated here, not pinned; it is pinned structurally by the embedding.dat / label.dat KAT.
+
+Outputs (all small):
+  kat_synthetic.npz       the two planted synthetic graphs (link/node/label/embedding .dat)
+  layer_single.npz        CustomRGCNConv (mode SINGLE) forward + autograd grads, C1 graph
+  layer_all.npz           RGCNConv loop (mode ALL) assembled from reference CustomRGCNConv
+                          per-relation transforms, forward + grads, C1 graph
+  mpnetm_synthetic.npz    MPNetm(2,64,4,64,2,1,[[1,0]]) seed-30 state_dict + eval logits
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import sys
+import tempfile
+import textwrap
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+STANDIN = {
+    "torch_geometric/__init__.py": "from . import nn, data, typing\n",
+    "torch_geometric/typing.py": textwrap.dedent("""
+        from typing import Optional
+        from torch import Tensor
+        Adj = Tensor
+        OptTensor = Optional[Tensor]
+    """),
+    "torch_geometric/data/__init__.py": textwrap.dedent("""
+        class Data:
+            def __init__(self, **kw):
+                for k, v in kw.items():
+                    setattr(self, k, v)
+    """),
+    "torch_geometric/nn/__init__.py": textwrap.dedent("""
+        from .conv import MessagePassing
+        from . import inits
+        class RGCNConv:
+            def __init__(self, *a, **k):
+                raise NotImplementedError('stand-in: PyG RGCNConv is not available')
+        __all__ = ['MessagePassing', 'RGCNConv', 'inits']
+    """),
+    "torch_geometric/nn/inits.py": textwrap.dedent("""
+        import math
+        import torch
+        def glorot(value):
+            if isinstance(value, torch.Tensor):
+                stdv = math.sqrt(6.0 / (value.size(-2) + value.size(-1)))
+                value.data.uniform_(-stdv, stdv)
+        def zeros(value):
+            if isinstance(value, torch.Tensor):
+                value.data.fill_(0.0)
+    """),
+    "torch_geometric/nn/conv/__init__.py": textwrap.dedent("""
+        import torch
+        class MessagePassing(torch.nn.Module):
+            # PyG 2.3.1 semantics for propagate(edge_index, x=..., size=...) with aggr='mean'
+            def __init__(self, aggr='add', flow='source_to_target', node_dim=-2, **kw):
+                super().__init__()
+                self.aggr = aggr
+                self.flow = flow
+                self.node_dim = node_dim
+            def propagate(self, edge_index, size=None, **kwargs):
+                i, j = (1, 0) if self.flow == 'source_to_target' else (0, 1)
+                x = kwargs['x']
+                x_j = x.index_select(self.node_dim, edge_index[j])
+                msg = self.message(x_j)
+                index = edge_index[i]
+                dim_size = size[i] if size is not None and size[i] is not None else x.size(self.node_dim)
+                assert self.aggr == 'mean' and self.node_dim == 0
+                count = msg.new_zeros(dim_size)
+                count.scatter_add_(0, index, msg.new_ones(msg.size(0)))
+                count = count.clamp(min=1)
+                out = msg.new_zeros((dim_size,) + tuple(msg.shape[1:]))
+                out.scatter_add_(0, index.view(-1, 1).expand_as(msg), msg)
+                return out / count.view(-1, 1)
+    """),
+    "torch_scatter/__init__.py": textwrap.dedent("""
+        def scatter(*a, **k):
+            raise NotImplementedError('stand-in torch_scatter')
+    """),
+    "torch_sparse/__init__.py": textwrap.dedent("""
+        class SparseTensor:
+            pass
+        def masked_select_nnz(*a, **k):
+            raise NotImplementedError('stand-in torch_sparse')
+        def matmul(*a, **k):
+            raise NotImplementedError('stand-in torch_sparse')
+    """),
+}
+
+
+def import_reference():
+    tmp = tempfile.mkdtemp(prefix="pyg_standin_")
+    for rel, src in STANDIN.items():
+        path = os.path.join(tmp, rel)
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            f.write(src)
+    sys.path.insert(0, tmp)
+    sys.path.insert(0, REF)
+    sys.dont_write_bytecode = True
+    layer = importlib.import_module("mp_rgcn_layer")
+    model = importlib.import_module("model")
+    return layer, model
+
+
+def synthetic_c1(seed=0, N=1000, R=3, dmax=10):
+    """C1 graph, mirrors create_graph…:233,245,249 with a seeded PCG64."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    deg = rng.integers(1, dmax + 1, size=N)
+    n1 = np.repeat(np.arange(N), deg)
+    n2 = rng.integers(0, N - 1, size=n1.size)
+    n2 = np.where(n2 >= n1, n2 + 1, n2) % N
+    rel = rng.integers(0, R, size=n1.size)
+    return np.stack([n1, n2]).astype(np.int64), rel.astype(np.int64)
+
+
+def read_dat(path):
+    return np.array([[int(v) for v in line.split()] for line in open(path) if line.strip()], dtype=np.int64)
+
+
+def make_kat():
+    out = {}
+    for tag, d in (("L3", "data/synthetic/metapath_length_3/overlap_0rels_0"),
+                   ("L4", "data/synthetic/metapath_length_4/overlap_0_rels_0")):
+        base = os.path.join(REF, d)
+        link = read_dat(os.path.join(base, "link.dat"))          # node_1 rel node_2
+        node = read_dat(os.path.join(base, "node.dat"))          # id red blue (one-hot)
+        label = read_dat(os.path.join(base, "label.dat"))        # id label
+        emb = read_dat(os.path.join(base, "embedding.dat"))      # id e1 e2 (per-hop truth)
+        meta = open(os.path.join(base, "metapath.dat")).read().split("\n")
+        out[f"{tag}_link"] = link
+        out[f"{tag}_node"] = node
+        out[f"{tag}_label"] = label
+        out[f"{tag}_embedding"] = emb
+        out[f"{tag}_metapath_rel"] = np.array([int(v) for v in meta[1].split()], dtype=np.int64)
+        out[f"{tag}_metapath_col"] = np.array([int(v) for v in meta[2].split()], dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, "kat_synthetic.npz"), **out)
+
+
+def grads_of(fn, tensors, gout):
+    for t in tensors:
+        t.grad = None
+    out = fn()
+    out.backward(gout)
+    return out.detach(), [t.grad.detach().clone() for t in tensors]
+
+
+def make_layer_goldens(layer):
+    ei, et = synthetic_c1()
+    edge_index = torch.from_numpy(ei)
+    edge_type = torch.from_numpy(et)
+    N, R = 1000, 3
+    single, allmode = {"edge_index": ei, "edge_type": et}, {"edge_index": ei, "edge_type": et}
+    for F_in in (2, 128):
+        F_out = 64
+        g = torch.Generator().manual_seed(1234 + F_in)
+        if F_in == 2:
+            x = torch.nn.functional.one_hot(torch.randint(0, 2, (N,), generator=g), 2).float()
+        else:
+            x = torch.rand(N, F_in, generator=g)
+        x.requires_grad_(True)
+        gout = torch.randn(N, F_out, generator=g)
+        # --- mode SINGLE: reference CustomRGCNConv, one layer per relation -------------
+        torch.manual_seed(30)
+        conv = layer.CustomRGCNConv(F_in, F_out, 1, flow="target_to_source")
+        single[f"F{F_in}_x"] = x.detach().numpy()
+        single[f"F{F_in}_gout"] = gout.numpy()
+        single[f"F{F_in}_weight"] = conv.weight.detach().numpy().copy()
+        single[f"F{F_in}_root"] = conv.root.detach().numpy().copy()
+        single[f"F{F_in}_bias"] = conv.bias.detach().numpy().copy()
+        for rel in range(R + 1):  # R = relation absent from the graph (empty mask)
+            params = [x, conv.weight, conv.root, conv.bias]
+            out, grads = grads_of(lambda: conv(0, rel, x, edge_index, edge_type), params, gout)
+            single[f"F{F_in}_r{rel}_out"] = out.numpy()
+            for name, gr in zip(("dx", "dweight", "droot", "dbias"), grads):
+                single[f"F{F_in}_r{rel}_{name}"] = gr.numpy()
+            # the mean itself (bit-exact target): h = propagate(masked)
+            mask = edge_type == rel
+            tmp = layer.masked_edge_index(edge_index, mask)
+            single[f"F{F_in}_r{rel}_masked"] = tmp.numpy()
+            single[f"F{F_in}_r{rel}_h"] = conv.propagate(tmp, x=x.detach(), size=(N, N)).numpy()
+        # --- mode ALL: Σ_r (reference transform of relation r) + x@root + bias ----------
+        torch.manual_seed(31)
+        W = torch.empty(R, F_in, F_out)
+        layer.glorot(W)
+        root = torch.empty(F_in, F_out)
+        layer.glorot(root)
+        bias = (torch.rand(F_out) - 0.5) * 0.1
+        W.requires_grad_(True), root.requires_grad_(True), bias.requires_grad_(True)
+        c = layer.CustomRGCNConv(F_in, F_out, 1, root_weight=False, bias=False, flow="target_to_source")
+
+        def forward_all():
+            # RGCNConv loop ≙ mp_rgcn_layer.py:249-258: out = out + h_r @ W[r]; then root, bias.
+            # Each h_r @ W_r is the reference CustomRGCNConv forward (:231-246) with its
+            # weight bound to W[r] (functional_call keeps the autograd path to W).
+            out = torch.zeros(N, F_out)
+            for rel in range(R):
+                out = out + torch.func.functional_call(c, {"weight": W[rel]},
+                                                       (0, rel, x, edge_index, edge_type))
+            out = out + x @ root
+            out = out + bias
+            return out
+
+        out, grads = grads_of(forward_all, [x, W, root, bias], gout)
+        allmode[f"F{F_in}_x"] = x.detach().numpy()
+        allmode[f"F{F_in}_gout"] = gout.numpy()
+        allmode[f"F{F_in}_weight"] = W.detach().numpy()
+        allmode[f"F{F_in}_root"] = root.detach().numpy()
+        allmode[f"F{F_in}_bias"] = bias.detach().numpy()
+        allmode[f"F{F_in}_out"] = out.numpy()
+        for name, gr in zip(("dx", "dweight", "droot", "dbias"), grads):
+            allmode[f"F{F_in}_{name}"] = gr.numpy()
+    np.savez_compressed(os.path.join(HERE, "layer_single.npz"), **single)
+    np.savez_compressed(os.path.join(HERE, "layer_all.npz"), **allmode)
+
+
+def make_mpnetm_golden(model):
+    kat = np.load(os.path.join(HERE, "kat_synthetic.npz"))
+    link = kat["L3_link"]
+    node = kat["L3_node"]
+    edge_index = torch.tensor(np.stack([link[:, 0], link[:, 2]]))
+    edge_type = torch.tensor(link[:, 1])
+    x = torch.from_numpy(node[:, 1:].astype(np.float32))   # get_node_features, main.py:347-355
+    torch.manual_seed(30)                                   # main.py:31
+    net = model.MPNetm(2, 64, 4, 64, 2, 1, [[1, 0]])        # model.py:179
+    net.eval()
+    with torch.no_grad():
+        logits = net(x, edge_index, edge_type)
+    out = {"logits": logits.numpy(), "x": x.numpy(), "metapath": np.array([1, 0])}
+    for k, v in net.state_dict().items():
+        out["sd." + k] = v.numpy()
+    np.savez_compressed(os.path.join(HERE, "mpnetm_synthetic.npz"), **out)
+
+
+def make_fb15k_triples():
+    """FB15K-237 dev+test triples as entity/relation indices (entities.txt / relations.txt
+    order). train.tsv is missing from the reference (.MISSING_LARGE_BLOBS:7); the bench's
+    FB15K-shaped graph (mpgnn_amd.data.fb15k237_graph) keeps these 38,000 real triples and
+    samples the rest relation-conditionally from them. Written into the package (data, not code)."""
+    base = os.path.join(REF, "data/fb15k-237")
+    ents = [l.strip() for l in open(os.path.join(base, "entities.txt")) if l.strip()]
+    rels = [l.strip() for l in open(os.path.join(base, "relations.txt")) if l.strip()]
+    e2i = {e: i for i, e in enumerate(ents)}
+    r2i = {r: i for i, r in enumerate(rels)}
+    tri = []
+    for f in ("dev.tsv", "test.tsv"):
+        for line in open(os.path.join(base, f)):
+            p = line.rstrip("\n").split("\t")
+            if len(p) == 3:
+                tri.append((e2i[p[0]], r2i[p[1]], e2i[p[2]]))
+    tri = np.array(tri, dtype=np.int32)
+    pkg = os.path.join(HERE, "..", "..", "mpgnn-metapath-graph-neural-network_amd", "data")
+    os.makedirs(pkg, exist_ok=True)
+    np.savez_compressed(os.path.join(pkg, "fb15k237_devtest.npz"), head=tri[:, 0], rel=tri[:, 1],
+                        tail=tri[:, 2], num_entities=np.int64(len(ents)), num_relations=np.int64(len(rels)))
+
+
+def main():
+    if not os.path.isdir(REF):
+        raise SystemExit("make_golden.py needs /root/reference (survey container only)")
+    torch.set_num_threads(1)
+    layer, model = import_reference()
+    make_kat()
+    make_layer_goldens(layer)
+    make_mpnetm_golden(model)
+    make_fb15k_triples()
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)), "bytes")
+
+
+if __name__ == "__main__":
+    main()

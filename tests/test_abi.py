@@ -1,0 +1,91 @@
+"""CPU: the C-ABI library loads and exports every symbol include/mpgnn_rgcn.h declares;
+host-only entry points behave; device entry points refuse a plan that is not on a device
+(no compute without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from tests.conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "mpgnn_rgcn.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mpgnn_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    syms = declared_symbols()
+    for s in ("mpgnn_plan_create", "mpgnn_plan_destroy", "mpgnn_plan_upload", "mpgnn_rgcn_fwd",
+              "mpgnn_rgcn_bwd", "mpgnn_rel_mean_fwd", "mpgnn_rgcn_workspace_bytes"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from mpgnn_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    bound = {name for name, _, _ in _lib.SIGNATURES}
+    assert bound == set(declared_symbols())
+
+
+def test_version_and_status_strings():
+    from mpgnn_amd._lib import lib
+    assert lib.mpgnn_abi_version() == 1
+    assert lib.mpgnn_status_string(0) == b"ok"
+    assert lib.mpgnn_status_string(-2) == b"index out of range"
+
+
+def test_kernels_refuse_plan_not_on_device():
+    from mpgnn_amd import _lib
+    from mpgnn_amd._lib import lib
+    import mpgnn_amd
+    g = mpgnn_amd.data.config_graph("C1")
+    p = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, g.num_nodes)
+    st = lib.mpgnn_rgcn_fwd(p.handle, 1, -1, 3, None, 128, None, None, None, 64, 0, g.num_nodes,
+                            None, None, None, None)
+    assert st == _lib.MPGNN_ERR_NOT_ON_DEVICE
+    assert b"upload" in lib.mpgnn_last_error()
+    st = lib.mpgnn_rel_mean_fwd(p.handle, 1, -1, 3, None, 128, None, None)
+    assert st == _lib.MPGNN_ERR_NOT_ON_DEVICE
+
+
+def test_bad_arguments():
+    from mpgnn_amd import _lib
+    from mpgnn_amd._lib import lib
+    h = ctypes.c_void_p()
+    assert lib.mpgnn_plan_create(None, None, 5, 10, 0, 10, ctypes.byref(h)) == _lib.MPGNN_ERR_ARG
+    assert lib.mpgnn_plan_create(None, None, -1, 10, 0, 10, ctypes.byref(h)) == _lib.MPGNN_ERR_ARG
+    assert lib.mpgnn_plan_destroy(None) == 0
+    import mpgnn_amd
+    g = mpgnn_amd.data.config_graph("C1")
+    p = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, g.num_nodes)
+    with pytest.raises(ValueError):
+        p.select(7, 0, 0)          # unknown mode
+
+
+def test_workspace_bytes_is_host_computable():
+    import mpgnn_amd
+    g = mpgnn_amd.data.config_graph("C1")
+    p = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, g.num_nodes)
+    b_all = p.workspace_bytes(mpgnn_amd.MODE_ALL, -1, 3, 128, 64, 0, g.num_nodes)
+    assert b_all >= p.num_segments * 64 * 4
+    b_one = p.workspace_bytes(mpgnn_amd.MODE_SINGLE, 1, 0, 128, 64, 0, g.num_nodes)
+    assert 0 < b_one <= b_all
+
+
+def test_product_path_fails_loudly_on_cpu_tensors():
+    import mpgnn_amd
+    g = mpgnn_amd.data.config_graph("C1")
+    conv = mpgnn_amd.RGCNConv(128, 64, 3, flow="target_to_source")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        conv(g.x, g.edge_index, g.edge_type)
+    c2 = mpgnn_amd.CustomRGCNConv(128, 64, 1, flow="target_to_source")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        c2(0, 1, g.x, g.edge_index, g.edge_type)

@@ -1,0 +1,135 @@
+"""CPU: the C++ graph plan (csrc/plan.cpp, via the C ABI) is bit-identical to the numpy
+oracle (oracle/plan_oracle.py) and reproduces the reference's masked edge lists
+(``edge_index[:, edge_type == r]``, mp_rgcn_layer.py:35) — order within each node_1 kept."""
+import numpy as np
+import pytest
+import torch
+
+import mpgnn_amd
+from mpgnn_amd import data
+from oracle import plan_oracle
+
+TABLES = ["rel_values", "rel_seg_ptr", "rel_edge_ptr", "e_col", "e_id", "s_ptr", "s_row", "s_rel",
+          "s_cnt", "s_pos", "rw_ptr", "rw_seg", "t_ptr", "t_seg", "ta_col", "ta_seg", "rel_invalid"]
+
+
+def graphs():
+    g1 = data.config_graph("C1")
+    yield "C1", g1.edge_index.numpy(), g1.edge_type.numpy(), g1.num_nodes
+    g2 = data.synthetic_graph(3000, 7, 40, seed=5)
+    yield "dense7", g2.edge_index.numpy(), g2.edge_type.numpy(), 3000
+    rng = np.random.default_rng(3)
+    # duplicates, self loops, relation gaps, negative and huge relation ids
+    ei = rng.integers(0, 50, size=(2, 400))
+    et = rng.choice([-7, 0, 3, 3, 9, 2**40], size=400)
+    yield "weird_ids", ei, et, 50
+    # invalid node ids in some relations
+    ei2 = rng.integers(0, 60, size=(2, 300))
+    et2 = rng.integers(0, 5, size=300)
+    ei2[0, 7] = 60      # relation et2[7] flagged
+    ei2[1, 11] = -1     # relation et2[11] flagged
+    yield "invalid", ei2, et2, 60
+    yield "empty", np.zeros((2, 0), np.int64), np.zeros(0, np.int64), 10
+    yield "single", np.array([[3], [5]]), np.array([1]), 8
+    yield "no_nodes", np.zeros((2, 0), np.int64), np.zeros(0, np.int64), 0
+
+
+@pytest.mark.parametrize("case", list(graphs()), ids=lambda c: c[0])
+@pytest.mark.parametrize("shard", [None, (0.0, 0.5), (0.5, 1.0), (0.2, 0.21)])
+def test_plan_tables_bit_exact(case, shard):
+    name, ei, et, N = case
+    lo, hi = (0, N) if shard is None else (int(shard[0] * N), int(shard[1] * N))
+    plan = mpgnn_amd.GraphPlan(torch.from_numpy(np.ascontiguousarray(ei)), torch.from_numpy(et), N,
+                               shard=(lo, hi))
+    ref = plan_oracle.build_plan(ei, et, N, lo, hi)
+    for tname in TABLES:
+        got = plan.table(tname)
+        assert got.dtype == ref[tname].dtype, tname
+        assert np.array_equal(got, ref[tname]), tname
+
+
+@pytest.mark.parametrize("case", list(graphs())[:3], ids=lambda c: c[0])
+def test_masked_edge_lists_match_reference_semantics(case):
+    name, ei, et, N = case
+    plan = mpgnn_amd.GraphPlan(torch.from_numpy(np.ascontiguousarray(ei)), torch.from_numpy(et), N)
+    rel_values = plan.table("rel_values")
+    rep = plan.table("rel_edge_ptr")
+    e_id = plan.table("e_id")
+    for d, r in enumerate(rel_values):
+        masked = plan_oracle.masked_edges(ei, et, r)            # reference order
+        ids = e_id[rep[d]:rep[d + 1]]
+        got = np.asarray(ei)[:, ids]
+        # same multiset of edges; our order = stable sort of the reference order by node_1
+        order = np.argsort(masked[0], kind="stable")
+        assert np.array_equal(got, masked[:, order])
+
+
+def test_segment_counts_are_global_across_shards():
+    g = data.config_graph("C1")
+    N = g.num_nodes
+    full = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, N)
+    key = lambda p: dict(zip(zip(p.table("s_row").tolist(), p.table("s_rel").tolist()),
+                             p.table("s_cnt").tolist()))
+    ref = key(full)
+    ranges = mpgnn_amd.distributed.shard_ranges(g.edge_index, N, 4)
+    total_edges = 0
+    for lo, hi in ranges:
+        p = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, N, shard=(lo, hi))
+        total_edges += p.num_edges
+        for k, c in key(p).items():
+            assert ref[k] == c
+        assert np.all((p.table("e_col") >= lo) & (p.table("e_col") < hi))
+    assert total_edges == full.num_edges
+
+
+def test_shard_ranges_balanced_and_cover():
+    g = data.config_graph("C2")
+    for world in (1, 2, 4, 8):
+        r = mpgnn_amd.distributed.shard_ranges(g.edge_index, g.num_nodes, world)
+        assert r[0][0] == 0 and r[-1][1] == g.num_nodes
+        assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+        col = g.edge_index[1].numpy()
+        counts = [int(((col >= lo) & (col < hi)).sum()) for lo, hi in r]
+        assert max(counts) - min(counts) <= 0.01 * g.num_edges + 64
+
+
+def test_select_ranges():
+    g = data.synthetic_graph(500, 6, 8, seed=1)
+    p = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, 500)
+    rsp = p.table("rel_seg_ptr")
+    assert p.select(mpgnn_amd.MODE_ALL, -1, 6) == (0, p.num_segments)
+    assert p.select(mpgnn_amd.MODE_ALL, -1, 3) == (0, int(rsp[3]))
+    assert p.select(mpgnn_amd.MODE_SINGLE, 4, 0) == (int(rsp[4]), int(rsp[5]))
+    b, e = p.select(mpgnn_amd.MODE_SINGLE, 99, 0)      # absent relation: empty mask, no error
+    assert b == e
+
+
+def test_invalid_index_raises_index_error_only_for_touched_relation():
+    ei = torch.tensor([[0, 1, 5], [1, 2, 0]])
+    et = torch.tensor([0, 0, 1])
+    p = mpgnn_amd.GraphPlan(ei, et, 3)          # node 5 >= N=3 in relation 1
+    p.select(mpgnn_amd.MODE_SINGLE, 0, 0)
+    with pytest.raises(IndexError):
+        p.select(mpgnn_amd.MODE_SINGLE, 1, 0)
+    with pytest.raises(IndexError):
+        p.select(mpgnn_amd.MODE_ALL, -1, 2)
+    p.select(mpgnn_amd.MODE_ALL, -1, 1)          # only relation 0 touched
+
+
+def test_source_to_target_flow_swaps_roles():
+    g = data.config_graph("C1")
+    a = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, g.num_nodes, flow="source_to_target")
+    b = mpgnn_amd.GraphPlan(g.edge_index.flip(0), g.edge_type, g.num_nodes)
+    for tname in TABLES:
+        assert np.array_equal(a.table(tname), b.table(tname))
+
+
+def test_plan_cache_reuses_and_invalidates():
+    g = data.config_graph("C1")
+    mpgnn_amd.plan_cache.clear()
+    p1 = mpgnn_amd.get_plan(g.edge_index, g.edge_type, g.num_nodes)
+    p2 = mpgnn_amd.get_plan(g.edge_index, g.edge_type, g.num_nodes)
+    assert p1 is p2
+    g.edge_type[0] = (g.edge_type[0] + 1) % 3       # in-place edit bumps _version
+    p3 = mpgnn_amd.get_plan(g.edge_index, g.edge_type, g.num_nodes)
+    assert p3 is not p1
