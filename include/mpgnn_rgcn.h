@@ -151,6 +151,18 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
                        float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
                        void* workspace, void* stream);
 
+/* --- options ----------------------------------------------------------------------------
+ * MPGNN_OPT_EXACT_ORDER = 1: every gather-sum adds its entries strictly in the reference's
+ * sequential order (no ordered-piece split of long runs). Default 0: runs longer than 32
+ * entries are summed as ordered 32-entry partial sums (deterministic, bounded serial work per
+ * wave); runs of <= 32 entries — the forward segment means of almost every segment — are
+ * bit-identical to the reference either way. mpgnn_rel_mean_fwd is always exact. */
+enum mpgnn_option {
+    MPGNN_OPT_EXACT_ORDER = 0,
+    MPGNN_OPT_ABLATE = 1 /* profiling only: 1 skips the forward gather, 2 the forward MFMA (wrong results) */
+};
+int32_t mpgnn_set_option(int32_t option, int64_t value);
+
 /* --- kernel timing (bench / profiling) ----------------------------------------------
  * When enabled, every kernel launch of the entry points above is bracketed by a pair of
  * hipEvents recorded on the launch stream; mpgnn_timing_query synchronises those events and
@@ -163,7 +175,8 @@ enum mpgnn_kernel_kind {
     MPGNN_K_OUTER = 4,     /* outer_accum_kernel: dW / droot / dbias partial slabs        */
     MPGNN_K_REDUCE = 5,    /* reduce_slabs_kernel                                         */
     MPGNN_K_MEAN = 6,      /* seg_tile_kernel: segment means only (mpgnn_rel_mean_fwd)    */
-    MPGNN_K_COUNT = 7
+    MPGNN_K_PIECE = 7,     /* piece_sum_kernel: ordered partial sums of long runs         */
+    MPGNN_K_COUNT = 8
 };
 int32_t mpgnn_timing_enable(int32_t on);
 int32_t mpgnn_timing_reset(void);

@@ -63,12 +63,15 @@ SIGNATURES = [
                               _P, _P, _P, _P]),
     ("mpgnn_rgcn_bwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _I32, _P, _P, _I64, _I64,
                               _P, _P, _P, _P, _P, _P]),
+    ("mpgnn_set_option", _I32, [_I32, _I64]),
     ("mpgnn_timing_enable", _I32, [_I32]),
     ("mpgnn_timing_reset", _I32, []),
     ("mpgnn_timing_query", _I32, [_I32, ctypes.POINTER(ctypes.c_double), _PI64]),
 ]
 
-KERNEL_KINDS = {"seg_fwd": 0, "row_fwd": 1, "seg_dgrad": 2, "row_dx": 3, "outer": 4, "reduce": 5, "mean": 6}
+KERNEL_KINDS = {"seg_fwd": 0, "row_fwd": 1, "seg_dgrad": 2, "row_dx": 3, "outer": 4, "reduce": 5, "mean": 6,
+                "piece": 7}
+OPT_EXACT_ORDER = 0
 
 
 def _load():
@@ -92,6 +95,11 @@ def kernel_timing(kind: str) -> tuple[float, int]:
     ms, n = ctypes.c_double(), ctypes.c_int64()
     check(lib.mpgnn_timing_query(KERNEL_KINDS[kind], ctypes.byref(ms), ctypes.byref(n)), "mpgnn_timing_query")
     return float(ms.value), int(n.value)
+
+
+def set_exact_order(on: bool) -> None:
+    """Force reference-sequential summation order everywhere (see include/mpgnn_rgcn.h)."""
+    check(lib.mpgnn_set_option(OPT_EXACT_ORDER, 1 if on else 0), "mpgnn_set_option")
 
 
 def check(status: int, what: str = "") -> None:

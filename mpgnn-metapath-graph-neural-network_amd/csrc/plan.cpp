@@ -82,6 +82,32 @@ static void counting_sort(const std::vector<int32_t>& items, int64_t nkeys, KeyF
     if (ptr_out) ptr_out->swap(ptr);
 }
 
+// Two-level list (see RaggedHost) over runs given by run_ptr.
+static void build_ragged(const std::vector<int32_t>& run_ptr, RaggedHost& L) {
+    const size_t runs = run_ptr.empty() ? 0 : run_ptr.size() - 1;
+    L.ent.clear();
+    L.ent_ptr.assign(runs + 1, 0);
+    L.run_piece_ptr.assign(runs + 1, 0);
+    L.piece_b.clear();
+    L.piece_e.clear();
+    for (size_t r = 0; r < runs; ++r) {
+        L.ent_ptr[r] = (int32_t)L.ent.size();
+        L.run_piece_ptr[r] = (int32_t)L.piece_b.size();
+        const int32_t a = run_ptr[r], b = run_ptr[r + 1];
+        if (b - a <= kPieceEntries) {
+            for (int32_t q = a; q < b; ++q) L.ent.push_back(q);
+        } else {
+            for (int32_t q = a; q < b; q += kPieceEntries) {
+                L.ent.push_back(-(int32_t)L.piece_b.size() - 1);
+                L.piece_b.push_back(q);
+                L.piece_e.push_back(std::min<int32_t>(q + kPieceEntries, b));
+            }
+        }
+    }
+    L.ent_ptr[runs] = (int32_t)L.ent.size();
+    L.run_piece_ptr[runs] = (int32_t)L.piece_b.size();
+}
+
 static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N, int64_t lo,
                      int64_t hi, mpgnn_plan* p) {
     const int64_t* n1 = ei;
@@ -211,6 +237,43 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
             p->ta_seg[q] = seg_of_edge[by_rel_col[q]];
         }
     }
+
+    // ---- ragged two-level lists (bounded serial work per wave) ---------------------------
+    build_ragged(p->s_ptr, p->seg_l);
+    build_ragged(p->t_ptr, p->t_l);
+    build_ragged(p->rw_ptr, p->rw_l);
+    {
+        // runs of equal (relation, node_2) in ta order
+        std::vector<int32_t> run_ptr{0};
+        std::vector<int32_t> run_key, run_rel;
+        for (int64_t d = 0; d < R; ++d) {
+            for (int32_t q = p->rel_edge_ptr[d]; q < p->rel_edge_ptr[d + 1];) {
+                int32_t q2 = q + 1;
+                while (q2 < p->rel_edge_ptr[d + 1] && p->ta_col[q2] == p->ta_col[q]) ++q2;
+                run_ptr.push_back(q2);
+                run_key.push_back(p->ta_col[q]);
+                run_rel.push_back((int32_t)d);
+                q = q2;
+            }
+        }
+        build_ragged(run_ptr, p->ta_l);
+        const size_t runs = run_key.size();
+        p->ta_key.resize(p->ta_l.ent.size());
+        for (size_t r = 0; r < runs; ++r)
+            for (int32_t q = p->ta_l.ent_ptr[r]; q < p->ta_l.ent_ptr[r + 1]; ++q) p->ta_key[q] = run_key[r];
+        p->rel_ta_ent_ptr.assign(R + 1, 0);
+        p->rel_ta_piece_ptr.assign(R + 1, 0);
+        size_t r = 0;
+        for (int64_t d = 0; d < R; ++d) {
+            p->rel_ta_ent_ptr[d] = p->ta_l.ent_ptr[r];
+            p->rel_ta_piece_ptr[d] = p->ta_l.run_piece_ptr[r];
+            while (r < runs && run_rel[r] == d) ++r;
+        }
+        p->rel_ta_ent_ptr[R] = p->ta_l.ent_ptr[runs];
+        p->rel_ta_piece_ptr[R] = p->ta_l.run_piece_ptr[runs];
+    }
+    p->rel_seg_piece_ptr.assign(R + 1, 0);
+    for (int64_t d = 0; d <= R; ++d) p->rel_seg_piece_ptr[d] = p->seg_l.run_piece_ptr[p->rel_seg_ptr[d]];
 
     // ---- relation-pure tiles and reduction chunks --------------------------------------
     p->rel_tile_ptr.assign(R + 1, 0);
@@ -386,6 +449,14 @@ int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
         {&p->d.tile_begin, &p->tile_begin}, {&p->d.tile_end, &p->tile_end},
         {&p->d.chunk_begin, &p->chunk_begin}, {&p->d.chunk_end, &p->chunk_end},
         {&p->d.rel_chunk_ptr, &p->rel_chunk_ptr}, {&p->d.rel_val32, &p->rel_val32},
+        {&p->d.seg_ent, &p->seg_l.ent}, {&p->d.seg_ent_ptr, &p->seg_l.ent_ptr},
+        {&p->d.seg_pb, &p->seg_l.piece_b}, {&p->d.seg_pe, &p->seg_l.piece_e},
+        {&p->d.t_ent, &p->t_l.ent}, {&p->d.t_ent_ptr, &p->t_l.ent_ptr},
+        {&p->d.t_pb, &p->t_l.piece_b}, {&p->d.t_pe, &p->t_l.piece_e},
+        {&p->d.ta_ent, &p->ta_l.ent}, {&p->d.ta_key, &p->ta_key},
+        {&p->d.ta_pb, &p->ta_l.piece_b}, {&p->d.ta_pe, &p->ta_l.piece_e},
+        {&p->d.rw_ent, &p->rw_l.ent}, {&p->d.rw_ent_ptr, &p->rw_l.ent_ptr},
+        {&p->d.rw_pb, &p->rw_l.piece_b}, {&p->d.rw_pe, &p->rw_l.piece_e},
     };
     size_t total = 0;
     std::vector<size_t> offs;

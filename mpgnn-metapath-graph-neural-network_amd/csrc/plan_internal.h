@@ -15,6 +15,18 @@ namespace mpgnn {
 constexpr int kTileRows = 64;
 // Relation-pure reduction chunks for the weight gradient (outer_accum_kernel).
 constexpr int kChunkRows = 256;
+// Ragged lists: a run (segment / gathered row) longer than this many entries is cut into
+// ordered pieces of at most kPieceEntries, summed by piece_sum_kernel; consumers then add the
+// piece partials in order.  Bounds the serial work of every wave (hub skew).
+constexpr int kPieceEntries = 32;
+
+// Two-level list over a position array: runs r cover positions [run_ptr[r], run_ptr[r+1]).
+// ent[] lists, run by run, either a position p (>= 0) or a piece reference -(k+1); a piece k
+// covers positions [piece_b[k], piece_e[k]).  ent_ptr[r] is the first entry of run r.
+struct RaggedHost {
+    std::vector<int32_t> ent, ent_ptr, piece_b, piece_e;
+    std::vector<int32_t> run_piece_ptr;  // [runs+1] first piece of each run
+};
 
 struct DeviceTables {
     int32_t* e_col = nullptr;
@@ -35,6 +47,11 @@ struct DeviceTables {
     int32_t* chunk_end = nullptr;   // [num_chunks]
     int32_t* rel_chunk_ptr = nullptr; // [nrel+1]
     int32_t* rel_val32 = nullptr;   // [nrel] relation id clamped to int32 (-1 when it does not fit)
+    // ragged lists (see RaggedHost)
+    int32_t *seg_ent = nullptr, *seg_ent_ptr = nullptr, *seg_pb = nullptr, *seg_pe = nullptr;
+    int32_t *t_ent = nullptr, *t_ent_ptr = nullptr, *t_pb = nullptr, *t_pe = nullptr;
+    int32_t *ta_ent = nullptr, *ta_key = nullptr, *ta_pb = nullptr, *ta_pe = nullptr;
+    int32_t *rw_ent = nullptr, *rw_ent_ptr = nullptr, *rw_pb = nullptr, *rw_pe = nullptr;
     void* block = nullptr;          // single hipMalloc holding every table above
     size_t block_bytes = 0;
 };
@@ -67,6 +84,15 @@ struct mpgnn_plan {
     std::vector<int32_t> tile_begin, tile_end; // [num_tiles]
     std::vector<int32_t> chunk_begin, chunk_end; // [num_chunks]
     std::vector<int32_t> rel_val32;            // [nrel]
+
+    // ragged lists: segments over edges (forward gather), node_2 over col-major edges (grad_x,
+    // all relations), (relation, node_2) runs over ta order (grad_x, one relation), node_1
+    // over row-major segments (forward combine)
+    mpgnn::RaggedHost seg_l, t_l, ta_l, rw_l;
+    std::vector<int32_t> ta_key;               // [ta entries] node_2 of each ta entry
+    std::vector<int32_t> rel_ta_ent_ptr;       // [nrel+1] ta entry range of each relation
+    std::vector<int32_t> rel_seg_piece_ptr;    // [nrel+1] seg pieces of each relation
+    std::vector<int32_t> rel_ta_piece_ptr;     // [nrel+1] ta pieces of each relation
 
     int device = -1;
     mpgnn::DeviceTables d;

@@ -76,7 +76,9 @@ __device__ __forceinline__ int readlane(int v, int lane) { return __builtin_amdg
 // position where row j's entries start (so row j covers positions [bnd_j, bnd_{j+1})), and the
 // positions of consecutive rows are contiguous.  Position p contributes source row
 //     src_row(p) = (idx ? idx[p] : p) - idx_off
-// unless a filter rejects it (fidx[p] outside [flo, fhi)).  Lanes span the feature dimension
+// unless a filter rejects it (fidx[p] outside [flo, fhi)).  With a two-level list (g.ent) the
+// wave walks entries instead: an entry >= 0 is a position as above, an entry -(k+1) adds the
+// partial sum P[k - piece_off] of an ordered piece of a long run (piece_sum_kernel).  Lanes span the feature dimension
 // (V floats per lane, T chunks of 64·V columns); every lane adds its columns in position
 // order starting from 0.0f, which is exactly ATen's sequential scatter_add_ into a zeroed
 // output — the sums are bit-identical to the reference.  Each finished row is optionally
@@ -90,6 +92,9 @@ struct GatherSrc {
     int idx_off;
     const int* fidx;   // nullable filter index
     int flo, fhi;
+    const int* ent;    // nullable: two-level entries (position >= 0 | -(piece+1))
+    const float* P;    // piece partial sums [*, F] (rows k - piece_off)
+    int piece_off;
 };
 
 template <int V, int T>
@@ -131,38 +136,45 @@ __device__ void wave_gather(const GatherSrc& g, int bnd, int nrows, const int* c
         flush_row<V, T>(acc, live, cnt_rows, row, lds + row * lda, width, g.F, grow, lane);
     };
 
+    // column offsets of this lane, clamped so that every load is unconditional (the value of
+    // a lane past F is never stored); a load behind a per-entry branch makes hipcc wait for
+    // each entry separately (cdna_hip_programming.md §5 trap (c))
+    int colc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, g.F - V);
+
     for (int pb = p_begin; pb < p_end; pb += 64) {
         const int np = min(64, p_end - pb);
         int my_src = 0;
         bool my_keep = false;
+        bool my_piece = false;
         if (lane < np) {
-            const int p = pb + lane;
-            my_keep = true;
-            if (g.fidx != nullptr) {
-                const int f = g.fidx[p];
-                my_keep = (f >= g.flo) && (f < g.fhi);
+            const int e = g.ent != nullptr ? g.ent[pb + lane] : pb + lane;
+            if (e >= 0) {
+                my_keep = true;
+                if (g.fidx != nullptr) {
+                    const int f = g.fidx[e];
+                    my_keep = (f >= g.flo) && (f < g.fhi);
+                }
+                my_src = (g.idx != nullptr ? g.idx[e] : e) - g.idx_off;
+            } else {
+                my_keep = true;
+                my_piece = true;
+                my_src = -e - 1 - g.piece_off;
             }
-            my_src = (g.idx != nullptr ? g.idx[p] : p) - g.idx_off;
+            if (!my_keep) my_src = 0;  // rejected entry: load a valid row, never added
         }
         const unsigned long long keep = __ballot(my_keep);
+        const unsigned long long from_piece = __ballot(my_piece);
         for (int u = 0; u < np; u += UNR) {
             float v[UNR][T][V];
 #pragma unroll
             for (int uu = 0; uu < UNR; ++uu) {
-                const int q = u + uu;
+                const int q = min(u + uu, np - 1);
+                const int row = readlane(my_src, q);
+                const float* base = (((from_piece >> q) & 1ull) ? g.P : g.src) + (size_t)row * g.F;
 #pragma unroll
-                for (int t = 0; t < T; ++t)
-#pragma unroll
-                    for (int c = 0; c < V; ++c) v[uu][t][c] = 0.0f;
-                if (q < np && ((keep >> q) & 1ull)) {
-                    const int row = readlane(my_src, q);
-                    const float* base = g.src + (size_t)row * g.F;
-#pragma unroll
-                    for (int t = 0; t < T; ++t) {
-                        const int col = (t * 64 + lane) * V;
-                        if (col < g.F) vload<V>(base + col, v[uu][t]);
-                    }
-                }
+                for (int t = 0; t < T; ++t) vload<V>(base + colc[t], v[uu][t]);
             }
 #pragma unroll
             for (int uu = 0; uu < UNR; ++uu) {
@@ -187,17 +199,131 @@ __device__ void wave_gather(const GatherSrc& g, int bnd, int nrows, const int* c
     for (; r < kRowsPerWave; ++r) flush(r);
 }
 
+// ----------------------------------------------------------------------------------------
+// piece_sum_kernel: P[k - k_lo] = Σ_{p in [pb[k], pe[k]), kept} src[idx(p) - idx_off]   (one
+// wave per piece, positions summed in order from 0.0f; a piece has <= kPieceEntries entries)
+// ----------------------------------------------------------------------------------------
+struct PieceArgs {
+    const int* pb;
+    const int* pe;
+    int k_lo, k_hi;
+    const float* src;
+    int F;
+    const int* idx;
+    int idx_off;
+    const int* fidx;
+    int flo, fhi;
+    float* P;
+};
+
+template <int V, int T>
+__global__ __launch_bounds__(kThreads) void piece_sum_kernel(PieceArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int k = a.k_lo + blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (k >= a.k_hi) return;
+    const int p0 = a.pb[k], p1 = a.pe[k];
+    const int np = p1 - p0;  // <= 32 <= 64
+    int my_src = 0;
+    bool my_keep = false;
+    if (lane < np) {
+        const int p = p0 + lane;
+        my_keep = true;
+        if (a.fidx != nullptr) {
+            const int f = a.fidx[p];
+            my_keep = (f >= a.flo) && (f < a.fhi);
+        }
+        my_src = (a.idx != nullptr ? a.idx[p] : p) - a.idx_off;
+    }
+    if (!my_keep) my_src = 0;
+    const unsigned long long keep = __ballot(my_keep);
+    float acc[T][V];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int c = 0; c < V; ++c) acc[t][c] = 0.0f;
+    int colc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, a.F - V);
+    constexpr int UNR = (V * T <= 2 ? 8 : 4);
+    for (int u = 0; u < np; u += UNR) {
+        float v[UNR][T][V];
+#pragma unroll
+        for (int uu = 0; uu < UNR; ++uu) {
+            const float* base = a.src + (size_t)readlane(my_src, min(u + uu, np - 1)) * a.F;
+#pragma unroll
+            for (int t = 0; t < T; ++t) vload<V>(base + colc[t], v[uu][t]);
+        }
+#pragma unroll
+        for (int uu = 0; uu < UNR; ++uu)
+            if (u + uu < np && ((keep >> (u + uu)) & 1ull)) {
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+#pragma unroll
+                    for (int c = 0; c < V; ++c) acc[t][c] += v[uu][t][c];
+            }
+    }
+    float* out = a.P + (size_t)(k - a.k_lo) * a.F;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int col = (t * 64 + lane) * V;
+        if (col < a.F) vstore<V>(out + col, acc[t]);
+    }
+}
+
 // Dense tile loader: rows [row0, row0+64) of A[*, K] into lds[64][lda] with zeros past
-// K (up to width) and past nrows.
+// K (up to width) and past nrows.  All of a thread's loads are issued before any LDS store
+// (float4 when the row stride allows), so the tile costs one memory latency, not 32.
 __device__ void load_dense_tile(const float* __restrict__ A, int K, int row0, int nrows, float* lds,
                                 int lda, int width) {
+    if ((K & 3) == 0 && (width & 3) == 0) {
+        const int w4 = width >> 2;
+        const int total = kTileRows * w4;  // float4 slots
+        constexpr int kBatch = 8;
+        for (int i0 = threadIdx.x; i0 < total; i0 += kBatch * kThreads) {
+            float4 v[kBatch];
+#pragma unroll
+            for (int it = 0; it < kBatch; ++it) {
+                const int i = min(i0 + it * kThreads, total - 1);
+                const int r = i / w4;
+                const int c = (i - r * w4) * 4;
+                const int rr = min(r, max(nrows - 1, 0));
+                const int cc = min(c, K - 4);
+                v[it] = *reinterpret_cast<const float4*>(A + (size_t)(row0 + rr) * K + cc);
+            }
+#pragma unroll
+            for (int it = 0; it < kBatch; ++it) {
+                const int i = i0 + it * kThreads;
+                if (i < total) {
+                    const int r = i / w4;
+                    const int c = (i - r * w4) * 4;
+                    const bool ok = r < nrows && c < K;
+                    *reinterpret_cast<float4*>(lds + r * lda + c) = ok ? v[it] : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+        }
+        return;
+    }
     const int total = kTileRows * width;
-    for (int i = threadIdx.x; i < total; i += kThreads) {
-        const int r = i / width;
-        const int c = i - r * width;
-        float v = 0.0f;
-        if (r < nrows && c < K) v = A[(size_t)(row0 + r) * K + c];
-        lds[r * lda + c] = v;
+    for (int i0 = threadIdx.x; i0 < total; i0 += 8 * kThreads) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * kThreads;
+            v[u] = 0.0f;
+            if (i < total) {
+                const int r = i / width;
+                const int c = i - r * width;
+                if (r < nrows && c < K) v[u] = A[(size_t)(row0 + r) * K + c];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * kThreads;
+            if (i < total) {
+                const int r = i / width;
+                lds[r * lda + (i - r * width)] = v[u];
+            }
+        }
     }
 }
 
@@ -216,89 +342,91 @@ struct BSrc {
     int trans;
 };
 
+// Wave w owns column strip w (32 columns) of the 128-column tile and BOTH 32-row halves, so
+// its two accumulators share every B value; waves whose strip starts past N idle.
 struct MfmaTile {
-    f32x16 acc[2];
-    int mb[2], nb[2];
-    bool valid[2];
+    f32x16 acc0, acc1;  // rows 0..31 / 32..63 of strip `nb`
+    int nb;
+    bool active;
 };
-
-__device__ __forceinline__ void load_b4(const BSrc& b, int k0, int n, float (&out)[4]) {
-    if (n >= b.N) {
-        out[0] = out[1] = out[2] = out[3] = 0.0f;
-        return;
-    }
-    if (b.trans) {
-        const float* p = b.W + (size_t)n * b.ldw + k0;
-        if (k0 + 3 < b.K && (b.ldw & 3) == 0) {
-            const float4 t = *reinterpret_cast<const float4*>(p);
-            out[0] = t.x; out[1] = t.y; out[2] = t.z; out[3] = t.w;
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) out[j] = (k0 + j < b.K) ? p[j] : 0.0f;
-        }
-    } else {
-        const float* p = b.W + (size_t)k0 * b.ldw + n;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) out[j] = (k0 + j < b.K) ? p[(size_t)j * b.ldw] : 0.0f;
-    }
-}
 
 __device__ __forceinline__ void mfma_tile(MfmaTile& mt, const float* A_lds, int lda, int Kp,
                                           const BSrc& b, int n_base, int wave, int lane) {
     const int c = lane & 31;
     const int h = lane >> 5;
-    int ns = (b.N - n_base + 31) / 32;
-    ns = ns > 4 ? 4 : ns;
-    const int nblk = 2 * ns;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int blk = wave + 4 * q;
-        mt.valid[q] = blk < nblk;
-        mt.mb[q] = mt.valid[q] ? blk / ns : 0;
-        mt.nb[q] = mt.valid[q] ? blk % ns : 0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mt.acc[q][r] = 0.0f;
+    for (int r = 0; r < 16; ++r) {
+        mt.acc0[r] = 0.0f;
+        mt.acc1[r] = 0.0f;
     }
-    if (!mt.valid[0]) return;
-    const bool share_b = !mt.valid[1] || mt.nb[1] == mt.nb[0];
-    const int n0 = n_base + mt.nb[0] * 32 + c;
-    const int n1 = n_base + mt.nb[1] * 32 + c;
+    mt.nb = wave;
+    mt.active = n_base + wave * 32 < b.N;
+    if (!mt.active) return;
     const int KH = Kp / 2;
-    const float* a0p = A_lds + (mt.mb[0] * 32 + c) * lda + h * KH;
-    const float* a1p = A_lds + (mt.mb[1] * 32 + c) * lda + h * KH;
-
-    float b0[4] = {0, 0, 0, 0}, b1[4] = {0, 0, 0, 0}, nb0[4] = {0, 0, 0, 0}, nb1[4] = {0, 0, 0, 0};
-    load_b4(b, h * KH, n0, b0);
-    if (!share_b) load_b4(b, h * KH, n1, b1);
-    for (int t = 0; t < KH; t += 4) {
-        const int kn = h * KH + t + 4;
-        if (t + 4 < KH) {
-            load_b4(b, kn, n0, nb0);
-            if (!share_b) load_b4(b, kn, n1, nb1);
-        }
+    const int n = min(n_base + wave * 32 + c, b.N - 1);  // clamped: columns >= N are never stored
+    const float* a0p = A_lds + c * lda + h * KH;
+    const float* a1p = A_lds + (32 + c) * lda + h * KH;
+    const int kb = h * KH;
+    f32x16 acc0 = mt.acc0, acc1 = mt.acc1;
+    // B values are loaded one group of 4 k ahead with clamped addresses; the k < K select is
+    // applied when the group is consumed, so the prefetch is never waited for early.
+    auto mfma8 = [&](const float (&braw)[4], int k0, int t) {
         const float4 a0 = *reinterpret_cast<const float4*>(a0p + t);
-        const float av0[4] = {a0.x, a0.y, a0.z, a0.w};
-        if (mt.valid[1]) {
-            const float4 a1 = *reinterpret_cast<const float4*>(a1p + t);
-            const float av1[4] = {a1.x, a1.y, a1.z, a1.w};
+        const float4 a1 = *reinterpret_cast<const float4*>(a1p + t);
+        float bq[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                mt.acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av0[j], b0[j], mt.acc[0], 0, 0, 0);
-                mt.acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av1[j], share_b ? b0[j] : b1[j], mt.acc[1], 0, 0, 0);
-            }
-        } else {
+        for (int j = 0; j < 4; ++j) bq[j] = (k0 + j < b.K) ? braw[j] : 0.0f;
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, bq[0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, bq[0], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, bq[1], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, bq[1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, bq[2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, bq[2], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, bq[3], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, bq[3], acc1, 0, 0, 0);
+    };
+    if (!b.trans) {
+        // B(k, n) = W[k*ldw + n]: rows k of W, 32 consecutive columns per half-wave
+        const float* wp = b.W + n;
+        auto ld4 = [&](int k0, float (&o)[4]) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                mt.acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av0[j], b0[j], mt.acc[0], 0, 0, 0);
+            for (int j = 0; j < 4; ++j) o[j] = wp[(size_t)min(k0 + j, b.K - 1) * b.ldw];
+        };
+        float b0[4], b1[4];
+        ld4(kb, b0);
+        for (int t = 0; t < KH; t += 8) {  // KH % 8 == 0 (Kp % 16 == 0): ping-pong, no copies
+            ld4(kb + t + 4, b1);
+            mfma8(b0, kb + t, t);
+            ld4(kb + t + 8, b0);
+            mfma8(b1, kb + t + 4, t + 4);
         }
-        if (t + 4 < KH) {
+    } else {
+        // B(k, n) = W[n*ldw + k]: row n of W, four consecutive k per load
+        const float* wp = b.W + (size_t)n * b.ldw;
+        const bool vec = (b.K & 3) == 0 && (b.ldw & 3) == 0;
+        auto ld4 = [&](int k0, float (&o)[4]) {
+            if (vec) {
+                const float4 tv = *reinterpret_cast<const float4*>(wp + min(k0, b.K - 4));
+                o[0] = tv.x;
+                o[1] = tv.y;
+                o[2] = tv.z;
+                o[3] = tv.w;
+            } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                b0[j] = nb0[j];
-                b1[j] = nb1[j];
+                for (int j = 0; j < 4; ++j) o[j] = wp[min(k0 + j, b.K - 1)];
             }
+        };
+        float b0[4], b1[4];
+        ld4(kb, b0);
+        for (int t = 0; t < KH; t += 8) {
+            ld4(kb + t + 4, b1);
+            mfma8(b0, kb + t, t);
+            ld4(kb + t + 8, b0);
+            mfma8(b1, kb + t + 4, t + 4);
         }
     }
+    mt.acc0 = acc0;
+    mt.acc1 = acc1;
 }
 
 // ----------------------------------------------------------------------------------------
@@ -311,12 +439,15 @@ struct SegTileArgs {
     int gather_kind;     // 0: mean of src[e_col[e]] over the segment's edges; 1: src[s_row[s]]
     const float* src;
     int F;               // gather width = K of the MFMA
-    const int* s_ptr;
+    const int* s_ptr;    // segment boundaries over edges (exact order) or over ragged entries
     const int* e_col;
     const int* s_row;
     const int* s_cnt;
     const int* s_rel;
     const int* s_pos;
+    const int* ent;      // nullable: ragged entries (s_ptr then indexes entries)
+    const float* P;      // piece partials of long segments
+    int piece_off;
     const float* W;      // nullable: no transform (segment means only)
     int w_per_rel;       // W_r = W + s_rel[s] * K * N
     int trans;
@@ -326,12 +457,13 @@ struct SegTileArgs {
     int y_div;           // divide the MFMA result by cnt (dgrad)
     int sel_b;
     float* H;            // nullable: copy of the gathered tile rows, row = s - sel_b, width F
+    int ablate;          // debug (MPGNN_OPT_ABLATE): 1 = skip gather, 2 = skip MFMA; wrong results
 };
 
 template <int V, int T>
 __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int Kp = round_up(a.F, 8);
+    const int Kp = round_up(a.F, 16);
     const int lda = Kp + 4;
     int* s_dst = reinterpret_cast<int*>(smem);            // [64] destination row of each tile row
     float* s_scale = smem + kTileRows;                    // [64] cnt as float (dgrad)
@@ -363,9 +495,15 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
     g.idx_off = 0;
     int bnd = 0;
     const int* cnt_rows = nullptr;
+    g.ent = nullptr;
+    g.P = nullptr;
+    g.piece_off = 0;
     if (a.gather_kind == 0) {
         if (lane <= wn) bnd = a.s_ptr[sw + lane];
         g.idx = a.e_col;
+        g.ent = a.ent;
+        g.P = a.P;
+        g.piece_off = a.piece_off;
         cnt_rows = a.s_cnt + sw;
     } else {
         bnd = sw + (lane <= wn ? lane : wn);
@@ -373,10 +511,16 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
     }
     // saved segment means (backward): row s - sel_b of H, consecutive for the wave's rows
     float* gout = (a.H != nullptr && blockIdx.y == 0) ? a.H + (size_t)(sw - a.sel_b) * a.F : nullptr;
-    wave_gather<V, T, (V * T <= 2 ? 8 : 4)>(g, bnd, wn, cnt_rows, A_lds + wr0 * lda, lda, Kp, gout, a.F,
-                                            lane);
+    if (!(a.ablate & 1))
+        wave_gather<V, T, (V * T <= 2 ? 8 : 4)>(g, bnd, wn, cnt_rows, A_lds + wr0 * lda, lda, Kp, gout, a.F,
+                                                lane);
     __syncthreads();
     if (a.W == nullptr) return;
+    if (a.ablate & 2) {  // keep the gathered tile observable, skip the contraction
+        if (threadIdx.x < kTileRows && threadIdx.x < nrows)
+            a.Y[(size_t)s_dst[threadIdx.x] * a.N] = A_lds[threadIdx.x * lda];
+        return;
+    }
 
     // ---- MFMA phase --------------------------------------------------------------------
     const float* W = a.W;
@@ -393,18 +537,20 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
 
     const int c = lane & 31;
     const int h = lane >> 5;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        if (!mt.valid[q]) continue;
-        const int col = n_base + mt.nb[q] * 32 + c;
-        if (col >= a.N) continue;
+    const int col = n_base + mt.nb * 32 + c;
+    if (mt.active && col < a.N) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int row = mt.mb[q] * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
             if (row < nrows) {
-                float v = mt.acc[q][r];
+                float v = mt.acc0[r];
                 if (a.y_div) v = v / s_scale[row];
                 a.Y[(size_t)s_dst[row] * a.N + col] = v;
+            }
+            if (row + 32 < nrows) {
+                float v = mt.acc1[r];
+                if (a.y_div) v = v / s_scale[row + 32];
+                a.Y[(size_t)s_dst[row + 32] * a.N + col] = v;
             }
         }
     }
@@ -423,6 +569,9 @@ struct RowTileArgs {
     int idx_off;
     const int* fidx;
     int flo, fhi;
+    const int* ent;     // nullable: ragged entries (ptr / keys then index entries)
+    const float* P;     // piece partials
+    int piece_off;
     const float* gsrc;  // gathered rows, width G
     int G;              // output width
     const float* A;     // dense rows [N, K] (nullable: no root term)
@@ -447,7 +596,7 @@ __global__ __launch_bounds__(kThreads) void row_tile_kernel(RowTileArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int Gp = round_up(a.G, 4);
     const int ldg = Gp;
-    const int Kp = round_up(a.K > 0 ? a.K : 1, 8);
+    const int Kp = round_up(a.K > 0 ? a.K : 1, 16);
     const int lda = Kp + 4;
     float* S_lds = smem;                         // [64][ldg]
     float* A_lds = smem + kTileRows * ldg;       // [64][lda]
@@ -475,6 +624,9 @@ __global__ __launch_bounds__(kThreads) void row_tile_kernel(RowTileArgs a) {
     g.fidx = a.fidx;
     g.flo = a.flo;
     g.fhi = a.fhi;
+    g.ent = a.ent;
+    g.P = a.P;
+    g.piece_off = a.piece_off;
     wave_gather<V, T, (V * T <= 2 ? 8 : 4)>(g, bnd, wn, nullptr, S_lds + wr0 * ldg, ldg, Gp, nullptr, 0,
                                             lane);
     const bool has_root = a.A != nullptr && a.W != nullptr;
@@ -493,23 +645,23 @@ __global__ __launch_bounds__(kThreads) void row_tile_kernel(RowTileArgs a) {
         b.ldw = a.trans ? a.K : a.G;
         MfmaTile mt;
         mfma_tile(mt, A_lds, lda, Kp, b, n_base, wave, lane);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            if (!mt.valid[q]) continue;
-            const int col = n_base + mt.nb[q] * 32 + c;
-            if (col >= a.G) continue;
+        const int col = n_base + mt.nb * 32 + c;
+        if (mt.active && col < a.G) {
             const float bv = a.bias != nullptr ? a.bias[col] : 0.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = mt.mb[q] * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (row < nrows) {
-                    const int i = row0 + row;
-                    float v = S_lds[row * ldg + col];
-                    if (i >= a.row_lo && i < a.row_hi) {
-                        v = v + mt.acc[q][r];
-                        if (a.bias != nullptr) v = v + bv;
+#pragma unroll
+                for (int half = 0; half < 2; ++half) {
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h + 32 * half;
+                    if (row < nrows) {
+                        const int i = row0 + row;
+                        float v = S_lds[row * ldg + col];
+                        if (i >= a.row_lo && i < a.row_hi) {
+                            v = v + (half ? mt.acc1[r] : mt.acc0[r]);
+                            if (a.bias != nullptr) v = v + bv;
+                        }
+                        a.out[(size_t)i * a.G + col] = v;
                     }
-                    a.out[(size_t)i * a.G + col] = v;
                 }
             }
         }
@@ -724,7 +876,7 @@ static bool pick_vt(int F, int* V, int* T) {
 
 template <int V, int T>
 static void launch_seg(const SegTileArgs& a, int ntiles, int ncoltiles, hipStream_t st) {
-    const int Kp = round_up(a.F, 8);
+    const int Kp = round_up(a.F, 16);
     const size_t lds = (size_t)(2 * kTileRows + kTileRows * (Kp + 4)) * sizeof(float);
     hipLaunchKernelGGL((seg_tile_kernel<V, T>), dim3(ntiles, ncoltiles), dim3(kThreads), lds, st, a);
 }
@@ -732,17 +884,29 @@ static void launch_seg(const SegTileArgs& a, int ntiles, int ncoltiles, hipStrea
 template <int V, int T>
 static void launch_row(const RowTileArgs& a, int nrowtiles, int ncoltiles, hipStream_t st) {
     const int Gp = round_up(a.G, 4);
-    const int Kp = round_up(a.K > 0 ? a.K : 1, 8);
+    const int Kp = round_up(a.K > 0 ? a.K : 1, 16);
     const bool has_root = a.A != nullptr && a.W != nullptr;
     const size_t lds = (size_t)(kTileRows * Gp + (has_root ? kTileRows * (Kp + 4) : 0)) * sizeof(float);
     hipLaunchKernelGGL((row_tile_kernel<V, T>), dim3(nrowtiles, ncoltiles), dim3(kThreads), lds, st, a);
 }
+
+template <int V, int T>
+static void launch_piece(const PieceArgs& a, hipStream_t st) {
+    const int n = a.k_hi - a.k_lo;
+    hipLaunchKernelGGL((piece_sum_kernel<V, T>), dim3((n + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
+}
+
+static bool g_exact_order = false;  // MPGNN_OPT_EXACT_ORDER: no ragged pieces anywhere
+static int g_ablate = 0;            // MPGNN_OPT_ABLATE (debug/profiling only)
 
 struct Selection {
     int64_t d_lo = 0, d_hi = 0;
     int sel_b = 0, sel_e = 0;
     int t_lo = 0, t_hi = 0;
     int c_lo = 0, c_hi = 0;
+    int sp_lo = 0, sp_hi = 0;   // seg-list pieces of the selection
+    int tap_lo = 0, tap_hi = 0; // ta-list pieces (mode SINGLE)
+    int ta_e_lo = 0, ta_e_hi = 0; // ta entry range (mode SINGLE)
     bool all_segments = false;  // selection covers every local segment
 };
 
@@ -756,6 +920,12 @@ static int32_t make_selection(const mpgnn_plan* p, int32_t mode, int64_t relatio
     s->t_hi = p->rel_tile_ptr[s->d_hi];
     s->c_lo = p->rel_chunk_ptr[s->d_lo];
     s->c_hi = p->rel_chunk_ptr[s->d_hi];
+    s->sp_lo = p->rel_seg_piece_ptr[s->d_lo];
+    s->sp_hi = p->rel_seg_piece_ptr[s->d_hi];
+    s->tap_lo = p->rel_ta_piece_ptr[s->d_lo];
+    s->tap_hi = p->rel_ta_piece_ptr[s->d_hi];
+    s->ta_e_lo = p->rel_ta_ent_ptr[s->d_lo];
+    s->ta_e_hi = p->rel_ta_ent_ptr[s->d_hi];
     s->all_segments = (s->sel_b == 0 && s->sel_e == p->S);
     return MPGNN_OK;
 }
@@ -777,8 +947,11 @@ static RootChunks root_chunks(int64_t lo, int64_t hi) {
     return r;
 }
 
+// Workspace: forward and backward regions are used by different calls, so they overlap.
 struct WsLayout {
-    size_t y = 0, g = 0, h = 0, p = 0, proot = 0, pb = 0, total = 0;
+    size_t y = 0, pseg = 0, prw = 0;                       // forward
+    size_t g = 0, h = 0, pdx = 0, p = 0, proot = 0, pb = 0; // backward
+    size_t total = 0;
 };
 
 static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s, int F_in, int F_out,
@@ -786,14 +959,19 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
     WsLayout w;
     const size_t S_sel = (size_t)(s.sel_e - s.sel_b);
     const size_t y_rows = (mode == MPGNN_MODE_ALL) ? (size_t)p->S : S_sel;
-    const size_t fwd = align256(y_rows * F_out * sizeof(float));
     size_t off = 0;
+    w.y = off; off += align256(y_rows * F_out * sizeof(float));
+    w.pseg = off; off += align256((size_t)(s.sp_hi - s.sp_lo) * F_in * sizeof(float));
+    w.prw = off; off += align256((mode == MPGNN_MODE_ALL ? p->rw_l.piece_b.size() : 0) * F_out * sizeof(float));
+    const size_t fwd = off;
+    off = 0;
+    const size_t dx_pieces = (mode == MPGNN_MODE_ALL) ? p->t_l.piece_b.size() : (size_t)(s.tap_hi - s.tap_lo);
     w.g = off; off += align256(S_sel * F_in * sizeof(float));
     w.h = off; off += align256(S_sel * F_in * sizeof(float));
+    w.pdx = off; off += align256(dx_pieces * F_in * sizeof(float));
     w.p = off; off += align256((size_t)(s.c_hi - s.c_lo) * F_in * F_out * sizeof(float));
     w.proot = off; off += align256((size_t)rc.n * F_in * F_out * sizeof(float));
     w.pb = off; off += align256((size_t)rc.n * F_out * sizeof(float));
-    w.y = 0;
     w.total = std::max<size_t>(std::max(fwd, off), 256);
     return w;
 }
@@ -817,11 +995,79 @@ static void clamp_rows(const mpgnn_plan* p, int64_t* lo, int64_t* hi) {
     *hi = std::max<int64_t>(*lo, std::min<int64_t>(*hi, p->N));
 }
 
+// Forward segment tiles: Y[seg] = mean(src over seg) @ W_rel(seg)   (W == nullptr: H only)
+static int32_t run_seg_forward(const mpgnn_plan* p, int32_t mode, const Selection& s, const float* x, int F_in,
+                               const float* W, int F_out, float* Y, float* H, float* Pseg, bool exact,
+                               int kind, hipStream_t strm) {
+    const int ntiles = s.t_hi - s.t_lo;
+    if (ntiles == 0) return MPGNN_OK;
+    int V, T;
+    pick_vt(F_in, &V, &T);
+    const bool ragged = !exact && s.sp_hi > s.sp_lo;
+    if (ragged) {
+        PieceArgs pa{};
+        pa.pb = p->d.seg_pb;
+        pa.pe = p->d.seg_pe;
+        pa.k_lo = s.sp_lo;
+        pa.k_hi = s.sp_hi;
+        pa.src = x;
+        pa.F = F_in;
+        pa.idx = p->d.e_col;
+        pa.P = Pseg;
+        TimedLaunch tl(MPGNN_K_PIECE, strm);
+        MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
+        int32_t st = hip_check(hipGetLastError(), "piece_sum_kernel(seg) launch");
+        if (st != MPGNN_OK) return st;
+    }
+    SegTileArgs a{};
+    a.tile_begin = p->d.tile_begin;
+    a.tile_end = p->d.tile_end;
+    a.tile_off = s.t_lo;
+    a.gather_kind = 0;
+    a.src = x;
+    a.F = F_in;
+    a.s_ptr = ragged ? p->d.seg_ent_ptr : p->d.s_ptr;
+    a.e_col = p->d.e_col;
+    a.s_row = p->d.s_row;
+    a.s_cnt = p->d.s_cnt;
+    a.s_rel = p->d.s_rel;
+    a.s_pos = p->d.s_pos;
+    a.ent = ragged ? p->d.seg_ent : nullptr;
+    a.P = Pseg;
+    a.piece_off = s.sp_lo;
+    a.W = W;
+    a.w_per_rel = (mode == MPGNN_MODE_ALL);
+    a.trans = 0;
+    a.N = W ? F_out : 1;
+    a.Y = Y;
+    a.y_use_pos = (mode == MPGNN_MODE_ALL);
+    a.y_div = 0;
+    a.sel_b = s.sel_b;
+    a.H = H;
+    a.ablate = g_ablate;
+    const int ncol = W ? (F_out + kColTile - 1) / kColTile : 1;
+    TimedLaunch tl(kind, strm);
+    MPGNN_VT_DISPATCH(V, T, launch_seg, a, ntiles, ncol, strm);
+    return hip_check(hipGetLastError(), "seg_tile_kernel launch");
+}
+
 }  // namespace mpgnn
 
 using namespace mpgnn;
 
 extern "C" {
+
+int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_EXACT_ORDER) {
+        g_exact_order = value != 0;
+        return MPGNN_OK;
+    }
+    if (option == MPGNN_OPT_ABLATE) {
+        g_ablate = (int)value;
+        return MPGNN_OK;
+    }
+    return arg_error("unknown option " + std::to_string(option));
+}
 
 int32_t mpgnn_rel_mean_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R,
                            const float* x, int32_t F, float* h, void* stream) {
@@ -829,34 +1075,11 @@ int32_t mpgnn_rel_mean_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, 
     if (st != MPGNN_OK) return st;
     Selection s;
     if ((st = make_selection(p, mode, relation, R, &s)) != MPGNN_OK) return st;
-    const int ntiles = s.t_hi - s.t_lo;
-    if (ntiles == 0) return MPGNN_OK;
+    if (s.t_hi == s.t_lo) return MPGNN_OK;
     if (!x || !h) return arg_error("NULL x or h");
-    int V, T;
-    pick_vt(F, &V, &T);
-    SegTileArgs a{};
-    a.tile_begin = p->d.tile_begin;
-    a.tile_end = p->d.tile_end;
-    a.tile_off = s.t_lo;
-    a.gather_kind = 0;
-    a.src = x;
-    a.F = F;
-    a.s_ptr = p->d.s_ptr;
-    a.e_col = p->d.e_col;
-    a.s_row = p->d.s_row;
-    a.s_cnt = p->d.s_cnt;
-    a.s_rel = p->d.s_rel;
-    a.s_pos = p->d.s_pos;
-    a.W = nullptr;
-    a.N = 1;
-    a.sel_b = s.sel_b;
-    a.H = h;
-    hipStream_t strm = static_cast<hipStream_t>(stream);
-    {
-        TimedLaunch tl(MPGNN_K_MEAN, strm);
-        MPGNN_VT_DISPATCH(V, T, launch_seg, a, ntiles, 1, strm);
-    }
-    return hip_check(hipGetLastError(), "seg_tile_kernel launch");
+    // always in exact edge order: bit-identical to PyG's scatter_add_ mean
+    return run_seg_forward(p, mode, s, x, F, nullptr, 1, nullptr, h, nullptr, true, MPGNN_K_MEAN,
+                           static_cast<hipStream_t>(stream));
 }
 
 int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R,
@@ -882,83 +1105,78 @@ int32_t mpgnn_rgcn_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
     if ((st = make_selection(p, mode, relation, R, &s)) != MPGNN_OK) return st;
     if (p->N == 0) return MPGNN_OK;
     if (!x || !weight || !out) return arg_error("NULL x, weight or out");
+    if (!workspace) return arg_error("NULL workspace");
     clamp_rows(p, &row_lo, &row_hi);
     hipStream_t strm = static_cast<hipStream_t>(stream);
-    const int ntiles = s.t_hi - s.t_lo;
-    float* Y = static_cast<float*>(workspace);
-    if (ntiles > 0 && !Y) return arg_error("NULL workspace");
+    const RootChunks rc = root_chunks(row_lo, row_hi);
+    const WsLayout w = ws_layout(p, mode, s, F_in, F_out, rc);
+    char* ws = static_cast<char*>(workspace);
+    float* Y = reinterpret_cast<float*>(ws + w.y);
+    const bool exact = g_exact_order;
     const int ncol = (F_out + kColTile - 1) / kColTile;
 
-    // 1) Y[seg] = mean(x over seg) @ W_rel(seg)
-    if (ntiles > 0) {
-        int V, T;
-        pick_vt(F_in, &V, &T);
-        SegTileArgs a{};
-        a.tile_begin = p->d.tile_begin;
-        a.tile_end = p->d.tile_end;
-        a.tile_off = s.t_lo;
-        a.gather_kind = 0;
-        a.src = x;
-        a.F = F_in;
-        a.s_ptr = p->d.s_ptr;
-        a.e_col = p->d.e_col;
-        a.s_row = p->d.s_row;
-        a.s_cnt = p->d.s_cnt;
-        a.s_rel = p->d.s_rel;
-        a.s_pos = p->d.s_pos;
-        a.W = weight;
-        a.w_per_rel = (mode == MPGNN_MODE_ALL);
-        a.trans = 0;
-        a.N = F_out;
-        a.Y = Y;
-        a.y_use_pos = (mode == MPGNN_MODE_ALL);
-        a.y_div = 0;
-        a.sel_b = s.sel_b;
-        a.H = h_save;
-        TimedLaunch tl(MPGNN_K_SEG_FWD, strm);
-        MPGNN_VT_DISPATCH(V, T, launch_seg, a, ntiles, ncol, strm);
-        if ((st = hip_check(hipGetLastError(), "seg_tile_kernel launch")) != MPGNN_OK) return st;
-    }
+    // 1) Y[seg] = mean(x over seg) @ W_rel(seg)     (+ h_save = the means)
+    st = run_seg_forward(p, mode, s, x, F_in, weight, F_out, Y, h_save, reinterpret_cast<float*>(ws + w.pseg),
+                         exact, MPGNN_K_SEG_FWD, strm);
+    if (st != MPGNN_OK) return st;
 
     // 2) out[i] = Σ_{seg of row i, relation order} Y[seg] + x[i] @ root + bias
-    {
-        int V, T;
-        pick_vt(F_out, &V, &T);
-        RowTileArgs a{};
-        a.N = (int)p->N;
-        if (mode == MPGNN_MODE_ALL) {
-            a.list_kind = 0;
-            a.ptr = p->d.rw_ptr;
-            a.idx = nullptr;
-            a.idx_off = 0;
-            a.fidx = s.all_segments ? nullptr : p->d.rw_seg;
-            a.flo = s.sel_b;
-            a.fhi = s.sel_e;
-        } else {
-            a.list_kind = 1;
-            a.keys = p->d.s_row;
-            a.kb = s.sel_b;
-            a.ke = s.sel_e;
-            a.idx = nullptr;
-            a.idx_off = s.sel_b;
-            a.fidx = nullptr;
+    int V, T;
+    pick_vt(F_out, &V, &T);
+    RowTileArgs a{};
+    a.N = (int)p->N;
+    a.P = reinterpret_cast<float*>(ws + w.prw);
+    if (mode == MPGNN_MODE_ALL) {
+        const bool ragged = !exact && !p->rw_l.piece_b.empty();
+        const int* fidx = s.all_segments ? nullptr : p->d.rw_seg;
+        if (ragged) {
+            PieceArgs pa{};
+            pa.pb = p->d.rw_pb;
+            pa.pe = p->d.rw_pe;
+            pa.k_lo = 0;
+            pa.k_hi = (int)p->rw_l.piece_b.size();
+            pa.src = Y;
+            pa.F = F_out;
+            pa.fidx = fidx;
+            pa.flo = s.sel_b;
+            pa.fhi = s.sel_e;
+            pa.P = reinterpret_cast<float*>(ws + w.prw);
+            TimedLaunch tl(MPGNN_K_PIECE, strm);
+            MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
+            if ((st = hip_check(hipGetLastError(), "piece_sum_kernel(rw) launch")) != MPGNN_OK) return st;
         }
-        a.gsrc = Y;
-        a.G = F_out;
-        a.A = root ? x : nullptr;
-        a.K = F_in;
-        a.W = root;
-        a.trans = 0;
-        a.bias = bias;
-        a.row_lo = (int)row_lo;
-        a.row_hi = (int)row_hi;
-        a.out = out;
-        const int nrt = (int)((p->N + kTileRows - 1) / kTileRows);
-        TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
-        MPGNN_VT_DISPATCH(V, T, launch_row, a, nrt, ncol, strm);
-        if ((st = hip_check(hipGetLastError(), "row_tile_kernel launch")) != MPGNN_OK) return st;
+        a.list_kind = 0;
+        a.ptr = ragged ? p->d.rw_ent_ptr : p->d.rw_ptr;
+        a.ent = ragged ? p->d.rw_ent : nullptr;
+        a.idx = nullptr;
+        a.idx_off = 0;
+        a.fidx = fidx;
+        a.flo = s.sel_b;
+        a.fhi = s.sel_e;
+    } else {
+        a.list_kind = 1;  // at most one segment per row: no pieces
+        a.keys = p->d.s_row;
+        a.kb = s.sel_b;
+        a.ke = s.sel_e;
+        a.idx = nullptr;
+        a.idx_off = s.sel_b;
+        a.fidx = nullptr;
+        a.ent = nullptr;
     }
-    return MPGNN_OK;
+    a.gsrc = Y;
+    a.G = F_out;
+    a.A = root ? x : nullptr;
+    a.K = F_in;
+    a.W = root;
+    a.trans = 0;
+    a.bias = bias;
+    a.row_lo = (int)row_lo;
+    a.row_hi = (int)row_hi;
+    a.out = out;
+    const int nrt = (int)((p->N + kTileRows - 1) / kTileRows);
+    TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
+    MPGNN_VT_DISPATCH(V, T, launch_row, a, nrt, ncol, strm);
+    return hip_check(hipGetLastError(), "row_tile_kernel launch");
 }
 
 int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
@@ -978,8 +1196,8 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
     char* ws = static_cast<char*>(workspace);
     if (!ws) return arg_error("NULL workspace");
     const int ntiles = s.t_hi - s.t_lo;
-    const int S_sel = s.sel_e - s.sel_b;
     const size_t wsize = (size_t)F_in * F_out;
+    const bool exact = g_exact_order;
 
     // ---- grad_x = Σ_r A_rᵀ ((dout @ W_rᵀ) / cnt) + dout @ rootᵀ ----------------------
     if (grad_x != nullptr && p->N > 0) {
@@ -1018,19 +1236,62 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         pick_vt(F_in, &V, &T);
         RowTileArgs a{};
         a.N = (int)p->N;
+        a.P = reinterpret_cast<float*>(ws + w.pdx);
+        PieceArgs pa{};
+        pa.src = G;
+        pa.F = F_in;
+        pa.idx_off = s.sel_b;
+        pa.P = reinterpret_cast<float*>(ws + w.pdx);
         if (mode == MPGNN_MODE_ALL) {
+            const bool ragged = !exact && !p->t_l.piece_b.empty();
+            const int* fidx = s.all_segments ? nullptr : p->d.t_seg;
+            if (ragged && ntiles > 0) {
+                pa.pb = p->d.t_pb;
+                pa.pe = p->d.t_pe;
+                pa.k_lo = 0;
+                pa.k_hi = (int)p->t_l.piece_b.size();
+                pa.idx = p->d.t_seg;
+                pa.fidx = fidx;
+                pa.flo = s.sel_b;
+                pa.fhi = s.sel_e;
+                TimedLaunch tl(MPGNN_K_PIECE, strm);
+                MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
+                if ((st = hip_check(hipGetLastError(), "piece_sum_kernel(t) launch")) != MPGNN_OK) return st;
+            }
             a.list_kind = 0;
-            a.ptr = p->d.t_ptr;
+            a.ptr = ragged ? p->d.t_ent_ptr : p->d.t_ptr;
+            a.ent = ragged ? p->d.t_ent : nullptr;
             a.idx = p->d.t_seg;
             a.idx_off = s.sel_b;
-            a.fidx = s.all_segments ? nullptr : p->d.t_seg;
+            a.fidx = fidx;
             a.flo = s.sel_b;
             a.fhi = s.sel_e;
+            a.piece_off = 0;
         } else {
+            const bool ragged = !exact;
+            if (ragged && s.tap_hi > s.tap_lo) {
+                pa.pb = p->d.ta_pb;
+                pa.pe = p->d.ta_pe;
+                pa.k_lo = s.tap_lo;
+                pa.k_hi = s.tap_hi;
+                pa.idx = p->d.ta_seg;
+                TimedLaunch tl(MPGNN_K_PIECE, strm);
+                MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
+                if ((st = hip_check(hipGetLastError(), "piece_sum_kernel(ta) launch")) != MPGNN_OK) return st;
+            }
             a.list_kind = 1;
-            a.keys = p->d.ta_col;
-            a.kb = (s.d_hi > s.d_lo) ? p->rel_edge_ptr[s.d_lo] : 0;
-            a.ke = (s.d_hi > s.d_lo) ? p->rel_edge_ptr[s.d_hi] : 0;
+            if (ragged) {
+                a.keys = p->d.ta_key;
+                a.kb = s.ta_e_lo;
+                a.ke = s.ta_e_hi;
+                a.ent = p->d.ta_ent;
+                a.piece_off = s.tap_lo;
+            } else {
+                a.keys = p->d.ta_col;
+                a.kb = (s.d_hi > s.d_lo) ? p->rel_edge_ptr[s.d_lo] : 0;
+                a.ke = (s.d_hi > s.d_lo) ? p->rel_edge_ptr[s.d_hi] : 0;
+                a.ent = nullptr;
+            }
             a.idx = p->d.ta_seg;
             a.idx_off = s.sel_b;
             a.fidx = nullptr;
@@ -1068,7 +1329,9 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
             const float* H = h_save;
             if (H == nullptr) {
                 float* Hw = reinterpret_cast<float*>(ws + w.h);
-                if ((st = mpgnn_rel_mean_fwd(p, mode, relation, R, x, F_in, Hw, stream)) != MPGNN_OK) return st;
+                st = run_seg_forward(p, mode, s, x, F_in, nullptr, 1, nullptr, Hw, reinterpret_cast<float*>(ws + w.pdx),
+                                     true, MPGNN_K_MEAN, strm);
+                if (st != MPGNN_OK) return st;
                 H = Hw;
             }
             float* P = reinterpret_cast<float*>(ws + w.p);
@@ -1109,7 +1372,6 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
             }
             if ((st = hip_check(hipGetLastError(), "reduce_slabs_kernel(dW) launch")) != MPGNN_OK) return st;
         }
-        (void)S_sel;
     }
 
     // ---- grad_root = xᵀ dout, grad_bias = Σ dout  (rows [row_lo, row_hi)) -------------

@@ -233,28 +233,36 @@ def test_net_forward_backward_vs_oracle(name):
 
 def test_adam_training_steps_track_oracle():
     """mpgnn_train semantics (main.py:1055-1082): full-batch NLL on train_idx, backward, Adam
-    (lr 0.01, wd 5e-4, main.py:1119). Five steps on GPU vs the same steps on the CPU oracle."""
+    (lr 0.01, wd 5e-4, main.py:1119). Five steps on GPU vs the same steps on the CPU oracle.
+    Adam normalises each gradient by its running RMS, so elements whose gradient is ~0 move by
+    ±lr on rounding noise alone: the check is on the loss trajectory (1e-4 rel) and on the
+    first step's parameters, not on every element after five steps."""
     g = data.config_graph("C1")
     torch.manual_seed(30)
     net = mpgnn_amd.MPNetm(128, 64, 3, 64, 3, 2, [[1, 0], [2]]).eval()   # eval: no dropout RNG
     ref_params = {k: v.detach().clone().requires_grad_(True) for k, v in net.state_dict().items()}
+    names = list(ref_params.keys())
     y = torch.randint(0, 3, (1000,), generator=torch.Generator().manual_seed(1))
     train_idx = torch.arange(0, 1000, 2)
     opt_ref = torch.optim.Adam(list(ref_params.values()), lr=0.01, weight_decay=0.0005)
     netg = net.to(DEV)
     opt = torch.optim.Adam(netg.parameters(), lr=0.01, weight_decay=0.0005)
     xg, eig, etg = g.x.to(DEV), g.edge_index.to(DEV), g.edge_type.to(DEV)
-    for _ in range(5):
+    for step in range(5):
         opt_ref.zero_grad()
         out = orc.mpnetm_forward(ref_params, g.x, g.edge_index, g.edge_type, [[1, 0], [2]])
-        torch.nn.functional.nll_loss(out[train_idx], y[train_idx]).backward()
+        loss_ref = torch.nn.functional.nll_loss(out[train_idx], y[train_idx])
+        loss_ref.backward()
         opt_ref.step()
         opt.zero_grad()
         outg = netg(xg, eig, etg)
-        torch.nn.functional.nll_loss(outg[train_idx.to(DEV)], y[train_idx].to(DEV)).backward()
+        loss = torch.nn.functional.nll_loss(outg[train_idx.to(DEV)], y[train_idx].to(DEV))
+        loss.backward()
+        if step == 0:  # before any update the gradients must agree (1e-4)
+            for k, p in zip(names, netg.parameters()):
+                rel_close(p.grad, ref_params[k].grad, what="grad " + k)
         opt.step()
-    for k, p in netg.state_dict().items():
-        rel_close(p, ref_params[k], tol=1e-3, what=k)
+        assert abs(float(loss) - float(loss_ref)) <= 1e-4 * abs(float(loss_ref)), (step, float(loss), float(loss_ref))
 
 
 # ------------------------------------------------------------------------------------------
@@ -323,3 +331,33 @@ def test_empty_graph_and_isolated_rows():
     out = conv(x, ei, et)
     ref = x.cpu() @ conv.root.detach().cpu() + conv.bias.detach().cpu()
     rel_close(out, ref, what="out")
+
+
+def test_exact_order_option_and_ragged_pieces_agree():
+    """Default path sums runs > 32 entries as ordered pieces; MPGNN_OPT_EXACT_ORDER restores
+    the reference's sequential order. Both must match the oracle. (For hub rows that sum ~6000
+    terms the sequential order itself carries ~3e-5 relative rounding error; the piece order
+    is the more accurate of the two.)"""
+    from mpgnn_amd import _lib
+    g = data.config_graph("fb15k237")
+    torch.manual_seed(0)
+    conv = mpgnn_amd.RGCNConv(128, 64, g.num_relations, flow="target_to_source").to(DEV)
+    xg = g.x.to(DEV).requires_grad_(True)
+    eig, etg = g.edge_index.to(DEV), g.edge_type.to(DEV)
+    res = []
+    try:
+        for exact in (False, True):
+            _lib.set_exact_order(exact)
+            xg.grad = None
+            conv.zero_grad()
+            o = conv(xg, eig, etg)
+            o.backward(torch.ones_like(o))
+            res.append((o.detach().clone(), xg.grad.clone(), conv.weight.grad.clone()))
+    finally:
+        _lib.set_exact_order(False)
+    for a, b in zip(*res):
+        rel_close(a, b, what="fast vs exact")
+    params = {k: v.detach().cpu() for k, v in conv.state_dict().items()}
+    ref = orc.rgcn_forward(g.x, g.edge_index, g.edge_type, params["weight"], params["root"], params["bias"])
+    rel_close(res[0][0], ref, what="fast vs oracle")
+    rel_close(res[1][0], ref, what="exact vs oracle")
