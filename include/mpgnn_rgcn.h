@@ -159,7 +159,8 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
  * bit-identical to the reference either way. mpgnn_rel_mean_fwd is always exact. */
 enum mpgnn_option {
     MPGNN_OPT_EXACT_ORDER = 0,
-    MPGNN_OPT_ABLATE = 1 /* profiling only: 1 skips the forward gather, 2 the forward MFMA (wrong results) */
+    MPGNN_OPT_ABLATE = 1, /* profiling only: bits skip phases of the forward tile kernel (wrong results) */
+    MPGNN_OPT_STAMPS = 2  /* profiling only: device pointer of a u64 [blocks][4 waves][8] timeline buffer, 0 = off */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 
@@ -179,6 +180,11 @@ enum mpgnn_kernel_kind {
     MPGNN_K_COUNT = 8
 };
 int32_t mpgnn_timing_enable(int32_t on);
+/* Debug: workgroups per CU the runtime admits at width F for the gather-tile kernel
+ * (seg_tile_kernel) and the persistent tile GEMM (tile_gemm_kernel), and the grid the
+ * latter is launched with. */
+int32_t mpgnn_debug_occupancy(int32_t F, int32_t* seg_tile_blocks_per_cu, int32_t* tile_gemm_blocks_per_cu,
+                              int32_t* tile_gemm_grid);
 int32_t mpgnn_timing_reset(void);
 int32_t mpgnn_timing_query(int32_t kernel_kind, double* total_ms, int64_t* launches);
 

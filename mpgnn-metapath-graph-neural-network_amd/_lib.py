@@ -65,6 +65,7 @@ SIGNATURES = [
                               _P, _P, _P, _P, _P, _P]),
     ("mpgnn_set_option", _I32, [_I32, _I64]),
     ("mpgnn_timing_enable", _I32, [_I32]),
+    ("mpgnn_debug_occupancy", _I32, [_I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
     ("mpgnn_timing_reset", _I32, []),
     ("mpgnn_timing_query", _I32, [_I32, ctypes.POINTER(ctypes.c_double), _PI64]),
 ]

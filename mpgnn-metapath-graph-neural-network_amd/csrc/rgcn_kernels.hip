@@ -7,16 +7,18 @@
 //   out     = Σ_r h_r @ W_r + x @ root + bias      mp_rgcn_layer.py:245,265,268 (mode SINGLE,
 //             one r, 2-D W) / RGCNConv loop ≙ mp_rgcn_layer.py:249-258 (mode ALL, W[R,F,F])
 //
-// Kernel map (DESIGN.md §Kernels):
-//   seg_tile_kernel    one workgroup = one relation-pure tile of 64 segments (node_1, r):
-//                      wavefront segmented gather-sum of x rows into an LDS tile (edge order,
-//                      bit-exact mean), then v_mfma_f32_32x32x2_f32 against W_r.  Forward
-//                      writes Y[seg] = h_seg @ W_r (+ h_seg itself for backward); backward
-//                      ("dgrad") writes G[seg] = (dout[node_1] @ W_rᵀ) / cnt.
-//   row_tile_kernel    one workgroup = 64 output rows: ordered sum of the rows' Y (or G)
-//                      entries into LDS + MFMA of the dense tile (x @ root, dout @ rootᵀ),
-//                      epilogue (Σ + root-term) + bias.
-//   outer_accum_kernel dW_r / droot partial slabs  P_c = A_cᵀ B_c over a chunk of rows (MFMA).
+// Kernel map (DESIGN.md §4):
+//   piece_sum_kernel   ordered partial sums of runs longer than kPieceEntries (one wave/piece)
+//   seg_tile_kernel    one workgroup = one 64-row tile. Relation tiles: 64 segments (node_1, r)
+//                      of one relation — wavefront segmented gather-sum of x rows into LDS
+//                      (edge order, bit-exact mean), then v_mfma_f32_32x32x2_f32 against W_r.
+//                      Root tiles: 64 consecutive nodes — x rows into LDS, MFMA against root.
+//                      Forward writes Y[seg] = h_seg @ W_r, Y_root[i] = x_i @ root; backward
+//                      ("dgrad") writes G[seg] = (dout[node_1] @ W_rᵀ) / cnt, G_root = dout @ rootᵀ.
+//   row_sum_kernel     out[i] = (Σ_{entries of row i, in order} src) + extra[i] + bias: the
+//                      forward combine Σ_r Y + Y_root + bias (reference add order) and the
+//                      transposed grad_x gather Σ G + G_root.
+//   outer_accum_kernel dW_r / droot / dbias partial slabs  P_c = A_cᵀ B_c over a chunk of rows.
 //   reduce_slabs_kernel ordered sum of the partial slabs of each group (deterministic).
 #include <hip/hip_runtime.h>
 
@@ -33,10 +35,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kThreads = 256;  // 4 waves of 64
 constexpr int kWaves = 4;
-constexpr int kRowsPerWave = kTileRows / kWaves;  // 16
+constexpr int kRowsPerWave = kTileRows / kWaves;  // 16 (seg_tile_kernel)
+constexpr int kSumRowsPerWave = 4;               // row_sum_kernel: 16 rows per workgroup
 constexpr int kColTile = 128;                    // output columns per workgroup (4 × 32-col strips)
 constexpr int kSlice = 32;                       // rows per K-slice in outer_accum_kernel
-constexpr int kMaxF = 256;  // LDS budget: row_tile_kernel holds 64×(G + K + 4) floats
+constexpr int kMaxF = 256;
 
 __host__ __device__ constexpr int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
@@ -69,21 +72,29 @@ __device__ __forceinline__ void vstore(float* p, const float (&v)[V]) {
 
 __device__ __forceinline__ int readlane(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 
+// Uniform read of a plan table through the constant address space: an SMEM load (lgkmcnt), so
+// waiting for it does not also drain the wave's outstanding vector loads and stores (vmcnt is
+// in order).  Only for tables the kernels never write.
+__device__ __forceinline__ int ld_uniform(const int* p, int i) {
+    return ((const __attribute__((address_space(4))) int*)(p))[i];
+}
+
 // ----------------------------------------------------------------------------------------
-// Wavefront segmented gather-sum into an LDS tile.
+// Wavefront segmented gather-sum.
 //
-// The wave owns `nrows` (≤ 16) consecutive tile rows.  Lane j (j ≤ nrows) holds in `bnd` the
-// position where row j's entries start (so row j covers positions [bnd_j, bnd_{j+1})), and the
-// positions of consecutive rows are contiguous.  Position p contributes source row
+// The wave owns `nrows` (≤ RPW) consecutive rows.  Lane j (j ≤ nrows) holds in `bnd` the
+// position where row j's entries start (row j covers entries [bnd_j, bnd_{j+1})); the entries
+// of consecutive rows are contiguous.  Entry q is a position p = (ent ? ent[q] : q) or, when
+// ent[q] < 0, the ordered partial sum P[-ent[q]-1 - piece_off] of a piece of a long run
+// (piece_sum_kernel).  Position p contributes source row
 //     src_row(p) = (idx ? idx[p] : p) - idx_off
-// unless a filter rejects it (fidx[p] outside [flo, fhi)).  With a two-level list (g.ent) the
-// wave walks entries instead: an entry >= 0 is a position as above, an entry -(k+1) adds the
-// partial sum P[k - piece_off] of an ordered piece of a long run (piece_sum_kernel).  Lanes span the feature dimension
-// (V floats per lane, T chunks of 64·V columns); every lane adds its columns in position
-// order starting from 0.0f, which is exactly ATen's sequential scatter_add_ into a zeroed
-// output — the sums are bit-identical to the reference.  Each finished row is optionally
-// divided by cnt[row] (IEEE division = `out / count` of PyG's mean), written to LDS with
-// zeros in [F, width), and optionally copied to global memory.
+// unless the filter rejects it (fidx[p] outside [flo, fhi)).  Lanes span the feature dimension
+// (V floats per lane, T chunks of 64·V columns); every lane adds its columns in entry order
+// starting from 0.0f, which is exactly ATen's sequential scatter_add_ into a zeroed output —
+// for runs without pieces the sums are bit-identical to the reference.  Loads are issued
+// unconditionally (clamped addresses) and software-pipelined one group of UNR entries ahead:
+// a load behind a per-entry branch makes hipcc wait for each entry separately
+// (cdna_hip_programming.md §5 trap (c)).  Each finished row is handed to flush(row, live, acc).
 // ----------------------------------------------------------------------------------------
 struct GatherSrc {
     const float* src;  // [*, F]
@@ -97,28 +108,8 @@ struct GatherSrc {
     int piece_off;
 };
 
-template <int V, int T>
-__device__ __forceinline__ void flush_row(float (&acc)[T][V], bool live, const int* cnt_rows, int r,
-                                          float* lds_row, int width, int F, float* grow, int lane) {
-    float scale_div = 1.0f;
-    const bool do_div = live && cnt_rows != nullptr;
-    if (do_div) scale_div = (float)cnt_rows[r];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-        const int col = (t * 64 + lane) * V;
-        float v[V];
-#pragma unroll
-        for (int q = 0; q < V; ++q) v[q] = live ? (do_div ? acc[t][q] / scale_div : acc[t][q]) : 0.0f;
-        if (col < width) vstore<V>(lds_row + col, v);
-        if (grow != nullptr && live && col < F) vstore<V>(grow + col, v);
-#pragma unroll
-        for (int q = 0; q < V; ++q) acc[t][q] = 0.0f;
-    }
-}
-
-template <int V, int T, int UNR>
-__device__ void wave_gather(const GatherSrc& g, int bnd, int nrows, const int* cnt_rows,
-                            float* lds, int lda, int width, float* gout, int gout_ld, int lane) {
+template <int V, int T, int UNR, int RPW, class Flush>
+__device__ __forceinline__ void wave_gather(const GatherSrc& g, int bnd, int nrows, int lane, Flush&& flush) {
     float acc[T][V];
 #pragma unroll
     for (int t = 0; t < T; ++t)
@@ -129,16 +120,6 @@ __device__ void wave_gather(const GatherSrc& g, int bnd, int nrows, const int* c
     const int p_end = readlane(bnd, nrows);
     int r = 0;
     int r_end = nrows > 0 ? readlane(bnd, 1) : p_end;
-
-    auto flush = [&](int row) {
-        const bool live = row < nrows;
-        float* grow = (gout != nullptr && live) ? gout + (size_t)row * gout_ld : nullptr;
-        flush_row<V, T>(acc, live, cnt_rows, row, lds + row * lda, width, g.F, grow, lane);
-    };
-
-    // column offsets of this lane, clamped so that every load is unconditional (the value of
-    // a lane past F is never stored); a load behind a per-entry branch makes hipcc wait for
-    // each entry separately (cdna_hip_programming.md §5 trap (c))
     int colc[T];
 #pragma unroll
     for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, g.F - V);
@@ -162,27 +143,29 @@ __device__ void wave_gather(const GatherSrc& g, int bnd, int nrows, const int* c
                 my_piece = true;
                 my_src = -e - 1 - g.piece_off;
             }
-            if (!my_keep) my_src = 0;  // rejected entry: load a valid row, never added
+            if (!my_keep) my_src = 0;  // rejected entry: a valid row is loaded, never added
         }
         const unsigned long long keep = __ballot(my_keep);
         const unsigned long long from_piece = __ballot(my_piece);
-        for (int u = 0; u < np; u += UNR) {
-            float v[UNR][T][V];
+        float v[2][UNR][T][V];
+        auto issue = [&](float (&dst)[UNR][T][V], int u) {
 #pragma unroll
             for (int uu = 0; uu < UNR; ++uu) {
                 const int q = min(u + uu, np - 1);
                 const int row = readlane(my_src, q);
                 const float* base = (((from_piece >> q) & 1ull) ? g.P : g.src) + (size_t)row * g.F;
 #pragma unroll
-                for (int t = 0; t < T; ++t) vload<V>(base + colc[t], v[uu][t]);
+                for (int t = 0; t < T; ++t) vload<V>(base + colc[t], dst[uu][t]);
             }
+        };
+        auto consume = [&](const float (&src)[UNR][T][V], int u) {
 #pragma unroll
             for (int uu = 0; uu < UNR; ++uu) {
                 const int q = u + uu;
                 if (q < np) {
                     const int p = pb + q;
                     while (p >= r_end) {
-                        flush(r);
+                        flush(r, true, acc);
                         ++r;
                         r_end = readlane(bnd, r + 1);
                     }
@@ -190,13 +173,30 @@ __device__ void wave_gather(const GatherSrc& g, int bnd, int nrows, const int* c
 #pragma unroll
                         for (int t = 0; t < T; ++t)
 #pragma unroll
-                            for (int c = 0; c < V; ++c) acc[t][c] += v[uu][t][c];
+                            for (int c = 0; c < V; ++c) acc[t][c] += src[uu][t][c];
                     }
                 }
             }
+        };
+        issue(v[0], 0);
+        for (int u = 0; u < np; u += 2 * UNR) {
+            if (u + UNR < np) issue(v[1], u + UNR);
+            consume(v[0], u);
+            if (u + UNR < np) {
+                if (u + 2 * UNR < np) issue(v[0], u + 2 * UNR);
+                consume(v[1], u + UNR);
+            }
         }
     }
-    for (; r < kRowsPerWave; ++r) flush(r);
+    for (; r < RPW; ++r) flush(r, r < nrows, acc);
+}
+
+template <int V, int T>
+__device__ __forceinline__ void zero_acc(float (&acc)[T][V]) {
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int q = 0; q < V; ++q) acc[t][q] = 0.0f;
 }
 
 // ----------------------------------------------------------------------------------------
@@ -221,81 +221,204 @@ __global__ __launch_bounds__(kThreads) void piece_sum_kernel(PieceArgs a) {
     const int lane = threadIdx.x & 63;
     const int k = a.k_lo + blockIdx.x * kWaves + (threadIdx.x >> 6);
     if (k >= a.k_hi) return;
-    const int p0 = a.pb[k], p1 = a.pe[k];
-    const int np = p1 - p0;  // <= 32 <= 64
-    int my_src = 0;
-    bool my_keep = false;
-    if (lane < np) {
-        const int p = p0 + lane;
-        my_keep = true;
-        if (a.fidx != nullptr) {
-            const int f = a.fidx[p];
-            my_keep = (f >= a.flo) && (f < a.fhi);
-        }
-        my_src = (a.idx != nullptr ? a.idx[p] : p) - a.idx_off;
-    }
-    if (!my_keep) my_src = 0;
-    const unsigned long long keep = __ballot(my_keep);
-    float acc[T][V];
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-        for (int c = 0; c < V; ++c) acc[t][c] = 0.0f;
-    int colc[T];
-#pragma unroll
-    for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, a.F - V);
-    constexpr int UNR = (V * T <= 2 ? 8 : 4);
-    for (int u = 0; u < np; u += UNR) {
-        float v[UNR][T][V];
-#pragma unroll
-        for (int uu = 0; uu < UNR; ++uu) {
-            const float* base = a.src + (size_t)readlane(my_src, min(u + uu, np - 1)) * a.F;
-#pragma unroll
-            for (int t = 0; t < T; ++t) vload<V>(base + colc[t], v[uu][t]);
-        }
-#pragma unroll
-        for (int uu = 0; uu < UNR; ++uu)
-            if (u + uu < np && ((keep >> (u + uu)) & 1ull)) {
-#pragma unroll
-                for (int t = 0; t < T; ++t)
-#pragma unroll
-                    for (int c = 0; c < V; ++c) acc[t][c] += v[uu][t][c];
-            }
-    }
+    GatherSrc g{};
+    g.src = a.src;
+    g.F = a.F;
+    g.idx = a.idx;
+    g.idx_off = a.idx_off;
+    g.fidx = a.fidx;
+    g.flo = a.flo;
+    g.fhi = a.fhi;
+    const int bnd = lane == 0 ? a.pb[k] : a.pe[k];
     float* out = a.P + (size_t)(k - a.k_lo) * a.F;
+    wave_gather<V, T, 8, 1>(g, bnd, 1, lane, [&](int, bool live, float (&acc)[T][V]) {
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-        const int col = (t * 64 + lane) * V;
-        if (col < a.F) vstore<V>(out + col, acc[t]);
-    }
+        for (int t = 0; t < T; ++t) {
+            const int col = (t * 64 + lane) * V;
+            if (live && col < a.F) vstore<V>(out + col, acc[t]);
+        }
+        zero_acc<V, T>(acc);
+    });
 }
 
-// Dense tile loader: rows [row0, row0+64) of A[*, K] into lds[64][lda] with zeros past
-// K (up to width) and past nrows.  All of a thread's loads are issued before any LDS store
-// (float4 when the row stride allows), so the tile costs one memory latency, not 32.
-__device__ void load_dense_tile(const float* __restrict__ A, int K, int row0, int nrows, float* lds,
-                                int lda, int width) {
+// ----------------------------------------------------------------------------------------
+// MFMA tile:  acc(64 × 128-column tile) = A_lds[64 × Kp] · B[K × N]
+// v_mfma_f32_32x32x2_f32: lane l holds A[i = l&31][kk = l>>5] and B[kk][j = l&31];
+// C/D: col = l&31, row = (r&3) + 8(r>>2) + 4(l>>5).  The K dimension is split in two halves
+// so that lane-half h walks k ∈ [h·Kp/2, (h+1)·Kp/2) contiguously (one ds_read_b128 feeds
+// four MFMAs); the MFMA sums over both halves, so every k is covered exactly once.
+// Wave w owns column strip w (32 columns) of the tile and BOTH 32-row halves, so its two
+// accumulators share every B value; waves whose strip starts past N idle.
+// ----------------------------------------------------------------------------------------
+struct BSrc {
+    const float* W;  // element (k, n) = trans ? W[n*ldw + k] : W[k*ldw + n]
+    int ldw;
+    int K, N;
+    int trans;
+};
+
+struct MfmaTile {
+    f32x16 acc0, acc1;  // rows 0..31 / 32..63 of strip `nb`
+    int nb;
+    bool active;
+};
+
+// B(k, n) of the tile: TRANS = false reads W[k*ldw + n] (rows k, 32 consecutive columns per
+// half-wave); TRANS = true reads W[n*ldw + k] (row n, four consecutive k per float4 load).
+// CLAMP = true handles K < Kp (zero-padded A columns): addresses are clamped to row K-1 and the
+// value is replaced by 0 when consumed.  Both are template parameters so the K loop is
+// straight-line code: a runtime branch there makes hipcc wait for every prefetch.  K is
+// padded to a multiple of 64 in LDS (zeros), so K < Kp needs CLAMP.
+template <bool TRANS, bool CLAMP>
+struct BLoader {
+    const float* W;  // uniform base (SGPRs); lanes add 32-bit element offsets (K·N ≤ 2^16)
+    int n, ldw, K;
+    __device__ __forceinline__ BLoader(const BSrc& b, int n_) {
+        W = b.W;
+        n = n_;
+        ldw = b.ldw;
+        K = b.K;
+    }
+    // KC consecutive k starting at k0.  The chunk base is clamped (whole chunk inside W) and
+    // the addresses are uniform base + 32-bit lane offset: no per-k 64-bit address survives in
+    // VGPRs (with per-k 64-bit products the persistent loop's LICM hoisted 64 of them: spills).
+    template <int KC>
+    __device__ __forceinline__ void load_chunk(int k0, float (&o)[KC]) const {
+        if constexpr (!CLAMP) {
+            const int kc = min(k0, K - KC);
+            if constexpr (!TRANS) {
+                const float* p = W + (size_t)kc * ldw;
+#pragma unroll
+                for (int j = 0; j < KC; ++j) o[j] = p[j * ldw + n];
+            } else {
+                const float* p = W + kc;
+#pragma unroll
+                for (int j = 0; j < KC; j += 4) {
+                    const float4 tv = *reinterpret_cast<const float4*>(p + n * ldw + j);
+                    o[j] = tv.x;
+                    o[j + 1] = tv.y;
+                    o[j + 2] = tv.z;
+                    o[j + 3] = tv.w;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < KC; ++j) {
+                const int k = min(k0 + j, K - 1);
+                o[j] = TRANS ? W[n * ldw + k] : W[k * ldw + n];
+            }
+        }
+    }
+};
+
+// K loop of one strip: B is staged in registers in chunks of KC k-values per lane, one chunk
+// ahead (a chunk feeds 2·KC MFMAs ≈ 2k SIMD cycles, more than an L2/Infinity-Cache round
+// trip); A comes from LDS (ds_read_b128 feeds four MFMAs).  sched_barrier(0) pins each chunk's
+// loads where they are written — left alone, the scheduler sinks them below the MFMAs and the
+// next chunk then waits for them.  KH % (2·KC) == 0 (Kp % 64 == 0).
+constexpr int kKC = 16;
+
+template <bool TRANS, bool CLAMP>
+__device__ __forceinline__ void mfma_loop(f32x16& acc0, f32x16& acc1, const float* a0p, const float* a1p, int KH,
+                                          int kb, const BSrc& b, int n) {
+    const BLoader<TRANS, CLAMP> ld(b, n);
+    auto load_chunk = [&](int k0, float (&o)[kKC]) { ld.template load_chunk<kKC>(k0, o); };
+    auto compute_chunk = [&](const float (&bc)[kKC], int t, int k0) {
+#pragma unroll
+        for (int j = 0; j < kKC; j += 4) {
+            const float4 a0 = *reinterpret_cast<const float4*>(a0p + t + j);
+            const float4 a1 = *reinterpret_cast<const float4*>(a1p + t + j);
+            float bq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bq[q] = (!CLAMP || k0 + j + q < b.K) ? bc[j + q] : 0.0f;
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, bq[0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, bq[0], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, bq[1], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, bq[1], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, bq[2], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, bq[2], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, bq[3], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, bq[3], acc1, 0, 0, 0);
+        }
+    };
+    float b0[kKC], b1[kKC];
+    load_chunk(kb, b0);
+    // the last pair is peeled so no chunk is loaded past KH (an unconsumed load would be
+    // waited for — with every store before it — where its registers are next written)
+    int t = 0;
+#pragma unroll 1
+    for (; t < KH - 2 * kKC; t += 2 * kKC) {
+        load_chunk(kb + t + kKC, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        compute_chunk(b0, t, kb + t);
+        __builtin_amdgcn_sched_barrier(0);
+        load_chunk(kb + t + 2 * kKC, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        compute_chunk(b1, t + kKC, kb + t + kKC);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    load_chunk(kb + t + kKC, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute_chunk(b0, t, kb + t);
+    __builtin_amdgcn_sched_barrier(0);
+    compute_chunk(b1, t + kKC, kb + t + kKC);
+}
+
+__device__ __forceinline__ void mfma_tile(MfmaTile& mt, const float* A_lds, int lda, int Kp,
+                                          const BSrc& b, int n_base, int wave, int lane) {
+    const int c = lane & 31;
+    const int h = lane >> 5;
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        acc0[r] = 0.0f;
+        acc1[r] = 0.0f;
+    }
+    mt.nb = wave;
+    mt.active = n_base + wave * 32 < b.N;
+    if (mt.active) {
+        const int KH = Kp / 2;
+        const int n = min(n_base + wave * 32 + c, b.N - 1);  // clamped: columns >= N are never stored
+        const float* a0p = A_lds + c * lda + h * KH;
+        const float* a1p = A_lds + (32 + c) * lda + h * KH;
+        const int kb = h * KH;
+        const bool exact_k = b.K == Kp;                        // no padded k: clamp-free loop
+        const bool vec_ok = (b.ldw & 3) == 0 && b.K >= kKC;
+        if (!b.trans) {
+            if (exact_k && b.K >= kKC) mfma_loop<false, false>(acc0, acc1, a0p, a1p, KH, kb, b, n);
+            else mfma_loop<false, true>(acc0, acc1, a0p, a1p, KH, kb, b, n);
+        } else {
+            if (exact_k && vec_ok) mfma_loop<true, false>(acc0, acc1, a0p, a1p, KH, kb, b, n);
+            else mfma_loop<true, true>(acc0, acc1, a0p, a1p, KH, kb, b, n);
+        }
+    }
+    mt.acc0 = acc0;
+    mt.acc1 = acc1;
+}
+
+// Dense tile loader: rows [0, nrows) of A[*, K] (contiguous, row stride K) into
+// lds[64][lda] with zeros past K (up to width) and past nrows.  Every load of a batch is
+// issued before any LDS store (float4 when K % 4 == 0).
+__device__ void load_dense_tile(const float* __restrict__ A, int K, int nrows, float* lds, int lda, int width) {
     if ((K & 3) == 0 && (width & 3) == 0) {
         const int w4 = width >> 2;
-        const int total = kTileRows * w4;  // float4 slots
+        const int total = kTileRows * w4;
         constexpr int kBatch = 8;
         for (int i0 = threadIdx.x; i0 < total; i0 += kBatch * kThreads) {
             float4 v[kBatch];
 #pragma unroll
             for (int it = 0; it < kBatch; ++it) {
                 const int i = min(i0 + it * kThreads, total - 1);
-                const int r = i / w4;
-                const int c = (i - r * w4) * 4;
-                const int rr = min(r, max(nrows - 1, 0));
-                const int cc = min(c, K - 4);
-                v[it] = *reinterpret_cast<const float4*>(A + (size_t)(row0 + rr) * K + cc);
+                const int r = min(i / w4, max(nrows - 1, 0));
+                const int c = min((i % w4) * 4, K - 4);
+                v[it] = *reinterpret_cast<const float4*>(A + (size_t)r * K + c);
             }
 #pragma unroll
             for (int it = 0; it < kBatch; ++it) {
                 const int i = i0 + it * kThreads;
                 if (i < total) {
                     const int r = i / w4;
-                    const int c = (i - r * w4) * 4;
+                    const int c = (i % w4) * 4;
                     const bool ok = r < nrows && c < K;
                     *reinterpret_cast<float4*>(lds + r * lda + c) = ok ? v[it] : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
@@ -308,197 +431,108 @@ __device__ void load_dense_tile(const float* __restrict__ A, int K, int row0, in
         float v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int i = i0 + u * kThreads;
-            v[u] = 0.0f;
-            if (i < total) {
-                const int r = i / width;
-                const int c = i - r * width;
-                if (r < nrows && c < K) v[u] = A[(size_t)(row0 + r) * K + c];
-            }
+            const int i = min(i0 + u * kThreads, total - 1);
+            const int r = min(i / width, max(nrows - 1, 0));
+            const int c = min(i % width, K - 1);
+            v[u] = A[(size_t)r * K + c];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int i = i0 + u * kThreads;
             if (i < total) {
                 const int r = i / width;
-                lds[r * lda + (i - r * width)] = v[u];
+                const int c = i % width;
+                lds[r * lda + c] = (r < nrows && c < K) ? v[u] : 0.0f;
             }
         }
     }
-}
-
-// ----------------------------------------------------------------------------------------
-// MFMA tile:  acc(64 × 128-column tile) = A_lds[64 × Kp] · B[K × N]
-// v_mfma_f32_32x32x2_f32: lane l holds A[i = l&31][kk = l>>5] and B[kk][j = l&31];
-// C/D: col = l&31, row = (r&3) + 8(r>>2) + 4(l>>5).  The K dimension is split in two halves
-// so that lane-half h walks k ∈ [h·Kp/2, (h+1)·Kp/2) contiguously (one ds_read_b128 feeds
-// four MFMAs); the MFMA sums over both halves, so every k is covered exactly once.
-// Wave w owns blocks b ∈ {w, w+4} of the (2 row-halves × NS strips) grid, b = mb·NS + nb.
-// ----------------------------------------------------------------------------------------
-struct BSrc {
-    const float* W;  // element (k, n) = trans ? W[n*ldw + k] : W[k*ldw + n]
-    int ldw;
-    int K, N;
-    int trans;
-};
-
-// Wave w owns column strip w (32 columns) of the 128-column tile and BOTH 32-row halves, so
-// its two accumulators share every B value; waves whose strip starts past N idle.
-struct MfmaTile {
-    f32x16 acc0, acc1;  // rows 0..31 / 32..63 of strip `nb`
-    int nb;
-    bool active;
-};
-
-__device__ __forceinline__ void mfma_tile(MfmaTile& mt, const float* A_lds, int lda, int Kp,
-                                          const BSrc& b, int n_base, int wave, int lane) {
-    const int c = lane & 31;
-    const int h = lane >> 5;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        mt.acc0[r] = 0.0f;
-        mt.acc1[r] = 0.0f;
-    }
-    mt.nb = wave;
-    mt.active = n_base + wave * 32 < b.N;
-    if (!mt.active) return;
-    const int KH = Kp / 2;
-    const int n = min(n_base + wave * 32 + c, b.N - 1);  // clamped: columns >= N are never stored
-    const float* a0p = A_lds + c * lda + h * KH;
-    const float* a1p = A_lds + (32 + c) * lda + h * KH;
-    const int kb = h * KH;
-    f32x16 acc0 = mt.acc0, acc1 = mt.acc1;
-    // B values are loaded one group of 4 k ahead with clamped addresses; the k < K select is
-    // applied when the group is consumed, so the prefetch is never waited for early.
-    auto mfma8 = [&](const float (&braw)[4], int k0, int t) {
-        const float4 a0 = *reinterpret_cast<const float4*>(a0p + t);
-        const float4 a1 = *reinterpret_cast<const float4*>(a1p + t);
-        float bq[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bq[j] = (k0 + j < b.K) ? braw[j] : 0.0f;
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, bq[0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, bq[0], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, bq[1], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, bq[1], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, bq[2], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, bq[2], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, bq[3], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, bq[3], acc1, 0, 0, 0);
-    };
-    if (!b.trans) {
-        // B(k, n) = W[k*ldw + n]: rows k of W, 32 consecutive columns per half-wave
-        const float* wp = b.W + n;
-        auto ld4 = [&](int k0, float (&o)[4]) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = wp[(size_t)min(k0 + j, b.K - 1) * b.ldw];
-        };
-        float b0[4], b1[4];
-        ld4(kb, b0);
-        for (int t = 0; t < KH; t += 8) {  // KH % 8 == 0 (Kp % 16 == 0): ping-pong, no copies
-            ld4(kb + t + 4, b1);
-            mfma8(b0, kb + t, t);
-            ld4(kb + t + 8, b0);
-            mfma8(b1, kb + t + 4, t + 4);
-        }
-    } else {
-        // B(k, n) = W[n*ldw + k]: row n of W, four consecutive k per load
-        const float* wp = b.W + (size_t)n * b.ldw;
-        const bool vec = (b.K & 3) == 0 && (b.ldw & 3) == 0;
-        auto ld4 = [&](int k0, float (&o)[4]) {
-            if (vec) {
-                const float4 tv = *reinterpret_cast<const float4*>(wp + min(k0, b.K - 4));
-                o[0] = tv.x;
-                o[1] = tv.y;
-                o[2] = tv.z;
-                o[3] = tv.w;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) o[j] = wp[min(k0 + j, b.K - 1)];
-            }
-        };
-        float b0[4], b1[4];
-        ld4(kb, b0);
-        for (int t = 0; t < KH; t += 8) {
-            ld4(kb + t + 4, b1);
-            mfma8(b0, kb + t, t);
-            ld4(kb + t + 8, b0);
-            mfma8(b1, kb + t + 4, t + 4);
-        }
-    }
-    mt.acc0 = acc0;
-    mt.acc1 = acc1;
 }
 
 // ----------------------------------------------------------------------------------------
 // seg_tile_kernel
+//   blocks [0, n_rel_tiles): relation tiles (plan tiles t_off + blockIdx.x), rows = segments
+//   blocks [n_rel_tiles, ...): root tiles, rows = nodes row_lo + 64·(blockIdx.x - n_rel_tiles)
 // ----------------------------------------------------------------------------------------
 struct SegTileArgs {
     const int* tile_begin;
     const int* tile_end;
     int tile_off;
-    int gather_kind;     // 0: mean of src[e_col[e]] over the segment's edges; 1: src[s_row[s]]
-    const float* src;
+    int n_rel_tiles;
+    int gather_kind;     // 0: mean of src[e_col[e]] over the segment's edges; 1: src[s_row[s]];
+                         // 2: dense rows src[s - sel_b] (precomputed segment means H)
+    const float* src;    // x (forward) or dout (dgrad); also the root-tile rows
     int F;               // gather width = K of the MFMA
     const int* s_ptr;    // segment boundaries over edges (exact order) or over ragged entries
     const int* e_col;
     const int* s_row;
     const int* s_cnt;
     const int* s_rel;
-    const int* s_pos;
     const int* ent;      // nullable: ragged entries (s_ptr then indexes entries)
     const float* P;      // piece partials of long segments
     int piece_off;
     const float* W;      // nullable: no transform (segment means only)
     int w_per_rel;       // W_r = W + s_rel[s] * K * N
+    const float* Wroot;  // root-tile B (same orientation as W)
     int trans;
     int N;               // output width
-    float* Y;            // output rows
-    int y_use_pos;       // row = s_pos[s] (row-major position) else s - sel_b
-    int y_div;           // divide the MFMA result by cnt (dgrad)
+    float* Y;            // relation-tile output rows s - sel_b
+    float* Yroot;        // root-tile output rows i - row_lo
+    int row_lo, row_hi;
+    int y_div;           // divide the relation-tile MFMA result by cnt (dgrad)
     int sel_b;
-    float* H;            // nullable: copy of the gathered tile rows, row = s - sel_b, width F
-    int ablate;          // debug (MPGNN_OPT_ABLATE): 1 = skip gather, 2 = skip MFMA; wrong results
+    float* H;            // nullable: copy of the gathered relation-tile rows, row = s - sel_b, width F
+    const float* Hsrc;   // gather_kind 2: precomputed relation-tile rows, row = s - sel_b
+    int ablate;          // debug (MPGNN_OPT_ABLATE): 1 skip gather, 2 skip MFMA+epilogue,
+                         // 4 skip epilogue stores, 8 skip MFMA loop only; wrong results
+    unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [block][8] timeline, or nullptr
 };
+
+// debug timeline stamp (diagnostic builds only pay for it: stamps == nullptr otherwise)
+__device__ __forceinline__ unsigned long long stamp_now() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
 
 template <int V, int T>
 __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int Kp = round_up(a.F, 16);
+    const int Kp = round_up(a.F, 64);
     const int lda = Kp + 4;
-    int* s_dst = reinterpret_cast<int*>(smem);            // [64] destination row of each tile row
-    float* s_scale = smem + kTileRows;                    // [64] cnt as float (dgrad)
-    float* A_lds = smem + 2 * kTileRows;                  // [64][lda]
+    float* s_scale = smem;                  // [64] cnt as float (dgrad)
+    float* A_lds = smem + kTileRows;        // [64][lda]
 
-    const int tile = blockIdx.x + a.tile_off;
-    const int s0 = a.tile_begin[tile];
-    const int nrows = a.tile_end[tile] - s0;
+    unsigned long long t_start = 0;
+    if (a.stamps != nullptr) t_start = stamp_now();
+    const bool root_tile = (int)blockIdx.x >= a.n_rel_tiles;
+    int s0, nrows;
+    if (!root_tile) {
+        const int tile = blockIdx.x + a.tile_off;
+        s0 = a.tile_begin[tile];
+        nrows = a.tile_end[tile] - s0;
+    } else {
+        s0 = a.row_lo + ((int)blockIdx.x - a.n_rel_tiles) * kTileRows;
+        nrows = min(kTileRows, a.row_hi - s0);
+    }
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-
-    if (threadIdx.x < kTileRows) {
-        const int r = threadIdx.x;
-        const int s = s0 + r;
-        s_dst[r] = r < nrows ? (a.y_use_pos ? a.s_pos[s] : s - a.sel_b) : -1;
-        s_scale[r] = r < nrows ? (float)a.s_cnt[s] : 1.0f;
-    }
+    const bool div_rows = !root_tile && a.y_div;
+    if (div_rows && threadIdx.x < kTileRows)
+        s_scale[threadIdx.x] = threadIdx.x < nrows ? (float)a.s_cnt[s0 + threadIdx.x] : 1.0f;
 
     // ---- gather phase: each wave builds 16 tile rows ---------------------------------
     const int wr0 = wave * kRowsPerWave;
     int wn = nrows - wr0;
     wn = wn < 0 ? 0 : (wn > kRowsPerWave ? kRowsPerWave : wn);
     const int sw = s0 + wr0;
-    GatherSrc g;
+    GatherSrc g{};
     g.src = a.src;
     g.F = a.F;
-    g.fidx = nullptr;
-    g.flo = g.fhi = 0;
-    g.idx_off = 0;
     int bnd = 0;
     const int* cnt_rows = nullptr;
-    g.ent = nullptr;
-    g.P = nullptr;
-    g.piece_off = 0;
-    if (a.gather_kind == 0) {
+    if (root_tile) {
+        bnd = sw + (lane <= wn ? lane : wn);  // positions = node ids, source row = position
+    } else if (a.gather_kind == 0) {
         if (lane <= wn) bnd = a.s_ptr[sw + lane];
         g.idx = a.e_col;
         g.ent = a.ent;
@@ -509,22 +543,38 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
         bnd = sw + (lane <= wn ? lane : wn);
         g.idx = a.s_row;
     }
-    // saved segment means (backward): row s - sel_b of H, consecutive for the wave's rows
-    float* gout = (a.H != nullptr && blockIdx.y == 0) ? a.H + (size_t)(sw - a.sel_b) * a.F : nullptr;
-    if (!(a.ablate & 1))
-        wave_gather<V, T, (V * T <= 2 ? 8 : 4)>(g, bnd, wn, cnt_rows, A_lds + wr0 * lda, lda, Kp, gout, a.F,
-                                                lane);
-    __syncthreads();
-    if (a.W == nullptr) return;
-    if (a.ablate & 2) {  // keep the gathered tile observable, skip the contraction
-        if (threadIdx.x < kTileRows && threadIdx.x < nrows)
-            a.Y[(size_t)s_dst[threadIdx.x] * a.N] = A_lds[threadIdx.x * lda];
-        return;
+    // saved segment means (backward): rows s - sel_b of H, consecutive for the wave's rows
+    float* hrow0 = (a.H != nullptr && !root_tile && blockIdx.y == 0) ? a.H + (size_t)(sw - a.sel_b) * a.F : nullptr;
+    float* lds_w = A_lds + wr0 * lda;
+    if (root_tile || a.gather_kind == 2) {
+        // contiguous rows: one coalesced float4 sweep of the whole 64-row tile
+        const float* base = root_tile ? a.src + (size_t)s0 * a.F : a.Hsrc + (size_t)(s0 - a.sel_b) * a.F;
+        if (!(a.ablate & 1)) load_dense_tile(base, a.F, nrows, A_lds, lda, Kp);
+    } else if (!(a.ablate & 1)) {
+        wave_gather<V, T, (V * T <= 2 ? 8 : 4), kRowsPerWave>(
+            g, bnd, wn, lane, [&](int r, bool live, float (&acc)[T][V]) {
+                const bool do_div = live && cnt_rows != nullptr;
+                const float cnt = do_div ? (float)cnt_rows[r] : 1.0f;
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    const int col = (t * 64 + lane) * V;
+                    float v[V];
+#pragma unroll
+                    for (int q = 0; q < V; ++q) v[q] = live ? (do_div ? acc[t][q] / cnt : acc[t][q]) : 0.0f;
+                    if (col < Kp) vstore<V>(lds_w + r * lda + col, v);
+                    if (hrow0 != nullptr && live && col < a.F) vstore<V>(hrow0 + (size_t)r * a.F + col, v);
+                }
+                zero_acc<V, T>(acc);
+            });
     }
+    __syncthreads();
+    unsigned long long t_loaded = 0;
+    if (a.stamps != nullptr) t_loaded = stamp_now();
+    if (a.W == nullptr) return;
 
     // ---- MFMA phase --------------------------------------------------------------------
-    const float* W = a.W;
-    if (a.w_per_rel) W += (size_t)a.s_rel[s0] * a.F * a.N;
+    const float* W = root_tile ? a.Wroot : a.W;
+    if (!root_tile && a.w_per_rel) W += (size_t)a.s_rel[s0] * a.F * a.N;
     BSrc b;
     b.W = W;
     b.K = a.F;
@@ -532,55 +582,434 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
     b.trans = a.trans;
     b.ldw = a.trans ? a.F : a.N;
     const int n_base = blockIdx.y * kColTile;
+    float* Yt = root_tile ? a.Yroot + (size_t)(s0 - a.row_lo) * a.N : a.Y + (size_t)(s0 - a.sel_b) * a.N;
+    if (a.ablate & 2) {  // keep the gathered tile observable, skip the contraction
+        if (threadIdx.x < nrows) Yt[(size_t)threadIdx.x * a.N] = A_lds[threadIdx.x * lda];
+        return;
+    }
     MfmaTile mt;
-    mfma_tile(mt, A_lds, lda, Kp, b, n_base, wave, lane);
-
+    if (a.ablate & 8) {
+        mt.nb = wave;
+        mt.active = n_base + wave * 32 < a.N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            mt.acc0[r] = A_lds[(lane & 31) * lda + r];
+            mt.acc1[r] = A_lds[(32 + (lane & 31)) * lda + r];
+        }
+    } else {
+        mfma_tile(mt, A_lds, lda, Kp, b, n_base, wave, lane);
+    }
     const int c = lane & 31;
     const int h = lane >> 5;
     const int col = n_base + mt.nb * 32 + c;
+    unsigned long long t_mfma = 0;
+    if (a.stamps != nullptr) t_mfma = stamp_now();
+    if (a.ablate & 4) {
+        float sum = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum += mt.acc0[r] + mt.acc1[r];
+        if (sum == 1234.5678f) a.Y[lane] = sum;
+        return;
+    }
     if (mt.active && col < a.N) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
             if (row < nrows) {
                 float v = mt.acc0[r];
-                if (a.y_div) v = v / s_scale[row];
-                a.Y[(size_t)s_dst[row] * a.N + col] = v;
+                if (div_rows) v = v / s_scale[row];
+                Yt[(size_t)row * a.N + col] = v;
             }
             if (row + 32 < nrows) {
                 float v = mt.acc1[r];
-                if (a.y_div) v = v / s_scale[row + 32];
-                a.Y[(size_t)s_dst[row + 32] * a.N + col] = v;
+                if (div_rows) v = v / s_scale[row + 32];
+                Yt[(size_t)(row + 32) * a.N + col] = v;
             }
         }
+    }
+    if (a.stamps != nullptr && (threadIdx.x & 63) == 0) {
+        const unsigned long long t_end = stamp_now();
+        const unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
+        const unsigned xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)); // HW_REG_XCC_ID
+        unsigned long long* o = a.stamps + ((size_t)blockIdx.x * gridDim.y + blockIdx.y) * 32 + (threadIdx.x >> 6) * 8;
+        o[0] = t_start;
+        o[1] = t_loaded;
+        o[2] = t_mfma;
+        o[3] = t_end;
+        o[4] = hw;
+        o[5] = xcc;
+        o[6] = (unsigned long long)nrows;
+        o[7] = root_tile;
     }
 }
 
 // ----------------------------------------------------------------------------------------
-// row_tile_kernel
+// tile_gemm_kernel — persistent, software-pipelined tile GEMM (forward transform and dgrad)
+//
+// Work item = (64-row tile, 128-column block).  Tiles [0, n_rel): relation-pure segment tiles
+// (plan tiles tile_off + i); tiles [n_rel, n_rel + n_root): node tiles row_lo + 64·j for the
+// root weight.  Each workgroup (2 per CU) walks work items blockIdx.x, +gridDim.x, … and keeps
+// the next item's A rows in flight in registers while the current item runs on the MFMA pipe;
+// the A tile is double-buffered in LDS (one barrier per item) and the epilogue stores drain
+// behind the next item's MFMAs.  (A straight launch of one tile per workgroup runs load → MFMA
+// → store in lockstep on every CU: memory and the matrix pipe never overlap.)
+//   a_kind 2: relation rows = Hsrc[s - sel_b] (segment means), root rows = src[i]   (forward)
+//   a_kind 1: relation rows = src[s_row[s]],    root rows = src[i]   (dgrad; / cnt on output)
 // ----------------------------------------------------------------------------------------
-struct RowTileArgs {
-    int N;              // rows of the output
-    int list_kind;      // 0: ptr[N+1] array; 1: lower_bound in keys[kb, ke)
+struct TileGemmArgs {
+    const int* tile_begin;
+    const int* tile_end;
+    int tile_off;
+    int n_rel, n_root, ncol;
+    int a_kind;
+    const float* src;
+    const float* Hsrc;
+    const int* s_row;
+    const int* s_cnt;
+    const int* s_rel;
+    int K;
+    const float* W;
+    int w_per_rel;
+    const float* Wroot;
+    int trans;
+    int N;
+    float* Y;
+    float* Yroot;
+    int row_lo, row_hi;
+    int y_div;
+    int sel_b;
+};
+
+struct TileItem {
+    int s0, nrows, n_base;
+    int root;  // int, not bool: a padded struct copy is not scalarised (scratch round trip)
+};
+
+__device__ __forceinline__ TileItem tile_item(const TileGemmArgs& a, int w) {
+    TileItem it;
+    const int tile = w / a.ncol;
+    it.n_base = (w - tile * a.ncol) * kColTile;
+    it.root = tile >= a.n_rel;
+    if (!it.root) {
+        const int tt = tile + a.tile_off;
+        it.s0 = ld_uniform(a.tile_begin, tt);
+        it.nrows = ld_uniform(a.tile_end, tt) - it.s0;
+    } else {
+        it.s0 = a.row_lo + (tile - a.n_rel) * kTileRows;
+        it.nrows = min(kTileRows, a.row_hi - it.s0);
+    }
+    return it;
+}
+
+// Issue the loads of an item's A rows (float4 slot j of this thread = tile element
+// threadIdx.x + j·256) into registers; addresses are clamped so every load is valid.
+template <int KB, int WPT>
+__device__ __forceinline__ void tile_issue(const TileGemmArgs& a, const TileItem& it, int tid, float4 (&v)[WPT], int& cnt_raw) {
+    constexpr int W4 = 16 * KB;
+    const bool gathered = !it.root && a.a_kind == 1;
+    const float* base = (it.root || a.a_kind == 1) ? a.src : a.Hsrc;
+    // contiguous rows: base row of the tile; gathered rows: index into s_row
+    const int off = it.root ? it.s0 : (gathered ? it.s0 : it.s0 - a.sel_b);
+    cnt_raw = 1;
+    int row[WPT];
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) row[j] = off + min((tid + j * kThreads) / W4, it.nrows - 1);
+    // uniform branch around the whole index batch (and the dgrad counts): the loads issue back
+    // to back and are waited for once (a per-element select compiles to a branch + vmcnt(0)
+    // around each load)
+    if (gathered) {
+        if (a.y_div) cnt_raw = a.s_cnt[it.s0 + min(tid & (kTileRows - 1), it.nrows - 1)];
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) row[j] = a.s_row[row[j]];
+    }
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) {
+        const int c = min(((tid + j * kThreads) % W4) * 4, a.K - 4);
+        v[j] = *reinterpret_cast<const float4*>(base + (size_t)row[j] * a.K + c);
+    }
+}
+
+template <int KB, int WPT>
+__device__ __forceinline__ void tile_commit(const TileGemmArgs& a, const TileItem& it, int tid, const float4 (&v)[WPT],
+                                            int cnt_raw, float* A, float* scale) {
+    constexpr int W4 = 16 * KB;
+    constexpr int lda = 64 * KB + 4;
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) {
+        const int i = tid + j * kThreads;
+        const int r = i / W4;
+        const int c = (i % W4) * 4;
+        const bool ok = r < it.nrows && c < a.K;
+        *reinterpret_cast<float4*>(A + r * lda + c) = ok ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (tid < kTileRows) scale[tid] = (float)cnt_raw;
+}
+
+// One strip (64 rows × 32 columns, this wave) of a persistent item: b0 arrives holding the
+// item's first B chunk; once its last chunk is in registers the NEXT item's first chunk is
+// loaded into b0, so it is in flight across the epilogue and the item boundary (a cold start
+// would expose a full L2/MALL miss per item).
+// ABL (profiling builds of the bench shape only, MPGNN_OPT_ABLATE bits >> 4): 1 no MFMA (a VALU
+// add consumes the operands), 2 no B loads, 4 no LDS A reads, 8 no epilogue stores.
+template <bool TRANS, bool CLAMP, int ABL = 0>
+__device__ __forceinline__ void mfma_strip(f32x16& acc0, f32x16& acc1, const float* a0p, const float* a1p, int KH,
+                                           int kb, const BLoader<TRANS, CLAMP>& ld, float (&b0)[kKC],
+                                           const BLoader<TRANS, CLAMP>& ld_next) {
+    // A fragments roll one 4-k step ahead: the ds_read_b128 pair for step j+1 is issued before
+    // step j's eight MFMAs, so LDS latency hides behind them (read just in time it was exposed
+    // every 8 MFMAs: ~10 µs of a 37 µs launch).  The read after the last step lands in the
+    // 4-float row pad (lda = Kp + 4) and is never used.
+    float4 ca0, ca1;
+    if constexpr ((ABL & 4) == 0) {
+        ca0 = *reinterpret_cast<const float4*>(a0p);
+        ca1 = *reinterpret_cast<const float4*>(a1p);
+    }
+    auto compute_chunk = [&](const float (&bc)[kKC], int t, int k0) {
+#pragma unroll
+        for (int j = 0; j < kKC; j += 4) {
+            float4 a0, a1;
+            if constexpr (ABL & 4) {
+                a0 = make_float4(1.f, 2.f, 3.f, (float)t);
+                a1 = a0;
+            } else {
+                a0 = ca0;
+                a1 = ca1;
+                ca0 = *reinterpret_cast<const float4*>(a0p + t + j + 4);
+                ca1 = *reinterpret_cast<const float4*>(a1p + t + j + 4);
+                __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of this step's MFMAs
+            }
+            float bq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bq[q] = (!CLAMP || k0 + j + q < ld.K) ? bc[j + q] : 0.0f;
+            if constexpr (ABL & 1) {
+                acc0[j] += a0.x + a0.y + a0.z + a0.w + bq[0] + bq[1] + bq[2] + bq[3];
+                acc1[j] += a1.x + a1.y + a1.z + a1.w;
+                continue;
+            }
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, bq[0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, bq[0], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, bq[1], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, bq[1], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, bq[2], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, bq[2], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, bq[3], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, bq[3], acc1, 0, 0, 0);
+        }
+    };
+    auto ldc = [&](const BLoader<TRANS, CLAMP>& l, int k0, float (&o)[kKC]) {
+        if constexpr (ABL & 2) {
+#pragma unroll
+            for (int j = 0; j < kKC; ++j) o[j] = (float)(k0 + j);
+        } else {
+            l.template load_chunk<kKC>(k0, o);
+        }
+    };
+    float b1[kKC];
+    int t = 0;
+#pragma unroll 1
+    for (; t < KH - 2 * kKC; t += 2 * kKC) {
+        ldc(ld, kb + t + kKC, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        compute_chunk(b0, t, kb + t);
+        __builtin_amdgcn_sched_barrier(0);
+        ldc(ld, kb + t + 2 * kKC, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        compute_chunk(b1, t + kKC, kb + t + kKC);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    ldc(ld, kb + t + kKC, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute_chunk(b0, t, kb + t);
+    __builtin_amdgcn_sched_barrier(0);
+    ldc(ld_next, kb, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    compute_chunk(b1, t + kKC, kb + t + kKC);
+}
+
+__device__ __forceinline__ int opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+__device__ __forceinline__ BSrc item_bsrc(const TileGemmArgs& a, const TileItem& it) {
+    BSrc b;
+    b.W = it.root ? a.Wroot : a.W;
+    if (!it.root && a.w_per_rel) b.W += (size_t)ld_uniform(a.s_rel, it.s0) * a.K * a.N;
+    b.K = a.K;
+    b.N = a.N;
+    b.trans = a.trans;
+    b.ldw = a.trans ? a.K : a.N;
+    return b;
+}
+
+// Item order: the 8 workgroup groups g = blockIdx % 8 (the blocks one XCD receives under
+// round-robin placement — a speed-only assumption) each own a contiguous eighth of the item
+// list, so the relation weights an XCD's L2 pulls in are one eighth of them; within a group
+// the workgroups stride through their eighth.  Bijective for any grid (every item is visited
+// exactly once whatever the placement).
+struct ItemOrder {
+    int base, stride, end;
+    __device__ __forceinline__ ItemOrder(int n_items) {
+        const int g = blockIdx.x & 7;
+        const int per = (n_items + 7) >> 3;
+        base = g * per + (blockIdx.x >> 3);
+        stride = ((int)gridDim.x - g + 7) >> 3;  // workgroups in group g
+        end = min(n_items, (g + 1) * per);
+    }
+};
+
+template <int KB, bool TRANS, bool CLAMP, int ABL = 0>
+__device__ __forceinline__ void tile_gemm_body(const TileGemmArgs& a, float* smem) {
+    constexpr int Kp = 64 * KB;
+    constexpr int KH = Kp / 2;
+    constexpr int lda = Kp + 4;
+    constexpr int ldo = kColTile + 4;                   // staged output tile row stride
+    constexpr int bstride = kTileRows * (lda > ldo ? lda : ldo);
+    constexpr int WPT = 4 * KB;                         // float4 per thread per tile
+    float* bufs = smem;                                 // [2][64][max(lda, ldo)]
+    float* scales = smem + 2 * bstride;                 // [2][64]
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int n_items = (a.n_rel + a.n_root) * a.ncol;
+    const ItemOrder ord(n_items);
+    int w = ord.base;
+    if (w >= ord.end) return;
+
+    float4 v[WPT];
+    int cnt_raw;
+    TileItem cur = tile_item(a, w);
+    tile_issue<KB, WPT>(a, cur, threadIdx.x, v, cnt_raw);
+    float b0[kKC];
+    {
+        const int lane = threadIdx.x & 63;
+        const BLoader<TRANS, CLAMP> ld0(item_bsrc(a, cur), min(cur.n_base + wave * 32 + (lane & 31), a.N - 1));
+        ld0.template load_chunk<kKC>((lane >> 5) * KH, b0);
+    }
+    tile_commit<KB, WPT>(a, cur, threadIdx.x, v, cnt_raw, bufs, scales);
+    __syncthreads();
+    for (int buf = 0; w < ord.end; buf ^= 1) {
+        // Laundered per item: otherwise LICM hoists every thread-invariant LDS/global offset
+        // of the loop body (dozens of them) and holds them live across the loop (spills).
+        const int tid = opaque(threadIdx.x);
+        const int lane = tid & 63;
+        const int c = lane & 31;
+        const int h = lane >> 5;
+        const int wn = w + ord.stride;
+        const bool has_next = wn < ord.end;
+        const TileItem nxt = has_next ? tile_item(a, wn) : cur;
+        if (has_next) tile_issue<KB, WPT>(a, nxt, tid, v, cnt_raw);  // in flight during this item's MFMAs
+        float* A = bufs + buf * bstride;
+        const bool active = cur.n_base + wave * 32 < a.N;
+        const BLoader<TRANS, CLAMP> ld_next(item_bsrc(a, nxt), min(nxt.n_base + wave * 32 + c, a.N - 1));
+        f32x16 acc0, acc1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            acc0[r] = 0.0f;
+            acc1[r] = 0.0f;
+        }
+        {   // unconditional (a wave past N computes clamped columns and stores nothing): a branch
+            // here would join b0 through register copies that wait for the preloaded chunk
+            const BLoader<TRANS, CLAMP> ld(item_bsrc(a, cur), min(cur.n_base + wave * 32 + c, a.N - 1));
+            mfma_strip<TRANS, CLAMP, ABL>(acc0, acc1, A + c * lda + h * KH, A + (32 + c) * lda + h * KH, KH, h * KH, ld,
+                                     b0, ld_next);
+        }
+        // epilogue: accumulators -> LDS (the consumed A buffer) -> whole-row coalesced stores
+        __syncthreads();
+        if (active) {
+            float* o = A + (4 * h) * ldo + wave * 32 + c;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2);
+                o[row * ldo] = acc0[r];
+                o[(row + 32) * ldo] = acc1[r];
+            }
+        }
+        __syncthreads();
+        if constexpr ((ABL & 8) != 0) {
+            if (A[tid] == 1234.5f) a.Y[tid] = 0.0f;  // keep the staged tile observable
+        } else {
+            float* Yt = cur.root ? a.Yroot + (size_t)(cur.s0 - a.row_lo) * a.N : a.Y + (size_t)(cur.s0 - a.sel_b) * a.N;
+            const bool div_rows = !cur.root && a.y_div;
+            const float* sc = scales + buf * kTileRows;
+            const int ncols = min(kColTile, a.N - cur.n_base);
+            if ((a.N & 3) == 0) {
+                const int c4n = ncols >> 2;  // float4 columns of this block
+#pragma unroll
+                for (int j = 0; j < kTileRows * (kColTile / 4) / kThreads; ++j) {
+                    const int i = tid + j * kThreads;
+                    const int row = i >> 5;
+                    const int c4 = i & 31;
+                    if (row < cur.nrows && c4 < c4n) {
+                        float4 val = *reinterpret_cast<const float4*>(A + row * ldo + c4 * 4);
+                        if (div_rows) {
+                            const float d = sc[row];
+                            val.x = val.x / d;
+                            val.y = val.y / d;
+                            val.z = val.z / d;
+                            val.w = val.w / d;
+                        }
+                        *reinterpret_cast<float4*>(Yt + (size_t)row * a.N + cur.n_base + c4 * 4) = val;
+                    }
+                }
+            } else {
+                for (int i = tid; i < kTileRows * kColTile; i += kThreads) {
+                    const int row = i >> 7;
+                    const int cc = i & 127;
+                    if (row < cur.nrows && cc < ncols) {
+                        float val = A[row * ldo + cc];
+                        if (div_rows) val = val / sc[row];
+                        Yt[(size_t)row * a.N + cur.n_base + cc] = val;
+                    }
+                }
+            }
+        }
+        if (has_next) tile_commit<KB, WPT>(a, nxt, tid, v, cnt_raw, bufs + (buf ^ 1) * bstride, scales + (buf ^ 1) * kTileRows);
+        __syncthreads();
+        cur = nxt;
+        w = wn;
+    }
+}
+
+template <int KB>  // Kp = 64·KB
+__global__ __launch_bounds__(kThreads, 2) void tile_gemm_kernel(TileGemmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    // the B-load variant is fixed for the launch: dispatched once, outside the item loop
+    const bool exact_k = a.K == 64 * KB && a.K >= kKC;
+    const int ldw = a.trans ? a.K : a.N;
+    if (!a.trans) {
+        if (exact_k) tile_gemm_body<KB, false, false>(a, smem);
+        else tile_gemm_body<KB, false, true>(a, smem);
+    } else {
+        if (exact_k && (ldw & 3) == 0) tile_gemm_body<KB, true, false>(a, smem);
+        else tile_gemm_body<KB, true, true>(a, smem);
+    }
+}
+
+// profiling-only ablated builds of the bench shape (K = 128, B not transposed)
+template <int ABL>
+__global__ __launch_bounds__(kThreads, 2) void tile_gemm_ablate_kernel(TileGemmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    tile_gemm_body<2, false, false, ABL>(a, smem);
+}
+
+// ----------------------------------------------------------------------------------------
+// row_sum_kernel:  out[i] = (Σ_{entries of row i, in order} src) + extra[i - lo] + bias
+//   (extra and bias only for rows i in [lo, hi)); the forward combine Σ_r Y + Y_root + bias
+//   and the transposed grad_x gather Σ G + G_root.  No LDS, 4 rows per wave.
+// ----------------------------------------------------------------------------------------
+struct RowSumArgs {
+    int N;              // one past the last row
+    int r_begin;        // first row (rows [r_begin, N))
+    int list_kind;      // 0: ptr[row] array; 1: lower_bound in keys[kb, ke)
     const int* ptr;
     const int* keys;
     int kb, ke;
-    const int* idx;
-    int idx_off;
-    const int* fidx;
-    int flo, fhi;
-    const int* ent;     // nullable: ragged entries (ptr / keys then index entries)
-    const float* P;     // piece partials
-    int piece_off;
-    const float* gsrc;  // gathered rows, width G
-    int G;              // output width
-    const float* A;     // dense rows [N, K] (nullable: no root term)
-    int K;
-    const float* W;     // root (K×G, trans=0) or root viewed transposed (trans=1, W[n*K + k])
-    int trans;
-    const float* bias;  // nullable
-    int row_lo, row_hi;
-    float* out;         // [N, G]
+    GatherSrc g;
+    const float* extra; // nullable [hi - lo, F]
+    const float* bias;  // nullable [F]
+    int lo, hi;
+    const int* cnt;     // nullable: divide row i by cnt[i] (segment means)
+    int out_off;        // out row = i - out_off
+    float* out;         // [*, F]
 };
 
 __device__ __forceinline__ int lower_bound_i32(const int* keys, int lo, int hi, int v) {
@@ -592,92 +1021,52 @@ __device__ __forceinline__ int lower_bound_i32(const int* keys, int lo, int hi, 
 }
 
 template <int V, int T>
-__global__ __launch_bounds__(kThreads) void row_tile_kernel(RowTileArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int Gp = round_up(a.G, 4);
-    const int ldg = Gp;
-    const int Kp = round_up(a.K > 0 ? a.K : 1, 16);
-    const int lda = Kp + 4;
-    float* S_lds = smem;                         // [64][ldg]
-    float* A_lds = smem + kTileRows * ldg;       // [64][lda]
-
-    const int row0 = blockIdx.x * kTileRows;
-    int nrows = a.N - row0;
-    nrows = nrows > kTileRows ? kTileRows : nrows;
+__global__ __launch_bounds__(kThreads) void row_sum_kernel(RowSumArgs a) {
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int wr0 = wave * kRowsPerWave;
-    int wn = nrows - wr0;
-    wn = wn < 0 ? 0 : (wn > kRowsPerWave ? kRowsPerWave : wn);
-
+    const int row0 = a.r_begin + (blockIdx.x * kWaves + wave) * kSumRowsPerWave;
+    if (row0 >= a.N) return;
+    const int wn = min(kSumRowsPerWave, a.N - row0);
     int bnd = 0;
-    if (lane <= kRowsPerWave) {
-        int i = row0 + wr0 + (lane <= wn ? lane : wn);
-        if (a.list_kind == 0) bnd = a.ptr[i];
-        else bnd = lower_bound_i32(a.keys, a.kb, a.ke, i);
+    if (lane <= kSumRowsPerWave) {
+        const int i = row0 + (lane <= wn ? lane : wn);
+        bnd = a.list_kind == 0 ? a.ptr[i] : lower_bound_i32(a.keys, a.kb, a.ke, i);
     }
-    GatherSrc g;
-    g.src = a.gsrc;
-    g.F = a.G;
-    g.idx = a.idx;
-    g.idx_off = a.idx_off;
-    g.fidx = a.fidx;
-    g.flo = a.flo;
-    g.fhi = a.fhi;
-    g.ent = a.ent;
-    g.P = a.P;
-    g.piece_off = a.piece_off;
-    wave_gather<V, T, (V * T <= 2 ? 8 : 4)>(g, bnd, wn, nullptr, S_lds + wr0 * ldg, ldg, Gp, nullptr, 0,
-                                            lane);
-    const bool has_root = a.A != nullptr && a.W != nullptr;
-    if (has_root) load_dense_tile(a.A, a.K, row0, nrows, A_lds, lda, Kp);
-    __syncthreads();
-
-    const int n_base = blockIdx.y * kColTile;
-    const int c = lane & 31;
-    const int h = lane >> 5;
-    if (has_root) {
-        BSrc b;
-        b.W = a.W;
-        b.K = a.K;
-        b.N = a.G;
-        b.trans = a.trans;
-        b.ldw = a.trans ? a.K : a.G;
-        MfmaTile mt;
-        mfma_tile(mt, A_lds, lda, Kp, b, n_base, wave, lane);
-        const int col = n_base + mt.nb * 32 + c;
-        if (mt.active && col < a.G) {
-            const float bv = a.bias != nullptr ? a.bias[col] : 0.0f;
+    const int F = a.g.F;
+    wave_gather<V, T, (V * T <= 2 ? 8 : 4), kSumRowsPerWave>(
+        a.g, bnd, wn, lane, [&](int r, bool live, float (&acc)[T][V]) {
+            const int i = row0 + r;
+            if (live) {
+                const bool own = i >= a.lo && i < a.hi;
+                const float div = a.cnt != nullptr ? (float)a.cnt[i] : 1.0f;
+                const float* ex = (own && a.extra != nullptr) ? a.extra + (size_t)(i - a.lo) * F : nullptr;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
+                for (int t = 0; t < T; ++t) {
+                    const int col = (t * 64 + lane) * V;
+                    if (col < F) {
+                        float v[V];
 #pragma unroll
-                for (int half = 0; half < 2; ++half) {
-                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h + 32 * half;
-                    if (row < nrows) {
-                        const int i = row0 + row;
-                        float v = S_lds[row * ldg + col];
-                        if (i >= a.row_lo && i < a.row_hi) {
-                            v = v + (half ? mt.acc1[r] : mt.acc0[r]);
-                            if (a.bias != nullptr) v = v + bv;
+                        for (int q = 0; q < V; ++q) v[q] = a.cnt != nullptr ? acc[t][q] / div : acc[t][q];
+                        if (ex != nullptr) {
+                            float e[V];
+                            vload<V>(ex + col, e);
+#pragma unroll
+                            for (int q = 0; q < V; ++q) v[q] = v[q] + e[q];
                         }
-                        a.out[(size_t)i * a.G + col] = v;
+                        if (own && a.bias != nullptr) {
+                            float bb[V];
+                            vload<V>(a.bias + col, bb);
+#pragma unroll
+                            for (int q = 0; q < V; ++q) v[q] = v[q] + bb[q];
+                        }
+                        vstore<V>(a.out + (size_t)(i - a.out_off) * F + col, v);
                     }
                 }
             }
-        }
-    } else {
-        // no root weight: out = Σ (+ bias on own rows)
-        const int cols = min(kColTile, a.G - n_base);
-        for (int e = threadIdx.x; e < nrows * cols; e += kThreads) {
-            const int row = e / cols;
-            const int col = n_base + (e - row * cols);
-            const int i = row0 + row;
-            float v = S_lds[row * ldg + col];
-            if (a.bias != nullptr && i >= a.row_lo && i < a.row_hi) v = v + a.bias[col];
-            a.out[(size_t)i * a.G + col] = v;
-        }
-    }
+            zero_acc<V, T>(acc);
+        });
 }
+
 
 // ----------------------------------------------------------------------------------------
 // outer_accum_kernel:  P[c] = Σ_{p in chunk c} A[a_row(p)]ᵀ ⊗ B[b_row(p)]   (M × Nn slab)
@@ -875,19 +1264,71 @@ static bool pick_vt(int F, int* V, int* T) {
     } while (0)
 
 template <int V, int T>
-static void launch_seg(const SegTileArgs& a, int ntiles, int ncoltiles, hipStream_t st) {
-    const int Kp = round_up(a.F, 16);
-    const size_t lds = (size_t)(2 * kTileRows + kTileRows * (Kp + 4)) * sizeof(float);
-    hipLaunchKernelGGL((seg_tile_kernel<V, T>), dim3(ntiles, ncoltiles), dim3(kThreads), lds, st, a);
+static void launch_seg(const SegTileArgs& a, int nblocks, int ncoltiles, hipStream_t st) {
+    const int Kp = round_up(a.F, 64);
+    const size_t lds = (size_t)(kTileRows + kTileRows * (Kp + 4)) * sizeof(float);
+    hipLaunchKernelGGL((seg_tile_kernel<V, T>), dim3(nblocks, ncoltiles), dim3(kThreads), lds, st, a);
+}
+
+static int cu_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
+template <int KB>
+static void launch_tile_gemm_kb(const TileGemmArgs& a, hipStream_t st) {
+    constexpr int lda = 64 * KB + 4;
+    constexpr int ldo = kColTile + 4;
+    const size_t lds = (size_t)(2 * kTileRows * (lda > ldo ? lda : ldo) + 2 * kTileRows) * sizeof(float);
+    const int per_cu = (2 * lds <= 160 * 1024) ? 2 : 1;
+    const int n_items = (a.n_rel + a.n_root) * a.ncol;
+    const int grid = std::min(n_items, cu_count() * per_cu);
+    hipLaunchKernelGGL((tile_gemm_kernel<KB>), dim3(grid), dim3(kThreads), lds, st, a);
+}
+
+template <int ABL>
+static void launch_tile_gemm_abl(const TileGemmArgs& a, hipStream_t st) {
+    constexpr int lda = 64 * 2 + 4;
+    constexpr int ldo = kColTile + 4;
+    const size_t lds = (size_t)(2 * kTileRows * (lda > ldo ? lda : ldo) + 2 * kTileRows) * sizeof(float);
+    const int n_items = (a.n_rel + a.n_root) * a.ncol;
+    const int grid = std::min(n_items, cu_count() * 2);
+    hipLaunchKernelGGL((tile_gemm_ablate_kernel<ABL>), dim3(grid), dim3(kThreads), lds, st, a);
+}
+
+static void launch_tile_gemm(const TileGemmArgs& a, hipStream_t st, int abl = 0) {
+    if (abl != 0 && a.K == 128 && !a.trans) {
+        switch (abl) {
+            case 1: launch_tile_gemm_abl<1>(a, st); return;
+            case 2: launch_tile_gemm_abl<2>(a, st); return;
+            case 3: launch_tile_gemm_abl<3>(a, st); return;
+            case 4: launch_tile_gemm_abl<4>(a, st); return;
+            case 6: launch_tile_gemm_abl<6>(a, st); return;
+            case 8: launch_tile_gemm_abl<8>(a, st); return;
+            case 9: launch_tile_gemm_abl<9>(a, st); return;
+            case 14: launch_tile_gemm_abl<14>(a, st); return;
+            default: break;
+        }
+    }
+    const int kb = (round_up(a.K, 64)) / 64;
+    if (kb <= 1) launch_tile_gemm_kb<1>(a, st);
+    else if (kb == 2) launch_tile_gemm_kb<2>(a, st);
+    else if (kb == 3) launch_tile_gemm_kb<3>(a, st);
+    else launch_tile_gemm_kb<4>(a, st);
 }
 
 template <int V, int T>
-static void launch_row(const RowTileArgs& a, int nrowtiles, int ncoltiles, hipStream_t st) {
-    const int Gp = round_up(a.G, 4);
-    const int Kp = round_up(a.K > 0 ? a.K : 1, 16);
-    const bool has_root = a.A != nullptr && a.W != nullptr;
-    const size_t lds = (size_t)(kTileRows * Gp + (has_root ? kTileRows * (Kp + 4) : 0)) * sizeof(float);
-    hipLaunchKernelGGL((row_tile_kernel<V, T>), dim3(nrowtiles, ncoltiles), dim3(kThreads), lds, st, a);
+static void launch_rowsum(const RowSumArgs& a, hipStream_t st) {
+    const int rows_per_block = kWaves * kSumRowsPerWave;
+    const int rows = a.N - a.r_begin;
+    hipLaunchKernelGGL((row_sum_kernel<V, T>), dim3((rows + rows_per_block - 1) / rows_per_block), dim3(kThreads),
+                       0, st, a);
 }
 
 template <int V, int T>
@@ -898,16 +1339,17 @@ static void launch_piece(const PieceArgs& a, hipStream_t st) {
 
 static bool g_exact_order = false;  // MPGNN_OPT_EXACT_ORDER: no ragged pieces anywhere
 static int g_ablate = 0;            // MPGNN_OPT_ABLATE (debug/profiling only)
+static unsigned long long* g_stamps = nullptr;  // MPGNN_OPT_STAMPS (debug/profiling only)
 
 struct Selection {
     int64_t d_lo = 0, d_hi = 0;
     int sel_b = 0, sel_e = 0;
     int t_lo = 0, t_hi = 0;
     int c_lo = 0, c_hi = 0;
-    int sp_lo = 0, sp_hi = 0;   // seg-list pieces of the selection
-    int tap_lo = 0, tap_hi = 0; // ta-list pieces (mode SINGLE)
+    int sp_lo = 0, sp_hi = 0;     // seg-list pieces of the selection
+    int tap_lo = 0, tap_hi = 0;   // ta-list pieces (mode SINGLE)
     int ta_e_lo = 0, ta_e_hi = 0; // ta entry range (mode SINGLE)
-    bool all_segments = false;  // selection covers every local segment
+    bool all_segments = false;    // selection covers every local segment
 };
 
 static int32_t make_selection(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, Selection* s) {
@@ -949,26 +1391,30 @@ static RootChunks root_chunks(int64_t lo, int64_t hi) {
 
 // Workspace: forward and backward regions are used by different calls, so they overlap.
 struct WsLayout {
-    size_t y = 0, pseg = 0, prw = 0;                       // forward
-    size_t g = 0, h = 0, pdx = 0, p = 0, proot = 0, pb = 0; // backward
+    size_t y = 0, yroot = 0, hf = 0, pseg = 0, prw = 0;     // forward
+    size_t g = 0, groot = 0, h = 0, pdx = 0, p = 0, proot = 0, pb = 0;  // backward
     size_t total = 0;
 };
 
 static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s, int F_in, int F_out,
-                          const RootChunks& rc) {
+                          int64_t row_lo, int64_t row_hi, const RootChunks& rc) {
     WsLayout w;
     const size_t S_sel = (size_t)(s.sel_e - s.sel_b);
-    const size_t y_rows = (mode == MPGNN_MODE_ALL) ? (size_t)p->S : S_sel;
+    const size_t rows = (size_t)(row_hi - row_lo);
+    const size_t fmax = (size_t)std::max(F_in, F_out);
     size_t off = 0;
-    w.y = off; off += align256(y_rows * F_out * sizeof(float));
-    w.pseg = off; off += align256((size_t)(s.sp_hi - s.sp_lo) * F_in * sizeof(float));
+    w.y = off; off += align256(S_sel * F_out * sizeof(float));
+    w.yroot = off; off += align256(rows * F_out * sizeof(float));
+    w.hf = off; off += align256(S_sel * F_in * sizeof(float));
+    w.pseg = off; off += align256((size_t)(s.sp_hi - s.sp_lo) * fmax * sizeof(float));
     w.prw = off; off += align256((mode == MPGNN_MODE_ALL ? p->rw_l.piece_b.size() : 0) * F_out * sizeof(float));
     const size_t fwd = off;
     off = 0;
     const size_t dx_pieces = (mode == MPGNN_MODE_ALL) ? p->t_l.piece_b.size() : (size_t)(s.tap_hi - s.tap_lo);
     w.g = off; off += align256(S_sel * F_in * sizeof(float));
+    w.groot = off; off += align256(rows * F_in * sizeof(float));
     w.h = off; off += align256(S_sel * F_in * sizeof(float));
-    w.pdx = off; off += align256(dx_pieces * F_in * sizeof(float));
+    w.pdx = off; off += align256(std::max(dx_pieces, (size_t)(s.sp_hi - s.sp_lo)) * F_in * sizeof(float));
     w.p = off; off += align256((size_t)(s.c_hi - s.c_lo) * F_in * F_out * sizeof(float));
     w.proot = off; off += align256((size_t)rc.n * F_in * F_out * sizeof(float));
     w.pb = off; off += align256((size_t)rc.n * F_out * sizeof(float));
@@ -995,23 +1441,28 @@ static void clamp_rows(const mpgnn_plan* p, int64_t* lo, int64_t* hi) {
     *hi = std::max<int64_t>(*lo, std::min<int64_t>(*hi, p->N));
 }
 
-// Forward segment tiles: Y[seg] = mean(src over seg) @ W_rel(seg)   (W == nullptr: H only)
-static int32_t run_seg_forward(const mpgnn_plan* p, int32_t mode, const Selection& s, const float* x, int F_in,
-                               const float* W, int F_out, float* Y, float* H, float* Pseg, bool exact,
-                               int kind, hipStream_t strm) {
-    const int ntiles = s.t_hi - s.t_lo;
-    if (ntiles == 0) return MPGNN_OK;
+// One seg_tile_kernel launch: relation tiles of the selection (+ root tiles when Wroot).
+//   forward (gather_kind 0): Y[s - sel_b] = mean(src over s) @ W_rel(s), H = the means,
+//                            Yroot[i - row_lo] = src[i] @ Wroot
+//   dgrad   (gather_kind 1): Y[s - sel_b] = (src[node_1(s)] @ W_relᵀ) / cnt, Yroot = src @ Wrootᵀ
+static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, int gather_kind, const float* src,
+                       int K, const float* W, const float* Wroot, int trans, int N, float* Y, float* Yroot,
+                       int64_t row_lo, int64_t row_hi, float* H, float* Pseg, bool exact, int kind,
+                       hipStream_t strm, const float* Hsrc = nullptr) {
+    const int n_rel = s.t_hi - s.t_lo;
+    const int n_root = (Wroot != nullptr) ? (int)((row_hi - row_lo + kTileRows - 1) / kTileRows) : 0;
+    if (n_rel + n_root == 0) return MPGNN_OK;
     int V, T;
-    pick_vt(F_in, &V, &T);
-    const bool ragged = !exact && s.sp_hi > s.sp_lo;
+    pick_vt(K, &V, &T);
+    const bool ragged = gather_kind == 0 && !exact && s.sp_hi > s.sp_lo;
     if (ragged) {
         PieceArgs pa{};
         pa.pb = p->d.seg_pb;
         pa.pe = p->d.seg_pe;
         pa.k_lo = s.sp_lo;
         pa.k_hi = s.sp_hi;
-        pa.src = x;
-        pa.F = F_in;
+        pa.src = src;
+        pa.F = K;
         pa.idx = p->d.e_col;
         pa.P = Pseg;
         TimedLaunch tl(MPGNN_K_PIECE, strm);
@@ -1019,36 +1470,124 @@ static int32_t run_seg_forward(const mpgnn_plan* p, int32_t mode, const Selectio
         int32_t st = hip_check(hipGetLastError(), "piece_sum_kernel(seg) launch");
         if (st != MPGNN_OK) return st;
     }
+    // tile_gemm stages A rows as float4 (K % 4 == 0); other widths take seg_tile_kernel
+    if (gather_kind != 0 && W != nullptr && (K & 3) == 0 && (g_ablate & 15) == 0 && !g_stamps) {
+        TileGemmArgs t{};
+        t.tile_begin = p->d.tile_begin;
+        t.tile_end = p->d.tile_end;
+        t.tile_off = s.t_lo;
+        t.n_rel = n_rel;
+        t.n_root = n_root;
+        t.ncol = (N + kColTile - 1) / kColTile;
+        t.a_kind = gather_kind;
+        t.src = src;
+        t.Hsrc = Hsrc;
+        t.s_row = p->d.s_row;
+        t.s_cnt = p->d.s_cnt;
+        t.s_rel = p->d.s_rel;
+        t.K = K;
+        t.W = W;
+        t.w_per_rel = (mode == MPGNN_MODE_ALL);
+        t.Wroot = Wroot;
+        t.trans = trans;
+        t.N = N;
+        t.Y = Y;
+        t.Yroot = Yroot;
+        t.row_lo = (int)row_lo;
+        t.row_hi = (int)row_hi;
+        t.y_div = gather_kind == 1;
+        t.sel_b = s.sel_b;
+        TimedLaunch tl(kind, strm);
+        launch_tile_gemm(t, strm, g_ablate >> 4);
+        return hip_check(hipGetLastError(), "tile_gemm_kernel launch");
+    }
     SegTileArgs a{};
     a.tile_begin = p->d.tile_begin;
     a.tile_end = p->d.tile_end;
     a.tile_off = s.t_lo;
-    a.gather_kind = 0;
-    a.src = x;
-    a.F = F_in;
+    a.n_rel_tiles = n_rel;
+    a.gather_kind = gather_kind;
+    a.src = src;
+    a.F = K;
     a.s_ptr = ragged ? p->d.seg_ent_ptr : p->d.s_ptr;
     a.e_col = p->d.e_col;
     a.s_row = p->d.s_row;
     a.s_cnt = p->d.s_cnt;
     a.s_rel = p->d.s_rel;
-    a.s_pos = p->d.s_pos;
     a.ent = ragged ? p->d.seg_ent : nullptr;
     a.P = Pseg;
     a.piece_off = s.sp_lo;
     a.W = W;
     a.w_per_rel = (mode == MPGNN_MODE_ALL);
-    a.trans = 0;
-    a.N = W ? F_out : 1;
+    a.Wroot = Wroot;
+    a.trans = trans;
+    a.N = W ? N : 1;
     a.Y = Y;
-    a.y_use_pos = (mode == MPGNN_MODE_ALL);
-    a.y_div = 0;
+    a.Yroot = Yroot;
+    a.row_lo = (int)row_lo;
+    a.row_hi = (int)row_hi;
+    a.y_div = gather_kind == 1;
     a.sel_b = s.sel_b;
     a.H = H;
+    a.Hsrc = Hsrc;
     a.ablate = g_ablate;
-    const int ncol = W ? (F_out + kColTile - 1) / kColTile : 1;
+    a.stamps = (kind == MPGNN_K_SEG_FWD) ? g_stamps : nullptr;
+    const int ncol = W ? (N + kColTile - 1) / kColTile : 1;
     TimedLaunch tl(kind, strm);
-    MPGNN_VT_DISPATCH(V, T, launch_seg, a, ntiles, ncol, strm);
+    MPGNN_VT_DISPATCH(V, T, launch_seg, a, n_rel + n_root, ncol, strm);
     return hip_check(hipGetLastError(), "seg_tile_kernel launch");
+}
+
+// Ordered row sums out[i] = Σ list(i) + extra + bias, with the pieces of long rows first.
+static int32_t run_rowsum(RowSumArgs a, const int* pb, const int* pe, int k_lo, int k_hi, float* P,
+                          hipStream_t strm) {
+    int V, T;
+    pick_vt(a.g.F, &V, &T);
+    if (k_hi > k_lo) {
+        PieceArgs pa{};
+        pa.pb = pb;
+        pa.pe = pe;
+        pa.k_lo = k_lo;
+        pa.k_hi = k_hi;
+        pa.src = a.g.src;
+        pa.F = a.g.F;
+        pa.idx = a.g.idx;
+        pa.idx_off = a.g.idx_off;
+        pa.fidx = a.g.fidx;
+        pa.flo = a.g.flo;
+        pa.fhi = a.g.fhi;
+        pa.P = P;
+        TimedLaunch tl(MPGNN_K_PIECE, strm);
+        MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
+        int32_t st = hip_check(hipGetLastError(), "piece_sum_kernel launch");
+        if (st != MPGNN_OK) return st;
+        a.g.P = P;
+        a.g.piece_off = k_lo;
+    }
+    if (a.N <= a.r_begin) return MPGNN_OK;
+    MPGNN_VT_DISPATCH(V, T, launch_rowsum, a, strm);
+    return hip_check(hipGetLastError(), "row_sum_kernel launch");
+}
+
+// Segment means H[s - sel_b] = (Σ_{e in s} x[node_2(e)]) / cnt(s) for the selection, through
+// the ragged row-sum (pieces of segments > kPieceEntries first) or in exact edge order.
+static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x, int F, float* H, float* Pseg,
+                         bool exact, hipStream_t strm) {
+    if (s.sel_e == s.sel_b) return MPGNN_OK;
+    const bool ragged = !exact && s.sp_hi > s.sp_lo;
+    RowSumArgs a{};
+    a.r_begin = s.sel_b;
+    a.N = s.sel_e;
+    a.list_kind = 0;
+    a.ptr = ragged ? p->d.seg_ent_ptr : p->d.s_ptr;
+    a.g.src = x;
+    a.g.F = F;
+    a.g.idx = p->d.e_col;
+    a.g.ent = ragged ? p->d.seg_ent : nullptr;
+    a.cnt = p->d.s_cnt;
+    a.out = H;
+    a.out_off = s.sel_b;
+    return run_rowsum(a, p->d.seg_pb, p->d.seg_pe, ragged ? s.sp_lo : 0, ragged ? s.sp_hi : 0, Pseg, strm);
 }
 
 }  // namespace mpgnn
@@ -1066,6 +1605,10 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
         g_ablate = (int)value;
         return MPGNN_OK;
     }
+    if (option == MPGNN_OPT_STAMPS) {
+        g_stamps = reinterpret_cast<unsigned long long*>(value);
+        return MPGNN_OK;
+    }
     return arg_error("unknown option " + std::to_string(option));
 }
 
@@ -1078,8 +1621,9 @@ int32_t mpgnn_rel_mean_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, 
     if (s.t_hi == s.t_lo) return MPGNN_OK;
     if (!x || !h) return arg_error("NULL x or h");
     // always in exact edge order: bit-identical to PyG's scatter_add_ mean
-    return run_seg_forward(p, mode, s, x, F, nullptr, 1, nullptr, h, nullptr, true, MPGNN_K_MEAN,
-                           static_cast<hipStream_t>(stream));
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    TimedLaunch tl(MPGNN_K_MEAN, strm);
+    return run_means(p, s, x, F, h, nullptr, true, strm);
 }
 
 int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R,
@@ -1090,7 +1634,8 @@ int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* p, int32_t mode, int64_t re
     int32_t st = make_selection(p, mode, relation, R, &s);
     if (st != MPGNN_OK) return st;
     clamp_rows(p, &row_lo, &row_hi);
-    WsLayout w = ws_layout(p, mode, s, std::max(F_in, 1), std::max(F_out, 1), root_chunks(row_lo, row_hi));
+    WsLayout w = ws_layout(p, mode, s, std::max(F_in, 1), std::max(F_out, 1), row_lo, row_hi,
+                           root_chunks(row_lo, row_hi));
     *bytes = (int64_t)w.total;
     return MPGNN_OK;
 }
@@ -1109,74 +1654,55 @@ int32_t mpgnn_rgcn_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
     clamp_rows(p, &row_lo, &row_hi);
     hipStream_t strm = static_cast<hipStream_t>(stream);
     const RootChunks rc = root_chunks(row_lo, row_hi);
-    const WsLayout w = ws_layout(p, mode, s, F_in, F_out, rc);
+    const WsLayout w = ws_layout(p, mode, s, F_in, F_out, row_lo, row_hi, rc);
     char* ws = static_cast<char*>(workspace);
     float* Y = reinterpret_cast<float*>(ws + w.y);
+    float* Yroot = root ? reinterpret_cast<float*>(ws + w.yroot) : nullptr;
     const bool exact = g_exact_order;
-    const int ncol = (F_out + kColTile - 1) / kColTile;
 
-    // 1) Y[seg] = mean(x over seg) @ W_rel(seg)     (+ h_save = the means)
-    st = run_seg_forward(p, mode, s, x, F_in, weight, F_out, Y, h_save, reinterpret_cast<float*>(ws + w.pseg),
-                         exact, MPGNN_K_SEG_FWD, strm);
+    // 1) H[seg] = mean(x over seg)  (the saved means when training)
+    float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
+    {
+        TimedLaunch tl(MPGNN_K_MEAN, strm);
+        st = run_means(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
+        if (st != MPGNN_OK) return st;
+    }
+    // 2) Y[seg] = H[seg] @ W_rel(seg); Yroot[i] = x[i] @ root   (MFMA tiles)
+    st = run_seg(p, mode, s, 2, x, F_in, weight, root, 0, F_out, Y, Yroot, row_lo, row_hi, nullptr, nullptr, true,
+                 MPGNN_K_SEG_FWD, strm, H);
     if (st != MPGNN_OK) return st;
 
-    // 2) out[i] = Σ_{seg of row i, relation order} Y[seg] + x[i] @ root + bias
-    int V, T;
-    pick_vt(F_out, &V, &T);
-    RowTileArgs a{};
+    // 2) out[i] = (Σ_{seg of row i, relation order} Y[seg] + Yroot[i]) + bias
+    RowSumArgs a{};
     a.N = (int)p->N;
-    a.P = reinterpret_cast<float*>(ws + w.prw);
+    a.g.src = Y;
+    a.g.F = F_out;
+    a.extra = Yroot;
+    a.bias = bias;
+    a.lo = (int)row_lo;
+    a.hi = (int)row_hi;
+    a.out = out;
+    int k_lo = 0, k_hi = 0;
     if (mode == MPGNN_MODE_ALL) {
         const bool ragged = !exact && !p->rw_l.piece_b.empty();
-        const int* fidx = s.all_segments ? nullptr : p->d.rw_seg;
-        if (ragged) {
-            PieceArgs pa{};
-            pa.pb = p->d.rw_pb;
-            pa.pe = p->d.rw_pe;
-            pa.k_lo = 0;
-            pa.k_hi = (int)p->rw_l.piece_b.size();
-            pa.src = Y;
-            pa.F = F_out;
-            pa.fidx = fidx;
-            pa.flo = s.sel_b;
-            pa.fhi = s.sel_e;
-            pa.P = reinterpret_cast<float*>(ws + w.prw);
-            TimedLaunch tl(MPGNN_K_PIECE, strm);
-            MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
-            if ((st = hip_check(hipGetLastError(), "piece_sum_kernel(rw) launch")) != MPGNN_OK) return st;
-        }
         a.list_kind = 0;
         a.ptr = ragged ? p->d.rw_ent_ptr : p->d.rw_ptr;
-        a.ent = ragged ? p->d.rw_ent : nullptr;
-        a.idx = nullptr;
-        a.idx_off = 0;
-        a.fidx = fidx;
-        a.flo = s.sel_b;
-        a.fhi = s.sel_e;
+        a.g.ent = ragged ? p->d.rw_ent : nullptr;
+        a.g.idx = p->d.rw_seg;
+        a.g.idx_off = s.sel_b;
+        a.g.fidx = s.all_segments ? nullptr : p->d.rw_seg;
+        a.g.flo = s.sel_b;
+        a.g.fhi = s.sel_e;
+        if (ragged) k_hi = (int)p->rw_l.piece_b.size();
     } else {
         a.list_kind = 1;  // at most one segment per row: no pieces
         a.keys = p->d.s_row;
         a.kb = s.sel_b;
         a.ke = s.sel_e;
-        a.idx = nullptr;
-        a.idx_off = s.sel_b;
-        a.fidx = nullptr;
-        a.ent = nullptr;
+        a.g.idx_off = s.sel_b;
     }
-    a.gsrc = Y;
-    a.G = F_out;
-    a.A = root ? x : nullptr;
-    a.K = F_in;
-    a.W = root;
-    a.trans = 0;
-    a.bias = bias;
-    a.row_lo = (int)row_lo;
-    a.row_hi = (int)row_hi;
-    a.out = out;
-    const int nrt = (int)((p->N + kTileRows - 1) / kTileRows);
     TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
-    MPGNN_VT_DISPATCH(V, T, launch_row, a, nrt, ncol, strm);
-    return hip_check(hipGetLastError(), "row_tile_kernel launch");
+    return run_rowsum(a, p->d.rw_pb, p->d.rw_pe, k_lo, k_hi, reinterpret_cast<float*>(ws + w.prw), strm);
 }
 
 int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
@@ -1192,127 +1718,66 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
     clamp_rows(p, &row_lo, &row_hi);
     hipStream_t strm = static_cast<hipStream_t>(stream);
     const RootChunks rc = root_chunks(row_lo, row_hi);
-    const WsLayout w = ws_layout(p, mode, s, F_in, F_out, rc);
+    const WsLayout w = ws_layout(p, mode, s, F_in, F_out, row_lo, row_hi, rc);
     char* ws = static_cast<char*>(workspace);
     if (!ws) return arg_error("NULL workspace");
-    const int ntiles = s.t_hi - s.t_lo;
     const size_t wsize = (size_t)F_in * F_out;
     const bool exact = g_exact_order;
 
     // ---- grad_x = Σ_r A_rᵀ ((dout @ W_rᵀ) / cnt) + dout @ rootᵀ ----------------------
     if (grad_x != nullptr && p->N > 0) {
         float* G = reinterpret_cast<float*>(ws + w.g);
-        if (ntiles > 0) {
-            int V, T;
-            pick_vt(F_out, &V, &T);
-            SegTileArgs a{};
-            a.tile_begin = p->d.tile_begin;
-            a.tile_end = p->d.tile_end;
-            a.tile_off = s.t_lo;
-            a.gather_kind = 1;
-            a.src = grad_out;
-            a.F = F_out;
-            a.s_ptr = p->d.s_ptr;
-            a.e_col = p->d.e_col;
-            a.s_row = p->d.s_row;
-            a.s_cnt = p->d.s_cnt;
-            a.s_rel = p->d.s_rel;
-            a.s_pos = p->d.s_pos;
-            a.W = weight;
-            a.w_per_rel = (mode == MPGNN_MODE_ALL);
-            a.trans = 1;
-            a.N = F_in;
-            a.Y = G;
-            a.y_use_pos = 0;
-            a.y_div = 1;
-            a.sel_b = s.sel_b;
-            a.H = nullptr;
-            const int ncol = (F_in + kColTile - 1) / kColTile;
-            TimedLaunch tl(MPGNN_K_SEG_DGRAD, strm);
-            MPGNN_VT_DISPATCH(V, T, launch_seg, a, ntiles, ncol, strm);
-            if ((st = hip_check(hipGetLastError(), "seg_tile_kernel(dgrad) launch")) != MPGNN_OK) return st;
-        }
-        int V, T;
-        pick_vt(F_in, &V, &T);
-        RowTileArgs a{};
+        float* Groot = root ? reinterpret_cast<float*>(ws + w.groot) : nullptr;
+        st = run_seg(p, mode, s, 1, grad_out, F_out, weight, root, 1, F_in, G, Groot, row_lo, row_hi, nullptr,
+                     nullptr, true, MPGNN_K_SEG_DGRAD, strm);
+        if (st != MPGNN_OK) return st;
+        RowSumArgs a{};
         a.N = (int)p->N;
-        a.P = reinterpret_cast<float*>(ws + w.pdx);
-        PieceArgs pa{};
-        pa.src = G;
-        pa.F = F_in;
-        pa.idx_off = s.sel_b;
-        pa.P = reinterpret_cast<float*>(ws + w.pdx);
+        a.g.src = G;
+        a.g.F = F_in;
+        a.g.idx_off = s.sel_b;
+        a.extra = Groot;
+        a.bias = nullptr;
+        a.lo = (int)row_lo;
+        a.hi = (int)row_hi;
+        a.out = grad_x;
+        int k_lo = 0, k_hi = 0;
+        const int *pb = nullptr, *pe = nullptr;
         if (mode == MPGNN_MODE_ALL) {
-            const bool ragged = !exact && !p->t_l.piece_b.empty();
-            const int* fidx = s.all_segments ? nullptr : p->d.t_seg;
-            if (ragged && ntiles > 0) {
-                pa.pb = p->d.t_pb;
-                pa.pe = p->d.t_pe;
-                pa.k_lo = 0;
-                pa.k_hi = (int)p->t_l.piece_b.size();
-                pa.idx = p->d.t_seg;
-                pa.fidx = fidx;
-                pa.flo = s.sel_b;
-                pa.fhi = s.sel_e;
-                TimedLaunch tl(MPGNN_K_PIECE, strm);
-                MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
-                if ((st = hip_check(hipGetLastError(), "piece_sum_kernel(t) launch")) != MPGNN_OK) return st;
-            }
+            const bool ragged = !exact && !p->t_l.piece_b.empty() && s.sel_e > s.sel_b;
             a.list_kind = 0;
             a.ptr = ragged ? p->d.t_ent_ptr : p->d.t_ptr;
-            a.ent = ragged ? p->d.t_ent : nullptr;
-            a.idx = p->d.t_seg;
-            a.idx_off = s.sel_b;
-            a.fidx = fidx;
-            a.flo = s.sel_b;
-            a.fhi = s.sel_e;
-            a.piece_off = 0;
-        } else {
-            const bool ragged = !exact;
-            if (ragged && s.tap_hi > s.tap_lo) {
-                pa.pb = p->d.ta_pb;
-                pa.pe = p->d.ta_pe;
-                pa.k_lo = s.tap_lo;
-                pa.k_hi = s.tap_hi;
-                pa.idx = p->d.ta_seg;
-                TimedLaunch tl(MPGNN_K_PIECE, strm);
-                MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
-                if ((st = hip_check(hipGetLastError(), "piece_sum_kernel(ta) launch")) != MPGNN_OK) return st;
-            }
-            a.list_kind = 1;
+            a.g.ent = ragged ? p->d.t_ent : nullptr;
+            a.g.idx = p->d.t_seg;
+            a.g.fidx = s.all_segments ? nullptr : p->d.t_seg;
+            a.g.flo = s.sel_b;
+            a.g.fhi = s.sel_e;
             if (ragged) {
+                pb = p->d.t_pb;
+                pe = p->d.t_pe;
+                k_hi = (int)p->t_l.piece_b.size();
+            }
+        } else {
+            a.list_kind = 1;
+            a.g.idx = p->d.ta_seg;
+            if (!exact) {
                 a.keys = p->d.ta_key;
                 a.kb = s.ta_e_lo;
                 a.ke = s.ta_e_hi;
-                a.ent = p->d.ta_ent;
-                a.piece_off = s.tap_lo;
+                a.g.ent = p->d.ta_ent;
+                pb = p->d.ta_pb;
+                pe = p->d.ta_pe;
+                k_lo = s.tap_lo;
+                k_hi = s.tap_hi;
             } else {
                 a.keys = p->d.ta_col;
                 a.kb = (s.d_hi > s.d_lo) ? p->rel_edge_ptr[s.d_lo] : 0;
                 a.ke = (s.d_hi > s.d_lo) ? p->rel_edge_ptr[s.d_hi] : 0;
-                a.ent = nullptr;
             }
-            a.idx = p->d.ta_seg;
-            a.idx_off = s.sel_b;
-            a.fidx = nullptr;
         }
-        a.gsrc = G;
-        a.G = F_in;
-        a.A = root ? grad_out : nullptr;
-        a.K = F_out;
-        a.W = root;
-        a.trans = 1;
-        a.bias = nullptr;
-        a.row_lo = (int)row_lo;
-        a.row_hi = (int)row_hi;
-        a.out = grad_x;
-        const int nrt = (int)((p->N + kTileRows - 1) / kTileRows);
-        const int ncol = (F_in + kColTile - 1) / kColTile;
-        {
-            TimedLaunch tl(MPGNN_K_ROW_DX, strm);
-            MPGNN_VT_DISPATCH(V, T, launch_row, a, nrt, ncol, strm);
-        }
-        if ((st = hip_check(hipGetLastError(), "row_tile_kernel(dx) launch")) != MPGNN_OK) return st;
+        TimedLaunch tl(MPGNN_K_ROW_DX, strm);
+        st = run_rowsum(a, pb, pe, k_lo, k_hi, reinterpret_cast<float*>(ws + w.pdx), strm);
+        if (st != MPGNN_OK) return st;
     }
 
     const int mt = (F_in + kColTile - 1) / kColTile;
@@ -1329,8 +1794,7 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
             const float* H = h_save;
             if (H == nullptr) {
                 float* Hw = reinterpret_cast<float*>(ws + w.h);
-                st = run_seg_forward(p, mode, s, x, F_in, nullptr, 1, nullptr, Hw, reinterpret_cast<float*>(ws + w.pdx),
-                                     true, MPGNN_K_MEAN, strm);
+                st = run_means(p, s, x, F_in, Hw, reinterpret_cast<float*>(ws + w.pdx), exact, strm);
                 if (st != MPGNN_OK) return st;
                 H = Hw;
             }
@@ -1428,6 +1892,35 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         }
     }
     return MPGNN_OK;
+}
+
+// Debug: workgroups per CU the runtime admits for the forward tile kernel at gather width F.
+int32_t mpgnn_debug_occupancy(int32_t F, int32_t* seg_tile_blocks_per_cu, int32_t* tile_gemm_blocks_per_cu,
+                              int32_t* tile_gemm_grid) {
+    if (!seg_tile_blocks_per_cu || !tile_gemm_blocks_per_cu || !tile_gemm_grid) return arg_error("NULL argument");
+    int V, T;
+    if (!pick_vt(F, &V, &T)) return MPGNN_ERR_UNSUPPORTED;
+    const int Kp = round_up(F, 64);
+    const size_t lds = (size_t)(kTileRows + kTileRows * (Kp + 4)) * sizeof(float);
+    int nb = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, seg_tile_kernel<2, 1>, kThreads, lds);
+    *seg_tile_blocks_per_cu = nb;
+    if (e != hipSuccess) return hip_check(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    const int kb = Kp / 64;
+    int nt = 0;
+    size_t lds_t = 0;
+    auto occ = [&](auto kern, int KB) {
+        const int lda = 64 * KB + 4, ldo = kColTile + 4;
+        lds_t = (size_t)(2 * kTileRows * (lda > ldo ? lda : ldo) + 2 * kTileRows) * sizeof(float);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nt, kern, kThreads, lds_t);
+    };
+    if (kb <= 1) e = occ(tile_gemm_kernel<1>, 1);
+    else if (kb == 2) e = occ(tile_gemm_kernel<2>, 2);
+    else if (kb == 3) e = occ(tile_gemm_kernel<3>, 3);
+    else e = occ(tile_gemm_kernel<4>, 4);
+    *tile_gemm_blocks_per_cu = nt;
+    *tile_gemm_grid = cu_count() * ((2 * lds_t <= 160 * 1024) ? 2 : 1);
+    return hip_check(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
 }
 
 int32_t mpgnn_timing_enable(int32_t on) {

@@ -58,6 +58,14 @@ def main():
         res["fwd_no_gather"] = timed(lambda: conv(x, ei, et), args.iters)
         _lib.lib.mpgnn_set_option(1, 2)
         res["fwd_no_mfma"] = timed(lambda: conv(x, ei, et), args.iters)
+        _lib.lib.mpgnn_set_option(1, 4)
+        res["fwd_no_epilogue"] = timed(lambda: conv(x, ei, et), args.iters)
+        _lib.lib.mpgnn_set_option(1, 8)
+        res["fwd_no_mfma_loop"] = timed(lambda: conv(x, ei, et), args.iters)
+        _lib.lib.mpgnn_set_option(1, 1 | 8)
+        res["fwd_epilogue_only"] = timed(lambda: conv(x, ei, et), args.iters)
+        _lib.lib.mpgnn_set_option(1, 1 | 4)
+        res["fwd_mfma_only"] = timed(lambda: conv(x, ei, et), args.iters)
         _lib.lib.mpgnn_set_option(1, 0)
         _lib.set_exact_order(True)
         res["fwd_exact"] = timed(lambda: conv(x, ei, et), args.iters)
@@ -69,6 +77,12 @@ def main():
         o.backward(torch.ones_like(o))
 
     res["fwd_bwd"] = timed(fb, args.iters)
+    import ctypes
+    occ, occ_t, grid_t = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    _lib.lib.mpgnn_debug_occupancy(F, ctypes.byref(occ), ctypes.byref(occ_t), ctypes.byref(grid_t))
+    res["seg_tile_blocks_per_cu"] = occ.value
+    res["tile_gemm_blocks_per_cu"] = occ_t.value
+    res["tile_gemm_grid"] = grid_t.value
     plan = mpgnn_amd.get_plan(ei, et, g.num_nodes)
     res["plan"] = {"S": plan.num_segments, "E": plan.num_edges, "tiles": plan.num_tiles}
     print(json.dumps(res))
