@@ -284,9 +284,14 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
             p->tile_end.push_back(std::min<int32_t>(s + kTileRows, p->rel_seg_ptr[d + 1]));
         }
         p->rel_tile_ptr[d + 1] = (int32_t)p->tile_begin.size();
-        for (int32_t s = p->rel_seg_ptr[d]; s < p->rel_seg_ptr[d + 1]; s += kChunkRows) {
+        // balanced chunks of at most kChunkRows segments (multiples of 32 rows but the last)
+        const int32_t sb = p->rel_seg_ptr[d], se = p->rel_seg_ptr[d + 1];
+        const int32_t nch = (se - sb + kChunkRows - 1) / kChunkRows;
+        const int32_t per = nch > 0 ? ((se - sb + nch - 1) / nch + 31) / 32 * 32 : 0;
+        for (int32_t s = sb; s < se; s += per) {
             p->chunk_begin.push_back(s);
-            p->chunk_end.push_back(std::min<int32_t>(s + kChunkRows, p->rel_seg_ptr[d + 1]));
+            p->chunk_end.push_back(std::min<int32_t>(s + per, se));
+            p->chunk_dst.push_back(nch == 1 ? p->rel_val32[d] : -1);
         }
         p->rel_chunk_ptr[d + 1] = (int32_t)p->chunk_begin.size();
     }
@@ -449,6 +454,7 @@ int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
         {&p->d.tile_begin, &p->tile_begin}, {&p->d.tile_end, &p->tile_end},
         {&p->d.chunk_begin, &p->chunk_begin}, {&p->d.chunk_end, &p->chunk_end},
         {&p->d.rel_chunk_ptr, &p->rel_chunk_ptr}, {&p->d.rel_val32, &p->rel_val32},
+        {&p->d.chunk_dst, &p->chunk_dst},
         {&p->d.seg_ent, &p->seg_l.ent}, {&p->d.seg_ent_ptr, &p->seg_l.ent_ptr},
         {&p->d.seg_pb, &p->seg_l.piece_b}, {&p->d.seg_pe, &p->seg_l.piece_e},
         {&p->d.t_ent, &p->t_l.ent}, {&p->d.t_ent_ptr, &p->t_l.ent_ptr},

@@ -13,8 +13,9 @@ namespace mpgnn {
 // Segments are packed into relation-pure tiles of this many rows: one workgroup of the
 // segment-transform kernel owns one tile (rgcn_kernels.hip, seg_tile_kernel).
 constexpr int kTileRows = 64;
-// Relation-pure reduction chunks for the weight gradient (outer_accum_kernel).
-constexpr int kChunkRows = 256;
+// Relation-pure reduction chunks for the weight gradient (outer_accum_kernel): at most this
+// many segments, balanced within a relation (bounds the longest workgroup's MFMA chain).
+constexpr int kChunkRows = 128;
 // Ragged lists: a run (segment / gathered row) longer than this many entries is cut into
 // ordered pieces of at most kPieceEntries, summed by piece_sum_kernel; consumers then add the
 // piece partials in order.  Bounds the serial work of every wave (hub skew).
@@ -46,6 +47,7 @@ struct DeviceTables {
     int32_t* chunk_begin = nullptr; // [num_chunks]
     int32_t* chunk_end = nullptr;   // [num_chunks]
     int32_t* rel_chunk_ptr = nullptr; // [nrel+1]
+    int32_t* chunk_dst = nullptr;   // [num_chunks] weight index when the relation has ONE chunk, else -1
     int32_t* rel_val32 = nullptr;   // [nrel] relation id clamped to int32 (-1 when it does not fit)
     // ragged lists (see RaggedHost)
     int32_t *seg_ent = nullptr, *seg_ent_ptr = nullptr, *seg_pb = nullptr, *seg_pe = nullptr;
@@ -84,6 +86,7 @@ struct mpgnn_plan {
     std::vector<int32_t> tile_begin, tile_end; // [num_tiles]
     std::vector<int32_t> chunk_begin, chunk_end; // [num_chunks]
     std::vector<int32_t> rel_val32;            // [nrel]
+    std::vector<int32_t> chunk_dst;            // [num_chunks] see DeviceTables::chunk_dst
 
     // ragged lists: segments over edges (forward gather), node_2 over col-major edges (grad_x,
     // all relations), (relation, node_2) runs over ta order (grad_x, one relation), node_1

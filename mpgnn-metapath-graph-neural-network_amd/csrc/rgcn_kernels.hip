@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -88,7 +89,7 @@ __device__ __forceinline__ int ld_uniform(const int* p, int i) {
 // ent[q] < 0, the ordered partial sum P[-ent[q]-1 - piece_off] of a piece of a long run
 // (piece_sum_kernel).  Position p contributes source row
 //     src_row(p) = (idx ? idx[p] : p) - idx_off
-// unless the filter rejects it (fidx[p] outside [flo, fhi)).  Lanes span the feature dimension
+// unless the filter rejects it (idx[p] outside [flo, fhi)).  Lanes span the feature dimension
 // (V floats per lane, T chunks of 64·V columns); every lane adds its columns in entry order
 // starting from 0.0f, which is exactly ATen's sequential scatter_add_ into a zeroed output —
 // for runs without pieces the sums are bit-identical to the reference.  Loads are issued
@@ -101,8 +102,9 @@ struct GatherSrc {
     int F;
     const int* idx;    // nullable
     int idx_off;
-    const int* fidx;   // nullable filter index
+    int filter;        // keep a position only when idx[p] lies in [flo, fhi)
     int flo, fhi;
+    const int* dummy;  // any valid int table: the target of loads whose result is discarded
     const int* ent;    // nullable: two-level entries (position >= 0 | -(piece+1))
     const float* P;    // piece partial sums [*, F] (rows k - piece_off)
     int piece_off;
@@ -126,25 +128,21 @@ __device__ __forceinline__ void wave_gather(const GatherSrc& g, int bnd, int nro
 
     for (int pb = p_begin; pb < p_end; pb += 64) {
         const int np = min(64, p_end - pb);
-        int my_src = 0;
-        bool my_keep = false;
-        bool my_piece = false;
-        if (lane < np) {
-            const int e = g.ent != nullptr ? g.ent[pb + lane] : pb + lane;
-            if (e >= 0) {
-                my_keep = true;
-                if (g.fidx != nullptr) {
-                    const int f = g.fidx[e];
-                    my_keep = (f >= g.flo) && (f < g.fhi);
-                }
-                my_src = (g.idx != nullptr ? g.idx[e] : e) - g.idx_off;
-            } else {
-                my_keep = true;
-                my_piece = true;
-                my_src = -e - 1 - g.piece_off;
-            }
-            if (!my_keep) my_src = 0;  // rejected entry: a valid row is loaded, never added
-        }
+        // branch-free index resolution: every load is issued (clamped or from the dummy
+        // table) and its result selected — a branch around a load makes hipcc wait for it at
+        // the join, and the join here comes before the row loads
+        const int qq = min(pb + lane, p_end - 1);
+        const bool has_ent = g.ent != nullptr;
+        const bool has_idx = g.idx != nullptr;
+        const int e_raw = (has_ent ? g.ent : g.dummy)[has_ent ? qq : 0];
+        const int e = has_ent ? e_raw : qq;
+        const bool my_piece = e < 0;
+        const int ix_raw = (has_idx ? g.idx : g.dummy)[has_idx ? max(e, 0) : 0];
+        const int ix = has_idx ? ix_raw : e;
+        bool my_keep = lane < np;
+        if (g.filter) my_keep = my_keep && (my_piece || (ix >= g.flo && ix < g.fhi));
+        int my_src = my_piece ? -e - 1 - g.piece_off : ix - g.idx_off;
+        my_src = my_keep ? my_src : 0;  // rejected entry: a valid row is loaded, never added
         const unsigned long long keep = __ballot(my_keep);
         const unsigned long long from_piece = __ballot(my_piece);
         float v[2][UNR][T][V];
@@ -178,14 +176,17 @@ __device__ __forceinline__ void wave_gather(const GatherSrc& g, int bnd, int nro
                 }
             }
         };
-        issue(v[0], 0);
+        // Two groups of UNR row loads are issued together, then consumed in order.  No buffer
+        // is carried across iterations: a loop-carried buffer is copied at the back edge, and
+        // the copy waits for the loads just issued into it (one round trip per group).
+        // sched_barrier(0) keeps the loads ahead of the adds.
         for (int u = 0; u < np; u += 2 * UNR) {
-            if (u + UNR < np) issue(v[1], u + UNR);
+            issue(v[0], u);
+            issue(v[1], u + UNR);  // entries past np are clamped loads, never added
+            __builtin_amdgcn_sched_barrier(0);
             consume(v[0], u);
-            if (u + UNR < np) {
-                if (u + 2 * UNR < np) issue(v[0], u + 2 * UNR);
-                consume(v[1], u + UNR);
-            }
+            consume(v[1], u + UNR);
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
     for (; r < RPW; ++r) flush(r, r < nrows, acc);
@@ -211,8 +212,9 @@ struct PieceArgs {
     int F;
     const int* idx;
     int idx_off;
-    const int* fidx;
+    int filter;
     int flo, fhi;
+    const int* dummy;
     float* P;
 };
 
@@ -226,7 +228,8 @@ __global__ __launch_bounds__(kThreads) void piece_sum_kernel(PieceArgs a) {
     g.F = a.F;
     g.idx = a.idx;
     g.idx_off = a.idx_off;
-    g.fidx = a.fidx;
+    g.filter = a.filter;
+    g.dummy = a.dummy;
     g.flo = a.flo;
     g.fhi = a.fhi;
     const int bnd = lane == 0 ? a.pb[k] : a.pe[k];
@@ -528,6 +531,7 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
     GatherSrc g{};
     g.src = a.src;
     g.F = a.F;
+    g.dummy = a.s_ptr;
     int bnd = 0;
     const int* cnt_rows = nullptr;
     if (root_tile) {
@@ -1033,50 +1037,91 @@ __global__ __launch_bounds__(kThreads) void row_sum_kernel(RowSumArgs a) {
         bnd = a.list_kind == 0 ? a.ptr[i] : lower_bound_i32(a.keys, a.kb, a.ke, i);
     }
     const int F = a.g.F;
-    wave_gather<V, T, (V * T <= 2 ? 8 : 4), kSumRowsPerWave>(
-        a.g, bnd, wn, lane, [&](int r, bool live, float (&acc)[T][V]) {
-            const int i = row0 + r;
-            if (live) {
-                const bool own = i >= a.lo && i < a.hi;
-                const float div = a.cnt != nullptr ? (float)a.cnt[i] : 1.0f;
-                const float* ex = (own && a.extra != nullptr) ? a.extra + (size_t)(i - a.lo) * F : nullptr;
+    // per-row operands of the flush, loaded up front with the row bounds: a load inside the
+    // flush waits (vmcnt is in order) for every row load already in flight
+    // (unconditional: absent operands read a valid dummy row and are discarded by selects)
+    const bool has_cnt = a.cnt != nullptr;
+    const int cnt_raw = (has_cnt ? a.cnt : a.g.dummy)[has_cnt ? min(row0 + min(lane, kSumRowsPerWave - 1), a.N - 1) : 0];
+    const int cnt_l = has_cnt ? cnt_raw : 1;
+    float ex[kSumRowsPerWave][T][V], bb[T][V];
+    int colc[T];
 #pragma unroll
-                for (int t = 0; t < T; ++t) {
-                    const int col = (t * 64 + lane) * V;
-                    if (col < F) {
-                        float v[V];
+    for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, F - V);
+    const bool has_ex = a.extra != nullptr && a.hi > a.lo;
+    const bool has_b = a.bias != nullptr;
 #pragma unroll
-                        for (int q = 0; q < V; ++q) v[q] = a.cnt != nullptr ? acc[t][q] / div : acc[t][q];
-                        if (ex != nullptr) {
-                            float e[V];
-                            vload<V>(ex + col, e);
+    for (int r = 0; r < kSumRowsPerWave; ++r) {
+        const int i = min(max(row0 + r, a.lo), a.hi - 1);  // clamped into the own range
+        const float* eb = has_ex ? a.extra + (size_t)(i - a.lo) * F : a.g.src;
 #pragma unroll
-                            for (int q = 0; q < V; ++q) v[q] = v[q] + e[q];
-                        }
-                        if (own && a.bias != nullptr) {
-                            float bb[V];
-                            vload<V>(a.bias + col, bb);
+        for (int t = 0; t < T; ++t) {
+            vload<V>(eb + (has_ex ? colc[t] : 0), ex[r][t]);
 #pragma unroll
-                            for (int q = 0; q < V; ++q) v[q] = v[q] + bb[q];
-                        }
-                        vstore<V>(a.out + (size_t)(i - a.out_off) * F + col, v);
+            for (int q = 0; q < V; ++q) ex[r][t][q] = has_ex ? ex[r][t][q] : 0.0f;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        vload<V>((has_b ? a.bias : a.g.src) + (has_b ? colc[t] : 0), bb[t]);
+#pragma unroll
+        for (int q = 0; q < V; ++q) bb[t][q] = has_b ? bb[t][q] : 0.0f;
+    }
+    // flush of row r: r is wave-uniform, so it is dispatched to a copy with a compile-time row
+    // (indexing ex[r] with a runtime r turned the array into LDS traffic)
+    auto flush_row = [&](auto RI, bool live, float (&acc)[T][V]) {
+        constexpr int r = decltype(RI)::value;
+        const int i = row0 + r;
+        if (live) {
+            const bool own = i >= a.lo && i < a.hi;
+            const float div = (float)readlane(cnt_l, r);
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const int col = (t * 64 + lane) * V;
+                if (col < F) {
+                    float v[V];
+#pragma unroll
+                    for (int q = 0; q < V; ++q) {
+                        v[q] = has_cnt ? acc[t][q] / div : acc[t][q];
+                        if (own) v[q] = (v[q] + ex[r][t][q]) + bb[t][q];  // zeros when absent
                     }
+                    vstore<V>(a.out + (size_t)(i - a.out_off) * F + col, v);
                 }
             }
-            zero_acc<V, T>(acc);
+        }
+        zero_acc<V, T>(acc);
+    };
+    static_assert(kSumRowsPerWave == 4, "flush dispatch below");
+    wave_gather<V, T, (V * T <= 2 ? 8 : 4), kSumRowsPerWave>(
+        a.g, bnd, wn, lane, [&](int r, bool live, float (&acc)[T][V]) {
+            if (r == 0) flush_row(std::integral_constant<int, 0>{}, live, acc);
+            else if (r == 1) flush_row(std::integral_constant<int, 1>{}, live, acc);
+            else if (r == 2) flush_row(std::integral_constant<int, 2>{}, live, acc);
+            else flush_row(std::integral_constant<int, 3>{}, live, acc);
         });
 }
 
 
 // ----------------------------------------------------------------------------------------
-// outer_accum_kernel:  P[c] = Σ_{p in chunk c} A[a_row(p)]ᵀ ⊗ B[b_row(p)]   (M × Nn slab)
-//   segment chunks: p = segment id, a_row = p - a_off (H), b_row = s_row[p] (dout)
-//   row chunks:     p = node id,    a_row = p (x),          b_row = p (dout)
+// outer_accum_kernel:  D[c] = Σ_{p in chunk c} A[a_row(p)]ᵀ ⊗ B[b_row(p)]   (M × Nn, one
+// 128 × 128 block per workgroup: grid (chunks, M/128, Nn/128))
+//   dW_r = Σ_{seg of r} h_segᵀ dout[node_1(seg)]   (A = H rows, B = dout rows via b_idx)
+//   droot = Σ_i x_iᵀ dout_i, dbias = Σ_i dout_i     (A = x, B = dout, contiguous rows)
+// A chunk's rows stream through LDS in slices of 32: the index loads run two slices ahead,
+// the row loads one slice ahead (registers), so each slice costs one barrier and its MFMAs
+// hide the next slice's memory.  The MFMA k-step pairs rows (2t, 2t+1) across the lane halves,
+// so a slice of nr rows takes ceil(nr/2) steps — a 3-segment relation runs 2 steps, not 16.
+// LDS rows are stored in pairs padded so that rows 2t and 2t+1 fall 32 banks apart (the two
+// lane halves of a ds_read_b32 are conflict-free).  D goes to a partial slab P[c] — or, when
+// the chunk is its group's only chunk (`dst_idx` ≥ 0), straight into dst[dst_idx]; the ordered
+// slab sum (reduce_slabs_kernel) then skips that group.
 // ----------------------------------------------------------------------------------------
 struct OuterArgs {
     const int* chunk_begin;  // nullable: row chunks [row_lo + c*chunk, ...)
     const int* chunk_end;
+    const int* chunk_dst;    // nullable: weight index of a relation's single chunk, else -1
     int chunk_off;
+    int dst_mode;            // 0 slabs only; 1 chunk_dst indexes dst (mode ALL); 2 chunk_dst >= 0
+                             // means "write dst itself" (one weight); 3 single root chunk -> dst
     int row_lo, row_hi, chunk_rows;
     const float* A;
     int M;
@@ -1085,21 +1130,24 @@ struct OuterArgs {
     int Nn;
     const int* b_idx;        // nullable
     float* P;                // [nchunks][M][Nn]
+    float* dst;              // direct destination (see dst_mode)
     float* Pb;               // nullable: [nchunks][Nn] column sums of B (bias grad)
+    float* dst_b;            // direct bias destination when dst_mode == 3
 };
 
-__global__ __launch_bounds__(kThreads) void outer_accum_kernel(OuterArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int ld = kColTile + 4;
-    float* A_lds = smem;                 // [kSlice][ld]
-    float* B_lds = smem + kSlice * ld;   // [kSlice][ld]
-    int* s_brow = reinterpret_cast<int*>(smem + 2 * kSlice * ld);  // [kSlice]
+constexpr int kOuterLd = 288;                        // one row pair: 128 + 32 pad + 128
+__device__ __forceinline__ int outer_row(int k) { return (k >> 1) * kOuterLd + (k & 1) * 160; }
+constexpr int kOuterBuf = (kSlice / 2) * kOuterLd;   // floats per 32-row matrix image
 
+template <bool VEC>
+__global__ __launch_bounds__(kThreads, 2) void outer_accum_kernel(OuterArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* bufs = smem;  // [2 buffers][A, B][kOuterBuf]
     const int cidx = blockIdx.x;
     int p0, p1;
     if (a.chunk_begin != nullptr) {
-        p0 = a.chunk_begin[cidx + a.chunk_off];
-        p1 = a.chunk_end[cidx + a.chunk_off];
+        p0 = ld_uniform(a.chunk_begin, cidx + a.chunk_off);
+        p1 = ld_uniform(a.chunk_end, cidx + a.chunk_off);
     } else {
         p0 = a.row_lo + cidx * a.chunk_rows;
         p1 = min(a.row_hi, p0 + a.chunk_rows);
@@ -1108,67 +1156,151 @@ __global__ __launch_bounds__(kThreads) void outer_accum_kernel(OuterArgs a) {
     const int n_base = blockIdx.z * kColTile;
     const int mcols = min(kColTile, a.M - m_base);
     const int ncols = min(kColTile, a.Nn - n_base);
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
     const int c = lane & 31;
     const int h = lane >> 5;
-    // wave w owns blocks b = w + 4q (q < 4) of the 4 × 4 grid, b = mb*4 + nb
+    const int nslices = (p1 - p0 + kSlice - 1) / kSlice;
+
+    // staging: thread t owns float4 slots i = t + j·256 (j < 4) of each 32 × 128 slice:
+    // row i >> 5, columns 4·(i & 31) .. +3 (scalar path: 16 floats, row i >> 7, column i & 127)
+    constexpr int NS = VEC ? 4 : 16;
+    float4 va[VEC ? 4 : 1], vb[VEC ? 4 : 1];
+    float sa[VEC ? 1 : 16], sb[VEC ? 1 : 16];
+    int bi[NS];  // B row index of each staged slot (next slice), loaded one slice earlier
+    int bi_next[NS];
+    auto slot_row = [&](int j) { return VEC ? ((tid + j * kThreads) >> 5) : ((tid + j * kThreads) >> 7); };
+    auto slot_col = [&](int j) { return VEC ? 4 * ((tid + j * kThreads) & 31) : ((tid + j * kThreads) & 127); };
+    auto load_idx = [&](int slice, int (&o)[NS]) {
+        const int ps = p0 + slice * kSlice;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int p = min(ps + slot_row(j), p1 - 1);
+            o[j] = a.b_idx != nullptr ? a.b_idx[p] : p;
+        }
+    };
+    auto issue = [&](int slice) {
+        const int ps = p0 + slice * kSlice;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int ra = min(ps + slot_row(j), p1 - 1) - a.a_off;
+            if constexpr (VEC) {
+                const int ca = min(m_base + slot_col(j), a.M - 4);
+                const int cb = min(n_base + slot_col(j), a.Nn - 4);
+                va[j] = *reinterpret_cast<const float4*>(a.A + (size_t)ra * a.M + ca);
+                vb[j] = *reinterpret_cast<const float4*>(a.B + (size_t)bi[j] * a.Nn + cb);
+            } else {
+                const int ca = min(m_base + slot_col(j), a.M - 1);
+                const int cb = min(n_base + slot_col(j), a.Nn - 1);
+                sa[j] = a.A[(size_t)ra * a.M + ca];
+                sb[j] = a.B[(size_t)bi[j] * a.Nn + cb];
+            }
+        }
+    };
+    auto commit = [&](int slice, float* buf) {
+        const int nr = min(kSlice, p1 - p0 - slice * kSlice);
+        float* Al = buf;
+        float* Bl = buf + kOuterBuf;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int r = slot_row(j);
+            const int col = slot_col(j);
+            const bool live = r < nr;
+            if constexpr (VEC) {
+                // bit mask, not a select of the array element (that one went through scratch)
+                const unsigned ka = (live && col < mcols) ? ~0u : 0u;
+                const unsigned kb = (live && col < ncols) ? ~0u : 0u;
+                auto msk = [](float4 v, unsigned k) {
+                    return make_float4(__uint_as_float(__float_as_uint(v.x) & k), __uint_as_float(__float_as_uint(v.y) & k),
+                                       __uint_as_float(__float_as_uint(v.z) & k), __uint_as_float(__float_as_uint(v.w) & k));
+                };
+                *reinterpret_cast<float4*>(Al + outer_row(r) + col) = msk(va[j], ka);
+                *reinterpret_cast<float4*>(Bl + outer_row(r) + col) = msk(vb[j], kb);
+            } else {
+                Al[outer_row(r) + col] = (live && col < mcols) ? sa[j] : 0.0f;
+                Bl[outer_row(r) + col] = (live && col < ncols) ? sb[j] : 0.0f;
+            }
+        }
+    };
+
     f32x16 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
-    const int nb = wave;  // every q of this wave shares column strip `wave`
     float bsum = 0.0f;
+    const bool do_bsum = a.Pb != nullptr && blockIdx.y == 0 && tid < kColTile;
 
-    for (int ps = p0; ps < p1; ps += kSlice) {
-        const int nr = min(kSlice, p1 - ps);
-        if (threadIdx.x < kSlice) {
-            const int p = ps + threadIdx.x;
-            s_brow[threadIdx.x] = threadIdx.x < nr ? (a.b_idx ? a.b_idx[p] : p) : 0;
-        }
-        __syncthreads();
-        for (int e = threadIdx.x; e < kSlice * kColTile; e += kThreads) {
-            const int r = e / kColTile;
-            const int col = e - r * kColTile;
-            float av = 0.0f, bv = 0.0f;
-            if (r < nr) {
-                if (col < mcols) av = a.A[(size_t)(ps + r - a.a_off) * a.M + m_base + col];
-                if (col < ncols) bv = a.B[(size_t)s_brow[r] * a.Nn + n_base + col];
-            }
-            A_lds[r * ld + col] = av;
-            B_lds[r * ld + col] = bv;
-        }
-        __syncthreads();
-        if (a.Pb != nullptr && blockIdx.y == 0 && threadIdx.x < kColTile) {
-            for (int r = 0; r < nr; ++r) bsum += B_lds[r * ld + threadIdx.x];
-        }
-#pragma unroll 4
-        for (int t = 0; t < kSlice / 2; ++t) {
-            const int k = h * (kSlice / 2) + t;
-            const float bv = B_lds[k * ld + nb * 32 + c];
+    if (nslices > 0) {
+        load_idx(0, bi);
+        if (nslices > 1) load_idx(1, bi_next);
+        issue(0);
+        commit(0, bufs);
+    }
+    __syncthreads();
+    for (int sl = 0; sl < nslices; ++sl) {
+        float* cur = bufs + (sl & 1) * 2 * kOuterBuf;
+        const bool more = sl + 1 < nslices;  // uniform
+        if (more) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float av = A_lds[k * ld + q * 32 + c];
-                acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[q], 0, 0, 0);
-            }
+            for (int j = 0; j < NS; ++j) bi[j] = bi_next[j];
+            if (sl + 2 < nslices) load_idx(sl + 2, bi_next);
+            issue(sl + 1);
         }
+        const int nr = min(kSlice, p1 - p0 - sl * kSlice);
+        if (do_bsum) {
+            const float* Bl = cur + kOuterBuf;
+            for (int r = 0; r < nr; ++r) bsum += Bl[outer_row(r) + tid];
+        }
+        // k-step t covers rows 2t (lanes h = 0) and 2t + 1 (h = 1); rows >= nr are zero
+        const float* Ar = cur + outer_row(h) + c;
+        const float* Br = cur + kOuterBuf + outer_row(h) + wave * 32 + c;
+        const int steps = (nr + 1) >> 1;
+        float av[4], bv;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) av[q] = Ar[q * 32];
+        bv = Br[0];
+        for (int t = 0; t < steps; ++t) {
+            float an[4], bn;
+            const int o = (t + 1 < steps ? t + 1 : t) * kOuterLd;  // next pair (rolled one step ahead)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) an[q] = Ar[o + q * 32];
+            bn = Br[o];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv, acc[q], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) av[q] = an[q];
+            bv = bn;
+        }
+        if (more) commit(sl + 1, bufs + ((sl + 1) & 1) * 2 * kOuterBuf);
         __syncthreads();
     }
-    float* P = a.P + (size_t)cidx * a.M * a.Nn;
-    const int col = n_base + nb * 32 + c;
-    if (col < a.Nn) {
+
+    // destination: the group's only chunk writes the result itself, others a partial slab
+    float* D = a.P + (size_t)cidx * a.M * a.Nn;
+    float* Db = a.Pb != nullptr ? a.Pb + (size_t)cidx * a.Nn : nullptr;
+    if (a.dst_mode == 1 || a.dst_mode == 2) {
+        const int di = ld_uniform(a.chunk_dst, cidx + a.chunk_off);
+        if (di >= 0) D = a.dst + (size_t)(a.dst_mode == 1 ? di : 0) * a.M * a.Nn;
+    } else if (a.dst_mode == 3) {
+        D = a.dst;
+        Db = a.dst_b;
+    }
+    const int col = n_base + wave * 32 + c;
+    if (D != nullptr && wave * 32 < ncols && col < a.Nn) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m_base + q * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < a.M) P[(size_t)m * a.Nn + col] = acc[q][r];
+                if (m < a.M) D[(size_t)m * a.Nn + col] = acc[q][r];
             }
         }
     }
-    if (a.Pb != nullptr && blockIdx.y == 0 && threadIdx.x < ncols)
-        a.Pb[(size_t)cidx * a.Nn + n_base + threadIdx.x] = bsum;
+    if (do_bsum && Db != nullptr && tid < ncols) Db[n_base + tid] = bsum;
 }
 
 // dst[group g] (elems floats) = Σ_{c in chunks of g, ascending} P[c]
@@ -1181,6 +1313,7 @@ struct ReduceArgs {
     const int* gdst;     // nullable: destination index of each group (else blockIdx.x)
     int g_base;          // group index offset into gptr / gdst
     float* dst;
+    int skip_single;     // groups of exactly one chunk were written directly: skip them
 };
 
 __global__ __launch_bounds__(kThreads) void reduce_slabs_kernel(ReduceArgs a) {
@@ -1192,8 +1325,20 @@ __global__ __launch_bounds__(kThreads) void reduce_slabs_kernel(ReduceArgs a) {
         c0 = a.gptr[a.g_base + g] - a.g_off;
         c1 = a.gptr[a.g_base + g + 1] - a.g_off;
     }
+    if (c1 - c0 == 1 && a.skip_single) return;  // written directly by outer_accum_kernel
+    // slabs are read 32 at a time (independent loads in flight: a chained loop paid one L2
+    // round trip per chunk), then added in chunk order
+    constexpr int kB = 32;
     float s = 0.0f;
-    for (int c = c0; c < c1; ++c) s += a.P[(size_t)c * a.elems + e];
+    const float* P = a.P + e;
+    for (int cb = c0; cb < c1; cb += kB) {
+        float v[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) v[u] = P[(size_t)min(cb + u, c1 - 1) * a.elems];
+#pragma unroll
+        for (int u = 0; u < kB; ++u)
+            if (cb + u < c1) s += v[u];
+    }
     const int d = a.gdst != nullptr ? a.gdst[a.g_base + g] : g;
     a.dst[(size_t)d * a.elems + e] = s;
 }
@@ -1539,8 +1684,9 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
 }
 
 // Ordered row sums out[i] = Σ list(i) + extra + bias, with the pieces of long rows first.
-static int32_t run_rowsum(RowSumArgs a, const int* pb, const int* pe, int k_lo, int k_hi, float* P,
-                          hipStream_t strm) {
+static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, const int* pe, int k_lo, int k_hi,
+                          float* P, hipStream_t strm) {
+    a.g.dummy = p->d.s_ptr;  // S + 1 >= 1 entries: always a valid target
     int V, T;
     pick_vt(a.g.F, &V, &T);
     if (k_hi > k_lo) {
@@ -1553,7 +1699,8 @@ static int32_t run_rowsum(RowSumArgs a, const int* pb, const int* pe, int k_lo, 
         pa.F = a.g.F;
         pa.idx = a.g.idx;
         pa.idx_off = a.g.idx_off;
-        pa.fidx = a.g.fidx;
+        pa.filter = a.g.filter;
+        pa.dummy = a.g.dummy;
         pa.flo = a.g.flo;
         pa.fhi = a.g.fhi;
         pa.P = P;
@@ -1587,7 +1734,7 @@ static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x
     a.cnt = p->d.s_cnt;
     a.out = H;
     a.out_off = s.sel_b;
-    return run_rowsum(a, p->d.seg_pb, p->d.seg_pe, ragged ? s.sp_lo : 0, ragged ? s.sp_hi : 0, Pseg, strm);
+    return run_rowsum(p, a, p->d.seg_pb, p->d.seg_pe, ragged ? s.sp_lo : 0, ragged ? s.sp_hi : 0, Pseg, strm);
 }
 
 }  // namespace mpgnn
@@ -1690,7 +1837,7 @@ int32_t mpgnn_rgcn_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         a.g.ent = ragged ? p->d.rw_ent : nullptr;
         a.g.idx = p->d.rw_seg;
         a.g.idx_off = s.sel_b;
-        a.g.fidx = s.all_segments ? nullptr : p->d.rw_seg;
+        a.g.filter = !s.all_segments;
         a.g.flo = s.sel_b;
         a.g.fhi = s.sel_e;
         if (ragged) k_hi = (int)p->rw_l.piece_b.size();
@@ -1702,7 +1849,7 @@ int32_t mpgnn_rgcn_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         a.g.idx_off = s.sel_b;
     }
     TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
-    return run_rowsum(a, p->d.rw_pb, p->d.rw_pe, k_lo, k_hi, reinterpret_cast<float*>(ws + w.prw), strm);
+    return run_rowsum(p, a, p->d.rw_pb, p->d.rw_pe, k_lo, k_hi, reinterpret_cast<float*>(ws + w.prw), strm);
 }
 
 int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
@@ -1749,7 +1896,7 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
             a.ptr = ragged ? p->d.t_ent_ptr : p->d.t_ptr;
             a.g.ent = ragged ? p->d.t_ent : nullptr;
             a.g.idx = p->d.t_seg;
-            a.g.fidx = s.all_segments ? nullptr : p->d.t_seg;
+            a.g.filter = !s.all_segments;
             a.g.flo = s.sel_b;
             a.g.fhi = s.sel_e;
             if (ragged) {
@@ -1776,13 +1923,18 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
             }
         }
         TimedLaunch tl(MPGNN_K_ROW_DX, strm);
-        st = run_rowsum(a, pb, pe, k_lo, k_hi, reinterpret_cast<float*>(ws + w.pdx), strm);
+        st = run_rowsum(p, a, pb, pe, k_lo, k_hi, reinterpret_cast<float*>(ws + w.pdx), strm);
         if (st != MPGNN_OK) return st;
     }
 
     const int mt = (F_in + kColTile - 1) / kColTile;
     const int nt = (F_out + kColTile - 1) / kColTile;
-    const size_t outer_lds = (size_t)(2 * kSlice * (kColTile + 4) + kSlice) * sizeof(float);
+    const size_t outer_lds = (size_t)(4 * kOuterBuf) * sizeof(float);
+    const bool outer_vec = (F_in & 3) == 0 && (F_out & 3) == 0;
+    auto launch_outer = [&](dim3 grid, const OuterArgs& o) {
+        if (outer_vec) hipLaunchKernelGGL(outer_accum_kernel<true>, grid, dim3(kThreads), outer_lds, strm, o);
+        else hipLaunchKernelGGL(outer_accum_kernel<false>, grid, dim3(kThreads), outer_lds, strm, o);
+    };
 
     // ---- grad_weight[r] = Σ_{seg of r} h_segᵀ dout[node_1(seg)] -------------------------
     if (grad_weight != nullptr) {
@@ -1802,7 +1954,9 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
             OuterArgs o{};
             o.chunk_begin = p->d.chunk_begin;
             o.chunk_end = p->d.chunk_end;
+            o.chunk_dst = p->d.chunk_dst;
             o.chunk_off = s.c_lo;
+            o.dst_mode = mode == MPGNN_MODE_ALL ? 1 : 2;
             o.A = H;
             o.M = F_in;
             o.a_off = s.sel_b;
@@ -1810,25 +1964,28 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
             o.Nn = F_out;
             o.b_idx = p->d.s_row;
             o.P = P;
+            o.dst = grad_weight;
             o.Pb = nullptr;
             {
                 TimedLaunch tl(MPGNN_K_OUTER, strm);
-                hipLaunchKernelGGL(outer_accum_kernel, dim3(nch, mt, nt), dim3(kThreads), outer_lds, strm, o);
+                launch_outer(dim3(nch, mt, nt), o);
             }
             if ((st = hip_check(hipGetLastError(), "outer_accum_kernel(dW) launch")) != MPGNN_OK) return st;
             ReduceArgs r{};
             r.P = P;
             r.elems = (int)wsize;
             r.dst = grad_weight;
+            r.skip_single = 1;
             const int ey = (int)((wsize + kThreads - 1) / kThreads);
-            TimedLaunch tl(MPGNN_K_REDUCE, strm);
             if (mode == MPGNN_MODE_ALL) {
+                TimedLaunch tl(MPGNN_K_REDUCE, strm);
                 r.gptr = p->d.rel_chunk_ptr;
                 r.g_off = s.c_lo;
                 r.gdst = p->d.rel_val32;
                 r.g_base = (int)s.d_lo;
                 hipLaunchKernelGGL(reduce_slabs_kernel, dim3((int)(s.d_hi - s.d_lo), ey), dim3(kThreads), 0, strm, r);
-            } else {
+            } else if (nch > 1) {  // one chunk: written directly
+                TimedLaunch tl(MPGNN_K_REDUCE, strm);
                 r.gptr = nullptr;
                 r.nchunks = nch;
                 r.gdst = nullptr;
@@ -1855,6 +2012,7 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         o.row_lo = rc.rows_lo;
         o.row_hi = rc.rows_hi;
         o.chunk_rows = rc.chunk;
+        o.dst_mode = rc.n == 1 ? 3 : 0;
         o.A = x;
         o.M = F_in;
         o.a_off = 0;
@@ -1862,12 +2020,15 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         o.Nn = F_out;
         o.b_idx = nullptr;
         o.P = P;
+        o.dst = grad_root;
         o.Pb = grad_bias ? Pb : nullptr;
+        o.dst_b = grad_bias;
         {
             TimedLaunch tl(MPGNN_K_OUTER, strm);
-            hipLaunchKernelGGL(outer_accum_kernel, dim3(rc.n, grad_root ? mt : 1, nt), dim3(kThreads), outer_lds, strm, o);
+            launch_outer(dim3(rc.n, grad_root ? mt : 1, nt), o);
         }
         if ((st = hip_check(hipGetLastError(), "outer_accum_kernel(root) launch")) != MPGNN_OK) return st;
+        if (rc.n == 1) return MPGNN_OK;  // written directly
         if (grad_root) {
             ReduceArgs r{};
             r.P = P;

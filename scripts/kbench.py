@@ -3,7 +3,7 @@
 
   python scripts/kbench.py [--config fb15k237] [--feat 128] [--iters 30]
 
-Reports per-kernel average durations (HIP events on the launch stream, via the C ABI timing
+Reports per kernel [µs per launch, µs per call, launches per call] (HIP events on the launch stream, via the C ABI timing
 hook) for: the default path, MPGNN_OPT_ABLATE=1 (no gather), =2 (no MFMA), exact order, and
 the backward kernels. Ablated runs produce wrong numbers by design (profiling only).
 """
@@ -32,8 +32,8 @@ def timed(fn, iters):
     out = {}
     for k in _lib.KERNEL_KINDS:
         ms, n = _lib.kernel_timing(k)
-        if n:
-            out[k] = round(ms / n * 1e3, 2)
+        if n:  # [µs per launch, µs per call, launches per call]
+            out[k] = [round(ms / n * 1e3, 2), round(ms / iters * 1e3, 2), round(n / iters, 2)]
     return out
 
 
