@@ -169,15 +169,16 @@ int32_t mpgnn_set_option(int32_t option, int64_t value);
  * hipEvents recorded on the launch stream; mpgnn_timing_query synchronises those events and
  * returns the summed duration and the launch count of one kernel kind. */
 enum mpgnn_kernel_kind {
-    MPGNN_K_SEG_FWD = 0,   /* seg_tile_kernel: gather-mean + MFMA with W_r (forward)      */
-    MPGNN_K_ROW_FWD = 1,   /* row_tile_kernel: Σ_r Y + x@root + bias (forward)            */
-    MPGNN_K_SEG_DGRAD = 2, /* seg_tile_kernel: (dout @ W_rᵀ) / cnt (backward)             */
-    MPGNN_K_ROW_DX = 3,    /* row_tile_kernel: transposed gather-sum + dout @ rootᵀ       */
-    MPGNN_K_OUTER = 4,     /* outer_accum_kernel: dW / droot / dbias partial slabs        */
+    MPGNN_K_SEG_FWD = 0,   /* tile_gemm_kernel: Y = H @ W_r, Y_root = x @ root (forward)   */
+    MPGNN_K_ROW_FWD = 1,   /* combine Σ_r Y + Y_root + bias (flat_rows / row_sum kernels)  */
+    MPGNN_K_SEG_DGRAD = 2, /* tile_gemm_kernel: (dout @ W_rᵀ) / cnt, dout @ rootᵀ          */
+    MPGNN_K_ROW_DX = 3,    /* grad_x transposed gather-sum + G_root (flat_rows / row_sum)  */
+    MPGNN_K_OUTER = 4,     /* outer_accum_kernel: dW / droot / dbias                      */
     MPGNN_K_REDUCE = 5,    /* reduce_slabs_kernel                                         */
-    MPGNN_K_MEAN = 6,      /* seg_tile_kernel: segment means only (mpgnn_rel_mean_fwd)    */
-    MPGNN_K_PIECE = 7,     /* piece_sum_kernel: ordered partial sums of long runs         */
-    MPGNN_K_COUNT = 8
+    MPGNN_K_MEAN = 6,      /* segment means H (flat_rows / row_sum kernels)               */
+    MPGNN_K_PIECE = 7,     /* ordered partial sums of long runs (exact-order lists)       */
+    MPGNN_K_FINAL = 8,     /* finalize_rows_kernel: split / empty rows, extra + bias      */
+    MPGNN_K_COUNT = 9
 };
 int32_t mpgnn_timing_enable(int32_t on);
 /* Debug: workgroups per CU the runtime admits at width F for the gather-tile kernel

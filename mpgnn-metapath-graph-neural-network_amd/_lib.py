@@ -71,7 +71,7 @@ SIGNATURES = [
 ]
 
 KERNEL_KINDS = {"seg_fwd": 0, "row_fwd": 1, "seg_dgrad": 2, "row_dx": 3, "outer": 4, "reduce": 5, "mean": 6,
-                "piece": 7}
+                "piece": 7, "final": 8}
 OPT_EXACT_ORDER = 0
 
 

@@ -108,6 +108,81 @@ static void build_ragged(const std::vector<int32_t>& run_ptr, RaggedHost& L) {
     L.run_piece_ptr[runs] = (int32_t)L.piece_b.size();
 }
 
+// Flat chunked list over runs r (positions [run_ptr[r], run_ptr[r+1]), output row r) with
+// forced cuts at run indices `cuts` (ascending, first 0, last = runs).
+static void build_flat(const std::vector<int32_t>& run_ptr, const std::vector<int32_t>& cuts, FlatHost& L) {
+    const int32_t runs = run_ptr.empty() ? 0 : (int32_t)run_ptr.size() - 1;
+    const int32_t P = runs > 0 ? run_ptr[runs] : 0;
+    L = FlatHost{};
+    L.row_of.resize(P);
+    for (int32_t r = 0; r < runs; ++r)
+        for (int32_t q = run_ptr[r]; q < run_ptr[r + 1]; ++q) L.row_of[q] = r;
+    L.chunk_ptr.push_back(0);
+    L.cut_chunk_ptr.push_back(0);
+    for (size_t ci = 0; ci + 1 < cuts.size(); ++ci) {
+        const int32_t pb = run_ptr[cuts[ci]], pe = run_ptr[cuts[ci + 1]];
+        int32_t cs = pb;  // current chunk start
+        int32_t q = pb;
+        while (q < pe) {
+            const int32_t r = L.row_of[q];
+            const int32_t rend = std::min(run_ptr[r + 1], pe);
+            if (rend - cs <= kFlatChunk) {  // the rest of run r fits the chunk
+                q = rend;
+                continue;
+            }
+            if (q > cs) {  // close the chunk before run r
+                L.chunk_ptr.push_back(q);
+                cs = q;
+                continue;
+            }
+            q = cs + kFlatChunk;  // run longer than a chunk: cut inside it
+            L.chunk_ptr.push_back(q);
+            cs = q;
+        }
+        if (q > cs) L.chunk_ptr.push_back(q);
+        L.cut_chunk_ptr.push_back((int32_t)L.chunk_ptr.size() - 1);
+    }
+    const int32_t nch = (int32_t)L.chunk_ptr.size() - 1;
+    L.chunk_info.resize(nch);
+    L.row_split.assign(runs, -1);
+    L.split_ptr.push_back(0);
+    L.cut_split_ptr.push_back(0);
+    int32_t slot = 0;
+    size_t ci = 0;
+    for (int32_t c = 0; c < nch; ++c) {
+        const int32_t a0 = L.chunk_ptr[c], a1 = L.chunk_ptr[c + 1];
+        const int32_t rf = L.row_of[a0], rl = L.row_of[a1 - 1];
+        const bool fs = run_ptr[rf] < a0, ls = run_ptr[rl + 1] > a1;
+        L.chunk_info[c] = (fs ? 1 : 0) | (ls ? 2 : 0) | (slot << 2);
+        // partial slots: the first run's (when split), then the last run's (when split and a
+        // different run); a chunk inside one long run has a single partial
+        auto add_partial = [&](int32_t row) {
+            if (L.row_split[row] < 0) {
+                L.row_split[row] = (int32_t)L.split_row.size();
+                L.split_row.push_back(row);
+                L.split_ptr.push_back(L.split_ptr.back());
+            }
+            L.split_slot.push_back(slot++);
+            ++L.split_ptr.back();
+        };
+        if (fs) add_partial(rf);
+        if (ls && (rl != rf || !fs)) add_partial(rl);
+        while (ci + 1 < L.cut_chunk_ptr.size() && L.cut_chunk_ptr[ci + 1] == c + 1) {
+            L.cut_split_ptr.push_back((int32_t)L.split_row.size());
+            ++ci;
+        }
+    }
+    while (L.cut_split_ptr.size() < L.cut_chunk_ptr.size()) L.cut_split_ptr.push_back((int32_t)L.split_row.size());
+    L.nslots = slot;
+}
+
+// Resolved entries: a position p becomes idx[p] (what the gather loads), a piece reference
+// stays negative — the gather then needs one index load per entry instead of two.
+static void resolve_ragged(RaggedHost& L, const std::vector<int32_t>& idx) {
+    L.res.resize(L.ent.size());
+    for (size_t q = 0; q < L.ent.size(); ++q) L.res[q] = L.ent[q] >= 0 ? idx[L.ent[q]] : L.ent[q];
+}
+
 static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N, int64_t lo,
                      int64_t hi, mpgnn_plan* p) {
     const int64_t* n1 = ei;
@@ -242,6 +317,17 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
     build_ragged(p->s_ptr, p->seg_l);
     build_ragged(p->t_ptr, p->t_l);
     build_ragged(p->rw_ptr, p->rw_l);
+    resolve_ragged(p->seg_l, p->e_col);
+    resolve_ragged(p->t_l, p->t_seg);
+    resolve_ragged(p->rw_l, p->rw_seg);
+    {
+        // segments over edges, cut at relation boundaries (mode SINGLE selects one relation)
+        std::vector<int32_t> seg_cuts(p->rel_seg_ptr.begin(), p->rel_seg_ptr.end());
+        build_flat(p->s_ptr, seg_cuts, p->seg_f);
+        const std::vector<int32_t> node_cuts{0, (int32_t)N};
+        build_flat(p->t_ptr, node_cuts, p->t_f);
+        build_flat(p->rw_ptr, node_cuts, p->rw_f);
+    }
     {
         // runs of equal (relation, node_2) in ta order
         std::vector<int32_t> run_ptr{0};
@@ -257,6 +343,7 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
             }
         }
         build_ragged(run_ptr, p->ta_l);
+        resolve_ragged(p->ta_l, p->ta_seg);
         const size_t runs = run_key.size();
         p->ta_key.resize(p->ta_l.ent.size());
         for (size_t r = 0; r < runs; ++r)
@@ -463,6 +550,20 @@ int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
         {&p->d.ta_pb, &p->ta_l.piece_b}, {&p->d.ta_pe, &p->ta_l.piece_e},
         {&p->d.rw_ent, &p->rw_l.ent}, {&p->d.rw_ent_ptr, &p->rw_l.ent_ptr},
         {&p->d.rw_pb, &p->rw_l.piece_b}, {&p->d.rw_pe, &p->rw_l.piece_e},
+        {&p->d.seg_res, &p->seg_l.res}, {&p->d.t_res, &p->t_l.res},
+        {&p->d.ta_res, &p->ta_l.res}, {&p->d.rw_res, &p->rw_l.res},
+        {&p->d.seg_f.chunk_ptr, &p->seg_f.chunk_ptr}, {&p->d.seg_f.chunk_info, &p->seg_f.chunk_info},
+        {&p->d.seg_f.row_of, &p->seg_f.row_of}, {&p->d.seg_f.split_row, &p->seg_f.split_row},
+        {&p->d.seg_f.split_ptr, &p->seg_f.split_ptr}, {&p->d.seg_f.split_slot, &p->seg_f.split_slot},
+        {&p->d.seg_f.row_split, &p->seg_f.row_split},
+        {&p->d.t_f.chunk_ptr, &p->t_f.chunk_ptr}, {&p->d.t_f.chunk_info, &p->t_f.chunk_info},
+        {&p->d.t_f.row_of, &p->t_f.row_of}, {&p->d.t_f.split_row, &p->t_f.split_row},
+        {&p->d.t_f.split_ptr, &p->t_f.split_ptr}, {&p->d.t_f.split_slot, &p->t_f.split_slot},
+        {&p->d.t_f.row_split, &p->t_f.row_split},
+        {&p->d.rw_f.chunk_ptr, &p->rw_f.chunk_ptr}, {&p->d.rw_f.chunk_info, &p->rw_f.chunk_info},
+        {&p->d.rw_f.row_of, &p->rw_f.row_of}, {&p->d.rw_f.split_row, &p->rw_f.split_row},
+        {&p->d.rw_f.split_ptr, &p->rw_f.split_ptr}, {&p->d.rw_f.split_slot, &p->rw_f.split_slot},
+        {&p->d.rw_f.row_split, &p->rw_f.row_split},
     };
     size_t total = 0;
     std::vector<size_t> offs;

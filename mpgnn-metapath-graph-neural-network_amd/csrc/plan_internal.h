@@ -26,7 +26,33 @@ constexpr int kPieceEntries = 32;
 // covers positions [piece_b[k], piece_e[k]).  ent_ptr[r] is the first entry of run r.
 struct RaggedHost {
     std::vector<int32_t> ent, ent_ptr, piece_b, piece_e;
+    std::vector<int32_t> res;            // [entries] idx[position] | -(piece+1)
     std::vector<int32_t> run_piece_ptr;  // [runs+1] first piece of each run
+};
+
+// Flat chunked list (flat_rows_kernel): the positions of a list whose consecutive runs are
+// output rows, cut into chunks of at most kFlatChunk positions — at run ends, except inside a
+// run longer than a chunk (and at forced cuts: relation boundaries of the segment list).  A
+// chunk's first / last run may be split with its neighbours; their partial sums go to carry
+// slots that the finalize kernel adds in chunk order.
+constexpr int kFlatChunk = 32;
+
+struct FlatHost {
+    std::vector<int32_t> chunk_ptr;   // [nch+1] positions
+    std::vector<int32_t> chunk_info;  // [nch] bit0: first run split, bit1: last run split, >>2: first slot
+    std::vector<int32_t> row_of;      // [positions] output row of each position
+    std::vector<int32_t> split_row;   // [nsplit] rows split across chunks
+    std::vector<int32_t> split_ptr;   // [nsplit+1] into split_slot
+    std::vector<int32_t> split_slot;  // partial slots of each split row, in chunk order
+    std::vector<int32_t> row_split;   // [nrows] split index of each row, -1 if not split
+    std::vector<int32_t> cut_chunk_ptr;  // [ncuts+1] chunk range of each forced-cut section
+    std::vector<int32_t> cut_split_ptr;  // [ncuts+1] split-row range of each section
+    int32_t nslots = 0;
+};
+
+struct FlatDev {
+    int32_t *chunk_ptr = nullptr, *chunk_info = nullptr, *row_of = nullptr;
+    int32_t *split_row = nullptr, *split_ptr = nullptr, *split_slot = nullptr, *row_split = nullptr;
 };
 
 struct DeviceTables {
@@ -54,6 +80,8 @@ struct DeviceTables {
     int32_t *t_ent = nullptr, *t_ent_ptr = nullptr, *t_pb = nullptr, *t_pe = nullptr;
     int32_t *ta_ent = nullptr, *ta_key = nullptr, *ta_pb = nullptr, *ta_pe = nullptr;
     int32_t *rw_ent = nullptr, *rw_ent_ptr = nullptr, *rw_pb = nullptr, *rw_pe = nullptr;
+    int32_t *seg_res = nullptr, *t_res = nullptr, *ta_res = nullptr, *rw_res = nullptr;  // resolved entries
+    FlatDev seg_f, t_f, rw_f;       // flat chunked lists (segment means, grad_x, combine)
     void* block = nullptr;          // single hipMalloc holding every table above
     size_t block_bytes = 0;
 };
@@ -92,6 +120,8 @@ struct mpgnn_plan {
     // all relations), (relation, node_2) runs over ta order (grad_x, one relation), node_1
     // over row-major segments (forward combine)
     mpgnn::RaggedHost seg_l, t_l, ta_l, rw_l;
+    mpgnn::FlatHost seg_f, t_f, rw_f;     // flat chunked lists: segments over edges (cut at
+                                          // relations), node_2 over col-major edges, node_1 over segments
     std::vector<int32_t> ta_key;               // [ta entries] node_2 of each ta entry
     std::vector<int32_t> rel_ta_ent_ptr;       // [nrel+1] ta entry range of each relation
     std::vector<int32_t> rel_seg_piece_ptr;    // [nrel+1] seg pieces of each relation

@@ -37,7 +37,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kThreads = 256;  // 4 waves of 64
 constexpr int kWaves = 4;
 constexpr int kRowsPerWave = kTileRows / kWaves;  // 16 (seg_tile_kernel)
-constexpr int kSumRowsPerWave = 4;               // row_sum_kernel: 16 rows per workgroup
+constexpr int kSumRowsPerWave = 8;               // row_sum_kernel: 32 rows per workgroup
 constexpr int kColTile = 128;                    // output columns per workgroup (4 × 32-col strips)
 constexpr int kSlice = 32;                       // rows per K-slice in outer_accum_kernel
 constexpr int kMaxF = 256;
@@ -1014,6 +1014,8 @@ struct RowSumArgs {
     const int* cnt;     // nullable: divide row i by cnt[i] (segment means)
     int out_off;        // out row = i - out_off
     float* out;         // [*, F]
+    unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS, means launch): [wave][8] timeline
+    const int* res;     // resolved entries of the ragged list g.ent (gather_rows_kernel)
 };
 
 __device__ __forceinline__ int lower_bound_i32(const int* keys, int lo, int hi, int v) {
@@ -1024,12 +1026,27 @@ __device__ __forceinline__ int lower_bound_i32(const int* keys, int lo, int hi, 
     return lo;
 }
 
-template <int V, int T>
+// Calls f(std::integral_constant<int, r>) for a wave-uniform runtime r in [0, N).
+template <int N, class F>
+__device__ __forceinline__ void dispatch_row(int r, F&& f) {
+    if constexpr (N > 1) {
+        if (r == N - 1) f(std::integral_constant<int, N - 1>{});
+        else dispatch_row<N - 1>(r, f);
+    } else {
+        f(std::integral_constant<int, 0>{});
+    }
+}
+
+// EXTRA: the launch adds extra rows and/or bias (combine, grad_x); the means launch does not
+// and keeps those registers free (occupancy).
+template <int V, int T, bool EXTRA>
 __global__ __launch_bounds__(kThreads) void row_sum_kernel(RowSumArgs a) {
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int row0 = a.r_begin + (blockIdx.x * kWaves + wave) * kSumRowsPerWave;
     if (row0 >= a.N) return;
+    unsigned long long t_start = 0;
+    if (a.stamps != nullptr) t_start = stamp_now();
     const int wn = min(kSumRowsPerWave, a.N - row0);
     int bnd = 0;
     if (lane <= kSumRowsPerWave) {
@@ -1043,14 +1060,15 @@ __global__ __launch_bounds__(kThreads) void row_sum_kernel(RowSumArgs a) {
     const bool has_cnt = a.cnt != nullptr;
     const int cnt_raw = (has_cnt ? a.cnt : a.g.dummy)[has_cnt ? min(row0 + min(lane, kSumRowsPerWave - 1), a.N - 1) : 0];
     const int cnt_l = has_cnt ? cnt_raw : 1;
-    float ex[kSumRowsPerWave][T][V], bb[T][V];
+    constexpr int NX = EXTRA ? kSumRowsPerWave : 1;
+    float ex[NX][T][V], bb[T][V];
     int colc[T];
 #pragma unroll
     for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, F - V);
-    const bool has_ex = a.extra != nullptr && a.hi > a.lo;
-    const bool has_b = a.bias != nullptr;
+    const bool has_ex = EXTRA && a.extra != nullptr && a.hi > a.lo;
+    const bool has_b = EXTRA && a.bias != nullptr;
 #pragma unroll
-    for (int r = 0; r < kSumRowsPerWave; ++r) {
+    for (int r = 0; r < NX; ++r) {
         const int i = min(max(row0 + r, a.lo), a.hi - 1);  // clamped into the own range
         const float* eb = has_ex ? a.extra + (size_t)(i - a.lo) * F : a.g.src;
 #pragma unroll
@@ -1082,7 +1100,8 @@ __global__ __launch_bounds__(kThreads) void row_sum_kernel(RowSumArgs a) {
 #pragma unroll
                     for (int q = 0; q < V; ++q) {
                         v[q] = has_cnt ? acc[t][q] / div : acc[t][q];
-                        if (own) v[q] = (v[q] + ex[r][t][q]) + bb[t][q];  // zeros when absent
+                        if constexpr (EXTRA)
+                            if (own) v[q] = (v[q] + ex[r][t][q]) + bb[t][q];  // zeros when absent
                     }
                     vstore<V>(a.out + (size_t)(i - a.out_off) * F + col, v);
                 }
@@ -1090,16 +1109,432 @@ __global__ __launch_bounds__(kThreads) void row_sum_kernel(RowSumArgs a) {
         }
         zero_acc<V, T>(acc);
     };
-    static_assert(kSumRowsPerWave == 4, "flush dispatch below");
+    unsigned long long t_pro = 0;
+    if (a.stamps != nullptr) {
+        __builtin_amdgcn_s_waitcnt(0);  // debug timeline only: prologue loads landed
+        t_pro = stamp_now();
+    }
     wave_gather<V, T, (V * T <= 2 ? 8 : 4), kSumRowsPerWave>(
         a.g, bnd, wn, lane, [&](int r, bool live, float (&acc)[T][V]) {
-            if (r == 0) flush_row(std::integral_constant<int, 0>{}, live, acc);
-            else if (r == 1) flush_row(std::integral_constant<int, 1>{}, live, acc);
-            else if (r == 2) flush_row(std::integral_constant<int, 2>{}, live, acc);
-            else flush_row(std::integral_constant<int, 3>{}, live, acc);
+            dispatch_row<kSumRowsPerWave>(r, [&](auto RI) { flush_row(RI, live, acc); });
         });
+    if (a.stamps != nullptr && lane == 0) {
+        const unsigned long long t_end = stamp_now();
+        unsigned long long* o = a.stamps + ((size_t)blockIdx.x * kWaves + wave) * 8;
+        o[0] = t_start;
+        o[1] = t_pro;
+        o[2] = t_end;
+        o[3] = (unsigned long long)(readlane(bnd, wn) - readlane(bnd, 0));  // entries
+        o[4] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));     // HW_REG_HW_ID
+        o[5] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));    // HW_REG_XCC_ID
+        o[6] = (unsigned long long)wn;
+        o[7] = 1;
+    }
 }
 
+
+// ----------------------------------------------------------------------------------------
+// flat_rows_kernel — the fast-path row sums (segment means, grad_x, forward combine).
+//
+// One wave per plan chunk: at most kFlatChunk consecutive positions of the list, cut at row
+// ends except inside rows longer than a chunk (FlatHost, plan_internal.h).  Every wave does the
+// same bounded work whatever the degree skew, and does it like a plain gather: one coalesced
+// load of the chunk's values and row ids, then its source rows in flight 16 at a time, summed
+// in position order.  A row that starts and ends in the chunk is written (divided by its entry
+// count for means); the chunk's first / last row, when split with a neighbouring chunk, goes to
+// a carry slot and finalize_rows_kernel adds the slots in chunk order.  Rows held in one chunk
+// are therefore summed exactly in the reference order; split rows (longer than a chunk, or
+// crossing one) are summed as ordered partials (tolerance 1e-4, like the ragged pieces).
+// ----------------------------------------------------------------------------------------
+struct FlatArgs {
+    const int* chunk_ptr;
+    const int* chunk_info;  // bit0 first row split, bit1 last row split, >>2 first carry slot
+    int c_lo, c_hi;         // chunks of this launch
+    const int* table;       // value per position: source row + idx_off
+    const int* row_of;      // output row per position
+    const float* src;       // [*, F]
+    int F;
+    int idx_off;
+    int filter, flo, fhi;   // keep a value only when flo <= value < fhi
+    const int* cnt;         // nullable: divide complete rows by cnt[row] (global counts in shards)
+    int row_off;            // out row = row - row_off
+    float* out;
+    float* carry;           // [slots][F]
+    const int* dummy;       // any valid int table
+};
+
+template <int V, int T>
+__global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
+    constexpr int U = 16;
+    const int lane = threadIdx.x & 63;
+    const int c = a.c_lo + (int)blockIdx.x * kWaves + (int)(threadIdx.x >> 6);
+    if (c >= a.c_hi) return;
+    const int p0 = ld_uniform(a.chunk_ptr, c);
+    const int n = ld_uniform(a.chunk_ptr, c + 1) - p0;  // 1 .. kFlatChunk
+    const int info = ld_uniform(a.chunk_info, c);
+    const int F = a.F;
+    const int pq = p0 + min(lane, n - 1);
+    const int val = a.table[pq];
+    const int row = a.row_of[pq];
+    bool keep = lane < n;
+    if (a.filter) keep = keep && val >= a.flo && val < a.fhi;
+    const int srow = keep ? val - a.idx_off : 0;
+    const bool has_cnt = a.cnt != nullptr;
+    const int cnt_l = (has_cnt ? a.cnt : a.dummy)[has_cnt ? row : 0];
+    const int next = __shfl_down(row, 1);
+    const unsigned long long lastm = __ballot(lane < n && (lane == n - 1 || next != row));
+    const unsigned long long keepm = __ballot(keep);
+    const int rf = readlane(row, 0);
+    const int rl = readlane(row, n - 1);
+    const bool fs = info & 1, ls = info & 2;
+    const int slot0 = info >> 2;
+    int colc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, F - V);
+
+    float acc[T][V];
+    zero_acc<V, T>(acc);
+    for (int u0 = 0; u0 < n; u0 += U) {
+        float v[U][T][V];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = readlane(srow, min(u0 + u, n - 1));
+            const float* base = a.src + (size_t)r * F;
+#pragma unroll
+            for (int t = 0; t < T; ++t) vload<V>(base + colc[t], v[u][t]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = u0 + u;
+            if (q < n) {
+                if ((keepm >> q) & 1ull) {
+#pragma unroll
+                    for (int t = 0; t < T; ++t)
+#pragma unroll
+                        for (int k = 0; k < V; ++k) acc[t][k] += v[u][t][k];
+                }
+                if ((lastm >> q) & 1ull) {
+                    const int rr = readlane(row, q);
+                    const bool split = (rr == rf && fs) || (rr == rl && ls);
+                    float* dst;
+                    bool div = false;
+                    if (!split) {
+                        dst = a.out + (size_t)(rr - a.row_off) * F;
+                        div = has_cnt;
+                    } else {
+                        const int slot = slot0 + ((fs && rr == rl && rl != rf) ? 1 : 0);
+                        dst = a.carry + (size_t)slot * F;
+                    }
+                    const float d = (float)readlane(cnt_l, q);
+#pragma unroll
+                    for (int t = 0; t < T; ++t) {
+                        const int col = (t * 64 + lane) * V;
+                        if (col < F) {
+                            float o[V];
+#pragma unroll
+                            for (int k = 0; k < V; ++k) o[k] = div ? acc[t][k] / d : acc[t][k];
+                            vstore<V>(dst + col, o);
+                        }
+                    }
+                    zero_acc<V, T>(acc);
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// finalize_rows_kernel — one wave per row.
+//   mode 0 (segment means): split rows k in [k0, k1): out[row] = (Σ carry slots in order) / cnt
+//   mode 1 (combine, grad_x): every row in [r_lo, r_hi):
+//       v = split ? Σ slots : (no entries ? 0 : out[row]);  own rows: v = (v + extra) + bias
+struct FinalArgs {
+    int mode;
+    const int* split_row;
+    const int* split_ptr;
+    const int* split_slot;
+    int k0, k1;
+    const int* row_split;  // mode 1
+    const int* row_ptr;    // mode 1: no entries when row_ptr[r] == row_ptr[r + 1]
+    int r_lo, r_hi;
+    const float* carry;
+    int F;
+    const int* cnt;        // nullable (mode 0)
+    const float* extra;    // nullable [hi - lo, F]
+    const float* bias;     // nullable [F]
+    int lo, hi;
+    int row_off;
+    float* out;
+    const float* dummy;    // any valid float row
+};
+
+template <int V, int T>
+__global__ __launch_bounds__(kThreads) void finalize_rows_kernel(FinalArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int w = (int)blockIdx.x * kWaves + (int)(threadIdx.x >> 6);
+    const int F = a.F;
+    int row, k;
+    if (a.mode == 0) {
+        k = a.k0 + w;
+        if (k >= a.k1) return;
+        row = ld_uniform(a.split_row, k);
+    } else {
+        row = a.r_lo + w;
+        if (row >= a.r_hi) return;
+        k = ld_uniform(a.row_split, row);
+    }
+    int colc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, F - V);
+    const bool own = row >= a.lo && row < a.hi;
+    const bool has_ex = a.extra != nullptr && own;
+    const bool has_b = a.bias != nullptr && own;
+    // operands first (independent loads in flight together)
+    float ex[T][V], bb[T][V];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        vload<V>(has_ex ? a.extra + (size_t)(row - a.lo) * F + colc[t] : a.dummy, ex[t]);
+        vload<V>(has_b ? a.bias + colc[t] : a.dummy, bb[t]);
+    }
+    float acc[T][V];
+    zero_acc<V, T>(acc);
+    if (k >= 0) {
+        const int s0 = ld_uniform(a.split_ptr, k), s1 = ld_uniform(a.split_ptr, k + 1);
+        for (int sb = s0; sb < s1; sb += 8) {
+            float v[8][T][V];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int sl = ld_uniform(a.split_slot, min(sb + u, s1 - 1));
+#pragma unroll
+                for (int t = 0; t < T; ++t) vload<V>(a.carry + (size_t)sl * F + colc[t], v[u][t]);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (sb + u < s1)
+#pragma unroll
+                    for (int t = 0; t < T; ++t)
+#pragma unroll
+                        for (int q = 0; q < V; ++q) acc[t][q] += v[u][t][q];
+        }
+        if (a.cnt != nullptr) {
+            const float d = (float)ld_uniform(a.cnt, row);
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+#pragma unroll
+                for (int q = 0; q < V; ++q) acc[t][q] = acc[t][q] / d;
+        }
+    } else if (a.mode == 1 && ld_uniform(a.row_ptr, row) != ld_uniform(a.row_ptr, row + 1)) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) vload<V>(a.out + (size_t)(row - a.row_off) * F + colc[t], acc[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int col = (t * 64 + lane) * V;
+        if (col < F) {
+            float o[V];
+#pragma unroll
+            for (int q = 0; q < V; ++q) {
+                o[q] = acc[t][q];
+                if (has_ex) o[q] = o[q] + ex[t][q];
+                if (has_b) o[q] = o[q] + bb[t][q];
+            }
+            vstore<V>(a.out + (size_t)(row - a.row_off) * F + col, o);
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// gather_rows_kernel — the row-sum / segment-mean gather for F % 4 == 0 (any summation
+// order: it reproduces row_sum_kernel bit for bit).
+//
+// A wave owns RPW = 4·G consecutive rows, split between G = 64 / S sub-waves of S lanes; each
+// lane carries 4 consecutive columns (16-byte loads), so one load instruction moves G rows of
+// F ≤ 4·S floats.  Sub-wave g sums its rows g, g + G, g + 2G, g + 3G one after the other, each
+// in entry order from 0.0f — the same sequential sums as the reference's scatter_add_.
+// Entry values (a source row, or -(piece+1) for the partial sum of a piece of a long run) are
+// fetched S per lane-slice in one load and handed to the sub-wave by ds_bpermute; each lane
+// forms its own address (no scalar readlane chain per row), and U rows per lane are in flight
+// before any is added.  Row operands (counts, extra rows, bias) are loaded in the prologue, so
+// the flush of a finished row is stores only.
+// ----------------------------------------------------------------------------------------
+struct GatherRowsArgs {
+    int N;              // one past the last row
+    int r_begin;        // first row
+    int row_kind;       // 0: entries [ptr[i], ptr[i+1]); 1: [lower_bound(keys, i), lower_bound(keys, i+1));
+                        // 2: [ptr[i], pe[i]) (pieces)
+    const int* ptr;
+    const int* pe;
+    const int* keys;
+    int kb, ke;
+    const int* table;   // entry values
+    const float* src;   // [*, F]
+    int F;
+    int idx_off;        // source row = value - idx_off
+    int filter, flo, fhi;  // keep a value v >= 0 only when flo <= v < fhi
+    const float* P;     // piece partial sums, row = -(v+1) - piece_off
+    int piece_off;
+    const float* extra; // nullable [hi - lo, F] added to own rows
+    const float* bias;  // nullable [F] added to own rows
+    int lo, hi;
+    const int* cnt;     // nullable: divide row i by cnt[i]
+    int out_off;
+    float* out;
+    const int* dummy;   // any valid int table
+};
+
+__device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+template <int S, bool EXTRA>
+__global__ __launch_bounds__(kThreads) void gather_rows_kernel(GatherRowsArgs a) {
+    constexpr int G = 64 / S;    // rows per load instruction
+    constexpr int KR = 4;        // rows per sub-wave
+    constexpr int RPW = KR * G;  // rows per wave
+    constexpr int U = 16;        // row loads in flight per lane
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int sub = lane / S;
+    const int sl = lane % S;
+    const int row0 = a.r_begin + (blockIdx.x * kWaves + wave) * RPW;
+    if (row0 >= a.N) return;
+    const int F = a.F;
+    const int col = min(4 * sl, F - 4);
+    const bool col_live = 4 * sl < F;
+
+    // ---- prologue: row bounds (lane j < RPW: row row0 + j), counts, extra rows, bias -----
+    int my_beg = 0, my_end = 0;
+    {
+        const int i = min(row0 + min(lane, RPW - 1), a.N - 1);
+        int b, e;
+        if (a.row_kind == 1) {
+            b = lower_bound_i32(a.keys, a.kb, a.ke, i);
+            e = lower_bound_i32(a.keys, b, a.ke, i + 1);
+        } else {
+            b = a.ptr[i];
+            e = (a.row_kind == 2 ? a.pe : a.ptr + 1)[i];
+        }
+        const bool valid = lane < RPW && row0 + lane < a.N;
+        my_beg = valid ? b : 0;
+        my_end = valid ? e : 0;
+    }
+    // (every array below is indexed only by unrolled compile-time indices: a runtime index
+    // turns it into LDS / scratch traffic)
+    int beg[KR], off[KR + 1];
+    off[0] = 0;
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+        const int j = sub + G * k;
+        beg[k] = __shfl(my_beg, j);
+        off[k + 1] = off[k] + (__shfl(my_end, j) - beg[k]);
+    }
+    const int total = off[KR];
+    int steps = total;  // wave maximum over the sub-waves
+#pragma unroll
+    for (int m = S; m < 64; m <<= 1) steps = max(steps, __shfl_xor(steps, m));
+    steps = __builtin_amdgcn_readfirstlane(steps);
+    const int row_s = row0 + sub;  // row of ordinal k: row_s + G·k
+
+    const bool has_cnt = a.cnt != nullptr;
+    float cntf[KR];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+        const int c = (has_cnt ? a.cnt : a.dummy)[has_cnt ? min(row_s + G * k, a.N - 1) : 0];
+        cntf[k] = has_cnt ? (float)c : 1.0f;
+    }
+    float4 ex[KR], bb = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < KR; ++k) ex[k] = bb;
+    if constexpr (EXTRA) {
+        const bool has_ex = a.extra != nullptr && a.hi > a.lo;
+        const bool has_b = a.bias != nullptr;
+        const unsigned me = has_ex ? ~0u : 0u, mb = has_b ? ~0u : 0u;
+        auto msk = [](float4 v, unsigned m) {
+            return make_float4(__uint_as_float(__float_as_uint(v.x) & m), __uint_as_float(__float_as_uint(v.y) & m),
+                               __uint_as_float(__float_as_uint(v.z) & m), __uint_as_float(__float_as_uint(v.w) & m));
+        };
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+            const int i = min(max(row_s + G * k, a.lo), a.hi - 1);
+            const float* eb = has_ex ? a.extra + (size_t)(i - a.lo) * F + col : a.src;
+            ex[k] = msk(*reinterpret_cast<const float4*>(eb), me);
+        }
+        bb = msk(*reinterpret_cast<const float4*>(has_b ? a.bias + col : a.src), mb);
+    }
+
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int kcur = 0;  // row (of this sub-wave) being summed
+    auto flush_to = [&](int kstop) {  // rows kcur .. kstop-1 are complete
+        while (kcur < kstop) {
+            const int i = row_s + G * kcur;
+            if (i < a.N && col_live) {
+                const float c = cntf[0];  // slot 0 always holds row kcur's operands
+                float4 v = acc;
+                if (has_cnt) v = make_float4(v.x / c, v.y / c, v.z / c, v.w / c);
+                if constexpr (EXTRA) {
+                    if (i >= a.lo && i < a.hi) v = f4_add(f4_add(v, ex[0]), bb);
+                }
+                *reinterpret_cast<float4*>(a.out + (size_t)(i - a.out_off) * F + col) = v;
+            }
+            // rows finish in order: shift the per-row operands down one slot (constant indices;
+            // selecting slot kcur was folded into an indexed LDS load)
+#pragma unroll
+            for (int k = 0; k + 1 < KR; ++k) {
+                cntf[k] = cntf[k + 1];
+                if constexpr (EXTRA) ex[k] = ex[k + 1];
+            }
+            acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            ++kcur;
+        }
+    };
+
+    for (int vb = 0; vb < steps; vb += S) {
+        // entry value of this lane's slot v = vb + sl of its sub-wave (one load per lane)
+        const int v = vb + sl;
+        int k = 0, q = beg[0] + v;
+#pragma unroll
+        for (int kk = 1; kk < KR; ++kk) {
+            const bool ge = v >= off[kk];
+            k = ge ? kk : k;
+            q = ge ? beg[kk] + (v - off[kk]) : q;
+        }
+        const bool in = v < total;
+        const bool has_table = a.table != nullptr;  // no table: the entry position is the value
+        const int val_raw = (in && has_table ? a.table : a.dummy)[in && has_table ? q : 0];
+        const int my_val = in ? (has_table ? val_raw : q) : 0;
+        const int my_k = in ? k : KR;
+        const int nst = min(S, steps - vb);  // wave-uniform
+        for (int u0 = 0; u0 < nst; u0 += U) {
+            float4 buf[U];
+            int bk[U];
+            bool keep[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int srcl = sub * S + min(u0 + u, S - 1);
+                const int val = __shfl(my_val, srcl);
+                const int kr = (u0 + u < nst) ? __shfl(my_k, srcl) : KR;
+                const bool piece = val < 0;
+                bool kp = kr < KR;
+                if (a.filter) kp = kp && (piece || (val >= a.flo && val < a.fhi));
+                int row = piece ? -val - 1 - a.piece_off : val - a.idx_off;
+                row = kp ? row : 0;
+                const float* base = piece ? a.P : a.src;
+                buf[u] = *reinterpret_cast<const float4*>(base + (size_t)row * F + col);
+                bk[u] = kr;
+                keep[u] = kp;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (bk[u] < KR && bk[u] != kcur) flush_to(bk[u]);
+                if (keep[u]) acc = f4_add(acc, buf[u]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    flush_to(KR);
+}
 
 // ----------------------------------------------------------------------------------------
 // outer_accum_kernel:  D[c] = Σ_{p in chunk c} A[a_row(p)]ᵀ ⊗ B[b_row(p)]   (M × Nn, one
@@ -1472,8 +1907,11 @@ template <int V, int T>
 static void launch_rowsum(const RowSumArgs& a, hipStream_t st) {
     const int rows_per_block = kWaves * kSumRowsPerWave;
     const int rows = a.N - a.r_begin;
-    hipLaunchKernelGGL((row_sum_kernel<V, T>), dim3((rows + rows_per_block - 1) / rows_per_block), dim3(kThreads),
-                       0, st, a);
+    const dim3 grid((rows + rows_per_block - 1) / rows_per_block);
+    if (a.extra != nullptr || a.bias != nullptr)
+        hipLaunchKernelGGL((row_sum_kernel<V, T, true>), grid, dim3(kThreads), 0, st, a);
+    else
+        hipLaunchKernelGGL((row_sum_kernel<V, T, false>), grid, dim3(kThreads), 0, st, a);
 }
 
 template <int V, int T>
@@ -1551,15 +1989,19 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
     w.y = off; off += align256(S_sel * F_out * sizeof(float));
     w.yroot = off; off += align256(rows * F_out * sizeof(float));
     w.hf = off; off += align256(S_sel * F_in * sizeof(float));
-    w.pseg = off; off += align256((size_t)(s.sp_hi - s.sp_lo) * fmax * sizeof(float));
-    w.prw = off; off += align256((mode == MPGNN_MODE_ALL ? p->rw_l.piece_b.size() : 0) * F_out * sizeof(float));
+    // piece partials (exact-order / mode SINGLE lists) or flat-list carry slots
+    const size_t seg_slots = std::max((size_t)(s.sp_hi - s.sp_lo), (size_t)p->seg_f.nslots);
+    w.pseg = off; off += align256(seg_slots * fmax * sizeof(float));
+    w.prw = off; off += align256((mode == MPGNN_MODE_ALL ? std::max(p->rw_l.piece_b.size(), (size_t)p->rw_f.nslots) : 0) *
+                                 F_out * sizeof(float));
     const size_t fwd = off;
     off = 0;
-    const size_t dx_pieces = (mode == MPGNN_MODE_ALL) ? p->t_l.piece_b.size() : (size_t)(s.tap_hi - s.tap_lo);
+    const size_t dx_pieces = (mode == MPGNN_MODE_ALL) ? std::max(p->t_l.piece_b.size(), (size_t)p->t_f.nslots)
+                                                      : (size_t)(s.tap_hi - s.tap_lo);
     w.g = off; off += align256(S_sel * F_in * sizeof(float));
     w.groot = off; off += align256(rows * F_in * sizeof(float));
     w.h = off; off += align256(S_sel * F_in * sizeof(float));
-    w.pdx = off; off += align256(std::max(dx_pieces, (size_t)(s.sp_hi - s.sp_lo)) * F_in * sizeof(float));
+    w.pdx = off; off += align256(std::max(dx_pieces, seg_slots) * F_in * sizeof(float));
     w.p = off; off += align256((size_t)(s.c_hi - s.c_lo) * F_in * F_out * sizeof(float));
     w.proot = off; off += align256((size_t)rc.n * F_in * F_out * sizeof(float));
     w.pb = off; off += align256((size_t)rc.n * F_out * sizeof(float));
@@ -1683,37 +2125,195 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
     return hip_check(hipGetLastError(), "seg_tile_kernel launch");
 }
 
+template <int S>
+static void launch_gather_rows_s(const GatherRowsArgs& a, hipStream_t st) {
+    constexpr int rows_per_block = kWaves * 4 * (64 / S);
+    const int rows = a.N - a.r_begin;
+    const dim3 grid((rows + rows_per_block - 1) / rows_per_block);
+    if (a.extra != nullptr || a.bias != nullptr)
+        hipLaunchKernelGGL((gather_rows_kernel<S, true>), grid, dim3(kThreads), 0, st, a);
+    else
+        hipLaunchKernelGGL((gather_rows_kernel<S, false>), grid, dim3(kThreads), 0, st, a);
+}
+
+static void launch_gather_rows(const GatherRowsArgs& a, hipStream_t st) {
+    if (a.F <= 32) launch_gather_rows_s<8>(a, st);
+    else if (a.F <= 64) launch_gather_rows_s<16>(a, st);
+    else if (a.F <= 128) launch_gather_rows_s<32>(a, st);
+    else launch_gather_rows_s<64>(a, st);
+}
+
 // Ordered row sums out[i] = Σ list(i) + extra + bias, with the pieces of long rows first.
+// F % 4 == 0 runs gather_rows_kernel (16-byte lanes, several rows per load instruction);
+// other widths the scalar row_sum_kernel.  Both sum every row in entry order.
 static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, const int* pe, int k_lo, int k_hi,
                           float* P, hipStream_t strm) {
     a.g.dummy = p->d.s_ptr;  // S + 1 >= 1 entries: always a valid target
+    const bool vec = (a.g.F & 3) == 0 && a.g.F <= kMaxF && a.stamps == nullptr;
     int V, T;
     pick_vt(a.g.F, &V, &T);
     if (k_hi > k_lo) {
-        PieceArgs pa{};
-        pa.pb = pb;
-        pa.pe = pe;
-        pa.k_lo = k_lo;
-        pa.k_hi = k_hi;
-        pa.src = a.g.src;
-        pa.F = a.g.F;
-        pa.idx = a.g.idx;
-        pa.idx_off = a.g.idx_off;
-        pa.filter = a.g.filter;
-        pa.dummy = a.g.dummy;
-        pa.flo = a.g.flo;
-        pa.fhi = a.g.fhi;
-        pa.P = P;
-        TimedLaunch tl(MPGNN_K_PIECE, strm);
-        MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
-        int32_t st = hip_check(hipGetLastError(), "piece_sum_kernel launch");
+        if (vec) {
+            GatherRowsArgs ga{};
+            ga.N = k_hi;
+            ga.r_begin = k_lo;
+            ga.row_kind = 2;
+            ga.ptr = pb;
+            ga.pe = pe;
+            ga.table = a.g.idx;
+            ga.src = a.g.src;
+            ga.F = a.g.F;
+            ga.idx_off = a.g.idx_off;
+            ga.filter = a.g.filter;
+            ga.flo = a.g.flo;
+            ga.fhi = a.g.fhi;
+            ga.out = P;
+            ga.out_off = k_lo;
+            ga.dummy = a.g.dummy;
+            TimedLaunch tl(MPGNN_K_PIECE, strm);
+            launch_gather_rows(ga, strm);
+        } else {
+            PieceArgs pa{};
+            pa.pb = pb;
+            pa.pe = pe;
+            pa.k_lo = k_lo;
+            pa.k_hi = k_hi;
+            pa.src = a.g.src;
+            pa.F = a.g.F;
+            pa.idx = a.g.idx;
+            pa.idx_off = a.g.idx_off;
+            pa.filter = a.g.filter;
+            pa.dummy = a.g.dummy;
+            pa.flo = a.g.flo;
+            pa.fhi = a.g.fhi;
+            pa.P = P;
+            TimedLaunch tl(MPGNN_K_PIECE, strm);
+            MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
+        }
+        int32_t st = hip_check(hipGetLastError(), "piece sum launch");
         if (st != MPGNN_OK) return st;
         a.g.P = P;
         a.g.piece_off = k_lo;
     }
     if (a.N <= a.r_begin) return MPGNN_OK;
+    if (vec) {
+        GatherRowsArgs ga{};
+        ga.N = a.N;
+        ga.r_begin = a.r_begin;
+        ga.row_kind = a.list_kind;
+        ga.ptr = a.ptr;
+        ga.keys = a.keys;
+        ga.kb = a.kb;
+        ga.ke = a.ke;
+        ga.table = a.g.ent != nullptr ? a.res : a.g.idx;
+        ga.src = a.g.src;
+        ga.F = a.g.F;
+        ga.idx_off = a.g.idx_off;
+        ga.filter = a.g.filter;
+        ga.flo = a.g.flo;
+        ga.fhi = a.g.fhi;
+        ga.P = a.g.P;
+        ga.piece_off = a.g.piece_off;
+        ga.extra = a.extra;
+        ga.bias = a.bias;
+        ga.lo = a.lo;
+        ga.hi = a.hi;
+        ga.cnt = a.cnt;
+        ga.out_off = a.out_off;
+        ga.out = a.out;
+        ga.dummy = a.g.dummy;
+        launch_gather_rows(ga, strm);
+        return hip_check(hipGetLastError(), "gather_rows_kernel launch");
+    }
     MPGNN_VT_DISPATCH(V, T, launch_rowsum, a, strm);
     return hip_check(hipGetLastError(), "row_sum_kernel launch");
+}
+
+template <int V, int T>
+static void launch_flat(const FlatArgs& a, hipStream_t st) {
+    const int n = a.c_hi - a.c_lo;
+    hipLaunchKernelGGL((flat_rows_kernel<V, T>), dim3((n + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
+}
+
+template <int V, int T>
+static void launch_final(const FinalArgs& a, int nrows, hipStream_t st) {
+    hipLaunchKernelGGL((finalize_rows_kernel<V, T>), dim3((nrows + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
+}
+
+// Fast-path row sums over a flat chunked list: flat_rows_kernel over chunks [c_lo, c_hi), then
+// finalize_rows_kernel — mode 0 over split rows [k_lo, k_hi) (means: no empty rows, no extra),
+// mode 1 over every row [r_lo, r_hi) (split and empty rows, extra + bias on own rows).
+struct FlatRun {
+    const FlatDev* fd;
+    int c_lo, c_hi, k_lo, k_hi;
+    const int* table;
+    int idx_off, filter, flo, fhi;
+    const float* src;
+    int F;
+    int row_off;
+    float* out;
+    float* carry;
+    int final_mode;
+    const int* row_ptr;   // mode 1
+    int r_lo, r_hi;       // mode 1
+    const int* cnt;       // mode 0
+    const float* extra;
+    const float* bias;
+    int lo, hi;
+};
+
+static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
+    int V, T;
+    pick_vt(f.F, &V, &T);
+    if (f.c_hi > f.c_lo) {
+        FlatArgs a{};
+        a.chunk_ptr = f.fd->chunk_ptr;
+        a.chunk_info = f.fd->chunk_info;
+        a.c_lo = f.c_lo;
+        a.c_hi = f.c_hi;
+        a.table = f.table;
+        a.row_of = f.fd->row_of;
+        a.src = f.src;
+        a.F = f.F;
+        a.idx_off = f.idx_off;
+        a.filter = f.filter;
+        a.flo = f.flo;
+        a.fhi = f.fhi;
+        a.cnt = f.cnt;
+        a.dummy = f.fd->chunk_ptr;
+        a.row_off = f.row_off;
+        a.out = f.out;
+        a.carry = f.carry;
+        MPGNN_VT_DISPATCH(V, T, launch_flat, a, strm);
+        int32_t st = hip_check(hipGetLastError(), "flat_rows_kernel launch");
+        if (st != MPGNN_OK) return st;
+    }
+    FinalArgs b{};
+    b.mode = f.final_mode;
+    b.split_row = f.fd->split_row;
+    b.split_ptr = f.fd->split_ptr;
+    b.split_slot = f.fd->split_slot;
+    b.k0 = f.k_lo;
+    b.k1 = f.k_hi;
+    b.row_split = f.fd->row_split;
+    b.row_ptr = f.row_ptr;
+    b.r_lo = f.r_lo;
+    b.r_hi = f.r_hi;
+    b.carry = f.carry;
+    b.F = f.F;
+    b.cnt = f.cnt;
+    b.extra = f.extra;
+    b.bias = f.bias;
+    b.lo = f.lo;
+    b.hi = f.hi;
+    b.row_off = f.row_off;
+    b.out = f.out;
+    b.dummy = f.out;
+    const int nrows = f.final_mode == 0 ? f.k_hi - f.k_lo : f.r_hi - f.r_lo;
+    if (nrows <= 0) return MPGNN_OK;
+    TimedLaunch tl(MPGNN_K_FINAL, strm);
+    MPGNN_VT_DISPATCH(V, T, launch_final, b, nrows, strm);
+    return hip_check(hipGetLastError(), "finalize_rows_kernel launch");
 }
 
 // Segment means H[s - sel_b] = (Σ_{e in s} x[node_2(e)]) / cnt(s) for the selection, through
@@ -1721,6 +2321,24 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
 static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x, int F, float* H, float* Pseg,
                          bool exact, hipStream_t strm) {
     if (s.sel_e == s.sel_b) return MPGNN_OK;
+    if (!exact && g_stamps == nullptr) {
+        // flat chunked list; chunks and splits of the relation range [d_lo, d_hi)
+        FlatRun f{};
+        f.fd = &p->d.seg_f;
+        f.c_lo = p->seg_f.cut_chunk_ptr[s.d_lo];
+        f.c_hi = p->seg_f.cut_chunk_ptr[s.d_hi];
+        f.k_lo = p->seg_f.cut_split_ptr[s.d_lo];
+        f.k_hi = p->seg_f.cut_split_ptr[s.d_hi];
+        f.table = p->d.e_col;
+        f.src = x;
+        f.F = F;
+        f.row_off = s.sel_b;
+        f.out = H;
+        f.carry = Pseg;
+        f.final_mode = 0;
+        f.cnt = p->d.s_cnt;
+        return run_flat(f, strm);
+    }
     const bool ragged = !exact && s.sp_hi > s.sp_lo;
     RowSumArgs a{};
     a.r_begin = s.sel_b;
@@ -1731,9 +2349,11 @@ static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x
     a.g.F = F;
     a.g.idx = p->d.e_col;
     a.g.ent = ragged ? p->d.seg_ent : nullptr;
+    a.res = p->d.seg_res;
     a.cnt = p->d.s_cnt;
     a.out = H;
     a.out_off = s.sel_b;
+    a.stamps = g_stamps != nullptr ? g_stamps + (1u << 20) : nullptr;  // after the tile kernel's region
     return run_rowsum(p, a, p->d.seg_pb, p->d.seg_pe, ragged ? s.sp_lo : 0, ragged ? s.sp_hi : 0, Pseg, strm);
 }
 
@@ -1830,11 +2450,38 @@ int32_t mpgnn_rgcn_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
     a.hi = (int)row_hi;
     a.out = out;
     int k_lo = 0, k_hi = 0;
+    if (mode == MPGNN_MODE_ALL && !exact) {
+        FlatRun f{};
+        f.fd = &p->d.rw_f;
+        f.c_lo = 0;
+        f.c_hi = (int)p->rw_f.chunk_ptr.size() - 1;
+        f.table = p->d.rw_seg;
+        f.idx_off = s.sel_b;
+        f.filter = !s.all_segments;
+        f.flo = s.sel_b;
+        f.fhi = s.sel_e;
+        f.src = Y;
+        f.F = F_out;
+        f.row_off = 0;
+        f.out = out;
+        f.carry = reinterpret_cast<float*>(ws + w.prw);
+        f.final_mode = 1;
+        f.row_ptr = p->d.rw_ptr;
+        f.r_lo = 0;
+        f.r_hi = (int)p->N;
+        f.extra = Yroot;
+        f.bias = bias;
+        f.lo = (int)row_lo;
+        f.hi = (int)row_hi;
+        TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
+        return run_flat(f, strm);
+    }
     if (mode == MPGNN_MODE_ALL) {
         const bool ragged = !exact && !p->rw_l.piece_b.empty();
         a.list_kind = 0;
         a.ptr = ragged ? p->d.rw_ent_ptr : p->d.rw_ptr;
         a.g.ent = ragged ? p->d.rw_ent : nullptr;
+        a.res = p->d.rw_res;
         a.g.idx = p->d.rw_seg;
         a.g.idx_off = s.sel_b;
         a.g.filter = !s.all_segments;
@@ -1890,11 +2537,37 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         a.out = grad_x;
         int k_lo = 0, k_hi = 0;
         const int *pb = nullptr, *pe = nullptr;
-        if (mode == MPGNN_MODE_ALL) {
+        if (mode == MPGNN_MODE_ALL && !exact) {
+            FlatRun f{};
+            f.fd = &p->d.t_f;
+            f.c_lo = 0;
+            f.c_hi = (int)p->t_f.chunk_ptr.size() - 1;
+            f.table = p->d.t_seg;
+            f.idx_off = s.sel_b;
+            f.filter = !s.all_segments;
+            f.flo = s.sel_b;
+            f.fhi = s.sel_e;
+            f.src = G;
+            f.F = F_in;
+            f.row_off = 0;
+            f.out = grad_x;
+            f.carry = reinterpret_cast<float*>(ws + w.pdx);
+            f.final_mode = 1;
+            f.row_ptr = p->d.t_ptr;
+            f.r_lo = 0;
+            f.r_hi = (int)p->N;
+            f.extra = Groot;
+            f.lo = (int)row_lo;
+            f.hi = (int)row_hi;
+            TimedLaunch tl(MPGNN_K_ROW_DX, strm);
+            st = run_flat(f, strm);
+            if (st != MPGNN_OK) return st;
+        } else if (mode == MPGNN_MODE_ALL) {
             const bool ragged = !exact && !p->t_l.piece_b.empty() && s.sel_e > s.sel_b;
             a.list_kind = 0;
             a.ptr = ragged ? p->d.t_ent_ptr : p->d.t_ptr;
             a.g.ent = ragged ? p->d.t_ent : nullptr;
+            a.res = p->d.t_res;
             a.g.idx = p->d.t_seg;
             a.g.filter = !s.all_segments;
             a.g.flo = s.sel_b;
@@ -1912,6 +2585,7 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
                 a.kb = s.ta_e_lo;
                 a.ke = s.ta_e_hi;
                 a.g.ent = p->d.ta_ent;
+                a.res = p->d.ta_res;
                 pb = p->d.ta_pb;
                 pe = p->d.ta_pe;
                 k_lo = s.tap_lo;
@@ -1922,9 +2596,11 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
                 a.ke = (s.d_hi > s.d_lo) ? p->rel_edge_ptr[s.d_hi] : 0;
             }
         }
-        TimedLaunch tl(MPGNN_K_ROW_DX, strm);
-        st = run_rowsum(p, a, pb, pe, k_lo, k_hi, reinterpret_cast<float*>(ws + w.pdx), strm);
-        if (st != MPGNN_OK) return st;
+        if (!(mode == MPGNN_MODE_ALL && !exact)) {
+            TimedLaunch tl(MPGNN_K_ROW_DX, strm);
+            st = run_rowsum(p, a, pb, pe, k_lo, k_hi, reinterpret_cast<float*>(ws + w.pdx), strm);
+            if (st != MPGNN_OK) return st;
+        }
     }
 
     const int mt = (F_in + kColTile - 1) / kColTile;
