@@ -160,7 +160,8 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
 enum mpgnn_option {
     MPGNN_OPT_EXACT_ORDER = 0,
     MPGNN_OPT_ABLATE = 1, /* profiling only: bits skip phases of the forward tile kernel (wrong results) */
-    MPGNN_OPT_STAMPS = 2  /* profiling only: device pointer of a u64 [blocks][4 waves][8] timeline buffer, 0 = off */
+    MPGNN_OPT_STAMPS = 2, /* profiling only: device pointer of a u64 [blocks][4 waves][8] timeline buffer, 0 = off */
+    MPGNN_OPT_TIMING_MASK = 3 /* kernel kinds timed while timing is enabled (bit k = kind k); default all */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

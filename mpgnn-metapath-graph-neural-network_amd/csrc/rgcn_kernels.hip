@@ -1788,6 +1788,19 @@ struct TimingRecord {
 static std::mutex g_timing_mu;
 static bool g_timing_on = false;
 static std::vector<TimingRecord> g_timing;
+static std::vector<hipEvent_t> g_event_pool;  // events of reset records, reused (no create per launch)
+
+static bool pooled_event(hipEvent_t* e) {  // g_timing_mu held
+    if (!g_event_pool.empty()) {
+        *e = g_event_pool.back();
+        g_event_pool.pop_back();
+        return true;
+    }
+    // timing-only events: no system-scope fence (no cache writeback / invalidate between the
+    // kernels being timed)
+    return hipEventCreateWithFlags(e, hipEventDisableSystemFence) == hipSuccess;
+}
+static int64_t g_timing_mask = ~int64_t(0);  // MPGNN_OPT_TIMING_MASK: kinds timed (bit = kind)
 
 struct TimedLaunch {
     int kind;
@@ -1796,11 +1809,8 @@ struct TimedLaunch {
     bool on;
     TimedLaunch(int k, hipStream_t s) : kind(k), stream(s) {
         std::lock_guard<std::mutex> lk(g_timing_mu);
-        on = g_timing_on;
-        if (on && hipEventCreate(&start) == hipSuccess && hipEventCreate(&stop) == hipSuccess)
-            (void)hipEventRecord(start, stream);
-        else
-            on = false;
+        on = g_timing_on && ((g_timing_mask >> k) & 1) && pooled_event(&start) && pooled_event(&stop);
+        if (on) (void)hipEventRecord(start, stream);
     }
     ~TimedLaunch() {
         if (!on) return;
@@ -2372,6 +2382,11 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
         g_ablate = (int)value;
         return MPGNN_OK;
     }
+    if (option == MPGNN_OPT_TIMING_MASK) {
+        std::lock_guard<std::mutex> lk(g_timing_mu);
+        g_timing_mask = value;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_STAMPS) {
         g_stamps = reinterpret_cast<unsigned long long*>(value);
         return MPGNN_OK;
@@ -2769,8 +2784,8 @@ int32_t mpgnn_timing_enable(int32_t on) {
 int32_t mpgnn_timing_reset(void) {
     std::lock_guard<std::mutex> lk(g_timing_mu);
     for (auto& r : g_timing) {
-        (void)hipEventDestroy(r.start);
-        (void)hipEventDestroy(r.stop);
+        g_event_pool.push_back(r.start);
+        g_event_pool.push_back(r.stop);
     }
     g_timing.clear();
     return MPGNN_OK;

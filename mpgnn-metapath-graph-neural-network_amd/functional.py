@@ -45,35 +45,54 @@ def _ptr(t):
     return None if t is None else t.data_ptr()
 
 
+# Workspace per (device, stream): calls on one stream run in stream order, so one growing
+# buffer serves them all (and keeps a fixed address for HIP-graph capture).
+_WS: dict = {}
+
+
+def _workspace(nbytes: int, device: torch.device) -> torch.Tensor:
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _WS[key] = ws
+    return ws
+
+
+def _forward(x, weight, root, bias, plan: GraphPlan, mode: int, relation: int, num_relations: int,
+             row_lo: int, row_hi: int, group, need_h: bool):
+    x = _dev(x, "x")
+    weight = _dev(weight, "weight")
+    root = _dev(root, "root") if root is not None else None
+    bias = _dev(bias, "bias") if bias is not None else None
+    plan.to_device(x.device)
+    N, f_in = x.shape
+    f_out = weight.shape[-1]
+    if N != plan.num_nodes:
+        raise ValueError(f"x has {N} rows, the graph plan was built for {plan.num_nodes} nodes")
+    if weight.shape[-2] != f_in:
+        raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({N}x{f_in} and "
+                           f"{weight.shape[-2]}x{f_out})")
+    seg_b, seg_e = plan.select(mode, relation, num_relations)
+    ws = _workspace(plan.workspace_bytes(mode, relation, num_relations, f_in, f_out, row_lo, row_hi), x.device)
+    out = torch.empty(N, f_out, dtype=torch.float32, device=x.device)
+    # segment means, kept for grad_weight (dW_r = Σ h_segᵀ dout[node_1])
+    h_save = torch.empty(seg_e - seg_b, f_in, dtype=torch.float32, device=x.device) if need_h else None
+    check(lib.mpgnn_rgcn_fwd(plan.handle, mode, int(relation), int(num_relations), x.data_ptr(), f_in,
+                             weight.data_ptr(), _ptr(root), _ptr(bias), f_out, row_lo, row_hi,
+                             out.data_ptr(), _ptr(h_save), ws.data_ptr(), _stream(x)),
+          "mpgnn_rgcn_fwd")
+    if group is not None:
+        dist.all_reduce(out, group=group)
+    return out, x, weight, root, h_save
+
+
 class _RGCNConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, root, bias, plan: GraphPlan, mode: int, relation: int,
                 num_relations: int, row_lo: int, row_hi: int, group):
-        x = _dev(x, "x")
-        weight = _dev(weight, "weight")
-        root = _dev(root, "root") if root is not None else None
-        bias = _dev(bias, "bias") if bias is not None else None
-        plan.to_device(x.device)
-        N, f_in = x.shape
-        f_out = weight.shape[-1]
-        if N != plan.num_nodes:
-            raise ValueError(f"x has {N} rows, the graph plan was built for {plan.num_nodes} nodes")
-        if weight.shape[-2] != f_in:
-            raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({N}x{f_in} and "
-                               f"{weight.shape[-2]}x{f_out})")
-        seg_b, seg_e = plan.select(mode, relation, num_relations)
-        ws = torch.empty(plan.workspace_bytes(mode, relation, num_relations, f_in, f_out, row_lo, row_hi),
-                         dtype=torch.uint8, device=x.device)
-        out = torch.empty(N, f_out, dtype=torch.float32, device=x.device)
-        h_save = None  # segment means, kept for grad_weight (dW_r = Σ h_segᵀ dout[node_1])
-        if ctx.needs_input_grad[1]:
-            h_save = torch.empty(seg_e - seg_b, f_in, dtype=torch.float32, device=x.device)
-        check(lib.mpgnn_rgcn_fwd(plan.handle, mode, int(relation), int(num_relations), x.data_ptr(), f_in,
-                                 weight.data_ptr(), _ptr(root), _ptr(bias), f_out, row_lo, row_hi,
-                                 out.data_ptr(), _ptr(h_save), ws.data_ptr(), _stream(x)),
-              "mpgnn_rgcn_fwd")
-        if group is not None:
-            dist.all_reduce(out, group=group)
+        out, x, weight, root, h_save = _forward(x, weight, root, bias, plan, mode, relation, num_relations,
+                                                row_lo, row_hi, group, ctx.needs_input_grad[1])
         ctx.plan = plan
         ctx.mode, ctx.relation, ctx.num_relations = mode, relation, num_relations
         ctx.rows = (row_lo, row_hi)
@@ -96,8 +115,8 @@ class _RGCNConvFn(torch.autograd.Function):
         gw = torch.empty_like(weight) if nw else None
         gr = torch.empty_like(root) if (nr and root is not None) else None
         gb = torch.empty(f_out, dtype=torch.float32, device=x.device) if (nb and ctx.has_bias) else None
-        ws = torch.empty(plan.workspace_bytes(ctx.mode, ctx.relation, ctx.num_relations, f_in, f_out,
-                                              *ctx.rows), dtype=torch.uint8, device=x.device)
+        ws = _workspace(plan.workspace_bytes(ctx.mode, ctx.relation, ctx.num_relations, f_in, f_out,
+                                             *ctx.rows), x.device)
         check(lib.mpgnn_rgcn_bwd(plan.handle, ctx.mode, int(ctx.relation), int(ctx.num_relations),
                                  x.data_ptr(), f_in, weight.data_ptr(), _ptr(root), f_out, _ptr(h_save),
                                  grad_out.data_ptr(), ctx.rows[0], ctx.rows[1], _ptr(gx), _ptr(gw),
@@ -113,6 +132,12 @@ def rgcn_conv(x: torch.Tensor, weight: torch.Tensor, root, bias, plan: GraphPlan
               relation: int = -1, num_relations: int = 0, row_range=None, group=None) -> torch.Tensor:
     """One relational conv layer on the GPU (see module docstring)."""
     lo, hi = row_range if row_range is not None else (0, plan.num_nodes)
+    if not torch.is_grad_enabled() or not (x.requires_grad or weight.requires_grad or
+                                           (root is not None and root.requires_grad) or
+                                           (bias is not None and bias.requires_grad)):
+        # inference: no autograd node, no saved means
+        return _forward(x, weight, root, bias, plan, int(mode), int(relation), int(num_relations),
+                        int(lo), int(hi), group, False)[0]
     return _RGCNConvFn.apply(x, weight, root, bias, plan, int(mode), int(relation),
                              int(num_relations), int(lo), int(hi), group)
 

@@ -49,6 +49,8 @@ class GraphPlan:
         self._h = handle
         self._device = None
         self._lock = threading.Lock()
+        self._sel_cache: dict = {}
+        self._ws_cache: dict = {}
         info = _lib.PlanInfo()
         check(lib.mpgnn_plan_get_info(self._h, ctypes.byref(info)))
         self.num_edges = int(info.num_edges)
@@ -72,6 +74,9 @@ class GraphPlan:
         return self._h
 
     def to_device(self, device: torch.device) -> "GraphPlan":
+        if isinstance(device, torch.device) and device.type == "cuda" and device.index is not None \
+                and device.index == self._device:
+            return self  # already resident (hot path of every layer call)
         if torch.device(device).type != "cuda":
             raise RuntimeError(
                 f"mpgnn_amd: tensors are on {device}; the relational aggregation runs only as HIP "
@@ -89,10 +94,15 @@ class GraphPlan:
 
     # -- queries ---------------------------------------------------------------------------
     def select(self, mode: int, relation: int, num_relations: int) -> tuple[int, int]:
+        key = (mode, int(relation), int(num_relations))
+        hit = self._sel_cache.get(key)  # the plan is immutable: answers are cached
+        if hit is not None:
+            return hit
         b, e = ctypes.c_int64(), ctypes.c_int64()
         check(lib.mpgnn_plan_select(self._h, mode, int(relation), int(num_relations),
                                     ctypes.byref(b), ctypes.byref(e)), "mpgnn_plan_select")
-        return int(b.value), int(e.value)
+        self._sel_cache[key] = (int(b.value), int(e.value))
+        return self._sel_cache[key]
 
     def table(self, name: str) -> np.ndarray:
         tid, dtype = _lib.TABLES[name]
@@ -104,11 +114,16 @@ class GraphPlan:
         return out
 
     def workspace_bytes(self, mode, relation, num_relations, f_in, f_out, row_lo, row_hi) -> int:
+        key = (mode, int(relation), int(num_relations), f_in, f_out, row_lo, row_hi)
+        hit = self._ws_cache.get(key)
+        if hit is not None:
+            return hit
         b = ctypes.c_int64()
         check(lib.mpgnn_rgcn_workspace_bytes(self._h, mode, int(relation), int(num_relations),
                                              f_in, f_out, row_lo, row_hi, ctypes.byref(b)),
               "mpgnn_rgcn_workspace_bytes")
-        return int(b.value)
+        self._ws_cache[key] = int(b.value)
+        return self._ws_cache[key]
 
 
 class _PlanCache:
