@@ -161,7 +161,8 @@ enum mpgnn_option {
     MPGNN_OPT_EXACT_ORDER = 0,
     MPGNN_OPT_ABLATE = 1, /* profiling only: bits skip phases of the forward tile kernel (wrong results) */
     MPGNN_OPT_STAMPS = 2, /* profiling only: device pointer of a u64 [blocks][4 waves][8] timeline buffer, 0 = off */
-    MPGNN_OPT_TIMING_MASK = 3 /* kernel kinds timed while timing is enabled (bit k = kind k); default all */
+    MPGNN_OPT_TIMING_MASK = 3, /* kernel kinds timed while timing is enabled (bit k = kind k); default all */
+    MPGNN_OPT_TILE_WS = 4  /* 1: wave-specialised tile GEMM for F <= 128 (2: without priority); 0 (default): two-workgroup variant */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

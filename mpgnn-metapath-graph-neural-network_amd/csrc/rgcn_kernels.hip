@@ -682,6 +682,9 @@ struct TileGemmArgs {
     int row_lo, row_hi;
     int y_div;
     int sel_b;
+    unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][8 items][8] timeline, ws kernel
+    int ws_prio;                 // memory waves at s_setprio 1 (ws kernel)
+    int ws_ablate;               // profiling: 1 skip output stores, 2 skip A loads (wrong results)
 };
 
 struct TileItem {
@@ -830,6 +833,46 @@ __device__ __forceinline__ void mfma_strip(f32x16& acc0, f32x16& acc1, const flo
     compute_chunk(b1, t + kKC, kb + t + kKC);
 }
 
+// Output rows of an item from an LDS staging tile [64][kColTile + 4] to Y / Y_root (float4
+// rows when N % 4 == 0), divided by the item's row scales for the dgrad.  256 threads (mt).
+__device__ __forceinline__ void tile_store(const TileGemmArgs& a, const TileItem& it, int mt, const float* S,
+                                           const float* sc) {
+    constexpr int ldo = kColTile + 4;
+    float* Yt = it.root ? a.Yroot + (size_t)(it.s0 - a.row_lo) * a.N : a.Y + (size_t)(it.s0 - a.sel_b) * a.N;
+    const bool div_rows = !it.root && a.y_div;
+    const int ncols = min(kColTile, a.N - it.n_base);
+    if ((a.N & 3) == 0) {
+        const int c4n = ncols >> 2;
+#pragma unroll
+        for (int j = 0; j < kTileRows * (kColTile / 4) / 256; ++j) {
+            const int i = mt + j * 256;
+            const int row = i >> 5;
+            const int c4 = i & 31;
+            if (row < it.nrows && c4 < c4n) {
+                float4 val = *reinterpret_cast<const float4*>(S + row * ldo + c4 * 4);
+                if (div_rows) {
+                    const float d = sc[row];
+                    val.x = val.x / d;
+                    val.y = val.y / d;
+                    val.z = val.z / d;
+                    val.w = val.w / d;
+                }
+                *reinterpret_cast<float4*>(Yt + (size_t)row * a.N + it.n_base + c4 * 4) = val;
+            }
+        }
+    } else {
+        for (int i = mt; i < kTileRows * kColTile; i += 256) {
+            const int row = i >> 7;
+            const int cc = i & 127;
+            if (row < it.nrows && cc < ncols) {
+                float val = S[row * ldo + cc];
+                if (div_rows) val = val / sc[row];
+                Yt[(size_t)row * a.N + it.n_base + cc] = val;
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ int opaque(int x) {
     asm volatile("" : "+v"(x));
     return x;
@@ -970,6 +1013,131 @@ __device__ __forceinline__ void tile_gemm_body(const TileGemmArgs& a, float* sme
         __syncthreads();
         cur = nxt;
         w = wn;
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// tile_gemm_ws_kernel — the same persistent tile GEMM with specialised waves (Kp ≤ 128).
+// One 512-thread workgroup per CU: waves 0-3 (one per SIMD) run the MFMA strips of item i from
+// LDS A buffer i%2 and park their accumulators in LDS staging buffer i%2; waves 4-7 meanwhile
+// load item i+1's A rows (global → registers → A buffer (i+1)%2) and store item i-1's output
+// rows (staging (i-1)%2 → global, float4).  One barrier per item; the memory phases of one item
+// and the matrix phase of its neighbour overlap by construction (with two identical workgroups
+// per CU they ran in lockstep and added up: tile_ablate.py).  Row scales (dgrad 1/cnt) are kept
+// in three rotating buffers: item i's are written during item i-1 and read during item i+1.
+// ----------------------------------------------------------------------------------------
+constexpr int kWsThreads = 512;
+
+template <int KB, bool TRANS, bool CLAMP, int ABL = 0>
+__device__ __forceinline__ void tile_gemm_ws_body(const TileGemmArgs& a, float* smem) {
+    constexpr int Kp = 64 * KB;
+    constexpr int KH = Kp / 2;
+    constexpr int lda = Kp + 4;
+    constexpr int ldo = kColTile + 4;
+    constexpr int WPT = 4 * KB;                 // float4 per memory thread per A tile
+    float* Abuf = smem;                         // [2][64][lda]
+    float* Stg = smem + 2 * kTileRows * lda;    // [2][64][ldo]
+    float* scales = Stg + 2 * kTileRows * ldo;  // [3][64]
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool mfma_wave = wave < 4;
+    const int n_items = (a.n_rel + a.n_root) * a.ncol;
+    const ItemOrder ord(n_items);
+    int w = ord.base;
+    if (w >= ord.end) return;
+
+    TileItem cur = tile_item(a, w);
+    float b0[kKC];
+    float4 v[WPT];  // memory waves: A rows of item i+2, loaded during item i (two items of lead)
+    int cnt_raw = 1;
+    if (mfma_wave) {
+        const int lane = threadIdx.x & 63;
+        const BLoader<TRANS, CLAMP> ld0(item_bsrc(a, cur), min(cur.n_base + wave * 32 + (lane & 31), a.N - 1));
+        ld0.template load_chunk<kKC>((lane >> 5) * KH, b0);
+    } else {
+        // the younger half loses VALU arbitration to the MFMA waves on every SIMD: a static
+        // priority lets its short latency-critical bursts through (MI355X_MICROARCH.md 8-wave note 4)
+        if (a.ws_prio) __builtin_amdgcn_s_setprio(1);
+        const int mt = threadIdx.x - 256;
+        tile_issue<KB, WPT>(a, cur, mt, v, cnt_raw);
+        tile_commit<KB, WPT>(a, cur, mt, v, cnt_raw, Abuf, scales);
+        if (w + ord.stride < ord.end) tile_issue<KB, WPT>(a, tile_item(a, w + ord.stride), mt, v, cnt_raw);
+    }
+    __syncthreads();
+    TileItem prev = cur;
+    unsigned long long* st = (a.stamps != nullptr && (threadIdx.x & 63) == 0 && (wave == 0 || wave == 4))
+                                 ? a.stamps + (size_t)blockIdx.x * 128 + (wave == 0 ? 0 : 8)
+                                 : nullptr;
+    for (int i = 0; w < ord.end; ++i) {
+        const int wn = w + ord.stride;
+        const bool has_next = wn < ord.end;
+        const TileItem nxt = has_next ? tile_item(a, wn) : cur;
+        if (st != nullptr && i < 8) st[i * 16 + 0] = stamp_now();
+        if (mfma_wave) {
+            const int tid = opaque(threadIdx.x);
+            const int lane = tid & 63;
+            const int c = lane & 31;
+            const int h = lane >> 5;
+            const float* A = Abuf + (i & 1) * kTileRows * lda;
+            const BLoader<TRANS, CLAMP> ld_next(item_bsrc(a, nxt), min(nxt.n_base + wave * 32 + c, a.N - 1));
+            const BLoader<TRANS, CLAMP> ld(item_bsrc(a, cur), min(cur.n_base + wave * 32 + c, a.N - 1));
+            f32x16 acc0, acc1;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                acc0[r] = 0.0f;
+                acc1[r] = 0.0f;
+            }
+            if (st != nullptr && i < 8) st[i * 16 + 4] = stamp_now();
+            mfma_strip<TRANS, CLAMP, ABL>(acc0, acc1, A + c * lda + h * KH, A + (32 + c) * lda + h * KH, KH, h * KH, ld,
+                                          b0, ld_next);
+            if (st != nullptr && i < 8) st[i * 16 + 5] = stamp_now();
+            float* o = Stg + (i & 1) * kTileRows * ldo + (4 * h) * ldo + wave * 32 + c;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2);
+                o[row * ldo] = acc0[r];
+                o[(row + 32) * ldo] = acc1[r];
+            }
+        } else {
+            const int mt = opaque(threadIdx.x - 256);
+            // item i+1's rows were loaded during item i-1: commit them, then load item i+2's
+            if (has_next)
+                tile_commit<KB, WPT>(a, nxt, mt, v, cnt_raw, Abuf + ((i + 1) & 1) * kTileRows * lda,
+                                     scales + ((i + 1) % 3) * kTileRows);
+            if (st != nullptr && i < 8) st[i * 16 + 4] = stamp_now();
+            const int wn2 = wn + ord.stride;
+            if (wn2 < ord.end && !(a.ws_ablate & 2)) tile_issue<KB, WPT>(a, tile_item(a, wn2), mt, v, cnt_raw);
+            if (st != nullptr && i < 8) st[i * 16 + 5] = stamp_now();
+            if (i > 0 && !(a.ws_ablate & 1))
+                tile_store(a, prev, mt, Stg + ((i - 1) & 1) * kTileRows * ldo, scales + ((i - 1) % 3) * kTileRows);
+        }
+        if (st != nullptr && i < 8) st[i * 16 + 1] = stamp_now();
+        __syncthreads();
+        if (st != nullptr && i < 8) st[i * 16 + 2] = stamp_now();
+        if (!has_next && !mfma_wave)  // last item: its accumulators are staged now
+            tile_store(a, cur, threadIdx.x - 256, Stg + (i & 1) * kTileRows * ldo, scales + (i % 3) * kTileRows);
+        prev = cur;
+        cur = nxt;
+        w = wn;
+    }
+}
+
+template <int KB>  // Kp = 64·KB ≤ 128
+__global__ __launch_bounds__(kWsThreads, 1) void tile_gemm_ws_kernel(TileGemmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    if constexpr (KB == 2) {
+        if (a.ws_ablate & 4) {  // profiling: MFMA waves use constant B (no weight loads)
+            tile_gemm_ws_body<2, false, false, 2>(a, smem);
+            return;
+        }
+    }
+    const bool exact_k = a.K == 64 * KB && a.K >= kKC;
+    const int ldw = a.trans ? a.K : a.N;
+    if (!a.trans) {
+        if (exact_k) tile_gemm_ws_body<KB, false, false>(a, smem);
+        else tile_gemm_ws_body<KB, false, true>(a, smem);
+    } else {
+        if (exact_k && (ldw & 3) == 0) tile_gemm_ws_body<KB, true, false>(a, smem);
+        else tile_gemm_ws_body<KB, true, true>(a, smem);
     }
 }
 
@@ -1892,7 +2060,25 @@ static void launch_tile_gemm_abl(const TileGemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((tile_gemm_ablate_kernel<ABL>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
+static bool g_tile_ws = false;  // MPGNN_OPT_TILE_WS: wave-specialised tile GEMM for Kp <= 128 (off: equal speed today)
+static int g_ws_prio = 1;      // MPGNN_OPT_TILE_WS value 2: memory waves without priority (profiling)
+
+template <int KB>
+static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
+    constexpr int lda = 64 * KB + 4;
+    constexpr int ldo = kColTile + 4;
+    const size_t lds = (size_t)(2 * kTileRows * lda + 2 * kTileRows * ldo + 3 * kTileRows) * sizeof(float);
+    const int n_items = (a.n_rel + a.n_root) * a.ncol;
+    const int grid = std::min(n_items, cu_count());
+    hipLaunchKernelGGL((tile_gemm_ws_kernel<KB>), dim3(grid), dim3(kWsThreads), lds, st, a);
+}
+
 static void launch_tile_gemm(const TileGemmArgs& a, hipStream_t st, int abl = 0) {
+    if (abl == 0 && g_tile_ws && round_up(a.K, 64) <= 128) {
+        if (round_up(a.K, 64) <= 64) launch_tile_gemm_ws<1>(a, st);
+        else launch_tile_gemm_ws<2>(a, st);
+        return;
+    }
     if (abl != 0 && a.K == 128 && !a.trans) {
         switch (abl) {
             case 1: launch_tile_gemm_abl<1>(a, st); return;
@@ -2068,7 +2254,8 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         if (st != MPGNN_OK) return st;
     }
     // tile_gemm stages A rows as float4 (K % 4 == 0); other widths take seg_tile_kernel
-    if (gather_kind != 0 && W != nullptr && (K & 3) == 0 && (g_ablate & 15) == 0 && !g_stamps) {
+    if (gather_kind != 0 && W != nullptr && (K & 3) == 0 && (g_ablate & 15) == 0 &&
+        (!g_stamps || (g_tile_ws && round_up(K, 64) <= 128))) {
         TileGemmArgs t{};
         t.tile_begin = p->d.tile_begin;
         t.tile_end = p->d.tile_end;
@@ -2094,6 +2281,9 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         t.row_hi = (int)row_hi;
         t.y_div = gather_kind == 1;
         t.sel_b = s.sel_b;
+        t.stamps = (kind == MPGNN_K_SEG_FWD) ? g_stamps : nullptr;
+        t.ws_prio = g_ws_prio;
+        t.ws_ablate = (g_ablate >> 8) & 7;
         TimedLaunch tl(kind, strm);
         launch_tile_gemm(t, strm, g_ablate >> 4);
         return hip_check(hipGetLastError(), "tile_gemm_kernel launch");
@@ -2380,6 +2570,11 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
     }
     if (option == MPGNN_OPT_ABLATE) {
         g_ablate = (int)value;
+        return MPGNN_OK;
+    }
+    if (option == MPGNN_OPT_TILE_WS) {
+        g_tile_ws = value != 0;
+        g_ws_prio = value == 2 ? 0 : 1;
         return MPGNN_OK;
     }
     if (option == MPGNN_OPT_TIMING_MASK) {
