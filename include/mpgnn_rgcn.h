@@ -72,7 +72,18 @@ enum mpgnn_table {
     MPGNN_T_TA_COL = 14,     /* int32 [E]      node_2 of each edge in (rel, node_2) order           */
     MPGNN_T_TA_SEG = 15,     /* int32 [E]      segment id of each edge in (rel, node_2) order       */
     MPGNN_T_REL_INVALID = 16,/* uint8 [nrel]   1 if an edge of this relation had a bad node index   */
-    MPGNN_T_COUNT = 17
+    /* flat chunked lists (fast-path row sums): for list L in {SEG = segments over edges (cut at
+     * relations), T = node_2 over col-major edges, RW = node_1 over row-major segments}:
+     * CHUNK_PTR [nch+1] positions (<= 32 each, cut at row ends), CHUNK_INFO [nch] (bit0 first row
+     * split, bit1 last row split, >>2 first carry slot), ROW_OF [positions], SPLIT_ROW [nsplit],
+     * SPLIT_PTR [nsplit+1], SPLIT_SLOT [slots]                                                     */
+    MPGNN_T_SEG_F_CHUNK_PTR = 17, MPGNN_T_SEG_F_CHUNK_INFO = 18, MPGNN_T_SEG_F_ROW_OF = 19,
+    MPGNN_T_SEG_F_SPLIT_ROW = 20, MPGNN_T_SEG_F_SPLIT_PTR = 21, MPGNN_T_SEG_F_SPLIT_SLOT = 22,
+    MPGNN_T_T_F_CHUNK_PTR = 23, MPGNN_T_T_F_CHUNK_INFO = 24, MPGNN_T_T_F_ROW_OF = 25,
+    MPGNN_T_T_F_SPLIT_ROW = 26, MPGNN_T_T_F_SPLIT_PTR = 27, MPGNN_T_T_F_SPLIT_SLOT = 28,
+    MPGNN_T_RW_F_CHUNK_PTR = 29, MPGNN_T_RW_F_CHUNK_INFO = 30, MPGNN_T_RW_F_ROW_OF = 31,
+    MPGNN_T_RW_F_SPLIT_ROW = 32, MPGNN_T_RW_F_SPLIT_PTR = 33, MPGNN_T_RW_F_SPLIT_SLOT = 34,
+    MPGNN_T_COUNT = 35
 };
 
 typedef struct mpgnn_plan_info {

@@ -30,6 +30,10 @@ TABLES = {
     "rw_seg": (11, "int32"), "t_ptr": (12, "int32"), "t_seg": (13, "int32"),
     "ta_col": (14, "int32"), "ta_seg": (15, "int32"), "rel_invalid": (16, "uint8"),
 }
+# flat chunked lists (fast-path row sums): <list>_f_<table>, ids 17..34
+for _i, _l in enumerate(("seg", "t", "rw")):
+    for _j, _n in enumerate(("chunk_ptr", "chunk_info", "row_of", "split_row", "split_ptr", "split_slot")):
+        TABLES[f"{_l}_f_{_n}"] = (17 + 6 * _i + _j, "int32")
 
 
 class PlanInfo(ctypes.Structure):

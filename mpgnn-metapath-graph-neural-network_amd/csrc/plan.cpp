@@ -485,6 +485,24 @@ static const void* table_ptr(const mpgnn_plan* p, int32_t t, int64_t* n, int32_t
         case MPGNN_T_TA_COL: *n = (int64_t)p->ta_col.size(); return p->ta_col.data();
         case MPGNN_T_TA_SEG: *n = (int64_t)p->ta_seg.size(); return p->ta_seg.data();
         case MPGNN_T_REL_INVALID: *eb = 1; *n = (int64_t)p->rel_invalid.size(); return p->rel_invalid.data();
+        default: break;
+    }
+    if (t >= MPGNN_T_SEG_F_CHUNK_PTR && t < MPGNN_T_COUNT) {
+        const int k = t - MPGNN_T_SEG_F_CHUNK_PTR;
+        const FlatHost& L = k < 6 ? p->seg_f : (k < 12 ? p->t_f : p->rw_f);
+        const std::vector<int32_t>* v = nullptr;
+        switch (k % 6) {
+            case 0: v = &L.chunk_ptr; break;
+            case 1: v = &L.chunk_info; break;
+            case 2: v = &L.row_of; break;
+            case 3: v = &L.split_row; break;
+            case 4: v = &L.split_ptr; break;
+            default: v = &L.split_slot; break;
+        }
+        *n = (int64_t)v->size();
+        return v->data();
+    }
+    switch (t) {
         default: *n = -1; return nullptr;
     }
 }

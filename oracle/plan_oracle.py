@@ -13,6 +13,7 @@ from __future__ import annotations
 import numpy as np
 
 TILE_ROWS = 64
+FLAT_CHUNK = 32
 
 
 def build_plan(edge_index: np.ndarray, edge_type: np.ndarray, num_nodes: int,
@@ -79,12 +80,68 @@ def build_plan(edge_index: np.ndarray, edge_type: np.ndarray, num_nodes: int,
     ta_col = e_col[by_rel_col].astype(np.int32)
     ta_seg = seg_of_edge[by_rel_col].astype(np.int32)
 
-    return dict(
+    out = dict(
         rel_values=rel_values.astype(np.int64), rel_seg_ptr=rel_seg_ptr, rel_edge_ptr=rel_edge_ptr,
         e_col=e_col, e_id=loc.astype(np.int32), s_ptr=s_ptr, s_row=s_row, s_rel=s_rel,
         s_cnt=s_cnt, s_pos=s_pos, rw_ptr=rw_ptr, rw_seg=rw_seg, t_ptr=t_ptr, t_seg=t_seg,
         ta_col=ta_col, ta_seg=ta_seg, rel_invalid=rel_invalid,
     )
+    for name, run_ptr, cuts in (("seg", s_ptr, rel_seg_ptr), ("t", t_ptr, np.array([0, N])),
+                                ("rw", rw_ptr, np.array([0, N]))):
+        for k, v in build_flat(run_ptr, cuts).items():
+            out[f"{name}_f_{k}"] = v
+    return out
+
+
+def build_flat(run_ptr: np.ndarray, cuts: np.ndarray, chunk: int = FLAT_CHUNK) -> dict:
+    """Flat chunked list over runs (run r = positions [run_ptr[r], run_ptr[r+1]), output row r),
+    as the fast-path row sums consume it: chunks of at most ``chunk`` positions, cut at run ends
+    (and at the forced run cuts ``cuts``); a run that does not fit an empty chunk is cut inside.
+    Per chunk: bit0 first run split (starts earlier), bit1 last run split (continues later),
+    first carry slot << 2; split runs with their carry slots in chunk order."""
+    run_ptr = np.asarray(run_ptr, dtype=np.int64)
+    runs = len(run_ptr) - 1
+    P = int(run_ptr[-1]) if runs > 0 else 0
+    row_of = np.repeat(np.arange(max(runs, 0)), np.diff(run_ptr)) if runs > 0 else np.zeros(0, np.int64)
+    bounds = [0]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        pb, pe = int(run_ptr[a]), int(run_ptr[b])
+        cs = pb
+        for r in range(int(a), int(b)):
+            q, end = int(run_ptr[r]), int(run_ptr[r + 1])
+            while q < end:
+                if end - cs <= chunk:      # the rest of run r joins the open chunk
+                    q = end
+                elif q > cs:               # close the chunk before run r
+                    bounds.append(q)
+                    cs = q
+                else:                      # run longer than a chunk: cut inside it
+                    q = cs + chunk
+                    bounds.append(q)
+                    cs = q
+        if pe > cs:
+            bounds.append(pe)
+    info, split_rows, split_ptr, split_slot = [], [], [0], []
+    seen = {}
+    slot = 0
+    for c in range(len(bounds) - 1):
+        a0, a1 = bounds[c], bounds[c + 1]
+        rf, rl = int(row_of[a0]), int(row_of[a1 - 1])
+        fs, ls = run_ptr[rf] < a0, run_ptr[rl + 1] > a1
+        info.append((1 if fs else 0) | (2 if ls else 0) | (slot << 2))
+        parts = ([rf] if fs else []) + ([rl] if ls and (rl != rf or not fs) else [])
+        for row in parts:
+            if row not in seen:
+                seen[row] = len(split_rows)
+                split_rows.append(row)
+                split_ptr.append(split_ptr[-1])
+            split_slot.append(slot)
+            slot += 1
+            split_ptr[-1] += 1
+    assert P == 0 or bounds[-1] == P
+    i32 = lambda v: np.asarray(v, dtype=np.int32)  # noqa: E731
+    return dict(chunk_ptr=i32(bounds), chunk_info=i32(info), row_of=i32(row_of), split_row=i32(split_rows),
+                split_ptr=i32(split_ptr), split_slot=i32(split_slot))
 
 
 def masked_edges(edge_index: np.ndarray, edge_type: np.ndarray, relation: int) -> np.ndarray:

@@ -11,6 +11,8 @@ from oracle import plan_oracle
 
 TABLES = ["rel_values", "rel_seg_ptr", "rel_edge_ptr", "e_col", "e_id", "s_ptr", "s_row", "s_rel",
           "s_cnt", "s_pos", "rw_ptr", "rw_seg", "t_ptr", "t_seg", "ta_col", "ta_seg", "rel_invalid"]
+FLAT = [f"{l}_f_{n}" for l in ("seg", "t", "rw")
+        for n in ("chunk_ptr", "chunk_info", "row_of", "split_row", "split_ptr", "split_slot")]
 
 
 def graphs():
@@ -133,3 +135,40 @@ def test_plan_cache_reuses_and_invalidates():
     g.edge_type[0] = (g.edge_type[0] + 1) % 3       # in-place edit bumps _version
     p3 = mpgnn_amd.get_plan(g.edge_index, g.edge_type, g.num_nodes)
     assert p3 is not p1
+
+
+@pytest.mark.parametrize("case", list(graphs()) + [("hubs", None, None, None)], ids=lambda c: c[0])
+@pytest.mark.parametrize("shard", [None, (0.3, 0.7)])
+def test_flat_lists_bit_exact_and_well_formed(case, shard):
+    """Flat chunked lists (fast-path row sums) == the numpy restatement, and well formed:
+    chunks of 1..32 positions covering every position once, cut at row ends unless the row is
+    longer than a chunk; split rows have one carry slot per chunk they touch."""
+    name, ei, et, N = case
+    if name == "hubs":  # long segments / in-lists: rows of 1, 31, 32, 33, 64, 65, 300 entries
+        rows = [1, 31, 32, 33, 64, 65, 300, 2, 5]
+        n1 = np.concatenate([np.full(k, i) for i, k in enumerate(rows)])
+        n2 = np.concatenate([np.arange(k) % 40 for k in rows])
+        ei, et, N = np.stack([n1, n2]), np.zeros(len(n1), np.int64), 40
+    lo, hi = (0, N) if shard is None else (int(shard[0] * N), int(shard[1] * N))
+    plan = mpgnn_amd.GraphPlan(torch.from_numpy(np.ascontiguousarray(ei)), torch.from_numpy(np.asarray(et)), N,
+                               shard=(lo, hi))
+    ref = plan_oracle.build_plan(ei, et, N, lo, hi)
+    for tname in FLAT:
+        got = plan.table(tname)
+        assert np.array_equal(got, ref[tname]), tname
+    for l, run_ptr in (("seg", ref["s_ptr"]), ("t", ref["t_ptr"]), ("rw", ref["rw_ptr"])):
+        cp = plan.table(f"{l}_f_chunk_ptr")
+        sizes = np.diff(cp)
+        assert (sizes >= 1).all() and (sizes <= 32).all(), l
+        assert cp[0] == 0 and cp[-1] == (run_ptr[-1] if len(run_ptr) else 0), l
+        ends = set(run_ptr.tolist())
+        row_of = plan.table(f"{l}_f_row_of")
+        for b in cp[1:-1]:
+            if b not in ends:  # a cut inside a row: that row is longer than one chunk
+                r = row_of[b]
+                assert run_ptr[r + 1] - run_ptr[r] > 32, (l, r)
+        sp, ss = plan.table(f"{l}_f_split_ptr"), plan.table(f"{l}_f_split_slot")
+        assert len(np.unique(ss)) == len(ss), l
+        for k, r in enumerate(plan.table(f"{l}_f_split_row")):
+            touched = np.unique(np.searchsorted(cp, np.arange(run_ptr[r], run_ptr[r + 1]), side="right"))
+            assert sp[k + 1] - sp[k] == len(touched), (l, r)
