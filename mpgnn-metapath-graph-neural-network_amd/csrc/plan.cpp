@@ -327,6 +327,22 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
         const std::vector<int32_t> node_cuts{0, (int32_t)N};
         build_flat(p->t_ptr, node_cuts, p->t_f);
         build_flat(p->rw_ptr, node_cuts, p->rw_f);
+        // augmented lists: own rows [lo, hi) get a trailing extra-row entry
+        auto augment = [&](const std::vector<int32_t>& ptr, const std::vector<int32_t>& val, FlatHost& F,
+                           std::vector<int32_t>& out_val) {
+            std::vector<int32_t> xptr(N + 1, 0);
+            out_val.clear();
+            out_val.reserve(val.size() + (size_t)(hi - lo));
+            for (int64_t i = 0; i < N; ++i) {
+                xptr[i] = (int32_t)out_val.size();
+                for (int32_t q = ptr[i]; q < ptr[i + 1]; ++q) out_val.push_back(val[q]);
+                if (i >= lo && i < hi) out_val.push_back(-(int32_t)(i - lo) - 1);
+            }
+            xptr[N] = (int32_t)out_val.size();
+            build_flat(xptr, node_cuts, F);
+        };
+        augment(p->t_ptr, p->t_seg, p->tx_f, p->tx_val);
+        augment(p->rw_ptr, p->rw_seg, p->rwx_f, p->rwx_val);
     }
     {
         // runs of equal (relation, node_2) in ta order
@@ -582,6 +598,14 @@ int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
         {&p->d.rw_f.row_of, &p->rw_f.row_of}, {&p->d.rw_f.split_row, &p->rw_f.split_row},
         {&p->d.rw_f.split_ptr, &p->rw_f.split_ptr}, {&p->d.rw_f.split_slot, &p->rw_f.split_slot},
         {&p->d.rw_f.row_split, &p->rw_f.row_split},
+        {&p->d.tx_f.chunk_ptr, &p->tx_f.chunk_ptr}, {&p->d.tx_f.chunk_info, &p->tx_f.chunk_info},
+        {&p->d.tx_f.row_of, &p->tx_f.row_of}, {&p->d.tx_f.split_row, &p->tx_f.split_row},
+        {&p->d.tx_f.split_ptr, &p->tx_f.split_ptr}, {&p->d.tx_f.split_slot, &p->tx_f.split_slot},
+        {&p->d.tx_f.row_split, &p->tx_f.row_split}, {&p->d.tx_val, &p->tx_val},
+        {&p->d.rwx_f.chunk_ptr, &p->rwx_f.chunk_ptr}, {&p->d.rwx_f.chunk_info, &p->rwx_f.chunk_info},
+        {&p->d.rwx_f.row_of, &p->rwx_f.row_of}, {&p->d.rwx_f.split_row, &p->rwx_f.split_row},
+        {&p->d.rwx_f.split_ptr, &p->rwx_f.split_ptr}, {&p->d.rwx_f.split_slot, &p->rwx_f.split_slot},
+        {&p->d.rwx_f.row_split, &p->rwx_f.row_split}, {&p->d.rwx_val, &p->rwx_val},
     };
     size_t total = 0;
     std::vector<size_t> offs;

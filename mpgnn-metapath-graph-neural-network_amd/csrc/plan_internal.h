@@ -82,6 +82,8 @@ struct DeviceTables {
     int32_t *rw_ent = nullptr, *rw_ent_ptr = nullptr, *rw_pb = nullptr, *rw_pe = nullptr;
     int32_t *seg_res = nullptr, *t_res = nullptr, *ta_res = nullptr, *rw_res = nullptr;  // resolved entries
     FlatDev seg_f, t_f, rw_f;       // flat chunked lists (segment means, grad_x, combine)
+    FlatDev tx_f, rwx_f;            // grad_x / combine lists with a trailing extra-row entry per own row
+    int32_t *tx_val = nullptr, *rwx_val = nullptr;  // their entry values (segment id | -(own row + 1))
     void* block = nullptr;          // single hipMalloc holding every table above
     size_t block_bytes = 0;
 };
@@ -122,6 +124,11 @@ struct mpgnn_plan {
     mpgnn::RaggedHost seg_l, t_l, ta_l, rw_l;
     mpgnn::FlatHost seg_f, t_f, rw_f;     // flat chunked lists: segments over edges (cut at
                                           // relations), node_2 over col-major edges, node_1 over segments
+    // grad_x / combine lists over [shard_lo, shard_hi) rows with one trailing entry per own row
+    // (value -(row - shard_lo + 1): the G_root / Y_root row), so the flat kernel sums
+    // (Σ entries) + extra in the reference order and no finalize pass is needed
+    mpgnn::FlatHost tx_f, rwx_f;
+    std::vector<int32_t> tx_val, rwx_val;
     std::vector<int32_t> ta_key;               // [ta entries] node_2 of each ta entry
     std::vector<int32_t> rel_ta_ent_ptr;       // [nrel+1] ta entry range of each relation
     std::vector<int32_t> rel_seg_piece_ptr;    // [nrel+1] seg pieces of each relation

@@ -1329,6 +1329,9 @@ struct FlatArgs {
     float* out;
     float* carry;           // [slots][F]
     const int* dummy;       // any valid int table
+    const float* extra;     // nullable: a value v < 0 is extra row -(v+1) (augmented lists)
+    const float* bias;      // nullable: added to complete rows in [lo, hi) after their sum
+    int lo, hi;
 };
 
 template <int V, int T>
@@ -1345,8 +1348,10 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
     const int val = a.table[pq];
     const int row = a.row_of[pq];
     bool keep = lane < n;
-    if (a.filter) keep = keep && val >= a.flo && val < a.fhi;
-    const int srow = keep ? val - a.idx_off : 0;
+    const bool isx = val < 0;  // augmented lists: the row's trailing extra entry
+    if (a.filter) keep = keep && (isx || (val >= a.flo && val < a.fhi));
+    const int srow = keep ? (isx ? -val - 1 : val - a.idx_off) : 0;
+    const unsigned long long xm = __ballot(keep && isx);
     const bool has_cnt = a.cnt != nullptr;
     const int cnt_l = (has_cnt ? a.cnt : a.dummy)[has_cnt ? row : 0];
     const int next = __shfl_down(row, 1);
@@ -1359,6 +1364,14 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
     int colc[T];
 #pragma unroll
     for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, F - V);
+    const bool has_b = a.bias != nullptr;
+    float bb[T][V];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        vload<V>(has_b ? a.bias + colc[t] : a.src, bb[t]);
+#pragma unroll
+        for (int k = 0; k < V; ++k) bb[t][k] = has_b ? bb[t][k] : 0.0f;
+    }
 
     float acc[T][V];
     zero_acc<V, T>(acc);
@@ -1366,8 +1379,9 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
         float v[U][T][V];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int r = readlane(srow, min(u0 + u, n - 1));
-            const float* base = a.src + (size_t)r * F;
+            const int q = min(u0 + u, n - 1);
+            const int r = readlane(srow, q);
+            const float* base = (((xm >> q) & 1ull) ? a.extra : a.src) + (size_t)r * F;
 #pragma unroll
             for (int t = 0; t < T; ++t) vload<V>(base + colc[t], v[u][t]);
         }
@@ -1386,10 +1400,11 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
                     const int rr = readlane(row, q);
                     const bool split = (rr == rf && fs) || (rr == rl && ls);
                     float* dst;
-                    bool div = false;
+                    bool div = false, addb = false;
                     if (!split) {
                         dst = a.out + (size_t)(rr - a.row_off) * F;
                         div = has_cnt;
+                        addb = has_b && rr >= a.lo && rr < a.hi;
                     } else {
                         const int slot = slot0 + ((fs && rr == rl && rl != rf) ? 1 : 0);
                         dst = a.carry + (size_t)slot * F;
@@ -1401,7 +1416,10 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
                         if (col < F) {
                             float o[V];
 #pragma unroll
-                            for (int k = 0; k < V; ++k) o[k] = div ? acc[t][k] / d : acc[t][k];
+                            for (int k = 0; k < V; ++k) {
+                                o[k] = div ? acc[t][k] / d : acc[t][k];
+                                if (addb) o[k] = o[k] + bb[t][k];
+                            }
                             vstore<V>(dst + col, o);
                         }
                     }
@@ -1468,17 +1486,20 @@ __global__ __launch_bounds__(kThreads) void finalize_rows_kernel(FinalArgs a) {
     float acc[T][V];
     zero_acc<V, T>(acc);
     if (k >= 0) {
+        // slots of one row: 32 in flight per round trip (a hub in-list has up to ~190)
+        constexpr int SB = (V * T <= 2) ? 32 : 16;
         const int s0 = ld_uniform(a.split_ptr, k), s1 = ld_uniform(a.split_ptr, k + 1);
-        for (int sb = s0; sb < s1; sb += 8) {
-            float v[8][T][V];
+        for (int sb = s0; sb < s1; sb += SB) {
+            const int my_sl = a.split_slot[min(sb + (lane & (SB - 1)), s1 - 1)];
+            float v[SB][T][V];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int sl = ld_uniform(a.split_slot, min(sb + u, s1 - 1));
+            for (int u = 0; u < SB; ++u) {
+                const int sl = readlane(my_sl, u);
 #pragma unroll
                 for (int t = 0; t < T; ++t) vload<V>(a.carry + (size_t)sl * F + colc[t], v[u][t]);
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < SB; ++u)
                 if (sb + u < s1)
 #pragma unroll
                     for (int t = 0; t < T; ++t)
@@ -2188,12 +2209,14 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
     // piece partials (exact-order / mode SINGLE lists) or flat-list carry slots
     const size_t seg_slots = std::max((size_t)(s.sp_hi - s.sp_lo), (size_t)p->seg_f.nslots);
     w.pseg = off; off += align256(seg_slots * fmax * sizeof(float));
-    w.prw = off; off += align256((mode == MPGNN_MODE_ALL ? std::max(p->rw_l.piece_b.size(), (size_t)p->rw_f.nslots) : 0) *
-                                 F_out * sizeof(float));
+    w.prw = off; off += align256((mode == MPGNN_MODE_ALL ? std::max({p->rw_l.piece_b.size(), (size_t)p->rw_f.nslots,
+                                                                     (size_t)p->rwx_f.nslots})
+                                                         : 0) * F_out * sizeof(float));
     const size_t fwd = off;
     off = 0;
-    const size_t dx_pieces = (mode == MPGNN_MODE_ALL) ? std::max(p->t_l.piece_b.size(), (size_t)p->t_f.nslots)
-                                                      : (size_t)(s.tap_hi - s.tap_lo);
+    const size_t dx_pieces = (mode == MPGNN_MODE_ALL)
+                                 ? std::max({p->t_l.piece_b.size(), (size_t)p->t_f.nslots, (size_t)p->tx_f.nslots})
+                                 : (size_t)(s.tap_hi - s.tap_lo);
     w.g = off; off += align256(S_sel * F_in * sizeof(float));
     w.groot = off; off += align256(rows * F_in * sizeof(float));
     w.h = off; off += align256(S_sel * F_in * sizeof(float));
@@ -2482,6 +2505,12 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
         a.cnt = f.cnt;
         a.dummy = f.fd->chunk_ptr;
         a.row_off = f.row_off;
+        if (f.final_mode == 0) {  // augmented lists carry the extra rows; bias at the flush
+            a.extra = f.extra;
+            a.bias = f.bias;
+            a.lo = f.lo;
+            a.hi = f.hi;
+        }
         a.out = f.out;
         a.carry = f.carry;
         MPGNN_VT_DISPATCH(V, T, launch_flat, a, strm);
@@ -2502,7 +2531,7 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
     b.carry = f.carry;
     b.F = f.F;
     b.cnt = f.cnt;
-    b.extra = f.extra;
+    b.extra = f.final_mode == 0 ? nullptr : f.extra;  // mode 0: extra rows are inside the slots
     b.bias = f.bias;
     b.lo = f.lo;
     b.hi = f.hi;
@@ -2660,6 +2689,37 @@ int32_t mpgnn_rgcn_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
     a.hi = (int)row_hi;
     a.out = out;
     int k_lo = 0, k_hi = 0;
+    const bool own_range = row_lo == p->shard_lo && row_hi == p->shard_hi;
+    if (mode == MPGNN_MODE_ALL && !exact && Yroot != nullptr && own_range) {
+        // augmented row-major list: Σ_r Y + Y_root per own row, + bias at the flush
+        if (row_lo != 0 || row_hi != p->N) {  // rows outside the shard may have no entry
+            st = hip_check(hipMemsetAsync(out, 0, (size_t)p->N * F_out * sizeof(float), strm), "memset out");
+            if (st != MPGNN_OK) return st;
+        }
+        FlatRun f{};
+        f.fd = &p->d.rwx_f;
+        f.c_lo = 0;
+        f.c_hi = (int)p->rwx_f.chunk_ptr.size() - 1;
+        f.k_lo = 0;
+        f.k_hi = (int)p->rwx_f.split_row.size();
+        f.table = p->d.rwx_val;
+        f.idx_off = s.sel_b;
+        f.filter = !s.all_segments;
+        f.flo = s.sel_b;
+        f.fhi = s.sel_e;
+        f.src = Y;
+        f.F = F_out;
+        f.row_off = 0;
+        f.out = out;
+        f.carry = reinterpret_cast<float*>(ws + w.prw);
+        f.final_mode = 0;
+        f.extra = Yroot;
+        f.bias = bias;
+        f.lo = (int)row_lo;
+        f.hi = (int)row_hi;
+        TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
+        return run_flat(f, strm);
+    }
     if (mode == MPGNN_MODE_ALL && !exact) {
         FlatRun f{};
         f.fd = &p->d.rw_f;
@@ -2747,7 +2807,37 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         a.out = grad_x;
         int k_lo = 0, k_hi = 0;
         const int *pb = nullptr, *pe = nullptr;
-        if (mode == MPGNN_MODE_ALL && !exact) {
+        const bool own_range = row_lo == p->shard_lo && row_hi == p->shard_hi;
+        if (mode == MPGNN_MODE_ALL && !exact && Groot != nullptr && own_range) {
+            // augmented transposed list: Σ G + G_root per own row
+            if (row_lo != 0 || row_hi != p->N) {
+                st = hip_check(hipMemsetAsync(grad_x, 0, (size_t)p->N * F_in * sizeof(float), strm), "memset grad_x");
+                if (st != MPGNN_OK) return st;
+            }
+            FlatRun f{};
+            f.fd = &p->d.tx_f;
+            f.c_lo = 0;
+            f.c_hi = (int)p->tx_f.chunk_ptr.size() - 1;
+            f.k_lo = 0;
+            f.k_hi = (int)p->tx_f.split_row.size();
+            f.table = p->d.tx_val;
+            f.idx_off = s.sel_b;
+            f.filter = !s.all_segments;
+            f.flo = s.sel_b;
+            f.fhi = s.sel_e;
+            f.src = G;
+            f.F = F_in;
+            f.row_off = 0;
+            f.out = grad_x;
+            f.carry = reinterpret_cast<float*>(ws + w.pdx);
+            f.final_mode = 0;
+            f.extra = Groot;
+            f.lo = (int)row_lo;
+            f.hi = (int)row_hi;
+            TimedLaunch tl(MPGNN_K_ROW_DX, strm);
+            st = run_flat(f, strm);
+            if (st != MPGNN_OK) return st;
+        } else if (mode == MPGNN_MODE_ALL && !exact) {
             FlatRun f{};
             f.fd = &p->d.t_f;
             f.c_lo = 0;
@@ -2825,8 +2915,12 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
     // ---- grad_weight[r] = Σ_{seg of r} h_segᵀ dout[node_1(seg)] -------------------------
     if (grad_weight != nullptr) {
         const size_t wbytes = (mode == MPGNN_MODE_ALL ? (size_t)std::max(R, 0) : 1) * wsize * sizeof(float);
-        if ((st = hip_check(hipMemsetAsync(grad_weight, 0, wbytes, strm), "memset grad_weight")) != MPGNN_OK)
-            return st;
+        // every weight index with a segment range is written (directly or by the slab reduce,
+        // zeros for an empty range); only indices absent from the plan need the memset
+        const bool all_written = (mode == MPGNN_MODE_ALL) ? (s.d_hi - s.d_lo) == (int64_t)R : (s.c_hi > s.c_lo);
+        if (!all_written)
+            if ((st = hip_check(hipMemsetAsync(grad_weight, 0, wbytes, strm), "memset grad_weight")) != MPGNN_OK)
+                return st;
         const int nch = s.c_hi - s.c_lo;
         if (nch > 0) {
             const float* H = h_save;
