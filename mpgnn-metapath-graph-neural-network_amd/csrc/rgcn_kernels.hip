@@ -2308,7 +2308,7 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         t.ws_prio = g_ws_prio;
         t.ws_ablate = (g_ablate >> 8) & 7;
         TimedLaunch tl(kind, strm);
-        launch_tile_gemm(t, strm, g_ablate >> 4);
+        launch_tile_gemm(t, strm, (g_ablate >> 4) & 15);  // bits 4-7: two-workgroup kernel ablations
         return hip_check(hipGetLastError(), "tile_gemm_kernel launch");
     }
     SegTileArgs a{};

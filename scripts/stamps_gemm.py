@@ -20,12 +20,17 @@ with torch.no_grad():
     for _ in range(5):
         conv(x, ei, et)
 torch.cuda.synchronize()
-buf = torch.zeros(1 << 20, dtype=torch.int64, device="cuda")
+abl = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+_lib.lib.mpgnn_set_option(4, 1)            # wave-specialised kernel (carries the stamps)
+_lib.lib.mpgnn_set_option(1, abl << 8)     # its ablation bits (1 stores, 2 A loads, 4 weight loads)
+buf = torch.zeros((1 << 20) + 65536 * 8, dtype=torch.int64, device="cuda")  # + row_sum stamps region
 _lib.lib.mpgnn_set_option(2, buf.data_ptr())
 with torch.no_grad():
     conv(x, ei, et)
 torch.cuda.synchronize()
 _lib.lib.mpgnn_set_option(2, 0)
+_lib.lib.mpgnn_set_option(1, 0)
+_lib.lib.mpgnn_set_option(4, 0)
 st = buf[: 256 * 128].cpu().numpy().reshape(256, 8, 2, 8)  # wg, item, (mfma, mem), stamps
 res = {}
 ph_m, ph_s, wait_m, wait_s, item_t = [], [], [], [], []
