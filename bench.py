@@ -15,9 +15,10 @@ all-reduce over xGMI: total work is fixed, so "scaling" is "strong".
 Also reported (separate loops, outside the timed step): the training epoch of
 main_rgcn.py:458-461 — train step (forward + NLL + backward + Adam) + validation forward.
 
-roofline: the dominant kernel (seg_tile_kernel, forward) timed live with HIP events on its
-launch stream over the timed region; algorithmic FLOPs = 2·S·F_in·F_out per launch
-(segment contraction) against the dense fp32 MFMA peak (157.3 TFLOP/s); algorithmic bytes
+roofline: the dominant kernel (tile_gemm_kernel, forward) timed live with HIP events on its
+launch stream over the timed region; algorithmic FLOPs = 2·(S + N)·F_in·F_out per launch
+(segment rows H @ W_r plus node rows x @ root, both computed by that launch) against the
+dense fp32 MFMA peak (157.3 TFLOP/s); algorithmic bytes (A rows in, Y rows out, weights)
 reported beside it.  traffic: HBM bytes per launch from rocprofv3 PMC counters
 (profiles/pmc_seg_fwd.json when present, else null).
 cpu_baseline: the CPU oracle (PyG-2.3.1 loop semantics, same ATen ops) timed on this host.
@@ -217,8 +218,9 @@ def main():
     S = plan.num_segments
     E_loc = plan.num_edges
     seg_avg_ms = seg_ms / max(seg_n, 1)
-    flops = 2.0 * S * F * F
-    alg_bytes = E_loc * (4 * F + 4) + S * (16 + 4 * F)   # gathered rows + col idx; seg meta + Y write
+    n_root = plan.num_nodes if world == 1 else (shard[1] - shard[0])
+    flops = 2.0 * (S + n_root) * F * F   # Y = H @ W_r over S segment rows + Y_root = x @ root
+    alg_bytes = 4 * F * (2 * S + 2 * n_root) + 4 * F * F * (plan.num_relations_present + 1)  # A rows in, Y out, W
     achieved_tf = flops / (seg_avg_ms * 1e-3) / 1e12 if seg_n else None
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_seg_fwd.json")
