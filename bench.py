@@ -124,7 +124,7 @@ def main():
     def step():
         h = x
         for conv in convs:
-            h = torch.relu(conv(h, ei, et, shard=shard, group=group))
+            h = conv(h, ei, et, shard=shard, group=group, activation="relu")  # F.relu(conv(...)), model.py:144,146
         return h
 
     # plan (built once per graph, cached) + warm-up

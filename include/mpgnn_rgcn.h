@@ -149,6 +149,19 @@ int32_t mpgnn_rgcn_fwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
                        int32_t F_out, int64_t row_lo, int64_t row_hi, float* out,
                        float* h_save, void* workspace, void* stream);
 
+enum mpgnn_activation { MPGNN_ACT_NONE = 0, MPGNN_ACT_RELU = 1 };
+
+/* Layer forward with the caller's activation fused into the combine epilogue:
+ *   out = act(Σ_r mean_r(x) @ W_r + x @ root + bias)
+ * i.e. `F.relu(conv(x, edge_index, edge_type))` of model.py:144-146 (Net) and the ReLU after
+ * each metapath layer of MPNetm (model.py:211,214) in one call. Unsharded plans only (a
+ * sharded layer's out is a partial sum: activate after the all-reduce); rows [0, N). */
+int32_t mpgnn_rgcn_fwd_act(const mpgnn_plan* plan, int32_t mode, int64_t relation,
+                           int32_t num_relations, const float* x, int32_t F_in,
+                           const float* weight, const float* root, const float* bias,
+                           int32_t F_out, float* out, float* h_save, void* workspace,
+                           int32_t act, void* stream);
+
 /* Layer backward given grad_out [N, F_out] and the h_save of the forward.
  * Any grad_* pointer may be NULL to skip that gradient.
  *   grad_x      [N, F_in]           (= Σ_r A_rᵀ (grad_out W_rᵀ) + grad_out rootᵀ)
@@ -173,7 +186,8 @@ enum mpgnn_option {
     MPGNN_OPT_ABLATE = 1, /* profiling only: bits skip phases of the forward tile kernel (wrong results) */
     MPGNN_OPT_STAMPS = 2, /* profiling only: device pointer of a u64 [blocks][4 waves][8] timeline buffer, 0 = off */
     MPGNN_OPT_TIMING_MASK = 3, /* kernel kinds timed while timing is enabled (bit k = kind k); default all */
-    MPGNN_OPT_TILE_WS = 4  /* 1: wave-specialised tile GEMM for F <= 128 (2: without priority); 0 (default): two-workgroup variant */
+    MPGNN_OPT_TILE_WS = 4, /* 1: wave-specialised tile GEMM for F <= 128 (2: without priority); 0 (default): two-workgroup variant */
+    MPGNN_OPT_REL_GEMM = 5 /* 1 (default): B-stationary GEMM (weights in registers) for F_in, F_out in {64,128} x {128}; 0: tile GEMM */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

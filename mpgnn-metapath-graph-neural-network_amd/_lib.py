@@ -65,6 +65,7 @@ SIGNATURES = [
     ("mpgnn_rgcn_workspace_bytes", _I32, [_P, _I32, _I64, _I32, _I32, _I32, _I64, _I64, _PI64]),
     ("mpgnn_rgcn_fwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _I64, _I64,
                               _P, _P, _P, _P]),
+    ("mpgnn_rgcn_fwd_act", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _P, _P, _P, _I32, _P]),
     ("mpgnn_rgcn_bwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _I32, _P, _P, _I64, _I64,
                               _P, _P, _P, _P, _P, _P]),
     ("mpgnn_set_option", _I32, [_I32, _I64]),
@@ -77,6 +78,7 @@ SIGNATURES = [
 KERNEL_KINDS = {"seg_fwd": 0, "row_fwd": 1, "seg_dgrad": 2, "row_dx": 3, "outer": 4, "reduce": 5, "mean": 6,
                 "piece": 7, "final": 8}
 OPT_EXACT_ORDER = 0
+ACT_NONE, ACT_RELU = 0, 1
 
 
 def _load():

@@ -13,6 +13,9 @@ namespace mpgnn {
 // Segments are packed into relation-pure tiles of this many rows: one workgroup of the
 // segment-transform kernel owns one tile (rgcn_kernels.hip, seg_tile_kernel).
 constexpr int kTileRows = 64;
+// 32-row relation-pure tiles of the B-stationary GEMM (rel_gemm_kernel): the work unit one
+// wave-quad turns into 32 output rows while W_r stays in registers.
+constexpr int kTile32 = 32;
 // Relation-pure reduction chunks for the weight gradient (outer_accum_kernel): at most this
 // many segments, balanced within a relation (bounds the longest workgroup's MFMA chain).
 constexpr int kChunkRows = 128;
@@ -70,6 +73,8 @@ struct DeviceTables {
     int32_t* ta_seg = nullptr;
     int32_t* tile_begin = nullptr;  // [num_tiles] first segment of the tile
     int32_t* tile_end = nullptr;    // [num_tiles] one past the last segment
+    int32_t* t32_begin = nullptr;   // [num_tiles32] first segment of a 32-row tile
+    int32_t* t32_end = nullptr;     // [num_tiles32] one past its last segment
     int32_t* chunk_begin = nullptr; // [num_chunks]
     int32_t* chunk_end = nullptr;   // [num_chunks]
     int32_t* rel_chunk_ptr = nullptr; // [nrel+1]
@@ -103,6 +108,7 @@ struct mpgnn_plan {
     std::vector<int32_t> rel_seg_ptr;  // [nrel+1]
     std::vector<int32_t> rel_edge_ptr; // [nrel+1]
     std::vector<int32_t> rel_tile_ptr; // [nrel+1]
+    std::vector<int32_t> rel_t32_ptr;  // [nrel+1] 32-row tiles of each relation
     std::vector<int32_t> rel_chunk_ptr;// [nrel+1]
 
     std::vector<int32_t> e_col, e_id;          // [E]
@@ -114,6 +120,7 @@ struct mpgnn_plan {
     std::vector<int32_t> t_seg;                // [E]
     std::vector<int32_t> ta_col, ta_seg;       // [E]
     std::vector<int32_t> tile_begin, tile_end; // [num_tiles]
+    std::vector<int32_t> t32_begin, t32_end;   // [num_tiles32]
     std::vector<int32_t> chunk_begin, chunk_end; // [num_chunks]
     std::vector<int32_t> rel_val32;            // [nrel]
     std::vector<int32_t> chunk_dst;            // [num_chunks] see DeviceTables::chunk_dst

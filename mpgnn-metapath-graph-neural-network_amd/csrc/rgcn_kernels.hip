@@ -1016,6 +1016,215 @@ __device__ __forceinline__ void tile_gemm_body(const TileGemmArgs& a, float* sme
     }
 }
 
+
+// ----------------------------------------------------------------------------------------
+// rel_gemm_kernel — B-stationary persistent GEMM for the forward transform and the dgrad
+// (K = 64·KB ∈ {64, 128}, N = 128 output columns).
+//
+//   forward: Y[s] = H[s] @ W_rel(s)              Y_root[i] = x[i] @ root
+//   dgrad:   G[s] = (dout[s_row[s]] @ W_relᵀ) / cnt[s]   G_root[i] = dout[i] @ rootᵀ
+//
+// Work items are 32-row relation-pure tiles (plan t32 tables) followed by 32-node root tiles;
+// workgroup b owns the contiguous item range [b·n/G, (b+1)·n/G), so consecutive items mostly
+// share a relation.  Wave w owns output columns [32w, 32w + 32) and holds its K × 32 slice of
+// the current relation's weight IN REGISTERS (KH = K/2 VGPRs: lane-half h carries
+// k ∈ [h·KH, (h+1)·KH), column 32w + (lane & 31)), so the weight is read once per relation
+// run instead of once per tile; the next run's slice is fetched into a second register set
+// during the last tile of the current run.  A tiles (32 rows × K) are double-buffered in LDS:
+// item i+1's rows are loaded into registers before item i's MFMAs and written to the other
+// buffer after them (one barrier per item).  v_mfma_f32_32x32x2_f32 (exact f32 fma chain):
+// each wave issues KH MFMAs per item from ds_read_b128 A fragments (one per four MFMAs).
+// Output rows leave straight from the accumulators: each accumulator register is two 128-B
+// row segments (C/D layout: col = lane & 31, row = (r & 3) + 8(r >> 2) + 4(lane >> 5)).
+// ----------------------------------------------------------------------------------------
+struct RelGemmArgs {
+    const int* t_begin;   // 32-row relation tiles (segments)
+    const int* t_end;
+    int t_lo;             // first tile of the selection
+    int n_rel, n_root;    // items [0, n_rel) tiles t_lo + i; [n_rel, n_rel + n_root) node rows
+    const float* Arel;    // forward: H (row s - sel_b); dgrad: dout gathered by s_row[s]
+    const float* Aroot;   // forward: x; dgrad: dout  (row i)
+    const int* s_row;
+    const int* s_cnt;
+    const int* s_rel;
+    const float* W;       // [R][K][N] (w_per_rel) or [K][N]; dgrad: [R][N][K] / [N][K] (transposed use)
+    int w_per_rel;
+    const float* Wroot;   // [K][N]; dgrad [N][K]
+    float* Y;             // rows s - sel_b
+    float* Yroot;         // rows i - row_lo
+    int sel_b, row_lo, row_hi;
+    unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][32] s_memtime timeline, or nullptr
+};
+
+template <int KB, bool DGRAD>
+struct RelGemm {
+    static constexpr int K = 64 * KB;
+    static constexpr int KH = K / 2;
+    static constexpr int N = 128;
+    static constexpr int lda = K + 4;
+    static constexpr int WPT = 32 * (K / 4) / kThreads;  // float4 of an A tile per thread
+
+    struct Item {
+        int r0, nrows, root;
+        const float* w;   // weight matrix of the item (uniform)
+    };
+
+    __device__ static __forceinline__ Item item(const RelGemmArgs& a, int i) {
+        Item it;
+        it.root = i >= a.n_rel;
+        if (!it.root) {
+            it.r0 = ld_uniform(a.t_begin, a.t_lo + i);
+            it.nrows = ld_uniform(a.t_end, a.t_lo + i) - it.r0;
+            it.w = a.W + (a.w_per_rel ? (size_t)ld_uniform(a.s_rel, it.r0) * K * N : 0);
+        } else {
+            it.r0 = a.row_lo + (i - a.n_rel) * 32;
+            it.nrows = min(32, a.row_hi - it.r0);
+            it.w = a.Wroot;
+        }
+        return it;
+    }
+
+    // A rows of an item into registers (clamped rows; zeroed at commit) + the dgrad row scale.
+    __device__ static __forceinline__ void issue(const RelGemmArgs& a, const Item& it, int tid, float4 (&v)[WPT],
+                                                 int& cnt) {
+        constexpr int W4 = K / 4;
+        int row[WPT];
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) row[j] = it.r0 + min((tid + j * kThreads) / W4, it.nrows - 1);
+        const float* base;
+        cnt = 1;
+        if (it.root) {
+            base = a.Aroot;
+        } else if constexpr (DGRAD) {
+            base = a.Aroot;
+            cnt = a.s_cnt[it.r0 + min(tid & 31, it.nrows - 1)];
+#pragma unroll
+            for (int j = 0; j < WPT; ++j) row[j] = a.s_row[row[j]];
+        } else {
+            base = a.Arel;
+#pragma unroll
+            for (int j = 0; j < WPT; ++j) row[j] -= a.sel_b;
+        }
+#pragma unroll
+        for (int j = 0; j < WPT; ++j)
+            v[j] = *reinterpret_cast<const float4*>(base + (size_t)row[j] * K + ((tid + j * kThreads) % W4) * 4);
+    }
+
+    __device__ static __forceinline__ void commit(const Item& it, int tid, const float4 (&v)[WPT], int cnt, float* A,
+                                                  float* sc) {
+        constexpr int W4 = K / 4;
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+            const int e = tid + j * kThreads;
+            const int r = e / W4;
+            *reinterpret_cast<float4*>(A + r * lda + (e % W4) * 4) =
+                r < it.nrows ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (tid < 32) sc[tid] = (float)cnt;
+    }
+
+    // this wave's K × 32 weight slice: lane-half h holds k = h·KH + j, column 32·wave + c
+    __device__ static __forceinline__ void load_b(const float* w, int wave, int lane, float (&b)[KH]) {
+        const int c = lane & 31, h = lane >> 5;
+        if constexpr (!DGRAD) {
+            const float* p = w + (size_t)(h * KH) * N + wave * 32 + c;
+#pragma unroll
+            for (int j = 0; j < KH; ++j) b[j] = p[j * N];
+        } else {  // B(k, n) = W[n][k]: K consecutive floats of row n = 32·wave + c
+            const float* p = w + (size_t)(wave * 32 + c) * K + h * KH;
+#pragma unroll
+            for (int j = 0; j < KH; j += 4) {
+                const float4 t = *reinterpret_cast<const float4*>(p + j);
+                b[j] = t.x;
+                b[j + 1] = t.y;
+                b[j + 2] = t.z;
+                b[j + 3] = t.w;
+            }
+        }
+    }
+
+    __device__ static void run(const RelGemmArgs& a, float* smem) {
+        float* As = smem;                 // [2][32][lda]
+        float* Sc = smem + 2 * 32 * lda;  // [2][32] dgrad row scales
+        const int tid = threadIdx.x;
+        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int n_items = a.n_rel + a.n_root;
+        const int G = (int)gridDim.x;
+        const int i_beg = (int)((long long)blockIdx.x * n_items / G);
+        const int i_end = (int)((long long)(blockIdx.x + 1) * n_items / G);
+        if (i_beg >= i_end) return;
+        unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 32 : nullptr;
+        auto stamp = [&](int k) {
+            if (stp != nullptr && tid == 0 && k < 32) stp[k] = stamp_now();
+        };
+        stamp(0);
+
+        float4 v[WPT];
+        int cnt;
+        Item cur = item(a, i_beg);
+        issue(a, cur, tid, v, cnt);
+        float b[KH];
+        load_b(cur.w, wave, lane, b);
+        commit(cur, tid, v, cnt, As, Sc);
+        __syncthreads();
+        stamp(1);
+        int buf = 0;
+        for (int i = i_beg; i < i_end; ++i) {
+            const bool has_next = i + 1 < i_end;
+            const Item nxt = has_next ? item(a, i + 1) : cur;
+            if (has_next) issue(a, nxt, tid, v, cnt);      // in flight during this item's MFMAs
+            const bool new_w = nxt.w != cur.w;
+            float bn[KH];
+            if (new_w) load_b(nxt.w, wave, lane, bn);      // the next relation run's slice
+            const float* Ab = As + buf * 32 * lda + c * lda + h * KH;
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+            float4 af = *reinterpret_cast<const float4*>(Ab);
+#pragma unroll
+            for (int j = 0; j < KH; j += 4) {
+                const float4 cf = af;
+                if (j + 4 < KH) af = *reinterpret_cast<const float4*>(Ab + j + 4);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], acc, 0, 0, 0);
+            }
+            stamp(2 + 2 * (i - i_beg));
+            // epilogue: each accumulator register = rows (r&3) + 8(r>>2) + 4h, column 32·wave + c
+            float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
+            const float* sc = Sc + buf * 32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row < cur.nrows) {
+                    float o = acc[r];
+                    if constexpr (DGRAD) {
+                        if (!cur.root) o = o / sc[row];
+                    }
+                    Yt[(size_t)row * N + wave * 32 + c] = o;
+                }
+            }
+            if (has_next) commit(nxt, tid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
+            if (new_w) {
+#pragma unroll
+                for (int j = 0; j < KH; ++j) b[j] = bn[j];
+            }
+            __syncthreads();
+            stamp(3 + 2 * (i - i_beg));
+            cur = nxt;
+            buf ^= 1;
+        }
+    }
+};
+
+template <int KB, bool DGRAD>
+__global__ __launch_bounds__(kThreads, 2) void rel_gemm_kernel(RelGemmArgs a) {
+    extern __shared__ float smem[];
+    RelGemm<KB, DGRAD>::run(a, smem);
+}
+
 // ----------------------------------------------------------------------------------------
 // tile_gemm_ws_kernel — the same persistent tile GEMM with specialised waves (Kp ≤ 128).
 // One 512-thread workgroup per CU: waves 0-3 (one per SIMD) run the MFMA strips of item i from
@@ -1332,6 +1541,7 @@ struct FlatArgs {
     const float* extra;     // nullable: a value v < 0 is extra row -(v+1) (augmented lists)
     const float* bias;      // nullable: added to complete rows in [lo, hi) after their sum
     int lo, hi;
+    int relu;               // fused activation on complete rows (unsharded combine only)
 };
 
 template <int V, int T>
@@ -1419,6 +1629,7 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
                             for (int k = 0; k < V; ++k) {
                                 o[k] = div ? acc[t][k] / d : acc[t][k];
                                 if (addb) o[k] = o[k] + bb[t][k];
+                                if (!split && a.relu) o[k] = fmaxf(o[k], 0.0f);
                             }
                             vstore<V>(dst + col, o);
                         }
@@ -1453,6 +1664,7 @@ struct FinalArgs {
     int row_off;
     float* out;
     const float* dummy;    // any valid float row
+    int relu;              // fused activation after the bias
 };
 
 template <int V, int T>
@@ -1527,6 +1739,7 @@ __global__ __launch_bounds__(kThreads) void finalize_rows_kernel(FinalArgs a) {
                 o[q] = acc[t][q];
                 if (has_ex) o[q] = o[q] + ex[t][q];
                 if (has_b) o[q] = o[q] + bb[t][q];
+                if (a.relu) o[q] = fmaxf(o[q], 0.0f);
             }
             vstore<V>(a.out + (size_t)(row - a.row_off) * F + col, o);
         }
@@ -2094,6 +2307,28 @@ static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((tile_gemm_ws_kernel<KB>), dim3(grid), dim3(kWsThreads), lds, st, a);
 }
 
+
+static bool g_rel_gemm = true;  // MPGNN_OPT_REL_GEMM: B-stationary GEMM for K ∈ {64, 128}, N = 128
+
+template <int KB, bool DGRAD>
+static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
+    constexpr int lda = 64 * KB + 4;
+    const size_t lds = (size_t)(2 * 32 * lda + 64) * sizeof(float);
+    const int n_items = a.n_rel + a.n_root;
+    const int grid = std::min(n_items, cu_count() * 2);
+    hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
+}
+
+static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, hipStream_t st) {
+    if (K == 64) {
+        if (dgrad) launch_rel_gemm_t<1, true>(a, st);
+        else launch_rel_gemm_t<1, false>(a, st);
+    } else {
+        if (dgrad) launch_rel_gemm_t<2, true>(a, st);
+        else launch_rel_gemm_t<2, false>(a, st);
+    }
+}
+
 static void launch_tile_gemm(const TileGemmArgs& a, hipStream_t st, int abl = 0) {
     if (abl == 0 && g_tile_ws && round_up(a.K, 64) <= 128) {
         if (round_up(a.K, 64) <= 64) launch_tile_gemm_ws<1>(a, st);
@@ -2145,6 +2380,7 @@ struct Selection {
     int64_t d_lo = 0, d_hi = 0;
     int sel_b = 0, sel_e = 0;
     int t_lo = 0, t_hi = 0;
+    int t32_lo = 0, t32_hi = 0;   // 32-row tiles (rel_gemm_kernel)
     int c_lo = 0, c_hi = 0;
     int sp_lo = 0, sp_hi = 0;     // seg-list pieces of the selection
     int tap_lo = 0, tap_hi = 0;   // ta-list pieces (mode SINGLE)
@@ -2160,6 +2396,8 @@ static int32_t make_selection(const mpgnn_plan* p, int32_t mode, int64_t relatio
     s->sel_e = p->rel_seg_ptr[s->d_hi];
     s->t_lo = p->rel_tile_ptr[s->d_lo];
     s->t_hi = p->rel_tile_ptr[s->d_hi];
+    s->t32_lo = p->rel_t32_ptr[s->d_lo];
+    s->t32_hi = p->rel_t32_ptr[s->d_hi];
     s->c_lo = p->rel_chunk_ptr[s->d_lo];
     s->c_hi = p->rel_chunk_ptr[s->d_hi];
     s->sp_lo = p->rel_seg_piece_ptr[s->d_lo];
@@ -2275,6 +2513,34 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
         int32_t st = hip_check(hipGetLastError(), "piece_sum_kernel(seg) launch");
         if (st != MPGNN_OK) return st;
+    }
+    // B-stationary GEMM (weights in registers per relation run) for the bench shapes
+    if (gather_kind != 0 && W != nullptr && g_rel_gemm && (K == 64 || K == 128) && N == 128 && g_ablate == 0 &&
+        (!g_stamps || !g_tile_ws) && trans == (gather_kind == 1 ? 1 : 0)) {
+        RelGemmArgs r{};
+        r.t_begin = p->d.t32_begin;
+        r.t_end = p->d.t32_end;
+        r.t_lo = s.t32_lo;
+        r.n_rel = s.t32_hi - s.t32_lo;
+        r.n_root = (Wroot != nullptr) ? (int)((row_hi - row_lo + 31) / 32) : 0;
+        if (r.n_rel + r.n_root == 0) return MPGNN_OK;
+        r.Arel = gather_kind == 2 ? Hsrc : src;
+        r.Aroot = src;
+        r.s_row = p->d.s_row;
+        r.s_cnt = p->d.s_cnt;
+        r.s_rel = p->d.s_rel;
+        r.W = W;
+        r.w_per_rel = (mode == MPGNN_MODE_ALL);
+        r.Wroot = Wroot;
+        r.Y = Y;
+        r.Yroot = Yroot;
+        r.sel_b = s.sel_b;
+        r.row_lo = (int)row_lo;
+        r.row_hi = (int)row_hi;
+        r.stamps = (kind == MPGNN_K_SEG_FWD) ? g_stamps : nullptr;
+        TimedLaunch tl(kind, strm);
+        launch_rel_gemm(r, K, gather_kind == 1, strm);
+        return hip_check(hipGetLastError(), "rel_gemm_kernel launch");
     }
     // tile_gemm stages A rows as float4 (K % 4 == 0); other widths take seg_tile_kernel
     if (gather_kind != 0 && W != nullptr && (K & 3) == 0 && (g_ablate & 15) == 0 &&
@@ -2463,6 +2729,12 @@ static void launch_final(const FinalArgs& a, int nrows, hipStream_t st) {
     hipLaunchKernelGGL((finalize_rows_kernel<V, T>), dim3((nrows + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
 }
 
+// In-place ReLU for the paths whose combine has no fused activation (exact order, mode SINGLE).
+__global__ __launch_bounds__(kThreads) void relu_kernel(float* __restrict__ p, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (size_t)gridDim.x * kThreads)
+        p[i] = fmaxf(p[i], 0.0f);
+}
+
 // Fast-path row sums over a flat chunked list: flat_rows_kernel over chunks [c_lo, c_hi), then
 // finalize_rows_kernel — mode 0 over split rows [k_lo, k_hi) (means: no empty rows, no extra),
 // mode 1 over every row [r_lo, r_hi) (split and empty rows, extra + bias on own rows).
@@ -2483,6 +2755,7 @@ struct FlatRun {
     const float* extra;
     const float* bias;
     int lo, hi;
+    int relu;             // fused activation (unsharded forward combine)
 };
 
 static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
@@ -2513,6 +2786,7 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
         }
         a.out = f.out;
         a.carry = f.carry;
+        a.relu = f.final_mode == 0 ? f.relu : 0;  // mode 1: the finalize adds extra + bias first
         MPGNN_VT_DISPATCH(V, T, launch_flat, a, strm);
         int32_t st = hip_check(hipGetLastError(), "flat_rows_kernel launch");
         if (st != MPGNN_OK) return st;
@@ -2538,6 +2812,7 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
     b.row_off = f.row_off;
     b.out = f.out;
     b.dummy = f.out;
+    b.relu = f.relu;
     const int nrows = f.final_mode == 0 ? f.k_hi - f.k_lo : f.r_hi - f.r_lo;
     if (nrows <= 0) return MPGNN_OK;
     TimedLaunch tl(MPGNN_K_FINAL, strm);
@@ -2601,6 +2876,10 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
         g_ablate = (int)value;
         return MPGNN_OK;
     }
+    if (option == MPGNN_OPT_REL_GEMM) {
+        g_rel_gemm = value != 0;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_TILE_WS) {
         g_tile_ws = value != 0;
         g_ws_prio = value == 2 ? 0 : 1;
@@ -2646,10 +2925,36 @@ int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* p, int32_t mode, int64_t re
     return MPGNN_OK;
 }
 
+static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
+                             int32_t F_in, const float* weight, const float* root, const float* bias,
+                             int32_t F_out, int64_t row_lo, int64_t row_hi, float* out, float* h_save,
+                             void* workspace, int32_t act, void* stream);
+
 int32_t mpgnn_rgcn_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
                        int32_t F_in, const float* weight, const float* root, const float* bias,
                        int32_t F_out, int64_t row_lo, int64_t row_hi, float* out, float* h_save,
                        void* workspace, void* stream) {
+    return rgcn_fwd_impl(p, mode, relation, R, x, F_in, weight, root, bias, F_out, row_lo, row_hi, out, h_save,
+                         workspace, MPGNN_ACT_NONE, stream);
+}
+
+int32_t mpgnn_rgcn_fwd_act(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
+                           int32_t F_in, const float* weight, const float* root, const float* bias,
+                           int32_t F_out, float* out, float* h_save, void* workspace, int32_t act,
+                           void* stream) {
+    if (act != MPGNN_ACT_NONE && act != MPGNN_ACT_RELU) return arg_error("unknown activation");
+    if (p && (p->shard_lo != 0 || p->shard_hi != p->N))
+        return arg_error("fused activation needs an unsharded plan (sharded outputs are partial sums)");
+    return rgcn_fwd_impl(p, mode, relation, R, x, F_in, weight, root, bias, F_out, 0, p ? p->N : 0, out, h_save,
+                         workspace, act, stream);
+}
+
+}  // extern "C"
+
+static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
+                             int32_t F_in, const float* weight, const float* root, const float* bias,
+                             int32_t F_out, int64_t row_lo, int64_t row_hi, float* out, float* h_save,
+                             void* workspace, int32_t act, void* stream) {
     int32_t st = check_common(p, F_in, F_out);
     if (st != MPGNN_OK) return st;
     Selection s;
@@ -2717,6 +3022,7 @@ int32_t mpgnn_rgcn_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         f.bias = bias;
         f.lo = (int)row_lo;
         f.hi = (int)row_hi;
+        f.relu = act == MPGNN_ACT_RELU;
         TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
         return run_flat(f, strm);
     }
@@ -2743,6 +3049,7 @@ int32_t mpgnn_rgcn_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         f.bias = bias;
         f.lo = (int)row_lo;
         f.hi = (int)row_hi;
+        f.relu = act == MPGNN_ACT_RELU;
         TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
         return run_flat(f, strm);
     }
@@ -2765,9 +3072,22 @@ int32_t mpgnn_rgcn_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         a.ke = s.sel_e;
         a.g.idx_off = s.sel_b;
     }
-    TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
-    return run_rowsum(p, a, p->d.rw_pb, p->d.rw_pe, k_lo, k_hi, reinterpret_cast<float*>(ws + w.prw), strm);
+    {
+        TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
+        st = run_rowsum(p, a, p->d.rw_pb, p->d.rw_pe, k_lo, k_hi, reinterpret_cast<float*>(ws + w.prw), strm);
+        if (st != MPGNN_OK) return st;
+    }
+    if (act == MPGNN_ACT_RELU) {
+        const size_t n = (size_t)p->N * F_out;
+        hipLaunchKernelGGL(relu_kernel, dim3((unsigned)std::min<size_t>((n + kThreads - 1) / kThreads, 4096)),
+                           dim3(kThreads), 0, strm, out, n);
+        return hip_check(hipGetLastError(), "relu_kernel launch");
+    }
+    return MPGNN_OK;
 }
+
+extern "C" {
+
 
 int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
                        int32_t F_in, const float* weight, const float* root, int32_t F_out,

@@ -18,7 +18,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from ._lib import MODE_ALL, MODE_SINGLE, check, lib
+from ._lib import ACT_NONE, ACT_RELU, MODE_ALL, MODE_SINGLE, check, lib
 from .plan import GraphPlan
 
 __all__ = ["rgcn_conv", "segment_means", "MODE_SINGLE", "MODE_ALL"]
@@ -60,7 +60,7 @@ def _workspace(nbytes: int, device: torch.device) -> torch.Tensor:
 
 
 def _forward(x, weight, root, bias, plan: GraphPlan, mode: int, relation: int, num_relations: int,
-             row_lo: int, row_hi: int, group, need_h: bool):
+             row_lo: int, row_hi: int, group, need_h: bool, act: int = ACT_NONE):
     x = _dev(x, "x")
     weight = _dev(weight, "weight")
     root = _dev(root, "root") if root is not None else None
@@ -78,10 +78,15 @@ def _forward(x, weight, root, bias, plan: GraphPlan, mode: int, relation: int, n
     out = torch.empty(N, f_out, dtype=torch.float32, device=x.device)
     # segment means, kept for grad_weight (dW_r = Σ h_segᵀ dout[node_1])
     h_save = torch.empty(seg_e - seg_b, f_in, dtype=torch.float32, device=x.device) if need_h else None
-    check(lib.mpgnn_rgcn_fwd(plan.handle, mode, int(relation), int(num_relations), x.data_ptr(), f_in,
-                             weight.data_ptr(), _ptr(root), _ptr(bias), f_out, row_lo, row_hi,
-                             out.data_ptr(), _ptr(h_save), ws.data_ptr(), _stream(x)),
-          "mpgnn_rgcn_fwd")
+    if act != ACT_NONE:  # fused activation: unsharded layers only (see rgcn_conv)
+        check(lib.mpgnn_rgcn_fwd_act(plan.handle, mode, int(relation), int(num_relations), x.data_ptr(), f_in,
+                                     weight.data_ptr(), _ptr(root), _ptr(bias), f_out, out.data_ptr(),
+                                     _ptr(h_save), ws.data_ptr(), act, _stream(x)), "mpgnn_rgcn_fwd_act")
+    else:
+        check(lib.mpgnn_rgcn_fwd(plan.handle, mode, int(relation), int(num_relations), x.data_ptr(), f_in,
+                                 weight.data_ptr(), _ptr(root), _ptr(bias), f_out, row_lo, row_hi,
+                                 out.data_ptr(), _ptr(h_save), ws.data_ptr(), _stream(x)),
+              "mpgnn_rgcn_fwd")
     if group is not None:
         dist.all_reduce(out, group=group)
     return out, x, weight, root, h_save
@@ -90,21 +95,24 @@ def _forward(x, weight, root, bias, plan: GraphPlan, mode: int, relation: int, n
 class _RGCNConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, root, bias, plan: GraphPlan, mode: int, relation: int,
-                num_relations: int, row_lo: int, row_hi: int, group):
+                num_relations: int, row_lo: int, row_hi: int, group, act: int):
         out, x, weight, root, h_save = _forward(x, weight, root, bias, plan, mode, relation, num_relations,
-                                                row_lo, row_hi, group, ctx.needs_input_grad[1])
+                                                row_lo, row_hi, group, ctx.needs_input_grad[1], act)
         ctx.plan = plan
         ctx.mode, ctx.relation, ctx.num_relations = mode, relation, num_relations
         ctx.rows = (row_lo, row_hi)
         ctx.group = group
         ctx.has_root, ctx.has_bias = root is not None, bias is not None
-        ctx.save_for_backward(x, weight, root, h_save)
+        ctx.act = act
+        ctx.save_for_backward(x, weight, root, h_save, out if act == ACT_RELU else None)
         return out
 
     @staticmethod
     def backward(ctx, grad_out):
-        x, weight, root, h_save = ctx.saved_tensors
+        x, weight, root, h_save, act_out = ctx.saved_tensors
         plan = ctx.plan
+        if ctx.act == ACT_RELU:  # ReLU backward (threshold_backward): pass where the output > 0
+            grad_out = grad_out * (act_out > 0)
         grad_out = grad_out.contiguous()
         if grad_out.data_ptr() % 16:
             grad_out = grad_out.clone()
@@ -125,21 +133,34 @@ class _RGCNConvFn(torch.autograd.Function):
             for g in (gx, gw, gr, gb):
                 if g is not None:
                     dist.all_reduce(g, group=ctx.group)
-        return gx, gw, gr, gb, None, None, None, None, None, None, None
+        return gx, gw, gr, gb, None, None, None, None, None, None, None, None
 
 
 def rgcn_conv(x: torch.Tensor, weight: torch.Tensor, root, bias, plan: GraphPlan, mode: int,
-              relation: int = -1, num_relations: int = 0, row_range=None, group=None) -> torch.Tensor:
-    """One relational conv layer on the GPU (see module docstring)."""
+              relation: int = -1, num_relations: int = 0, row_range=None, group=None,
+              activation=None) -> torch.Tensor:
+    """One relational conv layer on the GPU (see module docstring).
+
+    ``activation='relu'`` returns ``F.relu(layer(x))`` (model.py:144,146): fused into the
+    combine epilogue when the layer is unsharded, applied after the all-reduce otherwise."""
+    if activation not in (None, "relu"):
+        raise ValueError(f"activation must be None or 'relu', got {activation!r}")
     lo, hi = row_range if row_range is not None else (0, plan.num_nodes)
+    fuse = activation == "relu" and group is None and plan.shard == (0, plan.num_nodes) \
+        and (lo, hi) == (0, plan.num_nodes)
+    act = ACT_RELU if fuse else ACT_NONE
     if not torch.is_grad_enabled() or not (x.requires_grad or weight.requires_grad or
                                            (root is not None and root.requires_grad) or
                                            (bias is not None and bias.requires_grad)):
         # inference: no autograd node, no saved means
-        return _forward(x, weight, root, bias, plan, int(mode), int(relation), int(num_relations),
-                        int(lo), int(hi), group, False)[0]
-    return _RGCNConvFn.apply(x, weight, root, bias, plan, int(mode), int(relation),
-                             int(num_relations), int(lo), int(hi), group)
+        out = _forward(x, weight, root, bias, plan, int(mode), int(relation), int(num_relations),
+                       int(lo), int(hi), group, False, act)[0]
+    else:
+        out = _RGCNConvFn.apply(x, weight, root, bias, plan, int(mode), int(relation),
+                                int(num_relations), int(lo), int(hi), group, act)
+    if activation == "relu" and not fuse:
+        out = torch.relu(out)
+    return out
 
 
 def segment_means(x: torch.Tensor, plan: GraphPlan, mode: int, relation: int = -1,

@@ -32,7 +32,8 @@ class Net(torch.nn.Module):
     def forward(self, x, edge_index, edge_type, *, shard=None, group=None):
         for layer_index in range(0, self.metapath_length):
             conv = self.conv1 if layer_index == 0 else self.conv2
-            x = F.relu(conv(x, edge_index, edge_type, shard=shard, group=group))
+            # F.relu(conv(...)) of model.py:144,146, fused into the layer's combine kernel
+            x = conv(x, edge_index, edge_type, shard=shard, group=group, activation="relu")
         x = self.LinearLayer(x)
         return F.log_softmax(x, dim=1)
 

@@ -71,9 +71,11 @@ class RGCNConv(torch.nn.Module):
         glorot(self.root)
         zeros(self.bias)
 
-    def forward(self, x, edge_index, edge_type=None, *, shard=None, group=None):
+    def forward(self, x, edge_index, edge_type=None, *, shard=None, group=None, activation=None):
         """``shard=(lo, hi)`` + ``group``: this rank owns the edges whose gathered node lies in
-        [lo, hi) (dst-range sharding); partial outputs are all-reduced."""
+        [lo, hi) (dst-range sharding); partial outputs are all-reduced.
+        ``activation='relu'`` returns ``F.relu(conv(...))`` (model.py:144,146) with the ReLU
+        fused into the layer's last kernel when unsharded."""
         if isinstance(x, tuple):
             raise NotImplementedError("bipartite (x_l, x_r) input is not supported")
         if x is None or x.dtype == torch.long:
@@ -88,7 +90,8 @@ class RGCNConv(torch.nn.Module):
         plan = get_plan(edge_index, edge_type, x.size(0), flow=self.flow, shard=shard, device=x.device)
         row_range = shard if shard is not None else None
         return rgcn_conv(x, self.weight, self.root, self.bias, plan, MODE_ALL,
-                         num_relations=self.num_relations, row_range=row_range, group=group)
+                         num_relations=self.num_relations, row_range=row_range, group=group,
+                         activation=activation)
 
     def __repr__(self) -> str:
         return (f"{self.__class__.__name__}({self.in_channels}, "

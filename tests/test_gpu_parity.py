@@ -400,3 +400,119 @@ def test_wave_specialised_tile_gemm_matches_oracle(f_in, f_out, mode):
     rel_close(Wg.grad, Ws.grad, what="dW")
     rel_close(rg.grad, rs.grad, what="droot")
     rel_close(bg.grad, bs.grad, what="dbias")
+
+
+# ------------------------------------------------------------------------------------------
+# the fused ReLU
+# ------------------------------------------------------------------------------------------
+def _layer_all_outputs(g, F_out, seed, activation=None):
+    gen = torch.Generator().manual_seed(seed)
+    R, F_in = g.num_relations, g.x.shape[1]
+    W = ((torch.rand(R, F_in, F_out, generator=gen) - 0.5) * 0.2).to(DEV).requires_grad_(True)
+    root = ((torch.rand(F_in, F_out, generator=gen) - 0.5) * 0.2).to(DEV).requires_grad_(True)
+    bias = (torch.rand(F_out, generator=gen) - 0.5).to(DEV).requires_grad_(True)
+    gout = torch.randn(g.num_nodes, F_out, generator=gen).to(DEV)
+    plan = mpgnn_amd.get_plan(g.edge_index, g.edge_type, g.num_nodes)
+    xg = g.x.to(DEV).requires_grad_(True)
+    out = rgcn_conv(xg, W, root, bias, plan, MODE_ALL, num_relations=R, activation=activation)
+    out.backward(gout)
+    h = segment_means(g.x.to(DEV), plan, MODE_ALL, -1, R)
+    torch.cuda.synchronize()
+    return [v.detach().clone() for v in (out, h, xg.grad, W.grad, root.grad, bias.grad)]
+
+
+@pytest.mark.parametrize("cfg", ["C1", "fb15k237"])
+def test_fused_relu_equals_relu_of_layer(cfg):
+    """activation='relu' (fused into the combine epilogue) == F.relu(layer) bit for bit,
+    gradients included (threshold_backward on the fused output)."""
+    g = data.config_graph(cfg)
+    F_out = 64
+    fused = _layer_all_outputs(g, F_out, 7, activation="relu")
+    gen = torch.Generator().manual_seed(7)
+    R, F_in = g.num_relations, g.x.shape[1]
+    W = ((torch.rand(R, F_in, F_out, generator=gen) - 0.5) * 0.2).to(DEV).requires_grad_(True)
+    root = ((torch.rand(F_in, F_out, generator=gen) - 0.5) * 0.2).to(DEV).requires_grad_(True)
+    bias = (torch.rand(F_out, generator=gen) - 0.5).to(DEV).requires_grad_(True)
+    gout = torch.randn(g.num_nodes, F_out, generator=gen).to(DEV)
+    plan = mpgnn_amd.get_plan(g.edge_index, g.edge_type, g.num_nodes)
+    xg = g.x.to(DEV).requires_grad_(True)
+    out = torch.relu(rgcn_conv(xg, W, root, bias, plan, MODE_ALL, num_relations=R))
+    out.backward(gout)
+    torch.cuda.synchronize()
+    for name, a, b in zip(("out", "dx", "dW", "droot", "dbias"),
+                          (fused[0], fused[2], fused[3], fused[4], fused[5]),
+                          (out, xg.grad, W.grad, root.grad, bias.grad)):
+        assert torch.equal(a, b.detach()), (cfg, name)
+    assert bool((fused[0] >= 0).all()) and bool((fused[0] == 0).any())
+
+
+def test_fused_relu_mode_single_and_exact_paths():
+    """The paths without a fused epilogue (mode SINGLE, exact order) apply the ReLU after the
+    combine; Net with the fused activation matches the oracle's F.relu(conv) stack."""
+    from mpgnn_amd import _lib
+    g = data.config_graph("C1")
+    gen = torch.Generator().manual_seed(3)
+    W = ((torch.rand(g.x.shape[1], 32, generator=gen) - 0.5) * 0.2).to(DEV)
+    root = ((torch.rand(g.x.shape[1], 32, generator=gen) - 0.5) * 0.2).to(DEV)
+    bias = (torch.rand(32, generator=gen) - 0.5).to(DEV)
+    plan = mpgnn_amd.get_plan(g.edge_index, g.edge_type, g.num_nodes)
+    xg = g.x.to(DEV)
+    a = rgcn_conv(xg, W, root, bias, plan, MODE_SINGLE, relation=1, activation="relu")
+    b = torch.relu(rgcn_conv(xg, W, root, bias, plan, MODE_SINGLE, relation=1))
+    assert torch.equal(a, b)
+    try:
+        _lib.set_exact_order(True)
+        Wa = W[None].expand(g.num_relations, -1, -1).contiguous()
+        a = rgcn_conv(xg, Wa, root, bias, plan, MODE_ALL, num_relations=g.num_relations, activation="relu")
+        b = torch.relu(rgcn_conv(xg, Wa, root, bias, plan, MODE_ALL, num_relations=g.num_relations))
+        assert torch.equal(a, b)
+    finally:
+        _lib.set_exact_order(False)
+    torch.manual_seed(10)
+    net = mpgnn_amd.Net(g.x.shape[1], 32, g.num_relations, 32, 2, 3)
+    params = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    ref = orc.net_forward(params, g.x, g.edge_index, g.edge_type, 3)
+    out = net.to(DEV)(xg, g.edge_index.to(DEV), g.edge_type.to(DEV))
+    rel_close(out, ref, what="Net")
+
+
+@pytest.mark.parametrize("f_in", [64, 128])
+@pytest.mark.parametrize("mode", [MODE_SINGLE, MODE_ALL])
+def test_rel_gemm_matches_oracle_and_tile_gemm(f_in, mode):
+    """MPGNN_OPT_REL_GEMM (default on: weights held in registers per relation run, 32-row
+    tiles) for F_out = 128: forward and every gradient match the oracle and the tile GEMM."""
+    from mpgnn_amd import _lib
+    f_out = 128
+    g = data.config_graph("fb15k237") if f_in == 128 else \
+        data.synthetic_graph(2000, 9, 30, feat_dim=f_in, seed=5)
+    N, R = g.num_nodes, g.num_relations
+    gen = torch.Generator().manual_seed(f_in + mode)
+    W = (torch.rand((R, f_in, f_out) if mode == MODE_ALL else (f_in, f_out), generator=gen) - 0.5) * 0.2
+    root = (torch.rand(f_in, f_out, generator=gen) - 0.5) * 0.2
+    bias = torch.rand(f_out, generator=gen) - 0.5
+    gout = torch.randn(N, f_out, generator=gen)
+    rel = 2
+    xs = g.x.clone().requires_grad_(True)
+    Ws, rs, bs = W.clone().requires_grad_(True), root.clone().requires_grad_(True), bias.clone().requires_grad_(True)
+    if mode == MODE_ALL:
+        ref = orc.rgcn_forward(xs, g.edge_index, g.edge_type, Ws, rs, bs)
+    else:
+        ref = orc.rgcn_forward(xs, g.edge_index, torch.where(g.edge_type == rel, 0, -1), Ws[None], rs, bs)
+    ref.backward(gout)
+    plan = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, N)
+    res = []
+    try:
+        for on in (1, 0):
+            _lib.lib.mpgnn_set_option(5, on)
+            xg = g.x.to(DEV).requires_grad_(True)
+            Wg, rg, bg = (p.to(DEV).requires_grad_(True) for p in (W, root, bias))
+            out = rgcn_conv(xg, Wg, rg, bg, plan, mode, relation=rel, num_relations=R)
+            out.backward(gout.to(DEV))
+            torch.cuda.synchronize()
+            res.append([t_.detach().cpu() for t_ in (out, xg.grad, Wg.grad, rg.grad, bg.grad)])
+    finally:
+        _lib.lib.mpgnn_set_option(5, 1)
+    for name, a, b, r in zip(("out", "dx", "dW", "droot", "dbias"), res[0], res[1],
+                             (ref, xs.grad, Ws.grad, rs.grad, bs.grad)):
+        rel_close(a, r, what=name)
+        rel_close(a, b, what=name + " rel_gemm vs tile_gemm")
