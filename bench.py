@@ -15,7 +15,7 @@ all-reduce over xGMI: total work is fixed, so "scaling" is "strong".
 Also reported (separate loops, outside the timed step): the training epoch of
 main_rgcn.py:458-461 — train step (forward + NLL + backward + Adam) + validation forward.
 
-roofline: the dominant kernel (tile_gemm_kernel, forward) timed live with HIP events on its
+roofline: the dominant kernel (rel_gemm_kernel, forward) timed live with HIP events on its
 launch stream over the timed region; algorithmic FLOPs = 2·(S + N)·F_in·F_out per launch
 (segment rows H @ W_r plus node rows x @ root, both computed by that launch) against the
 dense fp32 MFMA peak (157.3 TFLOP/s); algorithmic bytes (A rows in, Y rows out, weights)
@@ -234,7 +234,7 @@ def main():
     roofline = {
         "bound": "mfma", "achieved": round(achieved_tf, 3) if achieved_tf else None, "peak": PEAK_FP32_MFMA,
         "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_MFMA, 4) if achieved_tf else None,
-        "traffic": traffic, "kernel": "tile_gemm_kernel (Y = H @ W_r, Y_root = x @ root; v_mfma_f32_32x32x2_f32)",
+        "traffic": traffic, "kernel": "rel_gemm_kernel (Y = H @ W_r, Y_root = x @ root; W_r slice held in registers; v_mfma_f32_32x32x2_f32)",
         "avg_launch_us": round(seg_avg_ms * 1e3, 2), "launches": seg_n,
         "alg_flops_per_launch": flops, "alg_bytes_per_launch": alg_bytes,
         "alg_GBps": round(alg_bytes / (seg_avg_ms * 1e-3) / 1e9, 1) if seg_n else None,

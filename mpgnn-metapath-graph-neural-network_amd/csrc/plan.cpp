@@ -381,6 +381,7 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
     // ---- relation-pure tiles and reduction chunks --------------------------------------
     p->rel_tile_ptr.assign(R + 1, 0);
     p->rel_t32_ptr.assign(R + 1, 0);
+    p->t32_cost.assign(1, 0);
     p->rel_chunk_ptr.assign(R + 1, 0);
     for (int64_t d = 0; d < R; ++d) {
         for (int32_t s = p->rel_seg_ptr[d]; s < p->rel_seg_ptr[d + 1]; s += kTile32) {
@@ -388,6 +389,10 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
             p->t32_end.push_back(std::min<int32_t>(s + kTile32, p->rel_seg_ptr[d + 1]));
         }
         p->rel_t32_ptr[d + 1] = (int32_t)p->t32_begin.size();
+        for (size_t t = p->t32_cost.size() - 1; t < p->t32_begin.size(); ++t) {
+            const int64_t e = p->s_ptr[p->t32_end[t]] - p->s_ptr[p->t32_begin[t]];
+            p->t32_cost.push_back(p->t32_cost.back() + item_cost(e));
+        }
         for (int32_t s = p->rel_seg_ptr[d]; s < p->rel_seg_ptr[d + 1]; s += kTileRows) {
             p->tile_begin.push_back(s);
             p->tile_end.push_back(std::min<int32_t>(s + kTileRows, p->rel_seg_ptr[d + 1]));
@@ -580,6 +585,7 @@ int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
         {&p->d.ta_col, &p->ta_col},     {&p->d.ta_seg, &p->ta_seg},
         {&p->d.tile_begin, &p->tile_begin}, {&p->d.tile_end, &p->tile_end},
         {&p->d.t32_begin, &p->t32_begin}, {&p->d.t32_end, &p->t32_end},
+        {&p->d.t32_cost, &p->t32_cost},
         {&p->d.chunk_begin, &p->chunk_begin}, {&p->d.chunk_end, &p->chunk_end},
         {&p->d.rel_chunk_ptr, &p->rel_chunk_ptr}, {&p->d.rel_val32, &p->rel_val32},
         {&p->d.chunk_dst, &p->chunk_dst},

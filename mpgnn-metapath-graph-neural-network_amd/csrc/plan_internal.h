@@ -16,6 +16,14 @@ constexpr int kTileRows = 64;
 // 32-row relation-pure tiles of the B-stationary GEMM (rel_gemm_kernel): the work unit one
 // wave-quad turns into 32 output rows while W_r stays in registers.
 constexpr int kTile32 = 32;
+// Cost model of one item of the fused mean + transform kernel, in units of 64 shader cycles:
+// the MFMA strip takes 64 units; gathering an edge's 512-B row costs ≈ 23 cycles per CU.  Items
+// are split over workgroups by prefix cost (fused_mean_gemm_kernel).
+constexpr int kRootItemCost = 64;
+inline int32_t item_cost(int64_t edges) {
+    const int64_t g = (23 * edges + 1000) / 64;
+    return (int32_t)(g > 64 ? g : 64);
+}
 // Relation-pure reduction chunks for the weight gradient (outer_accum_kernel): at most this
 // many segments, balanced within a relation (bounds the longest workgroup's MFMA chain).
 constexpr int kChunkRows = 128;
@@ -75,6 +83,7 @@ struct DeviceTables {
     int32_t* tile_end = nullptr;    // [num_tiles] one past the last segment
     int32_t* t32_begin = nullptr;   // [num_tiles32] first segment of a 32-row tile
     int32_t* t32_end = nullptr;     // [num_tiles32] one past its last segment
+    int32_t* t32_cost = nullptr;    // [num_tiles32 + 1] prefix of fused-kernel item costs
     int32_t* chunk_begin = nullptr; // [num_chunks]
     int32_t* chunk_end = nullptr;   // [num_chunks]
     int32_t* rel_chunk_ptr = nullptr; // [nrel+1]
@@ -121,6 +130,7 @@ struct mpgnn_plan {
     std::vector<int32_t> ta_col, ta_seg;       // [E]
     std::vector<int32_t> tile_begin, tile_end; // [num_tiles]
     std::vector<int32_t> t32_begin, t32_end;   // [num_tiles32]
+    std::vector<int32_t> t32_cost;             // [num_tiles32 + 1] prefix sum of item_cost()
     std::vector<int32_t> chunk_begin, chunk_end; // [num_chunks]
     std::vector<int32_t> rel_val32;            // [nrel]
     std::vector<int32_t> chunk_dst;            // [num_chunks] see DeviceTables::chunk_dst

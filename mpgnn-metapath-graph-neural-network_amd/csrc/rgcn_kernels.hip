@@ -1084,6 +1084,35 @@ struct RelGemm {
         return it;
     }
 
+    // Descriptors of the workgroup's items i_beg + lane (lanes < 64), fetched once with vector
+    // loads; per item they are read back with readlane (no dependent scalar loads in the loop).
+    struct ItemTable {
+        int r0, nrows, wrel;  // wrel: weight index (relation id), -1 = root weight
+    };
+    __device__ static __forceinline__ ItemTable item_table(const RelGemmArgs& a, int i_beg, int i_end, int lane) {
+        ItemTable t;
+        const int i = min(i_beg + lane, i_end - 1);
+        if (i < a.n_rel) {
+            t.r0 = a.t_begin[a.t_lo + i];
+            t.nrows = a.t_end[a.t_lo + i] - t.r0;
+            t.wrel = a.w_per_rel ? a.s_rel[t.r0] : 0;
+        } else {
+            t.r0 = a.row_lo + (i - a.n_rel) * 32;
+            t.nrows = min(32, a.row_hi - t.r0);
+            t.wrel = -1;
+        }
+        return t;
+    }
+    __device__ static __forceinline__ Item item_at(const RelGemmArgs& a, const ItemTable& t, int k) {
+        Item it;
+        it.r0 = readlane(t.r0, k);
+        it.nrows = readlane(t.nrows, k);
+        const int wr = readlane(t.wrel, k);
+        it.root = wr < 0;
+        it.w = it.root ? a.Wroot : a.W + (size_t)wr * K * N;
+        return it;
+    }
+
     // A rows of an item into registers (clamped rows; zeroed at commit) + the dgrad row scale.
     __device__ static __forceinline__ void issue(const RelGemmArgs& a, const Item& it, int tid, float4 (&v)[WPT],
                                                  int& cnt) {
@@ -1150,19 +1179,31 @@ struct RelGemm {
         const int lane = tid & 63, c = lane & 31, h = lane >> 5;
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         const int n_items = a.n_rel + a.n_root;
+        // range index: workgroups b, b + 8, b + 16, … (one XCD under round-robin placement, a
+        // speed-only assumption) take consecutive item ranges, so a relation run split over
+        // several workgroups has its weight slice served from one XCD's L2
         const int G = (int)gridDim.x;
-        const int i_beg = (int)((long long)blockIdx.x * n_items / G);
-        const int i_end = (int)((long long)(blockIdx.x + 1) * n_items / G);
+        const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
+        const int rng = g * q + min(g, rem) + ((int)blockIdx.x >> 3);
+        const int i_beg = (int)((long long)rng * n_items / G);
+        const int i_end = (int)((long long)(rng + 1) * n_items / G);
         if (i_beg >= i_end) return;
         unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 32 : nullptr;
         auto stamp = [&](int k) {
-            if (stp != nullptr && tid == 0 && k < 32) stp[k] = stamp_now();
+            if (stp != nullptr && tid == 0 && k < 30) stp[k] = stamp_now();
         };
+        auto stamp_rt = [&](int k) {  // s_memrealtime (100 MHz, chip-wide)
+            if (stp != nullptr && tid == 0) stp[k] = __builtin_amdgcn_s_memrealtime();
+        };
+        stamp_rt(30);
         stamp(0);
 
         float4 v[WPT];
         int cnt;
-        Item cur = item(a, i_beg);
+        // up to 64 items per workgroup through the register table, the rest by scalar loads
+        const ItemTable tab = item_table(a, i_beg, i_end, lane);
+        auto get_item = [&](int i) { return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i); };
+        Item cur = get_item(i_beg);
         issue(a, cur, tid, v, cnt);
         float b[KH];
         load_b(cur.w, wave, lane, b);
@@ -1172,7 +1213,7 @@ struct RelGemm {
         int buf = 0;
         for (int i = i_beg; i < i_end; ++i) {
             const bool has_next = i + 1 < i_end;
-            const Item nxt = has_next ? item(a, i + 1) : cur;
+            const Item nxt = has_next ? get_item(i + 1) : cur;
             if (has_next) issue(a, nxt, tid, v, cnt);      // in flight during this item's MFMAs
             const bool new_w = nxt.w != cur.w;
             float bn[KH];
@@ -1216,6 +1257,7 @@ struct RelGemm {
             cur = nxt;
             buf ^= 1;
         }
+        stamp_rt(31);
     }
 };
 
@@ -1223,6 +1265,362 @@ template <int KB, bool DGRAD>
 __global__ __launch_bounds__(kThreads, 2) void rel_gemm_kernel(RelGemmArgs a) {
     extern __shared__ float smem[];
     RelGemm<KB, DGRAD>::run(a, smem);
+}
+
+
+// ----------------------------------------------------------------------------------------
+// fused_mean_gemm_kernel — the forward layer core for F_in = F_out = 128 in one persistent
+// launch (one 512-thread workgroup per CU): the relation-typed segment means (PyG propagate,
+// mp_rgcn_layer.py:236) are formed in LDS and contracted with W_r on the matrix cores
+// (mp_rgcn_layer.py:245 / the RGCNConv loop), without a round trip of H through memory.
+//
+//   waves 4-7 ("gather"):  build item i+1's A tile in LDS buffer (i+1)%2 — for a relation tile,
+//       the means of its ≤ 32 segments: x rows of the edges (e_col, relation-major edge order)
+//       gathered 32 in flight per wave (one 512-B row per load instruction, readlane-broadcast
+//       addresses), each segment summed in edge order from 0.0f and divided by its GLOBAL count
+//       (IEEE); for a root tile, 32 rows of x.  The tile's edges are cut into four ranges of
+//       equal edge count, moved to segment starts unless the segment is longer than kSplitMax:
+//       segments up to kSplitMax edges are summed by one wave in the reference's exact order
+//       (bit-identical means); a longer one is summed as per-wave partials that the last wave
+//       to finish adds in edge order (LDS arrival counter).  Means are also written to H when
+//       the caller keeps them for the backward.
+//   waves 0-3 ("matrix"):  contract item i from LDS buffer i%2 with the relation's weight slice
+//       held in registers (wave w: columns [32w, 32w+32), as rel_gemm_kernel), prefetch the next
+//       relation run's slice, store the 32 output rows straight from the accumulators.
+// One barrier per item.  Items are 32-row relation-pure tiles (plan t32 tables) followed by
+// 32-node root tiles; workgroups take contiguous item ranges of equal prefix cost
+// (plan t32_cost, item_cost in plan_internal.h), consecutive ranges on one XCD.
+// ----------------------------------------------------------------------------------------
+struct FusedArgs {
+    const int* t_begin;
+    const int* t_end;
+    const int* t_cost;    // prefix cost per 32-row tile
+    int t_lo, n_rel, n_root;
+    const int* s_ptr;
+    const int* e_col;
+    const int* s_cnt;
+    const int* s_rel;
+    const float* x;
+    const float* W;
+    int w_per_rel;
+    const float* Wroot;
+    float* Y;
+    float* Yroot;
+    float* H;             // nullable: segment means [S_sel, 128] for the backward
+    int sel_b, row_lo, row_hi;
+    unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][64] timeline, or nullptr
+};
+
+constexpr int kFusedThreads = 512;
+constexpr int kFusedLda = 128 + 4;
+constexpr int kSplitMax = 64;
+
+__device__ __forceinline__ int fused_cum(const FusedArgs& a, int i, int relsum) {
+    return i <= a.n_rel ? a.t_cost[a.t_lo + i] - a.t_cost[a.t_lo] : relsum + (i - a.n_rel) * kRootItemCost;
+}
+
+// smallest item index i with cum(i) >= target (cum is strictly increasing, cum(0) = 0)
+__device__ int fused_find(const FusedArgs& a, long long target, int relsum, int lane) {
+    if (target <= 0) return 0;
+    int lo = 0, hi = a.n_rel + a.n_root;
+    while (hi - lo > 1) {
+        const int span = hi - lo;
+        const int idx = min(hi, lo + (int)(((long long)(lane + 1) * span + 63) / 64));
+        const unsigned long long m = __ballot(fused_cum(a, idx, relsum) >= target);
+        const int f = __ffsll((long long)m) - 1;  // lane 63 samples hi: always set
+        const int nlo = f > 0 ? readlane(idx, f - 1) : lo;
+        hi = readlane(idx, f);
+        lo = nlo;
+    }
+    return hi;
+}
+
+struct FusedItem {
+    int r0, nrows, root;
+    const float* w;
+};
+
+__device__ __forceinline__ FusedItem fused_item(const FusedArgs& a, int i) {
+    FusedItem it;
+    it.root = i >= a.n_rel;
+    if (!it.root) {
+        it.r0 = ld_uniform(a.t_begin, a.t_lo + i);
+        it.nrows = ld_uniform(a.t_end, a.t_lo + i) - it.r0;
+        it.w = a.W + (a.w_per_rel ? (size_t)ld_uniform(a.s_rel, it.r0) * 128 * 128 : 0);
+    } else {
+        it.r0 = a.row_lo + (i - a.n_rel) * 32;
+        it.nrows = min(32, a.row_hi - it.r0);
+        it.w = a.Wroot;
+    }
+    return it;
+}
+
+// Gather waves run a two-item software pipeline: while item i+1's rows are gathered, item
+// i+2's segment table (s_ptr, s_cnt) is in flight, and once it lands the wave's edge range of
+// item i+2 is cut and its first 32 e_col entries are requested — so an item's gather starts with
+// its indices in registers and pays one memory round trip for its x rows.
+struct GatherStage {
+    int sp;     // lane l <= n: s_ptr[s0 + l] (lane n: end of the tile's edges)
+    int cntv;   // lane l < n: GLOBAL count of segment s0 + l
+    int pb, pe; // this wave's edge range
+    int col;    // e_col[pb + lane] (first 32 positions of the range)
+};
+
+__device__ __forceinline__ void gather_meta(const FusedArgs& a, const FusedItem& it, int lane, GatherStage& g) {
+    if (it.root) return;
+    g.sp = a.s_ptr[it.r0 + min(lane, it.nrows)];
+    g.cntv = a.s_cnt[it.r0 + min(lane, it.nrows - 1)];
+}
+
+// segment containing position p of a staged item (e0 <= p < e1)
+__device__ __forceinline__ int stage_seg(const GatherStage& g, int n, int p, int lane) {
+    return __popcll(__ballot(lane < n && g.sp <= p)) - 1;
+}
+
+// Cut the tile's edges into four ranges of equal edge count, moved to a segment start unless
+// that segment is longer than kSplitMax; then request the wave's first 32 e_col entries.
+__device__ __forceinline__ void gather_range(const FusedArgs& a, const FusedItem& it, int gw, int lane,
+                                             GatherStage& g) {
+    if (it.root) return;
+    const int n = it.nrows;
+    const int e0 = readlane(g.sp, 0), e1 = readlane(g.sp, n);
+    const int T = e1 - e0;
+    int cut_prev = e0;
+    g.pb = e0;
+    g.pe = e1;
+#pragma unroll
+    for (int k = 1; k <= 3; ++k) {
+        int c = e0 + (int)(((long long)T * k) / 4);
+        if (c < e1) {
+            const int m = stage_seg(g, n, c, lane);
+            const int st = readlane(g.sp, m);
+            if (readlane(g.sp, m + 1) - st <= kSplitMax) c = st;
+        }
+        c = max(c, cut_prev);
+        if (k == gw) g.pb = c;
+        if (k == gw + 1) g.pe = c;
+        cut_prev = c;
+    }
+    g.col = a.e_col[max(min(g.pb + lane, g.pe - 1), 0)];
+}
+
+// Sum the staged item into its A tile (see the kernel comment).
+__device__ void gather_sum(const FusedArgs& a, const FusedItem& it, const GatherStage& g, float* A, float* slot,
+                           int* slot_seg, int* ctr, int gw, int lane, unsigned long long* st) {
+    auto stamp = [&](int k) {
+        if (st != nullptr && gw == 0 && lane == 0) st[k] = stamp_now();
+    };
+    const int c2 = 2 * lane;
+    if (it.root) {
+        float2 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int row = gw + 4 * j;
+            v[j] = *reinterpret_cast<const float2*>(a.x + (size_t)(it.r0 + min(row, it.nrows - 1)) * 128 + c2);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int row = gw + 4 * j;
+            *reinterpret_cast<float2*>(A + row * kFusedLda + c2) = row < it.nrows ? v[j] : make_float2(0.f, 0.f);
+        }
+        return;
+    }
+    stamp(0);
+    const int n = it.nrows, s0 = it.r0;
+    for (int row = n + gw; row < 32; row += 4)
+        *reinterpret_cast<float2*>(A + row * kFusedLda + c2) = make_float2(0.f, 0.f);
+    if (lane == 0) {
+        slot_seg[2 * gw] = -1;
+        slot_seg[2 * gw + 1] = -1;
+    }
+    auto finish = [&](int t, float2 sum) {  // complete segment t: mean -> A row (and H)
+        const float d = (float)readlane(g.cntv, t);
+        const float2 mean = make_float2(sum.x / d, sum.y / d);
+        *reinterpret_cast<float2*>(A + t * kFusedLda + c2) = mean;
+        if (a.H != nullptr) *reinterpret_cast<float2*>(a.H + (size_t)(s0 + t - a.sel_b) * 128 + c2) = mean;
+    };
+    const int pb = g.pb, pe = g.pe;
+    if (pb < pe) {
+        int t = stage_seg(g, n, pb, lane);
+        int se = readlane(g.sp, t + 1);
+        bool head = readlane(g.sp, t) < pb;  // segment started in an earlier wave's range
+        const int tc0 = head ? t + 1 : t;    // first segment this wave completes
+        float2 acc = make_float2(0.f, 0.f);
+        constexpr int U = 32;
+        for (int p0 = pb; p0 < pe; p0 += U) {
+            const int cnt = min(U, pe - p0);
+            const int col = p0 == pb ? g.col : a.e_col[p0 + min(lane, cnt - 1)];
+            float2 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int r = readlane(col, min(u, cnt - 1));
+                v[u] = *reinterpret_cast<const float2*>(a.x + (size_t)r * 128 + c2);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (u < cnt) {
+                    acc.x += v[u].x;
+                    acc.y += v[u].y;
+                    if (p0 + u + 1 == se) {  // segment t ends here: its sum -> A row, or head slot
+                        float* dst = head ? slot + (2 * gw) * 128 : A + t * kFusedLda;
+                        *reinterpret_cast<float2*>(dst + c2) = acc;
+                        if (head && lane == 0) slot_seg[2 * gw] = t;
+                        head = false;
+                        acc = make_float2(0.f, 0.f);
+                        ++t;
+                        se = t < n ? readlane(g.sp, t + 1) : 0x7fffffff;
+                    }
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (t < n && readlane(g.sp, t) < pe && pe < se) {  // segment t continues past the range: partial
+            const int j = head ? 0 : 1;
+            *reinterpret_cast<float2*>(slot + (2 * gw + j) * 128 + c2) = acc;
+            if (lane == 0) slot_seg[2 * gw + j] = t;
+        }
+        stamp(1);
+        // divide the segments completed here (sums were parked in their A rows)
+        for (int tt = tc0; tt < t; ++tt) finish(tt, *reinterpret_cast<const float2*>(A + tt * kFusedLda + c2));
+    }
+    // last gather wave to arrive adds the partials of split segments in edge order (LDS writes
+    // drained first; no vmcnt wait, so the next item's prefetches stay in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int old = 0;
+    if (lane == 0) old = atomicAdd(ctr, 1);
+    old = readlane(old, 0);
+    if ((old & 3) == 3) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        int cur = -1;
+        float2 acc = make_float2(0.f, 0.f);
+        for (int k = 0; k < 8; ++k) {
+            const int sg = slot_seg[k];
+            if (sg < 0) continue;
+            const float2 v = *reinterpret_cast<const float2*>(slot + k * 128 + c2);
+            if (sg == cur) {
+                acc.x += v.x;
+                acc.y += v.y;
+            } else {
+                if (cur >= 0) finish(cur, acc);
+                cur = sg;
+                acc = v;
+            }
+        }
+        if (cur >= 0) finish(cur, acc);
+    }
+    stamp(2);
+}
+
+// Workgroup barrier that retires LDS traffic only: global loads in flight (prefetched indices,
+// the next relation's weight slice) and stores stay outstanding across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__global__ __launch_bounds__(kFusedThreads, 1) void fused_mean_gemm_kernel(FusedArgs a) {
+    __shared__ float As[2 * 32 * kFusedLda];
+    __shared__ float slot[8 * 128];
+    __shared__ int slot_seg[8];
+    __shared__ int ctr;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, c = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool matrix = wave < 4;
+    const int gw = wave - 4;
+    const int n_items = a.n_rel + a.n_root;
+    // contiguous item range of equal prefix cost; ranges b, b+8, … on one XCD (speed only)
+    const int G = (int)gridDim.x;
+    const int g8 = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
+    const int rng = g8 * q + min(g8, rem) + ((int)blockIdx.x >> 3);
+    const int relsum = a.t_cost[a.t_lo + a.n_rel] - a.t_cost[a.t_lo];
+    const long long total = (long long)relsum + (long long)a.n_root * kRootItemCost;
+    unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 64 : nullptr;
+    auto stamp = [&](int k) {
+        if (stp != nullptr && lane == 0 && wave == 0 && k < 62) stp[k] = stamp_now();
+    };
+    if (stp != nullptr && tid == 0) stp[62] = __builtin_amdgcn_s_memrealtime();
+    stamp(0);
+    const int i_beg = fused_find(a, total * rng / G, relsum, lane);
+    const int i_end = fused_find(a, total * (rng + 1) / G, relsum, lane);
+    if (i_beg >= i_end || n_items == 0) return;
+    stamp(1);
+    if (tid == 0) ctr = 0;
+    __syncthreads();
+
+    constexpr int KH = 64;
+    float b[KH];
+    FusedItem cur = fused_item(a, i_beg);
+    GatherStage nx{};  // staged item i+1 (gather waves)
+    if (matrix) {
+        const float* p = cur.w + (size_t)(h * KH) * 128 + wave * 32 + c;
+#pragma unroll
+        for (int j = 0; j < KH; ++j) b[j] = p[j * 128];
+    } else {
+        GatherStage g0{};
+        gather_meta(a, cur, lane, g0);
+        gather_range(a, cur, gw, lane, g0);
+        if (i_beg + 1 < i_end) gather_meta(a, fused_item(a, i_beg + 1), lane, nx);
+        gather_sum(a, cur, g0, As, slot, slot_seg, &ctr, gw, lane, nullptr);
+        if (i_beg + 1 < i_end) gather_range(a, fused_item(a, i_beg + 1), gw, lane, nx);
+    }
+    lds_barrier();
+    stamp(2);
+    int buf = 0;
+    for (int i = i_beg; i < i_end; ++i) {
+        const bool has_next = i + 1 < i_end;
+        const FusedItem nxt = has_next ? fused_item(a, i + 1) : cur;
+        if (matrix) {
+            const bool new_w = nxt.w != cur.w;
+            float bn[KH];
+            if (new_w) {
+                const float* p = nxt.w + (size_t)(h * KH) * 128 + wave * 32 + c;
+#pragma unroll
+                for (int j = 0; j < KH; ++j) bn[j] = p[j * 128];
+            }
+            const float* Ab = As + buf * 32 * kFusedLda + c * kFusedLda + h * KH;
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+            float4 af = *reinterpret_cast<const float4*>(Ab);
+#pragma unroll
+            for (int j = 0; j < KH; j += 4) {
+                const float4 cf = af;
+                if (j + 4 < KH) af = *reinterpret_cast<const float4*>(Ab + j + 4);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], acc, 0, 0, 0);
+            }
+            float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * 128 : a.Y + (size_t)(cur.r0 - a.sel_b) * 128;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row < cur.nrows) Yt[(size_t)row * 128 + wave * 32 + c] = acc[r];
+            }
+            stamp(3 + 5 * (i - i_beg));
+            if (new_w) {
+#pragma unroll
+                for (int j = 0; j < KH; ++j) b[j] = bn[j];
+            }
+        } else if (has_next) {
+            const bool has_next2 = i + 2 < i_end;
+            GatherStage nn{};
+            const FusedItem it2 = has_next2 ? fused_item(a, i + 2) : nxt;
+            if (has_next2) gather_meta(a, it2, lane, nn);
+            gather_sum(a, nxt, nx, As + (buf ^ 1) * 32 * kFusedLda, slot, slot_seg, &ctr, gw, lane,
+                       (stp != nullptr && 7 + 5 * (i - i_beg) < 62) ? stp + 4 + 5 * (i - i_beg) : nullptr);
+            if (has_next2) gather_range(a, it2, gw, lane, nn);
+            nx = nn;
+        }
+        lds_barrier();
+        stamp(7 + 5 * (i - i_beg));
+        cur = nxt;
+        buf ^= 1;
+    }
+    if (stp != nullptr && tid == 0) stp[63] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ----------------------------------------------------------------------------------------
@@ -2309,6 +2707,7 @@ static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
 
 
 static bool g_rel_gemm = true;  // MPGNN_OPT_REL_GEMM: B-stationary GEMM for K ∈ {64, 128}, N = 128
+static bool g_fused = false;    // MPGNN_OPT_FUSED: fused means + transform for F_in = F_out = 128 (opt-in: latency-bound today)
 
 template <int KB, bool DGRAD>
 static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
@@ -2876,6 +3275,10 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
         g_ablate = (int)value;
         return MPGNN_OK;
     }
+    if (option == MPGNN_OPT_FUSED) {
+        g_fused = value != 0;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_REL_GEMM) {
         g_rel_gemm = value != 0;
         return MPGNN_OK;
@@ -2971,17 +3374,50 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     float* Yroot = root ? reinterpret_cast<float*>(ws + w.yroot) : nullptr;
     const bool exact = g_exact_order;
 
-    // 1) H[seg] = mean(x over seg)  (the saved means when training)
-    float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
-    {
-        TimedLaunch tl(MPGNN_K_MEAN, strm);
-        st = run_means(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
+    if (!exact && g_fused && F_in == 128 && F_out == 128 && g_ablate == 0) {
+        // 1+2) fused: segment means formed in LDS and contracted on the matrix cores in one launch
+        FusedArgs f{};
+        f.t_begin = p->d.t32_begin;
+        f.t_end = p->d.t32_end;
+        f.t_cost = p->d.t32_cost;
+        f.t_lo = s.t32_lo;
+        f.n_rel = s.t32_hi - s.t32_lo;
+        f.n_root = root ? (int)((row_hi - row_lo + 31) / 32) : 0;
+        f.s_ptr = p->d.s_ptr;
+        f.e_col = p->d.e_col;
+        f.s_cnt = p->d.s_cnt;
+        f.s_rel = p->d.s_rel;
+        f.x = x;
+        f.W = weight;
+        f.w_per_rel = (mode == MPGNN_MODE_ALL);
+        f.Wroot = root;
+        f.Y = Y;
+        f.Yroot = Yroot;
+        f.H = h_save;
+        f.sel_b = s.sel_b;
+        f.row_lo = (int)row_lo;
+        f.row_hi = (int)row_hi;
+        f.stamps = g_stamps;
+        if (f.n_rel + f.n_root > 0) {
+            TimedLaunch tl(MPGNN_K_SEG_FWD, strm);
+            const int grid = std::min(f.n_rel + f.n_root, cu_count());
+            hipLaunchKernelGGL(fused_mean_gemm_kernel, dim3(grid), dim3(kFusedThreads), 0, strm, f);
+            st = hip_check(hipGetLastError(), "fused_mean_gemm_kernel launch");
+            if (st != MPGNN_OK) return st;
+        }
+    } else {
+        // 1) H[seg] = mean(x over seg)  (the saved means when training)
+        float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
+        {
+            TimedLaunch tl(MPGNN_K_MEAN, strm);
+            st = run_means(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
+            if (st != MPGNN_OK) return st;
+        }
+        // 2) Y[seg] = H[seg] @ W_rel(seg); Yroot[i] = x[i] @ root   (MFMA tiles)
+        st = run_seg(p, mode, s, 2, x, F_in, weight, root, 0, F_out, Y, Yroot, row_lo, row_hi, nullptr, nullptr, true,
+                     MPGNN_K_SEG_FWD, strm, H);
         if (st != MPGNN_OK) return st;
     }
-    // 2) Y[seg] = H[seg] @ W_rel(seg); Yroot[i] = x[i] @ root   (MFMA tiles)
-    st = run_seg(p, mode, s, 2, x, F_in, weight, root, 0, F_out, Y, Yroot, row_lo, row_hi, nullptr, nullptr, true,
-                 MPGNN_K_SEG_FWD, strm, H);
-    if (st != MPGNN_OK) return st;
 
     // 2) out[i] = (Σ_{seg of row i, relation order} Y[seg] + Yroot[i]) + bias
     RowSumArgs a{};

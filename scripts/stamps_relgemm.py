@@ -29,11 +29,9 @@ _lib.lib.mpgnn_set_option(2, 0)
 st = buf[: 512 * 32].cpu().numpy().reshape(512, 32).astype(np.float64)
 live = st[:, 0] > 0
 st = st[live]
-t0 = st[:, 0].min()
 res = {"wgs": int(live.sum())}
-start = st[:, 0] - t0
 pro = st[:, 1] - st[:, 0]
-mf, ep, end = [], [], []
+mf, ep = [], []
 for row in st:
     k = 0
     prev = row[1]
@@ -42,8 +40,17 @@ for row in st:
         ep.append(row[3 + 2 * k] - row[2 + 2 * k])
         prev = row[3 + 2 * k]
         k += 1
-    end.append(prev - t0)
-for name, a in [("start", start), ("prologue", pro), ("mfma_item", mf), ("epi_commit_barrier", ep), ("end", end)]:
+rt0 = st[:, 30].min()
+rt_start = (st[:, 30] - rt0) * 10.0  # ns (100 MHz)
+rt_end = (st[:, 31] - rt0) * 10.0
+clk = (st[:, 2 * 0 + 0] * 0)  # placeholder
+span_clk = np.array([max(r[k] for k in range(30) if r[k] > 0) - r[0] for r in st])
+ghz = span_clk / np.maximum(rt_end - rt_start, 1.0)
+res["clock_GHz_p50"] = float(np.median(ghz))
+for name, a in [("rt_start_ns", rt_start), ("rt_end_ns", rt_end), ("rt_span_ns", rt_end - rt_start)]:
+    res[name] = {"p10": float(np.percentile(a, 10)), "p50": float(np.median(a)), "p90": float(np.percentile(a, 90)),
+                 "max": float(a.max())}
+for name, a in [("prologue", pro), ("mfma_item", mf), ("epi_commit_barrier", ep)]:
     a = np.asarray(a)
     res[name] = {"p10": float(np.percentile(a, 10)), "p50": float(np.median(a)), "p90": float(np.percentile(a, 90)),
                  "max": float(a.max()), "n": len(a)}
