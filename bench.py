@@ -16,7 +16,8 @@ Also reported (separate loops, outside the timed step): the training epoch of
 main_rgcn.py:458-461 — train step (forward + NLL + backward + Adam) + validation forward.
 
 roofline: the dominant kernel (rel_gemm_kernel, forward) timed live with HIP events on its
-launch stream over the timed region; algorithmic FLOPs = 2·(S + N)·F_in·F_out per launch
+launch stream over a second pass of the same K steps (events between kernels drain the queue,
+so they are kept out of the headline's timed region); algorithmic FLOPs = 2·(S + N)·F_in·F_out per launch
 (segment rows H @ W_r plus node rows x @ root, both computed by that launch) against the
 dense fp32 MFMA peak (157.3 TFLOP/s); algorithmic bytes (A rows in, Y rows out, weights)
 reported beside it.  traffic: HBM bytes per launch from rocprofv3 PMC counters
@@ -135,9 +136,6 @@ def main():
     plan = mpgnn_amd.get_plan(ei, et, g.num_nodes, shard=shard, device=dev)
 
     # ---- timed region: K forward steps --------------------------------------------------
-    _lib.lib.mpgnn_timing_reset()
-    _lib.lib.mpgnn_set_option(3, 1 << _lib.KERNEL_KINDS["seg_fwd"])  # time only the roofline kernel
-    _lib.lib.mpgnn_timing_enable(1)
     if group is not None:
         dist.barrier(group=group)
     torch.cuda.synchronize()
@@ -149,7 +147,20 @@ def main():
     if group is not None:
         dist.barrier(group=group)
     elapsed = time.perf_counter() - t0
+
+    # ---- roofline pass: the same K steps again with the dominant kernel bracketed by HIP
+    # events on its launch stream (C-ABI timing hook).  Kept out of the timed region: an event
+    # between two kernels drains the queue (~4 us per event pair on this stack), which would
+    # charge the headline number for the measurement itself.
+    _lib.lib.mpgnn_timing_reset()
+    _lib.lib.mpgnn_set_option(3, 1 << _lib.KERNEL_KINDS["seg_fwd"])  # time only the roofline kernel
+    _lib.lib.mpgnn_timing_enable(1)
+    with torch.no_grad():
+        for _ in range(args.steps):
+            step()
+    torch.cuda.synchronize()
     _lib.lib.mpgnn_timing_enable(0)
+    _lib.lib.mpgnn_set_option(3, -1)
     seg_ms, seg_n = _lib.kernel_timing("seg_fwd")
     row_ms, row_n = _lib.kernel_timing("row_fwd")
     if group is not None:
@@ -227,7 +238,8 @@ def main():
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
-            if pmc.get("workload") == "fb15k237" and pmc.get("feat") == F and world == 1:
+            if pmc.get("workload") == "fb15k237" and pmc.get("feat") == F and world == 1 and \
+                    pmc.get("kernel", "").startswith("mpgnn::rel_gemm_kernel"):
                 traffic = pmc.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None

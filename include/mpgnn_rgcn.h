@@ -188,7 +188,8 @@ enum mpgnn_option {
     MPGNN_OPT_TIMING_MASK = 3, /* kernel kinds timed while timing is enabled (bit k = kind k); default all */
     MPGNN_OPT_TILE_WS = 4, /* 1: wave-specialised tile GEMM for F <= 128 (2: without priority); 0 (default): two-workgroup variant */
     MPGNN_OPT_REL_GEMM = 5, /* 1 (default): B-stationary GEMM (weights in registers) for F_in, F_out in {64,128} x {128}; 0: tile GEMM */
-    MPGNN_OPT_FUSED = 6     /* 1 (default): forward means + transform fused in one launch for F_in = F_out = 128; 0: two launches */
+    MPGNN_OPT_FUSED = 6,    /* 1: forward means + transform fused in one launch for F_in = F_out = 128; 0 (default): two launches */
+    MPGNN_OPT_FLAT_U = 7    /* 16 (default) or 32: x rows in flight per wave in the flat row-sum kernel (same results) */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

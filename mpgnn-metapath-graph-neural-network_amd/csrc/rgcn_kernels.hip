@@ -1942,9 +1942,8 @@ struct FlatArgs {
     int relu;               // fused activation on complete rows (unsharded combine only)
 };
 
-template <int V, int T>
+template <int V, int T, int U = 16>
 __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
-    constexpr int U = 16;
     const int lane = threadIdx.x & 63;
     const int c = a.c_lo + (int)blockIdx.x * kWaves + (int)(threadIdx.x >> 6);
     if (c >= a.c_hi) return;
@@ -3117,9 +3116,17 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
     return hip_check(hipGetLastError(), "row_sum_kernel launch");
 }
 
+static int g_flat_u = 16;  // MPGNN_OPT_FLAT_U: rows in flight per wave in flat_rows_kernel (16 or 32; 32 for V·T <= 2 only)
+
 template <int V, int T>
 static void launch_flat(const FlatArgs& a, hipStream_t st) {
     const int n = a.c_hi - a.c_lo;
+    if constexpr (V * T <= 2) {
+        if (g_flat_u == 32) {
+            hipLaunchKernelGGL((flat_rows_kernel<V, T, 32>), dim3((n + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
+            return;
+        }
+    }
     hipLaunchKernelGGL((flat_rows_kernel<V, T>), dim3((n + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
 }
 
@@ -3273,6 +3280,11 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
     }
     if (option == MPGNN_OPT_ABLATE) {
         g_ablate = (int)value;
+        return MPGNN_OK;
+    }
+    if (option == MPGNN_OPT_FLAT_U) {
+        if (value != 16 && value != 32) return arg_error("MPGNN_OPT_FLAT_U must be 16 or 32");
+        g_flat_u = (int)value;
         return MPGNN_OK;
     }
     if (option == MPGNN_OPT_FUSED) {

@@ -1,15 +1,16 @@
 #!/usr/bin/env python3
 """Summarise FETCH_SIZE / WRITE_SIZE passes (rocprofv3 --pmc, kernel-trace only) into
-profiles/pmc_seg_fwd.json: HBM bytes per launch of the forward tile GEMM, corrected as
-MI355X_MICROARCH.md §HBM prescribes for gfx950 (FETCH_SIZE reports half of the read bytes:
-doubled; WRITE_SIZE exact).  Usage: pmc_traffic.py <fetch_dir> <write_dir> <out.json>"""
+profiles/pmc_seg_fwd.json: HBM bytes per launch of the forward transform kernel (the bench's
+roofline kernel), corrected as MI355X_MICROARCH.md §HBM prescribes for gfx950 (FETCH_SIZE reports
+half of the read bytes: doubled; WRITE_SIZE exact).
+Usage: pmc_traffic.py <fetch_dir> <write_dir> <out.json> [kernel name prefix]"""
 import csv
 import glob
 import json
 import os
 import sys
 
-KERNEL = "mpgnn::tile_gemm_kernel<2>"
+KERNEL = sys.argv[4] if len(sys.argv) > 4 else "mpgnn::rel_gemm_kernel<2, false>"
 
 
 def avg(root, counter):
