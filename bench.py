@@ -201,7 +201,7 @@ def main():
             graph = {"error": f"{type(e).__name__}: {e}"[:200]}
 
     # ---- epoch (main_rgcn.py:458-461): train fwd+bwd+Adam + validation forward ------------
-    opt = torch.optim.Adam(net.parameters(), lr=0.01, weight_decay=0.0005)
+    opt = mpgnn_amd.main._adam(net)  # Adam(lr 0.01, wd 5e-4), fused multi-tensor kernel on the GPU
     y = torch.randint(0, 2, (g.num_nodes,), generator=torch.Generator().manual_seed(0)).to(dev)
     train_idx = torch.arange(0, g.num_nodes, 3, device=dev)
 

@@ -193,6 +193,16 @@ enum mpgnn_option {
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 
+/* --- graph file reader --------------------------------------------------------------
+ * link.dat (`node_1 \t relation \t node_2`, one edge per line) → the tensors of
+ * get_edge_index_and_type_no_reverse (main.py:366-372 ≡ main_rgcn.py:357-363), replacing the
+ * pandas.read_csv + Python-list conversion of main.py:150-151,369-371. Host only (no GPU).
+ * mpgnn_links_count: number of non-blank lines. mpgnn_links_parse: fills edge_index
+ * (int64 [2, rows], row 0 = node_1, row 1 = node_2) and edge_type (int64 [rows]) in file
+ * order; MPGNN_ERR_ARG if the file does not hold exactly `rows` three-integer lines. */
+int32_t mpgnn_links_count(const char* path, int64_t* rows);
+int32_t mpgnn_links_parse(const char* path, int64_t* edge_index, int64_t* edge_type, int64_t rows);
+
 /* --- kernel timing (bench / profiling) ----------------------------------------------
  * When enabled, every kernel launch of the entry points above is bracketed by a pair of
  * hipEvents recorded on the launch stream; mpgnn_timing_query synchronises those events and

@@ -6,7 +6,8 @@ francescoferrini/MPGNN-Metapath-Graph-Neural-Network.
   model.MPNetm / model.Net       ← reference model.py wrappers (unchanged PyTorch around the layers)
   functional.rgcn_conv           autograd op over the C ABI (include/mpgnn_rgcn.h)
   plan.GraphPlan                 one-time sorted segment tables of a graph (cached)
-  data, distributed              graph inputs (C1-C5) and dst-range sharding
+  data, distributed              graph inputs (C1-C5, native link.dat reader) and dst-range sharding
+  main, main_rgcn, metrics       training / evaluation loops of main.py and main_rgcn.py
 
 The directory name is not a Python identifier; import it as ``mpgnn_amd`` (repo-root shim).
 """
@@ -14,10 +15,11 @@ from . import _lib  # noqa: F401  (loads libmpgnn_rgcn.so — ImportError if mis
 from .functional import MODE_ALL, MODE_SINGLE, rgcn_conv, segment_means
 from .model import MPNetm, Net
 from .mp_rgcn_layer import CustomRGCNConv, masked_edge_index
-from .nn import RGCNConv
-from . import data, distributed  # noqa: E402
+from .nn import CustomFastRGCNConv, FastRGCNConv, RGCNConv
+from . import data, distributed, metrics  # noqa: E402
+from . import main, main_rgcn  # noqa: E402  (training-loop drop-ins, main.py / main_rgcn.py)
 from .plan import GraphPlan, get_plan, plan_cache
 
-__all__ = ["CustomRGCNConv", "RGCNConv", "MPNetm", "Net", "GraphPlan", "get_plan", "plan_cache",
+__all__ = ["CustomRGCNConv", "RGCNConv", "FastRGCNConv", "CustomFastRGCNConv", "MPNetm", "Net", "GraphPlan", "get_plan", "plan_cache",
            "rgcn_conv", "segment_means", "masked_edge_index", "MODE_SINGLE", "MODE_ALL"]
 __version__ = "0.1.0"

@@ -73,6 +73,8 @@ SIGNATURES = [
     ("mpgnn_debug_occupancy", _I32, [_I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
     ("mpgnn_timing_reset", _I32, []),
     ("mpgnn_timing_query", _I32, [_I32, ctypes.POINTER(ctypes.c_double), _PI64]),
+    ("mpgnn_links_count", _I32, [ctypes.c_char_p, _PI64]),
+    ("mpgnn_links_parse", _I32, [ctypes.c_char_p, _P, _P, _I64]),
 ]
 
 KERNEL_KINDS = {"seg_fwd": 0, "row_fwd": 1, "seg_dgrad": 2, "row_dx": 3, "outer": 4, "reduce": 5, "mean": 6,

@@ -1,0 +1,209 @@
+// link.dat reader: `node_1 \t relation \t node_2` rows → the graph
+// tensors the layers consume, laid out as get_edge_index_and_type_no_reverse builds them
+// (main.py:366-372 ≡ main_rgcn.py:357-363: edge_index row 0 = node_1, row 1 = node_2,
+// edge_type = relation, file order kept). The reference goes through pandas.read_csv
+// (main.py:150-151) and Python lists; here the file is memory-mapped and parsed by a pool of
+// threads over newline-aligned byte ranges (count pass, prefix sum, fill pass).
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mpgnn_rgcn.h"
+#include "plan_internal.h"
+
+namespace {
+
+struct Mapped {
+    const char* p = nullptr;
+    size_t n = 0;
+    int fd = -1;
+    ~Mapped() {
+        if (p && n) munmap(const_cast<char*>(p), n);
+        if (fd >= 0) close(fd);
+    }
+};
+
+int32_t map_file(const char* path, Mapped& m) {
+    if (!path) {
+        mpgnn::set_last_error("link file path is null");
+        return MPGNN_ERR_ARG;
+    }
+    m.fd = open(path, O_RDONLY);
+    if (m.fd < 0) {
+        mpgnn::set_last_error(std::string("cannot open ") + path + ": " + strerror(errno));
+        return MPGNN_ERR_ARG;
+    }
+    struct stat st;
+    if (fstat(m.fd, &st) != 0) {
+        mpgnn::set_last_error(std::string("cannot stat ") + path);
+        return MPGNN_ERR_ARG;
+    }
+    m.n = (size_t)st.st_size;
+    if (m.n == 0) return MPGNN_OK;
+    void* p = mmap(nullptr, m.n, PROT_READ, MAP_PRIVATE, m.fd, 0);
+    if (p == MAP_FAILED) {
+        mpgnn::set_last_error(std::string("cannot map ") + path);
+        m.n = 0;
+        return MPGNN_ERR_ALLOC;
+    }
+    madvise(p, m.n, MADV_SEQUENTIAL);
+    m.p = (const char*)p;
+    return MPGNN_OK;
+}
+
+inline bool is_blank(char c) { return c == ' ' || c == '\t' || c == '\r'; }
+
+// A line holds a row when it has a non-blank character.
+inline bool line_has_data(const char* b, const char* e) {
+    for (; b < e; ++b)
+        if (!is_blank(*b)) return true;
+    return false;
+}
+
+// Byte ranges [cut[t], cut[t+1]) that start at a line start.
+std::vector<size_t> split_lines(const Mapped& m, int parts) {
+    std::vector<size_t> cut(parts + 1, m.n);
+    cut[0] = 0;
+    for (int t = 1; t < parts; ++t) {
+        size_t pos = std::max(cut[t - 1], m.n * (size_t)t / (size_t)parts);
+        if (pos > 0 && pos < m.n && m.p[pos - 1] != '\n') {
+            const void* nl = memchr(m.p + pos, '\n', m.n - pos);
+            pos = nl ? (size_t)((const char*)nl - m.p) + 1 : m.n;
+        }
+        cut[t] = pos;
+    }
+    return cut;
+}
+
+int64_t count_rows(const char* b, const char* e) {
+    int64_t rows = 0;
+    while (b < e) {
+        const char* nl = (const char*)memchr(b, '\n', (size_t)(e - b));
+        const char* le = nl ? nl : e;
+        rows += line_has_data(b, le) ? 1 : 0;
+        b = le + 1;
+    }
+    return rows;
+}
+
+inline bool parse_int(const char*& s, const char* e, int64_t& v) {
+    while (s < e && is_blank(*s)) ++s;
+    bool neg = false;
+    if (s < e && (*s == '-' || *s == '+')) neg = (*s++ == '-');
+    if (s >= e || *s < '0' || *s > '9') return false;
+    uint64_t acc = 0;
+    while (s < e && *s >= '0' && *s <= '9') acc = acc * 10 + (uint64_t)(*s++ - '0');
+    // integral floats as pandas would read them ("3.0"): accept a zero fraction only
+    if (s < e && *s == '.') {
+        ++s;
+        while (s < e && *s == '0') ++s;
+        if (s < e && *s >= '1' && *s <= '9') return false;
+    }
+    if (s < e && !is_blank(*s)) return false;
+    v = neg ? -(int64_t)acc : (int64_t)acc;
+    return true;
+}
+
+int parse_threads(size_t bytes) {
+    unsigned hw = std::thread::hardware_concurrency();
+    int t = (int)std::min<size_t>(hw ? std::min(hw, 16u) : 1u, bytes / (1u << 20) + 1);
+    return std::max(1, t);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t mpgnn_links_count(const char* path, int64_t* rows) {
+    if (!rows) {
+        mpgnn::set_last_error("mpgnn_links_count: rows is null");
+        return MPGNN_ERR_ARG;
+    }
+    Mapped m;
+    int32_t st = map_file(path, m);
+    if (st != MPGNN_OK) return st;
+    const int parts = parse_threads(m.n);
+    std::vector<size_t> cut = split_lines(m, parts);
+    std::vector<int64_t> cnt(parts, 0);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < parts; ++t)
+        pool.emplace_back([&, t] { cnt[t] = count_rows(m.p + cut[t], m.p + cut[t + 1]); });
+    for (auto& th : pool) th.join();
+    int64_t total = 0;
+    for (int64_t c : cnt) total += c;
+    *rows = total;
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_links_parse(const char* path, int64_t* edge_index, int64_t* edge_type, int64_t rows) {
+    if (rows < 0 || (rows > 0 && (!edge_index || !edge_type))) {
+        mpgnn::set_last_error("mpgnn_links_parse: null output or negative row count");
+        return MPGNN_ERR_ARG;
+    }
+    Mapped m;
+    int32_t st = map_file(path, m);
+    if (st != MPGNN_OK) return st;
+    const int parts = parse_threads(m.n);
+    std::vector<size_t> cut = split_lines(m, parts);
+    std::vector<int64_t> cnt(parts, 0), first(parts + 1, 0);
+    {
+        std::vector<std::thread> pool;
+        for (int t = 0; t < parts; ++t)
+            pool.emplace_back([&, t] { cnt[t] = count_rows(m.p + cut[t], m.p + cut[t + 1]); });
+        for (auto& th : pool) th.join();
+    }
+    for (int t = 0; t < parts; ++t) first[t + 1] = first[t] + cnt[t];
+    if (first[parts] != rows) {
+        mpgnn::set_last_error("mpgnn_links_parse: file has " + std::to_string(first[parts]) +
+                              " rows, caller passed " + std::to_string(rows));
+        return MPGNN_ERR_ARG;
+    }
+    std::vector<int64_t> bad(parts, -1);  // row index of the first malformed row per part
+    std::vector<std::thread> pool;
+    for (int t = 0; t < parts; ++t)
+        pool.emplace_back([&, t] {
+            const char* b = m.p + cut[t];
+            const char* e = m.p + cut[t + 1];
+            int64_t r = first[t];
+            while (b < e) {
+                const char* nl = (const char*)memchr(b, '\n', (size_t)(e - b));
+                const char* le = nl ? nl : e;
+                if (line_has_data(b, le)) {
+                    const char* s = b;
+                    int64_t n1, rel, n2;
+                    bool ok = parse_int(s, le, n1) && parse_int(s, le, rel) && parse_int(s, le, n2);
+                    if (ok) {
+                        while (s < le && is_blank(*s)) ++s;
+                        ok = s == le;  // exactly three columns
+                    }
+                    if (!ok) {
+                        bad[t] = r;
+                        return;
+                    }
+                    edge_index[r] = n1;
+                    edge_index[rows + r] = n2;
+                    edge_type[r] = rel;
+                    ++r;
+                }
+                b = le + 1;
+            }
+        });
+    for (auto& th : pool) th.join();
+    for (int t = 0; t < parts; ++t)
+        if (bad[t] >= 0) {
+            mpgnn::set_last_error("mpgnn_links_parse: row " + std::to_string(bad[t]) +
+                                  " is not three integer columns (node_1, relation, node_2)");
+            return MPGNN_ERR_ARG;
+        }
+    return MPGNN_OK;
+}
+
+}  // extern "C"

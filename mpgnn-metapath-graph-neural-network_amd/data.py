@@ -10,6 +10,7 @@ File formats (reference loaders, main.py:138-195, 347-372):
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from dataclasses import dataclass
 
@@ -57,10 +58,17 @@ def _read_tsv_numeric(path: str, dtype) -> np.ndarray:
 
 def load_links(link_file: str) -> tuple[torch.Tensor, torch.Tensor]:
     """link.dat → (edge_index, edge_type) — main.py:150-151 + get_edge_index_and_type_no_reverse
-    (main.py:366-372)."""
-    a = _read_tsv_numeric(link_file, np.int64)
-    edge_index = torch.from_numpy(np.ascontiguousarray(np.stack([a[:, 0], a[:, 2]])))
-    edge_type = torch.from_numpy(np.ascontiguousarray(a[:, 1]))
+    (main.py:366-372). Parsed by the library's multi-threaded reader (mpgnn_links_count /
+    mpgnn_links_parse, csrc/io.cpp); a malformed row raises ValueError."""
+    from . import _lib
+    path = os.fsencode(link_file)
+    rows = ctypes.c_int64()
+    _lib.check(_lib.lib.mpgnn_links_count(path, ctypes.byref(rows)), "mpgnn_links_count")
+    n = int(rows.value)
+    edge_index = torch.empty((2, n), dtype=torch.int64)
+    edge_type = torch.empty((n,), dtype=torch.int64)
+    _lib.check(_lib.lib.mpgnn_links_parse(path, edge_index.data_ptr(), edge_type.data_ptr(), n),
+               "mpgnn_links_parse")
     return edge_index, edge_type
 
 

@@ -1,0 +1,184 @@
+"""Drop-in for the MPGNN training loop of the reference ``main.py``:
+the graph loaders it feeds the layers with and ``mpgnn_train`` / ``mpgnn_validation`` /
+``mpgnn_test`` / ``mpgnn_parallel_multiple(_x)`` (main.py:1055-1160), driving
+``MPNetm`` (model.py:179-228) whose CustomRGCNConv layers run on the gfx950 kernels.
+
+Same names, arguments, return values and printed lines as the reference. What changes is
+where things live: the model and the ``data`` tensors stay on the GPU, losses are reduced on
+the device, and the macro-F1 scores are finished from per-class counts (``metrics``) instead
+of Python lists — one host sync per scoring call. The metapath search driver around these
+functions (main.py:1163-1460) is outside the hot path (SURVEY §2, §7 of DESIGN.md).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import data as _data
+from .metrics import class_weight_balanced, f1_macro_many
+from .model import MPNetm
+
+__all__ = ["Data", "load_files", "get_node_features", "get_edge_index_and_type_no_reverse",
+           "load_graph", "mpgnn_train", "mpgnn_validation", "mpgnn_test",
+           "mpgnn_parallel_multiple", "mpgnn_parallel_multiple_x", "EPOCHS"]
+
+EPOCHS = 999  # ``for epoch in range(1, 1000)`` (main.py:1121, 1144)
+
+
+class Data:
+    """Attribute bag standing in for ``torch_geometric.data.Data`` as the loops use it
+    (main.py:1470-1480: x, edge_index, edge_type, train_idx/_y, val_idx/_y, test_idx/_y)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    def to(self, device) -> "Data":
+        return Data(**{k: (v.to(device) if torch.is_tensor(v) else v) for k, v in self.__dict__.items()})
+
+    def __repr__(self) -> str:
+        parts = [f"{k}={list(v.shape) if torch.is_tensor(v) else v}" for k, v in self.__dict__.items()]
+        return f"Data({', '.join(parts)})"
+
+
+# ---------------------------------------------------------------------------------------
+# loaders (A1)
+# ---------------------------------------------------------------------------------------
+def load_files(node_file_path, link_file_path, label_file_path):
+    """main.py:174-191: (labels tensor, features DataFrame, links DataFrame, [labels],
+    number of relation types). pandas frames as in the reference, for code that keeps using
+    them; ``load_graph`` is the fast path to the tensors."""
+    import pandas as pd
+    features = pd.read_csv(node_file_path, sep="\t", header=None)
+    features = features.dropna(axis=1, how="all")
+    features.rename(columns={0: "node", 1: "features"}, inplace=True)
+    labels_df = pd.read_csv(label_file_path, sep="\t", header=None)
+    labels_df.rename(columns={0: "node", 1: "label"}, inplace=True)
+    labels = torch.tensor(labels_df["label"].values)
+    links = pd.read_csv(link_file_path, sep="\t", header=None)
+    links.rename(columns={0: "node_1", 1: "relation_type", 2: "node_2"}, inplace=True)
+    tot_relation_types = len(set(links["relation_type"].to_list()))
+    return labels, features, links, [labels], tot_relation_types
+
+
+def get_node_features(colors):
+    """main.py:347-355: one-hot columns of the colour frame (``pd.get_dummies``, 'node'
+    dropped), columns reversed, float32."""
+    import pandas as pd
+    node_features = pd.get_dummies(colors)
+    node_features.drop(["node"], axis=1, inplace=True)
+    x = node_features.to_numpy().astype(np.float32)
+    return torch.from_numpy(np.flip(x, 1).copy())
+
+
+def get_edge_index_and_type_no_reverse(links):
+    """main.py:366-372: links frame → (edge_index int64 [2, E] = (node_1, node_2),
+    edge_type int64 [E]), file order kept."""
+    n1 = np.ascontiguousarray(links["node_1"].to_numpy(dtype=np.int64))
+    n2 = np.ascontiguousarray(links["node_2"].to_numpy(dtype=np.int64))
+    edge_index = torch.from_numpy(np.stack([n1, n2]))
+    edge_type = torch.from_numpy(np.ascontiguousarray(links["relation_type"].to_numpy(dtype=np.int64)))
+    return edge_index, edge_type
+
+
+def load_graph(link_file_path):
+    """link.dat straight to ``get_edge_index_and_type_no_reverse``'s output through the
+    library's native reader (csrc/io.cpp) — no DataFrame, no Python lists."""
+    return _data.load_links(link_file_path)
+
+
+# ---------------------------------------------------------------------------------------
+# loop (A11)
+# ---------------------------------------------------------------------------------------
+def _adam(model):
+    """Adam(lr=0.01, weight_decay=0.0005) of main.py:1119 / main_rgcn.py:454. On the GPU the
+    fused implementation (one multi-tensor kernel per step instead of one per Adam sub-step;
+    same update rule, rounding-level differences) — scripts/epoch_ab.py: 1.23 → 1.12 ms per
+    FB15K epoch."""
+    params = list(model.parameters())
+    fused = bool(params) and all(p.is_cuda for p in params)
+    return torch.optim.Adam(params, lr=0.01, weight_decay=0.0005, fused=fused)
+
+
+def _num_classes(out: torch.Tensor) -> int:
+    return int(out.shape[1]) if out.dim() > 1 else 1
+
+
+def mpgnn_train(model, optimizer, data):
+    """main.py:1055-1082: full-batch forward, unweighted NLL on train_idx, backward, step.
+    Returns (float loss, balanced class weights) like the reference (the weights are
+    computed there but not applied, main.py:1065)."""
+    model.train()
+    optimizer.zero_grad()
+    out = model(data.x, data.edge_index, data.edge_type)
+    weights = class_weight_balanced(data.train_y)
+    loss = F.nll_loss(out[data.train_idx].squeeze(-1), data.train_y)
+    loss.backward()
+    optimizer.step()
+    return float(loss.detach()), weights
+
+
+@torch.no_grad()
+def mpgnn_validation(model, data, class_weight):
+    """main.py:1084-1099 → (f1 train, f1 val, f1 val, val loss tensor); both val scores are
+    the same macro F1, as in the reference."""
+    model.eval()
+    pred = model(data.x, data.edge_index, data.edge_type)
+    loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
+    c = _num_classes(pred)
+    f1_train, f1_val = f1_macro_many([(torch.argmax(pred[data.train_idx], 1), data.train_y),
+                                      (torch.argmax(pred[data.val_idx], 1), data.val_y)], c)
+    return f1_train, f1_val, f1_val, loss_val
+
+
+@torch.no_grad()
+def mpgnn_test(model, data, class_weight):
+    """main.py:1101-1115 → (test loss tensor, test macro F1)."""
+    model.eval()
+    pred = model(data.x, data.edge_index, data.edge_type)
+    loss_test = F.nll_loss(pred[data.test_idx].squeeze(-1), data.test_y)
+    (f1_test,) = f1_macro_many([(torch.argmax(pred[data.test_idx], 1), data.test_y)], _num_classes(pred))
+    return loss_test, f1_test
+
+
+def _fit(data_mpgnn, input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, metapaths, epochs):
+    model = MPNetm(input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, len(metapaths), metapaths)
+    model = model.to(data_mpgnn.x.device)
+    optimizer = _adam(model)
+    best_micro = 0.
+    best_model = model
+    class_weight = None
+    f1_valt_macro = 0.
+    for _epoch in range(1, epochs + 1):
+        _loss, class_weight = mpgnn_train(model, optimizer, data_mpgnn)
+        _train_acc, f1_val_macro, f1_valt_macro, _loss_val = mpgnn_validation(model, data_mpgnn, class_weight)
+        if f1_val_macro > best_micro:
+            best_micro = f1_val_macro
+            best_model = model  # the reference keeps a reference, not a copy (main.py:1125)
+    return model, best_model, class_weight, f1_valt_macro
+
+
+def mpgnn_parallel_multiple(data_mpgnn, input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, metapaths,
+                            epochs: int = EPOCHS):
+    """main.py:1117-1136: train an MPNetm over ``metapaths`` for 999 epochs with Adam
+    (lr 0.01, wd 5e-4); returns the last epoch's validation macro F1."""
+    _, best_model, class_weight, f1_valt_macro = _fit(data_mpgnn, input_dim, hidden_dim, num_rel, output_dim,
+                                                      ll_output_dim, metapaths, epochs)
+    mpgnn_test(best_model, data_mpgnn, class_weight)
+    return f1_valt_macro
+
+
+def mpgnn_parallel_multiple_x(data_mpgnn, input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, metapaths,
+                              testing, epochs: int = EPOCHS):
+    """main.py:1138-1160: as ``mpgnn_parallel_multiple`` (a single metapath may be given as a
+    flat list); prints the test line; returns the test macro F1 when ``testing`` else the last
+    validation macro F1."""
+    if isinstance(metapaths[0], int):
+        metapaths = [metapaths]
+    _, best_model, class_weight, f1_valt_macro = _fit(data_mpgnn, input_dim, hidden_dim, num_rel, output_dim,
+                                                      ll_output_dim, metapaths, epochs)
+    test_loss, f1_macro_test = mpgnn_test(best_model, data_mpgnn, class_weight)
+    print("test loss %0.3f" % test_loss, "test macro %0.3f" % f1_macro_test)
+    if testing == False:  # noqa: E712  (reference: 0 and False both select validation)
+        return f1_valt_macro
+    return f1_macro_test

@@ -1,0 +1,92 @@
+"""Drop-in for the RGCN-baseline training loop of the reference ``main_rgcn.py`` (SURVEY §8a
+A11): ``mpgnn_train`` (class-balanced NLL) / ``mpgnn_validation`` / ``mpgnn_test`` /
+``mpgnn_parallel_multiple`` (main_rgcn.py:369-472) driving ``Net`` (model.py:132-149) whose
+RGCNConv layers run on the gfx950 kernels. The loaders are shared with ``main``
+(main_rgcn.py:345-363 ≡ main.py:347-372).
+
+Same names, arguments, return values and printed lines as the reference; model and data stay
+on the GPU and the macro-F1 scores are finished from device-side counts (``metrics``).
+``shard``/``group`` (keyword-only, default off) run the dst-range sharded layers (§8e).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .main import _adam, Data, get_edge_index_and_type_no_reverse, get_node_features, load_files, load_graph  # noqa: F401
+from .metrics import class_weight_balanced, f1_macro_many
+from .model import Net
+
+__all__ = ["Data", "mpgnn_train", "mpgnn_validation", "mpgnn_test", "mpgnn_parallel_multiple", "EPOCHS"]
+
+EPOCHS = 999  # ``for epoch in range(1, 1000)`` (main_rgcn.py:457)
+
+
+def _forward(model, data):
+    kw = getattr(data, "shard_kw", None) or {}
+    return model(data.x, data.edge_index, data.edge_type, **kw)
+
+
+def mpgnn_train(model, optimizer, data):
+    """main_rgcn.py:369-393: forward, NLL on train_idx weighted by the balanced class weights
+    (main_rgcn.py:376-380), backward, step → (float loss, weights)."""
+    model.train()
+    optimizer.zero_grad()
+    out = _forward(model, data)
+    weights = class_weight_balanced(data.train_y)
+    weights_tensor = torch.tensor(weights, dtype=torch.float, device=out.device)
+    loss = F.nll_loss(out[data.train_idx].squeeze(-1), data.train_y, weight=weights_tensor)
+    loss.backward()
+    optimizer.step()
+    return float(loss.detach()), weights
+
+
+@torch.no_grad()
+def mpgnn_validation(model, data, class_weight):
+    """main_rgcn.py:395-416 → (f1 train, f1 val, f1 val, val loss tensor)."""
+    model.eval()
+    pred = _forward(model, data)
+    loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
+    c = int(pred.shape[1])
+    f1_train, f1_val = f1_macro_many([(torch.argmax(pred[data.train_idx], 1), data.train_y),
+                                      (torch.argmax(pred[data.val_idx], 1), data.val_y)], c)
+    return f1_train, f1_val, f1_val, loss_val
+
+
+@torch.no_grad()
+def mpgnn_test(model, data, class_weight):
+    """main_rgcn.py:418-432 → (test loss tensor, test macro F1)."""
+    model.eval()
+    pred = _forward(model, data)
+    loss_test = F.nll_loss(pred[data.test_idx].squeeze(-1), data.test_y)
+    (f1_test,) = f1_macro_many([(torch.argmax(pred[data.test_idx], 1), data.test_y)], int(pred.shape[1]))
+    return loss_test, f1_test
+
+
+def mpgnn_parallel_multiple(data_mpgnn, input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, metapath_length,
+                            epochs: int = EPOCHS, verbose: bool = True):
+    """main_rgcn.py:452-472: train ``Net`` (L = metapath_length) for 999 epochs with Adam
+    (lr 0.01, wd 5e-4), running train / validation / test every epoch and printing every
+    10th; returns the test macro F1 of ``best_model`` (the same object as the trained model,
+    as in the reference)."""
+    model = Net(input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, metapath_length)
+    model = model.to(data_mpgnn.x.device)
+    optimizer = _adam(model)
+    best_micro = 0.
+    best_model = model
+    class_weight = None
+    for epoch in range(1, epochs + 1):
+        loss, class_weight = mpgnn_train(model, optimizer, data_mpgnn)
+        train_acc, f1_val_micro, f1_val_macro, loss_val = mpgnn_validation(model, data_mpgnn, class_weight)
+        test_loss, f1_micro_test = mpgnn_test(model, data_mpgnn, class_weight)
+        if f1_val_macro > best_micro:
+            best_micro = f1_val_macro
+            best_model = model
+        if verbose and epoch % 10 == 0:
+            print(epoch, "train loss %0.3f" % loss, "validation loss %0.3f" % loss_val,
+                  "train micro: %0.3f" % train_acc, "validation micro: %0.3f" % f1_val_micro,
+                  "test micro: %0.3f" % f1_micro_test)
+    test_loss, f1_micro_test = mpgnn_test(best_model, data_mpgnn, class_weight)
+    if verbose:
+        print("test loss %0.3f" % test_loss, "test micro %0.3f" % f1_micro_test)
+    return f1_micro_test

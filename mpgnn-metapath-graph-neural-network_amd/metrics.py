@@ -1,0 +1,71 @@
+"""Loss weights and scores of the reference training loop, computed next to the logits.
+
+The reference scores every epoch with scikit-learn on Python lists
+(``f1_score(torch.argmax(pred[idx], 1).tolist(), y.tolist(), average='macro')``,
+main.py:1094-1098, main_rgcn.py:409-415), which copies every prediction to the host. Here the
+per-class confusion counts are reduced on the device and only those counts (3 × classes
+int64) cross to the host, where the F-score is finished with the same float64 arithmetic and
+the same numpy reduction scikit-learn 1.7 uses (``precision_recall_fscore_support``:
+``f = 2·tp / (true_sum + pred_sum)`` over the sorted union of labels, then ``np.average``).
+Results are identical to scikit-learn's (tests/test_loop.py).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+__all__ = ["f1_macro", "f1_macro_many", "class_weight_balanced"]
+
+
+def _confusion_counts(pred: torch.Tensor, y: torch.Tensor, num_classes: int) -> torch.Tensor:
+    """[3, C] int64: (count of each label in pred, in y, agreeing positions per label)."""
+    pred = pred.reshape(-1).to(torch.int64)
+    y = y.reshape(-1).to(device=pred.device, dtype=torch.int64)
+    hit = torch.where(pred == y, y, torch.full_like(y, num_classes))  # misses → overflow bin
+    return torch.stack([torch.bincount(pred, minlength=num_classes)[:num_classes],
+                        torch.bincount(y, minlength=num_classes)[:num_classes],
+                        torch.bincount(hit, minlength=num_classes + 1)[:num_classes]])
+
+
+def _finish(counts: np.ndarray) -> float:
+    pred_sum, true_sum, tp = (counts[0].astype(np.int64), counts[1].astype(np.int64),
+                              counts[2].astype(np.int64))
+    labels = (pred_sum + true_sum) > 0  # sklearn: unique_labels(y_true, y_pred), sorted
+    denom = true_sum[labels].astype(np.float64) + pred_sum[labels].astype(np.float64)
+    f = 2.0 * tp[labels].astype(np.float64) / denom
+    return float(np.average(f))
+
+
+def f1_macro_many(pairs: list[tuple[torch.Tensor, torch.Tensor]], num_classes: int) -> list[float]:
+    """Macro F1 of several (predictions, labels) pairs with ONE device→host copy.
+    Labels must lie in [0, num_classes) (the logits' width; nll_loss enforces it)."""
+    if not pairs:
+        return []
+    counts = torch.stack([_confusion_counts(p, y, num_classes) for p, y in pairs]).cpu().numpy()
+    return [_finish(c) for c in counts]
+
+
+def f1_macro(pred: torch.Tensor, y: torch.Tensor, num_classes: int) -> float:
+    """``sklearn.metrics.f1_score(pred, y, average='macro')`` (symmetric in its arguments)."""
+    return f1_macro_many([(pred, y)], num_classes)[0]
+
+
+_CW_CACHE: dict = {}
+
+
+def class_weight_balanced(y: torch.Tensor) -> np.ndarray:
+    """``class_weight.compute_class_weight('balanced', classes=np.unique(y), y=y)``
+    (main_rgcn.py:378): n_samples / (n_classes · bincount) over the classes present.
+    The loops recompute it every epoch on an unchanged label tensor; the answer is cached by
+    tensor identity and version so the labels cross to the host once."""
+    key = (y.data_ptr(), y.numel(), y._version, str(y.device))
+    hit = _CW_CACHE.get(key)
+    if hit is not None:
+        return hit.copy()
+    yn = y.detach().cpu().numpy().reshape(-1)
+    classes, counts = np.unique(yn, return_counts=True)
+    w = yn.shape[0] / (classes.shape[0] * counts.astype(np.float64))
+    if len(_CW_CACHE) > 64:
+        _CW_CACHE.clear()
+    _CW_CACHE[key] = w
+    return w.copy()

@@ -18,7 +18,7 @@ from .functional import MODE_ALL, rgcn_conv
 from .mp_rgcn_layer import glorot, zeros
 from .plan import FLOWS, get_plan
 
-__all__ = ["RGCNConv"]
+__all__ = ["RGCNConv", "FastRGCNConv", "CustomFastRGCNConv"]
 
 
 class RGCNConv(torch.nn.Module):
@@ -96,3 +96,22 @@ class RGCNConv(torch.nn.Module):
     def __repr__(self) -> str:
         return (f"{self.__class__.__name__}({self.in_channels}, "
                 f"{self.out_channels}, num_relations={self.num_relations})")
+
+
+class FastRGCNConv(RGCNConv):
+    """``CustomFastRGCNConv`` (mp_rgcn_layer.py:287-357) / PyG ``FastRGCNConv``: the
+    transform-then-aggregate formulation of the same layer — per edge ``x_j @ W[edge_type]``
+    (:344), scaled by ``1 / deg_(i, rel)`` (:350-355), scatter-summed (:357), ``+ x @ root +
+    bias`` (:313-317). Mathematically equal to ``RGCNConv`` (summation order aside), so it runs
+    the same aggregate-then-transform kernels, which do 2·S·F_in·F_out instead of
+    2·E·F_in·F_out MFMA work (S = distinct (row, relation) segments ≤ E) and never materialise
+    the [E, F_in, F_out] weight gather.
+
+    The reference class inherits CustomRGCNConv's 2-D ``weight [F_in, F_out]``
+    (mp_rgcn_layer.py:135-136), with which ``torch.bmm`` at :344 raises; this class takes the
+    3-D ``weight [R, F_in, F_out]`` of PyG FastRGCNConv (the class it was adapted from), the
+    only shape its forward can run with. ``oracle.rgcn_oracle.fast_rgcn_forward`` restates the
+    per-edge arithmetic; tests/test_gpu_parity.py checks this layer against it."""
+
+
+CustomFastRGCNConv = FastRGCNConv

@@ -106,6 +106,29 @@ def rgcn_forward(x: Tensor, edge_index: Tensor, edge_type: Tensor, weight: Tenso
     return out
 
 
+def fast_rgcn_forward(x: Tensor, edge_index: Tensor, edge_type: Tensor, weight: Tensor,
+                      root: Tensor | None, bias: Tensor | None, flow: str = "target_to_source") -> Tensor:
+    """CustomFastRGCNConv (mp_rgcn_layer.py:287-357) with the 3-D weight of PyG FastRGCNConv:
+    per-edge transform x_j @ W[edge_type] (:344), scaled by 1 / deg_(i, rel) (:350-355),
+    scatter-summed into row i (:357), then + x @ root (:313) + bias (:316). Transform-then-
+    aggregate: the same function as rgcn_forward up to summation order."""
+    n, r = x.size(0), weight.size(0)
+    i, j = (0, 1) if flow == "target_to_source" else (1, 0)
+    index = edge_index[i]
+    x_j = x.index_select(0, edge_index[j])
+    msg = torch.bmm(x_j.unsqueeze(-2), weight[edge_type]).squeeze(-2)
+    norm = torch.nn.functional.one_hot(edge_type, r).to(torch.float)
+    norm = torch.zeros(n, r, dtype=torch.float).index_add_(0, index, norm)[index]
+    norm = torch.gather(norm, 1, edge_type.view(-1, 1))
+    norm = 1.0 / norm.clamp_(1.0)
+    out = torch.zeros(n, weight.size(-1), dtype=x.dtype).index_add_(0, index, norm * msg)
+    if root is not None:
+        out = out + x @ root
+    if bias is not None:
+        out = out + bias
+    return out
+
+
 def segment_means(x: Tensor, edge_index: Tensor, edge_type: Tensor, relation: int,
                   flow: str = "target_to_source") -> Tensor:
     """h = propagate_mean over the edges of one relation (the bit-exact part of the path)."""

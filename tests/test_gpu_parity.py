@@ -582,3 +582,26 @@ def test_fused_saved_means_bit_exact():
     h = h.cpu()
     assert torch.equal(h[short], ref[short])
     rel_close(h[~short], ref[~short], tol=1e-6, what="split segments")
+
+
+# ------------------------------------------------------------------------------------------
+# CustomFastRGCNConv (A7): transform-then-aggregate semantics on the same kernels
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("f_in,f_out", [(16, 16), (128, 64)])
+def test_fast_rgcn_conv_matches_per_edge_oracle(f_in, f_out):
+    g = data.synthetic_graph(500, 5, 10, feat_dim=f_in, seed=11 + f_in)
+    torch.manual_seed(30)
+    conv = mpgnn_amd.CustomFastRGCNConv(f_in, f_out, 5, flow="target_to_source")
+    with torch.no_grad():
+        conv.bias.uniform_(-0.5, 0.5)
+    xs = g.x.clone().requires_grad_(True)
+    ref = orc.fast_rgcn_forward(xs, g.edge_index, g.edge_type, conv.weight.detach(), conv.root.detach(),
+                                conv.bias.detach())
+    gout = torch.randn_like(ref)
+    ref.backward(gout)
+    convg = conv.to(DEV)
+    xg = g.x.to(DEV).requires_grad_(True)
+    out = convg(xg, g.edge_index.to(DEV), g.edge_type.to(DEV))
+    rel_close(out, ref, what="fast out")
+    out.backward(gout.to(DEV))
+    rel_close(xg.grad, xs.grad, what="fast dx")

@@ -1,0 +1,212 @@
+"""Training-loop drop-in: the native link.dat reader, the device-side
+scores against scikit-learn, the loop's host logic with a CPU oracle model, and (GPU) the
+loops of main.py / main_rgcn.py against the same loop run on the CPU oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+from sklearn.metrics import f1_score
+from sklearn.utils import class_weight as skl_class_weight
+
+import mpgnn_amd
+from mpgnn_amd import data, main, main_rgcn, metrics
+from oracle import rgcn_oracle as orc
+
+DEV = "cuda"
+
+
+# ------------------------------------------------------------------------------------------
+# native link.dat reader (main.py:150-151,366-372)
+# ------------------------------------------------------------------------------------------
+def _write(path, text):
+    with open(path, "w", newline="") as f:
+        f.write(text)
+
+
+@pytest.mark.parametrize("graph", ["L3", "L4"])
+def test_load_links_matches_reference_layout_on_kat_graphs(tmp_path, golden, graph):
+    """The reference's own link.dat rows (KAT fixture) parse to the tensors
+    get_edge_index_and_type_no_reverse builds: row 0 = node_1, row 1 = node_2, file order."""
+    rows = golden("kat_synthetic.npz")[f"{graph}_link"]
+    p = tmp_path / "link.dat"
+    np.savetxt(p, rows, fmt="%d", delimiter="\t")
+    ei, et = data.load_links(str(p))
+    assert ei.dtype == torch.int64 and et.dtype == torch.int64
+    assert np.array_equal(ei.numpy(), np.stack([rows[:, 0], rows[:, 2]]))
+    assert np.array_equal(et.numpy(), rows[:, 1])
+    # and the pandas path of the reference (load_files + get_edge_index_and_type_no_reverse)
+    import pandas as pd
+    links = pd.read_csv(p, sep="\t", header=None).rename(columns={0: "node_1", 1: "relation_type", 2: "node_2"})
+    ei2, et2 = main.get_edge_index_and_type_no_reverse(links)
+    assert torch.equal(ei, ei2) and torch.equal(et, et2)
+
+
+def test_load_links_edge_cases(tmp_path):
+    p = str(tmp_path / "l.dat")
+    _write(p, "")
+    ei, et = data.load_links(p)
+    assert ei.shape == (2, 0) and et.shape == (0,)
+    # CRLF, blank lines, spaces, no trailing newline, integral floats, negative ids kept
+    _write(p, "1\t2\t3\r\n\n  4 5\t6  \n\t\n7\t8\t9.0\n-1\t0\t2")
+    ei, et = data.load_links(p)
+    assert ei.tolist() == [[1, 4, 7, -1], [3, 6, 9, 2]] and et.tolist() == [2, 5, 8, 0]
+    for bad in ("1\t2\n", "1\t2\t3\t4\n", "1\tx\t3\n", "1\t2\t3.5\n"):
+        _write(p, "0\t0\t0\n" + bad)
+        with pytest.raises(ValueError):
+            data.load_links(p)
+    with pytest.raises(ValueError):
+        data.load_links(str(tmp_path / "missing.dat"))
+
+
+def test_load_links_large_file_multithreaded(tmp_path):
+    """> 1 MiB so the reader splits the file over several threads; boundaries are exact."""
+    rng = np.random.default_rng(3)
+    rows = np.stack([rng.integers(0, 10**6, 200_000), rng.integers(0, 237, 200_000),
+                     rng.integers(0, 10**6, 200_000)], 1)
+    p = tmp_path / "big.dat"
+    np.savetxt(p, rows, fmt="%d", delimiter="\t")
+    assert os.path.getsize(p) > (3 << 20)
+    ei, et = data.load_links(str(p))
+    assert np.array_equal(ei.numpy(), np.stack([rows[:, 0], rows[:, 2]])) and np.array_equal(et.numpy(), rows[:, 1])
+
+
+# ------------------------------------------------------------------------------------------
+# scores and loss weights (main.py:1062-1098, main_rgcn.py:376-415)
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("seed", range(8))
+def test_f1_macro_identical_to_sklearn(seed):
+    rng = np.random.default_rng(seed)
+    c = int(rng.integers(2, 12))
+    n = int(rng.integers(1, 400))
+    y = rng.integers(0, c, n)
+    pred = rng.integers(0, c, n) if seed % 2 else np.where(rng.random(n) < 0.7, y, rng.integers(0, c, n))
+    if seed == 3:
+        pred[:] = 0  # a class predicted nowhere / present nowhere
+    ref = f1_score(pred.tolist(), y.tolist(), average="macro")  # the reference's argument order
+    got = metrics.f1_macro(torch.from_numpy(pred), torch.from_numpy(y), c)
+    assert got == ref, (got, ref)
+    many = metrics.f1_macro_many([(torch.from_numpy(pred), torch.from_numpy(y)),
+                                  (torch.from_numpy(y), torch.from_numpy(pred))], c)
+    assert many == [ref, f1_score(y.tolist(), pred.tolist(), average="macro")]
+
+
+def test_class_weight_balanced_identical_to_sklearn():
+    for seed in range(4):
+        y = torch.from_numpy(np.random.default_rng(seed).integers(0, 3 + seed, 97))
+        ref = skl_class_weight.compute_class_weight("balanced", classes=np.unique(y.numpy()), y=y.tolist())
+        assert np.array_equal(metrics.class_weight_balanced(y), ref)
+        assert np.array_equal(metrics.class_weight_balanced(y), ref)  # cached answer
+
+
+# ------------------------------------------------------------------------------------------
+# loop host logic with the CPU oracle as the model (no GPU)
+# ------------------------------------------------------------------------------------------
+class _OracleNet(torch.nn.Module):
+    """model.py:Net restated by the oracle (CPU), with Net's parameter names."""
+
+    def __init__(self, params, layers):
+        super().__init__()
+        self.p = torch.nn.ParameterDict({k.replace(".", "__"): torch.nn.Parameter(v.clone()) for k, v in params.items()})
+        self.layers = layers
+
+    def forward(self, x, edge_index, edge_type):
+        params = {k.replace("__", "."): v for k, v in self.p.items()}
+        return orc.net_forward(params, x, edge_index, edge_type, self.layers)
+
+
+def _task(g, classes=3, seed=1):
+    gen = torch.Generator().manual_seed(seed)
+    y = torch.randint(0, classes, (g.num_nodes,), generator=gen)
+    perm = torch.randperm(g.num_nodes, generator=gen)
+    n = g.num_nodes
+    tr, va, te = perm[: n // 2], perm[n // 2: 3 * n // 4], perm[3 * n // 4:]
+    return main.Data(x=g.x, edge_index=g.edge_index, edge_type=g.edge_type, train_idx=tr, train_y=y[tr],
+                     val_idx=va, val_y=y[va], test_idx=te, test_y=y[te])
+
+
+def _net_params(g, f_in, hidden, classes, seed=30):
+    torch.manual_seed(seed)
+    r = g.num_relations
+    gl = lambda *s: torch.nn.init.xavier_uniform_(torch.empty(*s)) if len(s) == 2 else \
+        torch.stack([torch.nn.init.xavier_uniform_(torch.empty(*s[1:])) for _ in range(s[0])])  # noqa: E731
+    return {"conv1.weight": gl(r, f_in, hidden), "conv1.root": gl(f_in, hidden), "conv1.bias": torch.zeros(hidden),
+            "conv2.weight": gl(r, hidden, hidden), "conv2.root": gl(hidden, hidden), "conv2.bias": torch.zeros(hidden),
+            "LinearLayer.weight": gl(classes, hidden), "LinearLayer.bias": torch.zeros(classes)}
+
+
+def test_rgcn_loop_functions_on_cpu_oracle_model():
+    g = data.synthetic_graph(300, 3, 6, feat_dim=16, seed=2)
+    d = _task(g)
+    net = _OracleNet(_net_params(g, 16, 32, 3), 2)
+    opt = torch.optim.Adam(net.parameters(), lr=0.01, weight_decay=0.0005)
+    losses = []
+    for _ in range(4):
+        loss, w = main_rgcn.mpgnn_train(net, opt, d)
+        losses.append(loss)
+        f1_tr, f1_v, f1_v2, lv = main_rgcn.mpgnn_validation(net, d, w)
+        assert 0.0 <= f1_tr <= 1.0 and f1_v == f1_v2 and torch.is_tensor(lv)
+        # scores equal scikit-learn on the reference's list path
+        pred = net(d.x, d.edge_index, d.edge_type)
+        ref = f1_score(torch.argmax(pred[d.val_idx], 1).tolist(), d.val_y.tolist(), average="macro")
+        assert f1_v == ref
+    assert np.array_equal(w, skl_class_weight.compute_class_weight("balanced", classes=np.unique(d.train_y.numpy()),
+                                                                   y=d.train_y.tolist()))
+    assert losses[-1] < losses[0]
+    lt, f1_t = main_rgcn.mpgnn_test(net, d, w)
+    assert 0.0 <= f1_t <= 1.0
+
+
+# ------------------------------------------------------------------------------------------
+# GPU: the loops vs the same loop on the CPU oracle
+# ------------------------------------------------------------------------------------------
+@pytest.mark.gpu
+def test_rgcn_epochs_track_oracle_loop():
+    """main_rgcn.py:456-461 epochs (weighted NLL, Adam) with Net on the GPU vs _OracleNet on
+    the CPU from the same parameters: the loss trajectory agrees to 1e-4 relative for the
+    first epochs (Adam amplifies rounding noise of ~0 gradients later, see test_gpu_parity)."""
+    g = data.config_graph("C1")
+    d = _task(g)
+    torch.manual_seed(30)
+    net = mpgnn_amd.Net(128, 64, g.num_relations, 64, 3, 2)
+    ref = _OracleNet({k: v.detach() for k, v in net.state_dict().items()}, 2)
+    netg = net.to(DEV)
+    dg = d.to(DEV)
+    opt = torch.optim.Adam(netg.parameters(), lr=0.01, weight_decay=0.0005)
+    opt_ref = torch.optim.Adam(ref.parameters(), lr=0.01, weight_decay=0.0005)
+    for epoch in range(3):
+        loss, w = main_rgcn.mpgnn_train(netg, opt, dg)
+        loss_ref, w_ref = main_rgcn.mpgnn_train(ref, opt_ref, d)
+        assert np.array_equal(w, w_ref)
+        assert abs(loss - loss_ref) <= 1e-4 * abs(loss_ref), (epoch, loss, loss_ref)
+        _, _, _, lv = main_rgcn.mpgnn_validation(netg, dg, w)
+        _, _, _, lv_ref = main_rgcn.mpgnn_validation(ref, d, w_ref)
+        assert abs(float(lv) - float(lv_ref)) <= 1e-4 * abs(float(lv_ref))
+
+
+@pytest.mark.gpu
+def test_mpgnn_parallel_multiple_x_learns_planted_metapath(golden, capsys):
+    """main.py:1138-1160 on the reference's planted synthetic graph (KAT fixture, metapath
+    length 3): training MPNetm over the planted metapath reaches a high test macro F1, and the
+    reference's printed line is produced."""
+    z = golden("kat_synthetic.npz")
+    link, node, label = z["L3_link"], z["L3_node"], z["L3_label"]
+    ei = torch.from_numpy(np.stack([link[:, 0], link[:, 2]]))
+    et = torch.from_numpy(link[:, 1].copy())
+    n = node.shape[0]
+    x = torch.from_numpy(node[:, 1:].astype(np.float32))  # one-hot colours (red, blue)
+    y = torch.zeros(n, dtype=torch.int64)
+    y[torch.from_numpy(label[:, 0])] = torch.from_numpy(label[:, 1])
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(0))
+    tr, va, te = perm[: n * 6 // 10], perm[n * 6 // 10: n * 8 // 10], perm[n * 8 // 10:]
+    d = main.Data(x=x, edge_index=ei, edge_type=et, train_idx=tr, train_y=y[tr], val_idx=va, val_y=y[va],
+                  test_idx=te, test_y=y[te]).to(DEV)
+    torch.manual_seed(30)
+    mp = [int(r) for r in z["L3_metapath_rel"]]  # layer 0 aggregates over mp[0] (model.py:210)
+    f1 = main.mpgnn_parallel_multiple_x(d, x.shape[1], 64, int(et.max()) + 1, 64, 2, mp, True, epochs=200)
+    out = capsys.readouterr().out
+    assert "test loss" in out
+    print(out, f1)
+    assert f1 > 0.9, f1
+    val = main.mpgnn_parallel_multiple(d, x.shape[1], 64, int(et.max()) + 1, 64, 2, [mp], epochs=3)
+    assert 0.0 <= val <= 1.0

@@ -120,3 +120,23 @@ def test_seeded_init_single_layer(golden):
         assert torch.equal(conv.weight.detach(), t(g[f"F{F_in}_weight"]))
         assert torch.equal(conv.root.detach(), t(g[f"F{F_in}_root"]))
         assert torch.equal(conv.bias.detach(), t(g[f"F{F_in}_bias"]))
+
+
+def test_fast_rgcn_oracle_equals_loop_oracle():
+    """CustomFastRGCNConv's transform-then-aggregate arithmetic
+    (mp_rgcn_layer.py:324-357, 3-D weight) equals the RGCNConv loop (A6) up to summation order;
+    rows without edges get x@root + bias only."""
+    from mpgnn_amd import data
+    g = data.synthetic_graph(400, 4, 8, feat_dim=24, seed=5)
+    torch.manual_seed(0)
+    w, root, bias = torch.randn(4, 24, 16), torch.randn(24, 16), torch.randn(16)
+    a = orc.rgcn_forward(g.x, g.edge_index, g.edge_type, w, root, bias)
+    b = orc.fast_rgcn_forward(g.x, g.edge_index, g.edge_type, w, root, bias)
+    assert torch.allclose(a, b, rtol=1e-5, atol=1e-5)
+    # one relation absent from the graph, one isolated row
+    keep = (g.edge_type != 2) & (g.edge_index[0] != 7)
+    ei, et = g.edge_index[:, keep], g.edge_type[keep]
+    a = orc.rgcn_forward(g.x, ei, et, w, root, bias)
+    b = orc.fast_rgcn_forward(g.x, ei, et, w, root, bias)
+    assert torch.allclose(a, b, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(b[7], g.x[7] @ root + bias, rtol=1e-6, atol=1e-6)
