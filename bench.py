@@ -52,12 +52,30 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--layers", type=int, default=3)
-    ap.add_argument("--feat", type=int, default=128)
-    ap.add_argument("--epoch-steps", type=int, default=10)
+    ap.add_argument("--workload", default="fb15k237", choices=["fb15k237", "C2", "C5"],
+                    help="fb15k237 = C3/C4 (the headline); C2 / C5 = the other BASELINE.json configs")
+    ap.add_argument("--layers", type=int, default=None, help="default 3 (C3, C5) / 2 (C2)")
+    ap.add_argument("--feat", type=int, default=None, help="default 128 (C2, C3) / 256 (C5)")
+    ap.add_argument("--epoch-steps", type=int, default=None, help="0 skips the epoch leg (default 10; 2 at C5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=2)
-    return ap.parse_args()
+    a = ap.parse_args()
+    dflt = {"fb15k237": (3, 128, 10), "C2": (2, 128, 10), "C5": (3, 256, 2)}[a.workload]
+    a.layers = dflt[0] if a.layers is None else a.layers
+    a.feat = dflt[1] if a.feat is None else a.feat
+    a.epoch_steps = dflt[2] if a.epoch_steps is None else a.epoch_steps
+    return a
+
+
+WORKLOADS = {
+    "fb15k237": ("C3 FB15K-237 (N=14541, R=237, E=310116)",
+                 "synthetic: FB15K-237-shaped graph (38,000 real dev+test triples + relation-conditional "
+                 "samples to E=310,116), U[0,1) features, seed-10 random-init weights"),
+    "C2": ("C2 synthetic (N=100000, R=16, out-degree U{1..32})",
+           "synthetic: seeded generator of create_graph (SURVEY §8d C2), U[0,1) features, seed-10 weights"),
+    "C5": ("C5 synthetic (N=2000000, R=64, out-degree U{1..31})",
+           "synthetic: seeded generator of create_graph (SURVEY §8d C5), U[0,1) features, seed-10 weights"),
+}
 
 
 def setup_dist(n):
@@ -72,6 +90,38 @@ def setup_dist(n):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         group = dist.group.WORLD
     return rank, world, local, group
+
+
+def cpu_baseline_sampled(g, net_cpu, layers, reps):
+    """C2 / C5: the full CPU stack would take minutes to hours (R dense N×F×F GEMMs per layer),
+    so the oracle's loop body is timed for ONE relation of the first layer (index_select,
+    scatter_add_, div, mm — rgcn_oracle.rgcn_forward's iteration) and scaled by R·layers, plus
+    the root GEMM per layer; labelled as extrapolated."""
+    from oracle import rgcn_oracle as orc
+    w = net_cpu.conv1.weight.detach()
+    root = net_cpu.conv1.root.detach()
+    x, ei, et = g.x, g.edge_index, g.edge_type
+    size = (x.size(0), x.size(0))
+    with torch.no_grad():
+        times = []
+        for _ in range(reps + 1):
+            t0 = time.perf_counter()
+            tmp = orc.masked_edge_index(ei, et == 0)
+            h = orc.propagate_mean(tmp, x, size)
+            _ = h @ w[0]
+            t_rel = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            _ = x @ root
+            t_root = time.perf_counter() - t0
+            times.append((t_rel, t_root))
+    times = sorted(times[1:])
+    t_rel, t_root = times[len(times) // 2]
+    est = layers * (g.num_relations * t_rel + t_root)
+    return {"value": layers * g.num_edges / est, "unit": "edges/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle loop body for relation 0 of layer 1 ({reps} timed + 1 warm-up, median "
+                      f"{t_rel * 1e3:.1f} ms) + root GEMM ({t_root * 1e3:.1f} ms), extrapolated x{g.num_relations} "
+                      f"relations x{layers} layers = {est:.1f} s per forward (extrapolated, not run in full)"}
 
 
 def cpu_baseline(g, net_cpu, layers, reps):
@@ -109,7 +159,12 @@ def main():
     args = parse()
     rank, world, local, group = setup_dist(args.gpus)
     dev = torch.device("cuda", local)
-    g = data.fb15k237_graph(feat_dim=args.feat, seed=0)
+    if args.workload == "fb15k237":
+        g = data.fb15k237_graph(feat_dim=args.feat, seed=0)
+    else:
+        g = data.config_graph(args.workload)
+        if g.x.shape[1] != args.feat:
+            g.x = torch.rand((g.num_nodes, args.feat), generator=torch.Generator().manual_seed(1))
     F = args.feat
     torch.manual_seed(10)  # main_rgcn.py:31
     net_cpu = mpgnn_amd.Net(F, F, g.num_relations, F, 2, args.layers)
@@ -199,6 +254,9 @@ def main():
                              "replayed: every kernel runs every step, host launch overhead removed"}
         except Exception as e:  # capture unsupported here: report, keep the eager number
             graph = {"error": f"{type(e).__name__}: {e}"[:200]}
+        cg = None  # free the graph's private pool and the capture stream's workspace
+        mpgnn_amd.functional.release_workspaces()
+        torch.cuda.empty_cache()
 
     # ---- epoch (main_rgcn.py:458-461): train fwd+bwd+Adam + validation forward ------------
     opt = mpgnn_amd.main._adam(net)  # Adam(lr 0.01, wd 5e-4), fused multi-tensor kernel on the GPU
@@ -216,14 +274,16 @@ def main():
         with torch.no_grad():
             net(x, ei, et, shard=shard, group=group)
 
-    for _ in range(2):
-        epoch()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(args.epoch_steps):
-        epoch()
-    torch.cuda.synchronize()
-    epoch_ms = (time.perf_counter() - t1) * 1e3 / args.epoch_steps
+    epoch_ms = None
+    if args.epoch_steps > 0:
+        for _ in range(2):
+            epoch()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.epoch_steps):
+            epoch()
+        torch.cuda.synchronize()
+        epoch_ms = (time.perf_counter() - t1) * 1e3 / args.epoch_steps
 
     # ---- roofline of the dominant kernel (per launch, this rank) --------------------------
     S = plan.num_segments
@@ -238,7 +298,7 @@ def main():
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
-            if pmc.get("workload") == "fb15k237" and pmc.get("feat") == F and world == 1 and \
+            if pmc.get("workload") == args.workload and pmc.get("feat") == F and world == 1 and \
                     pmc.get("kernel", "").startswith("mpgnn::rel_gemm_kernel"):
                 traffic = pmc.get("hbm_bytes_per_launch")
         except Exception:
@@ -246,7 +306,10 @@ def main():
     roofline = {
         "bound": "mfma", "achieved": round(achieved_tf, 3) if achieved_tf else None, "peak": PEAK_FP32_MFMA,
         "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_MFMA, 4) if achieved_tf else None,
-        "traffic": traffic, "kernel": "rel_gemm_kernel (Y = H @ W_r, Y_root = x @ root; W_r slice held in registers; v_mfma_f32_32x32x2_f32)",
+        "traffic": traffic,
+        "kernel": ("rel_gemm_kernel (Y = H @ W_r, Y_root = x @ root; W_r slice held in registers; "
+                   "v_mfma_f32_32x32x2_f32)") if F in (64, 128) else
+                  "tile_gemm_kernel (Y = H @ W_r, Y_root = x @ root; persistent LDS-tiled; v_mfma_f32_32x32x2_f32)",
         "avg_launch_us": round(seg_avg_ms * 1e3, 2), "launches": seg_n,
         "alg_flops_per_launch": flops, "alg_bytes_per_launch": alg_bytes,
         "alg_GBps": round(alg_bytes / (seg_avg_ms * 1e-3) / 1e9, 1) if seg_n else None,
@@ -258,20 +321,22 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(g, net_cpu, args.layers, args.cpu_reps)
+            if args.workload == "fb15k237":
+                cpu = cpu_baseline(g, net_cpu, args.layers, args.cpu_reps)
+            else:
+                cpu = cpu_baseline_sampled(g, net_cpu, args.layers, args.cpu_reps)
         result = {
             "metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: FB15K-237-shaped graph (38,000 real dev+test triples + relation-conditional "
-                    "samples to E=310,116), U[0,1) features, seed-10 random-init weights",
-            "config": {"workload": "C3 FB15K-237 (N=14541, R=237, E=310116): RGCN Net stack forward, "
+            "data": WORKLOADS[args.workload][1],
+            "config": {"workload": WORKLOADS[args.workload][0] + ": RGCN Net stack forward, "
                                    f"L={args.layers}, F_in=F_hidden=F_out={F}",
                        "graph": {"nodes": g.num_nodes, "relations": g.num_relations, "edges": g.num_edges,
                                  "segments": S if world == 1 else None},
                        "parallelism": "single GPU" if world == 1 else f"dst-range shards x{world} + RCCL all-reduce"},
             "graph_replay": graph,
-            "epoch_ms": round(epoch_ms, 3),
+            "epoch_ms": round(epoch_ms, 3) if epoch_ms is not None else None,
             "epoch_def": "main_rgcn.py:458-461 train (fwd+NLL+bwd+Adam) + validation forward",
             "roofline": roofline,
             "cpu_baseline": cpu,

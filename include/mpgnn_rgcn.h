@@ -137,6 +137,11 @@ int32_t mpgnn_rel_mean_fwd(const mpgnn_plan* plan, int32_t mode, int64_t relatio
 int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* plan, int32_t mode, int64_t relation,
                                    int32_t num_relations, int32_t F_in, int32_t F_out,
                                    int64_t row_lo, int64_t row_hi, int64_t* bytes);
+/* Forward-only part of it (enough for mpgnn_rgcn_fwd / mpgnn_rgcn_fwd_act; the backward's
+ * gradient partials are not reserved) — inference / no-grad callers at C5 scale save ~50 GB. */
+int32_t mpgnn_rgcn_fwd_workspace_bytes(const mpgnn_plan* plan, int32_t mode, int64_t relation,
+                                       int32_t num_relations, int32_t F_in, int32_t F_out,
+                                       int64_t row_lo, int64_t row_hi, int64_t* bytes);
 
 /* Layer forward:  out = Σ_{r} mean_r(x) @ W_r  + x @ root + bias
  *   (mode SINGLE: the single relation `relation`, W = weight [F_in, F_out];

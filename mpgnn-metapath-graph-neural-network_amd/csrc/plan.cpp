@@ -383,6 +383,13 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
     p->rel_t32_ptr.assign(R + 1, 0);
     p->t32_cost.assign(1, 0);
     p->rel_chunk_ptr.assign(R + 1, 0);
+    // Reduction chunk length: kChunkRows, grown with the graph so that there are about
+    // kChunkTarget chunks in all. Every chunk writes an F_in × F_out partial slab that the
+    // reduce kernel reads back, so at C5 (S = 27.5 M, F = 256) 128-row chunks would write as
+    // many slab bytes as the whole input of dW (56 GB); 4096 chunks keep the slabs at ~1 GB
+    // and still give > 16 workgroups per CU.
+    const int64_t s_all = p->rel_seg_ptr[R];
+    const int32_t chunk_cap = (int32_t)std::max<int64_t>(kChunkRows, (s_all + kChunkTarget - 1) / kChunkTarget + 31) / 32 * 32;
     for (int64_t d = 0; d < R; ++d) {
         for (int32_t s = p->rel_seg_ptr[d]; s < p->rel_seg_ptr[d + 1]; s += kTile32) {
             p->t32_begin.push_back(s);
@@ -398,9 +405,9 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
             p->tile_end.push_back(std::min<int32_t>(s + kTileRows, p->rel_seg_ptr[d + 1]));
         }
         p->rel_tile_ptr[d + 1] = (int32_t)p->tile_begin.size();
-        // balanced chunks of at most kChunkRows segments (multiples of 32 rows but the last)
+        // balanced chunks of at most chunk_cap segments (multiples of 32 rows but the last)
         const int32_t sb = p->rel_seg_ptr[d], se = p->rel_seg_ptr[d + 1];
-        const int32_t nch = (se - sb + kChunkRows - 1) / kChunkRows;
+        const int32_t nch = (se - sb + chunk_cap - 1) / chunk_cap;
         const int32_t per = nch > 0 ? ((se - sb + nch - 1) / nch + 31) / 32 * 32 : 0;
         for (int32_t s = sb; s < se; s += per) {
             p->chunk_begin.push_back(s);

@@ -27,6 +27,7 @@ inline int32_t item_cost(int64_t edges) {
 // Relation-pure reduction chunks for the weight gradient (outer_accum_kernel): at most this
 // many segments, balanced within a relation (bounds the longest workgroup's MFMA chain).
 constexpr int kChunkRows = 128;
+constexpr int64_t kChunkTarget = 4096;  // reduction chunks per graph (chunk length grows past kChunkRows)
 // Ragged lists: a run (segment / gathered row) longer than this many entries is cut into
 // ordered pieces of at most kPieceEntries, summed by piece_sum_kernel; consumers then add the
 // piece partials in order.  Bounds the serial work of every wave (hub skew).

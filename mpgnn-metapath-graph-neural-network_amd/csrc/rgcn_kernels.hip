@@ -2829,7 +2829,8 @@ static RootChunks root_chunks(int64_t lo, int64_t hi) {
 struct WsLayout {
     size_t y = 0, yroot = 0, hf = 0, pseg = 0, prw = 0;     // forward
     size_t g = 0, groot = 0, h = 0, pdx = 0, p = 0, proot = 0, pb = 0;  // backward
-    size_t total = 0;
+    size_t total = 0;      // max(forward, backward): what mpgnn_rgcn_bwd needs
+    size_t fwd_total = 0;  // forward part only (mpgnn_rgcn_fwd / _fwd_act)
 };
 
 static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s, int F_in, int F_out,
@@ -2849,6 +2850,7 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
                                                                      (size_t)p->rwx_f.nslots})
                                                          : 0) * F_out * sizeof(float));
     const size_t fwd = off;
+    w.fwd_total = std::max<size_t>(fwd, 256);
     off = 0;
     const size_t dx_pieces = (mode == MPGNN_MODE_ALL)
                                  ? std::max({p->t_l.piece_b.size(), (size_t)p->t_f.nslots, (size_t)p->tx_f.nslots})
@@ -3337,6 +3339,20 @@ int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* p, int32_t mode, int64_t re
     WsLayout w = ws_layout(p, mode, s, std::max(F_in, 1), std::max(F_out, 1), row_lo, row_hi,
                            root_chunks(row_lo, row_hi));
     *bytes = (int64_t)w.total;
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_rgcn_fwd_workspace_bytes(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R,
+                                       int32_t F_in, int32_t F_out, int64_t row_lo, int64_t row_hi,
+                                       int64_t* bytes) {
+    if (!p || !bytes) return arg_error("NULL argument");
+    Selection s;
+    int32_t st = make_selection(p, mode, relation, R, &s);
+    if (st != MPGNN_OK) return st;
+    clamp_rows(p, &row_lo, &row_hi);
+    WsLayout w = ws_layout(p, mode, s, std::max(F_in, 1), std::max(F_out, 1), row_lo, row_hi,
+                           root_chunks(row_lo, row_hi));
+    *bytes = (int64_t)w.fwd_total;
     return MPGNN_OK;
 }
 

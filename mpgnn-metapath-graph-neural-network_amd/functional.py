@@ -54,9 +54,19 @@ def _workspace(nbytes: int, device: torch.device) -> torch.Tensor:
     key = (device.index, torch.cuda.current_stream(device).cuda_stream)
     ws = _WS.get(key)
     if ws is None or ws.numel() < nbytes:
+        # drop the smaller buffer first: the caching allocator hands its block back in stream
+        # order, so the peak is the new size, not old + new (matters at C5: ~58 GB each)
+        _WS.pop(key, None)
+        del ws
         ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         _WS[key] = ws
     return ws
+
+
+def release_workspaces() -> None:
+    """Drop the cached per-(device, stream) scratch buffers (e.g. after a HIP-graph capture on
+    a side stream); the next call allocates again."""
+    _WS.clear()
 
 
 def _forward(x, weight, root, bias, plan: GraphPlan, mode: int, relation: int, num_relations: int,
@@ -74,7 +84,8 @@ def _forward(x, weight, root, bias, plan: GraphPlan, mode: int, relation: int, n
         raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({N}x{f_in} and "
                            f"{weight.shape[-2]}x{f_out})")
     seg_b, seg_e = plan.select(mode, relation, num_relations)
-    ws = _workspace(plan.workspace_bytes(mode, relation, num_relations, f_in, f_out, row_lo, row_hi), x.device)
+    ws = _workspace(plan.workspace_bytes(mode, relation, num_relations, f_in, f_out, row_lo, row_hi,
+                                         forward_only=True), x.device)
     out = torch.empty(N, f_out, dtype=torch.float32, device=x.device)
     # segment means, kept for grad_weight (dW_r = Σ h_segᵀ dout[node_1])
     h_save = torch.empty(seg_e - seg_b, f_in, dtype=torch.float32, device=x.device) if need_h else None

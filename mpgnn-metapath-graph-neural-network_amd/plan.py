@@ -113,14 +113,15 @@ class GraphPlan:
                                     out.nbytes), "mpgnn_plan_export")
         return out
 
-    def workspace_bytes(self, mode, relation, num_relations, f_in, f_out, row_lo, row_hi) -> int:
-        key = (mode, int(relation), int(num_relations), f_in, f_out, row_lo, row_hi)
+    def workspace_bytes(self, mode, relation, num_relations, f_in, f_out, row_lo, row_hi,
+                        forward_only: bool = False) -> int:
+        key = (mode, int(relation), int(num_relations), f_in, f_out, row_lo, row_hi, forward_only)
         hit = self._ws_cache.get(key)
         if hit is not None:
             return hit
         b = ctypes.c_int64()
-        check(lib.mpgnn_rgcn_workspace_bytes(self._h, mode, int(relation), int(num_relations),
-                                             f_in, f_out, row_lo, row_hi, ctypes.byref(b)),
+        fn = lib.mpgnn_rgcn_fwd_workspace_bytes if forward_only else lib.mpgnn_rgcn_workspace_bytes
+        check(fn(self._h, mode, int(relation), int(num_relations), f_in, f_out, row_lo, row_hi, ctypes.byref(b)),
               "mpgnn_rgcn_workspace_bytes")
         self._ws_cache[key] = int(b.value)
         return self._ws_cache[key]
