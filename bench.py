@@ -288,7 +288,10 @@ def main():
     # ---- roofline of the dominant kernel (per launch, this rank) --------------------------
     S = plan.num_segments
     E_loc = plan.num_edges
-    seg_avg_ms = seg_ms / max(seg_n, 1)
+    # the layer's transform may be split over several launches (root rows + relation groups,
+    # MPGNN_OPT_OVERLAP): the roofline is per LAYER = the summed durations of its launches
+    layer_calls = args.steps * args.layers
+    seg_avg_ms = seg_ms / max(layer_calls, 1)
     n_root = plan.num_nodes if world == 1 else (shard[1] - shard[0])
     flops = 2.0 * (S + n_root) * F * F   # Y = H @ W_r over S segment rows + Y_root = x @ root
     alg_bytes = 4 * F * (2 * S + 2 * n_root) + 4 * F * F * (plan.num_relations_present + 1)  # A rows in, Y out, W
@@ -311,6 +314,9 @@ def main():
                    "v_mfma_f32_32x32x2_f32)") if F in (64, 128) else
                   "tile_gemm_kernel (Y = H @ W_r, Y_root = x @ root; persistent LDS-tiled; v_mfma_f32_32x32x2_f32)",
         "avg_launch_us": round(seg_avg_ms * 1e3, 2), "launches": seg_n,
+        "launches_per_layer": round(seg_n / max(layer_calls, 1), 2),
+        "note": "avg_launch_us = summed duration of one layer's transform launches (root rows + relation "
+                "groups; they run on a second stream beside the segment means, so contention is included)",
         "alg_flops_per_launch": flops, "alg_bytes_per_launch": alg_bytes,
         "alg_GBps": round(alg_bytes / (seg_avg_ms * 1e-3) / 1e9, 1) if seg_n else None,
         "hbm_frac_if_streamed": round(alg_bytes / (seg_avg_ms * 1e-3) / 1e9 / PEAK_HBM, 4) if seg_n else None,

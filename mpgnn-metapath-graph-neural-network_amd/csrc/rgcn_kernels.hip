@@ -2786,10 +2786,26 @@ struct Selection {
     bool all_segments = false;    // selection covers every local segment
 };
 
+static void fill_selection(const mpgnn_plan* p, Selection* s);
+
 static int32_t make_selection(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, Selection* s) {
     int32_t st = select_relations(p, mode, relation, R, &s->d_lo, &s->d_hi);
     if (st != MPGNN_OK) return st;
     if (p->nrel == 0) return MPGNN_OK;
+    fill_selection(p, s);
+    return MPGNN_OK;
+}
+
+// Sub-selection of the dense relation range [d_lo, d_hi) (overlapped forward groups).
+static Selection range_selection(const mpgnn_plan* p, int64_t d_lo, int64_t d_hi) {
+    Selection s;
+    s.d_lo = d_lo;
+    s.d_hi = d_hi;
+    if (p->nrel > 0) fill_selection(p, &s);
+    return s;
+}
+
+static void fill_selection(const mpgnn_plan* p, Selection* s) {
     s->sel_b = p->rel_seg_ptr[s->d_lo];
     s->sel_e = p->rel_seg_ptr[s->d_hi];
     s->t_lo = p->rel_tile_ptr[s->d_lo];
@@ -2805,7 +2821,6 @@ static int32_t make_selection(const mpgnn_plan* p, int32_t mode, int64_t relatio
     s->ta_e_lo = p->rel_ta_ent_ptr[s->d_lo];
     s->ta_e_hi = p->rel_ta_ent_ptr[s->d_hi];
     s->all_segments = (s->sel_b == 0 && s->sel_e == p->S);
-    return MPGNN_OK;
 }
 
 static size_t align256(size_t b) { return (b + 255) / 256 * 256; }
@@ -3269,6 +3284,90 @@ static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x
     return run_rowsum(p, a, p->d.seg_pb, p->d.seg_pe, ragged ? s.sp_lo : 0, ragged ? s.sp_hi : 0, Pseg, strm);
 }
 
+// ----------------------------------------------------------------------------------------
+// Overlapped forward (MPGNN_OPT_OVERLAP): the segment means (gather-bound, flat_rows_kernel)
+// and the transform (MFMA-bound, rel_gemm_kernel / tile_gemm_kernel) of one layer run on two
+// streams.  The relation range is cut into G groups of about equal segment count; the caller's
+// stream computes the means group by group and records an event after each; a second
+// (high-priority) stream first transforms the root rows (x @ root needs no means, so it runs
+// beside group 0's means), then each group's segment rows as soon as its event fires, and
+// the caller's stream joins it before the combine.  Same kernels, same work, same results
+// (each output element is produced by the same kernel code from the same inputs).
+// ----------------------------------------------------------------------------------------
+constexpr int kMaxOverlapGroups = 8;
+static int g_overlap = 0;  // groups; 0 (default) = off: one stream. Measured slower at C3
+
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t in = nullptr, done = nullptr, grp[kMaxOverlapGroups] = {};
+    bool ok = false, failed = false;
+};
+static SideStream g_side[64];
+static std::mutex g_side_mu;
+
+static SideStream* side_stream(int device) {
+    if (device < 0 || device >= 64) return nullptr;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != device) return nullptr;
+    std::lock_guard<std::mutex> lk(g_side_mu);
+    SideStream& ss = g_side[device];
+    if (ss.ok) return &ss;
+    if (ss.failed) return nullptr;
+    int lo = 0, hi = 0;
+    bool good = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+                hipStreamCreateWithPriority(&ss.s, hipStreamNonBlocking, hi) == hipSuccess &&
+                hipEventCreateWithFlags(&ss.in, hipEventDisableTiming) == hipSuccess &&
+                hipEventCreateWithFlags(&ss.done, hipEventDisableTiming) == hipSuccess;
+    for (int g = 0; good && g < kMaxOverlapGroups; ++g)
+        good = hipEventCreateWithFlags(&ss.grp[g], hipEventDisableTiming) == hipSuccess;
+    ss.ok = good;
+    ss.failed = !good;
+    return good ? &ss : nullptr;
+}
+
+// Means + transform of the selection s with the overlap above. H / Y rows are offset from
+// s.sel_b, Yroot rows from row_lo (as in the one-stream path).
+static int32_t fwd_overlapped(const mpgnn_plan* p, int32_t mode, const Selection& s, int groups, SideStream* ss,
+                              const float* x, int F_in, const float* weight, const float* root, int F_out, float* H,
+                              float* Pseg, float* Y, float* Yroot, int64_t row_lo, int64_t row_hi, hipStream_t strm) {
+    int32_t st = hip_check(hipEventRecord(ss->in, strm), "hipEventRecord");
+    if (st == MPGNN_OK) st = hip_check(hipStreamWaitEvent(ss->s, ss->in, 0), "hipStreamWaitEvent");
+    if (st != MPGNN_OK) return st;
+    if (root != nullptr) {  // root rows: no dependency on the means
+        Selection none = s;
+        none.t_lo = none.t_hi = none.t32_lo = none.t32_hi = 0;
+        st = run_seg(p, mode, none, 2, x, F_in, weight, root, 0, F_out, Y, Yroot, row_lo, row_hi, nullptr, nullptr,
+                     true, MPGNN_K_SEG_FWD, ss->s, H);
+        if (st != MPGNN_OK) return st;
+    }
+    const int64_t S_sel = s.sel_e - s.sel_b;
+    int64_t d = s.d_lo;
+    for (int g = 0; g < groups && d < s.d_hi; ++g) {
+        // group g ends at the first relation boundary at or past (g+1)/G of the segments
+        const int64_t target = s.sel_b + (S_sel * (g + 1) + groups - 1) / groups;
+        int64_t d_end = d + 1;
+        while (d_end < s.d_hi && p->rel_seg_ptr[d_end] < target) ++d_end;
+        if (g == groups - 1) d_end = s.d_hi;
+        const Selection sub = range_selection(p, d, d_end);
+        const size_t off = (size_t)(sub.sel_b - s.sel_b);
+        {
+            TimedLaunch tl(MPGNN_K_MEAN, strm);
+            st = run_means(p, sub, x, F_in, H + off * F_in, Pseg, false, strm);
+            if (st != MPGNN_OK) return st;
+        }
+        st = hip_check(hipEventRecord(ss->grp[g], strm), "hipEventRecord");
+        if (st == MPGNN_OK) st = hip_check(hipStreamWaitEvent(ss->s, ss->grp[g], 0), "hipStreamWaitEvent");
+        if (st != MPGNN_OK) return st;
+        st = run_seg(p, mode, sub, 2, x, F_in, weight, nullptr, 0, F_out, Y + off * F_out, nullptr, row_lo, row_hi,
+                     nullptr, nullptr, true, MPGNN_K_SEG_FWD, ss->s, H + off * F_in);
+        if (st != MPGNN_OK) return st;
+        d = d_end;
+    }
+    st = hip_check(hipEventRecord(ss->done, ss->s), "hipEventRecord");
+    if (st == MPGNN_OK) st = hip_check(hipStreamWaitEvent(strm, ss->done, 0), "hipStreamWaitEvent");
+    return st;
+}
+
 }  // namespace mpgnn
 
 using namespace mpgnn;
@@ -3276,6 +3375,11 @@ using namespace mpgnn;
 extern "C" {
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_OVERLAP) {
+        if (value < 0 || value > kMaxOverlapGroups) return arg_error("MPGNN_OPT_OVERLAP must be 0..8");
+        g_overlap = (int)value;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_EXACT_ORDER) {
         g_exact_order = value != 0;
         return MPGNN_OK;
@@ -3436,6 +3540,14 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     } else {
         // 1) H[seg] = mean(x over seg)  (the saved means when training)
         float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
+        SideStream* ss = (g_overlap > 0 && !exact && g_stamps == nullptr && g_ablate == 0 && s.sel_e > s.sel_b)
+                             ? side_stream(p->device) : nullptr;
+        if (ss != nullptr) {
+            const int groups = mode == MPGNN_MODE_ALL ? g_overlap : 1;
+            st = fwd_overlapped(p, mode, s, groups, ss, x, F_in, weight, root, F_out, H,
+                                reinterpret_cast<float*>(ws + w.pseg), Y, Yroot, row_lo, row_hi, strm);
+            if (st != MPGNN_OK) return st;
+        } else {
         {
             TimedLaunch tl(MPGNN_K_MEAN, strm);
             st = run_means(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
@@ -3445,6 +3557,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         st = run_seg(p, mode, s, 2, x, F_in, weight, root, 0, F_out, Y, Yroot, row_lo, row_hi, nullptr, nullptr, true,
                      MPGNN_K_SEG_FWD, strm, H);
         if (st != MPGNN_OK) return st;
+        }
     }
 
     // 2) out[i] = (Σ_{seg of row i, relation order} Y[seg] + Yroot[i]) + bias
