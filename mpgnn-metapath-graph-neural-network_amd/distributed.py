@@ -16,7 +16,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-__all__ = ["shard_ranges", "edge_balanced_ranges"]
+__all__ = ["shard_ranges", "edge_balanced_ranges", "rank_slice", "metapath_fanout", "best_metapaths"]
 
 
 def edge_balanced_ranges(gathered: np.ndarray | torch.Tensor, num_nodes: int, world: int) -> list[tuple[int, int]]:
@@ -40,3 +40,52 @@ def shard_ranges(edge_index: torch.Tensor, num_nodes: int, world: int,
     """Per-rank gathered-node ranges for ``edge_index`` (row 1 under target_to_source)."""
     gathered = edge_index[1] if flow == "target_to_source" else edge_index[0]
     return edge_balanced_ranges(gathered, num_nodes, world)
+
+
+# ---------------------------------------------------------------------------------------
+# metapath-candidate fan-out (SURVEY §8f #3): replicas only
+# ---------------------------------------------------------------------------------------
+def rank_slice(items: list, world: int, rank: int) -> list:
+    """The contiguous share of ``items`` rank ``rank`` trains (main.py:1432-1438: the first
+    ``len % world`` ranks take one extra item; ≡ np.array_split(items, world)[rank],
+    main.py:1319)."""
+    n = len(items)
+    size, rem = n // world, n % world
+    start = rank * size + min(rank, rem)
+    return items[start:start + size + (1 if rank < rem else 0)]
+
+
+def metapath_fanout(data_mpgnn, input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, metapaths,
+                    group=None, train_fn=None, **train_kw) -> dict:
+    """Score every candidate metapath with ``mpgnn_parallel_multiple`` (main.py:1117) across
+    the ranks of ``group`` — main.py:1430-1449: each rank trains its contiguous share of
+    ``metapaths`` (one MPNetm per metapath, on its own GPU) and the {str(metapath): validation
+    macro F1} dicts are gathered. The reference gathers to rank 0 over mpi4py; here every rank
+    gets the merged dict (all_gather_object over torch.distributed). Candidates are
+    independent trainings: no data-path collective, one object gather at the end.
+    ``train_fn`` defaults to ``main.mpgnn_parallel_multiple`` (extra keywords go to it)."""
+    import torch.distributed as dist
+    if train_fn is None:
+        from .main import mpgnn_parallel_multiple as train_fn
+    if group is not None or (dist.is_available() and dist.is_initialized()):
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+    else:
+        world, rank = 1, 0
+    partial = {}
+    for meta in rank_slice(list(metapaths), world, rank):
+        partial[str(meta)] = train_fn(data_mpgnn, input_dim, hidden_dim, num_rel, output_dim, ll_output_dim,
+                                      [meta], **train_kw)
+    if world == 1:
+        return partial
+    gathered = [None] * world
+    dist.all_gather_object(gathered, partial, group=group)
+    final = {}
+    for d in gathered:  # rank order, as the reference's final_dict.update loop (main.py:1447-1449)
+        final.update(d)
+    return final
+
+
+def best_metapaths(scores: dict, k: int = 3) -> dict:
+    """main.py:1451-1452: the ``k`` best candidates by score, descending (stable for ties)."""
+    ordered = dict(sorted(scores.items(), key=lambda item: item[1], reverse=True))
+    return dict(list(ordered.items())[:k])

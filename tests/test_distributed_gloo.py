@@ -97,3 +97,63 @@ def test_dst_sharded_allreduce_matches_unsharded(name):
         p.join(timeout=60)
     for rank, ok, msgs in results:
         assert ok, (rank, msgs)
+
+
+# ------------------------------------------------------------------------------------------
+# metapath-candidate fan-out (main.py:1430-1452): replicas only
+# ------------------------------------------------------------------------------------------
+def _fake_train(data, input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, metapaths, **kw):
+    meta = metapaths[0]
+    return float(sum((i + 1) * r for i, r in enumerate(meta)) % 7) / 7.0 + kw.get("bump", 0.0)
+
+
+def _fanout_worker(rank, world, port, cands, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from mpgnn_amd import distributed as mdist
+        seen = []
+
+        def train(*a, **kw):
+            seen.append(a[6][0])
+            return _fake_train(*a, **kw)
+        scores = mdist.metapath_fanout(None, 2, 64, 4, 64, 2, cands, train_fn=train, bump=0.0)
+        q.put((rank, seen, scores))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, None, repr(e)))
+
+
+def test_rank_slice_matches_reference_partition():
+    from mpgnn_amd.distributed import rank_slice
+    for n in range(0, 12):
+        items = list(range(n))
+        for world in (1, 2, 3, 8):
+            parts = [rank_slice(items, world, r) for r in range(world)]
+            assert sum(parts, []) == items
+            ref = [list(a) for a in np.array_split(np.arange(n), world)]
+            assert [list(p) for p in parts] == ref
+
+
+def test_metapath_fanout_world2_gloo():
+    cands = [[1, 0], [2], [0, 2, 1], [3, 3], [1], [2, 0]]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fanout_worker, args=(r, 2, port, cands, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    res.sort(key=lambda t: t[0])
+    assert all(r[1] is not None for r in res), res
+    assert res[0][1] == cands[:3] and res[1][1] == cands[3:]          # contiguous shares
+    expected = {str(m): _fake_train(None, 0, 0, 0, 0, 0, [m]) for m in cands}
+    assert res[0][2] == expected and res[1][2] == expected            # every rank has the merged dict
+    from mpgnn_amd.distributed import best_metapaths
+    best = best_metapaths(expected)
+    assert list(best.values()) == sorted(expected.values(), reverse=True)[:3]

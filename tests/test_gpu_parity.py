@@ -685,3 +685,35 @@ def test_c2_layer_backward_long_reduction_chunks():
     rel_close(xg.grad, xs.grad, what="C2 dx")
     for name, pg, pr in zip(("dW", "droot", "dbias"), (convg.weight, convg.root, convg.bias), params):
         rel_close(pg.grad, pr.grad, what="C2 " + name)
+
+
+@pytest.mark.parametrize("groups", [1, 2, 3, 8])
+def test_overlapped_forward_bitwise_equal(groups):
+    """MPGNN_OPT_OVERLAP: means and transform pipelined over two streams produce the same bits
+    as the one-stream forward (same kernels, same inputs), mode ALL and SINGLE, with and
+    without saved means (training)."""
+    from mpgnn_amd import _lib
+    g = data.config_graph("fb15k237")
+    torch.manual_seed(30)
+    conv = mpgnn_amd.RGCNConv(128, 128, g.num_relations, flow="target_to_source").to(DEV)
+    single = mpgnn_amd.CustomRGCNConv(128, 128, 1, flow="target_to_source").to(DEV)
+    x, ei, et = g.x.to(DEV), g.edge_index.to(DEV), g.edge_type.to(DEV)
+
+    def run():
+        xg = x.clone().requires_grad_(True)
+        out = conv(xg, ei, et, activation="relu")
+        out.sum().backward()
+        with torch.no_grad():
+            o2 = conv(x, ei, et)
+            o3 = single(0, 5, x, ei, et)
+        return [out.detach().clone(), xg.grad.clone(), conv.weight.grad.clone(), o2, o3]
+
+    ref = run()
+    conv.zero_grad()
+    _lib.check(_lib.lib.mpgnn_set_option(8, groups))
+    try:
+        got = run()
+    finally:
+        _lib.lib.mpgnn_set_option(8, 0)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)

@@ -210,3 +210,30 @@ def test_mpgnn_parallel_multiple_x_learns_planted_metapath(golden, capsys):
     assert f1 > 0.9, f1
     val = main.mpgnn_parallel_multiple(d, x.shape[1], 64, int(et.max()) + 1, 64, 2, [mp], epochs=3)
     assert 0.0 <= val <= 1.0
+
+
+@pytest.mark.gpu
+def test_metapath_fanout_single_rank_trains_each_candidate(golden):
+    """main.py:1430-1452 on one rank: every candidate metapath is trained with
+    mpgnn_parallel_multiple and scored; the planted metapath is among the best."""
+    from mpgnn_amd import distributed as mdist
+    z = golden("kat_synthetic.npz")
+    link, node, label = z["L3_link"], z["L3_node"], z["L3_label"]
+    n = node.shape[0]
+    y = torch.zeros(n, dtype=torch.int64)
+    y[torch.from_numpy(label[:, 0])] = torch.from_numpy(label[:, 1])
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(0))
+    tr, va, te = perm[: n * 6 // 10], perm[n * 6 // 10: n * 8 // 10], perm[n * 8 // 10:]
+    d = main.Data(x=torch.from_numpy(node[:, 1:].astype(np.float32)),
+                  edge_index=torch.from_numpy(np.stack([link[:, 0], link[:, 2]])),
+                  edge_type=torch.from_numpy(link[:, 1].copy()), train_idx=tr, train_y=y[tr], val_idx=va,
+                  val_y=y[va], test_idx=te, test_y=y[te]).to(DEV)
+    planted = [int(r) for r in z["L3_metapath_rel"]]
+    cands = [planted, [0, 0], [2, 1], [1]]
+    torch.manual_seed(30)
+    scores = mdist.metapath_fanout(d, 2, 64, int(link[:, 1].max()) + 1, 64, 2, cands, epochs=150)
+    assert set(scores) == {str(c) for c in cands}
+    assert all(0.0 <= v <= 1.0 for v in scores.values())
+    best = mdist.best_metapaths(scores, k=1)
+    assert scores[str(planted)] == max(scores.values()), scores
+    assert list(best) == [str(planted)] or scores[list(best)[0]] == scores[str(planted)]
