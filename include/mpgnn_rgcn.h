@@ -195,9 +195,12 @@ enum mpgnn_option {
     MPGNN_OPT_REL_GEMM = 5, /* 1 (default): B-stationary GEMM (weights in registers) for F_in, F_out in {64,128} x {128}; 0: tile GEMM */
     MPGNN_OPT_FUSED = 6,    /* 1: forward means + transform fused in one launch for F_in = F_out = 128; 0 (default): two launches */
     MPGNN_OPT_FLAT_U = 7,   /* 16 (default) or 32: x rows in flight per wave in the flat row-sum kernel (same results) */
-    MPGNN_OPT_OVERLAP = 8   /* forward: segment means and transform of G relation groups pipelined over the caller's
+    MPGNN_OPT_OVERLAP = 8,  /* forward: segment means and transform of G relation groups pipelined over the caller's
                                stream and a second stream (1..8 groups; 0 = one stream, the default: at C3 the two kernels contend for
                                the CUs and the cross-stream events cost more than the overlap gains); same results */
+    MPGNN_OPT_REL_WGS = 9,  /* rel_gemm_kernel workgroups per CU: 2 (default) or 1; same results */
+    MPGNN_OPT_REL_STAGGER = 10 /* rel_gemm_kernel: the second half of the grid first sleeps this many 64-clock
+                                  quanta (de-phases the two workgroups of a CU); same results */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

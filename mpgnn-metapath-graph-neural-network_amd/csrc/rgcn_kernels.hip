@@ -1053,6 +1053,7 @@ struct RelGemmArgs {
     float* Y;             // rows s - sel_b
     float* Yroot;         // rows i - row_lo
     int sel_b, row_lo, row_hi;
+    int stagger;                 // s_sleep quanta (64 clk) the second half of the grid waits first
     unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][32] s_memtime timeline, or nullptr
 };
 
@@ -1196,6 +1197,10 @@ struct RelGemm {
             if (stp != nullptr && tid == 0) stp[k] = __builtin_amdgcn_s_memrealtime();
         };
         stamp_rt(30);
+        // the two workgroups of a CU (blocks b and b + G/2 under the dispatcher's fill order)
+        // otherwise run their MFMA and load/store phases in lockstep: offset the second one
+        if (a.stagger > 0 && (int)blockIdx.x >= G / 2)
+            for (int k = 0; k < a.stagger; ++k) __builtin_amdgcn_s_sleep(1);
         stamp(0);
 
         float4 v[WPT];
@@ -1208,6 +1213,12 @@ struct RelGemm {
         float b[KH];
         load_b(cur.w, wave, lane, b);
         commit(cur, tid, v, cnt, As, Sc);
+        // Consume the prologue's weight loads here. Otherwise the wait-count pass merges their
+        // pending state into the loop header and, in EVERY iteration, makes the MFMAs wait on
+        // vmcnt values that only the in-flight prefetches (next A tile, next weight slice)
+        // can satisfy — serialising the prefetch latency with the MFMA chain.
+#pragma unroll
+        for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(b[j]));
         __syncthreads();
         stamp(1);
         int buf = 0;
@@ -2705,6 +2716,8 @@ static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
 }
 
 
+static int g_rel_stagger = 0;    // MPGNN_OPT_REL_STAGGER: s_sleep quanta for the second half of the grid
+static int g_rel_wg_per_cu = 2;  // MPGNN_OPT_REL_WGS: rel_gemm_kernel workgroups per CU (1 or 2)
 static bool g_rel_gemm = true;  // MPGNN_OPT_REL_GEMM: B-stationary GEMM for K ∈ {64, 128}, N = 128
 static bool g_fused = false;    // MPGNN_OPT_FUSED: fused means + transform for F_in = F_out = 128 (opt-in: latency-bound today)
 
@@ -2713,7 +2726,7 @@ static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
     constexpr int lda = 64 * KB + 4;
     const size_t lds = (size_t)(2 * 32 * lda + 64) * sizeof(float);
     const int n_items = a.n_rel + a.n_root;
-    const int grid = std::min(n_items, cu_count() * 2);
+    const int grid = std::min(n_items, cu_count() * g_rel_wg_per_cu);
     hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
@@ -2953,6 +2966,7 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         r.row_lo = (int)row_lo;
         r.row_hi = (int)row_hi;
         r.stamps = (kind == MPGNN_K_SEG_FWD) ? g_stamps : nullptr;
+        r.stagger = g_rel_stagger;
         TimedLaunch tl(kind, strm);
         launch_rel_gemm(r, K, gather_kind == 1, strm);
         return hip_check(hipGetLastError(), "rel_gemm_kernel launch");
@@ -3375,6 +3389,16 @@ using namespace mpgnn;
 extern "C" {
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_REL_STAGGER) {
+        if (value < 0 || value > 4096) return arg_error("MPGNN_OPT_REL_STAGGER must be 0..4096");
+        g_rel_stagger = (int)value;
+        return MPGNN_OK;
+    }
+    if (option == MPGNN_OPT_REL_WGS) {
+        if (value != 1 && value != 2) return arg_error("MPGNN_OPT_REL_WGS must be 1 or 2");
+        g_rel_wg_per_cu = (int)value;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_OVERLAP) {
         if (value < 0 || value > kMaxOverlapGroups) return arg_error("MPGNN_OPT_OVERLAP must be 0..8");
         g_overlap = (int)value;
