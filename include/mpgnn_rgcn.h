@@ -199,8 +199,10 @@ enum mpgnn_option {
                                stream and a second stream (1..8 groups; 0 = one stream, the default: at C3 the two kernels contend for
                                the CUs and the cross-stream events cost more than the overlap gains); same results */
     MPGNN_OPT_REL_WGS = 9,  /* rel_gemm_kernel workgroups per CU: 2 (default) or 1; same results */
-    MPGNN_OPT_REL_STAGGER = 10 /* rel_gemm_kernel: the second half of the grid first sleeps this many 64-clock
+    MPGNN_OPT_REL_STAGGER = 10, /* rel_gemm_kernel: the second half of the grid first sleeps this many 64-clock
                                   quanta (de-phases the two workgroups of a CU); same results */
+    MPGNN_OPT_PLAN_THREADS = 11 /* host threads of mpgnn_plan_create: 0 (default) = hardware concurrency capped
+                                   at 16; the tables do not depend on it */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

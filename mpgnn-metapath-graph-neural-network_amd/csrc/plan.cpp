@@ -18,10 +18,14 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "plan_internal.h"
@@ -69,43 +73,155 @@ int32_t select_relations(const mpgnn_plan* p, int32_t mode, int64_t relation, in
     return fail(MPGNN_ERR_ARG, "unknown mode " + std::to_string(mode));
 }
 
+// ---- host parallelism ------------------------------------------------------------------
+// The build is a chain of O(E) passes with scattered accesses (32 M edges at C5). Passes over
+// independent elements split into contiguous thread ranges; the counting sorts keep their
+// stability by giving thread t the t-th contiguous slice of the input and the t-th slot of
+// every bucket. Results do not depend on the thread count (tests/test_plan.py).
+int g_plan_threads = 0;  // MPGNN_OPT_PLAN_THREADS: 0 = hardware concurrency, capped at 16
+static constexpr int64_t kParMin = 1 << 16;  // fewer elements: one thread
+
+static int plan_threads(int64_t n) {
+    if (n < kParMin) return 1;
+    int t = g_plan_threads > 0 ? g_plan_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    return (int)std::max<int64_t>(1, std::min<int64_t>(t, n / (kParMin / 4)));
+}
+
+// fn(t, begin, end) over T contiguous ranges of [0, n)
+template <class Fn>
+static void parallel_ranges(int64_t n, int T, Fn fn) {
+    if (T <= 1) {
+        fn(0, (int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> pool;
+    pool.reserve(T - 1);
+    for (int t = 1; t < T; ++t) pool.emplace_back([&, t] { fn(t, n * t / T, n * (t + 1) / T); });
+    fn(0, (int64_t)0, n / T);
+    for (auto& th : pool) th.join();
+}
+
+template <class Fn>
+static void parallel_for(int64_t n, Fn fn) {
+    parallel_ranges(n, plan_threads(n), [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) fn(i);
+    });
+}
+
+// Exclusive prefix sum in place; returns the total.
+static int64_t exclusive_scan(std::vector<int32_t>& v) {
+    int64_t acc = 0;
+    for (auto& x : v) {
+        const int64_t c = x;
+        x = (int32_t)acc;
+        acc += c;
+    }
+    return acc;
+}
+
+// Starts of the runs of [0, n) where same(a - 1, a) is false (a = 0 always starts), then n.
+template <class SameFn>
+static std::vector<int32_t> run_starts(int64_t n, SameFn same) {
+    std::vector<uint8_t> head(n);
+    parallel_for(n, [&](int64_t a) { head[a] = a == 0 || !same(a - 1, a); });
+    const int T = plan_threads(n);
+    std::vector<int64_t> part(T + 1, 0);
+    parallel_ranges(n, T, [&](int t, int64_t b, int64_t e) {
+        int64_t c = 0;
+        for (int64_t a = b; a < e; ++a) c += head[a];
+        part[t + 1] = c;
+    });
+    for (int t = 0; t < T; ++t) part[t + 1] += part[t];
+    std::vector<int32_t> starts(part[T] + 1, (int32_t)n);
+    parallel_ranges(n, T, [&](int t, int64_t b, int64_t e) {
+        int64_t w = part[t];
+        for (int64_t a = b; a < e; ++a)
+            if (head[a]) starts[w++] = (int32_t)a;
+    });
+    return starts;
+}
+
 // Stable counting sort of `items` by key(item) in [0, nkeys). Returns the bucket pointers.
 template <class KeyFn>
 static void counting_sort(const std::vector<int32_t>& items, int64_t nkeys, KeyFn key,
                           std::vector<int32_t>& out, std::vector<int32_t>* ptr_out) {
+    const int64_t n = (int64_t)items.size();
+    // per-thread histograms cost T·nkeys: use threads only when the input dominates
+    const int T = (nkeys <= 4 * n) ? plan_threads(n) : 1;
     std::vector<int32_t> ptr(nkeys + 1, 0);
-    for (int32_t it : items) ptr[key(it) + 1]++;
-    for (int64_t k = 0; k < nkeys; ++k) ptr[k + 1] += ptr[k];
     out.assign(items.size(), 0);
-    std::vector<int32_t> cur(ptr.begin(), ptr.end() - 1);
-    for (int32_t it : items) out[cur[key(it)]++] = it;
+    if (T == 1) {
+        for (int32_t it : items) ptr[key(it) + 1]++;
+        for (int64_t k = 0; k < nkeys; ++k) ptr[k + 1] += ptr[k];
+        std::vector<int32_t> cur(ptr.begin(), ptr.end() - 1);
+        for (int32_t it : items) out[cur[key(it)]++] = it;
+    } else {
+        std::vector<std::vector<int32_t>> hist(T);
+        parallel_ranges(n, T, [&](int t, int64_t b, int64_t e) {
+            hist[t].assign(nkeys, 0);
+            int32_t* h = hist[t].data();
+            for (int64_t i = b; i < e; ++i) h[key(items[i])]++;
+        });
+        // bucket k starts at ptr[k]; thread t writes after threads < t: hist[t][k] becomes its cursor
+        parallel_ranges(nkeys, T, [&](int, int64_t kb, int64_t ke) {
+            for (int64_t k = kb; k < ke; ++k) {
+                int32_t c = 0;
+                for (int t = 0; t < T; ++t) c += hist[t][k];
+                ptr[k + 1] = c;
+            }
+        });
+        for (int64_t k = 0; k < nkeys; ++k) ptr[k + 1] += ptr[k];
+        parallel_ranges(nkeys, T, [&](int, int64_t kb, int64_t ke) {
+            for (int64_t k = kb; k < ke; ++k) {
+                int32_t c = ptr[k];
+                for (int t = 0; t < T; ++t) {
+                    const int32_t h = hist[t][k];
+                    hist[t][k] = c;
+                    c += h;
+                }
+            }
+        });
+        parallel_ranges(n, T, [&](int t, int64_t b, int64_t e) {
+            int32_t* cur = hist[t].data();
+            for (int64_t i = b; i < e; ++i) out[cur[key(items[i])]++] = items[i];
+        });
+    }
     if (ptr_out) ptr_out->swap(ptr);
 }
 
-// Two-level list (see RaggedHost) over runs given by run_ptr.
+// Two-level list (see RaggedHost) over runs given by run_ptr: counts per run, prefix sums,
+// then every run fills its own entries and pieces.
 static void build_ragged(const std::vector<int32_t>& run_ptr, RaggedHost& L) {
-    const size_t runs = run_ptr.empty() ? 0 : run_ptr.size() - 1;
-    L.ent.clear();
+    const int64_t runs = run_ptr.empty() ? 0 : (int64_t)run_ptr.size() - 1;
     L.ent_ptr.assign(runs + 1, 0);
     L.run_piece_ptr.assign(runs + 1, 0);
-    L.piece_b.clear();
-    L.piece_e.clear();
-    for (size_t r = 0; r < runs; ++r) {
-        L.ent_ptr[r] = (int32_t)L.ent.size();
-        L.run_piece_ptr[r] = (int32_t)L.piece_b.size();
+    parallel_for(runs, [&](int64_t r) {
+        const int32_t len = run_ptr[r + 1] - run_ptr[r];
+        const int32_t np = len <= kPieceEntries ? 0 : (len + kPieceEntries - 1) / kPieceEntries;
+        L.ent_ptr[r] = np == 0 ? len : np;
+        L.run_piece_ptr[r] = np;
+    });
+    const int64_t n_ent = exclusive_scan(L.ent_ptr);
+    const int64_t n_pc = exclusive_scan(L.run_piece_ptr);
+    L.ent_ptr[runs] = (int32_t)n_ent;
+    L.run_piece_ptr[runs] = (int32_t)n_pc;
+    L.ent.assign(n_ent, 0);
+    L.piece_b.assign(n_pc, 0);
+    L.piece_e.assign(n_pc, 0);
+    parallel_for(runs, [&](int64_t r) {
         const int32_t a = run_ptr[r], b = run_ptr[r + 1];
-        if (b - a <= kPieceEntries) {
-            for (int32_t q = a; q < b; ++q) L.ent.push_back(q);
+        int32_t w = L.ent_ptr[r];
+        if (L.run_piece_ptr[r + 1] == L.run_piece_ptr[r]) {
+            for (int32_t q = a; q < b; ++q) L.ent[w++] = q;
         } else {
-            for (int32_t q = a; q < b; q += kPieceEntries) {
-                L.ent.push_back(-(int32_t)L.piece_b.size() - 1);
-                L.piece_b.push_back(q);
-                L.piece_e.push_back(std::min<int32_t>(q + kPieceEntries, b));
+            int32_t k = L.run_piece_ptr[r];
+            for (int32_t q = a; q < b; q += kPieceEntries, ++k) {
+                L.ent[w++] = -k - 1;
+                L.piece_b[k] = q;
+                L.piece_e[k] = std::min<int32_t>(q + kPieceEntries, b);
             }
         }
-    }
-    L.ent_ptr[runs] = (int32_t)L.ent.size();
-    L.run_piece_ptr[runs] = (int32_t)L.piece_b.size();
+    });
 }
 
 // Flat chunked list over runs r (positions [run_ptr[r], run_ptr[r+1]), output row r) with
@@ -115,8 +231,9 @@ static void build_flat(const std::vector<int32_t>& run_ptr, const std::vector<in
     const int32_t P = runs > 0 ? run_ptr[runs] : 0;
     L = FlatHost{};
     L.row_of.resize(P);
-    for (int32_t r = 0; r < runs; ++r)
-        for (int32_t q = run_ptr[r]; q < run_ptr[r + 1]; ++q) L.row_of[q] = r;
+    parallel_for(runs, [&](int64_t r) {
+        for (int32_t q = run_ptr[r]; q < run_ptr[r + 1]; ++q) L.row_of[q] = (int32_t)r;
+    });
     L.chunk_ptr.push_back(0);
     L.cut_chunk_ptr.push_back(0);
     for (size_t ci = 0; ci + 1 < cuts.size(); ++ci) {
@@ -180,11 +297,23 @@ static void build_flat(const std::vector<int32_t>& run_ptr, const std::vector<in
 // stays negative — the gather then needs one index load per entry instead of two.
 static void resolve_ragged(RaggedHost& L, const std::vector<int32_t>& idx) {
     L.res.resize(L.ent.size());
-    for (size_t q = 0; q < L.ent.size(); ++q) L.res[q] = L.ent[q] >= 0 ? idx[L.ent[q]] : L.ent[q];
+    parallel_for((int64_t)L.ent.size(), [&](int64_t q) { L.res[q] = L.ent[q] >= 0 ? idx[L.ent[q]] : L.ent[q]; });
 }
+
+struct PhaseTimer {
+    bool on = std::getenv("MPGNN_PLAN_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what) {
+        if (!on) return;
+        auto n = std::chrono::steady_clock::now();
+        fprintf(stderr, "[plan] %-28s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
 
 static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N, int64_t lo,
                      int64_t hi, mpgnn_plan* p) {
+    PhaseTimer tm;
     const int64_t* n1 = ei;
     const int64_t* n2 = ei + E;
     p->N = N;
@@ -210,7 +339,7 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
                     map[v] = nd++;
                     p->rel_values.push_back(mn + (int64_t)v);
                 }
-            for (int64_t e = 0; e < E; ++e) rel_d[e] = map[et[e] - mn];
+            parallel_for(E, [&](int64_t e) { rel_d[e] = map[et[e] - mn]; });
         } else {
             std::vector<int64_t> vals(et, et + E);
             std::sort(vals.begin(), vals.end());
@@ -229,6 +358,7 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
         p->rel_val32[d] = (v >= 0 && v <= std::numeric_limits<int32_t>::max()) ? (int32_t)v : -1;
     }
 
+    tm.mark("dense relation ids");
     // ---- valid edges, global (relation, node_1, edge) order ------------------------------
     std::vector<int32_t> valid;
     valid.reserve(E);
@@ -243,76 +373,109 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
     counting_sort(valid, N, [&](int32_t e) { return (int64_t)n1[e]; }, by_row, nullptr);
     counting_sort(by_row, R, [&](int32_t e) { return (int64_t)rel_d[e]; }, by_rel_row, nullptr);
 
+    tm.mark("valid + 2 counting sorts");
     // ---- segments: runs of equal (relation, node_1); keep those with a local edge --------
+    // pass 1: run starts (global segments); pass 2: local edge count of each; prefix sums
+    // give segment ids and edge offsets; pass 3: every kept segment fills its own entries.
     p->rel_seg_ptr.assign(R + 1, 0);
     p->rel_edge_ptr.assign(R + 1, 0);
-    p->s_ptr.push_back(0);
     const int64_t V = (int64_t)by_rel_row.size();
-    std::vector<int32_t> seg_of_edge;  // segment id of each local edge (relation-major order)
-    for (int64_t a = 0; a < V;) {
-        const int32_t e0 = by_rel_row[a];
-        const int32_t d = rel_d[e0];
-        const int64_t row = n1[e0];
-        int64_t b = a + 1;
-        while (b < V && rel_d[by_rel_row[b]] == d && n1[by_rel_row[b]] == row) ++b;
-        const int32_t cnt = (int32_t)(b - a);  // GLOBAL count of (row, relation)
-        bool any_local = false;
-        for (int64_t k = a; k < b; ++k) {
-            const int32_t e = by_rel_row[k];
+    const std::vector<int32_t> gstart = run_starts(V, [&](int64_t a, int64_t b) {  // global segments, + V
+        const int32_t ea = by_rel_row[a], eb = by_rel_row[b];
+        return rel_d[ea] == rel_d[eb] && n1[ea] == n1[eb];
+    });
+    const int64_t G = (int64_t)gstart.size() - 1;
+    std::vector<int32_t> seg_id(G), edge_off(G);  // kept: local edge count, then offsets
+    parallel_for(G, [&](int64_t g) {
+        int32_t c = 0;
+        for (int32_t a = gstart[g]; a < gstart[g + 1]; ++a) {
+            const int64_t c2 = n2[by_rel_row[a]];
+            c += (c2 >= lo && c2 < hi) ? 1 : 0;
+        }
+        edge_off[g] = c;
+        seg_id[g] = c > 0 ? 1 : 0;
+    });
+    const int64_t S_loc = exclusive_scan(seg_id);
+    const int64_t E_loc = exclusive_scan(edge_off);
+    p->e_col.assign(E_loc, 0);
+    p->e_id.assign(E_loc, 0);
+    p->s_row.assign(S_loc, 0);
+    p->s_rel.assign(S_loc, 0);
+    p->s_cnt.assign(S_loc, 0);
+    p->s_ptr.assign(S_loc + 1, (int32_t)E_loc);
+    std::vector<int32_t> seg_of_edge(E_loc);  // segment id of each local edge (relation-major order)
+    parallel_for(G, [&](int64_t g) {
+        const int32_t a0 = gstart[g], a1 = gstart[g + 1];
+        const int32_t next_off = g + 1 < G ? edge_off[g + 1] : (int32_t)E_loc;
+        if (next_off == edge_off[g]) return;  // no local edge: segment not kept
+        const int32_t sid = seg_id[g];
+        const int32_t e0 = by_rel_row[a0];
+        int32_t w = edge_off[g];
+        for (int32_t a = a0; a < a1; ++a) {
+            const int32_t e = by_rel_row[a];
             if (n2[e] >= lo && n2[e] < hi) {
-                p->e_col.push_back((int32_t)n2[e]);
-                p->e_id.push_back(e);
-                seg_of_edge.push_back((int32_t)p->s_row.size());
-                any_local = true;
+                p->e_col[w] = (int32_t)n2[e];
+                p->e_id[w] = e;
+                seg_of_edge[w] = sid;
+                ++w;
             }
         }
-        if (any_local) {
-            p->s_row.push_back((int32_t)row);
-            p->s_rel.push_back(p->rel_val32[d]);
-            p->s_cnt.push_back(cnt);
-            p->s_ptr.push_back((int32_t)p->e_col.size());
-            p->rel_seg_ptr[d + 1]++;
-        }
-        a = b;
+        p->s_row[sid] = (int32_t)n1[e0];
+        p->s_rel[sid] = p->rel_val32[rel_d[e0]];
+        p->s_cnt[sid] = a1 - a0;  // GLOBAL count of (row, relation)
+        p->s_ptr[sid] = edge_off[g];
+    });
+    for (int64_t g = 0; g < G; ++g) {  // kept segments per dense relation
+        const int32_t next_off = g + 1 < G ? edge_off[g + 1] : (int32_t)E_loc;
+        if (next_off != edge_off[g]) p->rel_seg_ptr[rel_d[by_rel_row[gstart[g]]] + 1]++;
     }
-    p->E = (int64_t)p->e_col.size();
-    p->S = (int64_t)p->s_row.size();
+    p->E = E_loc;
+    p->S = S_loc;
     for (int64_t d = 0; d < R; ++d) p->rel_seg_ptr[d + 1] += p->rel_seg_ptr[d];
     for (int64_t d = 0; d < R; ++d)
         p->rel_edge_ptr[d + 1] = p->s_ptr[p->rel_seg_ptr[d + 1]];
+    tm.mark("segments");
 
     // dense relation of each segment (segments are relation-major)
     std::vector<int32_t> seg_d(p->S);
-    for (int64_t d = 0; d < R; ++d)
+    parallel_for(R, [&](int64_t d) {
         for (int32_t s = p->rel_seg_ptr[d]; s < p->rel_seg_ptr[d + 1]; ++s) seg_d[s] = (int32_t)d;
+    });
 
     // ---- row-major segment order (node_1, relation) -------------------------------------
     {
         std::vector<int32_t> segs(p->S);
-        for (int64_t s = 0; s < p->S; ++s) segs[s] = (int32_t)s;
+        parallel_for(p->S, [&](int64_t s) { segs[s] = (int32_t)s; });
         counting_sort(segs, N, [&](int32_t s) { return (int64_t)p->s_row[s]; }, p->rw_seg, &p->rw_ptr);
         p->s_pos.assign(p->S, 0);
-        for (int64_t q = 0; q < p->S; ++q) p->s_pos[p->rw_seg[q]] = (int32_t)q;
+        parallel_for(p->S, [&](int64_t q) { p->s_pos[p->rw_seg[q]] = (int32_t)q; });
     }
 
+    tm.mark("row-major order");
     // ---- transposed orders for grad_x ---------------------------------------------------
     {
         std::vector<int32_t> edges(p->E);
-        for (int64_t k = 0; k < p->E; ++k) edges[k] = (int32_t)k;
+        parallel_for(p->E, [&](int64_t k) { edges[k] = (int32_t)k; });
         std::vector<int32_t> by_col;  // (node_2, relation, node_1, edge)
         counting_sort(edges, N, [&](int32_t k) { return (int64_t)p->e_col[k]; }, by_col, &p->t_ptr);
         p->t_seg.resize(p->E);
-        for (int64_t q = 0; q < p->E; ++q) p->t_seg[q] = seg_of_edge[by_col[q]];
+        parallel_for(p->E, [&](int64_t q) { p->t_seg[q] = seg_of_edge[by_col[q]]; });
+        // edges are relation-major, so an edge's dense relation follows from its position
+        std::vector<int32_t> edge_d(p->E);
+        parallel_for(R, [&](int64_t d) {
+            for (int32_t k = p->rel_edge_ptr[d]; k < p->rel_edge_ptr[d + 1]; ++k) edge_d[k] = (int32_t)d;
+        });
         std::vector<int32_t> by_rel_col;  // (relation, node_2, node_1, edge)
-        counting_sort(by_col, R, [&](int32_t k) { return (int64_t)seg_d[seg_of_edge[k]]; }, by_rel_col, nullptr);
+        counting_sort(by_col, R, [&](int32_t k) { return (int64_t)edge_d[k]; }, by_rel_col, nullptr);
         p->ta_col.resize(p->E);
         p->ta_seg.resize(p->E);
-        for (int64_t q = 0; q < p->E; ++q) {
+        parallel_for(p->E, [&](int64_t q) {
             p->ta_col[q] = p->e_col[by_rel_col[q]];
             p->ta_seg[q] = seg_of_edge[by_rel_col[q]];
-        }
+        });
     }
 
+    tm.mark("transposed orders");
     // ---- ragged two-level lists (bounded serial work per wave) ---------------------------
     build_ragged(p->s_ptr, p->seg_l);
     build_ragged(p->t_ptr, p->t_l);
@@ -320,6 +483,7 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
     resolve_ragged(p->seg_l, p->e_col);
     resolve_ragged(p->t_l, p->t_seg);
     resolve_ragged(p->rw_l, p->rw_seg);
+    tm.mark("ragged lists");
     {
         // segments over edges, cut at relation boundaries (mode SINGLE selects one relation)
         std::vector<int32_t> seg_cuts(p->rel_seg_ptr.begin(), p->rel_seg_ptr.end());
@@ -331,39 +495,42 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
         auto augment = [&](const std::vector<int32_t>& ptr, const std::vector<int32_t>& val, FlatHost& F,
                            std::vector<int32_t>& out_val) {
             std::vector<int32_t> xptr(N + 1, 0);
-            out_val.clear();
-            out_val.reserve(val.size() + (size_t)(hi - lo));
-            for (int64_t i = 0; i < N; ++i) {
-                xptr[i] = (int32_t)out_val.size();
-                for (int32_t q = ptr[i]; q < ptr[i + 1]; ++q) out_val.push_back(val[q]);
-                if (i >= lo && i < hi) out_val.push_back(-(int32_t)(i - lo) - 1);
-            }
-            xptr[N] = (int32_t)out_val.size();
+            parallel_for(N, [&](int64_t i) { xptr[i] = ptr[i] + (int32_t)std::clamp<int64_t>(i, lo, hi) - (int32_t)lo; });
+            xptr[N] = ptr[N] + (int32_t)(hi - lo);
+            out_val.assign(xptr[N], 0);
+            parallel_for(N, [&](int64_t i) {
+                int32_t w = xptr[i];
+                for (int32_t q = ptr[i]; q < ptr[i + 1]; ++q) out_val[w++] = val[q];
+                if (i >= lo && i < hi) out_val[w] = -(int32_t)(i - lo) - 1;
+            });
             build_flat(xptr, node_cuts, F);
         };
         augment(p->t_ptr, p->t_seg, p->tx_f, p->tx_val);
         augment(p->rw_ptr, p->rw_seg, p->rwx_f, p->rwx_val);
     }
+    tm.mark("flat lists");
     {
         // runs of equal (relation, node_2) in ta order
-        std::vector<int32_t> run_ptr{0};
-        std::vector<int32_t> run_key, run_rel;
-        for (int64_t d = 0; d < R; ++d) {
-            for (int32_t q = p->rel_edge_ptr[d]; q < p->rel_edge_ptr[d + 1];) {
-                int32_t q2 = q + 1;
-                while (q2 < p->rel_edge_ptr[d + 1] && p->ta_col[q2] == p->ta_col[q]) ++q2;
-                run_ptr.push_back(q2);
-                run_key.push_back(p->ta_col[q]);
-                run_rel.push_back((int32_t)d);
-                q = q2;
-            }
-        }
+        std::vector<int32_t> edge_d(p->E);  // dense relation of each position (relation-major)
+        parallel_for(R, [&](int64_t d) {
+            for (int32_t k = p->rel_edge_ptr[d]; k < p->rel_edge_ptr[d + 1]; ++k) edge_d[k] = (int32_t)d;
+        });
+        const std::vector<int32_t> run_ptr = run_starts(p->E, [&](int64_t a, int64_t b) {
+            return edge_d[a] == edge_d[b] && p->ta_col[a] == p->ta_col[b];
+        });
+        const int64_t nruns = (int64_t)run_ptr.size() - 1;
+        std::vector<int32_t> run_key(nruns), run_rel(nruns);
+        parallel_for(nruns, [&](int64_t r) {
+            run_key[r] = p->ta_col[run_ptr[r]];
+            run_rel[r] = edge_d[run_ptr[r]];
+        });
         build_ragged(run_ptr, p->ta_l);
         resolve_ragged(p->ta_l, p->ta_seg);
         const size_t runs = run_key.size();
         p->ta_key.resize(p->ta_l.ent.size());
-        for (size_t r = 0; r < runs; ++r)
+        parallel_for((int64_t)runs, [&](int64_t r) {
             for (int32_t q = p->ta_l.ent_ptr[r]; q < p->ta_l.ent_ptr[r + 1]; ++q) p->ta_key[q] = run_key[r];
+        });
         p->rel_ta_ent_ptr.assign(R + 1, 0);
         p->rel_ta_piece_ptr.assign(R + 1, 0);
         size_t r = 0;
@@ -375,6 +542,7 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
         p->rel_ta_ent_ptr[R] = p->ta_l.ent_ptr[runs];
         p->rel_ta_piece_ptr[R] = p->ta_l.run_piece_ptr[runs];
     }
+    tm.mark("ta ragged");
     p->rel_seg_piece_ptr.assign(R + 1, 0);
     for (int64_t d = 0; d <= R; ++d) p->rel_seg_piece_ptr[d] = p->seg_l.run_piece_ptr[p->rel_seg_ptr[d]];
 
@@ -416,6 +584,7 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
         }
         p->rel_chunk_ptr[d + 1] = (int32_t)p->chunk_begin.size();
     }
+    tm.mark("tiles + chunks");
     return MPGNN_OK;
 }
 

@@ -159,6 +159,7 @@ struct mpgnn_plan {
 namespace mpgnn {
 
 void set_last_error(const std::string& msg);
+extern int g_plan_threads;  // host threads of mpgnn_plan_create (0 = hardware concurrency, ≤ 16)
 
 // Resolve (mode, relation, R) to a contiguous dense-relation range [d_lo, d_hi).
 // Returns MPGNN_ERR_INDEX if a selected relation is flagged invalid.

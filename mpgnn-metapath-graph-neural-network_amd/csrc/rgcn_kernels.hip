@@ -3389,6 +3389,11 @@ using namespace mpgnn;
 extern "C" {
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_PLAN_THREADS) {
+        if (value < 0 || value > 256) return arg_error("MPGNN_OPT_PLAN_THREADS must be 0..256");
+        g_plan_threads = (int)value;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_REL_STAGGER) {
         if (value < 0 || value > 4096) return arg_error("MPGNN_OPT_REL_STAGGER must be 0..4096");
         g_rel_stagger = (int)value;

@@ -172,3 +172,23 @@ def test_flat_lists_bit_exact_and_well_formed(case, shard):
         for k, r in enumerate(plan.table(f"{l}_f_split_row")):
             touched = np.unique(np.searchsorted(cp, np.arange(run_ptr[r], run_ptr[r + 1]), side="right"))
             assert sp[k + 1] - sp[k] == len(touched), (l, r)
+
+
+@pytest.mark.parametrize("shard", [None, (20_000, 70_000)])
+def test_parallel_plan_build_independent_of_thread_count(shard):
+    """The host builder splits its passes over threads (MPGNN_OPT_PLAN_THREADS); at C2 size
+    (1.65 M edges, well above the one-thread threshold) every exported table is identical
+    with 1, 3 and the default number of threads."""
+    from mpgnn_amd import _lib
+    g = data.config_graph("C2")
+    plans = []
+    try:
+        for threads in (1, 3, 0):
+            _lib.check(_lib.lib.mpgnn_set_option(11, threads))
+            plans.append(mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, g.num_nodes, shard=shard))
+    finally:
+        _lib.lib.mpgnn_set_option(11, 0)
+    for name in _lib.TABLES:
+        ref = plans[0].table(name)
+        for p in plans[1:]:
+            assert np.array_equal(p.table(name), ref), name
