@@ -201,8 +201,10 @@ enum mpgnn_option {
     MPGNN_OPT_REL_WGS = 9,  /* rel_gemm_kernel workgroups per CU: 2 (default) or 1; same results */
     MPGNN_OPT_REL_STAGGER = 10, /* rel_gemm_kernel: the second half of the grid first sleeps this many 64-clock
                                   quanta (de-phases the two workgroups of a CU); same results */
-    MPGNN_OPT_PLAN_THREADS = 11 /* host threads of mpgnn_plan_create: 0 (default) = hardware concurrency capped
+    MPGNN_OPT_PLAN_THREADS = 11, /* host threads of mpgnn_plan_create: 0 (default) = hardware concurrency capped
                                    at 16; the tables do not depend on it */
+    MPGNN_OPT_REL_QUEUE = 12    /* rel_gemm_kernel: 1 = items taken from per-group atomic counters (dynamic
+                                   schedule), 0 = fixed contiguous ranges; same results */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

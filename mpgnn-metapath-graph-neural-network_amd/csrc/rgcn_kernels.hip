@@ -1054,6 +1054,7 @@ struct RelGemmArgs {
     float* Yroot;         // rows i - row_lo
     int sel_b, row_lo, row_hi;
     int stagger;                 // s_sleep quanta (64 clk) the second half of the grid waits first
+    int* queue;                  // nullable: per-group item counters (dynamic schedule), zero between launches
     unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][32] s_memtime timeline, or nullptr
 };
 
@@ -1270,12 +1271,114 @@ struct RelGemm {
         }
         stamp_rt(31);
     }
+
+    // Dynamic schedule (MPGNN_OPT_REL_QUEUE): workgroups b ≡ g (mod 8) form group g and take
+    // the items of [g·n/8, (g+1)·n/8) one at a time from the group's counter (atomicAdd), two
+    // grabs ahead of the MFMAs, instead of a fixed contiguous range — a workgroup slowed by
+    // memory contention takes fewer items. Items stay relation-ordered within a group (weight
+    // slices shared through the group's L2). The last workgroup of a group to finish resets its
+    // counters, so the next launch (stream order) starts from zero.
+    __device__ static void run_dynamic(const RelGemmArgs& a, float* smem) {
+        float* As = smem;                 // [2][32][lda]
+        float* Sc = smem + 2 * 32 * lda;  // [2][32] dgrad row scales
+        int* Sq = reinterpret_cast<int*>(Sc + 64);  // [2] grabbed item index
+        const int tid = threadIdx.x;
+        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int n_items = a.n_rel + a.n_root;
+        const int G = (int)gridDim.x;
+        const int ng = min(8, G);  // every group has at least one member
+        const int grp = (int)blockIdx.x % ng;
+        const int lo = (int)((long long)grp * n_items / ng);
+        const int hi = (int)((long long)(grp + 1) * n_items / ng);
+        const int members = G / ng + (grp < G % ng ? 1 : 0);
+        int* ctr = a.queue + grp * 64;  // own 256-B line per counter
+        int* done = ctr + 32;
+        if (tid == 0) {
+            Sq[0] = lo + atomicAdd(ctr, 1);
+            Sq[1] = lo + atomicAdd(ctr, 1);
+        }
+        __syncthreads();
+        int cur_i = __builtin_amdgcn_readfirstlane(Sq[0]);
+        int nxt_i = __builtin_amdgcn_readfirstlane(Sq[1]);
+        if (cur_i < hi) {
+            float4 v[WPT];
+            int cnt;
+            Item cur = item(a, cur_i);
+            issue(a, cur, tid, v, cnt);
+            float b[KH];
+            load_b(cur.w, wave, lane, b);
+            commit(cur, tid, v, cnt, As, Sc);
+#pragma unroll
+            for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(b[j]));
+            __syncthreads();
+            int buf = 0, slot = 0;
+            while (true) {
+                const bool has_next = nxt_i < hi;
+                int nn = hi;
+                if (tid == 0 && has_next) nn = lo + atomicAdd(ctr, 1);  // read after the MFMAs
+                const Item nxt = has_next ? item(a, nxt_i) : cur;
+                if (has_next) issue(a, nxt, tid, v, cnt);
+                const bool new_w = nxt.w != cur.w;
+                float bn[KH];
+                if (new_w) load_b(nxt.w, wave, lane, bn);
+                const float* Ab = As + buf * 32 * lda + c * lda + h * KH;
+                f32x16 acc;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+                float4 af = *reinterpret_cast<const float4*>(Ab);
+#pragma unroll
+                for (int j = 0; j < KH; j += 4) {
+                    const float4 cf = af;
+                    if (j + 4 < KH) af = *reinterpret_cast<const float4*>(Ab + j + 4);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], acc, 0, 0, 0);
+                }
+                float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
+                const float* sc = Sc + buf * 32;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (row < cur.nrows) {
+                        float o = acc[r];
+                        if constexpr (DGRAD) {
+                            if (!cur.root) o = o / sc[row];
+                        }
+                        Yt[(size_t)row * N + wave * 32 + c] = o;
+                    }
+                }
+                if (has_next) commit(nxt, tid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
+                if (tid == 0) Sq[slot] = nn;
+                if (new_w) {
+#pragma unroll
+                    for (int j = 0; j < KH; ++j) b[j] = bn[j];
+                }
+                __syncthreads();
+                const int nn_all = __builtin_amdgcn_readfirstlane(Sq[slot]);
+                slot ^= 1;
+                if (!has_next) break;
+                cur = nxt;
+                cur_i = nxt_i;
+                nxt_i = nn_all;
+                buf ^= 1;
+            }
+        }
+        if (tid == 0) {
+            if (atomicAdd(done, 1) == members - 1) {  // every member has stopped grabbing
+                atomicExch(ctr, 0);
+                atomicExch(done, 0);
+            }
+        }
+    }
 };
 
 template <int KB, bool DGRAD>
 __global__ __launch_bounds__(kThreads, 2) void rel_gemm_kernel(RelGemmArgs a) {
     extern __shared__ float smem[];
-    RelGemm<KB, DGRAD>::run(a, smem);
+    if (a.queue != nullptr) RelGemm<KB, DGRAD>::run_dynamic(a, smem);
+    else RelGemm<KB, DGRAD>::run(a, smem);
 }
 
 
@@ -2716,6 +2819,27 @@ static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
 }
 
 
+static bool g_rel_queue = false;  // MPGNN_OPT_REL_QUEUE: dynamic item schedule in rel_gemm_kernel
+static std::mutex g_queue_mu;
+static std::vector<std::pair<hipStream_t, int*>> g_queues;  // per launch stream: 8 groups × 64 ints, zeroed
+
+// The counters of a stream (allocated and zeroed on first use; never while the stream is
+// being captured into a graph — the static schedule runs instead).
+static int* rel_queue(hipStream_t st) {
+    std::lock_guard<std::mutex> lk(g_queue_mu);
+    for (auto& q : g_queues)
+        if (q.first == st) return q.second;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    int* d = nullptr;
+    if (hipMalloc(&d, 8 * 64 * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemset(d, 0, 8 * 64 * sizeof(int)) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    g_queues.push_back({st, d});
+    return d;
+}
 static int g_rel_stagger = 0;    // MPGNN_OPT_REL_STAGGER: s_sleep quanta for the second half of the grid
 static int g_rel_wg_per_cu = 2;  // MPGNN_OPT_REL_WGS: rel_gemm_kernel workgroups per CU (1 or 2)
 static bool g_rel_gemm = true;  // MPGNN_OPT_REL_GEMM: B-stationary GEMM for K ∈ {64, 128}, N = 128
@@ -2724,7 +2848,7 @@ static bool g_fused = false;    // MPGNN_OPT_FUSED: fused means + transform for 
 template <int KB, bool DGRAD>
 static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
     constexpr int lda = 64 * KB + 4;
-    const size_t lds = (size_t)(2 * 32 * lda + 64) * sizeof(float);
+    const size_t lds = (size_t)(2 * 32 * lda + 64 + 4) * sizeof(float);
     const int n_items = a.n_rel + a.n_root;
     const int grid = std::min(n_items, cu_count() * g_rel_wg_per_cu);
     hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
@@ -2967,6 +3091,7 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         r.row_hi = (int)row_hi;
         r.stamps = (kind == MPGNN_K_SEG_FWD) ? g_stamps : nullptr;
         r.stagger = g_rel_stagger;
+        r.queue = (g_rel_queue && !g_stamps) ? rel_queue(strm) : nullptr;
         TimedLaunch tl(kind, strm);
         launch_rel_gemm(r, K, gather_kind == 1, strm);
         return hip_check(hipGetLastError(), "rel_gemm_kernel launch");
@@ -3389,6 +3514,10 @@ using namespace mpgnn;
 extern "C" {
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_REL_QUEUE) {
+        g_rel_queue = value != 0;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_PLAN_THREADS) {
         if (value < 0 || value > 256) return arg_error("MPGNN_OPT_PLAN_THREADS must be 0..256");
         g_plan_threads = (int)value;

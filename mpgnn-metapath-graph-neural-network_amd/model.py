@@ -1,7 +1,8 @@
 """Drop-in for the reference ``model.py`` MPGNN wrappers (model.py:132-149, 179-228).
 
-The wrappers stay plain PyTorch (ReLU, Dropout, Linear, LogSoftmax) exactly as in the
-reference; only the relational layers are the gfx950 ones. Module/parameter names, their
+The wrappers stay plain PyTorch (ReLU, Dropout, Linear, LogSoftmax) as in the reference; the
+relational layers are the gfx950 ones, and the Linear layers' weight gradient is reduced in
+node slices (``linear``: same forward, same parameters, blocked summation order). Module/parameter names, their
 order and a seeded initialisation are identical to the reference, so ``state_dict``s load
 either way. ``MPNet`` (model.py:153-176) is not provided: it calls its convs with 4 arguments
 where CustomRGCNConv.forward needs 5 (mp_rgcn_layer.py:158) and cannot run in the reference.
@@ -16,7 +17,52 @@ import torch.nn.functional as F
 from .mp_rgcn_layer import CustomRGCNConv
 from .nn import RGCNConv
 
-__all__ = ["Net", "MPNetm"]
+__all__ = ["Net", "MPNetm", "linear"]
+
+
+class _SplitKLinear(torch.autograd.Function):
+    """``F.linear`` whose weight gradient is reduced in slices over the node dimension.
+
+    The wrappers' Linear layers see every node as a row (N = 14,541 at C3, 2 M at C5) but have
+    few outputs (2 classes, 64 hidden): ``grad_weight = grad_outᵀ @ x`` is then a [O × F] GEMM
+    with K = N, which the BLAS library tiles into a handful of long serial-K workgroups (66 µs
+    for O = 2 at C3, 6 % of the epoch). Here K is cut into slices of ≤ 1024 rows: one batched
+    GEMM over the slices + a sum over them — the same products in fp32, summed in a different
+    (blocked) order. Forward and grad_input are exactly the autograd ones (``F.linear``, ``mm``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = g.mm(weight)
+        if ctx.needs_input_grad[1]:
+            n = x.shape[0]
+            slices = max(1, min(256, (n + 1023) // 1024))
+            if slices == 1:
+                gw = g.t().mm(x)
+            else:
+                rows = (n + slices - 1) // slices
+                pad = rows * slices - n
+                gp = F.pad(g, (0, 0, 0, pad)) if pad else g
+                xp = F.pad(x, (0, 0, 0, pad)) if pad else x
+                gw = torch.bmm(gp.view(slices, rows, -1).transpose(1, 2), xp.view(slices, rows, -1)).sum(0)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = g.sum(0)
+        return gx, gw, gb
+
+
+def linear(layer: torch.nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    """``layer(x)`` with the split-K weight gradient above (same parameters, same forward)."""
+    if x.dim() != 2 or not x.is_cuda:
+        return layer(x)
+    return _SplitKLinear.apply(x, layer.weight, layer.bias)
 
 
 class Net(torch.nn.Module):
@@ -34,7 +80,7 @@ class Net(torch.nn.Module):
             conv = self.conv1 if layer_index == 0 else self.conv2
             # F.relu(conv(...)) of model.py:144,146, fused into the layer's combine kernel
             x = conv(x, edge_index, edge_type, shard=shard, group=group, activation="relu")
-        x = self.LinearLayer(x)
+        x = linear(self.LinearLayer, x)
         return F.log_softmax(x, dim=1)
 
 
@@ -76,6 +122,6 @@ class MPNetm(torch.nn.Module):
                     h = self.dropout2(h)
             embeddings.append(h)
         concatenated_embedding = torch.cat(embeddings, dim=1)
-        h = F.relu(self.fc1(concatenated_embedding))
-        h = self.fc2(h)
+        h = F.relu(linear(self.fc1, concatenated_embedding))
+        h = linear(self.fc2, h)
         return self.log_softmax(h)

@@ -55,3 +55,11 @@ for name, a in [("prologue", pro), ("mfma_item", mf), ("epi_commit_barrier", ep)
     res[name] = {"p10": float(np.percentile(a, 10)), "p50": float(np.median(a)), "p90": float(np.percentile(a, 90)),
                  "max": float(a.max()), "n": len(a)}
 print(json.dumps(res))
+# per-workgroup: items processed vs end time (load balance)
+items = np.array([sum(1 for k in range(30) if 3 + 2 * k < 30 and r[3 + 2 * k] > 0) for r in st])
+ends = rt_end
+bal = {}
+for n in sorted(set(items.tolist())):
+    m = items == n
+    bal[int(n)] = {"wgs": int(m.sum()), "end_p50_ns": float(np.median(ends[m])), "end_max_ns": float(ends[m].max())}
+print(json.dumps({"balance": bal}))

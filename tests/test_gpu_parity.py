@@ -717,3 +717,55 @@ def test_overlapped_forward_bitwise_equal(groups):
         _lib.lib.mpgnn_set_option(8, 0)
     for a, b in zip(got, ref):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n,f_in,f_out", [(14541, 128, 2), (1000, 128, 64), (300, 64, 3)])
+def test_split_k_linear_matches_nn_linear(n, f_in, f_out):
+    """model.linear: forward bit-identical to nn.Linear; grad_weight (sliced over rows) and
+    grad_bias / grad_input within fp32 rounding of autograd's."""
+    from mpgnn_amd.model import linear
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(f_in, f_out).to(DEV)
+    x = torch.randn(n, f_in, device=DEV, requires_grad=True)
+    g = torch.randn(n, f_out, device=DEV)
+    ref = lin(x)
+    ref.backward(g)
+    ref_grads = [x.grad.clone(), lin.weight.grad.clone(), lin.bias.grad.clone()]
+    x.grad = None
+    lin.zero_grad()
+    out = linear(lin, x)
+    assert torch.equal(out, ref)
+    out.backward(g)
+    for got, want, what in zip([x.grad, lin.weight.grad, lin.bias.grad], ref_grads, ["dx", "dW", "db"]):
+        rel_close(got, want, tol=1e-5, what=what)
+
+
+def test_rel_gemm_dynamic_schedule_bitwise_equal():
+    """MPGNN_OPT_REL_QUEUE: items taken from atomic counters give the same bits as the fixed
+    ranges (each item is computed by the same code from the same inputs), over repeated
+    launches (the counters reset themselves), forward and dgrad, and a tiny grid (< 8 groups)."""
+    from mpgnn_amd import _lib
+    g = data.config_graph("fb15k237")
+    small = data.synthetic_graph(60, 2, 3, feat_dim=128, seed=4)
+    torch.manual_seed(30)
+    conv = mpgnn_amd.RGCNConv(128, 128, g.num_relations, flow="target_to_source").to(DEV)
+    conv_s = mpgnn_amd.RGCNConv(128, 128, 2, flow="target_to_source").to(DEV)
+
+    def run():
+        res = []
+        for c, gg in ((conv, g), (conv_s, small)):
+            x = gg.x.to(DEV).requires_grad_(True)
+            out = c(x, gg.edge_index.to(DEV), gg.edge_type.to(DEV))
+            out.square().sum().backward()
+            res += [out.detach().clone(), x.grad.clone()]
+        return res
+
+    ref = run()
+    _lib.check(_lib.lib.mpgnn_set_option(12, 1))
+    try:
+        for _ in range(3):
+            got = run()
+            for a, b in zip(got, ref):
+                assert torch.equal(a, b)
+    finally:
+        _lib.lib.mpgnn_set_option(12, 0)
