@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc
+OUT=${OUT:-gpurun_out/pmc}
 mkdir -p "$OUT"
 ARGS=${ARGS:---iters 20}
 i=0
