@@ -203,8 +203,10 @@ enum mpgnn_option {
                                   quanta (de-phases the two workgroups of a CU); same results */
     MPGNN_OPT_PLAN_THREADS = 11, /* host threads of mpgnn_plan_create: 0 (default) = hardware concurrency capped
                                    at 16; the tables do not depend on it */
-    MPGNN_OPT_REL_QUEUE = 12    /* rel_gemm_kernel: 1 = items taken from per-group atomic counters (dynamic
+    MPGNN_OPT_REL_QUEUE = 12,   /* rel_gemm_kernel: 1 = items taken from per-group atomic counters (dynamic
                                    schedule), 0 = fixed contiguous ranges; same results */
+    MPGNN_OPT_MERGE_GRAD = 13   /* backward: 1 (default) = weight / root / bias outer products in one launch and
+                                   their slab reductions in one more; 0 = one launch each; same results */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

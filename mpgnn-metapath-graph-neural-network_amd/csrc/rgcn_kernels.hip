@@ -2488,10 +2488,9 @@ __device__ __forceinline__ int outer_row(int k) { return (k >> 1) * kOuterLd + (
 constexpr int kOuterBuf = (kSlice / 2) * kOuterLd;   // floats per 32-row matrix image
 
 template <bool VEC>
-__global__ __launch_bounds__(kThreads, 2) void outer_accum_kernel(OuterArgs a) {
+__device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int cidx) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* bufs = smem;  // [2 buffers][A, B][kOuterBuf]
-    const int cidx = blockIdx.x;
     int p0, p1;
     if (a.chunk_begin != nullptr) {
         p0 = ld_uniform(a.chunk_begin, cidx + a.chunk_off);
@@ -2651,6 +2650,20 @@ __global__ __launch_bounds__(kThreads, 2) void outer_accum_kernel(OuterArgs a) {
     if (do_bsum && Db != nullptr && tid < ncols) Db[n_base + tid] = bsum;
 }
 
+template <bool VEC>
+__global__ __launch_bounds__(kThreads, 2) void outer_accum_kernel(OuterArgs a) {
+    outer_accum_body<VEC>(a, (int)blockIdx.x);
+}
+
+// The weight-gradient chunks and the root / bias chunks of one backward call in ONE launch:
+// blocks [0, n_a) take `a`, the rest `b` (the root part alone is ~60-110 workgroups, a
+// mostly idle chip for a whole launch).
+template <bool VEC>
+__global__ __launch_bounds__(kThreads, 2) void outer_accum2_kernel(OuterArgs a, OuterArgs b, int n_a) {
+    if ((int)blockIdx.x < n_a) outer_accum_body<VEC>(a, (int)blockIdx.x);
+    else outer_accum_body<VEC>(b, (int)blockIdx.x - n_a);
+}
+
 // dst[group g] (elems floats) = Σ_{c in chunks of g, ascending} P[c]
 struct ReduceArgs {
     const float* P;
@@ -2664,8 +2677,7 @@ struct ReduceArgs {
     int skip_single;     // groups of exactly one chunk were written directly: skip them
 };
 
-__global__ __launch_bounds__(kThreads) void reduce_slabs_kernel(ReduceArgs a) {
-    const int g = blockIdx.x;
+__device__ __forceinline__ void reduce_slabs_body(const ReduceArgs& a, const int g) {
     const int e = blockIdx.y * kThreads + threadIdx.x;
     if (e >= a.elems) return;
     int c0 = 0, c1 = a.nchunks;
@@ -2689,6 +2701,18 @@ __global__ __launch_bounds__(kThreads) void reduce_slabs_kernel(ReduceArgs a) {
     }
     const int d = a.gdst != nullptr ? a.gdst[a.g_base + g] : g;
     a.dst[(size_t)d * a.elems + e] = s;
+}
+
+__global__ __launch_bounds__(kThreads) void reduce_slabs_kernel(ReduceArgs a) { reduce_slabs_body(a, (int)blockIdx.x); }
+
+// Up to three reductions (dW groups, droot, dbias) in one launch: blocks [0, n0) → r0,
+// [n0, n0 + n1) → r1, the rest → r2; grid.y covers the widest.
+__global__ __launch_bounds__(kThreads) void reduce_slabs3_kernel(ReduceArgs r0, ReduceArgs r1, ReduceArgs r2, int n0,
+                                                                 int n1) {
+    const int b = (int)blockIdx.x;
+    if (b < n0) reduce_slabs_body(r0, b);
+    else if (b < n0 + n1) reduce_slabs_body(r1, b - n0);
+    else reduce_slabs_body(r2, b - n0 - n1);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -2819,6 +2843,7 @@ static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
 }
 
 
+static bool g_merge_grad = true;  // MPGNN_OPT_MERGE_GRAD: dW + droot/dbias in one outer launch, one reduce launch
 static bool g_rel_queue = false;  // MPGNN_OPT_REL_QUEUE: dynamic item schedule in rel_gemm_kernel
 static std::mutex g_queue_mu;
 static std::vector<std::pair<hipStream_t, int*>> g_queues;  // per launch stream: 8 groups × 64 ints, zeroed
@@ -3514,6 +3539,10 @@ using namespace mpgnn;
 extern "C" {
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_MERGE_GRAD) {
+        g_merge_grad = value != 0;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_REL_QUEUE) {
         g_rel_queue = value != 0;
         return MPGNN_OK;
@@ -3968,6 +3997,17 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
     };
 
     // ---- grad_weight[r] = Σ_{seg of r} h_segᵀ dout[node_1(seg)] -------------------------
+    // ---- grad_root = xᵀ dout, grad_bias = Σ dout  (rows [row_lo, row_hi)) ---------------
+    // Both outer-product accumulations go out as ONE launch when their grids match, and the
+    // slab reductions (dW groups, droot, dbias) as one more.
+    struct Part {
+        ReduceArgs r;
+        int gx, ey;
+    };
+    std::vector<Part> reduces;
+    bool have_w = false, have_root = false;
+    OuterArgs ow{}, orr{};
+    int nch = 0;
     if (grad_weight != nullptr) {
         const size_t wbytes = (mode == MPGNN_MODE_ALL ? (size_t)std::max(R, 0) : 1) * wsize * sizeof(float);
         // every weight index with a segment range is written (directly or by the slab reduce,
@@ -3976,7 +4016,7 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         if (!all_written)
             if ((st = hip_check(hipMemsetAsync(grad_weight, 0, wbytes, strm), "memset grad_weight")) != MPGNN_OK)
                 return st;
-        const int nch = s.c_hi - s.c_lo;
+        nch = s.c_hi - s.c_lo;
         if (nch > 0) {
             const float* H = h_save;
             if (H == nullptr) {
@@ -3986,26 +4026,21 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
                 H = Hw;
             }
             float* P = reinterpret_cast<float*>(ws + w.p);
-            OuterArgs o{};
-            o.chunk_begin = p->d.chunk_begin;
-            o.chunk_end = p->d.chunk_end;
-            o.chunk_dst = p->d.chunk_dst;
-            o.chunk_off = s.c_lo;
-            o.dst_mode = mode == MPGNN_MODE_ALL ? 1 : 2;
-            o.A = H;
-            o.M = F_in;
-            o.a_off = s.sel_b;
-            o.B = grad_out;
-            o.Nn = F_out;
-            o.b_idx = p->d.s_row;
-            o.P = P;
-            o.dst = grad_weight;
-            o.Pb = nullptr;
-            {
-                TimedLaunch tl(MPGNN_K_OUTER, strm);
-                launch_outer(dim3(nch, mt, nt), o);
-            }
-            if ((st = hip_check(hipGetLastError(), "outer_accum_kernel(dW) launch")) != MPGNN_OK) return st;
+            ow.chunk_begin = p->d.chunk_begin;
+            ow.chunk_end = p->d.chunk_end;
+            ow.chunk_dst = p->d.chunk_dst;
+            ow.chunk_off = s.c_lo;
+            ow.dst_mode = mode == MPGNN_MODE_ALL ? 1 : 2;
+            ow.A = H;
+            ow.M = F_in;
+            ow.a_off = s.sel_b;
+            ow.B = grad_out;
+            ow.Nn = F_out;
+            ow.b_idx = p->d.s_row;
+            ow.P = P;
+            ow.dst = grad_weight;
+            ow.Pb = nullptr;
+            have_w = true;
             ReduceArgs r{};
             r.P = P;
             r.elems = (int)wsize;
@@ -4013,79 +4048,103 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
             r.skip_single = 1;
             const int ey = (int)((wsize + kThreads - 1) / kThreads);
             if (mode == MPGNN_MODE_ALL) {
-                TimedLaunch tl(MPGNN_K_REDUCE, strm);
                 r.gptr = p->d.rel_chunk_ptr;
                 r.g_off = s.c_lo;
                 r.gdst = p->d.rel_val32;
                 r.g_base = (int)s.d_lo;
-                hipLaunchKernelGGL(reduce_slabs_kernel, dim3((int)(s.d_hi - s.d_lo), ey), dim3(kThreads), 0, strm, r);
+                reduces.push_back({r, (int)(s.d_hi - s.d_lo), ey});
             } else if (nch > 1) {  // one chunk: written directly
-                TimedLaunch tl(MPGNN_K_REDUCE, strm);
                 r.gptr = nullptr;
                 r.nchunks = nch;
                 r.gdst = nullptr;
-                hipLaunchKernelGGL(reduce_slabs_kernel, dim3(1, ey), dim3(kThreads), 0, strm, r);
+                reduces.push_back({r, 1, ey});
             }
-            if ((st = hip_check(hipGetLastError(), "reduce_slabs_kernel(dW) launch")) != MPGNN_OK) return st;
         }
     }
-
-    // ---- grad_root = xᵀ dout, grad_bias = Σ dout  (rows [row_lo, row_hi)) -------------
     if (grad_root != nullptr || grad_bias != nullptr) {
         if (rc.n == 0) {
             if (grad_root && (st = hip_check(hipMemsetAsync(grad_root, 0, wsize * sizeof(float), strm), "memset")))
                 return st;
             if (grad_bias && (st = hip_check(hipMemsetAsync(grad_bias, 0, F_out * sizeof(float), strm), "memset")))
                 return st;
-            return MPGNN_OK;
+        } else {
+            if (!x) return arg_error("NULL x");
+            float* P = reinterpret_cast<float*>(ws + w.proot);
+            float* Pb = reinterpret_cast<float*>(ws + w.pb);
+            orr.chunk_begin = nullptr;
+            orr.row_lo = rc.rows_lo;
+            orr.row_hi = rc.rows_hi;
+            orr.chunk_rows = rc.chunk;
+            orr.dst_mode = rc.n == 1 ? 3 : 0;
+            orr.A = x;
+            orr.M = F_in;
+            orr.a_off = 0;
+            orr.B = grad_out;
+            orr.Nn = F_out;
+            orr.b_idx = nullptr;
+            orr.P = P;
+            orr.dst = grad_root;
+            orr.Pb = grad_bias ? Pb : nullptr;
+            orr.dst_b = grad_bias;
+            have_root = true;
+            if (rc.n > 1 && grad_root) {
+                ReduceArgs r{};
+                r.P = P;
+                r.elems = (int)wsize;
+                r.nchunks = rc.n;
+                r.dst = grad_root;
+                reduces.push_back({r, 1, (int)((wsize + kThreads - 1) / kThreads)});
+            }
+            if (rc.n > 1 && grad_bias) {
+                ReduceArgs r{};
+                r.P = Pb;
+                r.elems = F_out;
+                r.nchunks = rc.n;
+                r.dst = grad_bias;
+                reduces.push_back({r, 1, (F_out + kThreads - 1) / kThreads});
+            }
         }
-        if (!x) return arg_error("NULL x");
-        float* P = reinterpret_cast<float*>(ws + w.proot);
-        float* Pb = reinterpret_cast<float*>(ws + w.pb);
-        OuterArgs o{};
-        o.chunk_begin = nullptr;
-        o.row_lo = rc.rows_lo;
-        o.row_hi = rc.rows_hi;
-        o.chunk_rows = rc.chunk;
-        o.dst_mode = rc.n == 1 ? 3 : 0;
-        o.A = x;
-        o.M = F_in;
-        o.a_off = 0;
-        o.B = grad_out;
-        o.Nn = F_out;
-        o.b_idx = nullptr;
-        o.P = P;
-        o.dst = grad_root;
-        o.Pb = grad_bias ? Pb : nullptr;
-        o.dst_b = grad_bias;
-        {
+    }
+    const int root_y = grad_root ? mt : 1;
+    if (have_w && have_root && root_y == mt && g_merge_grad) {
+        TimedLaunch tl(MPGNN_K_OUTER, strm);
+        if (outer_vec)
+            hipLaunchKernelGGL(outer_accum2_kernel<true>, dim3(nch + rc.n, mt, nt), dim3(kThreads), outer_lds, strm, ow,
+                               orr, nch);
+        else
+            hipLaunchKernelGGL(outer_accum2_kernel<false>, dim3(nch + rc.n, mt, nt), dim3(kThreads), outer_lds, strm,
+                               ow, orr, nch);
+        if ((st = hip_check(hipGetLastError(), "outer_accum2_kernel launch")) != MPGNN_OK) return st;
+    } else {
+        if (have_w) {
             TimedLaunch tl(MPGNN_K_OUTER, strm);
-            launch_outer(dim3(rc.n, grad_root ? mt : 1, nt), o);
+            launch_outer(dim3(nch, mt, nt), ow);
+            if ((st = hip_check(hipGetLastError(), "outer_accum_kernel(dW) launch")) != MPGNN_OK) return st;
         }
-        if ((st = hip_check(hipGetLastError(), "outer_accum_kernel(root) launch")) != MPGNN_OK) return st;
-        if (rc.n == 1) return MPGNN_OK;  // written directly
-        if (grad_root) {
-            ReduceArgs r{};
-            r.P = P;
-            r.elems = (int)wsize;
-            r.nchunks = rc.n;
-            r.dst = grad_root;
-            TimedLaunch tl(MPGNN_K_REDUCE, strm);
-            hipLaunchKernelGGL(reduce_slabs_kernel, dim3(1, (int)((wsize + kThreads - 1) / kThreads)), dim3(kThreads),
-                               0, strm, r);
-            if ((st = hip_check(hipGetLastError(), "reduce_slabs_kernel(root) launch")) != MPGNN_OK) return st;
+        if (have_root) {
+            TimedLaunch tl(MPGNN_K_OUTER, strm);
+            launch_outer(dim3(rc.n, root_y, nt), orr);
+            if ((st = hip_check(hipGetLastError(), "outer_accum_kernel(root) launch")) != MPGNN_OK) return st;
         }
-        if (grad_bias) {
-            ReduceArgs r{};
-            r.P = Pb;
-            r.elems = F_out;
-            r.nchunks = rc.n;
-            r.dst = grad_bias;
-            TimedLaunch tl(MPGNN_K_REDUCE, strm);
-            hipLaunchKernelGGL(reduce_slabs_kernel, dim3(1, (F_out + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                               strm, r);
-            if ((st = hip_check(hipGetLastError(), "reduce_slabs_kernel(bias) launch")) != MPGNN_OK) return st;
+    }
+    if (reduces.empty()) return MPGNN_OK;
+    if (g_merge_grad) {
+        ReduceArgs r3[3] = {reduces[0].r, reduces[0].r, reduces[0].r};
+        int gx[3] = {0, 0, 0}, ey = 0;
+        for (size_t k = 0; k < reduces.size(); ++k) {
+            r3[k] = reduces[k].r;
+            gx[k] = reduces[k].gx;
+            ey = std::max(ey, reduces[k].ey);
         }
+        TimedLaunch tl(MPGNN_K_REDUCE, strm);
+        hipLaunchKernelGGL(reduce_slabs3_kernel, dim3(gx[0] + gx[1] + gx[2], ey), dim3(kThreads), 0, strm, r3[0],
+                           r3[1], r3[2], gx[0], gx[1]);
+        return hip_check(hipGetLastError(), "reduce_slabs3_kernel launch");
+    }
+    for (const Part& pt : reduces) {
+        TimedLaunch tl(MPGNN_K_REDUCE, strm);
+        hipLaunchKernelGGL(reduce_slabs_kernel, dim3(pt.gx, pt.ey), dim3(kThreads), 0, strm, pt.r);
+        if ((st = hip_check(hipGetLastError(), "reduce_slabs_kernel launch")) != MPGNN_OK) return st;
     }
     return MPGNN_OK;
 }

@@ -769,3 +769,35 @@ def test_rel_gemm_dynamic_schedule_bitwise_equal():
                 assert torch.equal(a, b)
     finally:
         _lib.lib.mpgnn_set_option(12, 0)
+
+
+@pytest.mark.parametrize("mode", [MODE_SINGLE, MODE_ALL])
+def test_merged_gradient_launches_bitwise_equal(mode):
+    """MPGNN_OPT_MERGE_GRAD: dW and droot/dbias outer products in one launch + one slab-reduce
+    launch give the same bits as the separate launches (all, weight-only and bias-only grads)."""
+    from mpgnn_amd import _lib
+    g = data.config_graph("fb15k237")
+    R = g.num_relations
+    gen = torch.Generator().manual_seed(5)
+    W = torch.rand((R, 128, 64) if mode == MODE_ALL else (128, 64), generator=gen) - 0.5
+    root, bias = torch.rand(128, 64, generator=gen) - 0.5, torch.rand(64, generator=gen) - 0.5
+    gout = torch.randn(g.num_nodes, 64, generator=gen).to(DEV)
+    plan = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, g.num_nodes)
+
+    def run(req):
+        xg = g.x.to(DEV).requires_grad_(req[0])
+        ps = [t.to(DEV).requires_grad_(r) for t, r in zip((W, root, bias), req[1:])]
+        out = rgcn_conv(xg, *ps, plan, mode, relation=3, num_relations=R)
+        out.backward(gout)
+        return [t.grad.clone() for t in [xg] + ps if t.requires_grad]
+
+    for req in [(True, True, True, True), (False, True, False, False), (False, False, False, True),
+                (False, True, True, False)]:
+        ref = run(req)
+        _lib.check(_lib.lib.mpgnn_set_option(13, 0))
+        try:
+            sep = run(req)
+        finally:
+            _lib.lib.mpgnn_set_option(13, 1)
+        for a, b in zip(ref, sep):
+            assert torch.equal(a, b), req
