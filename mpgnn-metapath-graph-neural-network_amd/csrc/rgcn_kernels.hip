@@ -2707,12 +2707,26 @@ __global__ __launch_bounds__(kThreads) void reduce_slabs_kernel(ReduceArgs a) { 
 
 // Up to three reductions (dW groups, droot, dbias) in one launch: blocks [0, n0) → r0,
 // [n0, n0 + n1) → r1, the rest → r2; grid.y covers the widest.
+// Weight indices without a segment (relations absent from the graph) get zeros from the
+// same launch instead of a memset of the whole gradient.
+constexpr int kMaxZeroIds = 32;
+struct ZeroList {
+    float* dst;
+    int elems;
+    int n;
+    int ids[kMaxZeroIds];
+};
+
 __global__ __launch_bounds__(kThreads) void reduce_slabs3_kernel(ReduceArgs r0, ReduceArgs r1, ReduceArgs r2, int n0,
-                                                                 int n1) {
+                                                                 int n1, int n2, ZeroList z) {
     const int b = (int)blockIdx.x;
     if (b < n0) reduce_slabs_body(r0, b);
     else if (b < n0 + n1) reduce_slabs_body(r1, b - n0);
-    else reduce_slabs_body(r2, b - n0 - n1);
+    else if (b < n0 + n1 + n2) reduce_slabs_body(r2, b - n0 - n1);
+    else {
+        const int e = blockIdx.y * kThreads + threadIdx.x;
+        if (e < z.elems) z.dst[(size_t)z.ids[b - n0 - n1 - n2] * z.elems + e] = 0.0f;
+    }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -4005,6 +4019,7 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         int gx, ey;
     };
     std::vector<Part> reduces;
+    ZeroList zl{};
     bool have_w = false, have_root = false;
     OuterArgs ow{}, orr{};
     int nch = 0;
@@ -4013,9 +4028,20 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         // every weight index with a segment range is written (directly or by the slab reduce,
         // zeros for an empty range); only indices absent from the plan need the memset
         const bool all_written = (mode == MPGNN_MODE_ALL) ? (s.d_hi - s.d_lo) == (int64_t)R : (s.c_hi > s.c_lo);
-        if (!all_written)
+        if (!all_written && mode == MPGNN_MODE_ALL && g_merge_grad && (int64_t)R - (s.d_hi - s.d_lo) <= kMaxZeroIds) {
+            // the few absent relation ids are zeroed by the reduce launch
+            zl.dst = grad_weight;
+            zl.elems = (int)wsize;
+            int64_t d = s.d_lo;
+            for (int32_t id = 0; id < R; ++id) {
+                while (d < s.d_hi && p->rel_values[d] < id) ++d;
+                if (d < s.d_hi && p->rel_values[d] == id) continue;
+                zl.ids[zl.n++] = id;
+            }
+        } else if (!all_written) {
             if ((st = hip_check(hipMemsetAsync(grad_weight, 0, wbytes, strm), "memset grad_weight")) != MPGNN_OK)
                 return st;
+        }
         nch = s.c_hi - s.c_lo;
         if (nch > 0) {
             const float* H = h_save;
@@ -4127,18 +4153,18 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
             if ((st = hip_check(hipGetLastError(), "outer_accum_kernel(root) launch")) != MPGNN_OK) return st;
         }
     }
-    if (reduces.empty()) return MPGNN_OK;
+    if (reduces.empty() && zl.n == 0) return MPGNN_OK;
     if (g_merge_grad) {
-        ReduceArgs r3[3] = {reduces[0].r, reduces[0].r, reduces[0].r};
-        int gx[3] = {0, 0, 0}, ey = 0;
+        ReduceArgs r3[3] = {};
+        int gx[3] = {0, 0, 0}, ey = zl.n > 0 ? (zl.elems + kThreads - 1) / kThreads : 0;
         for (size_t k = 0; k < reduces.size(); ++k) {
             r3[k] = reduces[k].r;
             gx[k] = reduces[k].gx;
             ey = std::max(ey, reduces[k].ey);
         }
         TimedLaunch tl(MPGNN_K_REDUCE, strm);
-        hipLaunchKernelGGL(reduce_slabs3_kernel, dim3(gx[0] + gx[1] + gx[2], ey), dim3(kThreads), 0, strm, r3[0],
-                           r3[1], r3[2], gx[0], gx[1]);
+        hipLaunchKernelGGL(reduce_slabs3_kernel, dim3(gx[0] + gx[1] + gx[2] + zl.n, ey), dim3(kThreads), 0, strm, r3[0],
+                           r3[1], r3[2], gx[0], gx[1], gx[2], zl);
         return hip_check(hipGetLastError(), "reduce_slabs3_kernel launch");
     }
     for (const Part& pt : reduces) {
