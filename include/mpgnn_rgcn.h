@@ -133,6 +133,15 @@ int32_t mpgnn_rel_mean_fwd(const mpgnn_plan* plan, int32_t mode, int64_t relatio
                            int32_t num_relations, const float* x, int32_t F, float* h,
                            void* stream);
 
+/* Backward of mpgnn_rel_mean_fwd (autograd of PyG propagate's mean, mp_rgcn_layer.py:236):
+ * dx[j] = Σ_{edges (i, r, j) of the selection} dh[seg(i, r)] / count(seg), dh [seg_end - seg_begin, F]
+ * in the plan's segment order, dx [N, F] (every row written; rows without an edge are 0).
+ * Scratch: mpgnn_rel_mean_bwd_workspace_bytes. */
+int32_t mpgnn_rel_mean_bwd_workspace_bytes(const mpgnn_plan* plan, int32_t mode, int64_t relation,
+                                           int32_t num_relations, int32_t F, int64_t* bytes);
+int32_t mpgnn_rel_mean_bwd(const mpgnn_plan* plan, int32_t mode, int64_t relation, int32_t num_relations,
+                           const float* dh, int32_t F, float* dx, void* workspace, void* stream);
+
 /* Bytes of scratch the fwd/bwd calls need (caller allocates, e.g. torch.empty(uint8)). */
 int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* plan, int32_t mode, int64_t relation,
                                    int32_t num_relations, int32_t F_in, int32_t F_out,

@@ -62,6 +62,8 @@ SIGNATURES = [
     ("mpgnn_status_string", ctypes.c_char_p, [_I32]),
     ("mpgnn_abi_version", _I32, []),
     ("mpgnn_rel_mean_fwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P]),
+    ("mpgnn_rel_mean_bwd_workspace_bytes", _I32, [_P, _I32, _I64, _I32, _I32, _PI64]),
+    ("mpgnn_rel_mean_bwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _P]),
     ("mpgnn_rgcn_workspace_bytes", _I32, [_P, _I32, _I64, _I32, _I32, _I32, _I64, _I64, _PI64]),
     ("mpgnn_rgcn_fwd_workspace_bytes", _I32, [_P, _I32, _I64, _I32, _I32, _I32, _I64, _I64, _PI64]),
     ("mpgnn_rgcn_fwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _I64, _I64,

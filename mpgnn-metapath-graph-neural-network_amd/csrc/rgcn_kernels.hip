@@ -2729,6 +2729,16 @@ __global__ __launch_bounds__(kThreads) void reduce_slabs3_kernel(ReduceArgs r0, 
     }
 }
 
+// G[s] = dh[s] / cnt[sel_b + s] for the segment rows of a selection (segment-means backward)
+__global__ __launch_bounds__(kThreads) void scale_rows_kernel(const float* dh, const int* cnt, int sel_b, int rows,
+                                                              int F, float* G) {
+    const size_t n = (size_t)rows * F;
+    for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (size_t)gridDim.x * kThreads) {
+        const int r = (int)(i / F);
+        G[i] = dh[i] / (float)cnt[sel_b + r];
+    }
+}
+
 // ----------------------------------------------------------------------------------------
 // kernel timing: hipEvent pairs on the launch stream (mpgnn_timing_*)
 // ----------------------------------------------------------------------------------------
@@ -3864,7 +3874,172 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     return MPGNN_OK;
 }
 
+// grad_x-style transposed gather: dx[j] = Σ_{edges (i, r, j) of the selection} G[seg] (+ Groot[j]
+// for own rows), over the flat / ragged / mode-SINGLE lists (used by mpgnn_rgcn_bwd and
+// mpgnn_rel_mean_bwd).
+static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s, const float* G, const float* Groot,
+                          int F_in, int64_t row_lo, int64_t row_hi, float* grad_x, float* Pdx, bool exact,
+                          hipStream_t strm) {
+    int32_t st = MPGNN_OK;
+    RowSumArgs a{};
+    a.N = (int)p->N;
+    a.g.src = G;
+    a.g.F = F_in;
+    a.g.idx_off = s.sel_b;
+    a.extra = Groot;
+    a.bias = nullptr;
+    a.lo = (int)row_lo;
+    a.hi = (int)row_hi;
+    a.out = grad_x;
+    int k_lo = 0, k_hi = 0;
+    const int *pb = nullptr, *pe = nullptr;
+    const bool own_range = row_lo == p->shard_lo && row_hi == p->shard_hi;
+    if (mode == MPGNN_MODE_ALL && !exact && Groot != nullptr && own_range) {
+        // augmented transposed list: Σ G + G_root per own row
+        if (row_lo != 0 || row_hi != p->N) {
+            st = hip_check(hipMemsetAsync(grad_x, 0, (size_t)p->N * F_in * sizeof(float), strm), "memset grad_x");
+            if (st != MPGNN_OK) return st;
+        }
+        FlatRun f{};
+        f.fd = &p->d.tx_f;
+        f.c_lo = 0;
+        f.c_hi = (int)p->tx_f.chunk_ptr.size() - 1;
+        f.k_lo = 0;
+        f.k_hi = (int)p->tx_f.split_row.size();
+        f.table = p->d.tx_val;
+        f.idx_off = s.sel_b;
+        f.filter = !s.all_segments;
+        f.flo = s.sel_b;
+        f.fhi = s.sel_e;
+        f.src = G;
+        f.F = F_in;
+        f.row_off = 0;
+        f.out = grad_x;
+        f.carry = Pdx;
+        f.final_mode = 0;
+        f.extra = Groot;
+        f.lo = (int)row_lo;
+        f.hi = (int)row_hi;
+        TimedLaunch tl(MPGNN_K_ROW_DX, strm);
+        st = run_flat(f, strm);
+        if (st != MPGNN_OK) return st;
+    } else if (mode == MPGNN_MODE_ALL && !exact) {
+        FlatRun f{};
+        f.fd = &p->d.t_f;
+        f.c_lo = 0;
+        f.c_hi = (int)p->t_f.chunk_ptr.size() - 1;
+        f.table = p->d.t_seg;
+        f.idx_off = s.sel_b;
+        f.filter = !s.all_segments;
+        f.flo = s.sel_b;
+        f.fhi = s.sel_e;
+        f.src = G;
+        f.F = F_in;
+        f.row_off = 0;
+        f.out = grad_x;
+        f.carry = Pdx;
+        f.final_mode = 1;
+        f.row_ptr = p->d.t_ptr;
+        f.r_lo = 0;
+        f.r_hi = (int)p->N;
+        f.extra = Groot;
+        f.lo = (int)row_lo;
+        f.hi = (int)row_hi;
+        TimedLaunch tl(MPGNN_K_ROW_DX, strm);
+        st = run_flat(f, strm);
+        if (st != MPGNN_OK) return st;
+    } else if (mode == MPGNN_MODE_ALL) {
+        const bool ragged = !exact && !p->t_l.piece_b.empty() && s.sel_e > s.sel_b;
+        a.list_kind = 0;
+        a.ptr = ragged ? p->d.t_ent_ptr : p->d.t_ptr;
+        a.g.ent = ragged ? p->d.t_ent : nullptr;
+        a.res = p->d.t_res;
+        a.g.idx = p->d.t_seg;
+        a.g.filter = !s.all_segments;
+        a.g.flo = s.sel_b;
+        a.g.fhi = s.sel_e;
+        if (ragged) {
+            pb = p->d.t_pb;
+            pe = p->d.t_pe;
+            k_hi = (int)p->t_l.piece_b.size();
+        }
+    } else {
+        a.list_kind = 1;
+        a.g.idx = p->d.ta_seg;
+        if (!exact) {
+            a.keys = p->d.ta_key;
+            a.kb = s.ta_e_lo;
+            a.ke = s.ta_e_hi;
+            a.g.ent = p->d.ta_ent;
+            a.res = p->d.ta_res;
+            pb = p->d.ta_pb;
+            pe = p->d.ta_pe;
+            k_lo = s.tap_lo;
+            k_hi = s.tap_hi;
+        } else {
+            a.keys = p->d.ta_col;
+            a.kb = (s.d_hi > s.d_lo) ? p->rel_edge_ptr[s.d_lo] : 0;
+            a.ke = (s.d_hi > s.d_lo) ? p->rel_edge_ptr[s.d_hi] : 0;
+        }
+    }
+    if (!(mode == MPGNN_MODE_ALL && !exact)) {
+        TimedLaunch tl(MPGNN_K_ROW_DX, strm);
+        st = run_rowsum(p, a, pb, pe, k_lo, k_hi, Pdx, strm);
+        if (st != MPGNN_OK) return st;
+    }
+    return MPGNN_OK;
+}
+
+// Workspace of mpgnn_rel_mean_bwd: G = dh / cnt (S_sel × F), then the gather's carry slots.
+static void mean_bwd_layout(const mpgnn_plan* p, int32_t mode, const Selection& s, int F, size_t* off_pdx,
+                            size_t* total) {
+    const size_t S_sel = (size_t)(s.sel_e - s.sel_b);
+    const size_t seg_slots = std::max((size_t)(s.sp_hi - s.sp_lo), (size_t)p->seg_f.nslots);
+    const size_t dx_pieces = (mode == MPGNN_MODE_ALL)
+                                 ? std::max({p->t_l.piece_b.size(), (size_t)p->t_f.nslots, (size_t)p->tx_f.nslots})
+                                 : (size_t)(s.tap_hi - s.tap_lo);
+    *off_pdx = align256(S_sel * F * sizeof(float));
+    *total = std::max<size_t>(*off_pdx + align256(std::max(dx_pieces, seg_slots) * F * sizeof(float)), 256);
+}
+
 extern "C" {
+
+int32_t mpgnn_rel_mean_bwd_workspace_bytes(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, int32_t F,
+                                           int64_t* bytes) {
+    if (!p || !bytes) return arg_error("NULL argument");
+    Selection s;
+    int32_t st = make_selection(p, mode, relation, R, &s);
+    if (st != MPGNN_OK) return st;
+    size_t off, total;
+    mean_bwd_layout(p, mode, s, std::max(F, 1), &off, &total);
+    *bytes = (int64_t)total;
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_rel_mean_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* dh, int32_t F,
+                           float* dx, void* workspace, void* stream) {
+    int32_t st = check_common(p, F, F);
+    if (st != MPGNN_OK) return st;
+    Selection s;
+    if ((st = make_selection(p, mode, relation, R, &s)) != MPGNN_OK) return st;
+    if (p->N == 0) return MPGNN_OK;
+    if (!dx || !workspace || (s.sel_e > s.sel_b && !dh)) return arg_error("NULL dh, dx or workspace");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    if (s.sel_e == s.sel_b)
+        return hip_check(hipMemsetAsync(dx, 0, (size_t)p->N * F * sizeof(float), strm), "memset dx");
+    size_t off_pdx, total;
+    mean_bwd_layout(p, mode, s, F, &off_pdx, &total);
+    char* ws = static_cast<char*>(workspace);
+    float* G = reinterpret_cast<float*>(ws);
+    const int rows = s.sel_e - s.sel_b;
+    const size_t n = (size_t)rows * F;
+    hipLaunchKernelGGL(scale_rows_kernel, dim3((unsigned)std::min<size_t>((n + kThreads - 1) / kThreads, 8192)),
+                       dim3(kThreads), 0, strm, dh, p->d.s_cnt, s.sel_b, rows, F, G);
+    if ((st = hip_check(hipGetLastError(), "scale_rows_kernel launch")) != MPGNN_OK) return st;
+    TimedLaunch tl(MPGNN_K_ROW_DX, strm);
+    return run_grad_x(p, mode, s, G, nullptr, F, p->shard_lo, p->shard_hi, dx,
+                      reinterpret_cast<float*>(ws + off_pdx), g_exact_order, strm);
+}
 
 
 int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
@@ -3893,114 +4068,10 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         st = run_seg(p, mode, s, 1, grad_out, F_out, weight, root, 1, F_in, G, Groot, row_lo, row_hi, nullptr,
                      nullptr, true, MPGNN_K_SEG_DGRAD, strm);
         if (st != MPGNN_OK) return st;
-        RowSumArgs a{};
-        a.N = (int)p->N;
-        a.g.src = G;
-        a.g.F = F_in;
-        a.g.idx_off = s.sel_b;
-        a.extra = Groot;
-        a.bias = nullptr;
-        a.lo = (int)row_lo;
-        a.hi = (int)row_hi;
-        a.out = grad_x;
-        int k_lo = 0, k_hi = 0;
-        const int *pb = nullptr, *pe = nullptr;
-        const bool own_range = row_lo == p->shard_lo && row_hi == p->shard_hi;
-        if (mode == MPGNN_MODE_ALL && !exact && Groot != nullptr && own_range) {
-            // augmented transposed list: Σ G + G_root per own row
-            if (row_lo != 0 || row_hi != p->N) {
-                st = hip_check(hipMemsetAsync(grad_x, 0, (size_t)p->N * F_in * sizeof(float), strm), "memset grad_x");
-                if (st != MPGNN_OK) return st;
-            }
-            FlatRun f{};
-            f.fd = &p->d.tx_f;
-            f.c_lo = 0;
-            f.c_hi = (int)p->tx_f.chunk_ptr.size() - 1;
-            f.k_lo = 0;
-            f.k_hi = (int)p->tx_f.split_row.size();
-            f.table = p->d.tx_val;
-            f.idx_off = s.sel_b;
-            f.filter = !s.all_segments;
-            f.flo = s.sel_b;
-            f.fhi = s.sel_e;
-            f.src = G;
-            f.F = F_in;
-            f.row_off = 0;
-            f.out = grad_x;
-            f.carry = reinterpret_cast<float*>(ws + w.pdx);
-            f.final_mode = 0;
-            f.extra = Groot;
-            f.lo = (int)row_lo;
-            f.hi = (int)row_hi;
-            TimedLaunch tl(MPGNN_K_ROW_DX, strm);
-            st = run_flat(f, strm);
-            if (st != MPGNN_OK) return st;
-        } else if (mode == MPGNN_MODE_ALL && !exact) {
-            FlatRun f{};
-            f.fd = &p->d.t_f;
-            f.c_lo = 0;
-            f.c_hi = (int)p->t_f.chunk_ptr.size() - 1;
-            f.table = p->d.t_seg;
-            f.idx_off = s.sel_b;
-            f.filter = !s.all_segments;
-            f.flo = s.sel_b;
-            f.fhi = s.sel_e;
-            f.src = G;
-            f.F = F_in;
-            f.row_off = 0;
-            f.out = grad_x;
-            f.carry = reinterpret_cast<float*>(ws + w.pdx);
-            f.final_mode = 1;
-            f.row_ptr = p->d.t_ptr;
-            f.r_lo = 0;
-            f.r_hi = (int)p->N;
-            f.extra = Groot;
-            f.lo = (int)row_lo;
-            f.hi = (int)row_hi;
-            TimedLaunch tl(MPGNN_K_ROW_DX, strm);
-            st = run_flat(f, strm);
-            if (st != MPGNN_OK) return st;
-        } else if (mode == MPGNN_MODE_ALL) {
-            const bool ragged = !exact && !p->t_l.piece_b.empty() && s.sel_e > s.sel_b;
-            a.list_kind = 0;
-            a.ptr = ragged ? p->d.t_ent_ptr : p->d.t_ptr;
-            a.g.ent = ragged ? p->d.t_ent : nullptr;
-            a.res = p->d.t_res;
-            a.g.idx = p->d.t_seg;
-            a.g.filter = !s.all_segments;
-            a.g.flo = s.sel_b;
-            a.g.fhi = s.sel_e;
-            if (ragged) {
-                pb = p->d.t_pb;
-                pe = p->d.t_pe;
-                k_hi = (int)p->t_l.piece_b.size();
-            }
-        } else {
-            a.list_kind = 1;
-            a.g.idx = p->d.ta_seg;
-            if (!exact) {
-                a.keys = p->d.ta_key;
-                a.kb = s.ta_e_lo;
-                a.ke = s.ta_e_hi;
-                a.g.ent = p->d.ta_ent;
-                a.res = p->d.ta_res;
-                pb = p->d.ta_pb;
-                pe = p->d.ta_pe;
-                k_lo = s.tap_lo;
-                k_hi = s.tap_hi;
-            } else {
-                a.keys = p->d.ta_col;
-                a.kb = (s.d_hi > s.d_lo) ? p->rel_edge_ptr[s.d_lo] : 0;
-                a.ke = (s.d_hi > s.d_lo) ? p->rel_edge_ptr[s.d_hi] : 0;
-            }
-        }
-        if (!(mode == MPGNN_MODE_ALL && !exact)) {
-            TimedLaunch tl(MPGNN_K_ROW_DX, strm);
-            st = run_rowsum(p, a, pb, pe, k_lo, k_hi, reinterpret_cast<float*>(ws + w.pdx), strm);
-            if (st != MPGNN_OK) return st;
-        }
+        st = run_grad_x(p, mode, s, G, Groot, F_in, row_lo, row_hi, grad_x, reinterpret_cast<float*>(ws + w.pdx),
+                        exact, strm);
+        if (st != MPGNN_OK) return st;
     }
-
     const int mt = (F_in + kColTile - 1) / kColTile;
     const int nt = (F_out + kColTile - 1) / kColTile;
     const size_t outer_lds = (size_t)(4 * kOuterBuf) * sizeof(float);

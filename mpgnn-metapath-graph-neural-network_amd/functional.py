@@ -15,6 +15,8 @@ summed by an all-reduce (RCCL over xGMI for the "nccl" backend) and so are the g
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 import torch.distributed as dist
 
@@ -174,13 +176,38 @@ def rgcn_conv(x: torch.Tensor, weight: torch.Tensor, root, bias, plan: GraphPlan
     return out
 
 
+class _SegmentMeansFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, plan: GraphPlan, mode: int, relation: int, num_relations: int):
+        b, e = plan.select(mode, relation, num_relations)
+        h = torch.empty(e - b, x.shape[1], dtype=torch.float32, device=x.device)
+        check(lib.mpgnn_rel_mean_fwd(plan.handle, int(mode), int(relation), int(num_relations), x.data_ptr(),
+                                     x.shape[1], h.data_ptr(), _stream(x)), "mpgnn_rel_mean_fwd")
+        ctx.plan, ctx.mode, ctx.relation, ctx.num_relations = plan, mode, relation, num_relations
+        ctx.shape = x.shape
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        plan = ctx.plan
+        dh = dh.contiguous()
+        F = ctx.shape[1]
+        dx = torch.empty(ctx.shape, dtype=torch.float32, device=dh.device)
+        nbytes = ctypes.c_int64()
+        check(lib.mpgnn_rel_mean_bwd_workspace_bytes(plan.handle, int(ctx.mode), int(ctx.relation),
+                                                     int(ctx.num_relations), F, ctypes.byref(nbytes)),
+              "mpgnn_rel_mean_bwd_workspace_bytes")
+        ws = _workspace(int(nbytes.value), dh.device)
+        check(lib.mpgnn_rel_mean_bwd(plan.handle, int(ctx.mode), int(ctx.relation), int(ctx.num_relations),
+                                     dh.data_ptr(), F, dx.data_ptr(), ws.data_ptr(), _stream(dh)),
+              "mpgnn_rel_mean_bwd")
+        return dx, None, None, None, None
+
+
 def segment_means(x: torch.Tensor, plan: GraphPlan, mode: int, relation: int = -1,
                   num_relations: int = 0) -> torch.Tensor:
-    """Segment means [S_sel, F] in relation-major segment order (PyG propagate's mean, bit-exact)."""
+    """Segment means [S_sel, F] in relation-major segment order (PyG propagate's mean, bit-exact),
+    differentiable: the backward scatters dh / count to the gathered rows (mpgnn_rel_mean_bwd)."""
     x = _dev(x, "x")
     plan.to_device(x.device)
-    b, e = plan.select(mode, relation, num_relations)
-    h = torch.empty(e - b, x.shape[1], dtype=torch.float32, device=x.device)
-    check(lib.mpgnn_rel_mean_fwd(plan.handle, int(mode), int(relation), int(num_relations), x.data_ptr(),
-                                 x.shape[1], h.data_ptr(), _stream(x)), "mpgnn_rel_mean_fwd")
-    return h
+    return _SegmentMeansFn.apply(x, plan, int(mode), int(relation), int(num_relations))

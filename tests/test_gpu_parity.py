@@ -801,3 +801,32 @@ def test_merged_gradient_launches_bitwise_equal(mode):
             _lib.lib.mpgnn_set_option(13, 1)
         for a, b in zip(ref, sep):
             assert torch.equal(a, b), req
+
+
+@pytest.mark.parametrize("name,mode,rel", [("C1", MODE_ALL, -1), ("C1", MODE_SINGLE, 1), ("fb15k237", MODE_ALL, -1),
+                                           ("fb15k237", MODE_SINGLE, 3), ("fb15k237", MODE_SINGLE, 10_000)])
+def test_segment_means_backward_vs_oracle(name, mode, rel):
+    """mpgnn_rel_mean_bwd (autograd of segment_means) vs the oracle's autograd through PyG's
+    mean (index_select / scatter_add_ / div, mp_rgcn_layer.py:236), 1e-4; an absent relation
+    gives dx = 0."""
+    g = data.config_graph(name)
+    R = g.num_relations
+    plan = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, g.num_nodes)
+    xg = g.x.to(DEV).requires_grad_(True)
+    h = segment_means(xg, plan, mode, rel, R)
+    dh = torch.randn(h.shape, generator=torch.Generator().manual_seed(2))
+    h.backward(dh.to(DEV))
+    b, e = plan.select(mode, rel, R)
+    s_row = torch.from_numpy(plan.table("s_row")[b:e].astype(np.int64))
+    s_rel = plan.table("s_rel")[b:e]
+    xs = g.x.clone().requires_grad_(True)
+    loss = torch.zeros(())
+    for r in np.unique(s_rel):
+        hr = orc.segment_means(xs, g.edge_index, g.edge_type, int(r))
+        m = torch.from_numpy(s_rel == r)
+        loss = loss + (hr[s_row[m]] * dh[m]).sum()
+    if len(s_rel):
+        loss.backward()
+        rel_close(xg.grad, xs.grad, what="dx")
+    else:
+        assert torch.count_nonzero(xg.grad) == 0
