@@ -214,8 +214,10 @@ enum mpgnn_option {
                                    at 16; the tables do not depend on it */
     MPGNN_OPT_REL_QUEUE = 12,   /* rel_gemm_kernel: 1 = items taken from per-group atomic counters (dynamic
                                    schedule), 0 = fixed contiguous ranges; same results */
-    MPGNN_OPT_MERGE_GRAD = 13   /* backward: 1 (default) = weight / root / bias outer products in one launch and
+    MPGNN_OPT_MERGE_GRAD = 13,  /* backward: 1 (default) = weight / root / bias outer products in one launch and
                                    their slab reductions in one more; 0 = one launch each; same results */
+    MPGNN_OPT_REL_DEEP = 14     /* rel_gemm_kernel: 1 = A rows fetched two items ahead (two register sets);
+                                   same results */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

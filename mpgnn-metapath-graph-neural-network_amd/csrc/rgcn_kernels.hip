@@ -1055,6 +1055,7 @@ struct RelGemmArgs {
     int sel_b, row_lo, row_hi;
     int stagger;                 // s_sleep quanta (64 clk) the second half of the grid waits first
     int* queue;                  // nullable: per-group item counters (dynamic schedule), zero between launches
+    int deep;                    // 1: A rows fetched two items ahead (run_deep)
     unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][32] s_memtime timeline, or nullptr
 };
 
@@ -1272,6 +1273,92 @@ struct RelGemm {
         stamp_rt(31);
     }
 
+    // Static ranges as run(), with the A rows of item i+2 issued at the start of item i (two
+    // register sets alternate), so a tile's loads have two MFMA phases to land before their
+    // LDS commit at the end of item i+1 instead of one (MPGNN_OPT_REL_DEEP).
+    __device__ static void run_deep(const RelGemmArgs& a, float* smem) {
+        float* As = smem;                 // [2][32][lda]
+        float* Sc = smem + 2 * 32 * lda;  // [2][32] dgrad row scales
+        const int tid = threadIdx.x;
+        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int n_items = a.n_rel + a.n_root;
+        const int G = (int)gridDim.x;
+        const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
+        const int rng = g * q + min(g, rem) + ((int)blockIdx.x >> 3);
+        const int i_beg = (int)((long long)rng * n_items / G);
+        const int i_end = (int)((long long)(rng + 1) * n_items / G);
+        if (i_beg >= i_end) return;
+        const ItemTable tab = item_table(a, i_beg, i_end, lane);
+        auto get_item = [&](int i) { return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i); };
+        float4 va[WPT], vb[WPT];
+        int ca = 1, cb = 1;
+        Item cur = get_item(i_beg);
+        issue(a, cur, tid, va, ca);
+        float b[KH];
+        load_b(cur.w, wave, lane, b);
+        Item n1 = cur;
+        if (i_beg + 1 < i_end) {
+            n1 = get_item(i_beg + 1);
+            issue(a, n1, tid, vb, cb);
+        }
+        commit(cur, tid, va, ca, As, Sc);
+#pragma unroll
+        for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(b[j]));
+        __syncthreads();
+        int buf = 0;
+        // vh: registers holding item i+1 (committed at the end of item i); vn: receive item i+2
+        auto body = [&](int i, float4 (&vh)[WPT], int& ch, float4 (&vn)[WPT], int& cn) {
+            const bool has1 = i + 1 < i_end, has2 = i + 2 < i_end;
+            const Item n2 = has2 ? get_item(i + 2) : n1;
+            if (has2) issue(a, n2, tid, vn, cn);
+            const bool new_w = has1 && n1.w != cur.w;
+            float bn[KH];
+            if (new_w) load_b(n1.w, wave, lane, bn);
+            const float* Ab = As + buf * 32 * lda + c * lda + h * KH;
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+            float4 af = *reinterpret_cast<const float4*>(Ab);
+#pragma unroll
+            for (int j = 0; j < KH; j += 4) {
+                const float4 cf = af;
+                if (j + 4 < KH) af = *reinterpret_cast<const float4*>(Ab + j + 4);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], acc, 0, 0, 0);
+            }
+            float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
+            const float* sc = Sc + buf * 32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row < cur.nrows) {
+                    float o = acc[r];
+                    if constexpr (DGRAD) {
+                        if (!cur.root) o = o / sc[row];
+                    }
+                    Yt[(size_t)row * N + wave * 32 + c] = o;
+                }
+            }
+            if (has1) commit(n1, tid, vh, ch, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
+            if (new_w) {
+#pragma unroll
+                for (int j = 0; j < KH; ++j) b[j] = bn[j];
+            }
+            __syncthreads();
+            cur = n1;
+            n1 = n2;
+            buf ^= 1;
+        };
+        for (int i = i_beg; i < i_end; i += 2) {
+            body(i, vb, cb, va, ca);
+            if (i + 1 >= i_end) break;
+            body(i + 1, va, ca, vb, cb);
+        }
+    }
+
     // Dynamic schedule (MPGNN_OPT_REL_QUEUE): workgroups b ≡ g (mod 8) form group g and take
     // the items of [g·n/8, (g+1)·n/8) one at a time from the group's counter (atomicAdd), two
     // grabs ahead of the MFMAs, instead of a fixed contiguous range — a workgroup slowed by
@@ -1378,6 +1465,7 @@ template <int KB, bool DGRAD>
 __global__ __launch_bounds__(kThreads, 2) void rel_gemm_kernel(RelGemmArgs a) {
     extern __shared__ float smem[];
     if (a.queue != nullptr) RelGemm<KB, DGRAD>::run_dynamic(a, smem);
+    else if (a.deep) RelGemm<KB, DGRAD>::run_deep(a, smem);
     else RelGemm<KB, DGRAD>::run(a, smem);
 }
 
@@ -2867,6 +2955,7 @@ static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
 }
 
 
+static bool g_rel_deep = false;   // MPGNN_OPT_REL_DEEP: rel_gemm A rows two items ahead
 static bool g_merge_grad = true;  // MPGNN_OPT_MERGE_GRAD: dW + droot/dbias in one outer launch, one reduce launch
 static bool g_rel_queue = false;  // MPGNN_OPT_REL_QUEUE: dynamic item schedule in rel_gemm_kernel
 static std::mutex g_queue_mu;
@@ -3141,6 +3230,7 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         r.stamps = (kind == MPGNN_K_SEG_FWD) ? g_stamps : nullptr;
         r.stagger = g_rel_stagger;
         r.queue = (g_rel_queue && !g_stamps) ? rel_queue(strm) : nullptr;
+        r.deep = (g_rel_deep && !g_stamps) ? 1 : 0;
         TimedLaunch tl(kind, strm);
         launch_rel_gemm(r, K, gather_kind == 1, strm);
         return hip_check(hipGetLastError(), "rel_gemm_kernel launch");
@@ -3563,6 +3653,10 @@ using namespace mpgnn;
 extern "C" {
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_REL_DEEP) {
+        g_rel_deep = value != 0;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_MERGE_GRAD) {
         g_merge_grad = value != 0;
         return MPGNN_OK;

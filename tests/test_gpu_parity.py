@@ -740,10 +740,12 @@ def test_split_k_linear_matches_nn_linear(n, f_in, f_out):
         rel_close(got, want, tol=1e-5, what=what)
 
 
-def test_rel_gemm_dynamic_schedule_bitwise_equal():
-    """MPGNN_OPT_REL_QUEUE: items taken from atomic counters give the same bits as the fixed
-    ranges (each item is computed by the same code from the same inputs), over repeated
-    launches (the counters reset themselves), forward and dgrad, and a tiny grid (< 8 groups)."""
+@pytest.mark.parametrize("option", [12, 14])
+def test_rel_gemm_schedule_variants_bitwise_equal(option):
+    """MPGNN_OPT_REL_QUEUE (12): items taken from atomic counters; MPGNN_OPT_REL_DEEP (14): A rows
+    two items ahead. Both give the same bits as the default schedule (each item is computed by
+    the same code from the same inputs), over repeated launches (the counters reset
+    themselves), forward and dgrad, and a tiny grid (< 8 groups)."""
     from mpgnn_amd import _lib
     g = data.config_graph("fb15k237")
     small = data.synthetic_graph(60, 2, 3, feat_dim=128, seed=4)
@@ -761,14 +763,14 @@ def test_rel_gemm_dynamic_schedule_bitwise_equal():
         return res
 
     ref = run()
-    _lib.check(_lib.lib.mpgnn_set_option(12, 1))
+    _lib.check(_lib.lib.mpgnn_set_option(option, 1))
     try:
         for _ in range(3):
             got = run()
             for a, b in zip(got, ref):
                 assert torch.equal(a, b)
     finally:
-        _lib.lib.mpgnn_set_option(12, 0)
+        _lib.lib.mpgnn_set_option(option, 0)
 
 
 @pytest.mark.parametrize("mode", [MODE_SINGLE, MODE_ALL])
