@@ -84,10 +84,18 @@ def setup_dist(n):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != n:
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    # rehearsal of the N > 1 flow on a one-GPU box: every rank on device 0 over gloo
+    # (MPGNN_BENCH_REHEARSE=1); the numbers of such a run are not a measurement
+    rehearse = os.environ.get("MPGNN_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     group = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         group = dist.group.WORLD
     return rank, world, local, group
 
