@@ -216,8 +216,10 @@ enum mpgnn_option {
                                    schedule), 0 = fixed contiguous ranges; same results */
     MPGNN_OPT_MERGE_GRAD = 13,  /* backward: 1 (default) = weight / root / bias outer products in one launch and
                                    their slab reductions in one more; 0 = one launch each; same results */
-    MPGNN_OPT_REL_DEEP = 14     /* rel_gemm_kernel: 1 = A rows fetched two items ahead (two register sets);
+    MPGNN_OPT_REL_DEEP = 14,    /* rel_gemm_kernel: 1 = A rows fetched two items ahead (two register sets);
                                    same results */
+    MPGNN_OPT_REL_DIRECT = 15   /* rel_gemm_kernel: 1 = LDS-free, every wave loads its own A fragments (no
+                                   barriers); same results */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

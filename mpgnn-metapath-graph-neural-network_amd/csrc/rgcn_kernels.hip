@@ -1359,6 +1359,92 @@ struct RelGemm {
         }
     }
 
+    // LDS-free variant (MPGNN_OPT_REL_DIRECT): every wave loads its own A fragments straight
+    // into registers — lane (r = lane & 31, h = lane >> 5) holds row r, k ∈ [h·KH, (h+1)·KH),
+    // KH/4 float4 loads — so the four waves of a workgroup never synchronise (no barrier, no
+    // LDS commit). The next item's fragments load during the current MFMA chain (two register
+    // sets alternate); a relation change reloads the weight slice after the chain. The four
+    // waves read the same A rows (the three later reads hit L1 / L2).
+    __device__ static __forceinline__ void issue_direct(const RelGemmArgs& a, const Item& it, int lane,
+                                                        float4 (&f)[KH / 4], float& inv) {
+        const int r = min(lane & 31, it.nrows - 1);
+        const int h = lane >> 5;
+        int row = it.r0 + r;
+        const float* base;
+        inv = 1.0f;
+        if (it.root) {
+            base = a.Aroot;
+        } else if constexpr (DGRAD) {
+            base = a.Aroot;
+            inv = (float)a.s_cnt[row];
+            row = a.s_row[row];
+        } else {
+            base = a.Arel;
+            row -= a.sel_b;
+        }
+        const float4* src = reinterpret_cast<const float4*>(base + (size_t)row * K + h * KH);
+#pragma unroll
+        for (int j = 0; j < KH / 4; ++j) f[j] = src[j];
+    }
+
+    __device__ static void run_direct(const RelGemmArgs& a) {
+        const int tid = threadIdx.x;
+        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int n_items = a.n_rel + a.n_root;
+        const int G = (int)gridDim.x;
+        const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
+        const int rng = g * q + min(g, rem) + ((int)blockIdx.x >> 3);
+        const int i_beg = (int)((long long)rng * n_items / G);
+        const int i_end = (int)((long long)(rng + 1) * n_items / G);
+        if (i_beg >= i_end) return;
+        const ItemTable tab = item_table(a, i_beg, i_end, lane);
+        auto get_item = [&](int i) { return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i); };
+        float4 fa[KH / 4], fb[KH / 4];
+        float inva = 1.0f, invb = 1.0f;
+        Item cur = get_item(i_beg);
+        issue_direct(a, cur, lane, fa, inva);
+        float b[KH];
+        load_b(cur.w, wave, lane, b);
+        // vh: fragments of item i (loaded one item earlier); vn: receive item i+1
+        auto body = [&](int i, float4 (&vh)[KH / 4], float& invh, float4 (&vn)[KH / 4], float& invn) {
+            const bool has1 = i + 1 < i_end;
+            const Item nxt = has1 ? get_item(i + 1) : cur;
+            if (has1) issue_direct(a, nxt, lane, vn, invn);
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+            for (int j = 0; j < KH / 4; ++j) {
+                const float4 cf = vh[j];
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[4 * j], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[4 * j + 1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[4 * j + 2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[4 * j + 3], acc, 0, 0, 0);
+            }
+            // epilogue: accumulator register r = rows (r&3) + 8(r>>2) + 4h, column 32·wave + c;
+            // the dgrad row scale of row q sits in lane q (and q + 32) of invh
+            float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                float o = acc[r];
+                if constexpr (DGRAD) {
+                    const float d = __shfl(invh, row);
+                    if (!cur.root) o = o / d;
+                }
+                if (row < cur.nrows) Yt[(size_t)row * N + wave * 32 + c] = o;
+            }
+            if (has1 && nxt.w != cur.w) load_b(nxt.w, wave, lane, b);  // after the chain: b is free
+            cur = nxt;
+        };
+        for (int i = i_beg; i < i_end; i += 2) {
+            body(i, fa, inva, fb, invb);
+            if (i + 1 >= i_end) break;
+            body(i + 1, fb, invb, fa, inva);
+        }
+    }
+
     // Dynamic schedule (MPGNN_OPT_REL_QUEUE): workgroups b ≡ g (mod 8) form group g and take
     // the items of [g·n/8, (g+1)·n/8) one at a time from the group's counter (atomicAdd), two
     // grabs ahead of the MFMAs, instead of a fixed contiguous range — a workgroup slowed by
@@ -1467,6 +1553,11 @@ __global__ __launch_bounds__(kThreads, 2) void rel_gemm_kernel(RelGemmArgs a) {
     if (a.queue != nullptr) RelGemm<KB, DGRAD>::run_dynamic(a, smem);
     else if (a.deep) RelGemm<KB, DGRAD>::run_deep(a, smem);
     else RelGemm<KB, DGRAD>::run(a, smem);
+}
+
+template <int KB, bool DGRAD>
+__global__ __launch_bounds__(kThreads, 2) void rel_gemm_direct_kernel(RelGemmArgs a) {
+    RelGemm<KB, DGRAD>::run_direct(a);
 }
 
 
@@ -2955,6 +3046,7 @@ static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
 }
 
 
+static bool g_rel_direct = false; // MPGNN_OPT_REL_DIRECT: LDS-free rel_gemm (waves load their own A fragments)
 static bool g_rel_deep = false;   // MPGNN_OPT_REL_DEEP: rel_gemm A rows two items ahead
 static bool g_merge_grad = true;  // MPGNN_OPT_MERGE_GRAD: dW + droot/dbias in one outer launch, one reduce launch
 static bool g_rel_queue = false;  // MPGNN_OPT_REL_QUEUE: dynamic item schedule in rel_gemm_kernel
@@ -2989,6 +3081,10 @@ static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
     const size_t lds = (size_t)(2 * 32 * lda + 64 + 4) * sizeof(float);
     const int n_items = a.n_rel + a.n_root;
     const int grid = std::min(n_items, cu_count() * g_rel_wg_per_cu);
+    if (a.deep == 2) {
+        hipLaunchKernelGGL((rel_gemm_direct_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), 0, st, a);
+        return;
+    }
     hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
@@ -3230,7 +3326,7 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         r.stamps = (kind == MPGNN_K_SEG_FWD) ? g_stamps : nullptr;
         r.stagger = g_rel_stagger;
         r.queue = (g_rel_queue && !g_stamps) ? rel_queue(strm) : nullptr;
-        r.deep = (g_rel_deep && !g_stamps) ? 1 : 0;
+        r.deep = g_stamps ? 0 : (g_rel_direct ? 2 : (g_rel_deep ? 1 : 0));
         TimedLaunch tl(kind, strm);
         launch_rel_gemm(r, K, gather_kind == 1, strm);
         return hip_check(hipGetLastError(), "rel_gemm_kernel launch");
@@ -3653,6 +3749,10 @@ using namespace mpgnn;
 extern "C" {
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_REL_DIRECT) {
+        g_rel_direct = value != 0;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_REL_DEEP) {
         g_rel_deep = value != 0;
         return MPGNN_OK;

@@ -740,7 +740,7 @@ def test_split_k_linear_matches_nn_linear(n, f_in, f_out):
         rel_close(got, want, tol=1e-5, what=what)
 
 
-@pytest.mark.parametrize("option", [12, 14])
+@pytest.mark.parametrize("option", [12, 14, 15])
 def test_rel_gemm_schedule_variants_bitwise_equal(option):
     """MPGNN_OPT_REL_QUEUE (12): items taken from atomic counters; MPGNN_OPT_REL_DEEP (14): A rows
     two items ahead. Both give the same bits as the default schedule (each item is computed by
