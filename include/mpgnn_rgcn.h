@@ -218,8 +218,10 @@ enum mpgnn_option {
                                    their slab reductions in one more; 0 = one launch each; same results */
     MPGNN_OPT_REL_DEEP = 14,    /* rel_gemm_kernel: 1 = A rows fetched two items ahead (two register sets);
                                    same results */
-    MPGNN_OPT_REL_DIRECT = 15   /* rel_gemm_kernel: 1 = LDS-free, every wave loads its own A fragments (no
+    MPGNN_OPT_REL_DIRECT = 15,  /* rel_gemm_kernel: 1 = LDS-free, every wave loads its own A fragments (no
                                    barriers); same results */
+    MPGNN_OPT_FLAT_CPW = 16     /* flat row-sum kernel: plan chunks per wave, 1 (default), 2 or 4, the next
+                                   chunk's metadata fetched behind the current rows; same results */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

@@ -2332,6 +2332,119 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
     }
 }
 
+// flat_rows_multi_kernel — as flat_rows_kernel, but each wave walks CPW consecutive chunks and
+// fetches the next chunk's metadata (chunk bounds, node ids, row ids) while the current chunk's
+// first rows are in flight (MPGNN_OPT_FLAT_CPW).
+template <int V, int T, int U, int CPW>
+__global__ __launch_bounds__(kThreads) void flat_rows_multi_kernel(FlatArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int c0 = a.c_lo + ((int)blockIdx.x * kWaves + (int)(threadIdx.x >> 6)) * CPW;
+    if (c0 >= a.c_hi) return;
+    const int c_end = min(a.c_hi, c0 + CPW);
+    const int F = a.F;
+    int m_p0, m_n, m_info, m_val, m_row;
+    auto load_meta = [&](int c) {
+        m_p0 = ld_uniform(a.chunk_ptr, c);
+        m_n = ld_uniform(a.chunk_ptr, c + 1) - m_p0;
+        m_info = ld_uniform(a.chunk_info, c);
+        const int q = m_p0 + min(lane, m_n - 1);
+        m_val = a.table[q];
+        m_row = a.row_of[q];
+    };
+    load_meta(c0);
+    for (int c = c0; c < c_end; ++c) {
+    const int n = m_n, info = m_info, val = m_val, row = m_row;
+    bool prefetched = false;
+    bool keep = lane < n;
+    const bool isx = val < 0;  // augmented lists: the row's trailing extra entry
+    if (a.filter) keep = keep && (isx || (val >= a.flo && val < a.fhi));
+    const int srow = keep ? (isx ? -val - 1 : val - a.idx_off) : 0;
+    const unsigned long long xm = __ballot(keep && isx);
+    const bool has_cnt = a.cnt != nullptr;
+    const int cnt_l = (has_cnt ? a.cnt : a.dummy)[has_cnt ? row : 0];
+    const int next = __shfl_down(row, 1);
+    const unsigned long long lastm = __ballot(lane < n && (lane == n - 1 || next != row));
+    const unsigned long long keepm = __ballot(keep);
+    const int rf = readlane(row, 0);
+    const int rl = readlane(row, n - 1);
+    const bool fs = info & 1, ls = info & 2;
+    const int slot0 = info >> 2;
+    int colc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, F - V);
+    const bool has_b = a.bias != nullptr;
+    float bb[T][V];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        vload<V>(has_b ? a.bias + colc[t] : a.src, bb[t]);
+#pragma unroll
+        for (int k = 0; k < V; ++k) bb[t][k] = has_b ? bb[t][k] : 0.0f;
+    }
+
+    float acc[T][V];
+    zero_acc<V, T>(acc);
+    for (int u0 = 0; u0 < n; u0 += U) {
+        float v[U][T][V];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = min(u0 + u, n - 1);
+            const int r = readlane(srow, q);
+            const float* base = (((xm >> q) & 1ull) ? a.extra : a.src) + (size_t)r * F;
+#pragma unroll
+            for (int t = 0; t < T; ++t) vload<V>(base + colc[t], v[u][t]);
+        }
+        if (!prefetched && c + 1 < c_end) {  // next chunk's metadata behind this chunk's rows
+            load_meta(c + 1);
+            prefetched = true;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = u0 + u;
+            if (q < n) {
+                if ((keepm >> q) & 1ull) {
+#pragma unroll
+                    for (int t = 0; t < T; ++t)
+#pragma unroll
+                        for (int k = 0; k < V; ++k) acc[t][k] += v[u][t][k];
+                }
+                if ((lastm >> q) & 1ull) {
+                    const int rr = readlane(row, q);
+                    const bool split = (rr == rf && fs) || (rr == rl && ls);
+                    float* dst;
+                    bool div = false, addb = false;
+                    if (!split) {
+                        dst = a.out + (size_t)(rr - a.row_off) * F;
+                        div = has_cnt;
+                        addb = has_b && rr >= a.lo && rr < a.hi;
+                    } else {
+                        const int slot = slot0 + ((fs && rr == rl && rl != rf) ? 1 : 0);
+                        dst = a.carry + (size_t)slot * F;
+                    }
+                    const float d = (float)readlane(cnt_l, q);
+#pragma unroll
+                    for (int t = 0; t < T; ++t) {
+                        const int col = (t * 64 + lane) * V;
+                        if (col < F) {
+                            float o[V];
+#pragma unroll
+                            for (int k = 0; k < V; ++k) {
+                                o[k] = div ? acc[t][k] / d : acc[t][k];
+                                if (addb) o[k] = o[k] + bb[t][k];
+                                if (!split && a.relu) o[k] = fmaxf(o[k], 0.0f);
+                            }
+                            vstore<V>(dst + col, o);
+                        }
+                    }
+                    zero_acc<V, T>(acc);
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    }
+}
+
 // finalize_rows_kernel — one wave per row.
 //   mode 0 (segment means): split rows k in [k0, k1): out[row] = (Σ carry slots in order) / cnt
 //   mode 1 (combine, grad_x): every row in [r_lo, r_hi):
@@ -3507,6 +3620,7 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
     return hip_check(hipGetLastError(), "row_sum_kernel launch");
 }
 
+static int g_flat_cpw = 1;  // MPGNN_OPT_FLAT_CPW: chunks per wave in the flat row-sum kernel (1, 2 or 4)
 static int g_flat_u = 16;  // MPGNN_OPT_FLAT_U: rows in flight per wave in flat_rows_kernel (16 or 32; 32 for V·T <= 2 only)
 
 template <int V, int T>
@@ -3517,6 +3631,16 @@ static void launch_flat(const FlatArgs& a, hipStream_t st) {
             hipLaunchKernelGGL((flat_rows_kernel<V, T, 32>), dim3((n + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
             return;
         }
+    }
+    if (g_flat_cpw == 2) {
+        hipLaunchKernelGGL((flat_rows_multi_kernel<V, T, 16, 2>), dim3((n + 2 * kWaves - 1) / (2 * kWaves)), dim3(kThreads),
+                           0, st, a);
+        return;
+    }
+    if (g_flat_cpw == 4) {
+        hipLaunchKernelGGL((flat_rows_multi_kernel<V, T, 16, 4>), dim3((n + 4 * kWaves - 1) / (4 * kWaves)), dim3(kThreads),
+                           0, st, a);
+        return;
     }
     hipLaunchKernelGGL((flat_rows_kernel<V, T>), dim3((n + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
 }
@@ -3749,6 +3873,11 @@ using namespace mpgnn;
 extern "C" {
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_FLAT_CPW) {
+        if (value != 1 && value != 2 && value != 4) return arg_error("MPGNN_OPT_FLAT_CPW must be 1, 2 or 4");
+        g_flat_cpw = (int)value;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_REL_DIRECT) {
         g_rel_direct = value != 0;
         return MPGNN_OK;

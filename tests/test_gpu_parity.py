@@ -740,8 +740,8 @@ def test_split_k_linear_matches_nn_linear(n, f_in, f_out):
         rel_close(got, want, tol=1e-5, what=what)
 
 
-@pytest.mark.parametrize("option", [12, 14, 15])
-def test_rel_gemm_schedule_variants_bitwise_equal(option):
+@pytest.mark.parametrize("option,value,default", [(12, 1, 0), (14, 1, 0), (15, 1, 0), (16, 2, 1), (16, 4, 1)])
+def test_rel_gemm_schedule_variants_bitwise_equal(option, value, default):
     """MPGNN_OPT_REL_QUEUE (12): items taken from atomic counters; MPGNN_OPT_REL_DEEP (14): A rows
     two items ahead. Both give the same bits as the default schedule (each item is computed by
     the same code from the same inputs), over repeated launches (the counters reset
@@ -763,14 +763,14 @@ def test_rel_gemm_schedule_variants_bitwise_equal(option):
         return res
 
     ref = run()
-    _lib.check(_lib.lib.mpgnn_set_option(option, 1))
+    _lib.check(_lib.lib.mpgnn_set_option(option, value))
     try:
         for _ in range(3):
             got = run()
             for a, b in zip(got, ref):
                 assert torch.equal(a, b)
     finally:
-        _lib.lib.mpgnn_set_option(option, 0)
+        _lib.lib.mpgnn_set_option(option, default)
 
 
 @pytest.mark.parametrize("mode", [MODE_SINGLE, MODE_ALL])
