@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=2)
     a = ap.parse_args()
-    dflt = {"fb15k237": (3, 128, 10), "C2": (2, 128, 10), "C5": (3, 256, 2)}[a.workload]
+    dflt = {"fb15k237": (3, 128, 30), "C2": (2, 128, 10), "C5": (3, 256, 2)}[a.workload]
     a.layers = dflt[0] if a.layers is None else a.layers
     a.feat = dflt[1] if a.feat is None else a.feat
     a.epoch_steps = dflt[2] if a.epoch_steps is None else a.epoch_steps
@@ -284,7 +284,7 @@ def main():
 
     epoch_ms = None
     if args.epoch_steps > 0:
-        for _ in range(2):
+        for _ in range(5):
             epoch()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
