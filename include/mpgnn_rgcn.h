@@ -220,8 +220,11 @@ enum mpgnn_option {
                                    same results */
     MPGNN_OPT_REL_DIRECT = 15,  /* rel_gemm_kernel: 1 = LDS-free, every wave loads its own A fragments (no
                                    barriers); same results */
-    MPGNN_OPT_FLAT_CPW = 16     /* flat row-sum kernel: plan chunks per wave, 1 (default), 2 or 4, the next
+    MPGNN_OPT_FLAT_CPW = 16,    /* flat row-sum kernel: plan chunks per wave, 1 (default), 2 or 4, the next
                                    chunk's metadata fetched behind the current rows; same results */
+    MPGNN_OPT_Y_ROWMAJOR = 17   /* forward, mode ALL: 1 = the transform writes its rows in the combine list's
+                                   order and the combine streams them; 0 (default) = relation-major rows gathered
+                                   by the combine; same results */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 
