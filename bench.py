@@ -226,6 +226,22 @@ def main():
     _lib.lib.mpgnn_set_option(3, -1)
     seg_ms, seg_n = _lib.kernel_timing("seg_fwd")
     row_ms, row_n = _lib.kernel_timing("row_fwd")
+
+    # ---- per-kernel breakdown: a third pass with every kernel kind timed (events between all
+    # kernels make each launch slightly longer than in the headline pass; attribution only)
+    _lib.lib.mpgnn_timing_reset()
+    _lib.lib.mpgnn_timing_enable(1)
+    with torch.no_grad():
+        for _ in range(args.steps):
+            step()
+    torch.cuda.synchronize()
+    _lib.lib.mpgnn_timing_enable(0)
+    per_layer = {}
+    for kind, label in (("mean", "segment means: flat_rows_kernel + split-row finalize"), ("final", "split-row finalize alone"),
+                        ("seg_fwd", "transform GEMM"), ("row_fwd", "combine (flat_rows_kernel)")):
+        k_ms, k_n = _lib.kernel_timing(kind)
+        if k_n:
+            per_layer[kind] = {"what": label, "us_per_layer": round(k_ms * 1e3 / (args.steps * args.layers), 2)}
     if group is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
@@ -233,6 +249,16 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     edges_per_step = args.layers * g.num_edges
     value = edges_per_step * args.steps / elapsed
+    # SURVEY §8d layer roofline: algorithmic bytes per forward layer
+    # B = E·(4·F_in + 4) + S·8 + N·4·F_out (gathered rows + their column ids, segment ptr/rel,
+    # output write); at 8 TB/s that bounds edges/s at E / (B / 8e12)
+    b_layer = g.num_edges * (4 * F + 4) + plan.num_segments * 8 + g.num_nodes * 4 * F
+    ideal = g.num_edges / (b_layer / (PEAK_HBM * 1e9))
+    hbm_roofline = {"bound": "hbm", "alg_bytes_per_layer": b_layer,
+                    "achieved_GBps": round(value / g.num_edges * b_layer / 1e9, 1), "peak_GBps": PEAK_HBM,
+                    "ideal_edges_per_s": round(ideal, 1), "frac": round(value / ideal, 4),
+                    "note": "whole-step edges/s against the aggregation's HBM roofline of SURVEY §8d (516 B per "
+                            "edge at F=128); at C3 x (7.4 MB) stays in L2/MALL, so the layer is bound on-die"}
 
     # ---- the same step replayed as one HIP graph (launch overhead removed) ---------------
     graph = None
@@ -404,6 +430,8 @@ def main():
             "epoch_graph": epoch_graph,
             "epoch_def": "main_rgcn.py:458-461 train (fwd+NLL+bwd+Adam) + validation forward",
             "roofline": roofline,
+            "hbm_roofline": hbm_roofline,
+            "kernels_per_layer": per_layer,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
