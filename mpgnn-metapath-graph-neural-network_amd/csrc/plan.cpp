@@ -226,7 +226,8 @@ static void build_ragged(const std::vector<int32_t>& run_ptr, RaggedHost& L) {
 
 // Flat chunked list over runs r (positions [run_ptr[r], run_ptr[r+1]), output row r) with
 // forced cuts at run indices `cuts` (ascending, first 0, last = runs).
-static void build_flat(const std::vector<int32_t>& run_ptr, const std::vector<int32_t>& cuts, FlatHost& L) {
+static void build_flat(const std::vector<int32_t>& run_ptr, const std::vector<int32_t>& cuts, FlatHost& L,
+                       int32_t chunk = kFlatChunk) {
     const int32_t runs = run_ptr.empty() ? 0 : (int32_t)run_ptr.size() - 1;
     const int32_t P = runs > 0 ? run_ptr[runs] : 0;
     L = FlatHost{};
@@ -243,7 +244,7 @@ static void build_flat(const std::vector<int32_t>& run_ptr, const std::vector<in
         while (q < pe) {
             const int32_t r = L.row_of[q];
             const int32_t rend = std::min(run_ptr[r + 1], pe);
-            if (rend - cs <= kFlatChunk) {  // the rest of run r fits the chunk
+            if (rend - cs <= chunk) {  // the rest of run r fits the chunk
                 q = rend;
                 continue;
             }
@@ -252,7 +253,7 @@ static void build_flat(const std::vector<int32_t>& run_ptr, const std::vector<in
                 cs = q;
                 continue;
             }
-            q = cs + kFlatChunk;  // run longer than a chunk: cut inside it
+            q = cs + chunk;  // run longer than a chunk: cut inside it
             L.chunk_ptr.push_back(q);
             cs = q;
         }
@@ -490,11 +491,11 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
         build_flat(p->s_ptr, seg_cuts, p->seg_f);
         const std::vector<int32_t> node_cuts{0, (int32_t)N};
         build_flat(p->t_ptr, node_cuts, p->t_f);
-        build_flat(p->rw_ptr, node_cuts, p->rw_f);
+        build_flat(p->rw_ptr, node_cuts, p->rw_f, kFlatChunkRowMajor);
         // augmented lists: own rows [lo, hi) get a trailing extra-row entry
         std::vector<int32_t> xptr(N + 1, 0);
         auto augment = [&](const std::vector<int32_t>& ptr, const std::vector<int32_t>& val, FlatHost& F,
-                           std::vector<int32_t>& out_val) {
+                           std::vector<int32_t>& out_val, int32_t chunk) {
             parallel_for(N, [&](int64_t i) { xptr[i] = ptr[i] + (int32_t)std::clamp<int64_t>(i, lo, hi) - (int32_t)lo; });
             xptr[N] = ptr[N] + (int32_t)(hi - lo);
             out_val.assign(xptr[N], 0);
@@ -503,10 +504,10 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
                 for (int32_t q = ptr[i]; q < ptr[i + 1]; ++q) out_val[w++] = val[q];
                 if (i >= lo && i < hi) out_val[w] = -(int32_t)(i - lo) - 1;
             });
-            build_flat(xptr, node_cuts, F);
+            build_flat(xptr, node_cuts, F, chunk);
         };
-        augment(p->t_ptr, p->t_seg, p->tx_f, p->tx_val);
-        augment(p->rw_ptr, p->rw_seg, p->rwx_f, p->rwx_val);
+        augment(p->t_ptr, p->t_seg, p->tx_f, p->tx_val, kFlatChunk);
+        augment(p->rw_ptr, p->rw_seg, p->rwx_f, p->rwx_val, kFlatChunkRowMajor);
         // positions in the rwx list (xptr is the row-major combine list's now)
         p->seg_rwx_pos.assign(p->S, 0);
         parallel_for(N, [&](int64_t i) {

@@ -14,6 +14,7 @@ import numpy as np
 
 TILE_ROWS = 64
 FLAT_CHUNK = 32
+FLAT_CHUNK_ROW_MAJOR = 16  # the row-major (combine) list (plan_internal.h kFlatChunkRowMajor)
 
 
 def build_plan(edge_index: np.ndarray, edge_type: np.ndarray, num_nodes: int,
@@ -86,9 +87,9 @@ def build_plan(edge_index: np.ndarray, edge_type: np.ndarray, num_nodes: int,
         s_cnt=s_cnt, s_pos=s_pos, rw_ptr=rw_ptr, rw_seg=rw_seg, t_ptr=t_ptr, t_seg=t_seg,
         ta_col=ta_col, ta_seg=ta_seg, rel_invalid=rel_invalid,
     )
-    for name, run_ptr, cuts in (("seg", s_ptr, rel_seg_ptr), ("t", t_ptr, np.array([0, N])),
-                                ("rw", rw_ptr, np.array([0, N]))):
-        for k, v in build_flat(run_ptr, cuts).items():
+    for name, run_ptr, cuts, chunk in (("seg", s_ptr, rel_seg_ptr, FLAT_CHUNK), ("t", t_ptr, np.array([0, N]), FLAT_CHUNK),
+                                       ("rw", rw_ptr, np.array([0, N]), FLAT_CHUNK_ROW_MAJOR)):
+        for k, v in build_flat(run_ptr, cuts, chunk).items():
             out[f"{name}_f_{k}"] = v
     return out
 

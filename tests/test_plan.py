@@ -156,17 +156,17 @@ def test_flat_lists_bit_exact_and_well_formed(case, shard):
     for tname in FLAT:
         got = plan.table(tname)
         assert np.array_equal(got, ref[tname]), tname
-    for l, run_ptr in (("seg", ref["s_ptr"]), ("t", ref["t_ptr"]), ("rw", ref["rw_ptr"])):
+    for l, run_ptr, chunk in (("seg", ref["s_ptr"], 32), ("t", ref["t_ptr"], 32), ("rw", ref["rw_ptr"], 16)):
         cp = plan.table(f"{l}_f_chunk_ptr")
         sizes = np.diff(cp)
-        assert (sizes >= 1).all() and (sizes <= 32).all(), l
+        assert (sizes >= 1).all() and (sizes <= chunk).all(), l
         assert cp[0] == 0 and cp[-1] == (run_ptr[-1] if len(run_ptr) else 0), l
         ends = set(run_ptr.tolist())
         row_of = plan.table(f"{l}_f_row_of")
         for b in cp[1:-1]:
             if b not in ends:  # a cut inside a row: that row is longer than one chunk
                 r = row_of[b]
-                assert run_ptr[r + 1] - run_ptr[r] > 32, (l, r)
+                assert run_ptr[r + 1] - run_ptr[r] > chunk, (l, r)
         sp, ss = plan.table(f"{l}_f_split_ptr"), plan.table(f"{l}_f_split_slot")
         assert len(np.unique(ss)) == len(ss), l
         for k, r in enumerate(plan.table(f"{l}_f_split_row")):
