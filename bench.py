@@ -9,8 +9,10 @@ One timed STEP = one forward pass of the 3 relational layers over the whole grap
 resident in HBM.  value = edges aggregated per second = 3 · E · steps / time (an edge
 aggregated = one (node_1, rel, node_2) edge folded into its (node_1, rel) segment in one
 layer).  With --gpus N (torchrun, one process per GPU) the graph is sharded by
-node_2 range (edge-balanced) and each layer's partial outputs are summed by an RCCL
-all-reduce over xGMI: total work is fixed, so "scaling" is "strong".
+node_2 range (edge-balanced) and each layer's partial outputs are summed by RCCL over xGMI —
+a reduce-scatter per layer (the next layer only gathers the rank's own node_2 rows), one
+all-gather after the last (distributed.sharded_stack_forward); the training epoch keeps the
+per-layer all-reduce of RGCNConv(shard=, group=). Total work is fixed: "scaling" is "strong".
 
 Also reported (separate loops, outside the timed step): the training epoch of
 main_rgcn.py:458-461 — train step (forward + NLL + backward + Adam) + validation forward.
@@ -40,7 +42,7 @@ sys.path.insert(0, ROOT)
 
 import mpgnn_amd  # noqa: E402
 from mpgnn_amd import _lib, data  # noqa: E402
-from mpgnn_amd.distributed import shard_ranges  # noqa: E402
+from mpgnn_amd.distributed import shard_ranges, sharded_stack_forward  # noqa: E402
 
 METRIC = "edges aggregated/sec + epoch time, FB15K-237 128-d at 1/2/4/8 MI355X"
 PEAK_FP32_MFMA = 157.3  # TFLOP/s dense (MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32)
@@ -181,14 +183,18 @@ def main():
     net = net.to(dev)
     x, ei, et = g.x.to(dev), g.edge_index.to(dev), g.edge_type.to(dev)
     shard = None
+    ranges = None
     if world > 1:
-        shard = shard_ranges(g.edge_index, g.num_nodes, world)[rank]
+        ranges = shard_ranges(g.edge_index, g.num_nodes, world)
+        shard = ranges[rank]
     convs = [net.conv1] + [net.conv2] * (args.layers - 1)
 
     def step():
+        if world > 1:  # partial sums reduce-scattered per layer, one all-gather at the end
+            return sharded_stack_forward(convs, x, ei, et, ranges, group)
         h = x
         for conv in convs:
-            h = conv(h, ei, et, shard=shard, group=group, activation="relu")  # F.relu(conv(...)), model.py:144,146
+            h = conv(h, ei, et, activation="relu")  # F.relu(conv(...)), model.py:144,146
         return h
 
     # plan (built once per graph, cached) + warm-up
@@ -424,7 +430,9 @@ def main():
                                    f"L={args.layers}, F_in=F_hidden=F_out={F}",
                        "graph": {"nodes": g.num_nodes, "relations": g.num_relations, "edges": g.num_edges,
                                  "segments": S if world == 1 else None},
-                       "parallelism": "single GPU" if world == 1 else f"dst-range shards x{world} + RCCL all-reduce"},
+                       "parallelism": "single GPU" if world == 1 else
+                       f"dst-range shards x{world}: per layer an RCCL reduce-scatter of the partial sums "
+                       "(each rank keeps the rows it gathers next), one all-gather after the last layer"},
             "graph_replay": graph,
             "epoch_ms": round(epoch_ms, 3) if epoch_ms is not None else None,
             "epoch_graph": epoch_graph,

@@ -16,7 +16,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-__all__ = ["shard_ranges", "edge_balanced_ranges", "rank_slice", "metapath_fanout", "best_metapaths"]
+__all__ = ["shard_ranges", "edge_balanced_ranges", "rank_slice", "metapath_fanout", "best_metapaths",
+           "sharded_stack_forward"]
 
 
 def edge_balanced_ranges(gathered: np.ndarray | torch.Tensor, num_nodes: int, world: int) -> list[tuple[int, int]]:
@@ -89,3 +90,47 @@ def best_metapaths(scores: dict, k: int = 3) -> dict:
     """main.py:1451-1452: the ``k`` best candidates by score, descending (stable for ties)."""
     ordered = dict(sorted(scores.items(), key=lambda item: item[1], reverse=True))
     return dict(list(ordered.items())[:k])
+
+
+# ---------------------------------------------------------------------------------------
+# inference stack with reduce-scatter between layers
+# ---------------------------------------------------------------------------------------
+def _padded_index(ranges: list[tuple[int, int]], device) -> tuple[torch.Tensor, int]:
+    """Row i of range k goes to padded slot k·m + (i - lo_k), m = the largest range."""
+    m = max(hi - lo for lo, hi in ranges)
+    idx = torch.cat([torch.arange(lo, hi, dtype=torch.int64) - lo + k * m for k, (lo, hi) in enumerate(ranges)])
+    return idx.to(device), m
+
+
+def sharded_stack_forward(convs, x: torch.Tensor, edge_index: torch.Tensor, edge_type: torch.Tensor,
+                          ranges: list[tuple[int, int]], group=None, activation: str | None = "relu") -> torch.Tensor:
+    """Forward of a relational layer stack (``relu(conv(h))`` per layer, model.py:141-146) over
+    dst-range shards with ONE reduction per layer that moves half the bytes of an all-reduce.
+
+    Rank k owns the gathered-node range ranges[k]: its layer output is a partial sum for every
+    row, but the next layer only gathers rows of its own range (its edges' node_2, its root
+    rows), so a reduce-scatter of the partials (RCCL over xGMI with the "nccl" backend) gives
+    each rank exactly the summed rows it needs; rows outside the range are never read. One
+    all-gather after the last layer assembles the full output. Inference path (no autograd
+    across ranks): the training path is the per-layer all-reduce of ``RGCNConv(shard=, group=)``."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi = ranges[rank]
+    idx, m = _padded_index(ranges, x.device)
+    n = x.shape[0]
+    h = x
+    for conv in convs:
+        part = conv(h, edge_index, edge_type, shard=(lo, hi), group=None)  # partial sums, all rows
+        f = part.shape[1]
+        pad = part.new_empty(world * m, f)
+        pad.index_copy_(0, idx, part)
+        mine = part.new_empty(m, f)
+        dist.reduce_scatter_tensor(mine, pad, group=group)
+        h = part.new_empty(n, f)  # only [lo, hi) is written: the only rows the next layer reads
+        h[lo:hi] = torch.relu(mine[:hi - lo]) if activation == "relu" else mine[:hi - lo]
+    slab = h.new_zeros(m, h.shape[1])
+    slab[:hi - lo] = h[lo:hi]
+    full = h.new_empty(world * m, h.shape[1])
+    dist.all_gather_into_tensor(full, slab, group=group)
+    return full.index_select(0, idx)

@@ -157,3 +157,64 @@ def test_metapath_fanout_world2_gloo():
     from mpgnn_amd.distributed import best_metapaths
     best = best_metapaths(expected)
     assert list(best.values()) == sorted(expected.values(), reverse=True)[:3]
+
+
+# ------------------------------------------------------------------------------------------
+# inference stack with reduce-scatter between layers (distributed.sharded_stack_forward)
+# ------------------------------------------------------------------------------------------
+def _stack_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.set_num_threads(1)
+        import mpgnn_amd
+        from mpgnn_amd import data
+        from oracle import rgcn_oracle as orc
+        from oracle.shard_oracle import shard_partial_forward
+        g = data.synthetic_graph(500, 4, 8, feat_dim=16, seed=9)
+        N, R = g.num_nodes, g.num_relations
+        gen = torch.Generator().manual_seed(3)
+        layers = [((torch.rand(R, 16, 16, generator=gen) - 0.5), torch.rand(16, 16, generator=gen) - 0.5,
+                   torch.rand(16, generator=gen) - 0.5) for _ in range(3)]
+        ranges = mpgnn_amd.distributed.shard_ranges(g.edge_index, N, world)
+
+        def make_conv(W, root, bias):
+            def conv(h, ei, et, shard=None, group=None):
+                assert group is None and shard == ranges[rank]
+                lo, hi = shard
+                hx = torch.zeros_like(h)
+                hx[lo:hi] = h[lo:hi]  # the kernels read only the rank's own rows
+                plan = mpgnn_amd.GraphPlan(ei, et, N, shard=shard)
+                tables = {k: plan.table(k) for k in ("e_col", "s_ptr", "s_row", "s_rel", "s_cnt")}
+                return shard_partial_forward(tables, hx, W, root, bias, shard)
+            return conv
+
+        convs = [make_conv(*p) for p in layers]
+        out = mpgnn_amd.distributed.sharded_stack_forward(convs, g.x, g.edge_index, g.edge_type, ranges)
+        ref = g.x
+        for W, root, bias in layers:
+            ref = torch.relu(orc.rgcn_forward(ref, g.edge_index, g.edge_type, W, root, bias))
+        err = float((out - ref).abs().max())
+        q.put((rank, err, float(ref.abs().max())))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_stack_reduce_scatter_matches_unsharded(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stack_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, err, scale in res:
+        assert err is not None, scale
+        assert err <= 1e-4 * scale + 1e-6, (rank, err, scale)

@@ -833,3 +833,22 @@ def test_segment_means_backward_vs_oracle(name, mode, rel):
         rel_close(xg.grad, xs.grad, what="dx")
     else:
         assert torch.count_nonzero(xg.grad) == 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_shard_forward_reads_only_own_rows(world):
+    """distributed.sharded_stack_forward leaves every row outside a rank's node_2 range
+    unwritten between layers: a shard's partial forward must not read them. Poisoning those
+    rows with NaN changes no bit of the partial output."""
+    from mpgnn_amd.distributed import shard_ranges
+    g = data.config_graph("fb15k237")
+    torch.manual_seed(30)
+    conv = mpgnn_amd.RGCNConv(128, 128, g.num_relations, flow="target_to_source").to(DEV)
+    x, ei, et = g.x.to(DEV), g.edge_index.to(DEV), g.edge_type.to(DEV)
+    for lo, hi in shard_ranges(g.edge_index, g.num_nodes, world):
+        with torch.no_grad():
+            clean = conv(x, ei, et, shard=(lo, hi))
+            xp = torch.full_like(x, float("nan"))
+            xp[lo:hi] = x[lo:hi]
+            poisoned = conv(xp, ei, et, shard=(lo, hi))
+        assert torch.equal(clean, poisoned), (lo, hi)
