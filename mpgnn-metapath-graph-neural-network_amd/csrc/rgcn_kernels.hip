@@ -1375,6 +1375,97 @@ struct RelGemm {
         }
     }
 
+    // Ping-pong schedule (MPGNN_OPT_REL_PINGPONG): one 512-thread workgroup per CU holding two
+    // wave groups (waves 0-3, 4-7), each with its own A double buffer, taking alternate items of
+    // the workgroup's range. The loop runs in phases separated by one barrier; in each phase one
+    // group runs its item's MFMA chain while the other stores its previous item's outputs,
+    // commits its next tile and swaps weight slices — so each SIMD's two waves alternate between
+    // the matrix pipe and the memory pipe instead of entering both in lockstep.
+    __device__ static void run_pingpong(const RelGemmArgs& a, float* smem) {
+        const int tid = threadIdx.x;  // 512 threads
+        const int grp = tid >> 8;
+        const int gtid = tid & 255;
+        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
+        const int wave = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+        float* As = smem + grp * (2 * 32 * lda + 64);  // this group's [2][32][lda] A tiles
+        float* Sc = As + 2 * 32 * lda;                 // and its [2][32] dgrad row scales
+        const int n_items = a.n_rel + a.n_root;
+        const int G = (int)gridDim.x;
+        const int g8 = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
+        const int rng = g8 * q + min(g8, rem) + ((int)blockIdx.x >> 3);
+        const int i_beg = (int)((long long)rng * n_items / G);
+        const int i_end = (int)((long long)(rng + 1) * n_items / G);
+        const int n_wg = i_end - i_beg;  // uniform across the workgroup (also when 0)
+        const int n_g = n_wg > grp ? (n_wg - grp + 1) / 2 : 0;  // items of this group: i_beg + grp + 2k
+        const int n_max = (n_wg + 1) / 2;
+        float4 v[WPT];
+        int cnt = 1;
+        Item cur{}, nxt{};
+        float b[KH], bn[KH];
+        if (n_g > 0) {
+            cur = item(a, i_beg + grp);
+            issue(a, cur, gtid, v, cnt);
+            load_b(cur.w, wave, lane, b);
+            commit(cur, gtid, v, cnt, As, Sc);
+#pragma unroll
+            for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(b[j]));
+        }
+        __syncthreads();
+        int buf = 0;
+        bool has_next = false, new_w = false;
+        f32x16 acc;
+        // group g runs the MFMAs of its k-th item in phase 2k + g and its epilogue in 2k + g + 1
+        for (int ph = 0; ph <= 2 * n_max; ++ph) {
+            const int k2 = ph - grp;
+            if (k2 >= 0 && (k2 >> 1) < n_g) {
+                const int k = k2 >> 1;
+                if ((k2 & 1) == 0) {
+                    has_next = k + 1 < n_g;
+                    nxt = has_next ? item(a, i_beg + grp + 2 * (k + 1)) : cur;
+                    if (has_next) issue(a, nxt, gtid, v, cnt);
+                    new_w = nxt.w != cur.w;
+                    if (new_w) load_b(nxt.w, wave, lane, bn);
+                    const float* Ab = As + buf * 32 * lda + c * lda + h * KH;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+                    float4 af = *reinterpret_cast<const float4*>(Ab);
+#pragma unroll
+                    for (int j = 0; j < KH; j += 4) {
+                        const float4 cf = af;
+                        if (j + 4 < KH) af = *reinterpret_cast<const float4*>(Ab + j + 4);
+                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], acc, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], acc, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], acc, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], acc, 0, 0, 0);
+                    }
+                } else {
+                    float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N
+                                         : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
+                    const float* sc = Sc + buf * 32;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (row < cur.nrows) {
+                            float o = acc[r];
+                            if constexpr (DGRAD) {
+                                if (!cur.root) o = o / sc[row];
+                            }
+                            Yt[(size_t)row * N + wave * 32 + c] = o;
+                        }
+                    }
+                    if (has_next) commit(nxt, gtid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
+                    if (new_w) {
+#pragma unroll
+                        for (int j = 0; j < KH; ++j) b[j] = bn[j];
+                    }
+                    cur = nxt;
+                    buf ^= 1;
+                }
+            }
+            __syncthreads();
+        }
+    }
+
     // LDS-free variant (MPGNN_OPT_REL_DIRECT): every wave loads its own A fragments straight
     // into registers — lane (r = lane & 31, h = lane >> 5) holds row r, k ∈ [h·KH, (h+1)·KH),
     // KH/4 float4 loads — so the four waves of a workgroup never synchronise (no barrier, no
@@ -1574,6 +1665,12 @@ __global__ __launch_bounds__(kThreads, 2) void rel_gemm_kernel(RelGemmArgs a) {
 template <int KB, bool DGRAD>
 __global__ __launch_bounds__(kThreads, 2) void rel_gemm_direct_kernel(RelGemmArgs a) {
     RelGemm<KB, DGRAD>::run_direct(a);
+}
+
+template <int KB, bool DGRAD>
+__global__ __launch_bounds__(2 * kThreads, 1) void rel_gemm_pingpong_kernel(RelGemmArgs a) {
+    extern __shared__ float smem[];
+    RelGemm<KB, DGRAD>::run_pingpong(a, smem);
 }
 
 
@@ -3176,6 +3273,7 @@ static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
 
 
 static bool g_y_rowmajor = false;  // MPGNN_OPT_Y_ROWMAJOR: forward transform output in combine order (opt-in)
+static bool g_rel_pingpong = false;  // MPGNN_OPT_REL_PINGPONG: two wave groups alternating MFMA / memory phases
 static bool g_rel_direct = false; // MPGNN_OPT_REL_DIRECT: LDS-free rel_gemm (waves load their own A fragments)
 static bool g_rel_deep = false;   // MPGNN_OPT_REL_DEEP: rel_gemm A rows two items ahead
 static bool g_merge_grad = true;  // MPGNN_OPT_MERGE_GRAD: dW + droot/dbias in one outer launch, one reduce launch
@@ -3213,6 +3311,11 @@ static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
     const int grid = std::min(n_items, cu_count() * g_rel_wg_per_cu);
     if (a.deep == 2) {
         hipLaunchKernelGGL((rel_gemm_direct_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), 0, st, a);
+        return;
+    }
+    if (a.deep == 3) {
+        hipLaunchKernelGGL((rel_gemm_pingpong_kernel<KB, DGRAD>), dim3(std::min(n_items, cu_count())),
+                           dim3(2 * kThreads), 2 * lds, st, a);
         return;
     }
     hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
@@ -3457,7 +3560,7 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         r.stamps = (kind == MPGNN_K_SEG_FWD) ? g_stamps : nullptr;
         r.stagger = g_rel_stagger;
         r.queue = (g_rel_queue && !g_stamps) ? rel_queue(strm) : nullptr;
-        r.deep = g_stamps ? 0 : (g_rel_direct ? 2 : (g_rel_deep ? 1 : 0));
+        r.deep = g_stamps ? 0 : (g_rel_pingpong ? 3 : (g_rel_direct ? 2 : (g_rel_deep ? 1 : 0)));
         r.y_pos = y_pos;
         r.yroot_pos = yroot_pos;
         if (y_pos != nullptr && (r.deep != 0 || r.queue != nullptr))
@@ -3896,6 +3999,10 @@ using namespace mpgnn;
 extern "C" {
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_REL_PINGPONG) {
+        g_rel_pingpong = value != 0;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_Y_ROWMAJOR) {
         g_y_rowmajor = value != 0;
         return MPGNN_OK;
@@ -4072,7 +4179,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     // instead of gathering it. Needs the B-stationary GEMM's default schedule and the full list.
     const bool rowmap = g_y_rowmajor && mode == MPGNN_MODE_ALL && !exact && root != nullptr && own_range &&
                         s.all_segments && g_rel_gemm && (F_in == 64 || F_in == 128) && F_out == 128 &&
-                        g_ablate == 0 && g_stamps == nullptr && !g_rel_deep && !g_rel_direct && !g_rel_queue &&
+                        g_ablate == 0 && g_stamps == nullptr && !g_rel_deep && !g_rel_direct && !g_rel_queue && !g_rel_pingpong &&
                         !g_fused && g_overlap == 0;
 
     if (!exact && g_fused && F_in == 128 && F_out == 128 && g_ablate == 0) {

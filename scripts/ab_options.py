@@ -60,4 +60,4 @@ for spec in sys.argv[1:] or ["7=16"]:
     print(json.dumps({"opts": spec, "ms_per_step": round(ms, 4), "max_abs_diff_vs_first": err, "us_per_launch": kern}),
           flush=True)
     for k, v in opts:  # back to defaults
-        _lib.lib.mpgnn_set_option(k, {7: 16, 5: 1, 6: 0, 4: 0, 0: 0, 8: 0, 9: 2, 10: 0, 12: 0, 14: 0, 15: 0, 16: 1, 17: 0}.get(k, 0))
+        _lib.lib.mpgnn_set_option(k, {7: 16, 5: 1, 6: 0, 4: 0, 0: 0, 8: 0, 9: 2, 10: 0, 12: 0, 14: 0, 15: 0, 16: 1, 17: 0, 18: 0}.get(k, 0))
