@@ -9,10 +9,12 @@ One timed STEP = one forward pass of the 3 relational layers over the whole grap
 resident in HBM.  value = edges aggregated per second = 3 · E · steps / time (an edge
 aggregated = one (node_1, rel, node_2) edge folded into its (node_1, rel) segment in one
 layer).  With --gpus N (torchrun, one process per GPU) the graph is sharded by
-node_2 range (edge-balanced) and each layer's partial outputs are summed by RCCL over xGMI —
-a reduce-scatter per layer (the next layer only gathers the rank's own node_2 rows), one
-all-gather after the last (distributed.sharded_stack_forward); the training epoch keeps the
-per-layer all-reduce of RGCNConv(shard=, group=). Total work is fixed: "scaling" is "strong".
+aggregating-node (node_1) range, edge-balanced: each rank computes complete output rows for its
+range and one RCCL all-gather over xGMI per layer assembles the next layer's input
+(distributed.sharded_stack_forward, shard_side="rows"; measured per-rank compute at 8 shards
+1.91x below one GPU vs 1.51x for node_2 shards, scripts/shard_compute.py); the training epoch
+runs RGCNConv(shard=, group=, shard_side="rows") with the per-layer all-reduce of the disjoint
+rows and the gradient all-reduces. Total work is fixed: "scaling" is "strong".
 
 Also reported (separate loops, outside the timed step): the training epoch of
 main_rgcn.py:458-461 — train step (forward + NLL + backward + Adam) + validation forward.
@@ -184,14 +186,14 @@ def main():
     x, ei, et = g.x.to(dev), g.edge_index.to(dev), g.edge_type.to(dev)
     shard = None
     ranges = None
-    if world > 1:
-        ranges = shard_ranges(g.edge_index, g.num_nodes, world)
+    if world > 1:  # shard by the aggregating node: complete rows per rank (scripts/shard_compute.py)
+        ranges = shard_ranges(g.edge_index, g.num_nodes, world, side="rows")
         shard = ranges[rank]
     convs = [net.conv1] + [net.conv2] * (args.layers - 1)
 
     def step():
-        if world > 1:  # partial sums reduce-scattered per layer, one all-gather at the end
-            return sharded_stack_forward(convs, x, ei, et, ranges, group)
+        if world > 1:  # each rank's complete rows all-gathered per layer
+            return sharded_stack_forward(convs, x, ei, et, ranges, group, shard_side="rows")
         h = x
         for conv in convs:
             h = conv(h, ei, et, activation="relu")  # F.relu(conv(...)), model.py:144,146
@@ -202,7 +204,7 @@ def main():
         for _ in range(max(args.warmup, 1)):
             step()
     torch.cuda.synchronize()
-    plan = mpgnn_amd.get_plan(ei, et, g.num_nodes, shard=shard, device=dev)
+    plan = mpgnn_amd.get_plan(ei, et, g.num_nodes, shard=shard, device=dev, shard_side="rows")
 
     # ---- timed region: K forward steps --------------------------------------------------
     if group is not None:
@@ -306,13 +308,13 @@ def main():
     def epoch():
         net.train()
         opt.zero_grad()
-        out = net(x, ei, et, shard=shard, group=group)
+        out = net(x, ei, et, shard=shard, group=group, shard_side="rows")
         loss = torch.nn.functional.nll_loss(out[train_idx], y[train_idx])
         loss.backward()
         opt.step()
         net.eval()
         with torch.no_grad():
-            net(x, ei, et, shard=shard, group=group)
+            net(x, ei, et, shard=shard, group=group, shard_side="rows")
 
     epoch_ms = None
     if args.epoch_steps > 0:
@@ -431,8 +433,9 @@ def main():
                        "graph": {"nodes": g.num_nodes, "relations": g.num_relations, "edges": g.num_edges,
                                  "segments": S if world == 1 else None},
                        "parallelism": "single GPU" if world == 1 else
-                       f"dst-range shards x{world}: per layer an RCCL reduce-scatter of the partial sums "
-                       "(each rank keeps the rows it gathers next), one all-gather after the last layer"},
+                       f"row-range shards x{world} (aggregating node, edge-balanced): each rank computes its "
+                       "complete output rows, one RCCL all-gather per layer (epoch: per-layer all-reduce of the "
+                       "disjoint rows, gradient all-reduces)"},
             "graph_replay": graph,
             "epoch_ms": round(epoch_ms, 3) if epoch_ms is not None else None,
             "epoch_graph": epoch_graph,

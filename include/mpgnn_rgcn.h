@@ -108,6 +108,17 @@ typedef struct mpgnn_plan_info {
 int32_t mpgnn_plan_create(const int64_t* edge_index, const int64_t* edge_type,
                           int64_t num_edges, int64_t num_nodes,
                           int64_t shard_lo, int64_t shard_hi, mpgnn_plan** out);
+/* Shard by either side of the edges: MPGNN_SHARD_GATHERED keeps the edges whose
+ * node_2 (the gathered row) is in [shard_lo, shard_hi) — every output row gets a partial sum
+ * (global per-(node_1, relation) counts), summed across ranks by an all-reduce /
+ * reduce-scatter; MPGNN_SHARD_ROWS keeps the edges whose node_1 (the aggregating row) is in
+ * the range — the rank computes complete output rows for its range only (zeros elsewhere),
+ * assembled across ranks by an all-gather (or an all-reduce of the disjoint rows).
+ * In both, x @ root + bias is added for the rows in [shard_lo, shard_hi) only. */
+enum mpgnn_shard_side { MPGNN_SHARD_GATHERED = 0, MPGNN_SHARD_ROWS = 1 };
+int32_t mpgnn_plan_create_sharded(const int64_t* edge_index, const int64_t* edge_type, int64_t num_edges,
+                                  int64_t num_nodes, int64_t shard_lo, int64_t shard_hi, int32_t side,
+                                  mpgnn_plan** out);
 int32_t mpgnn_plan_destroy(mpgnn_plan* plan);
 int32_t mpgnn_plan_get_info(const mpgnn_plan* plan, mpgnn_plan_info* info);
 /* Element count of an exported table, and a copy of it into host memory. */

@@ -23,6 +23,8 @@ MPGNN_ERR_UNSUPPORTED = -6
 MODE_SINGLE = 0
 MODE_ALL = 1
 
+SHARD_SIDES = {"gathered": 0, "rows": 1}  # mpgnn_shard_side
+
 TABLES = {
     "rel_values": (0, "int64"), "rel_seg_ptr": (1, "int32"), "rel_edge_ptr": (2, "int32"),
     "e_col": (3, "int32"), "e_id": (4, "int32"), "s_ptr": (5, "int32"), "s_row": (6, "int32"),
@@ -52,6 +54,7 @@ _I32, _I64 = ctypes.c_int32, ctypes.c_int64
 _PI64 = ctypes.POINTER(ctypes.c_int64)
 SIGNATURES = [
     ("mpgnn_plan_create", _I32, [_P, _P, _I64, _I64, _I64, _I64, ctypes.POINTER(_P)]),
+    ("mpgnn_plan_create_sharded", _I32, [_P, _P, _I64, _I64, _I64, _I64, _I32, ctypes.POINTER(_P)]),
     ("mpgnn_plan_destroy", _I32, [_P]),
     ("mpgnn_plan_get_info", _I32, [_P, ctypes.POINTER(PlanInfo)]),
     ("mpgnn_plan_table_size", _I32, [_P, _I32, _PI64, ctypes.POINTER(_I32)]),

@@ -313,7 +313,7 @@ struct PhaseTimer {
 };
 
 static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N, int64_t lo,
-                     int64_t hi, mpgnn_plan* p) {
+                     int64_t hi, int32_t side, mpgnn_plan* p) {
     PhaseTimer tm;
     const int64_t* n1 = ei;
     const int64_t* n2 = ei + E;
@@ -390,8 +390,9 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
     parallel_for(G, [&](int64_t g) {
         int32_t c = 0;
         for (int32_t a = gstart[g]; a < gstart[g + 1]; ++a) {
-            const int64_t c2 = n2[by_rel_row[a]];
-            c += (c2 >= lo && c2 < hi) ? 1 : 0;
+            const int32_t e = by_rel_row[a];
+            const int64_t k = side == MPGNN_SHARD_ROWS ? n1[e] : n2[e];
+            c += (k >= lo && k < hi) ? 1 : 0;
         }
         edge_off[g] = c;
         seg_id[g] = c > 0 ? 1 : 0;
@@ -414,7 +415,8 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
         int32_t w = edge_off[g];
         for (int32_t a = a0; a < a1; ++a) {
             const int32_t e = by_rel_row[a];
-            if (n2[e] >= lo && n2[e] < hi) {
+            const int64_t k = side == MPGNN_SHARD_ROWS ? n1[e] : n2[e];
+            if (k >= lo && k < hi) {
                 p->e_col[w] = (int32_t)n2[e];
                 p->e_id[w] = e;
                 seg_of_edge[w] = sid;
@@ -624,7 +626,15 @@ const char* mpgnn_status_string(int32_t s) {
 
 int32_t mpgnn_plan_create(const int64_t* edge_index, const int64_t* edge_type, int64_t num_edges,
                           int64_t num_nodes, int64_t shard_lo, int64_t shard_hi, mpgnn_plan** out) {
+    return mpgnn_plan_create_sharded(edge_index, edge_type, num_edges, num_nodes, shard_lo, shard_hi,
+                                     MPGNN_SHARD_GATHERED, out);
+}
+
+int32_t mpgnn_plan_create_sharded(const int64_t* edge_index, const int64_t* edge_type, int64_t num_edges,
+                                  int64_t num_nodes, int64_t shard_lo, int64_t shard_hi, int32_t side,
+                                  mpgnn_plan** out) {
     if (!out) return fail(MPGNN_ERR_ARG, "out is NULL");
+    if (side != MPGNN_SHARD_GATHERED && side != MPGNN_SHARD_ROWS) return fail(MPGNN_ERR_ARG, "unknown shard side");
     *out = nullptr;
     if (num_edges < 0 || num_nodes < 0) return fail(MPGNN_ERR_ARG, "negative size");
     if (num_edges > 0 && (!edge_index || !edge_type)) return fail(MPGNN_ERR_ARG, "edge arrays are NULL");
@@ -637,7 +647,7 @@ int32_t mpgnn_plan_create(const int64_t* edge_index, const int64_t* edge_type, i
     mpgnn_plan* p = new (std::nothrow) mpgnn_plan();
     if (!p) return fail(MPGNN_ERR_ALLOC, "plan allocation failed");
     try {
-        int32_t st = build(edge_index, edge_type, num_edges, num_nodes, shard_lo, shard_hi, p);
+        int32_t st = build(edge_index, edge_type, num_edges, num_nodes, shard_lo, shard_hi, side, p);
         if (st != MPGNN_OK) {
             delete p;
             return st;

@@ -37,10 +37,12 @@ def edge_balanced_ranges(gathered: np.ndarray | torch.Tensor, num_nodes: int, wo
 
 
 def shard_ranges(edge_index: torch.Tensor, num_nodes: int, world: int,
-                 flow: str = "target_to_source") -> list[tuple[int, int]]:
-    """Per-rank gathered-node ranges for ``edge_index`` (row 1 under target_to_source)."""
+                 flow: str = "target_to_source", side: str = "gathered") -> list[tuple[int, int]]:
+    """Per-rank node ranges balanced by edge count: of the gathered node (row 1 under
+    target_to_source) for ``side="gathered"``, of the aggregating node for ``side="rows"``."""
     gathered = edge_index[1] if flow == "target_to_source" else edge_index[0]
-    return edge_balanced_ranges(gathered, num_nodes, world)
+    aggregating = edge_index[0] if flow == "target_to_source" else edge_index[1]
+    return edge_balanced_ranges(aggregating if side == "rows" else gathered, num_nodes, world)
 
 
 # ---------------------------------------------------------------------------------------
@@ -103,7 +105,8 @@ def _padded_index(ranges: list[tuple[int, int]], device) -> tuple[torch.Tensor, 
 
 
 def sharded_stack_forward(convs, x: torch.Tensor, edge_index: torch.Tensor, edge_type: torch.Tensor,
-                          ranges: list[tuple[int, int]], group=None, activation: str | None = "relu") -> torch.Tensor:
+                          ranges: list[tuple[int, int]], group=None, activation: str | None = "relu",
+                          shard_side: str = "gathered") -> torch.Tensor:
     """Forward of a relational layer stack (``relu(conv(h))`` per layer, model.py:141-146) over
     dst-range shards with ONE reduction per layer that moves half the bytes of an all-reduce.
 
@@ -112,7 +115,13 @@ def sharded_stack_forward(convs, x: torch.Tensor, edge_index: torch.Tensor, edge
     rows), so a reduce-scatter of the partials (RCCL over xGMI with the "nccl" backend) gives
     each rank exactly the summed rows it needs; rows outside the range are never read. One
     all-gather after the last layer assembles the full output. Inference path (no autograd
-    across ranks): the training path is the per-layer all-reduce of ``RGCNConv(shard=, group=)``."""
+    across ranks): the training path is the per-layer all-reduce of ``RGCNConv(shard=, group=)``.
+
+    ``shard_side="rows"``: rank k owns the edges whose AGGREGATING node lies in ranges[k]
+    (ranges then balanced by node_1 edge counts, ``shard_ranges(..., side="rows")``); its layer
+    output is complete for its rows and zero elsewhere, every rank gathers from all rows, so each
+    layer ends with an all-gather of the rows (same bytes as the reduce-scatter) and every
+    per-rank pass — means, transform, combine — shrinks with the shard instead of only the edges."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -120,6 +129,15 @@ def sharded_stack_forward(convs, x: torch.Tensor, edge_index: torch.Tensor, edge
     idx, m = _padded_index(ranges, x.device)
     n = x.shape[0]
     h = x
+    if shard_side == "rows":
+        for conv in convs:
+            part = conv(h, edge_index, edge_type, shard=(lo, hi), group=None, shard_side="rows")
+            slab = part.new_zeros(m, part.shape[1])
+            slab[:hi - lo] = torch.relu(part[lo:hi]) if activation == "relu" else part[lo:hi]
+            full = part.new_empty(world * m, part.shape[1])
+            dist.all_gather_into_tensor(full, slab, group=group)
+            h = full.index_select(0, idx)
+        return h
     for conv in convs:
         part = conv(h, edge_index, edge_type, shard=(lo, hi), group=None)  # partial sums, all rows
         f = part.shape[1]

@@ -75,11 +75,11 @@ class Net(torch.nn.Module):
         self.conv2 = RGCNConv(hidden_dim, output_dim, num_rel, flow="target_to_source")
         self.LinearLayer = torch.nn.Linear(output_dim, ll_output_dim)
 
-    def forward(self, x, edge_index, edge_type, *, shard=None, group=None):
+    def forward(self, x, edge_index, edge_type, *, shard=None, group=None, shard_side="gathered"):
         for layer_index in range(0, self.metapath_length):
             conv = self.conv1 if layer_index == 0 else self.conv2
             # F.relu(conv(...)) of model.py:144,146, fused into the layer's combine kernel
-            x = conv(x, edge_index, edge_type, shard=shard, group=group, activation="relu")
+            x = conv(x, edge_index, edge_type, shard=shard, group=group, activation="relu", shard_side=shard_side)
         x = linear(self.LinearLayer, x)
         return F.log_softmax(x, dim=1)
 

@@ -71,9 +71,11 @@ class RGCNConv(torch.nn.Module):
         glorot(self.root)
         zeros(self.bias)
 
-    def forward(self, x, edge_index, edge_type=None, *, shard=None, group=None, activation=None):
+    def forward(self, x, edge_index, edge_type=None, *, shard=None, group=None, activation=None,
+                shard_side="gathered"):
         """``shard=(lo, hi)`` + ``group``: this rank owns the edges whose gathered node lies in
-        [lo, hi) (dst-range sharding); partial outputs are all-reduced.
+        [lo, hi) (dst-range sharding; ``shard_side="rows"``: whose aggregating
+        node lies in it, the rank's output rows then being complete); outputs are all-reduced.
         ``activation='relu'`` returns ``F.relu(conv(...))`` (model.py:144,146) with the ReLU
         fused into the layer's last kernel when unsharded."""
         if isinstance(x, tuple):
@@ -87,7 +89,8 @@ class RGCNConv(torch.nn.Module):
             raise NotImplementedError(f"aggr='{self.aggr}' (the reference path uses 'mean')")
         if self.num_bases is not None or self.num_blocks is not None:
             raise NotImplementedError("basis / block-diagonal decomposition is not on the RGCN path")
-        plan = get_plan(edge_index, edge_type, x.size(0), flow=self.flow, shard=shard, device=x.device)
+        plan = get_plan(edge_index, edge_type, x.size(0), flow=self.flow, shard=shard, device=x.device,
+                        shard_side=shard_side)
         row_range = shard if shard is not None else None
         return rgcn_conv(x, self.weight, self.root, self.bias, plan, MODE_ALL,
                          num_relations=self.num_relations, row_range=row_range, group=group,

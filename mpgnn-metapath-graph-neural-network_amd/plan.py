@@ -25,7 +25,8 @@ class GraphPlan:
     """Host + device segment tables for one graph (optionally one dst-range shard)."""
 
     def __init__(self, edge_index: torch.Tensor, edge_type: torch.Tensor, num_nodes: int,
-                 shard: tuple[int, int] | None = None, flow: str = "target_to_source"):
+                 shard: tuple[int, int] | None = None, flow: str = "target_to_source",
+                 shard_side: str = "gathered"):
         if flow not in FLOWS:
             raise ValueError(f"Expected 'flow' to be either {FLOWS} (got '{flow}')")
         if edge_index.dim() != 2 or edge_index.size(0) != 2:
@@ -41,11 +42,15 @@ class GraphPlan:
         self.flow = flow
         lo, hi = shard if shard is not None else (0, self.num_nodes)
         self.shard = (int(lo), int(hi))
+        if shard_side not in _lib.SHARD_SIDES:
+            raise ValueError(f"shard_side must be one of {tuple(_lib.SHARD_SIDES)}")
+        self.shard_side = shard_side
         handle = ctypes.c_void_p()
-        check(lib.mpgnn_plan_create(ei.data_ptr() if ei.numel() else None,
-                                    et.data_ptr() if et.numel() else None,
-                                    et.numel(), self.num_nodes, self.shard[0], self.shard[1],
-                                    ctypes.byref(handle)), "mpgnn_plan_create")
+        check(lib.mpgnn_plan_create_sharded(ei.data_ptr() if ei.numel() else None,
+                                            et.data_ptr() if et.numel() else None,
+                                            et.numel(), self.num_nodes, self.shard[0], self.shard[1],
+                                            _lib.SHARD_SIDES[shard_side], ctypes.byref(handle)),
+              "mpgnn_plan_create")
         self._h = handle
         self._device = None
         self._lock = threading.Lock()
@@ -136,10 +141,10 @@ class _PlanCache:
         self._lock = threading.Lock()
 
     def get(self, edge_index, edge_type, num_nodes, flow="target_to_source", shard=None,
-            device=None) -> GraphPlan:
+            device=None, shard_side="gathered") -> GraphPlan:
         key = (id(edge_index), edge_index._version, tuple(edge_index.shape), edge_index.data_ptr(),
                id(edge_type), edge_type._version, edge_type.data_ptr(), int(num_nodes), flow,
-               tuple(shard) if shard is not None else None)
+               tuple(shard) if shard is not None else None, shard_side if shard is not None else None)
         with self._lock:
             hit = self._d.get(key)
             if hit is not None:
@@ -148,7 +153,7 @@ class _PlanCache:
                     self._d.move_to_end(key)
                     return plan.to_device(device) if device is not None else plan
                 del self._d[key]
-        plan = GraphPlan(edge_index, edge_type, num_nodes, shard=shard, flow=flow)
+        plan = GraphPlan(edge_index, edge_type, num_nodes, shard=shard, flow=flow, shard_side=shard_side)
         if device is not None:
             plan.to_device(device)
         with self._lock:
@@ -165,5 +170,7 @@ class _PlanCache:
 plan_cache = _PlanCache()
 
 
-def get_plan(edge_index, edge_type, num_nodes, flow="target_to_source", shard=None, device=None):
-    return plan_cache.get(edge_index, edge_type, num_nodes, flow=flow, shard=shard, device=device)
+def get_plan(edge_index, edge_type, num_nodes, flow="target_to_source", shard=None, device=None,
+             shard_side="gathered"):
+    return plan_cache.get(edge_index, edge_type, num_nodes, flow=flow, shard=shard, device=device,
+                          shard_side=shard_side)

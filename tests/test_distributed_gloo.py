@@ -162,7 +162,7 @@ def test_metapath_fanout_world2_gloo():
 # ------------------------------------------------------------------------------------------
 # inference stack with reduce-scatter between layers (distributed.sharded_stack_forward)
 # ------------------------------------------------------------------------------------------
-def _stack_worker(rank, world, port, q):
+def _stack_worker(rank, world, port, q, side="gathered"):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     try:
@@ -179,21 +179,24 @@ def _stack_worker(rank, world, port, q):
         gen = torch.Generator().manual_seed(3)
         layers = [((torch.rand(R, 16, 16, generator=gen) - 0.5), torch.rand(16, 16, generator=gen) - 0.5,
                    torch.rand(16, generator=gen) - 0.5) for _ in range(3)]
-        ranges = mpgnn_amd.distributed.shard_ranges(g.edge_index, N, world)
+        ranges = mpgnn_amd.distributed.shard_ranges(g.edge_index, N, world, side=side)
 
         def make_conv(W, root, bias):
-            def conv(h, ei, et, shard=None, group=None):
-                assert group is None and shard == ranges[rank]
+            def conv(h, ei, et, shard=None, group=None, shard_side="gathered"):
+                assert group is None and shard == ranges[rank] and shard_side == side
                 lo, hi = shard
-                hx = torch.zeros_like(h)
-                hx[lo:hi] = h[lo:hi]  # the kernels read only the rank's own rows
-                plan = mpgnn_amd.GraphPlan(ei, et, N, shard=shard)
+                hx = h
+                if side == "gathered":
+                    hx = torch.zeros_like(h)
+                    hx[lo:hi] = h[lo:hi]  # the kernels read only the rank's own rows
+                plan = mpgnn_amd.GraphPlan(ei, et, N, shard=shard, shard_side=side)
                 tables = {k: plan.table(k) for k in ("e_col", "s_ptr", "s_row", "s_rel", "s_cnt")}
                 return shard_partial_forward(tables, hx, W, root, bias, shard)
             return conv
 
         convs = [make_conv(*p) for p in layers]
-        out = mpgnn_amd.distributed.sharded_stack_forward(convs, g.x, g.edge_index, g.edge_type, ranges)
+        out = mpgnn_amd.distributed.sharded_stack_forward(convs, g.x, g.edge_index, g.edge_type, ranges,
+                                                          shard_side=side)
         ref = g.x
         for W, root, bias in layers:
             ref = torch.relu(orc.rgcn_forward(ref, g.edge_index, g.edge_type, W, root, bias))
@@ -204,12 +207,14 @@ def _stack_worker(rank, world, port, q):
         q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_stack_reduce_scatter_matches_unsharded(world):
+@pytest.mark.parametrize("world,side", [(2, "gathered"), (3, "gathered"), (2, "rows"), (3, "rows")])
+def test_sharded_stack_reduce_scatter_matches_unsharded(world, side):
+    """side "gathered": reduce-scatter of partial sums per layer; side "rows": complete rows
+    per rank (plan sharded by the aggregating node), all-gather per layer."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_stack_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_stack_worker, args=(r, world, port, q, side)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in procs]

@@ -852,3 +852,36 @@ def test_shard_forward_reads_only_own_rows(world):
             xp[lo:hi] = x[lo:hi]
             poisoned = conv(xp, ei, et, shard=(lo, hi))
         assert torch.equal(clean, poisoned), (lo, hi)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_row_shards_complete_rows_and_sum_to_unsharded(world):
+    """shard_side="rows" (plan sharded by the aggregating node): each rank's output rows in its
+    range equal the unsharded layer's, rows outside it are exactly zero, so the sum over ranks
+    (the all-reduce of the training path) is the unsharded output; gradients summed over ranks
+    match the unsharded gradients."""
+    from mpgnn_amd.distributed import shard_ranges
+    g = data.config_graph("fb15k237")
+    torch.manual_seed(30)
+    conv = mpgnn_amd.RGCNConv(128, 128, g.num_relations, flow="target_to_source").to(DEV)
+    x, ei, et = g.x.to(DEV), g.edge_index.to(DEV), g.edge_type.to(DEV)
+    gout = torch.randn(g.num_nodes, 128, generator=torch.Generator().manual_seed(4)).to(DEV)
+    xr = x.clone().requires_grad_(True)
+    ref = conv(xr, ei, et)
+    ref.backward(gout)
+    ref_grads = [xr.grad.clone(), conv.weight.grad.clone(), conv.root.grad.clone(), conv.bias.grad.clone()]
+    total = torch.zeros_like(ref)
+    sums = [torch.zeros_like(t) for t in ref_grads]
+    for lo, hi in shard_ranges(g.edge_index, g.num_nodes, world, side="rows"):
+        conv.zero_grad()
+        xs = x.clone().requires_grad_(True)
+        part = conv(xs, ei, et, shard=(lo, hi), shard_side="rows")
+        part.backward(gout)
+        assert torch.count_nonzero(part[:lo]) == 0 and torch.count_nonzero(part[hi:]) == 0
+        rel_close(part[lo:hi], ref[lo:hi], what="own rows")
+        total += part.detach()
+        for acc, gr in zip(sums, [xs.grad, conv.weight.grad, conv.root.grad, conv.bias.grad]):
+            acc += gr
+    rel_close(total, ref, what="sum of row shards")
+    for got, want, what in zip(sums, ref_grads, ("dx", "dW", "droot", "dbias")):
+        rel_close(got, want, what=what)
