@@ -885,3 +885,32 @@ def test_row_shards_complete_rows_and_sum_to_unsharded(world):
     rel_close(total, ref, what="sum of row shards")
     for got, want, what in zip(sums, ref_grads, ("dx", "dW", "droot", "dbias")):
         rel_close(got, want, what=what)
+
+
+@pytest.mark.parametrize("n,f_out,root_weight", [(40, 1, True), (1, 8, True), (40, 1, False), (1, 8, False)])
+def test_squeeze_edge_cases_match_reference(n, f_out, root_weight):
+    """mp_rgcn_layer.py:246 squeezes `zeros + h @ W` before the in-place root add (:265): with a
+    root weight, F_out == 1 or N == 1 makes the reference raise RuntimeError, and so must the
+    drop-in; without one, the squeezed output is returned — same shape and values."""
+    gen = torch.Generator().manual_seed(n + f_out)
+    ei = torch.randint(0, n, (2, 3 * n), generator=gen)
+    et = torch.randint(0, 2, (3 * n,), generator=gen)
+    x = torch.rand(n, 6, generator=gen)
+    torch.manual_seed(30)
+    conv = mpgnn_amd.CustomRGCNConv(6, f_out, 1, root_weight=root_weight, flow="target_to_source")
+    W = conv.weight.detach().clone()
+    root = conv.root.detach().clone() if root_weight else None
+    bias = conv.bias.detach().clone()
+    try:
+        ref = orc.custom_rgcn_forward(x, ei, et, 1, W, root, bias)
+        ref_err = None
+    except RuntimeError as e:
+        ref, ref_err = None, e
+    conv = conv.to(DEV)
+    if ref_err is not None:
+        with pytest.raises(RuntimeError):
+            conv(0, 1, x.to(DEV), ei.to(DEV), et.to(DEV))
+    else:
+        out = conv(0, 1, x.to(DEV), ei.to(DEV), et.to(DEV))
+        assert out.shape == ref.shape
+        rel_close(out, ref, what="squeezed output")
