@@ -236,8 +236,11 @@ enum mpgnn_option {
     MPGNN_OPT_Y_ROWMAJOR = 17,  /* forward, mode ALL: 1 = the transform writes its rows in the combine list's
                                    order and the combine streams them; 0 (default) = relation-major rows gathered
                                    by the combine; same results */
-    MPGNN_OPT_REL_PINGPONG = 18 /* rel_gemm_kernel: 1 = one 512-thread workgroup per CU, two wave groups
+    MPGNN_OPT_REL_PINGPONG = 18, /* rel_gemm_kernel: 1 = one 512-thread workgroup per CU, two wave groups
                                    alternating MFMA and memory phases; same results */
+    MPGNN_OPT_REL_WIDE = 19     /* 1 (default): the B-stationary GEMM also takes F_in = F_out = 256 (two 128-column
+                                   blocks, weight slice reloaded after the chain on a relation change);
+                                   0: tile_gemm_kernel there */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

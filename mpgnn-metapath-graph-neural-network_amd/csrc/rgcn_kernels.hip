@@ -1061,11 +1061,14 @@ struct RelGemmArgs {
     unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][32] s_memtime timeline, or nullptr
 };
 
-template <int KB, bool DGRAD>
+template <int KB, bool DGRAD, int NB = 1>
 struct RelGemm {
     static constexpr int K = 64 * KB;
     static constexpr int KH = K / 2;
-    static constexpr int N = 128;
+    static constexpr int N = 128 * NB;  // output / weight row stride; a workgroup covers 128 columns
+    // first output column of this workgroup (grid.y = NB column blocks)
+    __device__ static __forceinline__ int col0() { return NB > 1 ? (int)blockIdx.y * 128 : 0; }
+    static constexpr bool kPrefetchB = KB <= 2;  // K = 256: two weight slices would not fit in registers
     static constexpr int lda = K + 4;
     static constexpr int WPT = 32 * (K / 4) / kThreads;  // float4 of an A tile per thread
 
@@ -1161,11 +1164,11 @@ struct RelGemm {
     __device__ static __forceinline__ void load_b(const float* w, int wave, int lane, float (&b)[KH]) {
         const int c = lane & 31, h = lane >> 5;
         if constexpr (!DGRAD) {
-            const float* p = w + (size_t)(h * KH) * N + wave * 32 + c;
+            const float* p = w + (size_t)(h * KH) * N + col0() + wave * 32 + c;
 #pragma unroll
             for (int j = 0; j < KH; ++j) b[j] = p[j * N];
         } else {  // B(k, n) = W[n][k]: K consecutive floats of row n = 32·wave + c
-            const float* p = w + (size_t)(wave * 32 + c) * K + h * KH;
+            const float* p = w + (size_t)(col0() + wave * 32 + c) * K + h * KH;
 #pragma unroll
             for (int j = 0; j < KH; j += 4) {
                 const float4 t = *reinterpret_cast<const float4*>(p + j);
@@ -1236,8 +1239,10 @@ struct RelGemm {
                 ypos = cur.root ? a.yroot_pos[cur.r0 - a.row_lo + rr] : a.y_pos[cur.r0 + rr];
             }
             const bool new_w = nxt.w != cur.w;
-            float bn[KH];
-            if (new_w) load_b(nxt.w, wave, lane, bn);      // the next relation run's slice
+            float bn[kPrefetchB ? KH : 1];
+            if constexpr (kPrefetchB) {
+                if (new_w) load_b(nxt.w, wave, lane, bn);  // the next relation run's slice
+            }
             const float* Ab = As + buf * 32 * lda + c * lda + h * KH;
             f32x16 acc;
 #pragma unroll
@@ -1260,7 +1265,7 @@ struct RelGemm {
                 for (int r = 0; r < 16; ++r) {
                     const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
                     const int pos = __shfl(ypos, row);
-                    if (row < cur.nrows) a.Y[(size_t)pos * N + wave * 32 + c] = acc[r];
+                    if (row < cur.nrows) a.Y[(size_t)pos * N + col0() + wave * 32 + c] = acc[r];
                 }
             } else {
                 float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
@@ -1272,14 +1277,18 @@ struct RelGemm {
                         if constexpr (DGRAD) {
                             if (!cur.root) o = o / sc[row];
                         }
-                        Yt[(size_t)row * N + wave * 32 + c] = o;
+                        Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
                     }
                 }
             }
             if (has_next) commit(nxt, tid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
             if (new_w) {
+                if constexpr (kPrefetchB) {
 #pragma unroll
-                for (int j = 0; j < KH; ++j) b[j] = bn[j];
+                    for (int j = 0; j < KH; ++j) b[j] = bn[j];
+                } else {
+                    load_b(nxt.w, wave, lane, b);  // after this item's chain: b is free
+                }
             }
             __syncthreads();
             stamp(3 + 2 * (i - i_beg));
@@ -1355,7 +1364,7 @@ struct RelGemm {
                     if constexpr (DGRAD) {
                         if (!cur.root) o = o / sc[row];
                     }
-                    Yt[(size_t)row * N + wave * 32 + c] = o;
+                    Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
                 }
             }
             if (has1) commit(n1, tid, vh, ch, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
@@ -1450,7 +1459,7 @@ struct RelGemm {
                             if constexpr (DGRAD) {
                                 if (!cur.root) o = o / sc[row];
                             }
-                            Yt[(size_t)row * N + wave * 32 + c] = o;
+                            Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
                         }
                     }
                     if (has_next) commit(nxt, gtid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
@@ -1540,7 +1549,7 @@ struct RelGemm {
                     const float d = __shfl(invh, row);
                     if (!cur.root) o = o / d;
                 }
-                if (row < cur.nrows) Yt[(size_t)row * N + wave * 32 + c] = o;
+                if (row < cur.nrows) Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
             }
             if (has1 && nxt.w != cur.w) load_b(nxt.w, wave, lane, b);  // after the chain: b is free
             cur = nxt;
@@ -1626,7 +1635,7 @@ struct RelGemm {
                         if constexpr (DGRAD) {
                             if (!cur.root) o = o / sc[row];
                         }
-                        Yt[(size_t)row * N + wave * 32 + c] = o;
+                        Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
                     }
                 }
                 if (has_next) commit(nxt, tid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
@@ -1654,12 +1663,16 @@ struct RelGemm {
     }
 };
 
-template <int KB, bool DGRAD>
+template <int KB, bool DGRAD, int NB = 1>
 __global__ __launch_bounds__(kThreads, 2) void rel_gemm_kernel(RelGemmArgs a) {
     extern __shared__ float smem[];
-    if (a.queue != nullptr) RelGemm<KB, DGRAD>::run_dynamic(a, smem);
-    else if (a.deep) RelGemm<KB, DGRAD>::run_deep(a, smem);
-    else RelGemm<KB, DGRAD>::run(a, smem);
+    if constexpr (NB > 1 || KB > 2) {
+        RelGemm<KB, DGRAD, NB>::run(a, smem);  // wide shapes: the default schedule only
+    } else {
+        if (a.queue != nullptr) RelGemm<KB, DGRAD>::run_dynamic(a, smem);
+        else if (a.deep) RelGemm<KB, DGRAD>::run_deep(a, smem);
+        else RelGemm<KB, DGRAD>::run(a, smem);
+    }
 }
 
 template <int KB, bool DGRAD>
@@ -3273,6 +3286,7 @@ static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
 
 
 static bool g_y_rowmajor = false;  // MPGNN_OPT_Y_ROWMAJOR: forward transform output in combine order (opt-in)
+static bool g_rel_wide = true;  // MPGNN_OPT_REL_WIDE: B-stationary GEMM also for F_in = F_out = 256 (C5)
 static bool g_rel_pingpong = false;  // MPGNN_OPT_REL_PINGPONG: two wave groups alternating MFMA / memory phases
 static bool g_rel_direct = false; // MPGNN_OPT_REL_DIRECT: LDS-free rel_gemm (waves load their own A fragments)
 static bool g_rel_deep = false;   // MPGNN_OPT_REL_DEEP: rel_gemm A rows two items ahead
@@ -3303,6 +3317,15 @@ static int g_rel_wg_per_cu = 2;  // MPGNN_OPT_REL_WGS: rel_gemm_kernel workgroup
 static bool g_rel_gemm = true;  // MPGNN_OPT_REL_GEMM: B-stationary GEMM for K ∈ {64, 128}, N = 128
 static bool g_fused = false;    // MPGNN_OPT_FUSED: fused means + transform for F_in = F_out = 128 (opt-in: latency-bound today)
 
+template <int KB, bool DGRAD, int NB>
+static void launch_rel_gemm_wide(const RelGemmArgs& a, hipStream_t st) {
+    constexpr int lda = 64 * KB + 4;
+    const size_t lds = (size_t)(2 * 32 * lda + 64 + 4) * sizeof(float);
+    const int n_items = a.n_rel + a.n_root;
+    const int grid = std::min(n_items, std::max(1, cu_count() * 2 / NB));
+    hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD, NB>), dim3(grid, NB), dim3(kThreads), lds, st, a);
+}
+
 template <int KB, bool DGRAD>
 static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
     constexpr int lda = 64 * KB + 4;
@@ -3322,6 +3345,11 @@ static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
 }
 
 static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, hipStream_t st) {
+    if (K == 256) {  // F_in = F_out = 256 (C5): two 128-column blocks, K = 256
+        if (dgrad) launch_rel_gemm_wide<4, true, 2>(a, st);
+        else launch_rel_gemm_wide<4, false, 2>(a, st);
+        return;
+    }
     if (K == 64) {
         if (dgrad) launch_rel_gemm_t<1, true>(a, st);
         else launch_rel_gemm_t<1, false>(a, st);
@@ -3535,7 +3563,8 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         if (st != MPGNN_OK) return st;
     }
     // B-stationary GEMM (weights in registers per relation run) for the bench shapes
-    if (gather_kind != 0 && W != nullptr && g_rel_gemm && (K == 64 || K == 128) && N == 128 && g_ablate == 0 &&
+    if (gather_kind != 0 && W != nullptr && g_rel_gemm && (((K == 64 || K == 128) && N == 128) || (K == 256 && N == 256 && g_rel_wide)) &&
+        g_ablate == 0 &&
         (!g_stamps || !g_tile_ws) && trans == (gather_kind == 1 ? 1 : 0)) {
         RelGemmArgs r{};
         r.t_begin = p->d.t32_begin;
@@ -3561,6 +3590,10 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         r.stagger = g_rel_stagger;
         r.queue = (g_rel_queue && !g_stamps) ? rel_queue(strm) : nullptr;
         r.deep = g_stamps ? 0 : (g_rel_pingpong ? 3 : (g_rel_direct ? 2 : (g_rel_deep ? 1 : 0)));
+        if (K == 256) {  // the wide kernel runs the default schedule only
+            r.deep = 0;
+            r.queue = nullptr;
+        }
         r.y_pos = y_pos;
         r.yroot_pos = yroot_pos;
         if (y_pos != nullptr && (r.deep != 0 || r.queue != nullptr))
@@ -3999,6 +4032,10 @@ using namespace mpgnn;
 extern "C" {
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_REL_WIDE) {
+        g_rel_wide = value != 0;
+        return MPGNN_OK;
+    }
     if (option == MPGNN_OPT_REL_PINGPONG) {
         g_rel_pingpong = value != 0;
         return MPGNN_OK;
