@@ -233,9 +233,8 @@ enum mpgnn_option {
                                    barriers); same results */
     MPGNN_OPT_FLAT_CPW = 16,    /* flat row-sum kernel: plan chunks per wave, 1 (default), 2 or 4, the next
                                    chunk's metadata fetched behind the current rows; same results */
-    MPGNN_OPT_Y_ROWMAJOR = 17,  /* forward, mode ALL: 1 = the transform writes its rows in the combine list's
-                                   order and the combine streams them; 0 (default) = relation-major rows gathered
-                                   by the combine; same results */
+    MPGNN_OPT_Y_ROWMAJOR = 17,  /* withdrawn (measured neutral, slowed the default transform): only 0 is
+                                   accepted, 1 returns MPGNN_ERR_ARG */
     MPGNN_OPT_REL_PINGPONG = 18, /* rel_gemm_kernel: 1 = one 512-thread workgroup per CU, two wave groups
                                    alternating MFMA and memory phases; same results */
     MPGNN_OPT_REL_WIDE = 19     /* 1 (default): the B-stationary GEMM also takes F_in = F_out = 256 (two 128-column

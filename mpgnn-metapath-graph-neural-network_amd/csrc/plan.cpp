@@ -510,16 +510,6 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
         };
         augment(p->t_ptr, p->t_seg, p->tx_f, p->tx_val, kFlatChunk);
         augment(p->rw_ptr, p->rw_seg, p->rwx_f, p->rwx_val, kFlatChunkRowMajor);
-        // positions in the rwx list (xptr is the row-major combine list's now)
-        p->seg_rwx_pos.assign(p->S, 0);
-        parallel_for(N, [&](int64_t i) {
-            for (int32_t q = p->rw_ptr[i]; q < p->rw_ptr[i + 1]; ++q)
-                p->seg_rwx_pos[p->rw_seg[q]] = xptr[i] + (q - p->rw_ptr[i]);
-        });
-        p->root_rwx_pos.assign(hi - lo, 0);
-        parallel_for(hi - lo, [&](int64_t k) { p->root_rwx_pos[k] = xptr[lo + k + 1] - 1; });
-        p->rwx_iota.resize(p->rwx_val.size());
-        parallel_for((int64_t)p->rwx_iota.size(), [&](int64_t q) { p->rwx_iota[q] = (int32_t)q; });
     }
     tm.mark("flat lists");
     {
@@ -816,8 +806,6 @@ int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
         {&p->d.rwx_f.row_of, &p->rwx_f.row_of}, {&p->d.rwx_f.split_row, &p->rwx_f.split_row},
         {&p->d.rwx_f.split_ptr, &p->rwx_f.split_ptr}, {&p->d.rwx_f.split_slot, &p->rwx_f.split_slot},
         {&p->d.rwx_f.row_split, &p->rwx_f.row_split}, {&p->d.rwx_val, &p->rwx_val},
-        {&p->d.seg_rwx_pos, &p->seg_rwx_pos}, {&p->d.root_rwx_pos, &p->root_rwx_pos},
-        {&p->d.rwx_iota, &p->rwx_iota},
     };
     size_t total = 0;
     std::vector<size_t> offs;

@@ -102,9 +102,6 @@ struct DeviceTables {
     FlatDev seg_f, t_f, rw_f;       // flat chunked lists (segment means, grad_x, combine)
     FlatDev tx_f, rwx_f;            // grad_x / combine lists with a trailing extra-row entry per own row
     int32_t *tx_val = nullptr, *rwx_val = nullptr;  // their entry values (segment id | -(own row + 1))
-    // row-major transform output: position in the rwx list of each segment / own row's extra
-    // entry, and the identity table the combine then walks (Y written in combine order)
-    int32_t *seg_rwx_pos = nullptr, *root_rwx_pos = nullptr, *rwx_iota = nullptr;
     void* block = nullptr;          // single hipMalloc holding every table above
     size_t block_bytes = 0;
 };
@@ -153,7 +150,6 @@ struct mpgnn_plan {
     // (Σ entries) + extra in the reference order and no finalize pass is needed
     mpgnn::FlatHost tx_f, rwx_f;
     std::vector<int32_t> tx_val, rwx_val;
-    std::vector<int32_t> seg_rwx_pos, root_rwx_pos, rwx_iota;  // see DeviceTables
     std::vector<int32_t> ta_key;               // [ta entries] node_2 of each ta entry
     std::vector<int32_t> rel_ta_ent_ptr;       // [nrel+1] ta entry range of each relation
     std::vector<int32_t> rel_seg_piece_ptr;    // [nrel+1] seg pieces of each relation

@@ -1056,8 +1056,6 @@ struct RelGemmArgs {
     int stagger;                 // s_sleep quanta (64 clk) the second half of the grid waits first
     int* queue;                  // nullable: per-group item counters (dynamic schedule), zero between launches
     int deep;                    // 1: A rows fetched two items ahead (run_deep)
-    const int* y_pos;            // nullable: output row of segment s is y_pos[s] (row-major combine order)
-    const int* yroot_pos;        //   and of node i is yroot_pos[i - row_lo]; Y then holds both (run() only)
     unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][32] s_memtime timeline, or nullptr
 };
 
@@ -1233,11 +1231,6 @@ struct RelGemm {
             const bool has_next = i + 1 < i_end;
             const Item nxt = has_next ? get_item(i + 1) : cur;
             if (has_next) issue(a, nxt, tid, v, cnt);      // in flight during this item's MFMAs
-            int ypos = 0;  // this lane's row position (row = lane & 31) when Y is row-major
-            if (a.y_pos != nullptr) {
-                const int rr = min(lane & 31, cur.nrows - 1);
-                ypos = cur.root ? a.yroot_pos[cur.r0 - a.row_lo + rr] : a.y_pos[cur.r0 + rr];
-            }
             const bool new_w = nxt.w != cur.w;
             float bn[kPrefetchB ? KH : 1];
             if constexpr (kPrefetchB) {
@@ -1260,25 +1253,16 @@ struct RelGemm {
             stamp(2 + 2 * (i - i_beg));
             // epilogue: each accumulator register = rows (r&3) + 8(r>>2) + 4h, column 32·wave + c
             const float* sc = Sc + buf * 32;
-            if (a.y_pos != nullptr) {  // rows scattered to their position in the combine list
+            float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const int pos = __shfl(ypos, row);
-                    if (row < cur.nrows) a.Y[(size_t)pos * N + col0() + wave * 32 + c] = acc[r];
-                }
-            } else {
-                float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (row < cur.nrows) {
-                        float o = acc[r];
-                        if constexpr (DGRAD) {
-                            if (!cur.root) o = o / sc[row];
-                        }
-                        Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row < cur.nrows) {
+                    float o = acc[r];
+                    if constexpr (DGRAD) {
+                        if (!cur.root) o = o / sc[row];
                     }
+                    Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
                 }
             }
             if (has_next) commit(nxt, tid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
@@ -3285,7 +3269,6 @@ static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
 }
 
 
-static bool g_y_rowmajor = false;  // MPGNN_OPT_Y_ROWMAJOR: forward transform output in combine order (opt-in)
 static bool g_rel_wide = true;  // MPGNN_OPT_REL_WIDE: B-stationary GEMM also for F_in = F_out = 256 (C5)
 static bool g_rel_pingpong = false;  // MPGNN_OPT_REL_PINGPONG: two wave groups alternating MFMA / memory phases
 static bool g_rel_direct = false; // MPGNN_OPT_REL_DIRECT: LDS-free rel_gemm (waves load their own A fragments)
@@ -3539,8 +3522,7 @@ static void clamp_rows(const mpgnn_plan* p, int64_t* lo, int64_t* hi) {
 static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, int gather_kind, const float* src,
                        int K, const float* W, const float* Wroot, int trans, int N, float* Y, float* Yroot,
                        int64_t row_lo, int64_t row_hi, float* H, float* Pseg, bool exact, int kind,
-                       hipStream_t strm, const float* Hsrc = nullptr, const int* y_pos = nullptr,
-                       const int* yroot_pos = nullptr) {
+                       hipStream_t strm, const float* Hsrc = nullptr) {
     const int n_rel = s.t_hi - s.t_lo;
     const int n_root = (Wroot != nullptr) ? (int)((row_hi - row_lo + kTileRows - 1) / kTileRows) : 0;
     if (n_rel + n_root == 0) return MPGNN_OK;
@@ -3594,15 +3576,10 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
             r.deep = 0;
             r.queue = nullptr;
         }
-        r.y_pos = y_pos;
-        r.yroot_pos = yroot_pos;
-        if (y_pos != nullptr && (r.deep != 0 || r.queue != nullptr))
-            return arg_error("row-major transform output needs the default rel_gemm schedule");
         TimedLaunch tl(kind, strm);
         launch_rel_gemm(r, K, gather_kind == 1, strm);
         return hip_check(hipGetLastError(), "rel_gemm_kernel launch");
     }
-    if (y_pos != nullptr) return arg_error("row-major transform output needs the B-stationary GEMM");
     // tile_gemm stages A rows as float4 (K % 4 == 0); other widths take seg_tile_kernel
     if (gather_kind != 0 && W != nullptr && (K & 3) == 0 && (g_ablate & 15) == 0 &&
         (!g_stamps || (g_tile_ws && round_up(K, 64) <= 128))) {
@@ -4040,8 +4017,8 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
         g_rel_pingpong = value != 0;
         return MPGNN_OK;
     }
-    if (option == MPGNN_OPT_Y_ROWMAJOR) {
-        g_y_rowmajor = value != 0;
+    if (option == MPGNN_OPT_Y_ROWMAJOR) {  // measured neutral and slowed the default GEMM: withdrawn
+        if (value != 0) return arg_error("MPGNN_OPT_Y_ROWMAJOR was withdrawn (DESIGN.md §4)");
         return MPGNN_OK;
     }
     if (option == MPGNN_OPT_FLAT_CPW) {
@@ -4211,14 +4188,6 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     float* Yroot = root ? reinterpret_cast<float*>(ws + w.yroot) : nullptr;
     const bool exact = g_exact_order;
     const bool own_range = row_lo == p->shard_lo && row_hi == p->shard_hi;
-    // Row-major transform output (MPGNN_OPT_Y_ROWMAJOR): the GEMM writes every segment row and
-    // root row at its position in the augmented combine list, so the combine streams Y in order
-    // instead of gathering it. Needs the B-stationary GEMM's default schedule and the full list.
-    const bool rowmap = g_y_rowmajor && mode == MPGNN_MODE_ALL && !exact && root != nullptr && own_range &&
-                        s.all_segments && g_rel_gemm && (F_in == 64 || F_in == 128) && F_out == 128 &&
-                        g_ablate == 0 && g_stamps == nullptr && !g_rel_deep && !g_rel_direct && !g_rel_queue && !g_rel_pingpong &&
-                        !g_fused && g_overlap == 0;
-
     if (!exact && g_fused && F_in == 128 && F_out == 128 && g_ablate == 0) {
         // 1+2) fused: segment means formed in LDS and contracted on the matrix cores in one launch
         FusedArgs f{};
@@ -4255,16 +4224,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
         SideStream* ss = (g_overlap > 0 && !exact && g_stamps == nullptr && g_ablate == 0 && s.sel_e > s.sel_b)
                              ? side_stream(p->device) : nullptr;
-        if (rowmap) {  // transform rows written in combine order (see below)
-            {
-                TimedLaunch tl(MPGNN_K_MEAN, strm);
-                st = run_means(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
-                if (st != MPGNN_OK) return st;
-            }
-            st = run_seg(p, mode, s, 2, x, F_in, weight, root, 0, F_out, Y, Y, row_lo, row_hi, nullptr, nullptr, true,
-                         MPGNN_K_SEG_FWD, strm, H, p->d.seg_rwx_pos, p->d.root_rwx_pos);
-            if (st != MPGNN_OK) return st;
-        } else if (ss != nullptr) {
+        if (ss != nullptr) {
             const int groups = mode == MPGNN_MODE_ALL ? g_overlap : 1;
             st = fwd_overlapped(p, mode, s, groups, ss, x, F_in, weight, root, F_out, H,
                                 reinterpret_cast<float*>(ws + w.pseg), Y, Yroot, row_lo, row_hi, strm);
@@ -4293,30 +4253,6 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     a.hi = (int)row_hi;
     a.out = out;
     int k_lo = 0, k_hi = 0;
-    if (rowmap) {  // Σ over consecutive rows of Y (segments, then the row's root row) + bias
-        FlatRun f{};
-        f.fd = &p->d.rwx_f;
-        f.c_lo = 0;
-        f.c_hi = (int)p->rwx_f.chunk_ptr.size() - 1;
-        f.k_lo = 0;
-        f.k_hi = (int)p->rwx_f.split_row.size();
-        f.table = p->d.rwx_iota;
-        f.idx_off = 0;
-        f.filter = false;
-        f.src = Y;
-        f.F = F_out;
-        f.row_off = 0;
-        f.out = out;
-        f.carry = reinterpret_cast<float*>(ws + w.prw);
-        f.final_mode = 0;
-        f.extra = nullptr;
-        f.bias = bias;
-        f.lo = (int)row_lo;
-        f.hi = (int)row_hi;
-        f.relu = act == MPGNN_ACT_RELU;
-        TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
-        return run_flat(f, strm);
-    }
     if (mode == MPGNN_MODE_ALL && !exact && Yroot != nullptr && own_range) {
         // augmented row-major list: Σ_r Y + Y_root per own row, + bias at the flush
         if (row_lo != 0 || row_hi != p->N) {  // rows outside the shard may have no entry

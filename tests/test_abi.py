@@ -70,6 +70,15 @@ def test_bad_arguments():
         p.select(7, 0, 0)          # unknown mode
 
 
+def test_withdrawn_option_is_refused():
+    """MPGNN_OPT_Y_ROWMAJOR (17) was withdrawn: 0 is accepted, 1 is refused with a message."""
+    from mpgnn_amd import _lib
+    lib = _lib.lib
+    assert lib.mpgnn_set_option(17, 0) == 0
+    assert lib.mpgnn_set_option(17, 1) == _lib.MPGNN_ERR_ARG
+    assert b"withdrawn" in lib.mpgnn_last_error()
+
+
 def test_workspace_bytes_is_host_computable():
     import mpgnn_amd
     g = mpgnn_amd.data.config_graph("C1")

@@ -741,7 +741,7 @@ def test_split_k_linear_matches_nn_linear(n, f_in, f_out):
 
 
 @pytest.mark.parametrize("option,value,default", [(12, 1, 0), (14, 1, 0), (15, 1, 0), (16, 2, 1), (16, 4, 1),
-                                                   (17, 1, 0), (18, 1, 0)])
+                                                   (18, 1, 0)])
 def test_rel_gemm_schedule_variants_bitwise_equal(option, value, default):
     """MPGNN_OPT_REL_QUEUE (12): items taken from atomic counters; MPGNN_OPT_REL_DEEP (14): A rows
     two items ahead. Both give the same bits as the default schedule (each item is computed by
