@@ -153,6 +153,12 @@ int32_t mpgnn_rel_mean_bwd_workspace_bytes(const mpgnn_plan* plan, int32_t mode,
 int32_t mpgnn_rel_mean_bwd(const mpgnn_plan* plan, int32_t mode, int64_t relation, int32_t num_relations,
                            const float* dh, int32_t F, float* dx, void* workspace, void* stream);
 
+/* ReLU backward of a layer whose ReLU was fused into the forward (mpgnn_rgcn_fwd_act):
+ * dst[i] = act_out[i] > 0 ? grad_out[i] : 0 for n floats, one pass (dst may alias grad_out).
+ * Replaces autograd's threshold_backward of F.relu(conv(...)) (model.py:144,146; main_rgcn
+ * Net) and of the ReLU after each metapath layer (model.py:213-215). */
+int32_t mpgnn_relu_bwd(const float* grad_out, const float* act_out, int64_t n, float* dst, void* stream);
+
 /* Bytes of scratch the fwd/bwd calls need (caller allocates, e.g. torch.empty(uint8)). */
 int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* plan, int32_t mode, int64_t relation,
                                    int32_t num_relations, int32_t F_in, int32_t F_out,
@@ -237,9 +243,16 @@ enum mpgnn_option {
                                    accepted, 1 returns MPGNN_ERR_ARG */
     MPGNN_OPT_REL_PINGPONG = 18, /* rel_gemm_kernel: 1 = one 512-thread workgroup per CU, two wave groups
                                    alternating MFMA and memory phases; same results */
-    MPGNN_OPT_REL_WIDE = 19     /* 1 (default): the B-stationary GEMM also takes F_in = F_out = 256 (two 128-column
+    MPGNN_OPT_REL_WIDE = 19,    /* 1 (default): the B-stationary GEMM also takes F_in = F_out = 256 (two 128-column
                                    blocks, weight slice reloaded after the chain on a relation change);
                                    0: tile_gemm_kernel there */
+    MPGNN_OPT_CHUNK_ROWS = 20,  /* backward weight-gradient reduction chunks: base length in rows (multiple of 32,
+                                   32..1024, default 192) of the root chunks and of the relation chunks of plans
+                                   created afterwards; same results up to fp32 summation order of the slabs */
+    MPGNN_OPT_OUTER_ROOT_FIRST = 21, /* backward, merged outer-product launch: 1 (default) = root / bias chunks take
+                                   the first workgroups, 0 = the weight-gradient chunks do; same results */
+    MPGNN_OPT_OUTER_SLICE = 22  /* backward, merged outer-product launch: rows per LDS slice, 16 (default: 36 KB
+                                   of LDS per workgroup, four workgroups per CU), 32 (72 KB, two) or 8; same results */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

@@ -74,6 +74,7 @@ SIGNATURES = [
     ("mpgnn_rgcn_fwd_act", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _P, _P, _P, _I32, _P]),
     ("mpgnn_rgcn_bwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _I32, _P, _P, _I64, _I64,
                               _P, _P, _P, _P, _P, _P]),
+    ("mpgnn_relu_bwd", _I32, [_P, _P, _I64, _P, _P]),
     ("mpgnn_set_option", _I32, [_I32, _I64]),
     ("mpgnn_timing_enable", _I32, [_I32]),
     ("mpgnn_debug_occupancy", _I32, [_I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),

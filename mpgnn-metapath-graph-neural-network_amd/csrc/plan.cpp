@@ -78,6 +78,7 @@ int32_t select_relations(const mpgnn_plan* p, int32_t mode, int64_t relation, in
 // independent elements split into contiguous thread ranges; the counting sorts keep their
 // stability by giving thread t the t-th contiguous slice of the input and the t-th slot of
 // every bucket. Results do not depend on the thread count (tests/test_plan.py).
+int g_chunk_rows = kChunkRows;
 int g_plan_threads = 0;  // MPGNN_OPT_PLAN_THREADS: 0 = hardware concurrency, capped at 16
 static constexpr int64_t kParMin = 1 << 16;  // fewer elements: one thread
 
@@ -560,7 +561,7 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
     // many slab bytes as the whole input of dW (56 GB); 4096 chunks keep the slabs at ~1 GB
     // and still give > 16 workgroups per CU.
     const int64_t s_all = p->rel_seg_ptr[R];
-    const int32_t chunk_cap = (int32_t)std::max<int64_t>(kChunkRows, (s_all + kChunkTarget - 1) / kChunkTarget + 31) / 32 * 32;
+    const int32_t chunk_cap = (int32_t)std::max<int64_t>(g_chunk_rows, (s_all + kChunkTarget - 1) / kChunkTarget + 31) / 32 * 32;
     for (int64_t d = 0; d < R; ++d) {
         for (int32_t s = p->rel_seg_ptr[d]; s < p->rel_seg_ptr[d + 1]; s += kTile32) {
             p->t32_begin.push_back(s);

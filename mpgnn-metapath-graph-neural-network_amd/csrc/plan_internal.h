@@ -26,7 +26,10 @@ inline int32_t item_cost(int64_t edges) {
 }
 // Relation-pure reduction chunks for the weight gradient (outer_accum_kernel): at most this
 // many segments, balanced within a relation (bounds the longest workgroup's MFMA chain).
-constexpr int kChunkRows = 128;
+// 192 with 16-row slices (MPGNN_OPT_OUTER_SLICE): FB15K backward outer + slab reduce 61.7 ->
+// 54.5 us per layer vs 256 / 32-row slices (128: 56.0; 512 leaves the outer launch too few
+// workgroups: 88 us); scripts/chunk_ab.py
+constexpr int kChunkRows = 192;
 constexpr int64_t kChunkTarget = 4096;  // reduction chunks per graph (chunk length grows past kChunkRows)
 // Ragged lists: a run (segment / gathered row) longer than this many entries is cut into
 // ordered pieces of at most kPieceEntries, summed by piece_sum_kernel; consumers then add the
@@ -162,6 +165,7 @@ struct mpgnn_plan {
 namespace mpgnn {
 
 void set_last_error(const std::string& msg);
+extern int g_chunk_rows;     // MPGNN_OPT_CHUNK_ROWS: reduction chunk base length (default kChunkRows)
 extern int g_plan_threads;  // host threads of mpgnn_plan_create (0 = hardware concurrency, ≤ 16)
 
 // Resolve (mode, relation, R) to a contiguous dense-relation range [d_lo, d_hi).

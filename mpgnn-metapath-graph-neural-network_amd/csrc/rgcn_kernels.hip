@@ -2889,10 +2889,12 @@ constexpr int kOuterLd = 288;                        // one row pair: 128 + 32 p
 __device__ __forceinline__ int outer_row(int k) { return (k >> 1) * kOuterLd + (k & 1) * 160; }
 constexpr int kOuterBuf = (kSlice / 2) * kOuterLd;   // floats per 32-row matrix image
 
-template <bool VEC>
+// SL: rows per slice (32, or 16 = half the LDS, three workgroups per CU: MPGNN_OPT_OUTER_SLICE)
+template <bool VEC, int SL = kSlice>
 __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int cidx) {
+    constexpr int OB = (SL / 2) * kOuterLd;  // floats per SL-row matrix image
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* bufs = smem;  // [2 buffers][A, B][kOuterBuf]
+    float* bufs = smem;  // [2 buffers][A, B][OB]
     int p0, p1;
     if (a.chunk_begin != nullptr) {
         p0 = ld_uniform(a.chunk_begin, cidx + a.chunk_off);
@@ -2910,19 +2912,19 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
     const int lane = tid & 63;
     const int c = lane & 31;
     const int h = lane >> 5;
-    const int nslices = (p1 - p0 + kSlice - 1) / kSlice;
+    const int nslices = (p1 - p0 + SL - 1) / SL;
 
     // staging: thread t owns float4 slots i = t + j·256 (j < 4) of each 32 × 128 slice:
     // row i >> 5, columns 4·(i & 31) .. +3 (scalar path: 16 floats, row i >> 7, column i & 127)
-    constexpr int NS = VEC ? 4 : 16;
-    float4 va[VEC ? 4 : 1], vb[VEC ? 4 : 1];
-    float sa[VEC ? 1 : 16], sb[VEC ? 1 : 16];
+    constexpr int NS = VEC ? SL * 128 / (4 * kThreads) : SL * 128 / kThreads;
+    float4 va[VEC ? NS : 1], vb[VEC ? NS : 1];
+    float sa[VEC ? 1 : NS], sb[VEC ? 1 : NS];
     int bi[NS];  // B row index of each staged slot (next slice), loaded one slice earlier
     int bi_next[NS];
     auto slot_row = [&](int j) { return VEC ? ((tid + j * kThreads) >> 5) : ((tid + j * kThreads) >> 7); };
     auto slot_col = [&](int j) { return VEC ? 4 * ((tid + j * kThreads) & 31) : ((tid + j * kThreads) & 127); };
     auto load_idx = [&](int slice, int (&o)[NS]) {
-        const int ps = p0 + slice * kSlice;
+        const int ps = p0 + slice * SL;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             const int p = min(ps + slot_row(j), p1 - 1);
@@ -2930,7 +2932,7 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
         }
     };
     auto issue = [&](int slice) {
-        const int ps = p0 + slice * kSlice;
+        const int ps = p0 + slice * SL;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             const int ra = min(ps + slot_row(j), p1 - 1) - a.a_off;
@@ -2948,9 +2950,9 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
         }
     };
     auto commit = [&](int slice, float* buf) {
-        const int nr = min(kSlice, p1 - p0 - slice * kSlice);
+        const int nr = min(SL, p1 - p0 - slice * SL);
         float* Al = buf;
-        float* Bl = buf + kOuterBuf;
+        float* Bl = buf + OB;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             const int r = slot_row(j);
@@ -2989,7 +2991,7 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
     }
     __syncthreads();
     for (int sl = 0; sl < nslices; ++sl) {
-        float* cur = bufs + (sl & 1) * 2 * kOuterBuf;
+        float* cur = bufs + (sl & 1) * 2 * OB;
         const bool more = sl + 1 < nslices;  // uniform
         if (more) {
 #pragma unroll
@@ -2997,14 +2999,20 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
             if (sl + 2 < nslices) load_idx(sl + 2, bi_next);
             issue(sl + 1);
         }
-        const int nr = min(kSlice, p1 - p0 - sl * kSlice);
+        const int nr = min(SL, p1 - p0 - sl * SL);
         if (do_bsum) {
-            const float* Bl = cur + kOuterBuf;
-            for (int r = 0; r < nr; ++r) bsum += Bl[outer_row(r) + tid];
+            // rows >= nr were committed as zeros, so all 32 are added (x + 0 = x: same sum as
+            // stopping at nr); the loads are independent, only the adds chain, in row order
+            const float* Bl = cur + OB;
+            float bl[SL];
+#pragma unroll
+            for (int r = 0; r < SL; ++r) bl[r] = Bl[outer_row(r) + tid];
+#pragma unroll
+            for (int r = 0; r < SL; ++r) bsum += bl[r];
         }
         // k-step t covers rows 2t (lanes h = 0) and 2t + 1 (h = 1); rows >= nr are zero
         const float* Ar = cur + outer_row(h) + c;
-        const float* Br = cur + kOuterBuf + outer_row(h) + wave * 32 + c;
+        const float* Br = cur + OB + outer_row(h) + wave * 32 + c;
         const int steps = (nr + 1) >> 1;
         float av[4], bv;
 #pragma unroll
@@ -3024,7 +3032,7 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
             for (int q = 0; q < 4; ++q) av[q] = an[q];
             bv = bn;
         }
-        if (more) commit(sl + 1, bufs + ((sl + 1) & 1) * 2 * kOuterBuf);
+        if (more) commit(sl + 1, bufs + ((sl + 1) & 1) * 2 * OB);
         __syncthreads();
     }
 
@@ -3060,10 +3068,10 @@ __global__ __launch_bounds__(kThreads, 2) void outer_accum_kernel(OuterArgs a) {
 // The weight-gradient chunks and the root / bias chunks of one backward call in ONE launch:
 // blocks [0, n_a) take `a`, the rest `b` (the root part alone is ~60-110 workgroups, a
 // mostly idle chip for a whole launch).
-template <bool VEC>
-__global__ __launch_bounds__(kThreads, 2) void outer_accum2_kernel(OuterArgs a, OuterArgs b, int n_a) {
-    if ((int)blockIdx.x < n_a) outer_accum_body<VEC>(a, (int)blockIdx.x);
-    else outer_accum_body<VEC>(b, (int)blockIdx.x - n_a);
+template <bool VEC, int SL>
+__global__ __launch_bounds__(kThreads, SL == 32 ? 2 : SL == 16 ? 3 : 4) void outer_accum2_kernel(OuterArgs a, OuterArgs b, int n_a) {
+    if ((int)blockIdx.x < n_a) outer_accum_body<VEC, SL>(a, (int)blockIdx.x);
+    else outer_accum_body<VEC, SL>(b, (int)blockIdx.x - n_a);
 }
 
 // dst[group g] (elems floats) = Σ_{c in chunks of g, ascending} P[c]
@@ -3129,6 +3137,27 @@ __global__ __launch_bounds__(kThreads) void reduce_slabs3_kernel(ReduceArgs r0, 
         const int e = blockIdx.y * kThreads + threadIdx.x;
         if (e < z.elems) z.dst[(size_t)z.ids[b - n0 - n1 - n2] * z.elems + e] = 0.0f;
     }
+}
+
+// dst = act_out > 0 ? grad_out : 0 (ReLU backward, threshold_backward semantics: a NaN or inf
+// gradient where the output was clamped gives 0, as torch's does); float4 when all three
+// pointers are 16-byte aligned, the last n % 4 elements scalar.
+__global__ __launch_bounds__(kThreads) void relu_bwd_kernel(const float* g, const float* y, int64_t n, float* d, int vec) {
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (vec) {
+        const int64_t n4 = n / 4;
+        for (int64_t k = i; k < n4; k += stride) {
+            const float4 gv = reinterpret_cast<const float4*>(g)[k];
+            const float4 yv = reinterpret_cast<const float4*>(y)[k];
+            reinterpret_cast<float4*>(d)[k] = make_float4(yv.x > 0.0f ? gv.x : 0.0f, yv.y > 0.0f ? gv.y : 0.0f,
+                                                          yv.z > 0.0f ? gv.z : 0.0f, yv.w > 0.0f ? gv.w : 0.0f);
+        }
+        i += n4 * 4;
+        if (i >= n) return;
+        // tail: at most 3 elements, thread i handles element n4 * 4 + (its global id)
+    }
+    for (int64_t k = i; k < n; k += stride) d[k] = y[k] > 0.0f ? g[k] : 0.0f;
 }
 
 // G[s] = dh[s] / cnt[sel_b + s] for the segment rows of a selection (segment-means backward)
@@ -3273,6 +3302,8 @@ static bool g_rel_wide = true;  // MPGNN_OPT_REL_WIDE: B-stationary GEMM also fo
 static bool g_rel_pingpong = false;  // MPGNN_OPT_REL_PINGPONG: two wave groups alternating MFMA / memory phases
 static bool g_rel_direct = false; // MPGNN_OPT_REL_DIRECT: LDS-free rel_gemm (waves load their own A fragments)
 static bool g_rel_deep = false;   // MPGNN_OPT_REL_DEEP: rel_gemm A rows two items ahead
+static int g_outer_slice = 16;          // MPGNN_OPT_OUTER_SLICE: rows per LDS slice of the merged outer launch (32 or 16)
+static bool g_outer_root_first = true;  // MPGNN_OPT_OUTER_ROOT_FIRST: root / bias chunks dispatched before the dW chunks
 static bool g_merge_grad = true;  // MPGNN_OPT_MERGE_GRAD: dW + droot/dbias in one outer launch, one reduce launch
 static bool g_rel_queue = false;  // MPGNN_OPT_REL_QUEUE: dynamic item schedule in rel_gemm_kernel
 static std::mutex g_queue_mu;
@@ -3449,7 +3480,7 @@ static RootChunks root_chunks(int64_t lo, int64_t hi) {
     r.rows_lo = (int)lo;
     r.rows_hi = (int)hi;
     const int rows = (int)(hi - lo);
-    int ch = std::max(kChunkRows, round_up((rows + 1023) / 1024, kSlice));
+    int ch = std::max(g_chunk_rows, round_up((rows + 1023) / 1024, kSlice));
     r.chunk = ch;
     r.n = rows > 0 ? (rows + ch - 1) / ch : 0;
     return r;
@@ -4008,6 +4039,19 @@ using namespace mpgnn;
 
 extern "C" {
 
+int32_t mpgnn_relu_bwd(const float* grad_out, const float* act_out, int64_t n, float* dst, void* stream) {
+    if (n < 0) return arg_error("negative n");
+    if (n == 0) return MPGNN_OK;
+    if (!grad_out || !act_out || !dst) return arg_error("NULL grad_out, act_out or dst");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    const bool vec = ((reinterpret_cast<uintptr_t>(grad_out) | reinterpret_cast<uintptr_t>(act_out) |
+                       reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+    const int64_t units = vec ? (n + 3) / 4 : n;
+    const int blocks = (int)std::min<int64_t>((units + kThreads - 1) / kThreads, 8192);
+    hipLaunchKernelGGL(relu_bwd_kernel, dim3(blocks), dim3(kThreads), 0, strm, grad_out, act_out, n, dst, vec ? 1 : 0);
+    return hip_check(hipGetLastError(), "relu_bwd_kernel launch");
+}
+
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
     if (option == MPGNN_OPT_REL_WIDE) {
         g_rel_wide = value != 0;
@@ -4040,6 +4084,20 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
     }
     if (option == MPGNN_OPT_REL_QUEUE) {
         g_rel_queue = value != 0;
+        return MPGNN_OK;
+    }
+    if (option == MPGNN_OPT_OUTER_SLICE) {
+        if (value != 8 && value != 16 && value != 32) return arg_error("MPGNN_OPT_OUTER_SLICE must be 8, 16 or 32");
+        g_outer_slice = (int)value;
+        return MPGNN_OK;
+    }
+    if (option == MPGNN_OPT_OUTER_ROOT_FIRST) {
+        g_outer_root_first = value != 0;
+        return MPGNN_OK;
+    }
+    if (option == MPGNN_OPT_CHUNK_ROWS) {
+        if (value < 32 || value > 1024 || value % 32 != 0) return arg_error("MPGNN_OPT_CHUNK_ROWS must be 32..1024, a multiple of 32");
+        g_chunk_rows = (int)value;
         return MPGNN_OK;
     }
     if (option == MPGNN_OPT_PLAN_THREADS) {
@@ -4675,12 +4733,29 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
     const int root_y = grad_root ? mt : 1;
     if (have_w && have_root && root_y == mt && g_merge_grad) {
         TimedLaunch tl(MPGNN_K_OUTER, strm);
-        if (outer_vec)
-            hipLaunchKernelGGL(outer_accum2_kernel<true>, dim3(nch + rc.n, mt, nt), dim3(kThreads), outer_lds, strm, ow,
-                               orr, nch);
-        else
-            hipLaunchKernelGGL(outer_accum2_kernel<false>, dim3(nch + rc.n, mt, nt), dim3(kThreads), outer_lds, strm,
-                               ow, orr, nch);
+        // root chunks are all full length (the relation chunks of small relations are short):
+        // dispatched first, they stop being the launch's tail (MPGNN_OPT_OUTER_ROOT_FIRST)
+        const OuterArgs& first = g_outer_root_first ? orr : ow;
+        const OuterArgs& second = g_outer_root_first ? ow : orr;
+        const int n_first = g_outer_root_first ? rc.n : nch;
+        const dim3 grid2(nch + rc.n, mt, nt);
+        if (g_outer_slice == 8) {
+            const size_t lds8 = (size_t)(4 * (8 / 2) * kOuterLd) * sizeof(float);
+            if (outer_vec)
+                hipLaunchKernelGGL((outer_accum2_kernel<true, 8>), grid2, dim3(kThreads), lds8, strm, first, second, n_first);
+            else
+                hipLaunchKernelGGL((outer_accum2_kernel<false, 8>), grid2, dim3(kThreads), lds8, strm, first, second, n_first);
+        } else if (g_outer_slice == 16) {
+            const size_t lds16 = (size_t)(4 * (16 / 2) * kOuterLd) * sizeof(float);
+            if (outer_vec)
+                hipLaunchKernelGGL((outer_accum2_kernel<true, 16>), grid2, dim3(kThreads), lds16, strm, first, second, n_first);
+            else
+                hipLaunchKernelGGL((outer_accum2_kernel<false, 16>), grid2, dim3(kThreads), lds16, strm, first, second, n_first);
+        } else if (outer_vec) {
+            hipLaunchKernelGGL((outer_accum2_kernel<true, 32>), grid2, dim3(kThreads), outer_lds, strm, first, second, n_first);
+        } else {
+            hipLaunchKernelGGL((outer_accum2_kernel<false, 32>), grid2, dim3(kThreads), outer_lds, strm, first, second, n_first);
+        }
         if ((st = hip_check(hipGetLastError(), "outer_accum2_kernel launch")) != MPGNN_OK) return st;
     } else {
         if (have_w) {

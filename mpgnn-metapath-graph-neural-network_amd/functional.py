@@ -124,9 +124,12 @@ class _RGCNConvFn(torch.autograd.Function):
     def backward(ctx, grad_out):
         x, weight, root, h_save, act_out = ctx.saved_tensors
         plan = ctx.plan
-        if ctx.act == ACT_RELU:  # ReLU backward (threshold_backward): pass where the output > 0
-            grad_out = grad_out * (act_out > 0)
         grad_out = grad_out.contiguous()
+        if ctx.act == ACT_RELU:  # ReLU backward (threshold_backward): pass where the output > 0, one launch
+            masked = torch.empty_like(act_out)
+            check(lib.mpgnn_relu_bwd(grad_out.data_ptr(), act_out.data_ptr(), grad_out.numel(), masked.data_ptr(),
+                                     _stream(x)), "mpgnn_relu_bwd")
+            grad_out = masked
         if grad_out.data_ptr() % 16:
             grad_out = grad_out.clone()
         N, f_in = x.shape

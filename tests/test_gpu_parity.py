@@ -806,6 +806,50 @@ def test_merged_gradient_launches_bitwise_equal(mode):
             assert torch.equal(a, b), req
 
 
+@pytest.mark.parametrize("mode", [MODE_SINGLE, MODE_ALL])
+def test_outer_slice_and_dispatch_order_bitwise_equal(mode):
+    """MPGNN_OPT_OUTER_SLICE (8 / 16 / 32 rows per LDS slice) and MPGNN_OPT_OUTER_ROOT_FIRST only
+    change staging and workgroup order, not the row order of any MFMA accumulation chain: every
+    gradient keeps its bits. MPGNN_OPT_CHUNK_ROWS moves slab boundaries (fp32 order): 1e-4."""
+    from mpgnn_amd import _lib
+    from mpgnn_amd.plan import plan_cache
+    g = data.config_graph("fb15k237")
+    R = g.num_relations
+    gen = torch.Generator().manual_seed(6)
+    W = torch.rand((R, 128, 128) if mode == MODE_ALL else (128, 128), generator=gen) - 0.5
+    root, bias = torch.rand(128, 128, generator=gen) - 0.5, torch.rand(128, generator=gen) - 0.5
+    gout = torch.randn(g.num_nodes, 128, generator=gen).to(DEV)
+
+    def run():
+        plan = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, g.num_nodes)
+        xg = g.x.to(DEV).requires_grad_(True)
+        ps = [t.to(DEV).requires_grad_(True) for t in (W, root, bias)]
+        out = rgcn_conv(xg, *ps, plan, mode, relation=3, num_relations=R)
+        out.backward(gout)
+        return [t.grad.clone() for t in [xg] + ps]
+
+    ref = run()
+    try:
+        for opts in [{22: 32}, {22: 8}, {21: 0}, {21: 0, 22: 32}]:
+            for k, v in opts.items():
+                _lib.check(_lib.lib.mpgnn_set_option(k, v))
+            got = run()
+            for a, b in zip(got, ref):
+                assert torch.equal(a, b), opts
+            _lib.check(_lib.lib.mpgnn_set_option(21, 1))
+            _lib.check(_lib.lib.mpgnn_set_option(22, 16))
+        for rows in (64, 512):
+            _lib.check(_lib.lib.mpgnn_set_option(20, rows))
+            plan_cache.clear()
+            got = run()
+            for a, b in zip(got, ref):
+                torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
+    finally:
+        _lib.lib.mpgnn_set_option(20, 192)
+        _lib.lib.mpgnn_set_option(21, 1)
+        _lib.lib.mpgnn_set_option(22, 16)
+
+
 @pytest.mark.parametrize("name,mode,rel", [("C1", MODE_ALL, -1), ("C1", MODE_SINGLE, 1), ("fb15k237", MODE_ALL, -1),
                                            ("fb15k237", MODE_SINGLE, 3), ("fb15k237", MODE_SINGLE, 10_000)])
 def test_segment_means_backward_vs_oracle(name, mode, rel):
@@ -914,3 +958,21 @@ def test_squeeze_edge_cases_match_reference(n, f_out, root_weight):
         out = conv(0, 1, x.to(DEV), ei.to(DEV), et.to(DEV))
         assert out.shape == ref.shape
         rel_close(out, ref, what="squeezed output")
+
+
+@pytest.mark.parametrize("n,offset", [(14541 * 128, 0), (1001, 0), (1003, 1), (3, 0), (0, 0)])
+def test_relu_bwd_matches_threshold_backward(n, offset):
+    """mpgnn_relu_bwd = torch's ReLU backward (threshold_backward: 0 where the output is not > 0,
+    even for inf / NaN gradients), bit-exact, on aligned (float4) and misaligned (scalar) buffers."""
+    from mpgnn_amd import _lib
+    gen = torch.Generator().manual_seed(7)
+    g = torch.randn(n + offset, generator=gen)
+    y = torch.relu(torch.randn(n + offset, generator=gen))
+    if n > 8:
+        g[:4] = torch.tensor([float("nan"), float("inf"), -float("inf"), float("nan")])
+    g, y = g.to(DEV)[offset:], y.to(DEV)[offset:]
+    d = torch.full((n + offset,), 7.0, device=DEV)[offset:]
+    _lib.check(_lib.lib.mpgnn_relu_bwd(g.data_ptr(), y.data_ptr(), n, d.data_ptr(), None), "mpgnn_relu_bwd")
+    torch.cuda.synchronize()
+    ref = torch.ops.aten.threshold_backward(g, y, 0.0)
+    assert torch.equal(torch.nan_to_num(d, nan=123.0), torch.nan_to_num(ref, nan=123.0))
