@@ -251,8 +251,11 @@ enum mpgnn_option {
                                    created afterwards; same results up to fp32 summation order of the slabs */
     MPGNN_OPT_OUTER_ROOT_FIRST = 21, /* backward, merged outer-product launch: 1 (default) = root / bias chunks take
                                    the first workgroups, 0 = the weight-gradient chunks do; same results */
-    MPGNN_OPT_OUTER_SLICE = 22  /* backward, merged outer-product launch: rows per LDS slice, 16 (default: 36 KB
+    MPGNN_OPT_OUTER_SLICE = 22, /* backward, merged outer-product launch: rows per LDS slice, 16 (default: 36 KB
                                    of LDS per workgroup, four workgroups per CU), 32 (72 KB, two) or 8; same results */
+    MPGNN_OPT_DGRAD_IDX_AHEAD = 23 /* dgrad rel_gemm_kernel: 1 (default) = the gathered row numbers of an item are
+                                   loaded one item before its rows (one dependent round trip per item instead
+                                   of two); 0 = together; same results */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

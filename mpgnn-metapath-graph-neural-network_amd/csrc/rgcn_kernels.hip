@@ -1056,6 +1056,7 @@ struct RelGemmArgs {
     int stagger;                 // s_sleep quanta (64 clk) the second half of the grid waits first
     int* queue;                  // nullable: per-group item counters (dynamic schedule), zero between launches
     int deep;                    // 1: A rows fetched two items ahead (run_deep)
+    int idx_ahead;               // dgrad: gathered row numbers loaded one item ahead of the rows (run)
     unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][32] s_memtime timeline, or nullptr
 };
 
@@ -1145,6 +1146,28 @@ struct RelGemm {
             v[j] = *reinterpret_cast<const float4*>(base + (size_t)row[j] * K + ((tid + j * kThreads) % W4) * 4);
     }
 
+    // dgrad, split in two: the gathered row numbers (s_row) and scale (s_cnt) of an item, loaded
+    // one item earlier than its rows, so issuing the rows costs one round trip, not two
+    __device__ static __forceinline__ void gather_idx(const RelGemmArgs& a, const Item& it, int tid, int (&row)[WPT],
+                                                      int& cnt) {
+        constexpr int W4 = K / 4;
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) row[j] = it.r0 + min((tid + j * kThreads) / W4, it.nrows - 1);
+        cnt = 1;
+        if (!it.root) {
+            cnt = a.s_cnt[it.r0 + min(tid & 31, it.nrows - 1)];
+#pragma unroll
+            for (int j = 0; j < WPT; ++j) row[j] = a.s_row[row[j]];
+        }
+    }
+    __device__ static __forceinline__ void issue_rows(const RelGemmArgs& a, int tid, const int (&row)[WPT],
+                                                      float4 (&v)[WPT]) {
+        constexpr int W4 = K / 4;
+#pragma unroll
+        for (int j = 0; j < WPT; ++j)
+            v[j] = *reinterpret_cast<const float4*>(a.Aroot + (size_t)row[j] * K + ((tid + j * kThreads) % W4) * 4);
+    }
+
     __device__ static __forceinline__ void commit(const Item& it, int tid, const float4 (&v)[WPT], int cnt, float* A,
                                                   float* sc) {
         constexpr int W4 = K / 4;
@@ -1155,7 +1178,9 @@ struct RelGemm {
             *reinterpret_cast<float4*>(A + r * lda + (e % W4) * 4) =
                 r < it.nrows ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        if (tid < 32) sc[tid] = (float)cnt;
+        // the dgrad row scale as a reciprocal (one IEEE division per row and item here, a multiply
+        // per output in the epilogue instead of a 10-instruction division: ≤ 1.5 ulp apart)
+        if (tid < 32) sc[tid] = 1.0f / (float)cnt;
     }
 
     // this wave's K × 32 weight slice: lane-half h holds k = h·KH + j, column 32·wave + c
@@ -1215,6 +1240,11 @@ struct RelGemm {
         auto get_item = [&](int i) { return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i); };
         Item cur = get_item(i_beg);
         issue(a, cur, tid, v, cnt);
+        int nrow[DGRAD ? WPT : 1];  // dgrad: gathered rows + scale of the item after the current one
+        int ncnt = 1;
+        if constexpr (DGRAD) {
+            if (a.idx_ahead && i_beg + 1 < i_end) gather_idx(a, get_item(i_beg + 1), tid, nrow, ncnt);
+        }
         float b[KH];
         load_b(cur.w, wave, lane, b);
         commit(cur, tid, v, cnt, As, Sc);
@@ -1230,7 +1260,19 @@ struct RelGemm {
         for (int i = i_beg; i < i_end; ++i) {
             const bool has_next = i + 1 < i_end;
             const Item nxt = has_next ? get_item(i + 1) : cur;
-            if (has_next) issue(a, nxt, tid, v, cnt);      // in flight during this item's MFMAs
+            if (has_next) {  // in flight during this item's MFMAs
+                if constexpr (DGRAD) {
+                    if (a.idx_ahead) {
+                        issue_rows(a, tid, nrow, v);
+                        cnt = ncnt;
+                        if (i + 2 < i_end) gather_idx(a, get_item(i + 2), tid, nrow, ncnt);
+                    } else {
+                        issue(a, nxt, tid, v, cnt);
+                    }
+                } else {
+                    issue(a, nxt, tid, v, cnt);
+                }
+            }
             const bool new_w = nxt.w != cur.w;
             float bn[kPrefetchB ? KH : 1];
             if constexpr (kPrefetchB) {
@@ -1260,7 +1302,7 @@ struct RelGemm {
                 if (row < cur.nrows) {
                     float o = acc[r];
                     if constexpr (DGRAD) {
-                        if (!cur.root) o = o / sc[row];
+                        if (!cur.root) o = o * sc[row];
                     }
                     Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
                 }
@@ -1346,7 +1388,7 @@ struct RelGemm {
                 if (row < cur.nrows) {
                     float o = acc[r];
                     if constexpr (DGRAD) {
-                        if (!cur.root) o = o / sc[row];
+                        if (!cur.root) o = o * sc[row];
                     }
                     Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
                 }
@@ -1441,7 +1483,7 @@ struct RelGemm {
                         if (row < cur.nrows) {
                             float o = acc[r];
                             if constexpr (DGRAD) {
-                                if (!cur.root) o = o / sc[row];
+                                if (!cur.root) o = o * sc[row];
                             }
                             Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
                         }
@@ -1617,7 +1659,7 @@ struct RelGemm {
                     if (row < cur.nrows) {
                         float o = acc[r];
                         if constexpr (DGRAD) {
-                            if (!cur.root) o = o / sc[row];
+                            if (!cur.root) o = o * sc[row];
                         }
                         Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
                     }
@@ -3302,6 +3344,7 @@ static bool g_rel_wide = true;  // MPGNN_OPT_REL_WIDE: B-stationary GEMM also fo
 static bool g_rel_pingpong = false;  // MPGNN_OPT_REL_PINGPONG: two wave groups alternating MFMA / memory phases
 static bool g_rel_direct = false; // MPGNN_OPT_REL_DIRECT: LDS-free rel_gemm (waves load their own A fragments)
 static bool g_rel_deep = false;   // MPGNN_OPT_REL_DEEP: rel_gemm A rows two items ahead
+static bool g_dgrad_idx_ahead = true;   // MPGNN_OPT_DGRAD_IDX_AHEAD: dgrad rel_gemm loads gathered row numbers one item early
 static int g_outer_slice = 16;          // MPGNN_OPT_OUTER_SLICE: rows per LDS slice of the merged outer launch (32 or 16)
 static bool g_outer_root_first = true;  // MPGNN_OPT_OUTER_ROOT_FIRST: root / bias chunks dispatched before the dW chunks
 static bool g_merge_grad = true;  // MPGNN_OPT_MERGE_GRAD: dW + droot/dbias in one outer launch, one reduce launch
@@ -3603,6 +3646,7 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         r.stagger = g_rel_stagger;
         r.queue = (g_rel_queue && !g_stamps) ? rel_queue(strm) : nullptr;
         r.deep = g_stamps ? 0 : (g_rel_pingpong ? 3 : (g_rel_direct ? 2 : (g_rel_deep ? 1 : 0)));
+        r.idx_ahead = g_dgrad_idx_ahead ? 1 : 0;
         if (K == 256) {  // the wide kernel runs the default schedule only
             r.deep = 0;
             r.queue = nullptr;
@@ -4084,6 +4128,10 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
     }
     if (option == MPGNN_OPT_REL_QUEUE) {
         g_rel_queue = value != 0;
+        return MPGNN_OK;
+    }
+    if (option == MPGNN_OPT_DGRAD_IDX_AHEAD) {
+        g_dgrad_idx_ahead = value != 0;
         return MPGNN_OK;
     }
     if (option == MPGNN_OPT_OUTER_SLICE) {

@@ -2,7 +2,8 @@
 """A/B backward options on the bench's train step (3-layer RGCN forward + backward, FB15K
 shape): ms per fwd+bwd and per-kernel µs per launch (C-ABI timing hook), and the largest
 gradient difference against the first setting. Each argument is option=value[,option=value]
-(20 = MPGNN_OPT_CHUNK_ROWS, 21 = MPGNN_OPT_OUTER_ROOT_FIRST, 22 = MPGNN_OPT_OUTER_SLICE); the plan is rebuilt per setting
+(20 = MPGNN_OPT_CHUNK_ROWS, 21 = MPGNN_OPT_OUTER_ROOT_FIRST, 22 = MPGNN_OPT_OUTER_SLICE,
+23 = MPGNN_OPT_DGRAD_IDX_AHEAD); the plan is rebuilt per setting
 (relation chunks are laid out at plan build); every setting starts from the defaults.
 
   python scripts/chunk_ab.py 20=128 20=256 20=256,21=0
@@ -21,7 +22,7 @@ from mpgnn_amd.plan import plan_cache  # noqa: E402
 
 g = data.config_graph(sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "fb15k237")
 specs = [a for a in sys.argv[1:] if "=" in a] or ["20=128", "20=256"]
-DEFAULTS = {20: 192, 21: 1, 22: 16}
+DEFAULTS = {20: 192, 21: 1, 22: 16, 23: 1}
 torch.manual_seed(10)
 net = mpgnn_amd.Net(128, 128, g.num_relations, 128, 2, 3).cuda()
 x, ei, et = g.x.cuda(), g.edge_index.cuda(), g.edge_type.cuda()

@@ -808,7 +808,8 @@ def test_merged_gradient_launches_bitwise_equal(mode):
 
 @pytest.mark.parametrize("mode", [MODE_SINGLE, MODE_ALL])
 def test_outer_slice_and_dispatch_order_bitwise_equal(mode):
-    """MPGNN_OPT_OUTER_SLICE (8 / 16 / 32 rows per LDS slice) and MPGNN_OPT_OUTER_ROOT_FIRST only
+    """MPGNN_OPT_OUTER_SLICE (8 / 16 / 32 rows per LDS slice), MPGNN_OPT_OUTER_ROOT_FIRST and
+    MPGNN_OPT_DGRAD_IDX_AHEAD only
     change staging and workgroup order, not the row order of any MFMA accumulation chain: every
     gradient keeps its bits. MPGNN_OPT_CHUNK_ROWS moves slab boundaries (fp32 order): 1e-4."""
     from mpgnn_amd import _lib
@@ -830,7 +831,7 @@ def test_outer_slice_and_dispatch_order_bitwise_equal(mode):
 
     ref = run()
     try:
-        for opts in [{22: 32}, {22: 8}, {21: 0}, {21: 0, 22: 32}]:
+        for opts in [{22: 32}, {22: 8}, {21: 0}, {21: 0, 22: 32}, {23: 0}]:
             for k, v in opts.items():
                 _lib.check(_lib.lib.mpgnn_set_option(k, v))
             got = run()
@@ -838,6 +839,7 @@ def test_outer_slice_and_dispatch_order_bitwise_equal(mode):
                 assert torch.equal(a, b), opts
             _lib.check(_lib.lib.mpgnn_set_option(21, 1))
             _lib.check(_lib.lib.mpgnn_set_option(22, 16))
+            _lib.check(_lib.lib.mpgnn_set_option(23, 1))
         for rows in (64, 512):
             _lib.check(_lib.lib.mpgnn_set_option(20, rows))
             plan_cache.clear()
@@ -848,6 +850,7 @@ def test_outer_slice_and_dispatch_order_bitwise_equal(mode):
         _lib.lib.mpgnn_set_option(20, 192)
         _lib.lib.mpgnn_set_option(21, 1)
         _lib.lib.mpgnn_set_option(22, 16)
+        _lib.lib.mpgnn_set_option(23, 1)
 
 
 @pytest.mark.parametrize("name,mode,rel", [("C1", MODE_ALL, -1), ("C1", MODE_SINGLE, 1), ("fb15k237", MODE_ALL, -1),
