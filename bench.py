@@ -304,12 +304,13 @@ def main():
     opt = mpgnn_amd.main._adam(net)  # Adam(lr 0.01, wd 5e-4), fused multi-tensor kernel on the GPU
     y = torch.randint(0, 2, (g.num_nodes,), generator=torch.Generator().manual_seed(0)).to(dev)
     train_idx = torch.arange(0, g.num_nodes, 3, device=dev)
+    train_y = y[train_idx]  # data.train_y of the reference loop: fixed labels, indexed once
 
     def epoch():
         net.train()
         opt.zero_grad()
         out = net(x, ei, et, shard=shard, group=group, shard_side="rows")
-        loss = torch.nn.functional.nll_loss(out[train_idx], y[train_idx])
+        loss = torch.nn.functional.nll_loss(out.index_select(0, train_idx), train_y)
         loss.backward()
         opt.step()
         net.eval()
@@ -340,7 +341,7 @@ def main():
             def epoch_g():
                 netg.train()
                 out = netg(x, ei, et)
-                loss = torch.nn.functional.nll_loss(out[train_idx], y[train_idx])
+                loss = torch.nn.functional.nll_loss(out.index_select(0, train_idx), train_y)
                 loss.backward()
                 optg.step()
                 netg.eval()

@@ -104,6 +104,15 @@ def _num_classes(out: torch.Tensor) -> int:
     return int(out.shape[1]) if out.dim() > 1 else 1
 
 
+def take_rows(out: torch.Tensor, idx):
+    """``out[idx]`` (main.py:1062, main_rgcn.py:380). For a 1-D integer index tensor (the loaders'
+    train_idx: unique rows) this is ``index_select``: the same rows, and its backward is one
+    index_add instead of advanced indexing's sort-based accumulate (~8 launches per epoch)."""
+    if torch.is_tensor(idx) and idx.dim() == 1 and idx.dtype in (torch.int64, torch.int32):
+        return out.index_select(0, idx.to(out.device))
+    return out[idx]
+
+
 def mpgnn_train(model, optimizer, data):
     """main.py:1055-1082: full-batch forward, unweighted NLL on train_idx, backward, step.
     Returns (float loss, balanced class weights) like the reference (the weights are
@@ -112,7 +121,7 @@ def mpgnn_train(model, optimizer, data):
     optimizer.zero_grad()
     out = model(data.x, data.edge_index, data.edge_type)
     weights = class_weight_balanced(data.train_y)
-    loss = F.nll_loss(out[data.train_idx].squeeze(-1), data.train_y)
+    loss = F.nll_loss(take_rows(out, data.train_idx).squeeze(-1), data.train_y)
     loss.backward()
     optimizer.step()
     return float(loss.detach()), weights

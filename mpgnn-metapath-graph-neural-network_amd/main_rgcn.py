@@ -13,7 +13,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from .main import _adam, Data, get_edge_index_and_type_no_reverse, get_node_features, load_files, load_graph  # noqa: F401
+from .main import _adam, Data, get_edge_index_and_type_no_reverse, get_node_features, load_files, load_graph, take_rows  # noqa: F401
 from .metrics import class_weight_balanced, f1_macro_many
 from .model import Net
 
@@ -35,7 +35,7 @@ def mpgnn_train(model, optimizer, data):
     out = _forward(model, data)
     weights = class_weight_balanced(data.train_y)
     weights_tensor = torch.tensor(weights, dtype=torch.float, device=out.device)
-    loss = F.nll_loss(out[data.train_idx].squeeze(-1), data.train_y, weight=weights_tensor)
+    loss = F.nll_loss(take_rows(out, data.train_idx).squeeze(-1), data.train_y, weight=weights_tensor)
     loss.backward()
     optimizer.step()
     return float(loss.detach()), weights
