@@ -3202,6 +3202,68 @@ __global__ __launch_bounds__(kThreads) void relu_bwd_kernel(const float* g, cons
     for (int64_t k = i; k < n; k += stride) d[k] = y[k] > 0.0f ? g[k] : 0.0f;
 }
 
+// Linear-layer weight / bias gradient with K = N rows (the wrappers' heads: model.py:147,
+// :224-226): gw[o][f] = Σ_i g[i][o]·x[i][f], gb[o] = Σ_i g[i][o]. Stage 1: workgroup p sums
+// its row slice into partial P[p][o][0..F] (column F = the bias); thread t owns column
+// f = t % F and outputs o ≡ t / F (mod 256 / F) — the g loads are wave-uniform. Stage 2 sums
+// the partials in slice order (deterministic, no atomics).
+constexpr int kLinAcc = 32;  // outputs per thread (O ≤ kLinAcc · 256 / F)
+__global__ __launch_bounds__(kThreads) void linear_wgrad_part_kernel(const float* __restrict__ x,
+                                                                     const float* __restrict__ g, int N, int F, int O,
+                                                                     int rows, float* __restrict__ P) {
+    const int tid = threadIdx.x;
+    const int G = kThreads / F;
+    const int f = tid % F, grp = tid / F;
+    if (grp >= G) return;
+    const int r0 = (int)blockIdx.x * rows, r1 = min(N, r0 + rows);
+    float acc[kLinAcc], bacc[kLinAcc];
+#pragma unroll
+    for (int k = 0; k < kLinAcc; ++k) acc[k] = bacc[k] = 0.0f;
+    for (int i = r0; i < r1; ++i) {
+        const float xv = x[(size_t)i * F + f];
+        const float* gr = g + (size_t)i * O;
+#pragma unroll
+        for (int k = 0; k < kLinAcc; ++k) {
+            const int o = grp + k * G;
+            if (o < O) {
+                const float gv = gr[o];
+                acc[k] = __builtin_fmaf(gv, xv, acc[k]);
+                bacc[k] += gv;
+            }
+        }
+    }
+    float* Pp = P + (size_t)blockIdx.x * O * (F + 1);
+#pragma unroll
+    for (int k = 0; k < kLinAcc; ++k) {
+        const int o = grp + k * G;
+        if (o < O) {
+            Pp[(size_t)o * (F + 1) + f] = acc[k];
+            if (f == 0) Pp[(size_t)o * (F + 1) + F] = bacc[k];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void linear_wgrad_sum_kernel(const float* __restrict__ P, int parts, int F, int O,
+                                                                    float* __restrict__ gw, float* __restrict__ gb) {
+    const int e = (int)blockIdx.x * kThreads + threadIdx.x;
+    const int elems = O * (F + 1);
+    if (e >= elems) return;
+    const int o = e / (F + 1), f = e % (F + 1);
+    if (f == F && gb == nullptr) return;
+    constexpr int kB = 16;
+    float s = 0.0f;
+    for (int pb = 0; pb < parts; pb += kB) {
+        float v[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) v[u] = P[(size_t)min(pb + u, parts - 1) * elems + e];
+#pragma unroll
+        for (int u = 0; u < kB; ++u)
+            if (pb + u < parts) s += v[u];
+    }
+    if (f == F) gb[o] = s;
+    else gw[(size_t)o * F + f] = s;
+}
+
 // G[s] = dh[s] / cnt[sel_b + s] for the segment rows of a selection (segment-means backward)
 __global__ __launch_bounds__(kThreads) void scale_rows_kernel(const float* dh, const int* cnt, int sel_b, int rows,
                                                               int F, float* G) {
@@ -4094,6 +4156,40 @@ int32_t mpgnn_relu_bwd(const float* grad_out, const float* act_out, int64_t n, f
     const int blocks = (int)std::min<int64_t>((units + kThreads - 1) / kThreads, 8192);
     hipLaunchKernelGGL(relu_bwd_kernel, dim3(blocks), dim3(kThreads), 0, strm, grad_out, act_out, n, dst, vec ? 1 : 0);
     return hip_check(hipGetLastError(), "relu_bwd_kernel launch");
+}
+
+static int linear_parts(int64_t N) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, (N + 31) / 32)); }
+
+int32_t mpgnn_linear_wgrad_workspace_bytes(int64_t N, int32_t F, int32_t O, int64_t* bytes) {
+    if (!bytes) return arg_error("NULL bytes");
+    if (N < 0 || F <= 0 || O <= 0) return arg_error("bad N, F or O");
+    *bytes = (int64_t)linear_parts(N) * O * (F + 1) * (int64_t)sizeof(float);
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int32_t F, int32_t O, float* grad_weight,
+                           float* grad_bias, void* workspace, void* stream) {
+    if (N < 0 || F <= 0 || O <= 0) return arg_error("bad N, F or O");
+    if (F > kThreads || (int64_t)O > (int64_t)kLinAcc * (kThreads / F))
+        return arg_error("mpgnn_linear_wgrad: needs F <= 256 and O <= 32 * (256 / F)");
+    if (N > INT32_MAX) return arg_error("N too large");
+    if (!grad_weight || !workspace || (N > 0 && (!x || !grad_out))) return arg_error("NULL pointer");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    const int parts = linear_parts(N);
+    const int rows = (int)((N + parts - 1) / parts);
+    float* P = static_cast<float*>(workspace);
+    if (N == 0) {
+        int32_t st = hip_check(hipMemsetAsync(grad_weight, 0, (size_t)O * F * sizeof(float), strm), "memset");
+        if (st == MPGNN_OK && grad_bias) st = hip_check(hipMemsetAsync(grad_bias, 0, (size_t)O * sizeof(float), strm), "memset");
+        return st;
+    }
+    hipLaunchKernelGGL(linear_wgrad_part_kernel, dim3(parts), dim3(kThreads), 0, strm, x, grad_out, (int)N, F, O, rows, P);
+    int32_t st = hip_check(hipGetLastError(), "linear_wgrad_part_kernel launch");
+    if (st != MPGNN_OK) return st;
+    const int elems = O * (F + 1);
+    hipLaunchKernelGGL(linear_wgrad_sum_kernel, dim3((elems + kThreads - 1) / kThreads), dim3(kThreads), 0, strm, P, parts,
+                       F, O, grad_weight, grad_bias);
+    return hip_check(hipGetLastError(), "linear_wgrad_sum_kernel launch");
 }
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {

@@ -10,6 +10,8 @@ The score-function classes (model.py:12-125) are outside the hot path (SURVEY §
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -28,7 +30,9 @@ class _SplitKLinear(torch.autograd.Function):
     with K = N, which the BLAS library tiles into a handful of long serial-K workgroups (66 µs
     for O = 2 at C3, 6 % of the epoch). Here K is cut into slices of ≤ 1024 rows: one batched
     GEMM over the slices + a sum over them — the same products in fp32, summed in a different
-    (blocked) order. Forward and grad_input are exactly the autograd ones (``F.linear``, ``mm``)."""
+    (blocked) order; for the heads' shapes (F ≤ 256, O ≤ 32·256/F) the C ABI's
+    ``mpgnn_linear_wgrad`` does it in two launches, bias gradient included. Forward and
+    grad_input are exactly the autograd ones (``F.linear``, ``mm``)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -42,6 +46,24 @@ class _SplitKLinear(torch.autograd.Function):
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = g.mm(weight)
+        f, o = x.shape[1], g.shape[1]
+        if ctx.needs_input_grad[1] and f <= 256 and o <= 32 * (256 // f) and x.dtype == g.dtype == torch.float32:
+            # one HIP kernel pair (row-sliced partials + ordered slice sum, bias in the same pass)
+            # instead of pad + batched GEMM + two reductions (~8 launches)
+            from . import _lib
+            from .functional import _stream, _workspace
+            xc, gc = x.contiguous(), g.contiguous()
+            nbytes = ctypes.c_int64()
+            _lib.check(_lib.lib.mpgnn_linear_wgrad_workspace_bytes(xc.shape[0], f, o, ctypes.byref(nbytes)),
+                       "mpgnn_linear_wgrad_workspace_bytes")
+            ws = _workspace(int(nbytes.value), x.device)
+            gw = torch.empty(o, f, dtype=torch.float32, device=x.device)
+            want_b = ctx.has_bias and ctx.needs_input_grad[2]
+            gb = torch.empty(o, dtype=torch.float32, device=x.device) if want_b else None
+            _lib.check(_lib.lib.mpgnn_linear_wgrad(xc.data_ptr(), gc.data_ptr(), xc.shape[0], f, o, gw.data_ptr(),
+                                                   gb.data_ptr() if want_b else None, ws.data_ptr(), _stream(x)),
+                       "mpgnn_linear_wgrad")
+            return gx, gw, gb
         if ctx.needs_input_grad[1]:
             n = x.shape[0]
             slices = max(1, min(256, (n + 1023) // 1024))

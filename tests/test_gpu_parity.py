@@ -979,3 +979,27 @@ def test_relu_bwd_matches_threshold_backward(n, offset):
     torch.cuda.synchronize()
     ref = torch.ops.aten.threshold_backward(g, y, 0.0)
     assert torch.equal(torch.nan_to_num(d, nan=123.0), torch.nan_to_num(ref, nan=123.0))
+
+
+@pytest.mark.parametrize("n,f,o,bias", [(14541, 128, 2, True), (1000, 128, 64, True), (5, 256, 32, False),
+                                        (3000, 64, 128, True), (700, 512, 4, True)])
+def test_linear_head_gradients_vs_autograd(n, f, o, bias):
+    """model.linear (the wrappers' heads, model.py:147 / :224-226): forward and all gradients vs
+    plain autograd of F.linear, 1e-4 — the C-ABI mpgnn_linear_wgrad path (F <= 256) and the
+    sliced-GEMM fallback (F = 512)."""
+    from mpgnn_amd.model import linear
+    gen = torch.Generator().manual_seed(11)
+    layer = torch.nn.Linear(f, o, bias=bias).to(DEV)
+    x = torch.randn(n, f, generator=gen).to(DEV).requires_grad_(True)
+    go = torch.randn(n, o, generator=gen).to(DEV)
+    out = linear(layer, x)
+    out.backward(go)
+    got = [x.grad.clone(), layer.weight.grad.clone()] + ([layer.bias.grad.clone()] if bias else [])
+    x.grad = None
+    layer.zero_grad(set_to_none=True)
+    ref_out = torch.nn.functional.linear(x, layer.weight, layer.bias)
+    ref_out.backward(go)
+    ref = [x.grad, layer.weight.grad] + ([layer.bias.grad] if bias else [])
+    torch.testing.assert_close(out, ref_out, rtol=1e-4, atol=1e-4)
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * max(1.0, float(b.abs().max())))
