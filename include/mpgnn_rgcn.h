@@ -161,7 +161,7 @@ int32_t mpgnn_relu_bwd(const float* grad_out, const float* act_out, int64_t n, f
 
 /* Weight / bias gradient of the wrappers' Linear heads over all N node rows (Net.lin,
  * model.py:147; MPNetm.fc1/fc2, model.py:224-226): grad_weight[o][f] = Σ_i grad_out[i][o]·x[i][f],
- * grad_bias[o] = Σ_i grad_out[i][o] (nullable), row-sliced partials summed in slice order
+ * grad_bias[o] = Σ_i grad_out[i][o] (nullable), row-sliced partials summed in a fixed order
  * (deterministic). x [N,F], grad_out [N,O], grad_weight [O,F] row-major fp32; F <= 256 and
  * O <= 32·(256/F). Scratch: mpgnn_linear_wgrad_workspace_bytes. Replaces autograd's
  * grad_outᵀ @ x of F.linear (a serial-K library GEMM at K = N). */

@@ -1518,7 +1518,7 @@ struct RelGemm {
             base = a.Aroot;
         } else if constexpr (DGRAD) {
             base = a.Aroot;
-            inv = (float)a.s_cnt[row];
+            inv = 1.0f / (float)a.s_cnt[row];  // reciprocal, as RelGemm::commit stores it
             row = a.s_row[row];
         } else {
             base = a.Arel;
@@ -1573,7 +1573,7 @@ struct RelGemm {
                 float o = acc[r];
                 if constexpr (DGRAD) {
                     const float d = __shfl(invh, row);
-                    if (!cur.root) o = o / d;
+                    if (!cur.root) o = o * d;
                 }
                 if (row < cur.nrows) Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
             }
@@ -3206,8 +3206,10 @@ __global__ __launch_bounds__(kThreads) void relu_bwd_kernel(const float* g, cons
 // :224-226): gw[o][f] = Σ_i g[i][o]·x[i][f], gb[o] = Σ_i g[i][o]. Stage 1: workgroup p sums
 // its row slice into partial P[p][o][0..F] (column F = the bias); thread t owns column
 // f = t % F and outputs o ≡ t / F (mod 256 / F) — the g loads are wave-uniform. Stage 2 sums
-// the partials in slice order (deterministic, no atomics).
+// the partials in a fixed order (deterministic, no atomics).
 constexpr int kLinAcc = 32;  // outputs per thread (O ≤ kLinAcc · 256 / F)
+constexpr int kLinRows = 8;  // rows per load batch
+constexpr int kLinRowsPerPart = 64;
 __global__ __launch_bounds__(kThreads) void linear_wgrad_part_kernel(const float* __restrict__ x,
                                                                      const float* __restrict__ g, int N, int F, int O,
                                                                      int rows, float* __restrict__ P) {
@@ -3219,16 +3221,24 @@ __global__ __launch_bounds__(kThreads) void linear_wgrad_part_kernel(const float
     float acc[kLinAcc], bacc[kLinAcc];
 #pragma unroll
     for (int k = 0; k < kLinAcc; ++k) acc[k] = bacc[k] = 0.0f;
-    for (int i = r0; i < r1; ++i) {
-        const float xv = x[(size_t)i * F + f];
-        const float* gr = g + (size_t)i * O;
+    // rows in batches of kLinRows: the batch's loads are issued together (one round trip per
+    // batch, not per row), then added in row order
+    for (int i0 = r0; i0 < r1; i0 += kLinRows) {
+        float xv[kLinRows];
+#pragma unroll
+        for (int u = 0; u < kLinRows; ++u) xv[u] = x[(size_t)min(i0 + u, r1 - 1) * F + f];
 #pragma unroll
         for (int k = 0; k < kLinAcc; ++k) {
             const int o = grp + k * G;
             if (o < O) {
-                const float gv = gr[o];
-                acc[k] = __builtin_fmaf(gv, xv, acc[k]);
-                bacc[k] += gv;
+                float gv[kLinRows];
+#pragma unroll
+                for (int u = 0; u < kLinRows; ++u) gv[u] = i0 + u < r1 ? g[(size_t)(i0 + u) * O + o] : 0.0f;
+#pragma unroll
+                for (int u = 0; u < kLinRows; ++u) {
+                    acc[k] = __builtin_fmaf(gv[u], xv[u], acc[k]);
+                    bacc[k] += gv[u];
+                }
             }
         }
     }
@@ -3245,23 +3255,22 @@ __global__ __launch_bounds__(kThreads) void linear_wgrad_part_kernel(const float
 
 __global__ __launch_bounds__(kThreads) void linear_wgrad_sum_kernel(const float* __restrict__ P, int parts, int F, int O,
                                                                     float* __restrict__ gw, float* __restrict__ gb) {
-    const int e = (int)blockIdx.x * kThreads + threadIdx.x;
+    // one wave per element: lane l sums the partials p ≡ l (mod 64) in order, then the 64 lane
+    // sums are combined by a fixed butterfly (deterministic: the same order every launch)
+    const int e = (int)blockIdx.x * kWaves + (int)(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
     const int elems = O * (F + 1);
     if (e >= elems) return;
     const int o = e / (F + 1), f = e % (F + 1);
     if (f == F && gb == nullptr) return;
-    constexpr int kB = 16;
     float s = 0.0f;
-    for (int pb = 0; pb < parts; pb += kB) {
-        float v[kB];
+    for (int p = lane; p < parts; p += 64) s += P[(size_t)p * elems + e];
 #pragma unroll
-        for (int u = 0; u < kB; ++u) v[u] = P[(size_t)min(pb + u, parts - 1) * elems + e];
-#pragma unroll
-        for (int u = 0; u < kB; ++u)
-            if (pb + u < parts) s += v[u];
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+    if (lane == 0) {
+        if (f == F) gb[o] = s;
+        else gw[(size_t)o * F + f] = s;
     }
-    if (f == F) gb[o] = s;
-    else gw[(size_t)o * F + f] = s;
 }
 
 // G[s] = dh[s] / cnt[sel_b + s] for the segment rows of a selection (segment-means backward)
@@ -4158,7 +4167,9 @@ int32_t mpgnn_relu_bwd(const float* grad_out, const float* act_out, int64_t n, f
     return hip_check(hipGetLastError(), "relu_bwd_kernel launch");
 }
 
-static int linear_parts(int64_t N) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, (N + 31) / 32)); }
+static int linear_parts(int64_t N) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(4096, (N + kLinRowsPerPart - 1) / kLinRowsPerPart));
+}
 
 int32_t mpgnn_linear_wgrad_workspace_bytes(int64_t N, int32_t F, int32_t O, int64_t* bytes) {
     if (!bytes) return arg_error("NULL bytes");
@@ -4187,7 +4198,7 @@ int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int
     int32_t st = hip_check(hipGetLastError(), "linear_wgrad_part_kernel launch");
     if (st != MPGNN_OK) return st;
     const int elems = O * (F + 1);
-    hipLaunchKernelGGL(linear_wgrad_sum_kernel, dim3((elems + kThreads - 1) / kThreads), dim3(kThreads), 0, strm, P, parts,
+    hipLaunchKernelGGL(linear_wgrad_sum_kernel, dim3((elems + kWaves - 1) / kWaves), dim3(kThreads), 0, strm, P, parts,
                        F, O, grad_weight, grad_bias);
     return hip_check(hipGetLastError(), "linear_wgrad_sum_kernel launch");
 }
