@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="fb15k237", choices=["fb15k237", "C2", "C5"],
                     help="fb15k237 = C3/C4 (the headline); C2 / C5 = the other BASELINE.json configs")
+    ap.add_argument("--recipe", default="survey", choices=["survey", "relcond"],
+                    help="FB15K-237 edge recipe: survey = SURVEY §8d C3 (S ~ 208k, the headline); "
+                         "relcond = round-1 relation-conditional graph (S ~ 48k, lighter)")
     ap.add_argument("--layers", type=int, default=None, help="default 3 (C3, C5) / 2 (C2)")
     ap.add_argument("--feat", type=int, default=None, help="default 128 (C2, C3) / 256 (C5)")
     ap.add_argument("--epoch-steps", type=int, default=None, help="0 skips the epoch leg (default 10; 2 at C5)")
@@ -172,7 +175,7 @@ def main():
     rank, world, local, group = setup_dist(args.gpus)
     dev = torch.device("cuda", local)
     if args.workload == "fb15k237":
-        g = data.fb15k237_graph(feat_dim=args.feat, seed=0)
+        g = data.fb15k237_graph(feat_dim=args.feat, seed=0, recipe=args.recipe)
     else:
         g = data.config_graph(args.workload)
         if g.x.shape[1] != args.feat:

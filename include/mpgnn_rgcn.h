@@ -278,6 +278,13 @@ int32_t mpgnn_set_option(int32_t option, int64_t value);
  * order; MPGNN_ERR_ARG if the file does not hold exactly `rows` three-integer lines. */
 int32_t mpgnn_links_count(const char* path, int64_t* rows);
 int32_t mpgnn_links_parse(const char* path, int64_t* edge_index, int64_t* edge_type, int64_t rows);
+/* node.dat / label.dat (`id \t value …` numeric rows; the reference reads them with
+ * pandas.read_csv(sep='\t', header=None), main.py:140-147,176-182): mpgnn_tsv_shape returns the
+ * non-blank line count and the widest row's field count; mpgnn_tsv_parse_f64 fills a row-major
+ * float64 [rows, cols] matrix in file order, shorter rows padded with NaN (read_csv's fill);
+ * MPGNN_ERR_ARG on a non-numeric field, a row wider than cols or a row-count mismatch. */
+int32_t mpgnn_tsv_shape(const char* path, int64_t* rows, int64_t* cols);
+int32_t mpgnn_tsv_parse_f64(const char* path, double* out, int64_t rows, int64_t cols);
 
 /* --- kernel timing (bench / profiling) ----------------------------------------------
  * When enabled, every kernel launch of the entry points above is bracketed by a pair of

@@ -84,6 +84,8 @@ SIGNATURES = [
     ("mpgnn_timing_query", _I32, [_I32, ctypes.POINTER(ctypes.c_double), _PI64]),
     ("mpgnn_links_count", _I32, [ctypes.c_char_p, _PI64]),
     ("mpgnn_links_parse", _I32, [ctypes.c_char_p, _P, _P, _I64]),
+    ("mpgnn_tsv_shape", _I32, [ctypes.c_char_p, _PI64, _PI64]),
+    ("mpgnn_tsv_parse_f64", _I32, [ctypes.c_char_p, _P, _I64, _I64]),
 ]
 
 KERNEL_KINDS = {"seg_fwd": 0, "row_fwd": 1, "seg_dgrad": 2, "row_dx": 3, "outer": 4, "reduce": 5, "mean": 6,
@@ -92,11 +94,42 @@ OPT_EXACT_ORDER = 0
 ACT_NONE, ACT_RELU = 0, 1
 
 
+def _missing(name):
+    def fn(*_a, **_k):
+        raise RuntimeError(f"{name} is not in {LIB_PATH} (host-only sanitizer library)")
+    return fn
+
+
 def _load():
+    global LIB_PATH
+    override = os.environ.get("MPGNN_LIB_PATH")
+    if override:
+        # tests/test_host_sanitizers.py: the ASan/UBSan host-only build of plan.cpp + io.cpp
+        # (csrc/Makefile `asan`); symbols it does not export raise when called
+        LIB_PATH = os.path.abspath(override)
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                setattr(lib, name, _missing(name))
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        return lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `make -C csrc` or __graft_entry__.build(). "
             "mpgnn_amd has no CPU fallback.")
+    # a library shipped next to newer sources is stale: refuse it rather than run old kernels
+    # (MPGNN_ALLOW_STALE_LIB=1 skips the check; the sources are always present in-tree)
+    from . import _srchash
+    if os.environ.get("MPGNN_ALLOW_STALE_LIB") != "1" and _srchash.sources_present():
+        stamp = open(_srchash.STAMP).read().strip() if os.path.exists(_srchash.STAMP) else None
+        if stamp != _srchash.source_hash():
+            raise ImportError(
+                f"{LIB_PATH} was not built from the current sources (stamp {_srchash.STAMP} "
+                f"{'missing' if stamp is None else 'differs'}): rebuild with __graft_entry__.build().")
     lib = ctypes.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)

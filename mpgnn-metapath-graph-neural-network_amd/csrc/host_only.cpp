@@ -1,0 +1,19 @@
+// Host-only build of the plan builder and file readers (csrc/Makefile target `asan`): the
+// sanitizer library libmpgnn_host_asan.so links plan.cpp + io.cpp with this file instead of
+// the gfx950 kernels (ASan/UBSan host build). Only the plan-thread option exists
+// here; every other option is a kernel switch and reports MPGNN_ERR_UNSUPPORTED.
+#include "mpgnn_rgcn.h"
+#include "plan_internal.h"
+
+extern "C" int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    if (option == MPGNN_OPT_PLAN_THREADS) {
+        if (value < 0 || value > 256) {
+            mpgnn::set_last_error("MPGNN_OPT_PLAN_THREADS: must be 0..256");
+            return MPGNN_ERR_ARG;
+        }
+        mpgnn::g_plan_threads = (int)value;
+        return MPGNN_OK;
+    }
+    mpgnn::set_last_error("host-only library: kernel options are not available");
+    return MPGNN_ERR_UNSUPPORTED;
+}

@@ -4,6 +4,8 @@
 // edge_type = relation, file order kept). The reference goes through pandas.read_csv
 // (main.py:150-151) and Python lists; here the file is memory-mapped and parsed by a pool of
 // threads over newline-aligned byte ranges (count pass, prefix sum, fill pass).
+// node.dat / label.dat (main.py:140-147: `id \t value …` rows through pandas.read_csv) go
+// through the same machinery as a numeric matrix (mpgnn_tsv_shape / mpgnn_tsv_parse_f64).
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -11,6 +13,9 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <charconv>
+#include <cmath>
+#include <limits>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -112,6 +117,31 @@ inline bool parse_int(const char*& s, const char* e, int64_t& v) {
     return true;
 }
 
+// One numeric field (integer or decimal / exponent float, as pandas' C reader accepts them;
+// also "nan"/"inf" through from_chars). Advances s past the field.
+inline bool parse_double(const char*& s, const char* e, double& v) {
+    while (s < e && is_blank(*s)) ++s;
+    if (s >= e) return false;
+    const char* b = s;
+    if (*b == '+') ++b;  // from_chars rejects a leading '+'
+    auto r = std::from_chars(b, e, v, std::chars_format::general);
+    if (r.ec != std::errc() || r.ptr == b) return false;
+    s = r.ptr;
+    return s >= e || is_blank(*s);
+}
+
+// Number of fields of one line (whitespace separated), 0 for a blank line.
+inline int64_t count_fields(const char* b, const char* e) {
+    int64_t n = 0;
+    while (b < e) {
+        while (b < e && is_blank(*b)) ++b;
+        if (b >= e) break;
+        ++n;
+        while (b < e && !is_blank(*b)) ++b;
+    }
+    return n;
+}
+
 int parse_threads(size_t bytes) {
     unsigned hw = std::thread::hardware_concurrency();
     int t = (int)std::min<size_t>(hw ? std::min(hw, 16u) : 1u, bytes / (1u << 20) + 1);
@@ -201,6 +231,111 @@ int32_t mpgnn_links_parse(const char* path, int64_t* edge_index, int64_t* edge_t
         if (bad[t] >= 0) {
             mpgnn::set_last_error("mpgnn_links_parse: row " + std::to_string(bad[t]) +
                                   " is not three integer columns (node_1, relation, node_2)");
+            return MPGNN_ERR_ARG;
+        }
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_tsv_shape(const char* path, int64_t* rows, int64_t* cols) {
+    if (!rows || !cols) {
+        mpgnn::set_last_error("mpgnn_tsv_shape: rows / cols is null");
+        return MPGNN_ERR_ARG;
+    }
+    Mapped m;
+    int32_t st = map_file(path, m);
+    if (st != MPGNN_OK) return st;
+    const int parts = parse_threads(m.n);
+    std::vector<size_t> cut = split_lines(m, parts);
+    std::vector<int64_t> cnt(parts, 0), width(parts, 0);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < parts; ++t)
+        pool.emplace_back([&, t] {
+            const char* b = m.p + cut[t];
+            const char* e = m.p + cut[t + 1];
+            while (b < e) {
+                const char* nl = (const char*)memchr(b, '\n', (size_t)(e - b));
+                const char* le = nl ? nl : e;
+                int64_t f = count_fields(b, le);
+                if (f > 0) {
+                    ++cnt[t];
+                    width[t] = std::max(width[t], f);
+                }
+                b = le + 1;
+            }
+        });
+    for (auto& th : pool) th.join();
+    int64_t r = 0, c = 0;
+    for (int t = 0; t < parts; ++t) {
+        r += cnt[t];
+        c = std::max(c, width[t]);
+    }
+    *rows = r;
+    *cols = c;
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_tsv_parse_f64(const char* path, double* out, int64_t rows, int64_t cols) {
+    if (rows < 0 || cols < 0 || (rows > 0 && cols > 0 && !out)) {
+        mpgnn::set_last_error("mpgnn_tsv_parse_f64: null output or negative shape");
+        return MPGNN_ERR_ARG;
+    }
+    Mapped m;
+    int32_t st = map_file(path, m);
+    if (st != MPGNN_OK) return st;
+    const int parts = parse_threads(m.n);
+    std::vector<size_t> cut = split_lines(m, parts);
+    std::vector<int64_t> cnt(parts, 0), first(parts + 1, 0);
+    {
+        std::vector<std::thread> pool;
+        for (int t = 0; t < parts; ++t)
+            pool.emplace_back([&, t] { cnt[t] = count_rows(m.p + cut[t], m.p + cut[t + 1]); });
+        for (auto& th : pool) th.join();
+    }
+    for (int t = 0; t < parts; ++t) first[t + 1] = first[t] + cnt[t];
+    if (first[parts] != rows) {
+        mpgnn::set_last_error("mpgnn_tsv_parse_f64: file has " + std::to_string(first[parts]) +
+                              " rows, caller passed " + std::to_string(rows));
+        return MPGNN_ERR_ARG;
+    }
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    std::vector<int64_t> bad(parts, -1);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < parts; ++t)
+        pool.emplace_back([&, t] {
+            const char* b = m.p + cut[t];
+            const char* e = m.p + cut[t + 1];
+            int64_t r = first[t];
+            while (b < e) {
+                const char* nl = (const char*)memchr(b, '\n', (size_t)(e - b));
+                const char* le = nl ? nl : e;
+                if (line_has_data(b, le)) {
+                    const char* s = b;
+                    double* row = out + r * cols;
+                    int64_t c = 0;
+                    for (; c < cols; ++c) {
+                        while (s < le && is_blank(*s)) ++s;
+                        if (s >= le) break;
+                        if (!parse_double(s, le, row[c])) {
+                            bad[t] = r;
+                            return;
+                        }
+                    }
+                    while (s < le && is_blank(*s)) ++s;
+                    if (s != le) {  // more fields than cols
+                        bad[t] = r;
+                        return;
+                    }
+                    for (; c < cols; ++c) row[c] = nan;  // ragged row: pandas fills NaN
+                    ++r;
+                }
+                b = le + 1;
+            }
+        });
+    for (auto& th : pool) th.join();
+    for (int t = 0; t < parts; ++t)
+        if (bad[t] >= 0) {
+            mpgnn::set_last_error("mpgnn_tsv_parse_f64: row " + std::to_string(bad[t]) +
+                                  " has a non-numeric field or more than " + std::to_string(cols) + " fields");
             return MPGNN_ERR_ARG;
         }
     return MPGNN_OK;

@@ -71,6 +71,12 @@ __device__ __forceinline__ void vstore(float* p, const float (&v)[V]) {
     }
 }
 
+// ReLU with torch's semantics (clamp_min(x, 0)): x < 0 → 0, NaN and -0.0 pass through, so a
+// diverging run still shows NaN (fmaxf(NaN, 0) would return 0).
+__device__ __forceinline__ float relu_f(float v) { return v < 0.0f ? 0.0f : v; }
+// threshold_backward(grad, result, 0): result <= 0 → 0, else grad (NaN results pass grad)
+__device__ __forceinline__ float relu_bwd_f(float g, float y) { return y <= 0.0f ? 0.0f : g; }
+
 __device__ __forceinline__ int readlane(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 
 // Uniform read of a plan table through the constant address space: an SMEM load (lgkmcnt), so
@@ -2471,7 +2477,7 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
                             for (int k = 0; k < V; ++k) {
                                 o[k] = div ? acc[t][k] / d : acc[t][k];
                                 if (addb) o[k] = o[k] + bb[t][k];
-                                if (!split && a.relu) o[k] = fmaxf(o[k], 0.0f);
+                                if (!split && a.relu) o[k] = relu_f(o[k]);
                             }
                             vstore<V>(dst + col, o);
                         }
@@ -2583,7 +2589,7 @@ __global__ __launch_bounds__(kThreads) void flat_rows_multi_kernel(FlatArgs a) {
                             for (int k = 0; k < V; ++k) {
                                 o[k] = div ? acc[t][k] / d : acc[t][k];
                                 if (addb) o[k] = o[k] + bb[t][k];
-                                if (!split && a.relu) o[k] = fmaxf(o[k], 0.0f);
+                                if (!split && a.relu) o[k] = relu_f(o[k]);
                             }
                             vstore<V>(dst + col, o);
                         }
@@ -2694,7 +2700,7 @@ __global__ __launch_bounds__(kThreads) void finalize_rows_kernel(FinalArgs a) {
                 o[q] = acc[t][q];
                 if (has_ex) o[q] = o[q] + ex[t][q];
                 if (has_b) o[q] = o[q] + bb[t][q];
-                if (a.relu) o[q] = fmaxf(o[q], 0.0f);
+                if (a.relu) o[q] = relu_f(o[q]);
             }
             vstore<V>(a.out + (size_t)(row - a.row_off) * F + col, o);
         }
@@ -3192,14 +3198,14 @@ __global__ __launch_bounds__(kThreads) void relu_bwd_kernel(const float* g, cons
         for (int64_t k = i; k < n4; k += stride) {
             const float4 gv = reinterpret_cast<const float4*>(g)[k];
             const float4 yv = reinterpret_cast<const float4*>(y)[k];
-            reinterpret_cast<float4*>(d)[k] = make_float4(yv.x > 0.0f ? gv.x : 0.0f, yv.y > 0.0f ? gv.y : 0.0f,
-                                                          yv.z > 0.0f ? gv.z : 0.0f, yv.w > 0.0f ? gv.w : 0.0f);
+            reinterpret_cast<float4*>(d)[k] = make_float4(relu_bwd_f(gv.x, yv.x), relu_bwd_f(gv.y, yv.y),
+                                                          relu_bwd_f(gv.z, yv.z), relu_bwd_f(gv.w, yv.w));
         }
         i += n4 * 4;
         if (i >= n) return;
         // tail: at most 3 elements, thread i handles element n4 * 4 + (its global id)
     }
-    for (int64_t k = i; k < n; k += stride) d[k] = y[k] > 0.0f ? g[k] : 0.0f;
+    for (int64_t k = i; k < n; k += stride) d[k] = relu_bwd_f(g[k], y[k]);
 }
 
 // Linear-layer weight / bias gradient with K = N rows (the wrappers' heads: model.py:147,
@@ -3935,7 +3941,7 @@ static void launch_final(const FinalArgs& a, int nrows, hipStream_t st) {
 // In-place ReLU for the paths whose combine has no fused activation (exact order, mode SINGLE).
 __global__ __launch_bounds__(kThreads) void relu_kernel(float* __restrict__ p, size_t n) {
     for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (size_t)gridDim.x * kThreads)
-        p[i] = fmaxf(p[i], 0.0f);
+        p[i] = relu_f(p[i]);
 }
 
 // Fast-path row sums over a flat chunked list: flat_rows_kernel over chunks [c_lo, c_hi), then

@@ -61,14 +61,20 @@ def load_files(node_file_path, link_file_path, label_file_path):
     return labels, features, links, [labels], tot_relation_types
 
 
-def get_node_features(colors):
-    """main.py:347-355: one-hot columns of the colour frame (``pd.get_dummies``, 'node'
-    dropped), columns reversed, float32."""
+def _one_hot_colours(colors) -> np.ndarray:
+    """``pd.get_dummies`` of the colour frame with the 'node' column dropped, float32
+    (main.py:348-352 ≡ main_rgcn.py:346-350)."""
     import pandas as pd
     node_features = pd.get_dummies(colors)
     node_features.drop(["node"], axis=1, inplace=True)
-    x = node_features.to_numpy().astype(np.float32)
-    return torch.from_numpy(np.flip(x, 1).copy())
+    return node_features.to_numpy().astype(np.float32)
+
+
+def get_node_features(colors):
+    """main.py:347-355: one-hot columns of the colour frame, float32, in ``get_dummies``
+    column order. The column flip is commented out in this file (main.py:353); only the
+    RGCN driver flips (``main_rgcn.get_node_features``, main_rgcn.py:351)."""
+    return torch.from_numpy(np.ascontiguousarray(_one_hot_colours(colors)))
 
 
 def get_edge_index_and_type_no_reverse(links):

@@ -2,7 +2,8 @@
 A11): ``mpgnn_train`` (class-balanced NLL) / ``mpgnn_validation`` / ``mpgnn_test`` /
 ``mpgnn_parallel_multiple`` (main_rgcn.py:369-472) driving ``Net`` (model.py:132-149) whose
 RGCNConv layers run on the gfx950 kernels. The loaders are shared with ``main``
-(main_rgcn.py:345-363 ≡ main.py:347-372).
+(main_rgcn.py:357-363 ≡ main.py:366-372) except ``get_node_features``, which flips the
+one-hot columns here (main_rgcn.py:351) and not in main.py (main.py:353 is commented out).
 
 Same names, arguments, return values and printed lines as the reference; model and data stay
 on the GPU and the macro-F1 scores are finished from device-side counts (``metrics``).
@@ -10,16 +11,23 @@ on the GPU and the macro-F1 scores are finished from device-side counts (``metri
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
-from .main import _adam, Data, get_edge_index_and_type_no_reverse, get_node_features, load_files, load_graph, take_rows  # noqa: F401
+from .main import _adam, _one_hot_colours, Data, get_edge_index_and_type_no_reverse, load_files, load_graph, take_rows  # noqa: F401
 from .metrics import class_weight_balanced, f1_macro_many
 from .model import Net
 
-__all__ = ["Data", "mpgnn_train", "mpgnn_validation", "mpgnn_test", "mpgnn_parallel_multiple", "EPOCHS"]
+__all__ = ["Data", "get_node_features", "mpgnn_train", "mpgnn_validation", "mpgnn_test", "mpgnn_parallel_multiple", "EPOCHS"]
 
 EPOCHS = 999  # ``for epoch in range(1, 1000)`` (main_rgcn.py:457)
+
+
+def get_node_features(colors):
+    """main_rgcn.py:345-353: one-hot columns of the colour frame, float32, columns reversed
+    (``np.flip(x, 1)``, main_rgcn.py:351)."""
+    return torch.from_numpy(np.flip(_one_hot_colours(colors), 1).copy())
 
 
 def _forward(model, data):

@@ -11,6 +11,8 @@ Results are identical to scikit-learn's (tests/test_loop.py).
 """
 from __future__ import annotations
 
+import weakref
+
 import numpy as np
 import torch
 
@@ -50,22 +52,22 @@ def f1_macro(pred: torch.Tensor, y: torch.Tensor, num_classes: int) -> float:
     return f1_macro_many([(pred, y)], num_classes)[0]
 
 
-_CW_CACHE: dict = {}
+# one entry: (weakref to the label tensor, its _version, the weights). Keyed on the tensor
+# OBJECT (a weakref that dies with it), not its address: a new label tensor landing at a
+# freed address must not hit a stale entry.
+_CW_LAST: list = [None, -1, None]
 
 
 def class_weight_balanced(y: torch.Tensor) -> np.ndarray:
     """``class_weight.compute_class_weight('balanced', classes=np.unique(y), y=y)``
     (main_rgcn.py:378): n_samples / (n_classes · bincount) over the classes present.
-    The loops recompute it every epoch on an unchanged label tensor; the answer is cached by
-    tensor identity and version so the labels cross to the host once."""
-    key = (y.data_ptr(), y.numel(), y._version, str(y.device))
-    hit = _CW_CACHE.get(key)
-    if hit is not None:
-        return hit.copy()
+    The loops recompute it every epoch on an unchanged label tensor; the answer is cached for
+    that same tensor object (and version) so the labels cross to the host once."""
+    ref, ver, w = _CW_LAST
+    if ref is not None and ref() is y and ver == y._version:
+        return w.copy()
     yn = y.detach().cpu().numpy().reshape(-1)
     classes, counts = np.unique(yn, return_counts=True)
     w = yn.shape[0] / (classes.shape[0] * counts.astype(np.float64))
-    if len(_CW_CACHE) > 64:
-        _CW_CACHE.clear()
-    _CW_CACHE[key] = w
+    _CW_LAST[:] = [weakref.ref(y), y._version, w]
     return w.copy()

@@ -23,6 +23,11 @@ def pytest_collection_modifyitems(config, items):
             item.add_marker(skip)
 
 
+def pytest_sessionfinish(session, exitstatus):
+    from tests import _parity_report
+    _parity_report.dump()
+
+
 @pytest.fixture(scope="session")
 def golden():
     import numpy as np

@@ -2,9 +2,16 @@
 
 Bars (BASELINE.json north_star):
   * integer / index work and the mean aggregation: BIT-EXACT (torch.equal)
-  * fp32 activations and gradients: within 1e-4 relative, measured elementwise as
-        |gpu - ref| <= 1e-4 * |ref| + 1e-4 * max|ref|
-    (the max-scaled floor covers elements that cancel to ~0; GEMM reassociation on MFMA)
+  * fp32 activations and gradients: within 1e-4 relative, ELEMENTWISE:
+        |gpu - ref| <= 1e-4 * max(|ref|, 1e-3 * max|ref|)
+    i.e. every element with |ref| >= 1e-3·max is held to 1e-4 of itself, and the few that
+    cancel to below that are held to 1e-7·max (the same bar at the threshold). Every check
+    records its max relative error (tests/_parity_report.py → profiles/).
+  * where a reduction over thousands of terms cancels (weight gradients summed over all node
+    rows), the reference's OWN fp32 CPU path is already off the float64 truth by more than
+    1e-4 at some elements (conv1.weight 2.0e-4 on C1, measured: DESIGN.md §2). Such checks
+    pass `ref64` (the oracle run in float64): the GPU must then be within 1e-4 of the float64
+    truth, or at most 2x as far from it as the reference fp32 path itself is.
 """
 import numpy as np
 import pytest
@@ -14,22 +21,45 @@ import mpgnn_amd
 from mpgnn_amd import data
 from mpgnn_amd.functional import MODE_ALL, MODE_SINGLE, rgcn_conv, segment_means
 from oracle import rgcn_oracle as orc
+from tests._parity_report import record
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 TOL = 1e-4
+FLOOR = 1e-3
 
 
-def rel_close(got, ref, tol=TOL, what=""):
-    got = got.detach().float().cpu()
-    ref = ref.detach().float().cpu()
-    assert got.shape == ref.shape, (what, got.shape, ref.shape)
-    scale = float(ref.abs().max()) if ref.numel() else 0.0
+def max_rel_err(got, ref, floor=FLOOR) -> float:
+    """max_e |got - ref| / max(|ref_e|, floor·max|ref|)  (0 for empty / all-zero ref and got)."""
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    if ref.numel() == 0:
+        return 0.0
     err = (got - ref).abs()
-    bound = tol * ref.abs() + tol * scale
-    bad = err > bound
-    assert not bool(bad.any()), (f"{what}: {int(bad.sum())}/{ref.numel()} elements off, "
-                                 f"max err {float(err.max()):.3e}, scale {scale:.3e}")
+    scale = float(ref.abs().max())
+    if scale == 0.0:
+        return float("inf") if float(err.max()) > 0 else 0.0
+    return float((err / ref.abs().clamp_min(floor * scale)).max())
+
+
+def rel_close(got, ref, tol=TOL, what="", ref64=None):
+    got_f = got.detach().float().cpu()
+    ref_f = ref.detach().float().cpu()
+    assert got_f.shape == ref_f.shape, (what, got_f.shape, ref_f.shape)
+    assert bool(torch.isfinite(got_f).all()) == bool(torch.isfinite(ref_f).all()), (what, "non-finite values differ")
+    e = max_rel_err(got_f, ref_f)
+    if ref64 is None:
+        record(what, e, tol)
+        assert e <= tol, f"{what}: max elementwise rel err {e:.3e} > {tol:.0e}"
+        return e
+    e_gpu = max_rel_err(got_f, ref64)
+    e_cpu = max_rel_err(ref_f, ref64)
+    bar = max(tol, 2.0 * e_cpu)
+    record(what, e, tol, e_gpu64=e_gpu, e_cpu64=e_cpu)
+    assert e_gpu <= bar, (f"{what}: vs float64 truth gpu {e_gpu:.3e}, reference fp32 path {e_cpu:.3e} "
+                          f"(bar {bar:.3e}); gpu vs fp32 reference {e:.3e}")
+    return e
 
 
 def t(a):
@@ -223,12 +253,16 @@ def test_net_forward_backward_vs_oracle(name):
     gen = torch.Generator().manual_seed(3)
     gout = torch.randn(ref.shape, generator=gen)
     ref.backward(gout)
+    # the same oracle in float64: the truth both fp32 paths are measured against
+    p64 = {k: v.detach().double().requires_grad_(True) for k, v in params.items()}
+    ref64 = orc.net_forward(p64, g.x.double(), g.edge_index, g.edge_type, 3)
+    ref64.backward(gout.double())
     net = net.to(DEV)
     out = net(g.x.to(DEV), g.edge_index.to(DEV), g.edge_type.to(DEV))
-    rel_close(out, ref, what="log_softmax")
+    rel_close(out, ref, what=f"{name} log_softmax")
     out.backward(gout.to(DEV))
     for k, p in net.named_parameters():
-        rel_close(p.grad, params[k].grad, tol=2e-4 if "conv1" in k else TOL, what=k)
+        rel_close(p.grad, params[k].grad, what=f"{name} {k}", ref64=p64[k].grad)
 
 
 def test_adam_training_steps_track_oracle():
@@ -444,6 +478,30 @@ def test_fused_relu_equals_relu_of_layer(cfg):
                           (out, xg.grad, W.grad, root.grad, bias.grad)):
         assert torch.equal(a, b.detach()), (cfg, name)
     assert bool((fused[0] >= 0).all()) and bool((fused[0] == 0).any())
+
+
+def test_fused_relu_propagates_nan():
+    """A NaN in x reaches the outputs through the fused ReLU as torch.relu would pass it
+    (fmaxf(NaN, 0) = 0 would hide a diverging run); same NaN pattern as
+    relu(layer) and the same finite values elsewhere."""
+    g = data.config_graph("C1")
+    F_out = 32
+    gen = torch.Generator().manual_seed(11)
+    R, F_in = g.num_relations, g.x.shape[1]
+    W = ((torch.rand(R, F_in, F_out, generator=gen) - 0.5) * 0.2).to(DEV)
+    root = ((torch.rand(F_in, F_out, generator=gen) - 0.5) * 0.2).to(DEV)
+    bias = (torch.rand(F_out, generator=gen) - 0.5).to(DEV)
+    x = g.x.clone()
+    x[int(g.edge_index[1, 0])] = float("nan")  # a gathered row: NaN spreads to its neighbours' means
+    x[5, 3] = float("nan")                      # and a root row
+    plan = mpgnn_amd.get_plan(g.edge_index, g.edge_type, g.num_nodes)
+    with torch.no_grad():
+        fused = rgcn_conv(x.to(DEV), W, root, bias, plan, MODE_ALL, num_relations=R, activation="relu")
+        plain = torch.relu(rgcn_conv(x.to(DEV), W, root, bias, plan, MODE_ALL, num_relations=R))
+    torch.cuda.synchronize()
+    assert bool(torch.isnan(plain).any())
+    assert torch.equal(torch.isnan(fused), torch.isnan(plain))
+    assert torch.equal(torch.nan_to_num(fused, nan=0.0), torch.nan_to_num(plain, nan=0.0))
 
 
 def test_fused_relu_mode_single_and_exact_paths():
@@ -973,6 +1031,8 @@ def test_relu_bwd_matches_threshold_backward(n, offset):
     y = torch.relu(torch.randn(n + offset, generator=gen))
     if n > 8:
         g[:4] = torch.tensor([float("nan"), float("inf"), -float("inf"), float("nan")])
+        # NaN / -0.0 / inf OUTPUTS: threshold_backward passes grad where the output is NaN
+        y[offset + 4: offset + 8] = torch.tensor([float("nan"), -0.0, float("inf"), float("nan")])
     g, y = g.to(DEV)[offset:], y.to(DEV)[offset:]
     d = torch.full((n + offset,), 7.0, device=DEV)[offset:]
     _lib.check(_lib.lib.mpgnn_relu_bwd(g.data_ptr(), y.data_ptr(), n, d.data_ptr(), None), "mpgnn_relu_bwd")

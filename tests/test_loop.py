@@ -71,6 +71,66 @@ def test_load_links_large_file_multithreaded(tmp_path):
     assert np.array_equal(ei.numpy(), np.stack([rows[:, 0], rows[:, 2]])) and np.array_equal(et.numpy(), rows[:, 1])
 
 
+@pytest.mark.parametrize("graph", ["L3", "L4"])
+def test_node_features_column_order_per_reference_driver(tmp_path, golden, graph):
+    """main.py:347-355 keeps get_dummies' column order (its flip, main.py:353, is commented
+    out); main_rgcn.py:345-353 reverses the columns (main_rgcn.py:351). Run both loaders on
+    the reference's own node.dat rows (KAT fixture) through load_files, as the drivers do."""
+    node = golden("kat_synthetic.npz")[f"{graph}_node"]
+    label = golden("kat_synthetic.npz")[f"{graph}_label"]
+    link = golden("kat_synthetic.npz")[f"{graph}_link"]
+    for name, rows in (("node.dat", node), ("label.dat", label), ("link.dat", link)):
+        np.savetxt(tmp_path / name, rows, fmt="%d", delimiter="\t")
+    labels, features, links, _, nrel = main.load_files(str(tmp_path / "node.dat"), str(tmp_path / "link.dat"),
+                                                       str(tmp_path / "label.dat"))
+    cols = node[:, 1:].astype(np.float32)
+    x_mpgnn = main.get_node_features(features)
+    x_rgcn = main_rgcn.get_node_features(features)
+    assert x_mpgnn.dtype == torch.float32 and x_rgcn.dtype == torch.float32
+    assert np.array_equal(x_mpgnn.numpy(), cols)
+    assert np.array_equal(x_rgcn.numpy(), cols[:, ::-1])
+    assert not np.array_equal(x_mpgnn.numpy(), x_rgcn.numpy())  # the two drivers really differ here
+    # native readers (csrc/io.cpp) give the same matrices and labels
+    assert torch.equal(data.load_node_features(str(tmp_path / "node.dat")), x_mpgnn)
+    assert torch.equal(data.load_node_features(str(tmp_path / "node.dat"), flip=True), x_rgcn)
+    ids, y = data.load_labels(str(tmp_path / "label.dat"))
+    assert np.array_equal(ids.numpy(), label[:, 0]) and torch.equal(y, labels)
+    assert nrel == np.unique(link[:, 1]).size
+
+
+def test_tsv_reader_edge_cases(tmp_path):
+    p = str(tmp_path / "n.dat")
+    _write(p, "")
+    assert data.read_tsv_numeric(p).shape == (0, 0)
+    # ragged rows pad with NaN (pandas read_csv), floats / exponents / signs, CRLF, blank lines
+    _write(p, "0\t1.5\t-2e3\r\n\n1\t+4\n2 0.25 7\t\n")
+    a = data.read_tsv_numeric(p)
+    assert a.shape == (3, 3)
+    assert np.array_equal(a[:, :2], [[0, 1.5], [1, 4], [2, 0.25]])
+    assert a[0, 2] == -2000 and np.isnan(a[1, 2]) and a[2, 2] == 7
+    import pandas as pd
+    ref = pd.read_csv(p, sep=r"\s+", header=None).to_numpy(dtype=np.float64)
+    assert np.array_equal(np.isnan(a), np.isnan(ref)) and np.array_equal(np.nan_to_num(a), np.nan_to_num(ref))
+    for bad in ("0\tred\n", "1\t2x\n"):
+        _write(p, bad)
+        with pytest.raises(ValueError):
+            data.read_tsv_numeric(p)
+    _write(p, "0\t1.5\n")
+    with pytest.raises(ValueError):
+        data.load_labels(p)
+    with pytest.raises(ValueError):
+        data.read_tsv_numeric(str(tmp_path / "missing.dat"))
+
+
+def test_tsv_reader_large_file_multithreaded(tmp_path):
+    rng = np.random.default_rng(5)
+    a = np.concatenate([np.arange(150_000)[:, None], rng.random((150_000, 4)) * 100], 1)
+    p = tmp_path / "big.dat"
+    np.savetxt(p, a, fmt=["%d"] + ["%.17g"] * 4, delimiter="\t")
+    assert os.path.getsize(p) > (3 << 20)
+    assert np.array_equal(data.read_tsv_numeric(str(p)), a)  # %.17g round-trips float64 exactly
+
+
 # ------------------------------------------------------------------------------------------
 # scores and loss weights (main.py:1062-1098, main_rgcn.py:376-415)
 # ------------------------------------------------------------------------------------------
@@ -97,6 +157,21 @@ def test_class_weight_balanced_identical_to_sklearn():
         ref = skl_class_weight.compute_class_weight("balanced", classes=np.unique(y.numpy()), y=y.tolist())
         assert np.array_equal(metrics.class_weight_balanced(y), ref)
         assert np.array_equal(metrics.class_weight_balanced(y), ref)  # cached answer
+
+
+def test_class_weight_cache_keyed_on_the_tensor_object():
+    """A new label tensor at a recycled address (same numel, _version 0) must not hit the
+    previous tensor's cached weights (the cache was keyed on data_ptr)."""
+    buf = torch.tensor([0, 0, 0, 1], dtype=torch.int64)
+    w1 = metrics.class_weight_balanced(buf)
+    alias = buf.view(-1)  # another tensor object over the same storage and address
+    alias.copy_(torch.tensor([0, 1, 1, 1]))  # bumps the shared version counter too
+    w2 = metrics.class_weight_balanced(alias)
+    assert np.array_equal(w2, skl_class_weight.compute_class_weight("balanced", classes=np.array([0, 1]),
+                                                                    y=[0, 1, 1, 1]))
+    assert not np.array_equal(w1, w2)
+    y3 = torch.tensor([1, 1, 1, 0], dtype=torch.int64).as_strided((4,), (1,))
+    assert np.array_equal(metrics.class_weight_balanced(y3), w2)  # same class counts as alias
 
 
 # ------------------------------------------------------------------------------------------
