@@ -224,48 +224,18 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
  * bit-identical to the reference either way. mpgnn_rel_mean_fwd is always exact. */
 enum mpgnn_option {
     MPGNN_OPT_EXACT_ORDER = 0,
-    MPGNN_OPT_ABLATE = 1, /* profiling only: bits skip phases of the forward tile kernel (wrong results) */
-    MPGNN_OPT_STAMPS = 2, /* profiling only: device pointer of a u64 [blocks][4 waves][8] timeline buffer, 0 = off */
-    MPGNN_OPT_TIMING_MASK = 3, /* kernel kinds timed while timing is enabled (bit k = kind k); default all */
-    MPGNN_OPT_TILE_WS = 4, /* 1: wave-specialised tile GEMM for F <= 128 (2: without priority); 0 (default): two-workgroup variant */
-    MPGNN_OPT_REL_GEMM = 5, /* 1 (default): B-stationary GEMM (weights in registers) for F_in, F_out in {64,128} x {128}; 0: tile GEMM */
-    MPGNN_OPT_FUSED = 6,    /* 1: forward means + transform fused in one launch for F_in = F_out = 128; 0 (default): two launches */
-    MPGNN_OPT_FLAT_U = 7,   /* 16 (default) or 32: x rows in flight per wave in the flat row-sum kernel (same results) */
-    MPGNN_OPT_OVERLAP = 8,  /* forward: segment means and transform of G relation groups pipelined over the caller's
-                               stream and a second stream (1..8 groups; 0 = one stream, the default: at C3 the two kernels contend for
-                               the CUs and the cross-stream events cost more than the overlap gains); same results */
-    MPGNN_OPT_REL_WGS = 9,  /* rel_gemm_kernel workgroups per CU: 2 (default) or 1; same results */
-    MPGNN_OPT_REL_STAGGER = 10, /* rel_gemm_kernel: the second half of the grid first sleeps this many 64-clock
-                                  quanta (de-phases the two workgroups of a CU); same results */
+    MPGNN_OPT_TIMING_MASK = 3,   /* kernel kinds timed while timing is enabled (bit k = kind k); default all */
+    MPGNN_OPT_REL_GEMM = 5,      /* 1 (default): B-stationary GEMM (weights in registers) for F_in, F_out in
+                                    {64,128} x {128}; 0: the tile GEMM (the width fallback) */
     MPGNN_OPT_PLAN_THREADS = 11, /* host threads of mpgnn_plan_create: 0 (default) = hardware concurrency capped
-                                   at 16; the tables do not depend on it */
-    MPGNN_OPT_REL_QUEUE = 12,   /* rel_gemm_kernel: 1 = items taken from per-group atomic counters (dynamic
-                                   schedule), 0 = fixed contiguous ranges; same results */
-    MPGNN_OPT_MERGE_GRAD = 13,  /* backward: 1 (default) = weight / root / bias outer products in one launch and
-                                   their slab reductions in one more; 0 = one launch each; same results */
-    MPGNN_OPT_REL_DEEP = 14,    /* rel_gemm_kernel: 1 = A rows fetched two items ahead (two register sets);
-                                   same results */
-    MPGNN_OPT_REL_DIRECT = 15,  /* rel_gemm_kernel: 1 = LDS-free, every wave loads its own A fragments (no
-                                   barriers); same results */
-    MPGNN_OPT_FLAT_CPW = 16,    /* flat row-sum kernel: plan chunks per wave, 1 (default), 2 or 4, the next
-                                   chunk's metadata fetched behind the current rows; same results */
-    MPGNN_OPT_Y_ROWMAJOR = 17,  /* withdrawn (measured neutral, slowed the default transform): only 0 is
-                                   accepted, 1 returns MPGNN_ERR_ARG */
-    MPGNN_OPT_REL_PINGPONG = 18, /* rel_gemm_kernel: 1 = one 512-thread workgroup per CU, two wave groups
-                                   alternating MFMA and memory phases; same results */
-    MPGNN_OPT_REL_WIDE = 19,    /* 1 (default): the B-stationary GEMM also takes F_in = F_out = 256 (two 128-column
-                                   blocks, weight slice reloaded after the chain on a relation change);
-                                   0: tile_gemm_kernel there */
-    MPGNN_OPT_CHUNK_ROWS = 20,  /* backward weight-gradient reduction chunks: base length in rows (multiple of 32,
-                                   32..1024, default 192) of the root chunks and of the relation chunks of plans
-                                   created afterwards; same results up to fp32 summation order of the slabs */
-    MPGNN_OPT_OUTER_ROOT_FIRST = 21, /* backward, merged outer-product launch: 1 (default) = root / bias chunks take
-                                   the first workgroups, 0 = the weight-gradient chunks do; same results */
-    MPGNN_OPT_OUTER_SLICE = 22, /* backward, merged outer-product launch: rows per LDS slice, 16 (default: 36 KB
-                                   of LDS per workgroup, four workgroups per CU), 32 (72 KB, two) or 8; same results */
-    MPGNN_OPT_DGRAD_IDX_AHEAD = 23 /* dgrad rel_gemm_kernel: 1 (default) = the gathered row numbers of an item are
-                                   loaded one item before its rows (one dependent round trip per item instead
-                                   of two); 0 = together; same results */
+                                    at 16; the tables do not depend on it */
+    MPGNN_OPT_REL_WIDE = 19,     /* 1 (default): the B-stationary GEMM also takes F_in = F_out = 256 (two 128-column
+                                    blocks); 0: tile_gemm_kernel there */
+    MPGNN_OPT_CHUNK_ROWS = 20    /* backward weight-gradient reduction chunks: base length in rows (multiple of 32,
+                                    32..1024, default 192) of the root chunks and of the relation chunks of plans
+                                    created afterwards; same results up to fp32 summation order of the slabs */
+    /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
+       withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
 

@@ -491,17 +491,7 @@ struct SegTileArgs {
     int sel_b;
     float* H;            // nullable: copy of the gathered relation-tile rows, row = s - sel_b, width F
     const float* Hsrc;   // gather_kind 2: precomputed relation-tile rows, row = s - sel_b
-    int ablate;          // debug (MPGNN_OPT_ABLATE): 1 skip gather, 2 skip MFMA+epilogue,
-                         // 4 skip epilogue stores, 8 skip MFMA loop only; wrong results
-    unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [block][8] timeline, or nullptr
 };
-
-// debug timeline stamp (diagnostic builds only pay for it: stamps == nullptr otherwise)
-__device__ __forceinline__ unsigned long long stamp_now() {
-    unsigned long long t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    return t;
-}
 
 template <int V, int T>
 __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
@@ -511,8 +501,6 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
     float* s_scale = smem;                  // [64] cnt as float (dgrad)
     float* A_lds = smem + kTileRows;        // [64][lda]
 
-    unsigned long long t_start = 0;
-    if (a.stamps != nullptr) t_start = stamp_now();
     const bool root_tile = (int)blockIdx.x >= a.n_rel_tiles;
     int s0, nrows;
     if (!root_tile) {
@@ -559,8 +547,8 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
     if (root_tile || a.gather_kind == 2) {
         // contiguous rows: one coalesced float4 sweep of the whole 64-row tile
         const float* base = root_tile ? a.src + (size_t)s0 * a.F : a.Hsrc + (size_t)(s0 - a.sel_b) * a.F;
-        if (!(a.ablate & 1)) load_dense_tile(base, a.F, nrows, A_lds, lda, Kp);
-    } else if (!(a.ablate & 1)) {
+        load_dense_tile(base, a.F, nrows, A_lds, lda, Kp);
+    } else {
         wave_gather<V, T, (V * T <= 2 ? 8 : 4), kRowsPerWave>(
             g, bnd, wn, lane, [&](int r, bool live, float (&acc)[T][V]) {
                 const bool do_div = live && cnt_rows != nullptr;
@@ -578,8 +566,6 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
             });
     }
     __syncthreads();
-    unsigned long long t_loaded = 0;
-    if (a.stamps != nullptr) t_loaded = stamp_now();
     if (a.W == nullptr) return;
 
     // ---- MFMA phase --------------------------------------------------------------------
@@ -593,34 +579,11 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
     b.ldw = a.trans ? a.F : a.N;
     const int n_base = blockIdx.y * kColTile;
     float* Yt = root_tile ? a.Yroot + (size_t)(s0 - a.row_lo) * a.N : a.Y + (size_t)(s0 - a.sel_b) * a.N;
-    if (a.ablate & 2) {  // keep the gathered tile observable, skip the contraction
-        if (threadIdx.x < nrows) Yt[(size_t)threadIdx.x * a.N] = A_lds[threadIdx.x * lda];
-        return;
-    }
     MfmaTile mt;
-    if (a.ablate & 8) {
-        mt.nb = wave;
-        mt.active = n_base + wave * 32 < a.N;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            mt.acc0[r] = A_lds[(lane & 31) * lda + r];
-            mt.acc1[r] = A_lds[(32 + (lane & 31)) * lda + r];
-        }
-    } else {
-        mfma_tile(mt, A_lds, lda, Kp, b, n_base, wave, lane);
-    }
+    mfma_tile(mt, A_lds, lda, Kp, b, n_base, wave, lane);
     const int c = lane & 31;
     const int h = lane >> 5;
     const int col = n_base + mt.nb * 32 + c;
-    unsigned long long t_mfma = 0;
-    if (a.stamps != nullptr) t_mfma = stamp_now();
-    if (a.ablate & 4) {
-        float sum = 0.0f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sum += mt.acc0[r] + mt.acc1[r];
-        if (sum == 1234.5678f) a.Y[lane] = sum;
-        return;
-    }
     if (mt.active && col < a.N) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -636,20 +599,6 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
                 Yt[(size_t)(row + 32) * a.N + col] = v;
             }
         }
-    }
-    if (a.stamps != nullptr && (threadIdx.x & 63) == 0) {
-        const unsigned long long t_end = stamp_now();
-        const unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
-        const unsigned xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)); // HW_REG_XCC_ID
-        unsigned long long* o = a.stamps + ((size_t)blockIdx.x * gridDim.y + blockIdx.y) * 32 + (threadIdx.x >> 6) * 8;
-        o[0] = t_start;
-        o[1] = t_loaded;
-        o[2] = t_mfma;
-        o[3] = t_end;
-        o[4] = hw;
-        o[5] = xcc;
-        o[6] = (unsigned long long)nrows;
-        o[7] = root_tile;
     }
 }
 
@@ -688,9 +637,6 @@ struct TileGemmArgs {
     int row_lo, row_hi;
     int y_div;
     int sel_b;
-    unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][8 items][8] timeline, ws kernel
-    int ws_prio;                 // memory waves at s_setprio 1 (ws kernel)
-    int ws_ablate;               // profiling: 1 skip output stores, 2 skip A loads (wrong results)
 };
 
 struct TileItem {
@@ -762,43 +708,26 @@ __device__ __forceinline__ void tile_commit(const TileGemmArgs& a, const TileIte
 // item's first B chunk; once its last chunk is in registers the NEXT item's first chunk is
 // loaded into b0, so it is in flight across the epilogue and the item boundary (a cold start
 // would expose a full L2/MALL miss per item).
-// ABL (profiling builds of the bench shape only, MPGNN_OPT_ABLATE bits >> 4): 1 no MFMA (a VALU
-// add consumes the operands), 2 no B loads, 4 no LDS A reads, 8 no epilogue stores.
-template <bool TRANS, bool CLAMP, int ABL = 0>
+template <bool TRANS, bool CLAMP>
 __device__ __forceinline__ void mfma_strip(f32x16& acc0, f32x16& acc1, const float* a0p, const float* a1p, int KH,
                                            int kb, const BLoader<TRANS, CLAMP>& ld, float (&b0)[kKC],
-                                           const BLoader<TRANS, CLAMP>& ld_next) {
+                                           const BLoader<TRANS, CLAMP>& ld_next, int kb_next) {
     // A fragments roll one 4-k step ahead: the ds_read_b128 pair for step j+1 is issued before
     // step j's eight MFMAs, so LDS latency hides behind them (read just in time it was exposed
     // every 8 MFMAs: ~10 µs of a 37 µs launch).  The read after the last step lands in the
     // 4-float row pad (lda = Kp + 4) and is never used.
-    float4 ca0, ca1;
-    if constexpr ((ABL & 4) == 0) {
-        ca0 = *reinterpret_cast<const float4*>(a0p);
-        ca1 = *reinterpret_cast<const float4*>(a1p);
-    }
+    float4 ca0 = *reinterpret_cast<const float4*>(a0p);
+    float4 ca1 = *reinterpret_cast<const float4*>(a1p);
     auto compute_chunk = [&](const float (&bc)[kKC], int t, int k0) {
 #pragma unroll
         for (int j = 0; j < kKC; j += 4) {
-            float4 a0, a1;
-            if constexpr (ABL & 4) {
-                a0 = make_float4(1.f, 2.f, 3.f, (float)t);
-                a1 = a0;
-            } else {
-                a0 = ca0;
-                a1 = ca1;
-                ca0 = *reinterpret_cast<const float4*>(a0p + t + j + 4);
-                ca1 = *reinterpret_cast<const float4*>(a1p + t + j + 4);
-                __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of this step's MFMAs
-            }
+            const float4 a0 = ca0, a1 = ca1;
+            ca0 = *reinterpret_cast<const float4*>(a0p + t + j + 4);
+            ca1 = *reinterpret_cast<const float4*>(a1p + t + j + 4);
+            __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of this step's MFMAs
             float bq[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) bq[q] = (!CLAMP || k0 + j + q < ld.K) ? bc[j + q] : 0.0f;
-            if constexpr (ABL & 1) {
-                acc0[j] += a0.x + a0.y + a0.z + a0.w + bq[0] + bq[1] + bq[2] + bq[3];
-                acc1[j] += a1.x + a1.y + a1.z + a1.w;
-                continue;
-            }
             acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, bq[0], acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, bq[0], acc1, 0, 0, 0);
             acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, bq[1], acc0, 0, 0, 0);
@@ -809,14 +738,7 @@ __device__ __forceinline__ void mfma_strip(f32x16& acc0, f32x16& acc1, const flo
             acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, bq[3], acc1, 0, 0, 0);
         }
     };
-    auto ldc = [&](const BLoader<TRANS, CLAMP>& l, int k0, float (&o)[kKC]) {
-        if constexpr (ABL & 2) {
-#pragma unroll
-            for (int j = 0; j < kKC; ++j) o[j] = (float)(k0 + j);
-        } else {
-            l.template load_chunk<kKC>(k0, o);
-        }
-    };
+    auto ldc = [&](const BLoader<TRANS, CLAMP>& l, int k0, float (&o)[kKC]) { l.template load_chunk<kKC>(k0, o); };
     float b1[kKC];
     int t = 0;
 #pragma unroll 1
@@ -834,7 +756,7 @@ __device__ __forceinline__ void mfma_strip(f32x16& acc0, f32x16& acc1, const flo
     __builtin_amdgcn_sched_barrier(0);
     compute_chunk(b0, t, kb + t);
     __builtin_amdgcn_sched_barrier(0);
-    ldc(ld_next, kb, b0);
+    ldc(ld_next, kb_next, b0);
     __builtin_amdgcn_sched_barrier(0);
     compute_chunk(b1, t + kKC, kb + t + kKC);
 }
@@ -911,7 +833,7 @@ struct ItemOrder {
     }
 };
 
-template <int KB, bool TRANS, bool CLAMP, int ABL = 0>
+template <int KB, bool TRANS, bool CLAMP>
 __device__ __forceinline__ void tile_gemm_body(const TileGemmArgs& a, float* smem) {
     constexpr int Kp = 64 * KB;
     constexpr int KH = Kp / 2;
@@ -962,8 +884,28 @@ __device__ __forceinline__ void tile_gemm_body(const TileGemmArgs& a, float* sme
         {   // unconditional (a wave past N computes clamped columns and stores nothing): a branch
             // here would join b0 through register copies that wait for the preloaded chunk
             const BLoader<TRANS, CLAMP> ld(item_bsrc(a, cur), min(cur.n_base + wave * 32 + c, a.N - 1));
-            mfma_strip<TRANS, CLAMP, ABL>(acc0, acc1, A + c * lda + h * KH, A + (32 + c) * lda + h * KH, KH, h * KH, ld,
-                                     b0, ld_next);
+            const float* a0p = A + c * lda + h * KH;
+            const float* a1p = A + (32 + c) * lda + h * KH;
+            if constexpr (KB == 2) {  // (KB 3, 4: no registers left)
+                // two accumulation chains over the halves of this lane's K range, added before
+                // the epilogue: half the fma rounding chain (accuracy vs the float64 truth)
+                constexpr int KH2 = KH / 2;
+                f32x16 acc2, acc3;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    acc2[r] = 0.0f;
+                    acc3[r] = 0.0f;
+                }
+                mfma_strip<TRANS, CLAMP>(acc0, acc1, a0p, a1p, KH2, h * KH, ld, b0, ld, h * KH + KH2);
+                mfma_strip<TRANS, CLAMP>(acc2, acc3, a0p + KH2, a1p + KH2, KH2, h * KH + KH2, ld, b0, ld_next, h * KH);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    acc0[r] = acc0[r] + acc2[r];
+                    acc1[r] = acc1[r] + acc3[r];
+                }
+            } else {
+                mfma_strip<TRANS, CLAMP>(acc0, acc1, a0p, a1p, KH, h * KH, ld, b0, ld_next, h * KH);
+            }
         }
         // epilogue: accumulators -> LDS (the consumed A buffer) -> whole-row coalesced stores
         __syncthreads();
@@ -977,9 +919,7 @@ __device__ __forceinline__ void tile_gemm_body(const TileGemmArgs& a, float* sme
             }
         }
         __syncthreads();
-        if constexpr ((ABL & 8) != 0) {
-            if (A[tid] == 1234.5f) a.Y[tid] = 0.0f;  // keep the staged tile observable
-        } else {
+        {
             float* Yt = cur.root ? a.Yroot + (size_t)(cur.s0 - a.row_lo) * a.N : a.Y + (size_t)(cur.s0 - a.sel_b) * a.N;
             const bool div_rows = !cur.root && a.y_div;
             const float* sc = scales + buf * kTileRows;
@@ -1059,11 +999,6 @@ struct RelGemmArgs {
     float* Y;             // rows s - sel_b
     float* Yroot;         // rows i - row_lo
     int sel_b, row_lo, row_hi;
-    int stagger;                 // s_sleep quanta (64 clk) the second half of the grid waits first
-    int* queue;                  // nullable: per-group item counters (dynamic schedule), zero between launches
-    int deep;                    // 1: A rows fetched two items ahead (run_deep)
-    int idx_ahead;               // dgrad: gathered row numbers loaded one item ahead of the rows (run)
-    unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][32] s_memtime timeline, or nullptr
 };
 
 template <int KB, bool DGRAD, int NB = 1>
@@ -1212,6 +1147,7 @@ struct RelGemm {
     __device__ static void run(const RelGemmArgs& a, float* smem) {
         float* As = smem;                 // [2][32][lda]
         float* Sc = smem + 2 * 32 * lda;  // [2][32] dgrad row scales
+        float* Pt = Sc + 64 + 4;          // dgrad, K <= 128: [4 waves][16][64] first-half partials
         const int tid = threadIdx.x;
         const int lane = tid & 63, c = lane & 31, h = lane >> 5;
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1225,19 +1161,6 @@ struct RelGemm {
         const int i_beg = (int)((long long)rng * n_items / G);
         const int i_end = (int)((long long)(rng + 1) * n_items / G);
         if (i_beg >= i_end) return;
-        unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 32 : nullptr;
-        auto stamp = [&](int k) {
-            if (stp != nullptr && tid == 0 && k < 30) stp[k] = stamp_now();
-        };
-        auto stamp_rt = [&](int k) {  // s_memrealtime (100 MHz, chip-wide)
-            if (stp != nullptr && tid == 0) stp[k] = __builtin_amdgcn_s_memrealtime();
-        };
-        stamp_rt(30);
-        // the two workgroups of a CU (blocks b and b + G/2 under the dispatcher's fill order)
-        // otherwise run their MFMA and load/store phases in lockstep: offset the second one
-        if (a.stagger > 0 && (int)blockIdx.x >= G / 2)
-            for (int k = 0; k < a.stagger; ++k) __builtin_amdgcn_s_sleep(1);
-        stamp(0);
 
         float4 v[WPT];
         int cnt;
@@ -1249,7 +1172,7 @@ struct RelGemm {
         int nrow[DGRAD ? WPT : 1];  // dgrad: gathered rows + scale of the item after the current one
         int ncnt = 1;
         if constexpr (DGRAD) {
-            if (a.idx_ahead && i_beg + 1 < i_end) gather_idx(a, get_item(i_beg + 1), tid, nrow, ncnt);
+            if (i_beg + 1 < i_end) gather_idx(a, get_item(i_beg + 1), tid, nrow, ncnt);
         }
         float b[KH];
         load_b(cur.w, wave, lane, b);
@@ -1261,20 +1184,15 @@ struct RelGemm {
 #pragma unroll
         for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(b[j]));
         __syncthreads();
-        stamp(1);
         int buf = 0;
         for (int i = i_beg; i < i_end; ++i) {
             const bool has_next = i + 1 < i_end;
             const Item nxt = has_next ? get_item(i + 1) : cur;
             if (has_next) {  // in flight during this item's MFMAs
-                if constexpr (DGRAD) {
-                    if (a.idx_ahead) {
-                        issue_rows(a, tid, nrow, v);
-                        cnt = ncnt;
-                        if (i + 2 < i_end) gather_idx(a, get_item(i + 2), tid, nrow, ncnt);
-                    } else {
-                        issue(a, nxt, tid, v, cnt);
-                    }
+                if constexpr (DGRAD) {  // rows of the next item; row numbers of the one after
+                    issue_rows(a, tid, nrow, v);
+                    cnt = ncnt;
+                    if (i + 2 < i_end) gather_idx(a, get_item(i + 2), tid, nrow, ncnt);
                 } else {
                     issue(a, nxt, tid, v, cnt);
                 }
@@ -1285,20 +1203,37 @@ struct RelGemm {
                 if (new_w) load_b(nxt.w, wave, lane, bn);  // the next relation run's slice
             }
             const float* Ab = As + buf * 32 * lda + c * lda + h * KH;
-            f32x16 acc;
+            // K <= 128: two accumulation chains (k-steps j < KH/2 and j >= KH/2) added in the
+            // epilogue, half the rounding chain of one K-long fma chain (accuracy vs the float64
+            // truth). Forward: the second chain in registers; dgrad (no registers left): the first
+            // half's sums parked in LDS (this lane's own 16 floats, no barrier). K = 256: one chain.
+            constexpr bool kSplit = KB <= 2 && !DGRAD;
+            constexpr bool kSplitLds = KB <= 2 && DGRAD;
+            float* pt = Pt + (wave * 16) * 64 + lane;
+            f32x16 acc, acc2;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+            for (int r = 0; r < 16; ++r) {
+                acc[r] = 0.0f;
+                acc2[r] = 0.0f;
+            }
             float4 af = *reinterpret_cast<const float4*>(Ab);
 #pragma unroll
             for (int j = 0; j < KH; j += 4) {
                 const float4 cf = af;
                 if (j + 4 < KH) af = *reinterpret_cast<const float4*>(Ab + j + 4);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], acc, 0, 0, 0);
+                if (kSplitLds && j == KH / 2) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        pt[r * 64] = acc[r];
+                        acc[r] = 0.0f;
+                    }
+                }
+                f32x16& ac = (kSplit && j >= KH / 2) ? acc2 : acc;
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], ac, 0, 0, 0);
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], ac, 0, 0, 0);
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], ac, 0, 0, 0);
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], ac, 0, 0, 0);
             }
-            stamp(2 + 2 * (i - i_beg));
             // epilogue: each accumulator register = rows (r&3) + 8(r>>2) + 4h, column 32·wave + c
             const float* sc = Sc + buf * 32;
             float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
@@ -1306,7 +1241,7 @@ struct RelGemm {
             for (int r = 0; r < 16; ++r) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (row < cur.nrows) {
-                    float o = acc[r];
+                    float o = kSplit ? acc[r] + acc2[r] : (kSplitLds ? pt[r * 64] + acc[r] : acc[r]);
                     if constexpr (DGRAD) {
                         if (!cur.root) o = o * sc[row];
                     }
@@ -1323,374 +1258,8 @@ struct RelGemm {
                 }
             }
             __syncthreads();
-            stamp(3 + 2 * (i - i_beg));
             cur = nxt;
             buf ^= 1;
-        }
-        stamp_rt(31);
-    }
-
-    // Static ranges as run(), with the A rows of item i+2 issued at the start of item i (two
-    // register sets alternate), so a tile's loads have two MFMA phases to land before their
-    // LDS commit at the end of item i+1 instead of one (MPGNN_OPT_REL_DEEP).
-    __device__ static void run_deep(const RelGemmArgs& a, float* smem) {
-        float* As = smem;                 // [2][32][lda]
-        float* Sc = smem + 2 * 32 * lda;  // [2][32] dgrad row scales
-        const int tid = threadIdx.x;
-        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
-        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-        const int n_items = a.n_rel + a.n_root;
-        const int G = (int)gridDim.x;
-        const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
-        const int rng = g * q + min(g, rem) + ((int)blockIdx.x >> 3);
-        const int i_beg = (int)((long long)rng * n_items / G);
-        const int i_end = (int)((long long)(rng + 1) * n_items / G);
-        if (i_beg >= i_end) return;
-        const ItemTable tab = item_table(a, i_beg, i_end, lane);
-        auto get_item = [&](int i) { return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i); };
-        float4 va[WPT], vb[WPT];
-        int ca = 1, cb = 1;
-        Item cur = get_item(i_beg);
-        issue(a, cur, tid, va, ca);
-        float b[KH];
-        load_b(cur.w, wave, lane, b);
-        Item n1 = cur;
-        if (i_beg + 1 < i_end) {
-            n1 = get_item(i_beg + 1);
-            issue(a, n1, tid, vb, cb);
-        }
-        commit(cur, tid, va, ca, As, Sc);
-#pragma unroll
-        for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(b[j]));
-        __syncthreads();
-        int buf = 0;
-        // vh: registers holding item i+1 (committed at the end of item i); vn: receive item i+2
-        auto body = [&](int i, float4 (&vh)[WPT], int& ch, float4 (&vn)[WPT], int& cn) {
-            const bool has1 = i + 1 < i_end, has2 = i + 2 < i_end;
-            const Item n2 = has2 ? get_item(i + 2) : n1;
-            if (has2) issue(a, n2, tid, vn, cn);
-            const bool new_w = has1 && n1.w != cur.w;
-            float bn[KH];
-            if (new_w) load_b(n1.w, wave, lane, bn);
-            const float* Ab = As + buf * 32 * lda + c * lda + h * KH;
-            f32x16 acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-            float4 af = *reinterpret_cast<const float4*>(Ab);
-#pragma unroll
-            for (int j = 0; j < KH; j += 4) {
-                const float4 cf = af;
-                if (j + 4 < KH) af = *reinterpret_cast<const float4*>(Ab + j + 4);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], acc, 0, 0, 0);
-            }
-            float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
-            const float* sc = Sc + buf * 32;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (row < cur.nrows) {
-                    float o = acc[r];
-                    if constexpr (DGRAD) {
-                        if (!cur.root) o = o * sc[row];
-                    }
-                    Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
-                }
-            }
-            if (has1) commit(n1, tid, vh, ch, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
-            if (new_w) {
-#pragma unroll
-                for (int j = 0; j < KH; ++j) b[j] = bn[j];
-            }
-            __syncthreads();
-            cur = n1;
-            n1 = n2;
-            buf ^= 1;
-        };
-        for (int i = i_beg; i < i_end; i += 2) {
-            body(i, vb, cb, va, ca);
-            if (i + 1 >= i_end) break;
-            body(i + 1, va, ca, vb, cb);
-        }
-    }
-
-    // Ping-pong schedule (MPGNN_OPT_REL_PINGPONG): one 512-thread workgroup per CU holding two
-    // wave groups (waves 0-3, 4-7), each with its own A double buffer, taking alternate items of
-    // the workgroup's range. The loop runs in phases separated by one barrier; in each phase one
-    // group runs its item's MFMA chain while the other stores its previous item's outputs,
-    // commits its next tile and swaps weight slices — so each SIMD's two waves alternate between
-    // the matrix pipe and the memory pipe instead of entering both in lockstep.
-    __device__ static void run_pingpong(const RelGemmArgs& a, float* smem) {
-        const int tid = threadIdx.x;  // 512 threads
-        const int grp = tid >> 8;
-        const int gtid = tid & 255;
-        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
-        const int wave = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
-        float* As = smem + grp * (2 * 32 * lda + 64);  // this group's [2][32][lda] A tiles
-        float* Sc = As + 2 * 32 * lda;                 // and its [2][32] dgrad row scales
-        const int n_items = a.n_rel + a.n_root;
-        const int G = (int)gridDim.x;
-        const int g8 = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
-        const int rng = g8 * q + min(g8, rem) + ((int)blockIdx.x >> 3);
-        const int i_beg = (int)((long long)rng * n_items / G);
-        const int i_end = (int)((long long)(rng + 1) * n_items / G);
-        const int n_wg = i_end - i_beg;  // uniform across the workgroup (also when 0)
-        const int n_g = n_wg > grp ? (n_wg - grp + 1) / 2 : 0;  // items of this group: i_beg + grp + 2k
-        const int n_max = (n_wg + 1) / 2;
-        float4 v[WPT];
-        int cnt = 1;
-        Item cur{}, nxt{};
-        float b[KH], bn[KH];
-        if (n_g > 0) {
-            cur = item(a, i_beg + grp);
-            issue(a, cur, gtid, v, cnt);
-            load_b(cur.w, wave, lane, b);
-            commit(cur, gtid, v, cnt, As, Sc);
-#pragma unroll
-            for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(b[j]));
-        }
-        __syncthreads();
-        int buf = 0;
-        bool has_next = false, new_w = false;
-        f32x16 acc;
-        // group g runs the MFMAs of its k-th item in phase 2k + g and its epilogue in 2k + g + 1
-        for (int ph = 0; ph <= 2 * n_max; ++ph) {
-            const int k2 = ph - grp;
-            if (k2 >= 0 && (k2 >> 1) < n_g) {
-                const int k = k2 >> 1;
-                if ((k2 & 1) == 0) {
-                    has_next = k + 1 < n_g;
-                    nxt = has_next ? item(a, i_beg + grp + 2 * (k + 1)) : cur;
-                    if (has_next) issue(a, nxt, gtid, v, cnt);
-                    new_w = nxt.w != cur.w;
-                    if (new_w) load_b(nxt.w, wave, lane, bn);
-                    const float* Ab = As + buf * 32 * lda + c * lda + h * KH;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-                    float4 af = *reinterpret_cast<const float4*>(Ab);
-#pragma unroll
-                    for (int j = 0; j < KH; j += 4) {
-                        const float4 cf = af;
-                        if (j + 4 < KH) af = *reinterpret_cast<const float4*>(Ab + j + 4);
-                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], acc, 0, 0, 0);
-                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], acc, 0, 0, 0);
-                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], acc, 0, 0, 0);
-                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], acc, 0, 0, 0);
-                    }
-                } else {
-                    float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N
-                                         : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
-                    const float* sc = Sc + buf * 32;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                        if (row < cur.nrows) {
-                            float o = acc[r];
-                            if constexpr (DGRAD) {
-                                if (!cur.root) o = o * sc[row];
-                            }
-                            Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
-                        }
-                    }
-                    if (has_next) commit(nxt, gtid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
-                    if (new_w) {
-#pragma unroll
-                        for (int j = 0; j < KH; ++j) b[j] = bn[j];
-                    }
-                    cur = nxt;
-                    buf ^= 1;
-                }
-            }
-            __syncthreads();
-        }
-    }
-
-    // LDS-free variant (MPGNN_OPT_REL_DIRECT): every wave loads its own A fragments straight
-    // into registers — lane (r = lane & 31, h = lane >> 5) holds row r, k ∈ [h·KH, (h+1)·KH),
-    // KH/4 float4 loads — so the four waves of a workgroup never synchronise (no barrier, no
-    // LDS commit). The next item's fragments load during the current MFMA chain (two register
-    // sets alternate); a relation change reloads the weight slice after the chain. The four
-    // waves read the same A rows (the three later reads hit L1 / L2).
-    __device__ static __forceinline__ void issue_direct(const RelGemmArgs& a, const Item& it, int lane,
-                                                        float4 (&f)[KH / 4], float& inv) {
-        const int r = min(lane & 31, it.nrows - 1);
-        const int h = lane >> 5;
-        int row = it.r0 + r;
-        const float* base;
-        inv = 1.0f;
-        if (it.root) {
-            base = a.Aroot;
-        } else if constexpr (DGRAD) {
-            base = a.Aroot;
-            inv = 1.0f / (float)a.s_cnt[row];  // reciprocal, as RelGemm::commit stores it
-            row = a.s_row[row];
-        } else {
-            base = a.Arel;
-            row -= a.sel_b;
-        }
-        const float4* src = reinterpret_cast<const float4*>(base + (size_t)row * K + h * KH);
-#pragma unroll
-        for (int j = 0; j < KH / 4; ++j) f[j] = src[j];
-    }
-
-    __device__ static void run_direct(const RelGemmArgs& a) {
-        const int tid = threadIdx.x;
-        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
-        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-        const int n_items = a.n_rel + a.n_root;
-        const int G = (int)gridDim.x;
-        const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
-        const int rng = g * q + min(g, rem) + ((int)blockIdx.x >> 3);
-        const int i_beg = (int)((long long)rng * n_items / G);
-        const int i_end = (int)((long long)(rng + 1) * n_items / G);
-        if (i_beg >= i_end) return;
-        const ItemTable tab = item_table(a, i_beg, i_end, lane);
-        auto get_item = [&](int i) { return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i); };
-        float4 fa[KH / 4], fb[KH / 4];
-        float inva = 1.0f, invb = 1.0f;
-        Item cur = get_item(i_beg);
-        issue_direct(a, cur, lane, fa, inva);
-        float b[KH];
-        load_b(cur.w, wave, lane, b);
-        // vh: fragments of item i (loaded one item earlier); vn: receive item i+1
-        auto body = [&](int i, float4 (&vh)[KH / 4], float& invh, float4 (&vn)[KH / 4], float& invn) {
-            const bool has1 = i + 1 < i_end;
-            const Item nxt = has1 ? get_item(i + 1) : cur;
-            if (has1) issue_direct(a, nxt, lane, vn, invn);
-            f32x16 acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-#pragma unroll
-            for (int j = 0; j < KH / 4; ++j) {
-                const float4 cf = vh[j];
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[4 * j], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[4 * j + 1], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[4 * j + 2], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[4 * j + 3], acc, 0, 0, 0);
-            }
-            // epilogue: accumulator register r = rows (r&3) + 8(r>>2) + 4h, column 32·wave + c;
-            // the dgrad row scale of row q sits in lane q (and q + 32) of invh
-            float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                float o = acc[r];
-                if constexpr (DGRAD) {
-                    const float d = __shfl(invh, row);
-                    if (!cur.root) o = o * d;
-                }
-                if (row < cur.nrows) Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
-            }
-            if (has1 && nxt.w != cur.w) load_b(nxt.w, wave, lane, b);  // after the chain: b is free
-            cur = nxt;
-        };
-        for (int i = i_beg; i < i_end; i += 2) {
-            body(i, fa, inva, fb, invb);
-            if (i + 1 >= i_end) break;
-            body(i + 1, fb, invb, fa, inva);
-        }
-    }
-
-    // Dynamic schedule (MPGNN_OPT_REL_QUEUE): workgroups b ≡ g (mod 8) form group g and take
-    // the items of [g·n/8, (g+1)·n/8) one at a time from the group's counter (atomicAdd), two
-    // grabs ahead of the MFMAs, instead of a fixed contiguous range — a workgroup slowed by
-    // memory contention takes fewer items. Items stay relation-ordered within a group (weight
-    // slices shared through the group's L2). The last workgroup of a group to finish resets its
-    // counters, so the next launch (stream order) starts from zero.
-    __device__ static void run_dynamic(const RelGemmArgs& a, float* smem) {
-        float* As = smem;                 // [2][32][lda]
-        float* Sc = smem + 2 * 32 * lda;  // [2][32] dgrad row scales
-        int* Sq = reinterpret_cast<int*>(Sc + 64);  // [2] grabbed item index
-        const int tid = threadIdx.x;
-        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
-        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-        const int n_items = a.n_rel + a.n_root;
-        const int G = (int)gridDim.x;
-        const int ng = min(8, G);  // every group has at least one member
-        const int grp = (int)blockIdx.x % ng;
-        const int lo = (int)((long long)grp * n_items / ng);
-        const int hi = (int)((long long)(grp + 1) * n_items / ng);
-        const int members = G / ng + (grp < G % ng ? 1 : 0);
-        int* ctr = a.queue + grp * 64;  // own 256-B line per counter
-        int* done = ctr + 32;
-        if (tid == 0) {
-            Sq[0] = lo + atomicAdd(ctr, 1);
-            Sq[1] = lo + atomicAdd(ctr, 1);
-        }
-        __syncthreads();
-        int cur_i = __builtin_amdgcn_readfirstlane(Sq[0]);
-        int nxt_i = __builtin_amdgcn_readfirstlane(Sq[1]);
-        if (cur_i < hi) {
-            float4 v[WPT];
-            int cnt;
-            Item cur = item(a, cur_i);
-            issue(a, cur, tid, v, cnt);
-            float b[KH];
-            load_b(cur.w, wave, lane, b);
-            commit(cur, tid, v, cnt, As, Sc);
-#pragma unroll
-            for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(b[j]));
-            __syncthreads();
-            int buf = 0, slot = 0;
-            while (true) {
-                const bool has_next = nxt_i < hi;
-                int nn = hi;
-                if (tid == 0 && has_next) nn = lo + atomicAdd(ctr, 1);  // read after the MFMAs
-                const Item nxt = has_next ? item(a, nxt_i) : cur;
-                if (has_next) issue(a, nxt, tid, v, cnt);
-                const bool new_w = nxt.w != cur.w;
-                float bn[KH];
-                if (new_w) load_b(nxt.w, wave, lane, bn);
-                const float* Ab = As + buf * 32 * lda + c * lda + h * KH;
-                f32x16 acc;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-                float4 af = *reinterpret_cast<const float4*>(Ab);
-#pragma unroll
-                for (int j = 0; j < KH; j += 4) {
-                    const float4 cf = af;
-                    if (j + 4 < KH) af = *reinterpret_cast<const float4*>(Ab + j + 4);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], acc, 0, 0, 0);
-                }
-                float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
-                const float* sc = Sc + buf * 32;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (row < cur.nrows) {
-                        float o = acc[r];
-                        if constexpr (DGRAD) {
-                            if (!cur.root) o = o * sc[row];
-                        }
-                        Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
-                    }
-                }
-                if (has_next) commit(nxt, tid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
-                if (tid == 0) Sq[slot] = nn;
-                if (new_w) {
-#pragma unroll
-                    for (int j = 0; j < KH; ++j) b[j] = bn[j];
-                }
-                __syncthreads();
-                const int nn_all = __builtin_amdgcn_readfirstlane(Sq[slot]);
-                slot ^= 1;
-                if (!has_next) break;
-                cur = nxt;
-                cur_i = nxt_i;
-                nxt_i = nn_all;
-                buf ^= 1;
-            }
-        }
-        if (tid == 0) {
-            if (atomicAdd(done, 1) == members - 1) {  // every member has stopped grabbing
-                atomicExch(ctr, 0);
-                atomicExch(done, 0);
-            }
         }
     }
 };
@@ -1698,505 +1267,7 @@ struct RelGemm {
 template <int KB, bool DGRAD, int NB = 1>
 __global__ __launch_bounds__(kThreads, 2) void rel_gemm_kernel(RelGemmArgs a) {
     extern __shared__ float smem[];
-    if constexpr (NB > 1 || KB > 2) {
-        RelGemm<KB, DGRAD, NB>::run(a, smem);  // wide shapes: the default schedule only
-    } else {
-        if (a.queue != nullptr) RelGemm<KB, DGRAD>::run_dynamic(a, smem);
-        else if (a.deep) RelGemm<KB, DGRAD>::run_deep(a, smem);
-        else RelGemm<KB, DGRAD>::run(a, smem);
-    }
-}
-
-template <int KB, bool DGRAD>
-__global__ __launch_bounds__(kThreads, 2) void rel_gemm_direct_kernel(RelGemmArgs a) {
-    RelGemm<KB, DGRAD>::run_direct(a);
-}
-
-template <int KB, bool DGRAD>
-__global__ __launch_bounds__(2 * kThreads, 1) void rel_gemm_pingpong_kernel(RelGemmArgs a) {
-    extern __shared__ float smem[];
-    RelGemm<KB, DGRAD>::run_pingpong(a, smem);
-}
-
-
-// ----------------------------------------------------------------------------------------
-// fused_mean_gemm_kernel — the forward layer core for F_in = F_out = 128 in one persistent
-// launch (one 512-thread workgroup per CU): the relation-typed segment means (PyG propagate,
-// mp_rgcn_layer.py:236) are formed in LDS and contracted with W_r on the matrix cores
-// (mp_rgcn_layer.py:245 / the RGCNConv loop), without a round trip of H through memory.
-//
-//   waves 4-7 ("gather"):  build item i+1's A tile in LDS buffer (i+1)%2 — for a relation tile,
-//       the means of its ≤ 32 segments: x rows of the edges (e_col, relation-major edge order)
-//       gathered 32 in flight per wave (one 512-B row per load instruction, readlane-broadcast
-//       addresses), each segment summed in edge order from 0.0f and divided by its GLOBAL count
-//       (IEEE); for a root tile, 32 rows of x.  The tile's edges are cut into four ranges of
-//       equal edge count, moved to segment starts unless the segment is longer than kSplitMax:
-//       segments up to kSplitMax edges are summed by one wave in the reference's exact order
-//       (bit-identical means); a longer one is summed as per-wave partials that the last wave
-//       to finish adds in edge order (LDS arrival counter).  Means are also written to H when
-//       the caller keeps them for the backward.
-//   waves 0-3 ("matrix"):  contract item i from LDS buffer i%2 with the relation's weight slice
-//       held in registers (wave w: columns [32w, 32w+32), as rel_gemm_kernel), prefetch the next
-//       relation run's slice, store the 32 output rows straight from the accumulators.
-// One barrier per item.  Items are 32-row relation-pure tiles (plan t32 tables) followed by
-// 32-node root tiles; workgroups take contiguous item ranges of equal prefix cost
-// (plan t32_cost, item_cost in plan_internal.h), consecutive ranges on one XCD.
-// ----------------------------------------------------------------------------------------
-struct FusedArgs {
-    const int* t_begin;
-    const int* t_end;
-    const int* t_cost;    // prefix cost per 32-row tile
-    int t_lo, n_rel, n_root;
-    const int* s_ptr;
-    const int* e_col;
-    const int* s_cnt;
-    const int* s_rel;
-    const float* x;
-    const float* W;
-    int w_per_rel;
-    const float* Wroot;
-    float* Y;
-    float* Yroot;
-    float* H;             // nullable: segment means [S_sel, 128] for the backward
-    int sel_b, row_lo, row_hi;
-    unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS): [wg][64] timeline, or nullptr
-};
-
-constexpr int kFusedThreads = 512;
-constexpr int kFusedLda = 128 + 4;
-constexpr int kSplitMax = 64;
-
-__device__ __forceinline__ int fused_cum(const FusedArgs& a, int i, int relsum) {
-    return i <= a.n_rel ? a.t_cost[a.t_lo + i] - a.t_cost[a.t_lo] : relsum + (i - a.n_rel) * kRootItemCost;
-}
-
-// smallest item index i with cum(i) >= target (cum is strictly increasing, cum(0) = 0)
-__device__ int fused_find(const FusedArgs& a, long long target, int relsum, int lane) {
-    if (target <= 0) return 0;
-    int lo = 0, hi = a.n_rel + a.n_root;
-    while (hi - lo > 1) {
-        const int span = hi - lo;
-        const int idx = min(hi, lo + (int)(((long long)(lane + 1) * span + 63) / 64));
-        const unsigned long long m = __ballot(fused_cum(a, idx, relsum) >= target);
-        const int f = __ffsll((long long)m) - 1;  // lane 63 samples hi: always set
-        const int nlo = f > 0 ? readlane(idx, f - 1) : lo;
-        hi = readlane(idx, f);
-        lo = nlo;
-    }
-    return hi;
-}
-
-struct FusedItem {
-    int r0, nrows, root;
-    const float* w;
-};
-
-__device__ __forceinline__ FusedItem fused_item(const FusedArgs& a, int i) {
-    FusedItem it;
-    it.root = i >= a.n_rel;
-    if (!it.root) {
-        it.r0 = ld_uniform(a.t_begin, a.t_lo + i);
-        it.nrows = ld_uniform(a.t_end, a.t_lo + i) - it.r0;
-        it.w = a.W + (a.w_per_rel ? (size_t)ld_uniform(a.s_rel, it.r0) * 128 * 128 : 0);
-    } else {
-        it.r0 = a.row_lo + (i - a.n_rel) * 32;
-        it.nrows = min(32, a.row_hi - it.r0);
-        it.w = a.Wroot;
-    }
-    return it;
-}
-
-// Gather waves run a two-item software pipeline: while item i+1's rows are gathered, item
-// i+2's segment table (s_ptr, s_cnt) is in flight, and once it lands the wave's edge range of
-// item i+2 is cut and its first 32 e_col entries are requested — so an item's gather starts with
-// its indices in registers and pays one memory round trip for its x rows.
-struct GatherStage {
-    int sp;     // lane l <= n: s_ptr[s0 + l] (lane n: end of the tile's edges)
-    int cntv;   // lane l < n: GLOBAL count of segment s0 + l
-    int pb, pe; // this wave's edge range
-    int col;    // e_col[pb + lane] (first 32 positions of the range)
-};
-
-__device__ __forceinline__ void gather_meta(const FusedArgs& a, const FusedItem& it, int lane, GatherStage& g) {
-    if (it.root) return;
-    g.sp = a.s_ptr[it.r0 + min(lane, it.nrows)];
-    g.cntv = a.s_cnt[it.r0 + min(lane, it.nrows - 1)];
-}
-
-// segment containing position p of a staged item (e0 <= p < e1)
-__device__ __forceinline__ int stage_seg(const GatherStage& g, int n, int p, int lane) {
-    return __popcll(__ballot(lane < n && g.sp <= p)) - 1;
-}
-
-// Cut the tile's edges into four ranges of equal edge count, moved to a segment start unless
-// that segment is longer than kSplitMax; then request the wave's first 32 e_col entries.
-__device__ __forceinline__ void gather_range(const FusedArgs& a, const FusedItem& it, int gw, int lane,
-                                             GatherStage& g) {
-    if (it.root) return;
-    const int n = it.nrows;
-    const int e0 = readlane(g.sp, 0), e1 = readlane(g.sp, n);
-    const int T = e1 - e0;
-    int cut_prev = e0;
-    g.pb = e0;
-    g.pe = e1;
-#pragma unroll
-    for (int k = 1; k <= 3; ++k) {
-        int c = e0 + (int)(((long long)T * k) / 4);
-        if (c < e1) {
-            const int m = stage_seg(g, n, c, lane);
-            const int st = readlane(g.sp, m);
-            if (readlane(g.sp, m + 1) - st <= kSplitMax) c = st;
-        }
-        c = max(c, cut_prev);
-        if (k == gw) g.pb = c;
-        if (k == gw + 1) g.pe = c;
-        cut_prev = c;
-    }
-    g.col = a.e_col[max(min(g.pb + lane, g.pe - 1), 0)];
-}
-
-// Sum the staged item into its A tile (see the kernel comment).
-__device__ void gather_sum(const FusedArgs& a, const FusedItem& it, const GatherStage& g, float* A, float* slot,
-                           int* slot_seg, int* ctr, int gw, int lane, unsigned long long* st) {
-    auto stamp = [&](int k) {
-        if (st != nullptr && gw == 0 && lane == 0) st[k] = stamp_now();
-    };
-    const int c2 = 2 * lane;
-    if (it.root) {
-        float2 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int row = gw + 4 * j;
-            v[j] = *reinterpret_cast<const float2*>(a.x + (size_t)(it.r0 + min(row, it.nrows - 1)) * 128 + c2);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int row = gw + 4 * j;
-            *reinterpret_cast<float2*>(A + row * kFusedLda + c2) = row < it.nrows ? v[j] : make_float2(0.f, 0.f);
-        }
-        return;
-    }
-    stamp(0);
-    const int n = it.nrows, s0 = it.r0;
-    for (int row = n + gw; row < 32; row += 4)
-        *reinterpret_cast<float2*>(A + row * kFusedLda + c2) = make_float2(0.f, 0.f);
-    if (lane == 0) {
-        slot_seg[2 * gw] = -1;
-        slot_seg[2 * gw + 1] = -1;
-    }
-    auto finish = [&](int t, float2 sum) {  // complete segment t: mean -> A row (and H)
-        const float d = (float)readlane(g.cntv, t);
-        const float2 mean = make_float2(sum.x / d, sum.y / d);
-        *reinterpret_cast<float2*>(A + t * kFusedLda + c2) = mean;
-        if (a.H != nullptr) *reinterpret_cast<float2*>(a.H + (size_t)(s0 + t - a.sel_b) * 128 + c2) = mean;
-    };
-    const int pb = g.pb, pe = g.pe;
-    if (pb < pe) {
-        int t = stage_seg(g, n, pb, lane);
-        int se = readlane(g.sp, t + 1);
-        bool head = readlane(g.sp, t) < pb;  // segment started in an earlier wave's range
-        const int tc0 = head ? t + 1 : t;    // first segment this wave completes
-        float2 acc = make_float2(0.f, 0.f);
-        constexpr int U = 32;
-        for (int p0 = pb; p0 < pe; p0 += U) {
-            const int cnt = min(U, pe - p0);
-            const int col = p0 == pb ? g.col : a.e_col[p0 + min(lane, cnt - 1)];
-            float2 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int r = readlane(col, min(u, cnt - 1));
-                v[u] = *reinterpret_cast<const float2*>(a.x + (size_t)r * 128 + c2);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (u < cnt) {
-                    acc.x += v[u].x;
-                    acc.y += v[u].y;
-                    if (p0 + u + 1 == se) {  // segment t ends here: its sum -> A row, or head slot
-                        float* dst = head ? slot + (2 * gw) * 128 : A + t * kFusedLda;
-                        *reinterpret_cast<float2*>(dst + c2) = acc;
-                        if (head && lane == 0) slot_seg[2 * gw] = t;
-                        head = false;
-                        acc = make_float2(0.f, 0.f);
-                        ++t;
-                        se = t < n ? readlane(g.sp, t + 1) : 0x7fffffff;
-                    }
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (t < n && readlane(g.sp, t) < pe && pe < se) {  // segment t continues past the range: partial
-            const int j = head ? 0 : 1;
-            *reinterpret_cast<float2*>(slot + (2 * gw + j) * 128 + c2) = acc;
-            if (lane == 0) slot_seg[2 * gw + j] = t;
-        }
-        stamp(1);
-        // divide the segments completed here (sums were parked in their A rows)
-        for (int tt = tc0; tt < t; ++tt) finish(tt, *reinterpret_cast<const float2*>(A + tt * kFusedLda + c2));
-    }
-    // last gather wave to arrive adds the partials of split segments in edge order (LDS writes
-    // drained first; no vmcnt wait, so the next item's prefetches stay in flight)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    int old = 0;
-    if (lane == 0) old = atomicAdd(ctr, 1);
-    old = readlane(old, 0);
-    if ((old & 3) == 3) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        int cur = -1;
-        float2 acc = make_float2(0.f, 0.f);
-        for (int k = 0; k < 8; ++k) {
-            const int sg = slot_seg[k];
-            if (sg < 0) continue;
-            const float2 v = *reinterpret_cast<const float2*>(slot + k * 128 + c2);
-            if (sg == cur) {
-                acc.x += v.x;
-                acc.y += v.y;
-            } else {
-                if (cur >= 0) finish(cur, acc);
-                cur = sg;
-                acc = v;
-            }
-        }
-        if (cur >= 0) finish(cur, acc);
-    }
-    stamp(2);
-}
-
-// Workgroup barrier that retires LDS traffic only: global loads in flight (prefetched indices,
-// the next relation's weight slice) and stores stay outstanding across it.
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
-
-__global__ __launch_bounds__(kFusedThreads, 1) void fused_mean_gemm_kernel(FusedArgs a) {
-    __shared__ float As[2 * 32 * kFusedLda];
-    __shared__ float slot[8 * 128];
-    __shared__ int slot_seg[8];
-    __shared__ int ctr;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, c = lane & 31, h = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool matrix = wave < 4;
-    const int gw = wave - 4;
-    const int n_items = a.n_rel + a.n_root;
-    // contiguous item range of equal prefix cost; ranges b, b+8, … on one XCD (speed only)
-    const int G = (int)gridDim.x;
-    const int g8 = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
-    const int rng = g8 * q + min(g8, rem) + ((int)blockIdx.x >> 3);
-    const int relsum = a.t_cost[a.t_lo + a.n_rel] - a.t_cost[a.t_lo];
-    const long long total = (long long)relsum + (long long)a.n_root * kRootItemCost;
-    unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 64 : nullptr;
-    auto stamp = [&](int k) {
-        if (stp != nullptr && lane == 0 && wave == 0 && k < 62) stp[k] = stamp_now();
-    };
-    if (stp != nullptr && tid == 0) stp[62] = __builtin_amdgcn_s_memrealtime();
-    stamp(0);
-    const int i_beg = fused_find(a, total * rng / G, relsum, lane);
-    const int i_end = fused_find(a, total * (rng + 1) / G, relsum, lane);
-    if (i_beg >= i_end || n_items == 0) return;
-    stamp(1);
-    if (tid == 0) ctr = 0;
-    __syncthreads();
-
-    constexpr int KH = 64;
-    float b[KH];
-    FusedItem cur = fused_item(a, i_beg);
-    GatherStage nx{};  // staged item i+1 (gather waves)
-    if (matrix) {
-        const float* p = cur.w + (size_t)(h * KH) * 128 + wave * 32 + c;
-#pragma unroll
-        for (int j = 0; j < KH; ++j) b[j] = p[j * 128];
-    } else {
-        GatherStage g0{};
-        gather_meta(a, cur, lane, g0);
-        gather_range(a, cur, gw, lane, g0);
-        if (i_beg + 1 < i_end) gather_meta(a, fused_item(a, i_beg + 1), lane, nx);
-        gather_sum(a, cur, g0, As, slot, slot_seg, &ctr, gw, lane, nullptr);
-        if (i_beg + 1 < i_end) gather_range(a, fused_item(a, i_beg + 1), gw, lane, nx);
-    }
-    lds_barrier();
-    stamp(2);
-    int buf = 0;
-    for (int i = i_beg; i < i_end; ++i) {
-        const bool has_next = i + 1 < i_end;
-        const FusedItem nxt = has_next ? fused_item(a, i + 1) : cur;
-        if (matrix) {
-            const bool new_w = nxt.w != cur.w;
-            float bn[KH];
-            if (new_w) {
-                const float* p = nxt.w + (size_t)(h * KH) * 128 + wave * 32 + c;
-#pragma unroll
-                for (int j = 0; j < KH; ++j) bn[j] = p[j * 128];
-            }
-            const float* Ab = As + buf * 32 * kFusedLda + c * kFusedLda + h * KH;
-            f32x16 acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-            float4 af = *reinterpret_cast<const float4*>(Ab);
-#pragma unroll
-            for (int j = 0; j < KH; j += 4) {
-                const float4 cf = af;
-                if (j + 4 < KH) af = *reinterpret_cast<const float4*>(Ab + j + 4);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], acc, 0, 0, 0);
-            }
-            float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * 128 : a.Y + (size_t)(cur.r0 - a.sel_b) * 128;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (row < cur.nrows) Yt[(size_t)row * 128 + wave * 32 + c] = acc[r];
-            }
-            stamp(3 + 5 * (i - i_beg));
-            if (new_w) {
-#pragma unroll
-                for (int j = 0; j < KH; ++j) b[j] = bn[j];
-            }
-        } else if (has_next) {
-            const bool has_next2 = i + 2 < i_end;
-            GatherStage nn{};
-            const FusedItem it2 = has_next2 ? fused_item(a, i + 2) : nxt;
-            if (has_next2) gather_meta(a, it2, lane, nn);
-            gather_sum(a, nxt, nx, As + (buf ^ 1) * 32 * kFusedLda, slot, slot_seg, &ctr, gw, lane,
-                       (stp != nullptr && 7 + 5 * (i - i_beg) < 62) ? stp + 4 + 5 * (i - i_beg) : nullptr);
-            if (has_next2) gather_range(a, it2, gw, lane, nn);
-            nx = nn;
-        }
-        lds_barrier();
-        stamp(7 + 5 * (i - i_beg));
-        cur = nxt;
-        buf ^= 1;
-    }
-    if (stp != nullptr && tid == 0) stp[63] = __builtin_amdgcn_s_memrealtime();
-}
-
-// ----------------------------------------------------------------------------------------
-// tile_gemm_ws_kernel — the same persistent tile GEMM with specialised waves (Kp ≤ 128).
-// One 512-thread workgroup per CU: waves 0-3 (one per SIMD) run the MFMA strips of item i from
-// LDS A buffer i%2 and park their accumulators in LDS staging buffer i%2; waves 4-7 meanwhile
-// load item i+1's A rows (global → registers → A buffer (i+1)%2) and store item i-1's output
-// rows (staging (i-1)%2 → global, float4).  One barrier per item; the memory phases of one item
-// and the matrix phase of its neighbour overlap by construction (with two identical workgroups
-// per CU they ran in lockstep and added up: tile_ablate.py).  Row scales (dgrad 1/cnt) are kept
-// in three rotating buffers: item i's are written during item i-1 and read during item i+1.
-// ----------------------------------------------------------------------------------------
-constexpr int kWsThreads = 512;
-
-template <int KB, bool TRANS, bool CLAMP, int ABL = 0>
-__device__ __forceinline__ void tile_gemm_ws_body(const TileGemmArgs& a, float* smem) {
-    constexpr int Kp = 64 * KB;
-    constexpr int KH = Kp / 2;
-    constexpr int lda = Kp + 4;
-    constexpr int ldo = kColTile + 4;
-    constexpr int WPT = 4 * KB;                 // float4 per memory thread per A tile
-    float* Abuf = smem;                         // [2][64][lda]
-    float* Stg = smem + 2 * kTileRows * lda;    // [2][64][ldo]
-    float* scales = Stg + 2 * kTileRows * ldo;  // [3][64]
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool mfma_wave = wave < 4;
-    const int n_items = (a.n_rel + a.n_root) * a.ncol;
-    const ItemOrder ord(n_items);
-    int w = ord.base;
-    if (w >= ord.end) return;
-
-    TileItem cur = tile_item(a, w);
-    float b0[kKC];
-    float4 v[WPT];  // memory waves: A rows of item i+2, loaded during item i (two items of lead)
-    int cnt_raw = 1;
-    if (mfma_wave) {
-        const int lane = threadIdx.x & 63;
-        const BLoader<TRANS, CLAMP> ld0(item_bsrc(a, cur), min(cur.n_base + wave * 32 + (lane & 31), a.N - 1));
-        ld0.template load_chunk<kKC>((lane >> 5) * KH, b0);
-    } else {
-        // the younger half loses VALU arbitration to the MFMA waves on every SIMD: a static
-        // priority lets its short latency-critical bursts through (MI355X_MICROARCH.md 8-wave note 4)
-        if (a.ws_prio) __builtin_amdgcn_s_setprio(1);
-        const int mt = threadIdx.x - 256;
-        tile_issue<KB, WPT>(a, cur, mt, v, cnt_raw);
-        tile_commit<KB, WPT>(a, cur, mt, v, cnt_raw, Abuf, scales);
-        if (w + ord.stride < ord.end) tile_issue<KB, WPT>(a, tile_item(a, w + ord.stride), mt, v, cnt_raw);
-    }
-    __syncthreads();
-    TileItem prev = cur;
-    unsigned long long* st = (a.stamps != nullptr && (threadIdx.x & 63) == 0 && (wave == 0 || wave == 4))
-                                 ? a.stamps + (size_t)blockIdx.x * 128 + (wave == 0 ? 0 : 8)
-                                 : nullptr;
-    for (int i = 0; w < ord.end; ++i) {
-        const int wn = w + ord.stride;
-        const bool has_next = wn < ord.end;
-        const TileItem nxt = has_next ? tile_item(a, wn) : cur;
-        if (st != nullptr && i < 8) st[i * 16 + 0] = stamp_now();
-        if (mfma_wave) {
-            const int tid = opaque(threadIdx.x);
-            const int lane = tid & 63;
-            const int c = lane & 31;
-            const int h = lane >> 5;
-            const float* A = Abuf + (i & 1) * kTileRows * lda;
-            const BLoader<TRANS, CLAMP> ld_next(item_bsrc(a, nxt), min(nxt.n_base + wave * 32 + c, a.N - 1));
-            const BLoader<TRANS, CLAMP> ld(item_bsrc(a, cur), min(cur.n_base + wave * 32 + c, a.N - 1));
-            f32x16 acc0, acc1;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                acc0[r] = 0.0f;
-                acc1[r] = 0.0f;
-            }
-            if (st != nullptr && i < 8) st[i * 16 + 4] = stamp_now();
-            mfma_strip<TRANS, CLAMP, ABL>(acc0, acc1, A + c * lda + h * KH, A + (32 + c) * lda + h * KH, KH, h * KH, ld,
-                                          b0, ld_next);
-            if (st != nullptr && i < 8) st[i * 16 + 5] = stamp_now();
-            float* o = Stg + (i & 1) * kTileRows * ldo + (4 * h) * ldo + wave * 32 + c;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = (r & 3) + 8 * (r >> 2);
-                o[row * ldo] = acc0[r];
-                o[(row + 32) * ldo] = acc1[r];
-            }
-        } else {
-            const int mt = opaque(threadIdx.x - 256);
-            // item i+1's rows were loaded during item i-1: commit them, then load item i+2's
-            if (has_next)
-                tile_commit<KB, WPT>(a, nxt, mt, v, cnt_raw, Abuf + ((i + 1) & 1) * kTileRows * lda,
-                                     scales + ((i + 1) % 3) * kTileRows);
-            if (st != nullptr && i < 8) st[i * 16 + 4] = stamp_now();
-            const int wn2 = wn + ord.stride;
-            if (wn2 < ord.end && !(a.ws_ablate & 2)) tile_issue<KB, WPT>(a, tile_item(a, wn2), mt, v, cnt_raw);
-            if (st != nullptr && i < 8) st[i * 16 + 5] = stamp_now();
-            if (i > 0 && !(a.ws_ablate & 1))
-                tile_store(a, prev, mt, Stg + ((i - 1) & 1) * kTileRows * ldo, scales + ((i - 1) % 3) * kTileRows);
-        }
-        if (st != nullptr && i < 8) st[i * 16 + 1] = stamp_now();
-        __syncthreads();
-        if (st != nullptr && i < 8) st[i * 16 + 2] = stamp_now();
-        if (!has_next && !mfma_wave)  // last item: its accumulators are staged now
-            tile_store(a, cur, threadIdx.x - 256, Stg + (i & 1) * kTileRows * ldo, scales + (i % 3) * kTileRows);
-        prev = cur;
-        cur = nxt;
-        w = wn;
-    }
-}
-
-template <int KB>  // Kp = 64·KB ≤ 128
-__global__ __launch_bounds__(kWsThreads, 1) void tile_gemm_ws_kernel(TileGemmArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    if constexpr (KB == 2) {
-        if (a.ws_ablate & 4) {  // profiling: MFMA waves use constant B (no weight loads)
-            tile_gemm_ws_body<2, false, false, 2>(a, smem);
-            return;
-        }
-    }
-    const bool exact_k = a.K == 64 * KB && a.K >= kKC;
-    const int ldw = a.trans ? a.K : a.N;
-    if (!a.trans) {
-        if (exact_k) tile_gemm_ws_body<KB, false, false>(a, smem);
-        else tile_gemm_ws_body<KB, false, true>(a, smem);
-    } else {
-        if (exact_k && (ldw & 3) == 0) tile_gemm_ws_body<KB, true, false>(a, smem);
-        else tile_gemm_ws_body<KB, true, true>(a, smem);
-    }
+    RelGemm<KB, DGRAD, NB>::run(a, smem);
 }
 
 template <int KB>  // Kp = 64·KB
@@ -2212,13 +1283,6 @@ __global__ __launch_bounds__(kThreads, 2) void tile_gemm_kernel(TileGemmArgs a) 
         if (exact_k && (ldw & 3) == 0) tile_gemm_body<KB, true, false>(a, smem);
         else tile_gemm_body<KB, true, true>(a, smem);
     }
-}
-
-// profiling-only ablated builds of the bench shape (K = 128, B not transposed)
-template <int ABL>
-__global__ __launch_bounds__(kThreads, 2) void tile_gemm_ablate_kernel(TileGemmArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    tile_gemm_body<2, false, false, ABL>(a, smem);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -2240,7 +1304,6 @@ struct RowSumArgs {
     const int* cnt;     // nullable: divide row i by cnt[i] (segment means)
     int out_off;        // out row = i - out_off
     float* out;         // [*, F]
-    unsigned long long* stamps;  // debug (MPGNN_OPT_STAMPS, means launch): [wave][8] timeline
     const int* res;     // resolved entries of the ragged list g.ent (gather_rows_kernel)
 };
 
@@ -2271,8 +1334,6 @@ __global__ __launch_bounds__(kThreads) void row_sum_kernel(RowSumArgs a) {
     const int lane = threadIdx.x & 63;
     const int row0 = a.r_begin + (blockIdx.x * kWaves + wave) * kSumRowsPerWave;
     if (row0 >= a.N) return;
-    unsigned long long t_start = 0;
-    if (a.stamps != nullptr) t_start = stamp_now();
     const int wn = min(kSumRowsPerWave, a.N - row0);
     int bnd = 0;
     if (lane <= kSumRowsPerWave) {
@@ -2335,27 +1396,10 @@ __global__ __launch_bounds__(kThreads) void row_sum_kernel(RowSumArgs a) {
         }
         zero_acc<V, T>(acc);
     };
-    unsigned long long t_pro = 0;
-    if (a.stamps != nullptr) {
-        __builtin_amdgcn_s_waitcnt(0);  // debug timeline only: prologue loads landed
-        t_pro = stamp_now();
-    }
     wave_gather<V, T, (V * T <= 2 ? 8 : 4), kSumRowsPerWave>(
         a.g, bnd, wn, lane, [&](int r, bool live, float (&acc)[T][V]) {
             dispatch_row<kSumRowsPerWave>(r, [&](auto RI) { flush_row(RI, live, acc); });
         });
-    if (a.stamps != nullptr && lane == 0) {
-        const unsigned long long t_end = stamp_now();
-        unsigned long long* o = a.stamps + ((size_t)blockIdx.x * kWaves + wave) * 8;
-        o[0] = t_start;
-        o[1] = t_pro;
-        o[2] = t_end;
-        o[3] = (unsigned long long)(readlane(bnd, wn) - readlane(bnd, 0));  // entries
-        o[4] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));     // HW_REG_HW_ID
-        o[5] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));    // HW_REG_XCC_ID
-        o[6] = (unsigned long long)wn;
-        o[7] = 1;
-    }
 }
 
 
@@ -2487,119 +1531,6 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// flat_rows_multi_kernel — as flat_rows_kernel, but each wave walks CPW consecutive chunks and
-// fetches the next chunk's metadata (chunk bounds, node ids, row ids) while the current chunk's
-// first rows are in flight (MPGNN_OPT_FLAT_CPW).
-template <int V, int T, int U, int CPW>
-__global__ __launch_bounds__(kThreads) void flat_rows_multi_kernel(FlatArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int c0 = a.c_lo + ((int)blockIdx.x * kWaves + (int)(threadIdx.x >> 6)) * CPW;
-    if (c0 >= a.c_hi) return;
-    const int c_end = min(a.c_hi, c0 + CPW);
-    const int F = a.F;
-    int m_p0, m_n, m_info, m_val, m_row;
-    auto load_meta = [&](int c) {
-        m_p0 = ld_uniform(a.chunk_ptr, c);
-        m_n = ld_uniform(a.chunk_ptr, c + 1) - m_p0;
-        m_info = ld_uniform(a.chunk_info, c);
-        const int q = m_p0 + min(lane, m_n - 1);
-        m_val = a.table[q];
-        m_row = a.row_of[q];
-    };
-    load_meta(c0);
-    for (int c = c0; c < c_end; ++c) {
-    const int n = m_n, info = m_info, val = m_val, row = m_row;
-    bool prefetched = false;
-    bool keep = lane < n;
-    const bool isx = val < 0;  // augmented lists: the row's trailing extra entry
-    if (a.filter) keep = keep && (isx || (val >= a.flo && val < a.fhi));
-    const int srow = keep ? (isx ? -val - 1 : val - a.idx_off) : 0;
-    const unsigned long long xm = __ballot(keep && isx);
-    const bool has_cnt = a.cnt != nullptr;
-    const int cnt_l = (has_cnt ? a.cnt : a.dummy)[has_cnt ? row : 0];
-    const int next = __shfl_down(row, 1);
-    const unsigned long long lastm = __ballot(lane < n && (lane == n - 1 || next != row));
-    const unsigned long long keepm = __ballot(keep);
-    const int rf = readlane(row, 0);
-    const int rl = readlane(row, n - 1);
-    const bool fs = info & 1, ls = info & 2;
-    const int slot0 = info >> 2;
-    int colc[T];
-#pragma unroll
-    for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, F - V);
-    const bool has_b = a.bias != nullptr;
-    float bb[T][V];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-        vload<V>(has_b ? a.bias + colc[t] : a.src, bb[t]);
-#pragma unroll
-        for (int k = 0; k < V; ++k) bb[t][k] = has_b ? bb[t][k] : 0.0f;
-    }
-
-    float acc[T][V];
-    zero_acc<V, T>(acc);
-    for (int u0 = 0; u0 < n; u0 += U) {
-        float v[U][T][V];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int q = min(u0 + u, n - 1);
-            const int r = readlane(srow, q);
-            const float* base = (((xm >> q) & 1ull) ? a.extra : a.src) + (size_t)r * F;
-#pragma unroll
-            for (int t = 0; t < T; ++t) vload<V>(base + colc[t], v[u][t]);
-        }
-        if (!prefetched && c + 1 < c_end) {  // next chunk's metadata behind this chunk's rows
-            load_meta(c + 1);
-            prefetched = true;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int q = u0 + u;
-            if (q < n) {
-                if ((keepm >> q) & 1ull) {
-#pragma unroll
-                    for (int t = 0; t < T; ++t)
-#pragma unroll
-                        for (int k = 0; k < V; ++k) acc[t][k] += v[u][t][k];
-                }
-                if ((lastm >> q) & 1ull) {
-                    const int rr = readlane(row, q);
-                    const bool split = (rr == rf && fs) || (rr == rl && ls);
-                    float* dst;
-                    bool div = false, addb = false;
-                    if (!split) {
-                        dst = a.out + (size_t)(rr - a.row_off) * F;
-                        div = has_cnt;
-                        addb = has_b && rr >= a.lo && rr < a.hi;
-                    } else {
-                        const int slot = slot0 + ((fs && rr == rl && rl != rf) ? 1 : 0);
-                        dst = a.carry + (size_t)slot * F;
-                    }
-                    const float d = (float)readlane(cnt_l, q);
-#pragma unroll
-                    for (int t = 0; t < T; ++t) {
-                        const int col = (t * 64 + lane) * V;
-                        if (col < F) {
-                            float o[V];
-#pragma unroll
-                            for (int k = 0; k < V; ++k) {
-                                o[k] = div ? acc[t][k] / d : acc[t][k];
-                                if (addb) o[k] = o[k] + bb[t][k];
-                                if (!split && a.relu) o[k] = relu_f(o[k]);
-                            }
-                            vstore<V>(dst + col, o);
-                        }
-                    }
-                    zero_acc<V, T>(acc);
-                }
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
     }
 }
 
@@ -2936,6 +1867,7 @@ struct OuterArgs {
 constexpr int kOuterLd = 288;                        // one row pair: 128 + 32 pad + 128
 __device__ __forceinline__ int outer_row(int k) { return (k >> 1) * kOuterLd + (k & 1) * 160; }
 constexpr int kOuterBuf = (kSlice / 2) * kOuterLd;   // floats per 32-row matrix image
+constexpr int kOuterBlock = 32;                      // rows per accumulation block (a multiple of SL)
 
 // SL: rows per slice (32, or 16 = half the LDS, three workgroups per CU: MPGNN_OPT_OUTER_SLICE)
 template <bool VEC, int SL = kSlice>
@@ -3023,12 +1955,18 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
         }
     };
 
-    f32x16 acc[4];
+    // acc sums one block of kOuterBlock rows (an fma chain of kOuterBlock products), tot the
+    // blocks in row order: the rounding chain of a chunk of n rows is kOuterBlock + n/kOuterBlock
+    // instead of n (same for the bias column sums: bblk per block, bsum over blocks)
+    f32x16 acc[4], tot[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
-    float bsum = 0.0f;
+        for (int r = 0; r < 16; ++r) {
+            acc[q][r] = 0.0f;
+            tot[q][r] = 0.0f;
+        }
+    float bsum = 0.0f, bblk = 0.0f;
     const bool do_bsum = a.Pb != nullptr && blockIdx.y == 0 && tid < kColTile;
 
     if (nslices > 0) {
@@ -3056,7 +1994,7 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
 #pragma unroll
             for (int r = 0; r < SL; ++r) bl[r] = Bl[outer_row(r) + tid];
 #pragma unroll
-            for (int r = 0; r < SL; ++r) bsum += bl[r];
+            for (int r = 0; r < SL; ++r) bblk += bl[r];
         }
         // k-step t covers rows 2t (lanes h = 0) and 2t + 1 (h = 1); rows >= nr are zero
         const float* Ar = cur + outer_row(h) + c;
@@ -3080,6 +2018,17 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
             for (int q = 0; q < 4; ++q) av[q] = an[q];
             bv = bn;
         }
+        if (((sl + 1) * SL) % kOuterBlock == 0 || !more) {  // block boundary (uniform)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    tot[q][r] += acc[q][r];
+                    acc[q][r] = 0.0f;
+                }
+            bsum += bblk;
+            bblk = 0.0f;
+        }
         if (more) commit(sl + 1, bufs + ((sl + 1) & 1) * 2 * OB);
         __syncthreads();
     }
@@ -3101,7 +2050,7 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m_base + q * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < a.M) D[(size_t)m * a.Nn + col] = acc[q][r];
+                if (m < a.M) D[(size_t)m * a.Nn + col] = tot[q][r];
             }
         }
     }
@@ -3117,7 +2066,7 @@ __global__ __launch_bounds__(kThreads, 2) void outer_accum_kernel(OuterArgs a) {
 // blocks [0, n_a) take `a`, the rest `b` (the root part alone is ~60-110 workgroups, a
 // mostly idle chip for a whole launch).
 template <bool VEC, int SL>
-__global__ __launch_bounds__(kThreads, SL == 32 ? 2 : SL == 16 ? 3 : 4) void outer_accum2_kernel(OuterArgs a, OuterArgs b, int n_a) {
+__global__ __launch_bounds__(kThreads, 2) void outer_accum2_kernel(OuterArgs a, OuterArgs b, int n_a) {
     if ((int)blockIdx.x < n_a) outer_accum_body<VEC, SL>(a, (int)blockIdx.x);
     else outer_accum_body<VEC, SL>(b, (int)blockIdx.x - n_a);
 }
@@ -3145,23 +2094,26 @@ __device__ __forceinline__ void reduce_slabs_body(const ReduceArgs& a, const int
     }
     if (c1 - c0 == 1 && a.skip_single) return;  // written directly by outer_accum_kernel
     // slabs are read 32 at a time (independent loads in flight: a chained loop paid one L2
-    // round trip per chunk), then added in chunk order
+    // round trip per chunk); each block of 32 is summed as a pairwise tree (slabs past the end
+    // enter as 0), the blocks in chunk order: fixed order (deterministic), rounding chain
+    // 5 + blocks instead of one add per chunk
     constexpr int kB = 32;
     float s = 0.0f;
     const float* P = a.P + e;
     for (int cb = c0; cb < c1; cb += kB) {
         float v[kB];
 #pragma unroll
-        for (int u = 0; u < kB; ++u) v[u] = P[(size_t)min(cb + u, c1 - 1) * a.elems];
+        for (int u = 0; u < kB; ++u) v[u] = cb + u < c1 ? P[(size_t)(cb + u) * a.elems] : 0.0f;
 #pragma unroll
-        for (int u = 0; u < kB; ++u)
-            if (cb + u < c1) s += v[u];
+        for (int w = kB / 2; w >= 1; w >>= 1)
+#pragma unroll
+            for (int u = 0; u < w; ++u) v[u] = v[u] + v[u + w];
+        s += v[0];
     }
     const int d = a.gdst != nullptr ? a.gdst[a.g_base + g] : g;
     a.dst[(size_t)d * a.elems + e] = s;
 }
 
-__global__ __launch_bounds__(kThreads) void reduce_slabs_kernel(ReduceArgs a) { reduce_slabs_body(a, (int)blockIdx.x); }
 
 // Up to three reductions (dW groups, droot, dbias) in one launch: blocks [0, n0) → r0,
 // [n0, n0 + n1) → r1, the rest → r2; grid.y covers the widest.
@@ -3393,63 +2345,9 @@ static void launch_tile_gemm_kb(const TileGemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((tile_gemm_kernel<KB>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
-template <int ABL>
-static void launch_tile_gemm_abl(const TileGemmArgs& a, hipStream_t st) {
-    constexpr int lda = 64 * 2 + 4;
-    constexpr int ldo = kColTile + 4;
-    const size_t lds = (size_t)(2 * kTileRows * (lda > ldo ? lda : ldo) + 2 * kTileRows) * sizeof(float);
-    const int n_items = (a.n_rel + a.n_root) * a.ncol;
-    const int grid = std::min(n_items, cu_count() * 2);
-    hipLaunchKernelGGL((tile_gemm_ablate_kernel<ABL>), dim3(grid), dim3(kThreads), lds, st, a);
-}
-
-static bool g_tile_ws = false;  // MPGNN_OPT_TILE_WS: wave-specialised tile GEMM for Kp <= 128 (off: equal speed today)
-static int g_ws_prio = 1;      // MPGNN_OPT_TILE_WS value 2: memory waves without priority (profiling)
-
-template <int KB>
-static void launch_tile_gemm_ws(const TileGemmArgs& a, hipStream_t st) {
-    constexpr int lda = 64 * KB + 4;
-    constexpr int ldo = kColTile + 4;
-    const size_t lds = (size_t)(2 * kTileRows * lda + 2 * kTileRows * ldo + 3 * kTileRows) * sizeof(float);
-    const int n_items = (a.n_rel + a.n_root) * a.ncol;
-    const int grid = std::min(n_items, cu_count());
-    hipLaunchKernelGGL((tile_gemm_ws_kernel<KB>), dim3(grid), dim3(kWsThreads), lds, st, a);
-}
-
 
 static bool g_rel_wide = true;  // MPGNN_OPT_REL_WIDE: B-stationary GEMM also for F_in = F_out = 256 (C5)
-static bool g_rel_pingpong = false;  // MPGNN_OPT_REL_PINGPONG: two wave groups alternating MFMA / memory phases
-static bool g_rel_direct = false; // MPGNN_OPT_REL_DIRECT: LDS-free rel_gemm (waves load their own A fragments)
-static bool g_rel_deep = false;   // MPGNN_OPT_REL_DEEP: rel_gemm A rows two items ahead
-static bool g_dgrad_idx_ahead = true;   // MPGNN_OPT_DGRAD_IDX_AHEAD: dgrad rel_gemm loads gathered row numbers one item early
-static int g_outer_slice = 16;          // MPGNN_OPT_OUTER_SLICE: rows per LDS slice of the merged outer launch (32 or 16)
-static bool g_outer_root_first = true;  // MPGNN_OPT_OUTER_ROOT_FIRST: root / bias chunks dispatched before the dW chunks
-static bool g_merge_grad = true;  // MPGNN_OPT_MERGE_GRAD: dW + droot/dbias in one outer launch, one reduce launch
-static bool g_rel_queue = false;  // MPGNN_OPT_REL_QUEUE: dynamic item schedule in rel_gemm_kernel
-static std::mutex g_queue_mu;
-static std::vector<std::pair<hipStream_t, int*>> g_queues;  // per launch stream: 8 groups × 64 ints, zeroed
-
-// The counters of a stream (allocated and zeroed on first use; never while the stream is
-// being captured into a graph — the static schedule runs instead).
-static int* rel_queue(hipStream_t st) {
-    std::lock_guard<std::mutex> lk(g_queue_mu);
-    for (auto& q : g_queues)
-        if (q.first == st) return q.second;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    int* d = nullptr;
-    if (hipMalloc(&d, 8 * 64 * sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemset(d, 0, 8 * 64 * sizeof(int)) != hipSuccess) {
-        (void)hipFree(d);
-        return nullptr;
-    }
-    g_queues.push_back({st, d});
-    return d;
-}
-static int g_rel_stagger = 0;    // MPGNN_OPT_REL_STAGGER: s_sleep quanta for the second half of the grid
-static int g_rel_wg_per_cu = 2;  // MPGNN_OPT_REL_WGS: rel_gemm_kernel workgroups per CU (1 or 2)
 static bool g_rel_gemm = true;  // MPGNN_OPT_REL_GEMM: B-stationary GEMM for K ∈ {64, 128}, N = 128
-static bool g_fused = false;    // MPGNN_OPT_FUSED: fused means + transform for F_in = F_out = 128 (opt-in: latency-bound today)
 
 template <int KB, bool DGRAD, int NB>
 static void launch_rel_gemm_wide(const RelGemmArgs& a, hipStream_t st) {
@@ -3463,18 +2361,9 @@ static void launch_rel_gemm_wide(const RelGemmArgs& a, hipStream_t st) {
 template <int KB, bool DGRAD>
 static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
     constexpr int lda = 64 * KB + 4;
-    const size_t lds = (size_t)(2 * 32 * lda + 64 + 4) * sizeof(float);
+    const size_t lds = (size_t)(2 * 32 * lda + 64 + 4 + (DGRAD ? 4 * 16 * 64 : 0)) * sizeof(float);
     const int n_items = a.n_rel + a.n_root;
-    const int grid = std::min(n_items, cu_count() * g_rel_wg_per_cu);
-    if (a.deep == 2) {
-        hipLaunchKernelGGL((rel_gemm_direct_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), 0, st, a);
-        return;
-    }
-    if (a.deep == 3) {
-        hipLaunchKernelGGL((rel_gemm_pingpong_kernel<KB, DGRAD>), dim3(std::min(n_items, cu_count())),
-                           dim3(2 * kThreads), 2 * lds, st, a);
-        return;
-    }
+    const int grid = std::min(n_items, cu_count() * 2);  // two workgroups per CU
     hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
@@ -3493,25 +2382,7 @@ static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, hipStream_t
     }
 }
 
-static void launch_tile_gemm(const TileGemmArgs& a, hipStream_t st, int abl = 0) {
-    if (abl == 0 && g_tile_ws && round_up(a.K, 64) <= 128) {
-        if (round_up(a.K, 64) <= 64) launch_tile_gemm_ws<1>(a, st);
-        else launch_tile_gemm_ws<2>(a, st);
-        return;
-    }
-    if (abl != 0 && a.K == 128 && !a.trans) {
-        switch (abl) {
-            case 1: launch_tile_gemm_abl<1>(a, st); return;
-            case 2: launch_tile_gemm_abl<2>(a, st); return;
-            case 3: launch_tile_gemm_abl<3>(a, st); return;
-            case 4: launch_tile_gemm_abl<4>(a, st); return;
-            case 6: launch_tile_gemm_abl<6>(a, st); return;
-            case 8: launch_tile_gemm_abl<8>(a, st); return;
-            case 9: launch_tile_gemm_abl<9>(a, st); return;
-            case 14: launch_tile_gemm_abl<14>(a, st); return;
-            default: break;
-        }
-    }
+static void launch_tile_gemm(const TileGemmArgs& a, hipStream_t st) {
     const int kb = (round_up(a.K, 64)) / 64;
     if (kb <= 1) launch_tile_gemm_kb<1>(a, st);
     else if (kb == 2) launch_tile_gemm_kb<2>(a, st);
@@ -3537,8 +2408,6 @@ static void launch_piece(const PieceArgs& a, hipStream_t st) {
 }
 
 static bool g_exact_order = false;  // MPGNN_OPT_EXACT_ORDER: no ragged pieces anywhere
-static int g_ablate = 0;            // MPGNN_OPT_ABLATE (debug/profiling only)
-static unsigned long long* g_stamps = nullptr;  // MPGNN_OPT_STAMPS (debug/profiling only)
 
 struct Selection {
     int64_t d_lo = 0, d_hi = 0;
@@ -3697,8 +2566,7 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
     }
     // B-stationary GEMM (weights in registers per relation run) for the bench shapes
     if (gather_kind != 0 && W != nullptr && g_rel_gemm && (((K == 64 || K == 128) && N == 128) || (K == 256 && N == 256 && g_rel_wide)) &&
-        g_ablate == 0 &&
-        (!g_stamps || !g_tile_ws) && trans == (gather_kind == 1 ? 1 : 0)) {
+        trans == (gather_kind == 1 ? 1 : 0)) {
         RelGemmArgs r{};
         r.t_begin = p->d.t32_begin;
         r.t_end = p->d.t32_end;
@@ -3719,22 +2587,12 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         r.sel_b = s.sel_b;
         r.row_lo = (int)row_lo;
         r.row_hi = (int)row_hi;
-        r.stamps = (kind == MPGNN_K_SEG_FWD) ? g_stamps : nullptr;
-        r.stagger = g_rel_stagger;
-        r.queue = (g_rel_queue && !g_stamps) ? rel_queue(strm) : nullptr;
-        r.deep = g_stamps ? 0 : (g_rel_pingpong ? 3 : (g_rel_direct ? 2 : (g_rel_deep ? 1 : 0)));
-        r.idx_ahead = g_dgrad_idx_ahead ? 1 : 0;
-        if (K == 256) {  // the wide kernel runs the default schedule only
-            r.deep = 0;
-            r.queue = nullptr;
-        }
         TimedLaunch tl(kind, strm);
         launch_rel_gemm(r, K, gather_kind == 1, strm);
         return hip_check(hipGetLastError(), "rel_gemm_kernel launch");
     }
     // tile_gemm stages A rows as float4 (K % 4 == 0); other widths take seg_tile_kernel
-    if (gather_kind != 0 && W != nullptr && (K & 3) == 0 && (g_ablate & 15) == 0 &&
-        (!g_stamps || (g_tile_ws && round_up(K, 64) <= 128))) {
+    if (gather_kind != 0 && W != nullptr && (K & 3) == 0) {
         TileGemmArgs t{};
         t.tile_begin = p->d.tile_begin;
         t.tile_end = p->d.tile_end;
@@ -3760,11 +2618,8 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         t.row_hi = (int)row_hi;
         t.y_div = gather_kind == 1;
         t.sel_b = s.sel_b;
-        t.stamps = (kind == MPGNN_K_SEG_FWD) ? g_stamps : nullptr;
-        t.ws_prio = g_ws_prio;
-        t.ws_ablate = (g_ablate >> 8) & 7;
         TimedLaunch tl(kind, strm);
-        launch_tile_gemm(t, strm, (g_ablate >> 4) & 15);  // bits 4-7: two-workgroup kernel ablations
+        launch_tile_gemm(t, strm);
         return hip_check(hipGetLastError(), "tile_gemm_kernel launch");
     }
     SegTileArgs a{};
@@ -3796,8 +2651,6 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
     a.sel_b = s.sel_b;
     a.H = H;
     a.Hsrc = Hsrc;
-    a.ablate = g_ablate;
-    a.stamps = (kind == MPGNN_K_SEG_FWD) ? g_stamps : nullptr;
     const int ncol = W ? (N + kColTile - 1) / kColTile : 1;
     TimedLaunch tl(kind, strm);
     MPGNN_VT_DISPATCH(V, T, launch_seg, a, n_rel + n_root, ncol, strm);
@@ -3828,7 +2681,7 @@ static void launch_gather_rows(const GatherRowsArgs& a, hipStream_t st) {
 static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, const int* pe, int k_lo, int k_hi,
                           float* P, hipStream_t strm) {
     a.g.dummy = p->d.s_ptr;  // S + 1 >= 1 entries: always a valid target
-    const bool vec = (a.g.F & 3) == 0 && a.g.F <= kMaxF && a.stamps == nullptr;
+    const bool vec = (a.g.F & 3) == 0 && a.g.F <= kMaxF;
     int V, T;
     pick_vt(a.g.F, &V, &T);
     if (k_hi > k_lo) {
@@ -3908,28 +2761,9 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
     return hip_check(hipGetLastError(), "row_sum_kernel launch");
 }
 
-static int g_flat_cpw = 1;  // MPGNN_OPT_FLAT_CPW: chunks per wave in the flat row-sum kernel (1, 2 or 4)
-static int g_flat_u = 16;  // MPGNN_OPT_FLAT_U: rows in flight per wave in flat_rows_kernel (16 or 32; 32 for V·T <= 2 only)
-
 template <int V, int T>
 static void launch_flat(const FlatArgs& a, hipStream_t st) {
     const int n = a.c_hi - a.c_lo;
-    if constexpr (V * T <= 2) {
-        if (g_flat_u == 32) {
-            hipLaunchKernelGGL((flat_rows_kernel<V, T, 32>), dim3((n + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
-            return;
-        }
-    }
-    if (g_flat_cpw == 2) {
-        hipLaunchKernelGGL((flat_rows_multi_kernel<V, T, 16, 2>), dim3((n + 2 * kWaves - 1) / (2 * kWaves)), dim3(kThreads),
-                           0, st, a);
-        return;
-    }
-    if (g_flat_cpw == 4) {
-        hipLaunchKernelGGL((flat_rows_multi_kernel<V, T, 16, 4>), dim3((n + 4 * kWaves - 1) / (4 * kWaves)), dim3(kThreads),
-                           0, st, a);
-        return;
-    }
     hipLaunchKernelGGL((flat_rows_kernel<V, T>), dim3((n + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
 }
 
@@ -4034,7 +2868,7 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
 static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x, int F, float* H, float* Pseg,
                          bool exact, hipStream_t strm) {
     if (s.sel_e == s.sel_b) return MPGNN_OK;
-    if (!exact && g_stamps == nullptr) {
+    if (!exact) {
         // flat chunked list; chunks and splits of the relation range [d_lo, d_hi)
         FlatRun f{};
         f.fd = &p->d.seg_f;
@@ -4066,92 +2900,7 @@ static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x
     a.cnt = p->d.s_cnt;
     a.out = H;
     a.out_off = s.sel_b;
-    a.stamps = g_stamps != nullptr ? g_stamps + (1u << 20) : nullptr;  // after the tile kernel's region
     return run_rowsum(p, a, p->d.seg_pb, p->d.seg_pe, ragged ? s.sp_lo : 0, ragged ? s.sp_hi : 0, Pseg, strm);
-}
-
-// ----------------------------------------------------------------------------------------
-// Overlapped forward (MPGNN_OPT_OVERLAP): the segment means (gather-bound, flat_rows_kernel)
-// and the transform (MFMA-bound, rel_gemm_kernel / tile_gemm_kernel) of one layer run on two
-// streams.  The relation range is cut into G groups of about equal segment count; the caller's
-// stream computes the means group by group and records an event after each; a second
-// (high-priority) stream first transforms the root rows (x @ root needs no means, so it runs
-// beside group 0's means), then each group's segment rows as soon as its event fires, and
-// the caller's stream joins it before the combine.  Same kernels, same work, same results
-// (each output element is produced by the same kernel code from the same inputs).
-// ----------------------------------------------------------------------------------------
-constexpr int kMaxOverlapGroups = 8;
-static int g_overlap = 0;  // groups; 0 (default) = off: one stream. Measured slower at C3
-
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t in = nullptr, done = nullptr, grp[kMaxOverlapGroups] = {};
-    bool ok = false, failed = false;
-};
-static SideStream g_side[64];
-static std::mutex g_side_mu;
-
-static SideStream* side_stream(int device) {
-    if (device < 0 || device >= 64) return nullptr;
-    int cur = -1;
-    if (hipGetDevice(&cur) != hipSuccess || cur != device) return nullptr;
-    std::lock_guard<std::mutex> lk(g_side_mu);
-    SideStream& ss = g_side[device];
-    if (ss.ok) return &ss;
-    if (ss.failed) return nullptr;
-    int lo = 0, hi = 0;
-    bool good = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
-                hipStreamCreateWithPriority(&ss.s, hipStreamNonBlocking, hi) == hipSuccess &&
-                hipEventCreateWithFlags(&ss.in, hipEventDisableTiming) == hipSuccess &&
-                hipEventCreateWithFlags(&ss.done, hipEventDisableTiming) == hipSuccess;
-    for (int g = 0; good && g < kMaxOverlapGroups; ++g)
-        good = hipEventCreateWithFlags(&ss.grp[g], hipEventDisableTiming) == hipSuccess;
-    ss.ok = good;
-    ss.failed = !good;
-    return good ? &ss : nullptr;
-}
-
-// Means + transform of the selection s with the overlap above. H / Y rows are offset from
-// s.sel_b, Yroot rows from row_lo (as in the one-stream path).
-static int32_t fwd_overlapped(const mpgnn_plan* p, int32_t mode, const Selection& s, int groups, SideStream* ss,
-                              const float* x, int F_in, const float* weight, const float* root, int F_out, float* H,
-                              float* Pseg, float* Y, float* Yroot, int64_t row_lo, int64_t row_hi, hipStream_t strm) {
-    int32_t st = hip_check(hipEventRecord(ss->in, strm), "hipEventRecord");
-    if (st == MPGNN_OK) st = hip_check(hipStreamWaitEvent(ss->s, ss->in, 0), "hipStreamWaitEvent");
-    if (st != MPGNN_OK) return st;
-    if (root != nullptr) {  // root rows: no dependency on the means
-        Selection none = s;
-        none.t_lo = none.t_hi = none.t32_lo = none.t32_hi = 0;
-        st = run_seg(p, mode, none, 2, x, F_in, weight, root, 0, F_out, Y, Yroot, row_lo, row_hi, nullptr, nullptr,
-                     true, MPGNN_K_SEG_FWD, ss->s, H);
-        if (st != MPGNN_OK) return st;
-    }
-    const int64_t S_sel = s.sel_e - s.sel_b;
-    int64_t d = s.d_lo;
-    for (int g = 0; g < groups && d < s.d_hi; ++g) {
-        // group g ends at the first relation boundary at or past (g+1)/G of the segments
-        const int64_t target = s.sel_b + (S_sel * (g + 1) + groups - 1) / groups;
-        int64_t d_end = d + 1;
-        while (d_end < s.d_hi && p->rel_seg_ptr[d_end] < target) ++d_end;
-        if (g == groups - 1) d_end = s.d_hi;
-        const Selection sub = range_selection(p, d, d_end);
-        const size_t off = (size_t)(sub.sel_b - s.sel_b);
-        {
-            TimedLaunch tl(MPGNN_K_MEAN, strm);
-            st = run_means(p, sub, x, F_in, H + off * F_in, Pseg, false, strm);
-            if (st != MPGNN_OK) return st;
-        }
-        st = hip_check(hipEventRecord(ss->grp[g], strm), "hipEventRecord");
-        if (st == MPGNN_OK) st = hip_check(hipStreamWaitEvent(ss->s, ss->grp[g], 0), "hipStreamWaitEvent");
-        if (st != MPGNN_OK) return st;
-        st = run_seg(p, mode, sub, 2, x, F_in, weight, nullptr, 0, F_out, Y + off * F_out, nullptr, row_lo, row_hi,
-                     nullptr, nullptr, true, MPGNN_K_SEG_FWD, ss->s, H + off * F_in);
-        if (st != MPGNN_OK) return st;
-        d = d_end;
-    }
-    st = hip_check(hipEventRecord(ss->done, ss->s), "hipEventRecord");
-    if (st == MPGNN_OK) st = hip_check(hipStreamWaitEvent(strm, ss->done, 0), "hipStreamWaitEvent");
-    return st;
 }
 
 }  // namespace mpgnn
@@ -4210,113 +2959,34 @@ int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int
 }
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {
-    if (option == MPGNN_OPT_REL_WIDE) {
-        g_rel_wide = value != 0;
-        return MPGNN_OK;
+    switch (option) {
+        case MPGNN_OPT_EXACT_ORDER:
+            g_exact_order = value != 0;
+            return MPGNN_OK;
+        case MPGNN_OPT_TIMING_MASK: {
+            std::lock_guard<std::mutex> lk(g_timing_mu);
+            g_timing_mask = value;
+            return MPGNN_OK;
+        }
+        case MPGNN_OPT_REL_GEMM:
+            g_rel_gemm = value != 0;
+            return MPGNN_OK;
+        case MPGNN_OPT_PLAN_THREADS:
+            if (value < 0 || value > 256) return arg_error("MPGNN_OPT_PLAN_THREADS must be 0..256");
+            g_plan_threads = (int)value;
+            return MPGNN_OK;
+        case MPGNN_OPT_REL_WIDE:
+            g_rel_wide = value != 0;
+            return MPGNN_OK;
+        case MPGNN_OPT_CHUNK_ROWS:
+            if (value < 32 || value > 1024 || value % 32 != 0)
+                return arg_error("MPGNN_OPT_CHUNK_ROWS must be 32..1024, a multiple of 32");
+            g_chunk_rows = (int)value;
+            return MPGNN_OK;
+        default:
+            return arg_error("unknown option " + std::to_string(option) +
+                             " (measured-slower variants of round 1 were withdrawn: DESIGN.md §4)");
     }
-    if (option == MPGNN_OPT_REL_PINGPONG) {
-        g_rel_pingpong = value != 0;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_Y_ROWMAJOR) {  // measured neutral and slowed the default GEMM: withdrawn
-        if (value != 0) return arg_error("MPGNN_OPT_Y_ROWMAJOR was withdrawn (DESIGN.md §4)");
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_FLAT_CPW) {
-        if (value != 1 && value != 2 && value != 4) return arg_error("MPGNN_OPT_FLAT_CPW must be 1, 2 or 4");
-        g_flat_cpw = (int)value;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_REL_DIRECT) {
-        g_rel_direct = value != 0;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_REL_DEEP) {
-        g_rel_deep = value != 0;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_MERGE_GRAD) {
-        g_merge_grad = value != 0;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_REL_QUEUE) {
-        g_rel_queue = value != 0;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_DGRAD_IDX_AHEAD) {
-        g_dgrad_idx_ahead = value != 0;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_OUTER_SLICE) {
-        if (value != 8 && value != 16 && value != 32) return arg_error("MPGNN_OPT_OUTER_SLICE must be 8, 16 or 32");
-        g_outer_slice = (int)value;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_OUTER_ROOT_FIRST) {
-        g_outer_root_first = value != 0;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_CHUNK_ROWS) {
-        if (value < 32 || value > 1024 || value % 32 != 0) return arg_error("MPGNN_OPT_CHUNK_ROWS must be 32..1024, a multiple of 32");
-        g_chunk_rows = (int)value;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_PLAN_THREADS) {
-        if (value < 0 || value > 256) return arg_error("MPGNN_OPT_PLAN_THREADS must be 0..256");
-        g_plan_threads = (int)value;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_REL_STAGGER) {
-        if (value < 0 || value > 4096) return arg_error("MPGNN_OPT_REL_STAGGER must be 0..4096");
-        g_rel_stagger = (int)value;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_REL_WGS) {
-        if (value != 1 && value != 2) return arg_error("MPGNN_OPT_REL_WGS must be 1 or 2");
-        g_rel_wg_per_cu = (int)value;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_OVERLAP) {
-        if (value < 0 || value > kMaxOverlapGroups) return arg_error("MPGNN_OPT_OVERLAP must be 0..8");
-        g_overlap = (int)value;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_EXACT_ORDER) {
-        g_exact_order = value != 0;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_ABLATE) {
-        g_ablate = (int)value;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_FLAT_U) {
-        if (value != 16 && value != 32) return arg_error("MPGNN_OPT_FLAT_U must be 16 or 32");
-        g_flat_u = (int)value;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_FUSED) {
-        g_fused = value != 0;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_REL_GEMM) {
-        g_rel_gemm = value != 0;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_TILE_WS) {
-        g_tile_ws = value != 0;
-        g_ws_prio = value == 2 ? 0 : 1;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_TIMING_MASK) {
-        std::lock_guard<std::mutex> lk(g_timing_mu);
-        g_timing_mask = value;
-        return MPGNN_OK;
-    }
-    if (option == MPGNN_OPT_STAMPS) {
-        g_stamps = reinterpret_cast<unsigned long long*>(value);
-        return MPGNN_OK;
-    }
-    return arg_error("unknown option " + std::to_string(option));
 }
 
 int32_t mpgnn_rel_mean_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R,
@@ -4407,48 +3077,9 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     float* Yroot = root ? reinterpret_cast<float*>(ws + w.yroot) : nullptr;
     const bool exact = g_exact_order;
     const bool own_range = row_lo == p->shard_lo && row_hi == p->shard_hi;
-    if (!exact && g_fused && F_in == 128 && F_out == 128 && g_ablate == 0) {
-        // 1+2) fused: segment means formed in LDS and contracted on the matrix cores in one launch
-        FusedArgs f{};
-        f.t_begin = p->d.t32_begin;
-        f.t_end = p->d.t32_end;
-        f.t_cost = p->d.t32_cost;
-        f.t_lo = s.t32_lo;
-        f.n_rel = s.t32_hi - s.t32_lo;
-        f.n_root = root ? (int)((row_hi - row_lo + 31) / 32) : 0;
-        f.s_ptr = p->d.s_ptr;
-        f.e_col = p->d.e_col;
-        f.s_cnt = p->d.s_cnt;
-        f.s_rel = p->d.s_rel;
-        f.x = x;
-        f.W = weight;
-        f.w_per_rel = (mode == MPGNN_MODE_ALL);
-        f.Wroot = root;
-        f.Y = Y;
-        f.Yroot = Yroot;
-        f.H = h_save;
-        f.sel_b = s.sel_b;
-        f.row_lo = (int)row_lo;
-        f.row_hi = (int)row_hi;
-        f.stamps = g_stamps;
-        if (f.n_rel + f.n_root > 0) {
-            TimedLaunch tl(MPGNN_K_SEG_FWD, strm);
-            const int grid = std::min(f.n_rel + f.n_root, cu_count());
-            hipLaunchKernelGGL(fused_mean_gemm_kernel, dim3(grid), dim3(kFusedThreads), 0, strm, f);
-            st = hip_check(hipGetLastError(), "fused_mean_gemm_kernel launch");
-            if (st != MPGNN_OK) return st;
-        }
-    } else {
+    {
         // 1) H[seg] = mean(x over seg)  (the saved means when training)
         float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
-        SideStream* ss = (g_overlap > 0 && !exact && g_stamps == nullptr && g_ablate == 0 && s.sel_e > s.sel_b)
-                             ? side_stream(p->device) : nullptr;
-        if (ss != nullptr) {
-            const int groups = mode == MPGNN_MODE_ALL ? g_overlap : 1;
-            st = fwd_overlapped(p, mode, s, groups, ss, x, F_in, weight, root, F_out, H,
-                                reinterpret_cast<float*>(ws + w.pseg), Y, Yroot, row_lo, row_hi, strm);
-            if (st != MPGNN_OK) return st;
-        } else {
         {
             TimedLaunch tl(MPGNN_K_MEAN, strm);
             st = run_means(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
@@ -4458,7 +3089,6 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         st = run_seg(p, mode, s, 2, x, F_in, weight, root, 0, F_out, Y, Yroot, row_lo, row_hi, nullptr, nullptr, true,
                      MPGNN_K_SEG_FWD, strm, H);
         if (st != MPGNN_OK) return st;
-        }
     }
 
     // 2) out[i] = (Σ_{seg of row i, relation order} Y[seg] + Yroot[i]) + bias
@@ -4788,7 +3418,7 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         // every weight index with a segment range is written (directly or by the slab reduce,
         // zeros for an empty range); only indices absent from the plan need the memset
         const bool all_written = (mode == MPGNN_MODE_ALL) ? (s.d_hi - s.d_lo) == (int64_t)R : (s.c_hi > s.c_lo);
-        if (!all_written && mode == MPGNN_MODE_ALL && g_merge_grad && (int64_t)R - (s.d_hi - s.d_lo) <= kMaxZeroIds) {
+        if (!all_written && mode == MPGNN_MODE_ALL && (int64_t)R - (s.d_hi - s.d_lo) <= kMaxZeroIds) {
             // the few absent relation ids are zeroed by the reduce launch
             zl.dst = grad_weight;
             zl.elems = (int)wsize;
@@ -4892,31 +3522,16 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         }
     }
     const int root_y = grad_root ? mt : 1;
-    if (have_w && have_root && root_y == mt && g_merge_grad) {
+    if (have_w && have_root && root_y == mt) {
         TimedLaunch tl(MPGNN_K_OUTER, strm);
-        // root chunks are all full length (the relation chunks of small relations are short):
-        // dispatched first, they stop being the launch's tail (MPGNN_OPT_OUTER_ROOT_FIRST)
-        const OuterArgs& first = g_outer_root_first ? orr : ow;
-        const OuterArgs& second = g_outer_root_first ? ow : orr;
-        const int n_first = g_outer_root_first ? rc.n : nch;
+        // one launch: root chunks (all full length; the relation chunks of small relations are
+        // short) dispatched first so they are not the launch's tail, 16-row LDS slices
         const dim3 grid2(nch + rc.n, mt, nt);
-        if (g_outer_slice == 8) {
-            const size_t lds8 = (size_t)(4 * (8 / 2) * kOuterLd) * sizeof(float);
-            if (outer_vec)
-                hipLaunchKernelGGL((outer_accum2_kernel<true, 8>), grid2, dim3(kThreads), lds8, strm, first, second, n_first);
-            else
-                hipLaunchKernelGGL((outer_accum2_kernel<false, 8>), grid2, dim3(kThreads), lds8, strm, first, second, n_first);
-        } else if (g_outer_slice == 16) {
-            const size_t lds16 = (size_t)(4 * (16 / 2) * kOuterLd) * sizeof(float);
-            if (outer_vec)
-                hipLaunchKernelGGL((outer_accum2_kernel<true, 16>), grid2, dim3(kThreads), lds16, strm, first, second, n_first);
-            else
-                hipLaunchKernelGGL((outer_accum2_kernel<false, 16>), grid2, dim3(kThreads), lds16, strm, first, second, n_first);
-        } else if (outer_vec) {
-            hipLaunchKernelGGL((outer_accum2_kernel<true, 32>), grid2, dim3(kThreads), outer_lds, strm, first, second, n_first);
-        } else {
-            hipLaunchKernelGGL((outer_accum2_kernel<false, 32>), grid2, dim3(kThreads), outer_lds, strm, first, second, n_first);
-        }
+        const size_t lds16 = (size_t)(4 * (16 / 2) * kOuterLd) * sizeof(float);
+        if (outer_vec)
+            hipLaunchKernelGGL((outer_accum2_kernel<true, 16>), grid2, dim3(kThreads), lds16, strm, orr, ow, rc.n);
+        else
+            hipLaunchKernelGGL((outer_accum2_kernel<false, 16>), grid2, dim3(kThreads), lds16, strm, orr, ow, rc.n);
         if ((st = hip_check(hipGetLastError(), "outer_accum2_kernel launch")) != MPGNN_OK) return st;
     } else {
         if (have_w) {
@@ -4931,7 +3546,7 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         }
     }
     if (reduces.empty() && zl.n == 0) return MPGNN_OK;
-    if (g_merge_grad) {
+    {
         ReduceArgs r3[3] = {};
         int gx[3] = {0, 0, 0}, ey = zl.n > 0 ? (zl.elems + kThreads - 1) / kThreads : 0;
         for (size_t k = 0; k < reduces.size(); ++k) {
@@ -4944,12 +3559,6 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
                            r3[1], r3[2], gx[0], gx[1], gx[2], zl);
         return hip_check(hipGetLastError(), "reduce_slabs3_kernel launch");
     }
-    for (const Part& pt : reduces) {
-        TimedLaunch tl(MPGNN_K_REDUCE, strm);
-        hipLaunchKernelGGL(reduce_slabs_kernel, dim3(pt.gx, pt.ey), dim3(kThreads), 0, strm, pt.r);
-        if ((st = hip_check(hipGetLastError(), "reduce_slabs_kernel launch")) != MPGNN_OK) return st;
-    }
-    return MPGNN_OK;
 }
 
 // Debug: workgroups per CU the runtime admits for the forward tile kernel at gather width F.

@@ -23,7 +23,7 @@ step() {  # name timeout cmd...
 MODE=${1:-all}
 rocm-smi --showproductname > "$OUT/rocm_smi.txt" 2>&1 || true
 if [[ $MODE == all || $MODE == test ]]; then
-    step pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread
+    MPGNN_PARITY_REPORT=$OUT/parity.jsonl step pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread
     step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ $MODE == all || $MODE == bench ]]; then

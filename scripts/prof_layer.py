@@ -16,9 +16,7 @@ ap.add_argument("--config", default="fb15k237")
 ap.add_argument("--feat", type=int, default=128)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--backward", action="store_true")
-ap.add_argument("--ablate", type=int, default=0, help="MPGNN_OPT_ABLATE bits (profiling only)")
 args = ap.parse_args()
-mpgnn_amd._lib.lib.mpgnn_set_option(1, args.ablate)
 g = data.config_graph(args.config)
 x = torch.rand(g.num_nodes, args.feat, device="cuda", requires_grad=args.backward)
 ei, et = g.edge_index.cuda(), g.edge_type.cuda()

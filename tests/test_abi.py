@@ -71,12 +71,15 @@ def test_bad_arguments():
 
 
 def test_withdrawn_option_is_refused():
-    """MPGNN_OPT_Y_ROWMAJOR (17) was withdrawn: 0 is accepted, 1 is refused with a message."""
+    """The round-1 profiling switches and measured-slower variants (ids 1, 2, 4, 6-10, 12-18,
+    21-23) were withdrawn: refused with a message; the retained options still work."""
     from mpgnn_amd import _lib
     lib = _lib.lib
-    assert lib.mpgnn_set_option(17, 0) == 0
-    assert lib.mpgnn_set_option(17, 1) == _lib.MPGNN_ERR_ARG
-    assert b"withdrawn" in lib.mpgnn_last_error()
+    for opt in (1, 2, 4, 6, 7, 8, 9, 10, 12, 13, 14, 15, 16, 17, 18, 21, 22, 23):
+        assert lib.mpgnn_set_option(opt, 0) == _lib.MPGNN_ERR_ARG
+        assert b"withdrawn" in lib.mpgnn_last_error()
+    assert lib.mpgnn_set_option(20, 192) == 0
+    assert lib.mpgnn_set_option(11, 0) == 0
 
 
 def test_workspace_bytes_is_host_computable():
