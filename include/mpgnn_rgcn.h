@@ -83,7 +83,17 @@ enum mpgnn_table {
     MPGNN_T_T_F_SPLIT_ROW = 26, MPGNN_T_T_F_SPLIT_PTR = 27, MPGNN_T_T_F_SPLIT_SLOT = 28,
     MPGNN_T_RW_F_CHUNK_PTR = 29, MPGNN_T_RW_F_CHUNK_INFO = 30, MPGNN_T_RW_F_ROW_OF = 31,
     MPGNN_T_RW_F_SPLIT_ROW = 32, MPGNN_T_RW_F_SPLIT_PTR = 33, MPGNN_T_RW_F_SPLIT_SLOT = 34,
-    MPGNN_T_COUNT = 35
+    /* multi-edge segments (the only segment means the layers materialise): a segment with one
+     * local edge and global count 1 has mean == x[node_2] and is read from x directly */
+    MPGNN_T_S_SRC = 35,      /* int32 [S]      node_2 of a single-edge segment (>= 0), else -(m+1)  */
+    MPGNN_T_M_PTR = 36,      /* int32 [Sm+1]   edge range of multi-edge segment m in EM_COL         */
+    MPGNN_T_EM_COL = 37,     /* int32 [Em]     node_2 of the edges of multi-edge segments, in order */
+    MPGNN_T_M_CNT = 38,      /* int32 [Sm]     GLOBAL edge count of multi-edge segment m            */
+    MPGNN_T_REL_M_PTR = 39,  /* int32 [nrel+1] multi-edge segment range of each relation            */
+    /* SEGM = the flat chunked list of the multi-edge segments over EM_COL (cut at relations) */
+    MPGNN_T_SEGM_F_CHUNK_PTR = 40, MPGNN_T_SEGM_F_CHUNK_INFO = 41, MPGNN_T_SEGM_F_ROW_OF = 42,
+    MPGNN_T_SEGM_F_SPLIT_ROW = 43, MPGNN_T_SEGM_F_SPLIT_PTR = 44, MPGNN_T_SEGM_F_SPLIT_SLOT = 45,
+    MPGNN_T_COUNT = 46
 };
 
 typedef struct mpgnn_plan_info {
@@ -179,11 +189,19 @@ int32_t mpgnn_rgcn_fwd_workspace_bytes(const mpgnn_plan* plan, int32_t mode, int
                                        int32_t num_relations, int32_t F_in, int32_t F_out,
                                        int64_t row_lo, int64_t row_hi, int64_t* bytes);
 
+/* Rows of the h_save buffer of mpgnn_rgcn_fwd / _fwd_act / _bwd for a selection: the
+ * MULTI-EDGE segments of the selection (mpgnn_table MPGNN_T_REL_M_PTR range). The means of the
+ * single-edge segments are x rows themselves and are not stored (mpgnn_table MPGNN_T_S_SRC). */
+int32_t mpgnn_rgcn_hsave_rows(const mpgnn_plan* plan, int32_t mode, int64_t relation,
+                              int32_t num_relations, int64_t* rows);
+
 /* Layer forward:  out = Σ_{r} mean_r(x) @ W_r  + x @ root + bias
  *   (mode SINGLE: the single relation `relation`, W = weight [F_in, F_out];
  *    mode ALL: r = 0..num_relations-1, W_r = weight[r] of [R, F_in, F_out]).
  * root / bias may be NULL (root_weight=False / bias=False). out is [N, F_out].
- * h_save (nullable) receives the segment means [seg_end - seg_begin, F_in] for backward. */
+ * h_save (nullable) receives the multi-edge segment means [mpgnn_rgcn_hsave_rows, F_in] for
+ * backward (bit-identical to PyG's mean, as mpgnn_rel_mean_fwd); the backward reads the
+ * single-edge segments' means from x. */
 int32_t mpgnn_rgcn_fwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
                        int32_t num_relations, const float* x, int32_t F_in,
                        const float* weight, const float* root, const float* bias,
@@ -203,7 +221,8 @@ int32_t mpgnn_rgcn_fwd_act(const mpgnn_plan* plan, int32_t mode, int64_t relatio
                            int32_t F_out, float* out, float* h_save, void* workspace,
                            int32_t act, void* stream);
 
-/* Layer backward given grad_out [N, F_out] and the h_save of the forward.
+/* Layer backward given grad_out [N, F_out] and the h_save of the forward (NULL: recomputed).
+ * x (the forward's input) is needed for grad_weight (single-edge segment means) and grad_root.
  * Any grad_* pointer may be NULL to skip that gradient.
  *   grad_x      [N, F_in]           (= Σ_r A_rᵀ (grad_out W_rᵀ) + grad_out rootᵀ)
  *   grad_weight [F_in, F_out] or [R, F_in, F_out]

@@ -36,6 +36,11 @@ TABLES = {
 for _i, _l in enumerate(("seg", "t", "rw")):
     for _j, _n in enumerate(("chunk_ptr", "chunk_info", "row_of", "split_row", "split_ptr", "split_slot")):
         TABLES[f"{_l}_f_{_n}"] = (17 + 6 * _i + _j, "int32")
+# multi-edge segments (the compact means the layers materialise), ids 35..45
+TABLES.update({"s_src": (35, "int32"), "m_ptr": (36, "int32"), "em_col": (37, "int32"), "m_cnt": (38, "int32"),
+               "rel_m_ptr": (39, "int32")})
+for _j, _n in enumerate(("chunk_ptr", "chunk_info", "row_of", "split_row", "split_ptr", "split_slot")):
+    TABLES[f"segm_f_{_n}"] = (40 + _j, "int32")
 
 
 class PlanInfo(ctypes.Structure):
@@ -68,6 +73,7 @@ SIGNATURES = [
     ("mpgnn_rel_mean_bwd_workspace_bytes", _I32, [_P, _I32, _I64, _I32, _I32, _PI64]),
     ("mpgnn_rel_mean_bwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _P]),
     ("mpgnn_rgcn_workspace_bytes", _I32, [_P, _I32, _I64, _I32, _I32, _I32, _I64, _I64, _PI64]),
+    ("mpgnn_rgcn_hsave_rows", _I32, [_P, _I32, _I64, _I32, _PI64]),
     ("mpgnn_rgcn_fwd_workspace_bytes", _I32, [_P, _I32, _I64, _I32, _I32, _I32, _I64, _I64, _PI64]),
     ("mpgnn_rgcn_fwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _I64, _I64,
                               _P, _P, _P, _P]),

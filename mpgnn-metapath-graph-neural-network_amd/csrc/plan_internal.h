@@ -104,6 +104,9 @@ struct DeviceTables {
     int32_t *seg_res = nullptr, *t_res = nullptr, *ta_res = nullptr, *rw_res = nullptr;  // resolved entries
     FlatDev seg_f, t_f, rw_f;       // flat chunked lists (segment means, grad_x, combine)
     FlatDev tx_f, rwx_f;            // grad_x / combine lists with a trailing extra-row entry per own row
+    // multi-edge segments (see mpgnn_plan::s_src)
+    int32_t *s_src = nullptr, *m_ptr = nullptr, *em_col = nullptr, *m_cnt = nullptr;
+    FlatDev segm_f;                 // flat chunked list of the multi-edge segments over em_col
     int32_t *tx_val = nullptr, *rwx_val = nullptr;  // their entry values (segment id | -(own row + 1))
     void* block = nullptr;          // single hipMalloc holding every table above
     size_t block_bytes = 0;
@@ -141,11 +144,17 @@ struct mpgnn_plan {
     std::vector<int32_t> chunk_begin, chunk_end; // [num_chunks]
     std::vector<int32_t> rel_val32;            // [nrel]
     std::vector<int32_t> chunk_dst;            // [num_chunks] see DeviceTables::chunk_dst
+    // A segment whose mean is one x row (one local edge, global count 1): s_src = its node_2;
+    // otherwise s_src = -(m + 1), m = its multi-edge segment index (row m of the compact Hm)
+    std::vector<int32_t> s_src;                // [S]
+    std::vector<int32_t> m_ptr, em_col, m_cnt; // [Sm+1] / [Em] / [Sm]
+    std::vector<int32_t> rel_m_ptr;            // [nrel+1]
 
     // ragged lists: segments over edges (forward gather), node_2 over col-major edges (grad_x,
     // all relations), (relation, node_2) runs over ta order (grad_x, one relation), node_1
     // over row-major segments (forward combine)
     mpgnn::RaggedHost seg_l, t_l, ta_l, rw_l;
+    mpgnn::FlatHost segm_f;               // multi-edge segments over em_col (cut at relations)
     mpgnn::FlatHost seg_f, t_f, rw_f;     // flat chunked lists: segments over edges (cut at
                                           // relations), node_2 over col-major edges, node_1 over segments
     // grad_x / combine lists over [shard_lo, shard_hi) rows with one trailing entry per own row

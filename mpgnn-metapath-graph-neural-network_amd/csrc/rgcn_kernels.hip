@@ -612,7 +612,9 @@ __global__ __launch_bounds__(kThreads) void seg_tile_kernel(SegTileArgs a) {
 // the A tile is double-buffered in LDS (one barrier per item) and the epilogue stores drain
 // behind the next item's MFMAs.  (A straight launch of one tile per workgroup runs load → MFMA
 // → store in lockstep on every CU: memory and the matrix pipe never overlap.)
-//   a_kind 2: relation rows = Hsrc[s - sel_b] (segment means), root rows = src[i]   (forward)
+//   a_kind 2: relation rows = s_src[s] >= 0 ? src[s_src[s]] : Hsrc[-s_src[s] - 1 - m_lo]
+//             (segment means: x row of a single-edge segment / compact multi-edge mean),
+//             root rows = src[i]   (forward)
 //   a_kind 1: relation rows = src[s_row[s]],    root rows = src[i]   (dgrad; / cnt on output)
 // ----------------------------------------------------------------------------------------
 struct TileGemmArgs {
@@ -623,6 +625,8 @@ struct TileGemmArgs {
     int a_kind;
     const float* src;
     const float* Hsrc;
+    const int* s_src;
+    int m_lo;
     const int* s_row;
     const int* s_cnt;
     const int* s_rel;
@@ -665,26 +669,26 @@ __device__ __forceinline__ TileItem tile_item(const TileGemmArgs& a, int w) {
 template <int KB, int WPT>
 __device__ __forceinline__ void tile_issue(const TileGemmArgs& a, const TileItem& it, int tid, float4 (&v)[WPT], int& cnt_raw) {
     constexpr int W4 = 16 * KB;
-    const bool gathered = !it.root && a.a_kind == 1;
-    const float* base = (it.root || a.a_kind == 1) ? a.src : a.Hsrc;
-    // contiguous rows: base row of the tile; gathered rows: index into s_row
-    const int off = it.root ? it.s0 : (gathered ? it.s0 : it.s0 - a.sel_b);
+    // relation rows are gathered: through s_row (dgrad) or s_src (forward); root rows contiguous
+    const bool gathered = !it.root;
     cnt_raw = 1;
     int row[WPT];
 #pragma unroll
-    for (int j = 0; j < WPT; ++j) row[j] = off + min((tid + j * kThreads) / W4, it.nrows - 1);
+    for (int j = 0; j < WPT; ++j) row[j] = it.s0 + min((tid + j * kThreads) / W4, it.nrows - 1);
     // uniform branch around the whole index batch (and the dgrad counts): the loads issue back
     // to back and are waited for once (a per-element select compiles to a branch + vmcnt(0)
     // around each load)
     if (gathered) {
         if (a.y_div) cnt_raw = a.s_cnt[it.s0 + min(tid & (kTileRows - 1), it.nrows - 1)];
+        const int* idx = a.a_kind == 1 ? a.s_row : a.s_src;
 #pragma unroll
-        for (int j = 0; j < WPT; ++j) row[j] = a.s_row[row[j]];
+        for (int j = 0; j < WPT; ++j) row[j] = idx[row[j]];
     }
 #pragma unroll
     for (int j = 0; j < WPT; ++j) {
         const int c = min(((tid + j * kThreads) % W4) * 4, a.K - 4);
-        v[j] = *reinterpret_cast<const float4*>(base + (size_t)row[j] * a.K + c);
+        const float* base = row[j] >= 0 ? a.src + (size_t)row[j] * a.K : a.Hsrc + (size_t)(-row[j] - 1 - a.m_lo) * a.K;
+        v[j] = *reinterpret_cast<const float4*>(base + c);
     }
 }
 
@@ -988,8 +992,10 @@ struct RelGemmArgs {
     const int* t_end;
     int t_lo;             // first tile of the selection
     int n_rel, n_root;    // items [0, n_rel) tiles t_lo + i; [n_rel, n_rel + n_root) node rows
-    const float* Arel;    // forward: H (row s - sel_b); dgrad: dout gathered by s_row[s]
+    const float* Arel;    // forward: compact multi-edge means Hm (row m - m_lo); dgrad: unused
     const float* Aroot;   // forward: x; dgrad: dout  (row i)
+    const int* s_src;     // forward: A row of segment s = s_src[s] >= 0 ? x[s_src[s]] : Hm[-s_src[s] - 1 - m_lo]
+    int m_lo;
     const int* s_row;
     const int* s_cnt;
     const int* s_rel;
@@ -1061,34 +1067,11 @@ struct RelGemm {
         return it;
     }
 
-    // A rows of an item into registers (clamped rows; zeroed at commit) + the dgrad row scale.
-    __device__ static __forceinline__ void issue(const RelGemmArgs& a, const Item& it, int tid, float4 (&v)[WPT],
-                                                 int& cnt) {
-        constexpr int W4 = K / 4;
-        int row[WPT];
-#pragma unroll
-        for (int j = 0; j < WPT; ++j) row[j] = it.r0 + min((tid + j * kThreads) / W4, it.nrows - 1);
-        const float* base;
-        cnt = 1;
-        if (it.root) {
-            base = a.Aroot;
-        } else if constexpr (DGRAD) {
-            base = a.Aroot;
-            cnt = a.s_cnt[it.r0 + min(tid & 31, it.nrows - 1)];
-#pragma unroll
-            for (int j = 0; j < WPT; ++j) row[j] = a.s_row[row[j]];
-        } else {
-            base = a.Arel;
-#pragma unroll
-            for (int j = 0; j < WPT; ++j) row[j] -= a.sel_b;
-        }
-#pragma unroll
-        for (int j = 0; j < WPT; ++j)
-            v[j] = *reinterpret_cast<const float4*>(base + (size_t)row[j] * K + ((tid + j * kThreads) % W4) * 4);
-    }
-
-    // dgrad, split in two: the gathered row numbers (s_row) and scale (s_cnt) of an item, loaded
-    // one item earlier than its rows, so issuing the rows costs one round trip, not two
+    // The A rows of a relation item are gathered: forward, segment s reads x[s_src[s]] (a
+    // single-edge segment: its mean is that x row) or its compact mean Hm[-s_src[s] - 1 - m_lo];
+    // dgrad reads dout[s_row[s]] (scaled by 1/cnt at the output). The row numbers (and dgrad
+    // scale) of an item are loaded one item earlier than its rows, so issuing the rows costs
+    // one round trip, not two. Root items read rows r0.. of Aroot directly.
     __device__ static __forceinline__ void gather_idx(const RelGemmArgs& a, const Item& it, int tid, int (&row)[WPT],
                                                       int& cnt) {
         constexpr int W4 = K / 4;
@@ -1096,17 +1079,30 @@ struct RelGemm {
         for (int j = 0; j < WPT; ++j) row[j] = it.r0 + min((tid + j * kThreads) / W4, it.nrows - 1);
         cnt = 1;
         if (!it.root) {
-            cnt = a.s_cnt[it.r0 + min(tid & 31, it.nrows - 1)];
+            if constexpr (DGRAD) {
+                cnt = a.s_cnt[it.r0 + min(tid & 31, it.nrows - 1)];
 #pragma unroll
-            for (int j = 0; j < WPT; ++j) row[j] = a.s_row[row[j]];
+                for (int j = 0; j < WPT; ++j) row[j] = a.s_row[row[j]];
+            } else {
+#pragma unroll
+                for (int j = 0; j < WPT; ++j) row[j] = a.s_src[row[j]];
+            }
         }
     }
     __device__ static __forceinline__ void issue_rows(const RelGemmArgs& a, int tid, const int (&row)[WPT],
                                                       float4 (&v)[WPT]) {
         constexpr int W4 = K / 4;
 #pragma unroll
-        for (int j = 0; j < WPT; ++j)
-            v[j] = *reinterpret_cast<const float4*>(a.Aroot + (size_t)row[j] * K + ((tid + j * kThreads) % W4) * 4);
+        for (int j = 0; j < WPT; ++j) {
+            const int c4 = ((tid + j * kThreads) % W4) * 4;
+            const float* base;
+            if constexpr (DGRAD) {
+                base = a.Aroot + (size_t)row[j] * K;
+            } else {
+                base = row[j] >= 0 ? a.Aroot + (size_t)row[j] * K : a.Arel + (size_t)(-row[j] - 1 - a.m_lo) * K;
+            }
+            v[j] = *reinterpret_cast<const float4*>(base + c4);
+        }
     }
 
     __device__ static __forceinline__ void commit(const Item& it, int tid, const float4 (&v)[WPT], int cnt, float* A,
@@ -1168,12 +1164,14 @@ struct RelGemm {
         const ItemTable tab = item_table(a, i_beg, i_end, lane);
         auto get_item = [&](int i) { return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i); };
         Item cur = get_item(i_beg);
-        issue(a, cur, tid, v, cnt);
-        int nrow[DGRAD ? WPT : 1];  // dgrad: gathered rows + scale of the item after the current one
-        int ncnt = 1;
-        if constexpr (DGRAD) {
-            if (i_beg + 1 < i_end) gather_idx(a, get_item(i_beg + 1), tid, nrow, ncnt);
+        {
+            int crow[WPT];
+            gather_idx(a, cur, tid, crow, cnt);
+            issue_rows(a, tid, crow, v);
         }
+        int nrow[WPT];  // gathered rows (+ dgrad scale) of the item after the current one
+        int ncnt = 1;
+        if (i_beg + 1 < i_end) gather_idx(a, get_item(i_beg + 1), tid, nrow, ncnt);
         float b[KH];
         load_b(cur.w, wave, lane, b);
         commit(cur, tid, v, cnt, As, Sc);
@@ -1188,14 +1186,11 @@ struct RelGemm {
         for (int i = i_beg; i < i_end; ++i) {
             const bool has_next = i + 1 < i_end;
             const Item nxt = has_next ? get_item(i + 1) : cur;
-            if (has_next) {  // in flight during this item's MFMAs
-                if constexpr (DGRAD) {  // rows of the next item; row numbers of the one after
-                    issue_rows(a, tid, nrow, v);
-                    cnt = ncnt;
-                    if (i + 2 < i_end) gather_idx(a, get_item(i + 2), tid, nrow, ncnt);
-                } else {
-                    issue(a, nxt, tid, v, cnt);
-                }
+            if (has_next) {  // in flight during this item's MFMAs: rows of the next item, row
+                             // numbers of the one after
+                issue_rows(a, tid, nrow, v);
+                cnt = ncnt;
+                if (i + 2 < i_end) gather_idx(a, get_item(i + 2), tid, nrow, ncnt);
             }
             const bool new_w = nxt.w != cur.w;
             float bn[kPrefetchB ? KH : 1];
@@ -1855,6 +1850,9 @@ struct OuterArgs {
     const float* A;
     int M;
     int a_off;
+    const int* a_idx;        // nullable: A row of position p = a_idx[p] >= 0 ? A[a_idx[p]] : A2[-a_idx[p] - 1 - a2_off]
+    const float* A2;
+    int a2_off;
     const float* B;
     int Nn;
     const int* b_idx;        // nullable
@@ -1899,32 +1897,35 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
     constexpr int NS = VEC ? SL * 128 / (4 * kThreads) : SL * 128 / kThreads;
     float4 va[VEC ? NS : 1], vb[VEC ? NS : 1];
     float sa[VEC ? 1 : NS], sb[VEC ? 1 : NS];
-    int bi[NS];  // B row index of each staged slot (next slice), loaded one slice earlier
-    int bi_next[NS];
+    // A and B row index of each staged slot (next slice), loaded one slice earlier
+    int ai[NS], bi[NS];
+    int ai_next[NS], bi_next[NS];
     auto slot_row = [&](int j) { return VEC ? ((tid + j * kThreads) >> 5) : ((tid + j * kThreads) >> 7); };
     auto slot_col = [&](int j) { return VEC ? 4 * ((tid + j * kThreads) & 31) : ((tid + j * kThreads) & 127); };
-    auto load_idx = [&](int slice, int (&o)[NS]) {
+    auto load_idx = [&](int slice, int (&oa)[NS], int (&ob)[NS]) {
         const int ps = p0 + slice * SL;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             const int p = min(ps + slot_row(j), p1 - 1);
-            o[j] = a.b_idx != nullptr ? a.b_idx[p] : p;
+            ob[j] = a.b_idx != nullptr ? a.b_idx[p] : p;
+            oa[j] = a.a_idx != nullptr ? a.a_idx[p] : p - a.a_off;
         }
     };
+    auto arow = [&](int r) {
+        return r >= 0 ? a.A + (size_t)r * a.M : a.A2 + (size_t)(-r - 1 - a.a2_off) * a.M;
+    };
     auto issue = [&](int slice) {
-        const int ps = p0 + slice * SL;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            const int ra = min(ps + slot_row(j), p1 - 1) - a.a_off;
             if constexpr (VEC) {
                 const int ca = min(m_base + slot_col(j), a.M - 4);
                 const int cb = min(n_base + slot_col(j), a.Nn - 4);
-                va[j] = *reinterpret_cast<const float4*>(a.A + (size_t)ra * a.M + ca);
+                va[j] = *reinterpret_cast<const float4*>(arow(ai[j]) + ca);
                 vb[j] = *reinterpret_cast<const float4*>(a.B + (size_t)bi[j] * a.Nn + cb);
             } else {
                 const int ca = min(m_base + slot_col(j), a.M - 1);
                 const int cb = min(n_base + slot_col(j), a.Nn - 1);
-                sa[j] = a.A[(size_t)ra * a.M + ca];
+                sa[j] = arow(ai[j])[ca];
                 sb[j] = a.B[(size_t)bi[j] * a.Nn + cb];
             }
         }
@@ -1970,8 +1971,8 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
     const bool do_bsum = a.Pb != nullptr && blockIdx.y == 0 && tid < kColTile;
 
     if (nslices > 0) {
-        load_idx(0, bi);
-        if (nslices > 1) load_idx(1, bi_next);
+        load_idx(0, ai, bi);
+        if (nslices > 1) load_idx(1, ai_next, bi_next);
         issue(0);
         commit(0, bufs);
     }
@@ -1981,8 +1982,11 @@ __device__ __forceinline__ void outer_accum_body(const OuterArgs& a, const int c
         const bool more = sl + 1 < nslices;  // uniform
         if (more) {
 #pragma unroll
-            for (int j = 0; j < NS; ++j) bi[j] = bi_next[j];
-            if (sl + 2 < nslices) load_idx(sl + 2, bi_next);
+            for (int j = 0; j < NS; ++j) {
+                ai[j] = ai_next[j];
+                bi[j] = bi_next[j];
+            }
+            if (sl + 2 < nslices) load_idx(sl + 2, ai_next, bi_next);
             issue(sl + 1);
         }
         const int nr = min(SL, p1 - p0 - sl * SL);
@@ -2418,6 +2422,7 @@ struct Selection {
     int sp_lo = 0, sp_hi = 0;     // seg-list pieces of the selection
     int tap_lo = 0, tap_hi = 0;   // ta-list pieces (mode SINGLE)
     int ta_e_lo = 0, ta_e_hi = 0; // ta entry range (mode SINGLE)
+    int m_lo = 0, m_hi = 0;       // multi-edge segments (rows of the compact means Hm)
     bool all_segments = false;    // selection covers every local segment
 };
 
@@ -2455,6 +2460,8 @@ static void fill_selection(const mpgnn_plan* p, Selection* s) {
     s->tap_hi = p->rel_ta_piece_ptr[s->d_hi];
     s->ta_e_lo = p->rel_ta_ent_ptr[s->d_lo];
     s->ta_e_hi = p->rel_ta_ent_ptr[s->d_hi];
+    s->m_lo = p->rel_m_ptr[s->d_lo];
+    s->m_hi = p->rel_m_ptr[s->d_hi];
     s->all_segments = (s->sel_b == 0 && s->sel_e == p->S);
 }
 
@@ -2492,9 +2499,10 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
     size_t off = 0;
     w.y = off; off += align256(S_sel * F_out * sizeof(float));
     w.yroot = off; off += align256(rows * F_out * sizeof(float));
-    w.hf = off; off += align256(S_sel * F_in * sizeof(float));
+    const size_t Sm_sel = (size_t)(s.m_hi - s.m_lo);
+    w.hf = off; off += align256(Sm_sel * F_in * sizeof(float));  // compact multi-edge means
     // piece partials (exact-order / mode SINGLE lists) or flat-list carry slots
-    const size_t seg_slots = std::max((size_t)(s.sp_hi - s.sp_lo), (size_t)p->seg_f.nslots);
+    const size_t seg_slots = std::max({(size_t)(s.sp_hi - s.sp_lo), (size_t)p->seg_f.nslots, (size_t)p->segm_f.nslots});
     w.pseg = off; off += align256(seg_slots * fmax * sizeof(float));
     w.prw = off; off += align256((mode == MPGNN_MODE_ALL ? std::max({p->rw_l.piece_b.size(), (size_t)p->rw_f.nslots,
                                                                      (size_t)p->rwx_f.nslots})
@@ -2507,7 +2515,7 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
                                  : (size_t)(s.tap_hi - s.tap_lo);
     w.g = off; off += align256(S_sel * F_in * sizeof(float));
     w.groot = off; off += align256(rows * F_in * sizeof(float));
-    w.h = off; off += align256(S_sel * F_in * sizeof(float));
+    w.h = off; off += align256(Sm_sel * F_in * sizeof(float));
     w.pdx = off; off += align256(std::max(dx_pieces, seg_slots) * F_in * sizeof(float));
     w.p = off; off += align256((size_t)(s.c_hi - s.c_lo) * F_in * F_out * sizeof(float));
     w.proot = off; off += align256((size_t)rc.n * F_in * F_out * sizeof(float));
@@ -2543,6 +2551,7 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
                        int K, const float* W, const float* Wroot, int trans, int N, float* Y, float* Yroot,
                        int64_t row_lo, int64_t row_hi, float* H, float* Pseg, bool exact, int kind,
                        hipStream_t strm, const float* Hsrc = nullptr) {
+    const int m_lo = s.m_lo;
     const int n_rel = s.t_hi - s.t_lo;
     const int n_root = (Wroot != nullptr) ? (int)((row_hi - row_lo + kTileRows - 1) / kTileRows) : 0;
     if (n_rel + n_root == 0) return MPGNN_OK;
@@ -2574,8 +2583,10 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         r.n_rel = s.t32_hi - s.t32_lo;
         r.n_root = (Wroot != nullptr) ? (int)((row_hi - row_lo + 31) / 32) : 0;
         if (r.n_rel + r.n_root == 0) return MPGNN_OK;
-        r.Arel = gather_kind == 2 ? Hsrc : src;
+        r.Arel = Hsrc;
         r.Aroot = src;
+        r.s_src = p->d.s_src;
+        r.m_lo = m_lo;
         r.s_row = p->d.s_row;
         r.s_cnt = p->d.s_cnt;
         r.s_rel = p->d.s_rel;
@@ -2603,6 +2614,8 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         t.a_kind = gather_kind;
         t.src = src;
         t.Hsrc = Hsrc;
+        t.s_src = p->d.s_src;
+        t.m_lo = m_lo;
         t.s_row = p->d.s_row;
         t.s_cnt = p->d.s_cnt;
         t.s_rel = p->d.s_rel;
@@ -2622,6 +2635,25 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         launch_tile_gemm(t, strm);
         return hip_check(hipGetLastError(), "tile_gemm_kernel launch");
     }
+    // odd widths (F % 4 != 0): seg_tile_kernel recomputes the means of its tiles from x
+    // (gather kind 0) instead of reading the compact ones
+    if (gather_kind == 2) gather_kind = 0;
+    const bool ragged_t = gather_kind == 0 && !exact && s.sp_hi > s.sp_lo;
+    if (ragged_t && !ragged) {
+        PieceArgs pa{};
+        pa.pb = p->d.seg_pb;
+        pa.pe = p->d.seg_pe;
+        pa.k_lo = s.sp_lo;
+        pa.k_hi = s.sp_hi;
+        pa.src = src;
+        pa.F = K;
+        pa.idx = p->d.e_col;
+        pa.P = Pseg;
+        TimedLaunch tl(MPGNN_K_PIECE, strm);
+        MPGNN_VT_DISPATCH(V, T, launch_piece, pa, strm);
+        int32_t st = hip_check(hipGetLastError(), "piece_sum_kernel(seg) launch");
+        if (st != MPGNN_OK) return st;
+    }
     SegTileArgs a{};
     a.tile_begin = p->d.tile_begin;
     a.tile_end = p->d.tile_end;
@@ -2630,12 +2662,12 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
     a.gather_kind = gather_kind;
     a.src = src;
     a.F = K;
-    a.s_ptr = ragged ? p->d.seg_ent_ptr : p->d.s_ptr;
+    a.s_ptr = ragged_t ? p->d.seg_ent_ptr : p->d.s_ptr;
     a.e_col = p->d.e_col;
     a.s_row = p->d.s_row;
     a.s_cnt = p->d.s_cnt;
     a.s_rel = p->d.s_rel;
-    a.ent = ragged ? p->d.seg_ent : nullptr;
+    a.ent = ragged_t ? p->d.seg_ent : nullptr;
     a.P = Pseg;
     a.piece_off = s.sp_lo;
     a.W = W;
@@ -2903,6 +2935,43 @@ static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x
     return run_rowsum(p, a, p->d.seg_pb, p->d.seg_pe, ragged ? s.sp_lo : 0, ragged ? s.sp_hi : 0, Pseg, strm);
 }
 
+// Compact means of the selection's multi-edge segments: Hm[m - m_lo] = (Σ x[em_col]) / m_cnt[m]
+// for m in [m_lo, m_hi) — the flat chunked list (rows inside one chunk in reference order), or
+// the sequential row sum in exact mode. The single-edge segments' means are x rows (s_src).
+static int32_t run_means_multi(const mpgnn_plan* p, const Selection& s, const float* x, int F, float* Hm,
+                               float* carry, bool exact, hipStream_t strm) {
+    if (s.m_hi == s.m_lo) return MPGNN_OK;
+    if (!exact) {
+        FlatRun f{};
+        f.fd = &p->d.segm_f;
+        f.c_lo = p->segm_f.cut_chunk_ptr[s.d_lo];
+        f.c_hi = p->segm_f.cut_chunk_ptr[s.d_hi];
+        f.k_lo = p->segm_f.cut_split_ptr[s.d_lo];
+        f.k_hi = p->segm_f.cut_split_ptr[s.d_hi];
+        f.table = p->d.em_col;
+        f.src = x;
+        f.F = F;
+        f.row_off = s.m_lo;
+        f.out = Hm;
+        f.carry = carry;
+        f.final_mode = 0;
+        f.cnt = p->d.m_cnt;
+        return run_flat(f, strm);
+    }
+    RowSumArgs a{};
+    a.r_begin = s.m_lo;
+    a.N = s.m_hi;
+    a.list_kind = 0;
+    a.ptr = p->d.m_ptr;
+    a.g.src = x;
+    a.g.F = F;
+    a.g.idx = p->d.em_col;
+    a.cnt = p->d.m_cnt;
+    a.out = Hm;
+    a.out_off = s.m_lo;
+    return run_rowsum(p, a, nullptr, nullptr, 0, 0, carry, strm);
+}
+
 }  // namespace mpgnn
 
 using namespace mpgnn;
@@ -3017,6 +3086,15 @@ int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* p, int32_t mode, int64_t re
     return MPGNN_OK;
 }
 
+int32_t mpgnn_rgcn_hsave_rows(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, int64_t* rows) {
+    if (!p || !rows) return arg_error("NULL argument");
+    Selection s;
+    int32_t st = make_selection(p, mode, relation, R, &s);
+    if (st != MPGNN_OK) return st;
+    *rows = (int64_t)(s.m_hi - s.m_lo);
+    return MPGNN_OK;
+}
+
 int32_t mpgnn_rgcn_fwd_workspace_bytes(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R,
                                        int32_t F_in, int32_t F_out, int64_t row_lo, int64_t row_hi,
                                        int64_t* bytes) {
@@ -3078,14 +3156,15 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     const bool exact = g_exact_order;
     const bool own_range = row_lo == p->shard_lo && row_hi == p->shard_hi;
     {
-        // 1) H[seg] = mean(x over seg)  (the saved means when training)
+        // 1) Hm[m] = mean(x over multi-edge segment m)  (the saved means when training); a
+        //    single-edge segment's mean is its x row, read by the GEMM through s_src
         float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
         {
             TimedLaunch tl(MPGNN_K_MEAN, strm);
-            st = run_means(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
+            st = run_means_multi(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
             if (st != MPGNN_OK) return st;
         }
-        // 2) Y[seg] = H[seg] @ W_rel(seg); Yroot[i] = x[i] @ root   (MFMA tiles)
+        // 2) Y[seg] = mean(seg) @ W_rel(seg); Yroot[i] = x[i] @ root   (MFMA tiles)
         st = run_seg(p, mode, s, 2, x, F_in, weight, root, 0, F_out, Y, Yroot, row_lo, row_hi, nullptr, nullptr, true,
                      MPGNN_K_SEG_FWD, strm, H);
         if (st != MPGNN_OK) return st;
@@ -3434,10 +3513,11 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         }
         nch = s.c_hi - s.c_lo;
         if (nch > 0) {
+            if (!x) return arg_error("NULL x (grad_weight reads the single-edge segment means from x)");
             const float* H = h_save;
             if (H == nullptr) {
                 float* Hw = reinterpret_cast<float*>(ws + w.h);
-                st = run_means(p, s, x, F_in, Hw, reinterpret_cast<float*>(ws + w.pdx), exact, strm);
+                st = run_means_multi(p, s, x, F_in, Hw, reinterpret_cast<float*>(ws + w.pdx), exact, strm);
                 if (st != MPGNN_OK) return st;
                 H = Hw;
             }
@@ -3447,9 +3527,12 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
             ow.chunk_dst = p->d.chunk_dst;
             ow.chunk_off = s.c_lo;
             ow.dst_mode = mode == MPGNN_MODE_ALL ? 1 : 2;
-            ow.A = H;
+            ow.A = x;  // segment s: x[s_src[s]] or Hm[-s_src[s] - 1 - m_lo]
+            ow.a_idx = p->d.s_src;
+            ow.A2 = H;
+            ow.a2_off = s.m_lo;
             ow.M = F_in;
-            ow.a_off = s.sel_b;
+            ow.a_off = 0;
             ow.B = grad_out;
             ow.Nn = F_out;
             ow.b_idx = p->d.s_row;

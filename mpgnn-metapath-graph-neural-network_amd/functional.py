@@ -85,12 +85,13 @@ def _forward(x, weight, root, bias, plan: GraphPlan, mode: int, relation: int, n
     if weight.shape[-2] != f_in:
         raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({N}x{f_in} and "
                            f"{weight.shape[-2]}x{f_out})")
-    seg_b, seg_e = plan.select(mode, relation, num_relations)
     ws = _workspace(plan.workspace_bytes(mode, relation, num_relations, f_in, f_out, row_lo, row_hi,
                                          forward_only=True), x.device)
     out = torch.empty(N, f_out, dtype=torch.float32, device=x.device)
-    # segment means, kept for grad_weight (dW_r = Σ h_segᵀ dout[node_1])
-    h_save = torch.empty(seg_e - seg_b, f_in, dtype=torch.float32, device=x.device) if need_h else None
+    # multi-edge segment means, kept for grad_weight (dW_r = Σ h_segᵀ dout[node_1]; the
+    # single-edge segments' means are rows of x, which backward has anyway)
+    h_save = torch.empty(plan.hsave_rows(mode, relation, num_relations), f_in, dtype=torch.float32,
+                         device=x.device) if need_h else None
     if act != ACT_NONE:  # fused activation: unsharded layers only (see rgcn_conv)
         check(lib.mpgnn_rgcn_fwd_act(plan.handle, mode, int(relation), int(num_relations), x.data_ptr(), f_in,
                                      weight.data_ptr(), _ptr(root), _ptr(bias), f_out, out.data_ptr(),

@@ -118,6 +118,19 @@ class GraphPlan:
                                     out.nbytes), "mpgnn_plan_export")
         return out
 
+    def hsave_rows(self, mode: int, relation: int, num_relations: int) -> int:
+        """Rows of the saved means of a layer call: its multi-edge segments (the single-edge
+        segments' means are x rows, read through the plan's s_src table)."""
+        key = ("hsave", mode, int(relation), int(num_relations))
+        hit = self._sel_cache.get(key)
+        if hit is not None:
+            return hit
+        n = ctypes.c_int64()
+        check(lib.mpgnn_rgcn_hsave_rows(self._h, mode, int(relation), int(num_relations), ctypes.byref(n)),
+              "mpgnn_rgcn_hsave_rows")
+        self._sel_cache[key] = int(n.value)
+        return self._sel_cache[key]
+
     def workspace_bytes(self, mode, relation, num_relations, f_in, f_out, row_lo, row_hi,
                         forward_only: bool = False) -> int:
         key = (mode, int(relation), int(num_relations), f_in, f_out, row_lo, row_hi, forward_only)

@@ -87,8 +87,22 @@ def build_plan(edge_index: np.ndarray, edge_type: np.ndarray, num_nodes: int,
         s_cnt=s_cnt, s_pos=s_pos, rw_ptr=rw_ptr, rw_seg=rw_seg, t_ptr=t_ptr, t_seg=t_seg,
         ta_col=ta_col, ta_seg=ta_seg, rel_invalid=rel_invalid,
     )
+    # multi-edge segments: a segment whose mean is one x row (one local edge, global count 1) is
+    # read from x (s_src = node_2); the others are rows m of the compact means (s_src = -(m+1))
+    loc_cnt = np.diff(s_ptr)
+    multi = ~((loc_cnt == 1) & (s_cnt == 1))
+    m_of = np.cumsum(multi) - multi                      # exclusive prefix
+    s_src = np.where(multi, -(m_of + 1), e_col[np.minimum(s_ptr[:-1], max(len(e_col) - 1, 0))] if S else 0)
+    m_seg = np.nonzero(multi)[0]
+    m_ptr = np.append(0, np.cumsum(loc_cnt[m_seg])).astype(np.int32)
+    em_col = (np.concatenate([e_col[s_ptr[s]:s_ptr[s + 1]] for s in m_seg]) if len(m_seg)
+              else np.zeros(0, np.int64)).astype(np.int32)
+    rel_m_ptr = np.append(m_of, len(m_seg))[rel_seg_ptr].astype(np.int32)
+    out.update(s_src=np.asarray(s_src, dtype=np.int32).reshape(S), m_ptr=m_ptr, em_col=em_col,
+               m_cnt=s_cnt[m_seg].astype(np.int32), rel_m_ptr=rel_m_ptr)
     for name, run_ptr, cuts, chunk in (("seg", s_ptr, rel_seg_ptr, FLAT_CHUNK), ("t", t_ptr, np.array([0, N]), FLAT_CHUNK),
-                                       ("rw", rw_ptr, np.array([0, N]), FLAT_CHUNK_ROW_MAJOR)):
+                                       ("rw", rw_ptr, np.array([0, N]), FLAT_CHUNK_ROW_MAJOR),
+                                       ("segm", m_ptr, rel_m_ptr, FLAT_CHUNK)):
         for k, v in build_flat(run_ptr, cuts, chunk).items():
             out[f"{name}_f_{k}"] = v
     return out

@@ -10,8 +10,9 @@ from mpgnn_amd import data
 from oracle import plan_oracle
 
 TABLES = ["rel_values", "rel_seg_ptr", "rel_edge_ptr", "e_col", "e_id", "s_ptr", "s_row", "s_rel",
-          "s_cnt", "s_pos", "rw_ptr", "rw_seg", "t_ptr", "t_seg", "ta_col", "ta_seg", "rel_invalid"]
-FLAT = [f"{l}_f_{n}" for l in ("seg", "t", "rw")
+          "s_cnt", "s_pos", "rw_ptr", "rw_seg", "t_ptr", "t_seg", "ta_col", "ta_seg", "rel_invalid",
+          "s_src", "m_ptr", "em_col", "m_cnt", "rel_m_ptr"]
+FLAT = [f"{l}_f_{n}" for l in ("seg", "t", "rw", "segm")
         for n in ("chunk_ptr", "chunk_info", "row_of", "split_row", "split_ptr", "split_slot")]
 
 
@@ -156,7 +157,8 @@ def test_flat_lists_bit_exact_and_well_formed(case, shard):
     for tname in FLAT:
         got = plan.table(tname)
         assert np.array_equal(got, ref[tname]), tname
-    for l, run_ptr, chunk in (("seg", ref["s_ptr"], 32), ("t", ref["t_ptr"], 32), ("rw", ref["rw_ptr"], 16)):
+    for l, run_ptr, chunk in (("seg", ref["s_ptr"], 32), ("t", ref["t_ptr"], 32), ("rw", ref["rw_ptr"], 16),
+                              ("segm", ref["m_ptr"], 32)):
         cp = plan.table(f"{l}_f_chunk_ptr")
         sizes = np.diff(cp)
         assert (sizes >= 1).all() and (sizes <= chunk).all(), l
@@ -192,3 +194,31 @@ def test_parallel_plan_build_independent_of_thread_count(shard):
         ref = plans[0].table(name)
         for p in plans[1:]:
             assert np.array_equal(p.table(name), ref), name
+
+
+@pytest.mark.parametrize("case", list(graphs()), ids=lambda c: c[0])
+@pytest.mark.parametrize("shard", [None, (0.3, 0.7)])
+def test_multi_edge_segments_cover_exactly_the_non_trivial_means(case, shard):
+    """s_src: a segment reads x[node_2] iff it has one local edge and global count 1 (its mean is
+    that row bit for bit); every other segment owns one compact row m whose edge list is the
+    segment's own edge list in plan order, with the global count."""
+    name, ei, et, N = case
+    lo, hi = (0, N) if shard is None else (int(shard[0] * N), int(shard[1] * N))
+    plan = mpgnn_amd.GraphPlan(torch.from_numpy(np.ascontiguousarray(ei)), torch.from_numpy(et), N, shard=(lo, hi))
+    s_ptr, s_cnt, e_col = plan.table("s_ptr"), plan.table("s_cnt"), plan.table("e_col")
+    s_src, m_ptr, em_col, m_cnt = plan.table("s_src"), plan.table("m_ptr"), plan.table("em_col"), plan.table("m_cnt")
+    m = 0
+    for s in range(len(s_src)):
+        b, e = s_ptr[s], s_ptr[s + 1]
+        if e - b == 1 and s_cnt[s] == 1:
+            assert s_src[s] == e_col[b]
+        else:
+            assert s_src[s] == -(m + 1)
+            assert np.array_equal(em_col[m_ptr[m]:m_ptr[m + 1]], e_col[b:e])
+            assert m_cnt[m] == s_cnt[s]
+            m += 1
+    assert m == len(m_cnt) == len(m_ptr) - 1
+    rsp, rmp = plan.table("rel_seg_ptr"), plan.table("rel_m_ptr")
+    assert len(rmp) == len(rsp)
+    for d in range(len(rsp)):  # rel_m_ptr[d] = multi-edge segments before relation d's first segment
+        assert rmp[d] == int((s_src[:rsp[d]] < 0).sum())
