@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <mutex>
 #include <string>
@@ -923,6 +924,8 @@ __device__ __forceinline__ void tile_gemm_body(const TileGemmArgs& a, float* sme
             }
         }
         __syncthreads();
+        // next item's A tile first: its vmcnt wait then does not also wait for this item's stores
+        if (has_next) tile_commit<KB, WPT>(a, nxt, tid, v, cnt_raw, bufs + (buf ^ 1) * bstride, scales + (buf ^ 1) * kTileRows);
         {
             float* Yt = cur.root ? a.Yroot + (size_t)(cur.s0 - a.row_lo) * a.N : a.Y + (size_t)(cur.s0 - a.sel_b) * a.N;
             const bool div_rows = !cur.root && a.y_div;
@@ -959,7 +962,6 @@ __device__ __forceinline__ void tile_gemm_body(const TileGemmArgs& a, float* sme
                 }
             }
         }
-        if (has_next) tile_commit<KB, WPT>(a, nxt, tid, v, cnt_raw, bufs + (buf ^ 1) * bstride, scales + (buf ^ 1) * kTileRows);
         __syncthreads();
         cur = nxt;
         w = wn;
@@ -1005,16 +1007,49 @@ struct RelGemmArgs {
     float* Y;             // rows s - sel_b
     float* Yroot;         // rows i - row_lo
     int sel_b, row_lo, row_hi;
+#ifdef MPGNN_STAMPS
+    unsigned long long* stamps;
+#endif
 };
 
-template <int KB, bool DGRAD, int NB = 1>
+#ifdef MPGNN_STAMPS
+// Debug build only (csrc/Makefile `stamps`): per wave and item, shader-clock stamps of the
+// phases of rel_gemm_kernel, written by lane 0 with vector stores (scripts/stamps_gemm.py).
+constexpr int kStampItems = 32, kStampPhases = 6;
+static unsigned long long* g_stamps_host = nullptr;  // set by mpgnn_debug_stamps_set, passed as an argument
+#define MPGNN_STAMP_PTR a.stamps
+#define stamp(k, ph) stamp_at(a.stamps, k, ph)
+#define stamp_id() stamp_id_at(a.stamps)
+__device__ __forceinline__ void stamp_at(unsigned long long* g_stamps, int k, int ph) {
+    if (g_stamps != nullptr && (threadIdx.x & 63) == 0 && k < kStampItems) {
+        const size_t w = (size_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+        g_stamps[(w * (kStampItems + 1) + 1 + k) * kStampPhases + ph] = __builtin_readcyclecounter();
+    }
+}
+__device__ __forceinline__ void stamp_id_at(unsigned long long* g_stamps) {
+    if (g_stamps != nullptr && (threadIdx.x & 63) == 0) {
+        const size_t w = (size_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+        unsigned long long* o = g_stamps + w * (kStampItems + 1) * kStampPhases;
+        o[0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        o[1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+        o[2] = __builtin_readcyclecounter();
+    }
+}
+#else
+#define stamp(k, ph) ((void)0)
+#define stamp_id() ((void)0)
+#endif
+
+template <int KB, bool DGRAD, int NB = 1, int OCC = 2>
 struct RelGemm {
     static constexpr int K = 64 * KB;
     static constexpr int KH = K / 2;
     static constexpr int N = 128 * NB;  // output / weight row stride; a workgroup covers 128 columns
     // first output column of this workgroup (grid.y = NB column blocks)
     __device__ static __forceinline__ int col0() { return NB > 1 ? (int)blockIdx.y * 128 : 0; }
-    static constexpr bool kPrefetchB = KB <= 2;  // K = 256: two weight slices would not fit in registers
+    // the next relation run's weight slice prefetched into a second register set (K = 256: two
+    // slices would not fit; three workgroups per CU: neither)
+    static constexpr bool kPrefetchB = KB <= 2 && OCC <= 2;
     static constexpr int lda = K + 4;
     static constexpr int WPT = 32 * (K / 4) / kThreads;  // float4 of an A tile per thread
 
@@ -1140,7 +1175,136 @@ struct RelGemm {
         }
     }
 
+    // Forward loop, software-pipelined across items so the MFMA pipe sees one barrier per item
+    // and nothing else: item i's 16 output stores go out one per MFMA group of item i+1's
+    // chain (bounds-checked buffer stores: rows past a partial item's end are dropped by the
+    // descriptor, no exec branches), and item i+1's A tile is committed to the other LDS
+    // buffer three quarters into item i's chain (its rows were issued at the top of item i).
+    __device__ static void run_fwd(const RelGemmArgs& a, float* smem) {
+        float* As = smem;                 // [2][32][lda]
+        float* Sc = smem + 2 * 32 * lda;  // commit's (unused) row scales
+        const int tid = threadIdx.x;
+        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int n_items = a.n_rel + a.n_root;
+        const int G = (int)gridDim.x;
+        const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
+        const int rng = g * q + min(g, rem) + ((int)blockIdx.x >> 3);
+        const int i_beg = (int)((long long)rng * n_items / G);
+        const int i_end = (int)((long long)(rng + 1) * n_items / G);
+        if (i_beg >= i_end) return;
+
+        stamp_id();
+        float4 v[WPT];
+        int cnt;
+        const ItemTable tab = item_table(a, i_beg, i_end, lane);
+        auto get_item = [&](int i) { return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i); };
+        Item cur = get_item(i_beg);
+        {
+            int crow[WPT];
+            gather_idx(a, cur, tid, crow, cnt);
+            issue_rows(a, tid, crow, v);
+        }
+        int nrow[WPT];
+        int ncnt = 1;
+        if (i_beg + 1 < i_end) gather_idx(a, get_item(i_beg + 1), tid, nrow, ncnt);
+        float b[KH];
+        load_b(cur.w, wave, lane, b);
+        commit(cur, tid, v, cnt, As, Sc);
+#pragma unroll
+        for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(b[j]));
+        __syncthreads();
+
+        constexpr int NG = KH / 4;                 // MFMA groups (one A fragment each) per chain
+        constexpr int SPG = (16 + NG - 1) / NG;    // previous item's stores per group
+        constexpr int kCommitAt = (3 * NG) / 4;    // group after which the next tile is committed
+        constexpr bool kSplit = KB <= 2;           // two accumulation chains (accuracy)
+        // this lane's byte offset of output row `row` inside an item's first row (col block + strip)
+        const int col_b = (col0() + wave * 32 + c) * 4;
+        // the first chain stores through an empty descriptor (every store dropped): the stores
+        // are unconditional, so the wait-count pass never merges a store-free path into the loop
+        // (that would make the next item's index wait also wait for this item's stores)
+        float prev[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) prev[r] = 0.0f;
+        __amdgpu_buffer_rsrc_t prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.Y, (short)0, 0, 0x00020000);
+        auto store_prev = [&](int r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(prev[r]), prev_rsrc, row * (N * 4) + col_b, 0, 0);
+        };
+        int buf = 0;
+        for (int i = i_beg; i < i_end; ++i) {
+            stamp(i - i_beg, 0);
+            const bool has_next = i + 1 < i_end;
+            const Item nxt = has_next ? get_item(i + 1) : cur;
+            if (has_next) {
+                issue_rows(a, tid, nrow, v);
+                cnt = ncnt;
+                if (i + 2 < i_end) gather_idx(a, get_item(i + 2), tid, nrow, ncnt);
+            }
+            const bool new_w = nxt.w != cur.w;
+            float bn[kPrefetchB ? KH : 1];
+            if constexpr (kPrefetchB) {
+                if (new_w) load_b(nxt.w, wave, lane, bn);
+            }
+            const float* Ab = As + buf * 32 * lda + c * lda + h * KH;
+            f32x16 acc, acc2;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                acc[r] = 0.0f;
+                acc2[r] = 0.0f;
+            }
+            float4 af = *reinterpret_cast<const float4*>(Ab);
+#pragma unroll
+            for (int gi = 0; gi < NG; ++gi) {
+                const int j = 4 * gi;
+                const float4 cf = af;
+                if (j + 4 < KH) af = *reinterpret_cast<const float4*>(Ab + j + 4);
+                f32x16& ac = (kSplit && j >= KH / 2) ? acc2 : acc;
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.x, b[j], ac, 0, 0, 0);
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.y, b[j + 1], ac, 0, 0, 0);
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], ac, 0, 0, 0);
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], ac, 0, 0, 0);
+#pragma unroll
+                for (int u = 0; u < SPG; ++u)
+                    if (gi * SPG + u < 16) store_prev(gi * SPG + u);
+                if (gi == kCommitAt - 1 && has_next) {
+                    commit(nxt, tid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            stamp(i - i_beg, 1);
+            // this item's outputs become the next chain's stores
+#pragma unroll
+            for (int r = 0; r < 16; ++r) prev[r] = kSplit ? acc[r] + acc2[r] : acc[r];
+            {
+                float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
+                const int bytes = __builtin_amdgcn_readfirstlane(cur.nrows) * N * 4;
+                prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(Yt, (short)0, bytes, 0x00020000);
+            }
+            if (new_w) {
+                if constexpr (kPrefetchB) {
+#pragma unroll
+                    for (int j = 0; j < KH; ++j) b[j] = bn[j];
+                } else {
+                    load_b(nxt.w, wave, lane, b);
+                }
+            }
+            stamp(i - i_beg, 3);
+            __syncthreads();
+            stamp(i - i_beg, 4);
+            cur = nxt;
+            buf ^= 1;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) store_prev(r);
+    }
+
     __device__ static void run(const RelGemmArgs& a, float* smem) {
+        if constexpr (!DGRAD) {
+            run_fwd(a, smem);
+            return;
+        }
         float* As = smem;                 // [2][32][lda]
         float* Sc = smem + 2 * 32 * lda;  // [2][32] dgrad row scales
         float* Pt = Sc + 64 + 4;          // dgrad, K <= 128: [4 waves][16][64] first-half partials
@@ -1158,6 +1322,7 @@ struct RelGemm {
         const int i_end = (int)((long long)(rng + 1) * n_items / G);
         if (i_beg >= i_end) return;
 
+        stamp_id();
         float4 v[WPT];
         int cnt;
         // up to 64 items per workgroup through the register table, the rest by scalar loads
@@ -1184,6 +1349,7 @@ struct RelGemm {
         __syncthreads();
         int buf = 0;
         for (int i = i_beg; i < i_end; ++i) {
+            stamp(i - i_beg, 0);
             const bool has_next = i + 1 < i_end;
             const Item nxt = has_next ? get_item(i + 1) : cur;
             if (has_next) {  // in flight during this item's MFMAs: rows of the next item, row
@@ -1229,21 +1395,36 @@ struct RelGemm {
                 ac = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.z, b[j + 2], ac, 0, 0, 0);
                 ac = __builtin_amdgcn_mfma_f32_32x32x2f32(cf.w, b[j + 3], ac, 0, 0, 0);
             }
+            stamp(i - i_beg, 1);
+            // next item's A tile into the other LDS buffer BEFORE this item's output stores: its
+            // wait (vmcnt, in order) then covers only the row loads issued at the top of the
+            // item, not 16 stores issued just before it (each would cost a write round trip)
+            if (has_next) commit(nxt, tid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
+            stamp(i - i_beg, 2);
             // epilogue: each accumulator register = rows (r&3) + 8(r>>2) + 4h, column 32·wave + c
             const float* sc = Sc + buf * 32;
             float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
+            auto out_val = [&](int r, int row) {
+                float o = kSplit ? acc[r] + acc2[r] : (kSplitLds ? pt[r * 64] + acc[r] : acc[r]);
+                if constexpr (DGRAD) {
+                    if (!cur.root) o = o * sc[row];
+                }
+                return o;
+            };
+            float* Yc = Yt + col0() + wave * 32 + c;
+            if (cur.nrows == 32) {  // uniform: a full item stores straight, no per-row exec branches
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (row < cur.nrows) {
-                    float o = kSplit ? acc[r] + acc2[r] : (kSplitLds ? pt[r * 64] + acc[r] : acc[r]);
-                    if constexpr (DGRAD) {
-                        if (!cur.root) o = o * sc[row];
-                    }
-                    Yt[(size_t)row * N + col0() + wave * 32 + c] = o;
+                for (int r = 0; r < 16; ++r) {
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    Yc[(size_t)row * N] = out_val(r, row);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (row < cur.nrows) Yc[(size_t)row * N] = out_val(r, row);
                 }
             }
-            if (has_next) commit(nxt, tid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
             if (new_w) {
                 if constexpr (kPrefetchB) {
 #pragma unroll
@@ -1252,17 +1433,19 @@ struct RelGemm {
                     load_b(nxt.w, wave, lane, b);  // after this item's chain: b is free
                 }
             }
+            stamp(i - i_beg, 3);
             __syncthreads();
+            stamp(i - i_beg, 4);
             cur = nxt;
             buf ^= 1;
         }
     }
 };
 
-template <int KB, bool DGRAD, int NB = 1>
-__global__ __launch_bounds__(kThreads, 2) void rel_gemm_kernel(RelGemmArgs a) {
+template <int KB, bool DGRAD, int NB = 1, int OCC = 2>
+__global__ __launch_bounds__(kThreads, OCC) void rel_gemm_kernel(RelGemmArgs a) {
     extern __shared__ float smem[];
-    RelGemm<KB, DGRAD, NB>::run(a, smem);
+    RelGemm<KB, DGRAD, NB, OCC>::run(a, smem);
 }
 
 template <int KB>  // Kp = 64·KB
@@ -2362,13 +2545,25 @@ static void launch_rel_gemm_wide(const RelGemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD, NB>), dim3(grid, NB), dim3(kThreads), lds, st, a);
 }
 
+static int rel_occ() {  // experiment switch: workgroups per CU of the B-stationary GEMM
+    static int v = [] {
+        const char* e = std::getenv("MPGNN_REL_OCC");
+        return e ? std::max(2, std::min(3, std::atoi(e))) : 2;
+    }();
+    return v;
+}
+
 template <int KB, bool DGRAD>
 static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
     constexpr int lda = 64 * KB + 4;
     const size_t lds = (size_t)(2 * 32 * lda + 64 + 4 + (DGRAD ? 4 * 16 * 64 : 0)) * sizeof(float);
     const int n_items = a.n_rel + a.n_root;
-    const int grid = std::min(n_items, cu_count() * 2);  // two workgroups per CU
-    hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
+    const int occ = rel_occ();
+    const int grid = std::min(n_items, cu_count() * occ);
+    if (occ == 3)
+        hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD, 1, 3>), dim3(grid), dim3(kThreads), lds, st, a);
+    else
+        hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
 static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, hipStream_t st) {
@@ -2598,6 +2793,9 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         r.sel_b = s.sel_b;
         r.row_lo = (int)row_lo;
         r.row_hi = (int)row_hi;
+#ifdef MPGNN_STAMPS
+        r.stamps = gather_kind == 1 ? nullptr : g_stamps_host;
+#endif
         TimedLaunch tl(kind, strm);
         launch_rel_gemm(r, K, gather_kind == 1, strm);
         return hip_check(hipGetLastError(), "rel_gemm_kernel launch");
@@ -3672,6 +3870,13 @@ int32_t mpgnn_debug_occupancy(int32_t F, int32_t* seg_tile_blocks_per_cu, int32_
     *tile_gemm_grid = cu_count() * ((2 * lds_t <= 160 * 1024) ? 2 : 1);
     return hip_check(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
 }
+
+#ifdef MPGNN_STAMPS
+int32_t mpgnn_debug_stamps_set(void* dev_ptr) {
+    g_stamps_host = static_cast<unsigned long long*>(dev_ptr);
+    return MPGNN_OK;
+}
+#endif
 
 int32_t mpgnn_timing_enable(int32_t on) {
     std::lock_guard<std::mutex> lk(g_timing_mu);
