@@ -74,9 +74,11 @@ enum mpgnn_table {
     MPGNN_T_REL_INVALID = 16,/* uint8 [nrel]   1 if an edge of this relation had a bad node index   */
     /* flat chunked lists (fast-path row sums): for list L in {SEG = segments over edges (cut at
      * relations), T = node_2 over col-major edges, RW = node_1 over row-major segments}:
-     * CHUNK_PTR [nch+1] positions (<= 32 each, cut at row ends), CHUNK_INFO [nch] (bit0 first row
-     * split, bit1 last row split, >>2 first carry slot), ROW_OF [positions], SPLIT_ROW [nsplit],
-     * SPLIT_PTR [nsplit+1], SPLIT_SLOT [slots]                                                     */
+     * CHUNK_PTR [nch+1] positions (<= 32 each, cut at row ends; a longer row is cut into pieces
+     * that hold only that row), CHUNK_INFO [nch] (bit0 first row split, bit1 last row split, >>2
+     * carry slot — a long group's piece index), ROW_OF [positions], SPLIT_ROW [nsplit] (rows of
+     * more than 16 pieces: summed across workgroups by the finalize kernel), SPLIT_PTR [nsplit+1],
+     * SPLIT_SLOT [slots]                                                                         */
     MPGNN_T_SEG_F_CHUNK_PTR = 17, MPGNN_T_SEG_F_CHUNK_INFO = 18, MPGNN_T_SEG_F_ROW_OF = 19,
     MPGNN_T_SEG_F_SPLIT_ROW = 20, MPGNN_T_SEG_F_SPLIT_PTR = 21, MPGNN_T_SEG_F_SPLIT_SLOT = 22,
     MPGNN_T_T_F_CHUNK_PTR = 23, MPGNN_T_T_F_CHUNK_INFO = 24, MPGNN_T_T_F_ROW_OF = 25,
@@ -93,7 +95,13 @@ enum mpgnn_table {
     /* SEGM = the flat chunked list of the multi-edge segments over EM_COL (cut at relations) */
     MPGNN_T_SEGM_F_CHUNK_PTR = 40, MPGNN_T_SEGM_F_CHUNK_INFO = 41, MPGNN_T_SEGM_F_ROW_OF = 42,
     MPGNN_T_SEGM_F_SPLIT_ROW = 43, MPGNN_T_SEGM_F_SPLIT_PTR = 44, MPGNN_T_SEGM_F_SPLIT_SLOT = 45,
-    MPGNN_T_COUNT = 46
+    /* workgroup groups of the flat lists (SEG, T, RW, SEGM): GROUP_PTR [ngroups+1] chunk range of
+     * each workgroup (<= 4 chunks of complete rows, or the 2..16 pieces of one long row),
+     * GROUP_LONG [ngroups] 1 for a long row's group (pieces summed in LDS, in order)         */
+    MPGNN_T_SEG_F_GROUP_PTR = 46, MPGNN_T_SEG_F_GROUP_LONG = 47, MPGNN_T_T_F_GROUP_PTR = 48,
+    MPGNN_T_T_F_GROUP_LONG = 49, MPGNN_T_RW_F_GROUP_PTR = 50, MPGNN_T_RW_F_GROUP_LONG = 51,
+    MPGNN_T_SEGM_F_GROUP_PTR = 52, MPGNN_T_SEGM_F_GROUP_LONG = 53,
+    MPGNN_T_COUNT = 54
 };
 
 typedef struct mpgnn_plan_info {

@@ -41,6 +41,9 @@ TABLES.update({"s_src": (35, "int32"), "m_ptr": (36, "int32"), "em_col": (37, "i
                "rel_m_ptr": (39, "int32")})
 for _j, _n in enumerate(("chunk_ptr", "chunk_info", "row_of", "split_row", "split_ptr", "split_slot")):
     TABLES[f"segm_f_{_n}"] = (40 + _j, "int32")
+for _i, _l in enumerate(("seg", "t", "rw", "segm")):  # workgroup groups of the flat lists, ids 46..53
+    TABLES[f"{_l}_f_group_ptr"] = (46 + 2 * _i, "int32")
+    TABLES[f"{_l}_f_group_long"] = (47 + 2 * _i, "int32")
 
 
 class PlanInfo(ctypes.Structure):

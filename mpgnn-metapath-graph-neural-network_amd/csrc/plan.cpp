@@ -226,7 +226,7 @@ static void build_ragged(const std::vector<int32_t>& run_ptr, RaggedHost& L) {
 }
 
 // Flat chunked list over runs r (positions [run_ptr[r], run_ptr[r+1]), output row r) with
-// forced cuts at run indices `cuts` (ascending, first 0, last = runs).
+// forced cuts at run indices `cuts` (ascending, first 0, last = runs); see FlatHost.
 static void build_flat(const std::vector<int32_t>& run_ptr, const std::vector<int32_t>& cuts, FlatHost& L,
                        int32_t chunk = kFlatChunk) {
     const int32_t runs = run_ptr.empty() ? 0 : (int32_t)run_ptr.size() - 1;
@@ -236,62 +236,70 @@ static void build_flat(const std::vector<int32_t>& run_ptr, const std::vector<in
     parallel_for(runs, [&](int64_t r) {
         for (int32_t q = run_ptr[r]; q < run_ptr[r + 1]; ++q) L.row_of[q] = (int32_t)r;
     });
-    L.chunk_ptr.push_back(0);
-    L.cut_chunk_ptr.push_back(0);
-    for (size_t ci = 0; ci + 1 < cuts.size(); ++ci) {
-        const int32_t pb = run_ptr[cuts[ci]], pe = run_ptr[cuts[ci + 1]];
-        int32_t cs = pb;  // current chunk start
-        int32_t q = pb;
-        while (q < pe) {
-            const int32_t r = L.row_of[q];
-            const int32_t rend = std::min(run_ptr[r + 1], pe);
-            if (rend - cs <= chunk) {  // the rest of run r fits the chunk
-                q = rend;
-                continue;
-            }
-            if (q > cs) {  // close the chunk before run r
-                L.chunk_ptr.push_back(q);
-                cs = q;
-                continue;
-            }
-            q = cs + chunk;  // run longer than a chunk: cut inside it
-            L.chunk_ptr.push_back(q);
-            cs = q;
-        }
-        if (q > cs) L.chunk_ptr.push_back(q);
-        L.cut_chunk_ptr.push_back((int32_t)L.chunk_ptr.size() - 1);
-    }
-    const int32_t nch = (int32_t)L.chunk_ptr.size() - 1;
-    L.chunk_info.resize(nch);
     L.row_split.assign(runs, -1);
+    L.chunk_ptr.push_back(0);
+    L.group_ptr.push_back(0);
+    L.cut_group_ptr.push_back(0);
     L.split_ptr.push_back(0);
     L.cut_split_ptr.push_back(0);
     int32_t slot = 0;
-    size_t ci = 0;
-    for (int32_t c = 0; c < nch; ++c) {
-        const int32_t a0 = L.chunk_ptr[c], a1 = L.chunk_ptr[c + 1];
-        const int32_t rf = L.row_of[a0], rl = L.row_of[a1 - 1];
-        const bool fs = run_ptr[rf] < a0, ls = run_ptr[rl + 1] > a1;
-        L.chunk_info[c] = (fs ? 1 : 0) | (ls ? 2 : 0) | (slot << 2);
-        // partial slots: the first run's (when split), then the last run's (when split and a
-        // different run); a chunk inside one long run has a single partial
-        auto add_partial = [&](int32_t row) {
-            if (L.row_split[row] < 0) {
-                L.row_split[row] = (int32_t)L.split_row.size();
-                L.split_row.push_back(row);
+    auto nch = [&] { return (int32_t)L.chunk_ptr.size() - 1; };
+    auto close_group = [&](int32_t is_long) {
+        if (nch() > L.group_ptr.back()) {
+            L.group_ptr.push_back(nch());
+            L.group_long.push_back(is_long);
+        }
+    };
+    for (size_t ci = 0; ci + 1 < cuts.size(); ++ci) {
+        int32_t cs = run_ptr[cuts[ci]];  // start of the open chunk
+        for (int32_t r = cuts[ci]; r < cuts[ci + 1]; ++r) {
+            const int32_t q = run_ptr[r], e = run_ptr[r + 1];
+            if (e - q <= chunk) {
+                if (e - cs > chunk) {  // run r does not fit the open chunk: close it before r
+                    L.chunk_ptr.push_back(q);
+                    L.chunk_info.push_back(0);
+                    cs = q;
+                    if (nch() - L.group_ptr.back() == kFlatGroup) close_group(0);
+                }
+                continue;
+            }
+            // long run: close the open chunk and group, then the run's pieces
+            if (q > cs) {
+                L.chunk_ptr.push_back(q);
+                L.chunk_info.push_back(0);
+            }
+            close_group(0);
+            const int32_t k = (e - q + chunk - 1) / chunk;
+            const bool local = k <= kFlatLongPieces;
+            if (!local) {
+                L.row_split[r] = (int32_t)L.split_row.size();
+                L.split_row.push_back(r);
                 L.split_ptr.push_back(L.split_ptr.back());
             }
-            L.split_slot.push_back(slot++);
-            ++L.split_ptr.back();
-        };
-        if (fs) add_partial(rf);
-        if (ls && (rl != rf || !fs)) add_partial(rl);
-        while (ci + 1 < L.cut_chunk_ptr.size() && L.cut_chunk_ptr[ci + 1] == c + 1) {
-            L.cut_split_ptr.push_back((int32_t)L.split_row.size());
-            ++ci;
+            for (int32_t i = 0; i < k; ++i) {
+                L.chunk_ptr.push_back(std::min(q + (i + 1) * chunk, e));
+                const int32_t flags = (i > 0 ? 1 : 0) | (i + 1 < k ? 2 : 0);
+                if (local) {
+                    L.chunk_info.push_back(flags | (i << 2));
+                } else {
+                    L.chunk_info.push_back(flags | (slot << 2));
+                    L.split_slot.push_back(slot++);
+                    ++L.split_ptr.back();
+                    if (nch() - L.group_ptr.back() == kFlatGroup) close_group(0);
+                }
+            }
+            close_group(local ? 1 : 0);
+            cs = e;
         }
+        const int32_t pe = run_ptr[cuts[ci + 1]];
+        if (pe > cs) {
+            L.chunk_ptr.push_back(pe);
+            L.chunk_info.push_back(0);
+        }
+        close_group(0);
+        L.cut_group_ptr.push_back((int32_t)L.group_ptr.size() - 1);
+        L.cut_split_ptr.push_back((int32_t)L.split_row.size());
     }
-    while (L.cut_split_ptr.size() < L.cut_chunk_ptr.size()) L.cut_split_ptr.push_back((int32_t)L.split_row.size());
     L.nslots = slot;
 }
 
@@ -747,8 +755,15 @@ static const void* table_ptr(const mpgnn_plan* p, int32_t t, int64_t* n, int32_t
         case MPGNN_T_REL_M_PTR: *n = (int64_t)p->rel_m_ptr.size(); return p->rel_m_ptr.data();
         default: break;
     }
+    if (t >= MPGNN_T_SEG_F_GROUP_PTR && t < MPGNN_T_COUNT) {
+        const int k = t - MPGNN_T_SEG_F_GROUP_PTR;
+        const FlatHost* lists[4] = {&p->seg_f, &p->t_f, &p->rw_f, &p->segm_f};
+        const std::vector<int32_t>* v = (k & 1) ? &lists[k >> 1]->group_long : &lists[k >> 1]->group_ptr;
+        *n = (int64_t)v->size();
+        return v->data();
+    }
     const bool seg_lists = t >= MPGNN_T_SEG_F_CHUNK_PTR && t <= MPGNN_T_RW_F_SPLIT_SLOT;
-    if (seg_lists || (t >= MPGNN_T_SEGM_F_CHUNK_PTR && t < MPGNN_T_COUNT)) {
+    if (seg_lists || (t >= MPGNN_T_SEGM_F_CHUNK_PTR && t <= MPGNN_T_SEGM_F_SPLIT_SLOT)) {
         const int k = seg_lists ? t - MPGNN_T_SEG_F_CHUNK_PTR : t - MPGNN_T_SEGM_F_CHUNK_PTR;
         const FlatHost& L = !seg_lists ? p->segm_f : (k < 6 ? p->seg_f : (k < 12 ? p->t_f : p->rw_f));
         const std::vector<int32_t>* v = nullptr;
@@ -836,28 +851,28 @@ int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
         {&p->d.seg_f.chunk_ptr, &p->seg_f.chunk_ptr}, {&p->d.seg_f.chunk_info, &p->seg_f.chunk_info},
         {&p->d.seg_f.row_of, &p->seg_f.row_of}, {&p->d.seg_f.split_row, &p->seg_f.split_row},
         {&p->d.seg_f.split_ptr, &p->seg_f.split_ptr}, {&p->d.seg_f.split_slot, &p->seg_f.split_slot},
-        {&p->d.seg_f.row_split, &p->seg_f.row_split},
+        {&p->d.seg_f.row_split, &p->seg_f.row_split}, {&p->d.seg_f.group_ptr, &p->seg_f.group_ptr}, {&p->d.seg_f.group_long, &p->seg_f.group_long},
         {&p->d.t_f.chunk_ptr, &p->t_f.chunk_ptr}, {&p->d.t_f.chunk_info, &p->t_f.chunk_info},
         {&p->d.t_f.row_of, &p->t_f.row_of}, {&p->d.t_f.split_row, &p->t_f.split_row},
         {&p->d.t_f.split_ptr, &p->t_f.split_ptr}, {&p->d.t_f.split_slot, &p->t_f.split_slot},
-        {&p->d.t_f.row_split, &p->t_f.row_split},
+        {&p->d.t_f.row_split, &p->t_f.row_split}, {&p->d.t_f.group_ptr, &p->t_f.group_ptr}, {&p->d.t_f.group_long, &p->t_f.group_long},
         {&p->d.rw_f.chunk_ptr, &p->rw_f.chunk_ptr}, {&p->d.rw_f.chunk_info, &p->rw_f.chunk_info},
         {&p->d.rw_f.row_of, &p->rw_f.row_of}, {&p->d.rw_f.split_row, &p->rw_f.split_row},
         {&p->d.rw_f.split_ptr, &p->rw_f.split_ptr}, {&p->d.rw_f.split_slot, &p->rw_f.split_slot},
-        {&p->d.rw_f.row_split, &p->rw_f.row_split},
+        {&p->d.rw_f.row_split, &p->rw_f.row_split}, {&p->d.rw_f.group_ptr, &p->rw_f.group_ptr}, {&p->d.rw_f.group_long, &p->rw_f.group_long},
         {&p->d.tx_f.chunk_ptr, &p->tx_f.chunk_ptr}, {&p->d.tx_f.chunk_info, &p->tx_f.chunk_info},
         {&p->d.tx_f.row_of, &p->tx_f.row_of}, {&p->d.tx_f.split_row, &p->tx_f.split_row},
         {&p->d.tx_f.split_ptr, &p->tx_f.split_ptr}, {&p->d.tx_f.split_slot, &p->tx_f.split_slot},
-        {&p->d.tx_f.row_split, &p->tx_f.row_split}, {&p->d.tx_val, &p->tx_val},
+        {&p->d.tx_f.row_split, &p->tx_f.row_split}, {&p->d.tx_f.group_ptr, &p->tx_f.group_ptr}, {&p->d.tx_f.group_long, &p->tx_f.group_long}, {&p->d.tx_val, &p->tx_val},
         {&p->d.rwx_f.chunk_ptr, &p->rwx_f.chunk_ptr}, {&p->d.rwx_f.chunk_info, &p->rwx_f.chunk_info},
         {&p->d.rwx_f.row_of, &p->rwx_f.row_of}, {&p->d.rwx_f.split_row, &p->rwx_f.split_row},
         {&p->d.rwx_f.split_ptr, &p->rwx_f.split_ptr}, {&p->d.rwx_f.split_slot, &p->rwx_f.split_slot},
-        {&p->d.rwx_f.row_split, &p->rwx_f.row_split}, {&p->d.rwx_val, &p->rwx_val},
+        {&p->d.rwx_f.row_split, &p->rwx_f.row_split}, {&p->d.rwx_f.group_ptr, &p->rwx_f.group_ptr}, {&p->d.rwx_f.group_long, &p->rwx_f.group_long}, {&p->d.rwx_val, &p->rwx_val},
         {&p->d.s_src, &p->s_src}, {&p->d.m_ptr, &p->m_ptr}, {&p->d.em_col, &p->em_col}, {&p->d.m_cnt, &p->m_cnt},
         {&p->d.segm_f.chunk_ptr, &p->segm_f.chunk_ptr}, {&p->d.segm_f.chunk_info, &p->segm_f.chunk_info},
         {&p->d.segm_f.row_of, &p->segm_f.row_of}, {&p->d.segm_f.split_row, &p->segm_f.split_row},
         {&p->d.segm_f.split_ptr, &p->segm_f.split_ptr}, {&p->d.segm_f.split_slot, &p->segm_f.split_slot},
-        {&p->d.segm_f.row_split, &p->segm_f.row_split},
+        {&p->d.segm_f.row_split, &p->segm_f.row_split}, {&p->d.segm_f.group_ptr, &p->segm_f.group_ptr}, {&p->d.segm_f.group_long, &p->segm_f.group_long},
     };
     size_t total = 0;
     std::vector<size_t> offs;

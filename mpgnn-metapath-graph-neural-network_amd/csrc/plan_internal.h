@@ -46,30 +46,41 @@ struct RaggedHost {
 };
 
 // Flat chunked list (flat_rows_kernel): the positions of a list whose consecutive runs are
-// output rows, cut into chunks of at most kFlatChunk positions — at run ends, except inside a
-// run longer than a chunk (and at forced cuts: relation boundaries of the segment list).  A
-// chunk's first / last run may be split with its neighbours; their partial sums go to carry
-// slots that the finalize kernel adds in chunk order.
+// output rows, cut into chunks of at most kFlatChunk positions at run ends (and at forced cuts:
+// relation boundaries of the segment lists). A run longer than a chunk is cut into pieces of
+// kFlatChunk positions that hold only that run. Chunks are dealt to workgroups in GROUPS:
+//   - a normal group: up to kFlatGroup chunks of complete runs (one wave each);
+//   - a long group: the 2..kFlatLongPieces pieces of ONE run; the workgroup's waves sum the
+//     pieces into LDS and one wave adds them in piece order (no second launch);
+//   - pieces of a run longer than kFlatLongPieces chunks (grad_x hubs) go to normal groups as
+//     split chunks: their partials go to global carry slots that finalize_rows_kernel adds in
+//     chunk order.
 constexpr int kFlatChunk = 32;
 // The row-major (combine) lists have few positions (S + N ≈ 63 k at C3 vs E = 310 k for the
 // means), so they are cut finer to give the combine launch enough waves: 11.7 → 10.6 µs.
 constexpr int kFlatChunkRowMajor = 16;
+constexpr int kFlatGroup = 4;         // chunks per normal group (= waves per workgroup)
+constexpr int kFlatLongPieces = 16;   // pieces a long group sums in LDS (<= 16 · F floats)
 
 struct FlatHost {
     std::vector<int32_t> chunk_ptr;   // [nch+1] positions
-    std::vector<int32_t> chunk_info;  // [nch] bit0: first run split, bit1: last run split, >>2: first slot
+    std::vector<int32_t> chunk_info;  // [nch] bit0: first run split, bit1: last run split, >>2: carry slot
+                                      // (long-group pieces: the piece index, an LDS slot)
     std::vector<int32_t> row_of;      // [positions] output row of each position
-    std::vector<int32_t> split_row;   // [nsplit] rows split across chunks
+    std::vector<int32_t> group_ptr;   // [ngroups+1] chunk range of each workgroup
+    std::vector<int32_t> group_long;  // [ngroups] 1: long group (pieces of one run)
+    std::vector<int32_t> split_row;   // [nsplit] rows split across workgroups
     std::vector<int32_t> split_ptr;   // [nsplit+1] into split_slot
     std::vector<int32_t> split_slot;  // partial slots of each split row, in chunk order
     std::vector<int32_t> row_split;   // [nrows] split index of each row, -1 if not split
-    std::vector<int32_t> cut_chunk_ptr;  // [ncuts+1] chunk range of each forced-cut section
+    std::vector<int32_t> cut_group_ptr;  // [ncuts+1] group range of each forced-cut section
     std::vector<int32_t> cut_split_ptr;  // [ncuts+1] split-row range of each section
     int32_t nslots = 0;
 };
 
 struct FlatDev {
     int32_t *chunk_ptr = nullptr, *chunk_info = nullptr, *row_of = nullptr;
+    int32_t *group_ptr = nullptr, *group_long = nullptr;
     int32_t *split_row = nullptr, *split_ptr = nullptr, *split_slot = nullptr, *row_split = nullptr;
 };
 

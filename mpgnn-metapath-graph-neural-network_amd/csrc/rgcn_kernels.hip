@@ -1596,8 +1596,10 @@ __global__ __launch_bounds__(kThreads) void row_sum_kernel(RowSumArgs a) {
 // ----------------------------------------------------------------------------------------
 struct FlatArgs {
     const int* chunk_ptr;
-    const int* chunk_info;  // bit0 first row split, bit1 last row split, >>2 first carry slot
-    int c_lo, c_hi;         // chunks of this launch
+    const int* chunk_info;  // bit0 first row split, bit1 last row split, >>2 carry slot (long group: piece)
+    const int* group_ptr;   // chunk range of each workgroup
+    const int* group_long;  // 1: the pieces of one long row, summed in LDS in piece order
+    int g_lo, g_hi;         // groups of this launch
     const int* table;       // value per position: source row + idx_off
     const int* row_of;      // output row per position
     const float* src;       // [*, F]
@@ -1615,11 +1617,33 @@ struct FlatArgs {
     int relu;               // fused activation on complete rows (unsharded combine only)
 };
 
-template <int V, int T, int U = 16>
-__global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int c = a.c_lo + (int)blockIdx.x * kWaves + (int)(threadIdx.x >> 6);
-    if (c >= a.c_hi) return;
+// The finishing step of a complete row: / cnt (IEEE), + bias on own rows, fused ReLU.
+template <int V, int T>
+__device__ __forceinline__ void flat_finish_store(const FlatArgs& a, int rr, float d, bool div, const float (&bb)[T][V],
+                                                  const float (&acc)[T][V], int lane) {
+    const bool addb = a.bias != nullptr && rr >= a.lo && rr < a.hi;
+    float* dst = a.out + (size_t)(rr - a.row_off) * a.F;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int col = (t * 64 + lane) * V;
+        if (col < a.F) {
+            float o[V];
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+                o[k] = div ? acc[t][k] / d : acc[t][k];
+                if (addb) o[k] = o[k] + bb[t][k];
+                if (a.relu) o[k] = relu_f(o[k]);
+            }
+            vstore<V>(dst + col, o);
+        }
+    }
+}
+
+// One wave sums one chunk (<= 32 positions): complete rows are finished and stored; the
+// partial of a split row goes to carry slot `info >> 2` of `carry` (global slots, or the LDS
+// piece slots of a long group).
+template <int V, int T, int U>
+__device__ __forceinline__ void flat_chunk(const FlatArgs& a, int c, int lane, float* carry, const float (&bb)[T][V]) {
     const int p0 = ld_uniform(a.chunk_ptr, c);
     const int n = ld_uniform(a.chunk_ptr, c + 1) - p0;  // 1 .. kFlatChunk
     const int info = ld_uniform(a.chunk_info, c);
@@ -1644,14 +1668,6 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
     int colc[T];
 #pragma unroll
     for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, F - V);
-    const bool has_b = a.bias != nullptr;
-    float bb[T][V];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-        vload<V>(has_b ? a.bias + colc[t] : a.src, bb[t]);
-#pragma unroll
-        for (int k = 0; k < V; ++k) bb[t][k] = has_b ? bb[t][k] : 0.0f;
-    }
 
     float acc[T][V];
     zero_acc<V, T>(acc);
@@ -1679,29 +1695,14 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
                 if ((lastm >> q) & 1ull) {
                     const int rr = readlane(row, q);
                     const bool split = (rr == rf && fs) || (rr == rl && ls);
-                    float* dst;
-                    bool div = false, addb = false;
                     if (!split) {
-                        dst = a.out + (size_t)(rr - a.row_off) * F;
-                        div = has_cnt;
-                        addb = has_b && rr >= a.lo && rr < a.hi;
-                    } else {
-                        const int slot = slot0 + ((fs && rr == rl && rl != rf) ? 1 : 0);
-                        dst = a.carry + (size_t)slot * F;
-                    }
-                    const float d = (float)readlane(cnt_l, q);
+                        flat_finish_store<V, T>(a, rr, (float)readlane(cnt_l, q), has_cnt, bb, acc, lane);
+                    } else {  // a split chunk holds one row: its partial
+                        float* dst = carry + (size_t)slot0 * F;
 #pragma unroll
-                    for (int t = 0; t < T; ++t) {
-                        const int col = (t * 64 + lane) * V;
-                        if (col < F) {
-                            float o[V];
-#pragma unroll
-                            for (int k = 0; k < V; ++k) {
-                                o[k] = div ? acc[t][k] / d : acc[t][k];
-                                if (addb) o[k] = o[k] + bb[t][k];
-                                if (!split && a.relu) o[k] = relu_f(o[k]);
-                            }
-                            vstore<V>(dst + col, o);
+                        for (int t = 0; t < T; ++t) {
+                            const int col = (t * 64 + lane) * V;
+                            if (col < F) vstore<V>(dst + col, acc[t]);
                         }
                     }
                     zero_acc<V, T>(acc);
@@ -1710,6 +1711,53 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
         }
         __builtin_amdgcn_sched_barrier(0);
     }
+}
+
+// flat_rows_kernel — one workgroup per group: a normal group's waves take one chunk each; a
+// long group's waves sum the pieces w, w + 4, … into LDS slots, then wave 0 adds the slots in
+// piece order and finishes the row (one launch, no finalize for rows of <= 16 pieces).
+template <int V, int T, int U = 16>
+__global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds_pieces[];  // [kFlatLongPieces][F] (long groups)
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int g = a.g_lo + (int)blockIdx.x;
+    const int c0 = ld_uniform(a.group_ptr, g), c1 = ld_uniform(a.group_ptr, g + 1);
+    const bool lng = ld_uniform(a.group_long, g) != 0;
+    const int F = a.F;
+    int colc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, F - V);
+    const bool has_b = a.bias != nullptr;
+    float bb[T][V];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        vload<V>(has_b ? a.bias + colc[t] : a.src, bb[t]);
+#pragma unroll
+        for (int k = 0; k < V; ++k) bb[t][k] = has_b ? bb[t][k] : 0.0f;
+    }
+    if (!lng) {
+        const int c = c0 + wave;
+        if (c < c1) flat_chunk<V, T, U>(a, c, lane, a.carry, bb);
+        return;
+    }
+    for (int c = c0 + wave; c < c1; c += kWaves) flat_chunk<V, T, U>(a, c, lane, lds_pieces, bb);
+    __syncthreads();
+    if (wave != 0) return;
+    const int rr = a.row_of[ld_uniform(a.chunk_ptr, c0)];
+    float acc[T][V];
+    zero_acc<V, T>(acc);
+    for (int k = 0; k < c1 - c0; ++k) {  // pieces in order
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            float v[V];
+            vload<V>(lds_pieces + (size_t)k * F + colc[t], v);
+#pragma unroll
+            for (int q = 0; q < V; ++q) acc[t][q] += v[q];
+        }
+    }
+    const bool has_cnt = a.cnt != nullptr;
+    flat_finish_store<V, T>(a, rr, has_cnt ? (float)a.cnt[rr] : 1.0f, has_cnt, bb, acc, lane);
 }
 
 // finalize_rows_kernel — one wave per row.
@@ -2993,8 +3041,9 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
 
 template <int V, int T>
 static void launch_flat(const FlatArgs& a, hipStream_t st) {
-    const int n = a.c_hi - a.c_lo;
-    hipLaunchKernelGGL((flat_rows_kernel<V, T>), dim3((n + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
+    const int n = a.g_hi - a.g_lo;
+    const size_t lds = (size_t)kFlatLongPieces * a.F * sizeof(float);
+    hipLaunchKernelGGL((flat_rows_kernel<V, T>), dim3(n), dim3(kThreads), lds, st, a);
 }
 
 template <int V, int T>
@@ -3008,12 +3057,12 @@ __global__ __launch_bounds__(kThreads) void relu_kernel(float* __restrict__ p, s
         p[i] = relu_f(p[i]);
 }
 
-// Fast-path row sums over a flat chunked list: flat_rows_kernel over chunks [c_lo, c_hi), then
+// Fast-path row sums over a flat chunked list: flat_rows_kernel over groups [g_lo, g_hi), then
 // finalize_rows_kernel — mode 0 over split rows [k_lo, k_hi) (means: no empty rows, no extra),
 // mode 1 over every row [r_lo, r_hi) (split and empty rows, extra + bias on own rows).
 struct FlatRun {
     const FlatDev* fd;
-    int c_lo, c_hi, k_lo, k_hi;
+    int g_lo, g_hi, k_lo, k_hi;
     const int* table;
     int idx_off, filter, flo, fhi;
     const float* src;
@@ -3034,12 +3083,14 @@ struct FlatRun {
 static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
     int V, T;
     pick_vt(f.F, &V, &T);
-    if (f.c_hi > f.c_lo) {
+    if (f.g_hi > f.g_lo) {
         FlatArgs a{};
         a.chunk_ptr = f.fd->chunk_ptr;
         a.chunk_info = f.fd->chunk_info;
-        a.c_lo = f.c_lo;
-        a.c_hi = f.c_hi;
+        a.group_ptr = f.fd->group_ptr;
+        a.group_long = f.fd->group_long;
+        a.g_lo = f.g_lo;
+        a.g_hi = f.g_hi;
         a.table = f.table;
         a.row_of = f.fd->row_of;
         a.src = f.src;
@@ -3102,8 +3153,8 @@ static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x
         // flat chunked list; chunks and splits of the relation range [d_lo, d_hi)
         FlatRun f{};
         f.fd = &p->d.seg_f;
-        f.c_lo = p->seg_f.cut_chunk_ptr[s.d_lo];
-        f.c_hi = p->seg_f.cut_chunk_ptr[s.d_hi];
+        f.g_lo = p->seg_f.cut_group_ptr[s.d_lo];
+        f.g_hi = p->seg_f.cut_group_ptr[s.d_hi];
         f.k_lo = p->seg_f.cut_split_ptr[s.d_lo];
         f.k_hi = p->seg_f.cut_split_ptr[s.d_hi];
         f.table = p->d.e_col;
@@ -3142,8 +3193,8 @@ static int32_t run_means_multi(const mpgnn_plan* p, const Selection& s, const fl
     if (!exact) {
         FlatRun f{};
         f.fd = &p->d.segm_f;
-        f.c_lo = p->segm_f.cut_chunk_ptr[s.d_lo];
-        f.c_hi = p->segm_f.cut_chunk_ptr[s.d_hi];
+        f.g_lo = p->segm_f.cut_group_ptr[s.d_lo];
+        f.g_hi = p->segm_f.cut_group_ptr[s.d_hi];
         f.k_lo = p->segm_f.cut_split_ptr[s.d_lo];
         f.k_hi = p->segm_f.cut_split_ptr[s.d_hi];
         f.table = p->d.em_col;
@@ -3387,8 +3438,8 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         }
         FlatRun f{};
         f.fd = &p->d.rwx_f;
-        f.c_lo = 0;
-        f.c_hi = (int)p->rwx_f.chunk_ptr.size() - 1;
+        f.g_lo = 0;
+        f.g_hi = (int)p->rwx_f.group_ptr.size() - 1;
         f.k_lo = 0;
         f.k_hi = (int)p->rwx_f.split_row.size();
         f.table = p->d.rwx_val;
@@ -3413,8 +3464,8 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     if (mode == MPGNN_MODE_ALL && !exact) {
         FlatRun f{};
         f.fd = &p->d.rw_f;
-        f.c_lo = 0;
-        f.c_hi = (int)p->rw_f.chunk_ptr.size() - 1;
+        f.g_lo = 0;
+        f.g_hi = (int)p->rw_f.group_ptr.size() - 1;
         f.table = p->d.rw_seg;
         f.idx_off = s.sel_b;
         f.filter = !s.all_segments;
@@ -3498,8 +3549,8 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         }
         FlatRun f{};
         f.fd = &p->d.tx_f;
-        f.c_lo = 0;
-        f.c_hi = (int)p->tx_f.chunk_ptr.size() - 1;
+        f.g_lo = 0;
+        f.g_hi = (int)p->tx_f.group_ptr.size() - 1;
         f.k_lo = 0;
         f.k_hi = (int)p->tx_f.split_row.size();
         f.table = p->d.tx_val;
@@ -3522,8 +3573,8 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
     } else if (mode == MPGNN_MODE_ALL && !exact) {
         FlatRun f{};
         f.fd = &p->d.t_f;
-        f.c_lo = 0;
-        f.c_hi = (int)p->t_f.chunk_ptr.size() - 1;
+        f.g_lo = 0;
+        f.g_hi = (int)p->t_f.group_ptr.size() - 1;
         f.table = p->d.t_seg;
         f.idx_off = s.sel_b;
         f.filter = !s.all_segments;

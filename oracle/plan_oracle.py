@@ -15,6 +15,8 @@ import numpy as np
 TILE_ROWS = 64
 FLAT_CHUNK = 32
 FLAT_CHUNK_ROW_MAJOR = 16  # the row-major (combine) list (plan_internal.h kFlatChunkRowMajor)
+FLAT_GROUP = 4             # chunks per normal workgroup group (kFlatGroup)
+FLAT_LONG_PIECES = 16      # pieces of a run one workgroup sums in LDS (kFlatLongPieces)
 
 
 def build_plan(edge_index: np.ndarray, edge_type: np.ndarray, num_nodes: int,
@@ -110,53 +112,69 @@ def build_plan(edge_index: np.ndarray, edge_type: np.ndarray, num_nodes: int,
 
 def build_flat(run_ptr: np.ndarray, cuts: np.ndarray, chunk: int = FLAT_CHUNK) -> dict:
     """Flat chunked list over runs (run r = positions [run_ptr[r], run_ptr[r+1]), output row r),
-    as the fast-path row sums consume it: chunks of at most ``chunk`` positions, cut at run ends
-    (and at the forced run cuts ``cuts``); a run that does not fit an empty chunk is cut inside.
-    Per chunk: bit0 first run split (starts earlier), bit1 last run split (continues later),
-    first carry slot << 2; split runs with their carry slots in chunk order."""
+    as the fast-path row sums consume it (plan_internal.h FlatHost): chunks of at most ``chunk``
+    positions holding complete runs, cut at run ends (and at the forced run cuts ``cuts``); a run
+    longer than a chunk is cut into pieces that hold only that run. Workgroup groups: up to
+    FLAT_GROUP chunks of complete runs, or — for a run of 2..FLAT_LONG_PIECES pieces — that run's
+    pieces alone (group_long = 1; chunk_info carries the piece index). A run of more pieces is
+    split across groups of FLAT_GROUP pieces with one global carry slot per piece (split tables).
+    chunk_info: bit0 first run split (starts earlier), bit1 last run split (continues later),
+    >> 2 carry slot."""
     run_ptr = np.asarray(run_ptr, dtype=np.int64)
     runs = len(run_ptr) - 1
-    P = int(run_ptr[-1]) if runs > 0 else 0
     row_of = np.repeat(np.arange(max(runs, 0)), np.diff(run_ptr)) if runs > 0 else np.zeros(0, np.int64)
-    bounds = [0]
+    bounds, info, gptr, glong = [0], [], [0], []
+    split_rows, split_ptr, split_slot = [], [0], []
+    slot = 0
+
+    def close_group(is_long):
+        if len(bounds) - 1 > gptr[-1]:
+            gptr.append(len(bounds) - 1)
+            glong.append(is_long)
+
     for a, b in zip(cuts[:-1], cuts[1:]):
-        pb, pe = int(run_ptr[a]), int(run_ptr[b])
-        cs = pb
+        cs = int(run_ptr[a])
         for r in range(int(a), int(b)):
-            q, end = int(run_ptr[r]), int(run_ptr[r + 1])
-            while q < end:
-                if end - cs <= chunk:      # the rest of run r joins the open chunk
-                    q = end
-                elif q > cs:               # close the chunk before run r
+            q, e = int(run_ptr[r]), int(run_ptr[r + 1])
+            if e - q <= chunk:
+                if e - cs > chunk:         # run r does not fit the open chunk: close it before r
                     bounds.append(q)
+                    info.append(0)
                     cs = q
-                else:                      # run longer than a chunk: cut inside it
-                    q = cs + chunk
-                    bounds.append(q)
-                    cs = q
+                    if len(bounds) - 1 - gptr[-1] == FLAT_GROUP:
+                        close_group(0)
+                continue
+            if q > cs:                     # long run: close the open chunk and group
+                bounds.append(q)
+                info.append(0)
+            close_group(0)
+            k = (e - q + chunk - 1) // chunk
+            local = k <= FLAT_LONG_PIECES
+            if not local:
+                split_rows.append(r)
+                split_ptr.append(split_ptr[-1])
+            for i in range(k):
+                bounds.append(min(q + (i + 1) * chunk, e))
+                flags = (1 if i > 0 else 0) | (2 if i + 1 < k else 0)
+                if local:
+                    info.append(flags | (i << 2))
+                else:
+                    info.append(flags | (slot << 2))
+                    split_slot.append(slot)
+                    slot += 1
+                    split_ptr[-1] += 1
+                    if len(bounds) - 1 - gptr[-1] == FLAT_GROUP:
+                        close_group(0)
+            close_group(1 if local else 0)
+            cs = e
+        pe = int(run_ptr[b])
         if pe > cs:
             bounds.append(pe)
-    info, split_rows, split_ptr, split_slot = [], [], [0], []
-    seen = {}
-    slot = 0
-    for c in range(len(bounds) - 1):
-        a0, a1 = bounds[c], bounds[c + 1]
-        rf, rl = int(row_of[a0]), int(row_of[a1 - 1])
-        fs, ls = run_ptr[rf] < a0, run_ptr[rl + 1] > a1
-        info.append((1 if fs else 0) | (2 if ls else 0) | (slot << 2))
-        parts = ([rf] if fs else []) + ([rl] if ls and (rl != rf or not fs) else [])
-        for row in parts:
-            if row not in seen:
-                seen[row] = len(split_rows)
-                split_rows.append(row)
-                split_ptr.append(split_ptr[-1])
-            split_slot.append(slot)
-            slot += 1
-            split_ptr[-1] += 1
-    assert P == 0 or bounds[-1] == P
+            info.append(0)
+        close_group(0)
     i32 = lambda v: np.asarray(v, dtype=np.int32)  # noqa: E731
     return dict(chunk_ptr=i32(bounds), chunk_info=i32(info), row_of=i32(row_of), split_row=i32(split_rows),
-                split_ptr=i32(split_ptr), split_slot=i32(split_slot))
+                split_ptr=i32(split_ptr), split_slot=i32(split_slot), group_ptr=i32(gptr), group_long=i32(glong))
 
 
 def masked_edges(edge_index: np.ndarray, edge_type: np.ndarray, relation: int) -> np.ndarray:

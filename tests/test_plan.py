@@ -13,7 +13,8 @@ TABLES = ["rel_values", "rel_seg_ptr", "rel_edge_ptr", "e_col", "e_id", "s_ptr",
           "s_cnt", "s_pos", "rw_ptr", "rw_seg", "t_ptr", "t_seg", "ta_col", "ta_seg", "rel_invalid",
           "s_src", "m_ptr", "em_col", "m_cnt", "rel_m_ptr"]
 FLAT = [f"{l}_f_{n}" for l in ("seg", "t", "rw", "segm")
-        for n in ("chunk_ptr", "chunk_info", "row_of", "split_row", "split_ptr", "split_slot")]
+        for n in ("chunk_ptr", "chunk_info", "row_of", "split_row", "split_ptr", "split_slot", "group_ptr",
+                  "group_long")]
 
 
 def graphs():
@@ -142,11 +143,13 @@ def test_plan_cache_reuses_and_invalidates():
 @pytest.mark.parametrize("shard", [None, (0.3, 0.7)])
 def test_flat_lists_bit_exact_and_well_formed(case, shard):
     """Flat chunked lists (fast-path row sums) == the numpy restatement, and well formed:
-    chunks of 1..32 positions covering every position once, cut at row ends unless the row is
-    longer than a chunk; split rows have one carry slot per chunk they touch."""
+    chunks of 1..32 (16) positions covering every position once, cut at row ends; a row longer
+    than a chunk is cut into pieces holding only that row; groups of <= 4 chunks of complete
+    rows, or the 2..16 pieces of one row (long group); rows of more pieces have one global carry
+    slot per piece."""
     name, ei, et, N = case
-    if name == "hubs":  # long segments / in-lists: rows of 1, 31, 32, 33, 64, 65, 300 entries
-        rows = [1, 31, 32, 33, 64, 65, 300, 2, 5]
+    if name == "hubs":  # long segments / in-lists: rows of 1, 31, 32, 33, 64, 65, 300, 600 entries
+        rows = [1, 31, 32, 33, 64, 65, 300, 600, 2, 5]
         n1 = np.concatenate([np.full(k, i) for i, k in enumerate(rows)])
         n2 = np.concatenate([np.arange(k) % 40 for k in rows])
         ei, et, N = np.stack([n1, n2]), np.zeros(len(n1), np.int64), 40
@@ -165,13 +168,29 @@ def test_flat_lists_bit_exact_and_well_formed(case, shard):
         assert cp[0] == 0 and cp[-1] == (run_ptr[-1] if len(run_ptr) else 0), l
         ends = set(run_ptr.tolist())
         row_of = plan.table(f"{l}_f_row_of")
-        for b in cp[1:-1]:
-            if b not in ends:  # a cut inside a row: that row is longer than one chunk
-                r = row_of[b]
-                assert run_ptr[r + 1] - run_ptr[r] > chunk, (l, r)
+        info = plan.table(f"{l}_f_chunk_info")
+        for c in range(len(cp) - 1):
+            a0, a1 = cp[c], cp[c + 1]
+            rf, rl = row_of[a0], row_of[a1 - 1]
+            if a0 not in ends or a1 not in ends:  # a piece: one long row only
+                assert rf == rl and run_ptr[rf + 1] - run_ptr[rf] > chunk, (l, c)
+                assert (info[c] & 3) == ((a0 != run_ptr[rf]) | ((a1 != run_ptr[rf + 1]) << 1)), (l, c)
+            else:
+                assert info[c] == 0, (l, c)
+        gp, gl = plan.table(f"{l}_f_group_ptr"), plan.table(f"{l}_f_group_long")
+        assert gp[0] == 0 and gp[-1] == len(cp) - 1 and len(gl) == len(gp) - 1, l
+        for g in range(len(gl)):
+            n = gp[g + 1] - gp[g]
+            if gl[g]:  # all pieces of one row, in order, piece index in the info
+                rows_g = {row_of[cp[c]] for c in range(gp[g], gp[g + 1])}
+                assert len(rows_g) == 1 and 2 <= n <= 16, (l, g)
+                assert [info[c] >> 2 for c in range(gp[g], gp[g + 1])] == list(range(n)), (l, g)
+            else:
+                assert 1 <= n <= 4, (l, g)
         sp, ss = plan.table(f"{l}_f_split_ptr"), plan.table(f"{l}_f_split_slot")
         assert len(np.unique(ss)) == len(ss), l
         for k, r in enumerate(plan.table(f"{l}_f_split_row")):
+            assert run_ptr[r + 1] - run_ptr[r] > 16 * chunk, (l, r)
             touched = np.unique(np.searchsorted(cp, np.arange(run_ptr[r], run_ptr[r + 1]), side="right"))
             assert sp[k + 1] - sp[k] == len(touched), (l, r)
 
