@@ -1,32 +1,35 @@
 #!/usr/bin/env python3
-"""Bench: edges aggregated/sec of the metapath-RGCN relational stack on MI355X.
+"""Bench: edges aggregated/sec of the metapath-RGCN relational layers on MI355X.
 
-Workload (BASELINE.json configs[2]): FB15K-237-shaped graph, N = 14,541,
-R = 237, E = 310,116, 128-d features; the RGCN stack of model.py:Net (main_rgcn.py:547,
-L = 3: conv1 then the shared conv2 twice, ReLU after each) with 128-d hidden/output.
+Workload (BASELINE.json configs[2]): the FB15K-237-shaped graph of the §8d
+recipe (N = 14,541, R = 237, E = 310,116, S ≈ 208 k segments), 128-d features; mode ALL = the
+RGCN stack of model.py:Net (main_rgcn.py:547, L = 3: conv1 then the shared conv2 twice, ReLU
+after each). ``--mode single`` times the MPGNN metapath layer instead: MPNetm's CustomRGCNConv
+chain over one metapath (model.py:203-228, mp_rgcn_layer.py:225-246; C2: 2 hops, C5: 3 hops).
 
-One timed STEP = one forward pass of the 3 relational layers over the whole graph, inputs
-resident in HBM.  value = edges aggregated per second = 3 · E · steps / time (an edge
-aggregated = one (node_1, rel, node_2) edge folded into its (node_1, rel) segment in one
-layer).  With --gpus N (torchrun, one process per GPU) the graph is sharded by
-aggregating-node (node_1) range, edge-balanced: each rank computes complete output rows for its
-range and one RCCL all-gather over xGMI per layer assembles the next layer's input
-(distributed.sharded_stack_forward, shard_side="rows"; measured per-rank compute at 8 shards
-1.91x below one GPU vs 1.51x for node_2 shards, scripts/shard_compute.py); the training epoch
-runs RGCNConv(shard=, group=, shard_side="rows") with the per-layer all-reduce of the disjoint
-rows and the gradient all-reduces. Total work is fixed: "scaling" is "strong".
+One timed STEP = one forward pass of the relational layers over the whole graph, inputs
+resident in HBM.  value = edges aggregated per second = Σ_layers E_layer · steps / time (an edge
+aggregated = one (node_1, rel, node_2) edge folded into its (node_1, rel) segment in one layer,
+SURVEY §8d; mode ALL: E per layer, mode SINGLE: the edges of that layer's relation).
 
-Also reported (separate loops, outside the timed step): the training epoch of
-main_rgcn.py:458-461 — train step (forward + NLL + backward + Adam) + validation forward.
+--gpus N (torch.distributed.run, one process per GPU): the C4 line — the graph sharded by
+GATHERED-node (node_2) range, edge-balanced (the north-star partition): every rank
+computes partial sums for all rows from its own edges (global per-segment counts), one RCCL
+reduce-scatter over xGMI per layer hands each rank the summed rows of its own range (the only
+rows its next layer gathers), one all-gather after the last layer; the training epoch all-reduces
+each layer's partial output and the gradients. ``--shard-side rows`` times the aggregating-node
+(node_1) partition instead (labelled). Total work is fixed: "scaling" is "strong".
 
-roofline: the dominant kernel (rel_gemm_kernel, forward) timed live with HIP events on its
-launch stream over a second pass of the same K steps (events between kernels drain the queue,
-so they are kept out of the headline's timed region); algorithmic FLOPs = 2·(S + N)·F_in·F_out per launch
-(segment rows H @ W_r plus node rows x @ root, both computed by that launch) against the
-dense fp32 MFMA peak (157.3 TFLOP/s); algorithmic bytes (A rows in, Y rows out, weights)
-reported beside it.  traffic: HBM bytes per launch from rocprofv3 PMC counters
-(profiles/pmc_seg_fwd.json when present, else null).
-cpu_baseline: the CPU oracle (PyG-2.3.1 loop semantics, same ATen ops) timed on this host.
+Also reported (separate loops, outside the timed step): the training epoch — train step
+(forward + NLL + backward + Adam) + validation forward (main_rgcn.py:458-461 / main.py:1121-1134).
+
+roofline: the kernel with the largest share of the forward layer (per-kernel HIP-event pass on
+the launch stream; rocprofv3 summary in profiles/), against its own bound — the transform GEMM
+(rel_gemm_kernel, fp32 MFMA, 2·(S+N)·F_in·F_out FLOPs per launch) or the gathers (segment means /
+combine, HBM 8 TB/s, SURVEY §8d bytes). Every forward kernel kind is listed in roofline_kernels.
+traffic: HBM bytes per launch from the rocprofv3 PMC passes committed under profiles/ (FETCH_SIZE
+×2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), or null when no pass matches the workload.
+cpu_baseline: the CPU oracle (PyG-2.3.1 loop semantics, same ATen ops) on this host.
 """
 from __future__ import annotations
 
@@ -50,39 +53,46 @@ METRIC = "edges aggregated/sec + epoch time, FB15K-237 128-d at 1/2/4/8 MI355X"
 PEAK_FP32_MFMA = 157.3  # TFLOP/s dense (MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32)
 PEAK_HBM = 8000.0       # GB/s spec
 
+WORKLOADS = {
+    "fb15k237": ("C3 FB15K-237 (N=14541, R=237, E=310116, SURVEY 8d recipe)",
+                 "synthetic: FB15K-237-shaped graph, SURVEY 8d C3 recipe (relation ~ dev+test histogram, node_1/"
+                 "node_2 ~ dev+test entity frequency add-one smoothed over 14,541 entities), U[0,1) features, "
+                 "seed-10 random-init weights"),
+    "fb15k237_relcond": ("C3' FB15K-237 relation-conditional graph (round-1 headline, S ~ 48k)",
+                         "synthetic: 38,000 real dev+test triples + relation-conditional samples to E=310,116, "
+                         "U[0,1) features, seed-10 random-init weights"),
+    "C2": ("C2 synthetic (N=100000, R=16, out-degree U{1..32})",
+           "synthetic: seeded generator of create_graph (SURVEY 8d C2), U[0,1) features, seed-10 weights"),
+    "C5": ("C5 synthetic (N=2000000, R=64, out-degree U{1..31})",
+           "synthetic: seeded generator of create_graph (SURVEY 8d C5), U[0,1) features, seed-10 weights"),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="fb15k237", choices=["fb15k237", "C2", "C5"],
-                    help="fb15k237 = C3/C4 (the headline); C2 / C5 = the other BASELINE.json configs")
-    ap.add_argument("--recipe", default="survey", choices=["survey", "relcond"],
-                    help="FB15K-237 edge recipe: survey = SURVEY §8d C3 (S ~ 208k, the headline); "
-                         "relcond = round-1 relation-conditional graph (S ~ 48k, lighter)")
-    ap.add_argument("--layers", type=int, default=None, help="default 3 (C3, C5) / 2 (C2)")
+    ap.add_argument("--workload", default="fb15k237", choices=list(WORKLOADS))
+    ap.add_argument("--mode", default="all", choices=["all", "single"],
+                    help="all = RGCN Net (mode B, main_rgcn.py); single = MPNetm metapath chain (mode A, main.py)")
+    ap.add_argument("--metapath", default=None,
+                    help="mode single: comma-separated relations, one per layer (default C2 '1,0', C5 '2,1,0', "
+                         "FB15K the three most frequent relations)")
+    ap.add_argument("--shard-side", default="gathered", choices=["gathered", "rows"],
+                    help="--gpus N > 1: gathered = node_2 ranges + reduce-scatter (north star, C4); rows = node_1")
+    ap.add_argument("--layers", type=int, default=None, help="mode all: default 3 (C3, C5) / 2 (C2)")
     ap.add_argument("--feat", type=int, default=None, help="default 128 (C2, C3) / 256 (C5)")
-    ap.add_argument("--epoch-steps", type=int, default=None, help="0 skips the epoch leg (default 10; 2 at C5)")
+    ap.add_argument("--epoch-steps", type=int, default=None, help="0 skips the epoch leg (default 30; 10 C2; 2 C5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-reps", type=int, default=2)
+    ap.add_argument("--cpu-reps", type=int, default=5, help="timed CPU repetitions (median), after 2 warm-ups")
     a = ap.parse_args()
-    dflt = {"fb15k237": (3, 128, 30), "C2": (2, 128, 10), "C5": (3, 256, 2)}[a.workload]
+    base = "C3" if a.workload.startswith("fb15k237") else a.workload
+    dflt = {"C3": (3, 128, 30), "C2": (2, 128, 10), "C5": (3, 256, 2)}[base]
     a.layers = dflt[0] if a.layers is None else a.layers
     a.feat = dflt[1] if a.feat is None else a.feat
     a.epoch_steps = dflt[2] if a.epoch_steps is None else a.epoch_steps
     return a
-
-
-WORKLOADS = {
-    "fb15k237": ("C3 FB15K-237 (N=14541, R=237, E=310116)",
-                 "synthetic: FB15K-237-shaped graph (38,000 real dev+test triples + relation-conditional "
-                 "samples to E=310,116), U[0,1) features, seed-10 random-init weights"),
-    "C2": ("C2 synthetic (N=100000, R=16, out-degree U{1..32})",
-           "synthetic: seeded generator of create_graph (SURVEY §8d C2), U[0,1) features, seed-10 weights"),
-    "C5": ("C5 synthetic (N=2000000, R=64, out-degree U{1..31})",
-           "synthetic: seeded generator of create_graph (SURVEY §8d C5), U[0,1) features, seed-10 weights"),
-}
 
 
 def setup_dist(n):
@@ -107,19 +117,64 @@ def setup_dist(n):
     return rank, world, local, group
 
 
-def cpu_baseline_sampled(g, net_cpu, layers, reps):
-    """C2 / C5: the full CPU stack would take minutes to hours (R dense N×F×F GEMMs per layer),
-    so the oracle's loop body is timed for ONE relation of the first layer (index_select,
+def host_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model, "torch_threads": torch.get_num_threads()}
+
+
+def _median(xs):
+    xs = sorted(xs)
+    return xs[len(xs) // 2]
+
+
+def cpu_baseline_full(g, params, layers, reps):
+    """Oracle (CPU, the host threads torch uses) on the same graph: 2 warm-ups, `reps` timed
+    forwards of the mode-ALL stack; edges/s = layers·E / median time."""
+    from oracle import rgcn_oracle as orc
+    x, ei, et = g.x, g.edge_index, g.edge_type
+
+    def fwd():
+        h = x
+        for layer in range(layers):
+            p = "conv1." if layer == 0 else "conv2."
+            h = torch.relu(orc.rgcn_forward(h, ei, et, params[p + "weight"], params[p + "root"], params[p + "bias"]))
+        return h
+
+    with torch.no_grad():
+        for _ in range(2):
+            fwd()
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fwd()
+            times.append(time.perf_counter() - t0)
+    med = _median(times)
+    return {"value": layers * g.num_edges / med, "unit": "edges/s", "cores": torch.get_num_threads(), "kind": "port",
+            **host_info(),
+            "sample": f"{reps} timed (after 2 warm-up) forward passes of the {layers}-layer RGCN stack on the full "
+                      f"graph (oracle/rgcn_oracle.py, PyG-2.3.1 loop: index_select/scatter_add_/div/mm per relation); "
+                      f"median {med * 1e3:.1f} ms"}
+
+
+def cpu_baseline_rel0(g, params, layers, reps):
+    """C2 / C5 mode ALL: the full CPU stack would take minutes to hours (R dense N×F×F GEMMs per
+    layer), so the oracle's loop body is timed for ONE relation of the first layer (index_select,
     scatter_add_, div, mm — rgcn_oracle.rgcn_forward's iteration) and scaled by R·layers, plus
     the root GEMM per layer; labelled as extrapolated."""
     from oracle import rgcn_oracle as orc
-    w = net_cpu.conv1.weight.detach()
-    root = net_cpu.conv1.root.detach()
+    w, root = params["conv1.weight"], params["conv1.root"]
     x, ei, et = g.x, g.edge_index, g.edge_type
     size = (x.size(0), x.size(0))
     with torch.no_grad():
         times = []
-        for _ in range(reps + 1):
+        for k in range(reps + 2):
             t0 = time.perf_counter()
             tmp = orc.masked_edge_index(ei, et == 0)
             h = orc.propagate_mean(tmp, x, size)
@@ -128,86 +183,132 @@ def cpu_baseline_sampled(g, net_cpu, layers, reps):
             t0 = time.perf_counter()
             _ = x @ root
             t_root = time.perf_counter() - t0
-            times.append((t_rel, t_root))
-    times = sorted(times[1:])
-    t_rel, t_root = times[len(times) // 2]
+            if k >= 2:
+                times.append((t_rel, t_root))
+    t_rel, t_root = _median(times)
     est = layers * (g.num_relations * t_rel + t_root)
-    return {"value": layers * g.num_edges / est, "unit": "edges/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"oracle loop body for relation 0 of layer 1 ({reps} timed + 1 warm-up, median "
+    return {"value": layers * g.num_edges / est, "unit": "edges/s", "cores": torch.get_num_threads(), "kind": "port",
+            **host_info(),
+            "sample": f"oracle loop body for relation 0 of layer 1 ({reps} timed after 2 warm-up, median "
                       f"{t_rel * 1e3:.1f} ms) + root GEMM ({t_root * 1e3:.1f} ms), extrapolated x{g.num_relations} "
                       f"relations x{layers} layers = {est:.1f} s per forward (extrapolated, not run in full)"}
 
 
-def cpu_baseline(g, net_cpu, layers, reps):
-    """Oracle (CPU, all host threads torch uses) on the same graph: `reps` timed forwards of
-    the relational stack after one warm-up; edges/s = layers·E / median time."""
+def cpu_baseline_single(g, convs_cpu, metapath, edges, reps):
+    """Mode SINGLE: the oracle CustomRGCNConv chain (mp_rgcn_layer.py:225-271: masked_edge_index,
+    propagate mean, h @ W, x @ root, bias, ReLU) over the metapath, full graph."""
     from oracle import rgcn_oracle as orc
-    params = {k: v.detach() for k, v in net_cpu.state_dict().items()}
     x, ei, et = g.x, g.edge_index, g.edge_type
 
     def fwd():
         h = x
-        for layer in range(layers):
-            p = "conv1." if layer == 0 else "conv2."
-            h = torch.relu(orc.rgcn_forward(h, ei, et, params[p + "weight"], params[p + "root"],
-                                            params[p + "bias"]))
+        for conv, rel in zip(convs_cpu, metapath):
+            h = torch.relu(orc.custom_rgcn_forward(h, ei, et, rel, conv.weight.detach(), conv.root.detach(),
+                                                   conv.bias.detach()))
         return h
 
     with torch.no_grad():
-        fwd()
+        for _ in range(2):
+            fwd()
         times = []
         for _ in range(reps):
             t0 = time.perf_counter()
             fwd()
             times.append(time.perf_counter() - t0)
-    times.sort()
-    med = times[len(times) // 2]
-    return {"value": layers * g.num_edges / med, "unit": "edges/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"{reps} timed + 1 warm-up forward passes of the {layers}-layer RGCN stack on the full "
-                      f"FB15K-shaped graph (oracle/rgcn_oracle.py, PyG-2.3.1 loop: index_select/scatter_add_/"
-                      f"div/mm per relation); median {med * 1e3:.1f} ms"}
+    med = _median(times)
+    return {"value": edges / med, "unit": "edges/s", "cores": torch.get_num_threads(), "kind": "port", **host_info(),
+            "sample": f"{reps} timed (after 2 warm-up) forward passes of the {len(metapath)}-hop CustomRGCNConv chain "
+                      f"(oracle/rgcn_oracle.py custom_rgcn_forward) on the full graph; median {med * 1e3:.1f} ms"}
+
+
+def pmc_traffic(workload, mode, feat, kernel_prefix):
+    """HBM bytes per launch of `kernel_prefix` from the committed PMC summary, or None."""
+    path = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+    try:
+        rows = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    for r in rows:
+        if r.get("workload") == workload and r.get("mode") == mode and r.get("feat") == feat and \
+                r.get("kernel", "").startswith(kernel_prefix):
+            return r.get("hbm_bytes_per_launch")
+    return None
 
 
 def main():
     args = parse()
     rank, world, local, group = setup_dist(args.gpus)
     dev = torch.device("cuda", local)
-    if args.workload == "fb15k237":
-        g = data.fb15k237_graph(feat_dim=args.feat, seed=0, recipe=args.recipe)
+    if args.workload.startswith("fb15k237"):
+        g = data.fb15k237_graph(feat_dim=args.feat, seed=0,
+                                recipe="relcond" if args.workload == "fb15k237_relcond" else "survey")
     else:
         g = data.config_graph(args.workload)
         if g.x.shape[1] != args.feat:
             g.x = torch.rand((g.num_nodes, args.feat), generator=torch.Generator().manual_seed(1))
     F = args.feat
-    torch.manual_seed(10)  # main_rgcn.py:31
-    net_cpu = mpgnn_amd.Net(F, F, g.num_relations, F, 2, args.layers)
-    net = mpgnn_amd.Net(F, F, g.num_relations, F, 2, args.layers)
-    net.load_state_dict(net_cpu.state_dict())
-    net = net.to(dev)
     x, ei, et = g.x.to(dev), g.edge_index.to(dev), g.edge_type.to(dev)
-    shard = None
-    ranges = None
-    if world > 1:  # shard by the aggregating node: complete rows per rank (scripts/shard_compute.py)
-        ranges = shard_ranges(g.edge_index, g.num_nodes, world, side="rows")
+    single = args.mode == "single"
+    shard = ranges = None
+    side = args.shard_side
+    if world > 1:
+        ranges = shard_ranges(g.edge_index, g.num_nodes, world, side=side)
         shard = ranges[rank]
-    convs = [net.conv1] + [net.conv2] * (args.layers - 1)
+    torch.manual_seed(10)  # main_rgcn.py:31 / main.py:31-style seeding of the init
+    rel_counts = torch.bincount(g.edge_type, minlength=g.num_relations)
+    if single:
+        if args.metapath:
+            metapath = [int(v) for v in args.metapath.split(",")]
+        elif args.workload == "C2":
+            metapath = [1, 0]
+        elif args.workload == "C5":
+            metapath = [2, 1, 0]
+        else:
+            metapath = [int(v) for v in torch.argsort(rel_counts, descending=True, stable=True)[:3]]
+        model_cpu = mpgnn_amd.MPNetm(F, F, g.num_relations, F, 2, 1, [metapath])
+        model = mpgnn_amd.MPNetm(F, F, g.num_relations, F, 2, 1, [metapath])
+        model.load_state_dict(model_cpu.state_dict())
+        model = model.to(dev).eval()
+        convs = list(model.layers_list[0])
+        edges_per_step = int(sum(int(rel_counts[r]) for r in metapath))
+        if world > 1:
+            raise SystemExit("--mode single shards nothing (MPGNN candidates are replicas: distributed.metapath_fanout)")
 
-    def step():
-        if world > 1:  # each rank's complete rows all-gathered per layer
-            return sharded_stack_forward(convs, x, ei, et, ranges, group, shard_side="rows")
-        h = x
-        for conv in convs:
-            h = conv(h, ei, et, activation="relu")  # F.relu(conv(...)), model.py:144,146
-        return h
+        def step():
+            h = x
+            for li, (conv, rel) in enumerate(zip(convs, metapath)):
+                h = conv(li, rel, h, ei, et, activation="relu")  # F.relu(conv(...)), model.py:211,214
+            return h
+        layers = len(metapath)
+    else:
+        model_cpu = mpgnn_amd.Net(F, F, g.num_relations, F, 2, args.layers)
+        model = mpgnn_amd.Net(F, F, g.num_relations, F, 2, args.layers)
+        model.load_state_dict(model_cpu.state_dict())
+        model = model.to(dev)
+        convs = [model.conv1] + [model.conv2] * (args.layers - 1)
+        edges_per_step = args.layers * g.num_edges
+        layers = args.layers
+
+        def step():
+            if world > 1:  # partial sums per rank, reduce-scatter per layer (or all-gather of rows)
+                return sharded_stack_forward(convs, x, ei, et, ranges, group, shard_side=side)
+            h = x
+            for conv in convs:
+                h = conv(h, ei, et, activation="relu")  # F.relu(conv(...)), model.py:144,146
+            return h
 
     # plan (built once per graph, cached) + warm-up
+    t_plan = time.perf_counter()
+    with torch.no_grad():
+        step()
+    torch.cuda.synchronize()
+    first_step_s = time.perf_counter() - t_plan
     with torch.no_grad():
         for _ in range(max(args.warmup, 1)):
             step()
     torch.cuda.synchronize()
-    plan = mpgnn_amd.get_plan(ei, et, g.num_nodes, shard=shard, device=dev, shard_side="rows")
+    plan = mpgnn_amd.get_plan(ei, et, g.num_nodes, shard=shard, device=dev,
+                              shard_side=side if shard is not None else "gathered")
 
     # ---- timed region: K forward steps --------------------------------------------------
     if group is not None:
@@ -222,24 +323,8 @@ def main():
         dist.barrier(group=group)
     elapsed = time.perf_counter() - t0
 
-    # ---- roofline pass: the same K steps again with the dominant kernel bracketed by HIP
-    # events on its launch stream (C-ABI timing hook).  Kept out of the timed region: an event
-    # between two kernels drains the queue (~4 us per event pair on this stack), which would
-    # charge the headline number for the measurement itself.
-    _lib.lib.mpgnn_timing_reset()
-    _lib.lib.mpgnn_set_option(3, 1 << _lib.KERNEL_KINDS["seg_fwd"])  # time only the roofline kernel
-    _lib.lib.mpgnn_timing_enable(1)
-    with torch.no_grad():
-        for _ in range(args.steps):
-            step()
-    torch.cuda.synchronize()
-    _lib.lib.mpgnn_timing_enable(0)
-    _lib.lib.mpgnn_set_option(3, -1)
-    seg_ms, seg_n = _lib.kernel_timing("seg_fwd")
-    row_ms, row_n = _lib.kernel_timing("row_fwd")
-
-    # ---- per-kernel breakdown: a third pass with every kernel kind timed (events between all
-    # kernels make each launch slightly longer than in the headline pass; attribution only)
+    # ---- per-kernel pass: every kernel kind bracketed by HIP events on its launch stream (kept
+    # out of the timed region: an event pair between kernels drains the queue)
     _lib.lib.mpgnn_timing_reset()
     _lib.lib.mpgnn_timing_enable(1)
     with torch.no_grad():
@@ -247,29 +332,83 @@ def main():
             step()
     torch.cuda.synchronize()
     _lib.lib.mpgnn_timing_enable(0)
+    kinds = {"mean": "segment means (flat_rows_kernel over the multi-edge segments)",
+             "seg_fwd": "transform GEMM (rel_gemm_kernel)",
+             "row_fwd": "combine / output (flat_rows_kernel or gather_rows_kernel)",
+             "final": "split-row finalize", "piece": "ordered pieces"}
     per_layer = {}
-    for kind, label in (("mean", "segment means: flat_rows_kernel + split-row finalize"), ("final", "split-row finalize alone"),
-                        ("seg_fwd", "transform GEMM"), ("row_fwd", "combine (flat_rows_kernel)")):
+    for kind, label in kinds.items():
         k_ms, k_n = _lib.kernel_timing(kind)
         if k_n:
-            per_layer[kind] = {"what": label, "us_per_layer": round(k_ms * 1e3 / (args.steps * args.layers), 2)}
+            per_layer[kind] = {"what": label, "us_per_layer": round(k_ms * 1e3 / (args.steps * layers), 2),
+                               "launches_per_layer": round(k_n / (args.steps * layers), 2)}
     if group is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
-    edges_per_step = args.layers * g.num_edges
     value = edges_per_step * args.steps / elapsed
-    # SURVEY §8d layer roofline: algorithmic bytes per forward layer
-    # B = E·(4·F_in + 4) + S·8 + N·4·F_out (gathered rows + their column ids, segment ptr/rel,
-    # output write); at 8 TB/s that bounds edges/s at E / (B / 8e12)
-    b_layer = g.num_edges * (4 * F + 4) + plan.num_segments * 8 + g.num_nodes * 4 * F
-    ideal = g.num_edges / (b_layer / (PEAK_HBM * 1e9))
-    hbm_roofline = {"bound": "hbm", "alg_bytes_per_layer": b_layer,
-                    "achieved_GBps": round(value / g.num_edges * b_layer / 1e9, 1), "peak_GBps": PEAK_HBM,
-                    "ideal_edges_per_s": round(ideal, 1), "frac": round(value / ideal, 4),
-                    "note": "whole-step edges/s against the aggregation's HBM roofline of SURVEY §8d (516 B per "
-                            "edge at F=128); at C3 x (7.4 MB) stays in L2/MALL, so the layer is bound on-die"}
+
+    # ---- rooflines per forward kernel kind (per layer, this rank; first layer's selection) ----
+    mode_id = _lib.MODE_SINGLE if single else _lib.MODE_ALL
+    sel_rel = metapath[0] if single else -1
+    seg_b, seg_e = plan.select(mode_id, sel_rel, g.num_relations)
+    S = seg_e - seg_b
+    Sm = plan.hsave_rows(mode_id, sel_rel, g.num_relations)
+    m_ptr = plan.table("m_ptr")
+    rel_m = plan.table("rel_m_ptr")
+    d_lo = int(torch.searchsorted(torch.from_numpy(plan.table("rel_seg_ptr")).to(torch.int64), seg_b).item())
+    m_lo = int(rel_m[d_lo]) if len(rel_m) else 0
+    Em = int(m_ptr[m_lo + Sm] - m_ptr[m_lo]) if Sm else 0
+    n_rows = plan.num_nodes if world == 1 else (shard[1] - shard[0])
+    E_layer = (edges_per_step // layers) if not single else int(rel_counts[metapath[0]])
+    model_costs = {
+        "seg_fwd": ("mfma", 2.0 * (S + n_rows) * F * F, "2·(S + N)·F_in·F_out: segment rows (mean @ W_r) + node rows "
+                    "(x @ root)"),
+        "mean": ("hbm", Em * (4.0 * F + 4) + Sm * (4.0 * F + 8), "Em·(4F + 4) gathered x rows + col ids of the "
+                 "multi-edge segments, Sm·(4F + 8) mean rows written + counts / pointers"),
+        "row_fwd": ("hbm", (S + n_rows) * (4.0 * F + 4) + n_rows * 4.0 * F, "(S + N)·(4F + 4) Y / Y_root rows + ids "
+                    "gathered, N·4F output rows written"),
+    }
+    rooflines = []
+    for kind, (bound, work, model_txt) in model_costs.items():
+        if kind not in per_layer:
+            continue
+        us = per_layer[kind]["us_per_layer"]
+        if bound == "mfma":
+            ach = work / (us * 1e-6) / 1e12
+            peak, unit = PEAK_FP32_MFMA, "TFLOP/s"
+        else:
+            ach = work / (us * 1e-6) / 1e9
+            peak, unit = PEAK_HBM, "GB/s"
+        kname = {"seg_fwd": "rel_gemm_kernel", "mean": "flat_rows_kernel", "row_fwd": "flat_rows_kernel"}[kind]
+        rooflines.append({"kind": kind, "kernel": kname, "bound": bound, "achieved": round(ach, 2), "peak": peak,
+                          "unit": unit, "frac": round(ach / peak, 4), "us_per_layer": us,
+                          "share_of_layer": None, "algorithmic": model_txt,
+                          ("alg_flops_per_launch" if bound == "mfma" else "alg_bytes_per_launch"): work})
+    total_us = sum(v["us_per_layer"] for v in per_layer.values())
+    for r in rooflines:
+        r["share_of_layer"] = round(r["us_per_layer"] / total_us, 3) if total_us else None
+    dom = max(rooflines, key=lambda r: r["us_per_layer"]) if rooflines else None
+    roofline = None
+    if dom is not None:
+        mode_tag = "single" if single else "all"
+        traffic = pmc_traffic(args.workload, mode_tag, F, "mpgnn::" + dom["kernel"]) if world == 1 else None
+        roofline = {"bound": dom["bound"], "achieved": dom["achieved"], "peak": dom["peak"], "unit": dom["unit"],
+                    "frac": dom["frac"], "traffic": traffic, "kernel": dom["kernel"], "kind": dom["kind"],
+                    "avg_launch_us": dom["us_per_layer"], "share_of_layer": dom["share_of_layer"],
+                    "algorithmic": dom["algorithmic"],
+                    "note": "dominant kernel of the forward layer by the per-kernel HIP-event pass (events on the "
+                            "launch stream, one pair per launch; the headline timed region has none); traffic = "
+                            "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/r02_pmc_traffic.json)"}
+        # SURVEY 8d whole-step HBM roofline of the aggregation (kept beside the kernel roofline)
+    b_edge = 4 * F + 4
+    hbm_roofline = {"bound": "hbm", "bytes_per_edge": b_edge,
+                    "alg_bytes_per_step": edges_per_step * b_edge + layers * (S * 8 + g.num_nodes * 4 * F),
+                    "note": f"SURVEY 8d: B = E_l·(4·F + 4) + S_l·8 + N·4·F per layer ({b_edge} B per edge at F={F}); "
+                            "at C3 x stays in L2/MALL, so the gathers are bound on-die, not by HBM"}
+    hbm_roofline["achieved_GBps"] = round(hbm_roofline["alg_bytes_per_step"] / (ms_per_step * 1e-3) / 1e9, 1)
+    hbm_roofline["frac"] = round(hbm_roofline["achieved_GBps"] / PEAK_HBM, 4)
 
     # ---- the same step replayed as one HIP graph (launch overhead removed) ---------------
     graph = None
@@ -295,34 +434,39 @@ def main():
             g_el = time.perf_counter() - tg
             graph = {"value": round(edges_per_step * args.steps / g_el, 1),
                      "ms_per_step": round(g_el * 1e3 / args.steps, 4),
-                     "note": "same 3-layer forward captured once with torch.cuda.graph (hipGraph) and "
-                             "replayed: every kernel runs every step, host launch overhead removed"}
+                     "note": "same forward captured once with torch.cuda.graph (hipGraph) and replayed: every "
+                             "kernel runs every step, host launch overhead removed"}
         except Exception as e:  # capture unsupported here: report, keep the eager number
             graph = {"error": f"{type(e).__name__}: {e}"[:200]}
-        cg = None  # free the graph's private pool and the capture stream's workspace
+        cg = None
         mpgnn_amd.functional.release_workspaces()
         torch.cuda.empty_cache()
 
-    # ---- epoch (main_rgcn.py:458-461): train fwd+bwd+Adam + validation forward ------------
-    opt = mpgnn_amd.main._adam(net)  # Adam(lr 0.01, wd 5e-4), fused multi-tensor kernel on the GPU
+    # ---- epoch: train fwd + NLL + bwd + Adam, then a validation forward --------------------
+    opt = mpgnn_amd.main._adam(model)  # Adam(lr 0.01, wd 5e-4), fused multi-tensor kernel on the GPU
     y = torch.randint(0, 2, (g.num_nodes,), generator=torch.Generator().manual_seed(0)).to(dev)
     train_idx = torch.arange(0, g.num_nodes, 3, device=dev)
-    train_y = y[train_idx]  # data.train_y of the reference loop: fixed labels, indexed once
+    train_y = y[train_idx]  # data.train_y of the reference loops: labels indexed once
+
+    def fwd_model():
+        if single:
+            return model(x, ei, et)
+        return model(x, ei, et, shard=shard, group=group, shard_side=side)
 
     def epoch():
-        net.train()
+        model.train()
         opt.zero_grad()
-        out = net(x, ei, et, shard=shard, group=group, shard_side="rows")
+        out = fwd_model()
         loss = torch.nn.functional.nll_loss(out.index_select(0, train_idx), train_y)
         loss.backward()
         opt.step()
-        net.eval()
+        model.eval()
         with torch.no_grad():
-            net(x, ei, et, shard=shard, group=group, shard_side="rows")
+            fwd_model()
 
     epoch_ms = None
     if args.epoch_steps > 0:
-        for _ in range(5):
+        for _ in range(3):
             epoch()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
@@ -330,15 +474,21 @@ def main():
             epoch()
         torch.cuda.synchronize()
         epoch_ms = (time.perf_counter() - t1) * 1e3 / args.epoch_steps
+        if group is not None:
+            t = torch.tensor([epoch_ms], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            epoch_ms = float(t.item())
+    model.eval()
 
     # ---- the same epoch captured once as a HIP graph (host issue removed) -------------------
-    # torch's whole-network capture recipe: warm-up on a side stream, grads allocated inside
-    # the capture, Adam(fused, capturable); replay = train fwd + NLL + bwd + Adam + val fwd.
     epoch_graph = None
     if args.epoch_steps > 0 and world == 1:
         try:
-            netg = mpgnn_amd.Net(F, F, g.num_relations, F, 2, args.layers).to(dev)
-            netg.load_state_dict(net.state_dict())
+            if single:
+                netg = mpgnn_amd.MPNetm(F, F, g.num_relations, F, 2, 1, [metapath]).to(dev)
+            else:
+                netg = mpgnn_amd.Net(F, F, g.num_relations, F, 2, args.layers).to(dev)
+            netg.load_state_dict(model.state_dict())
             optg = torch.optim.Adam(netg.parameters(), lr=0.01, weight_decay=0.0005, fused=True, capturable=True)
 
             def epoch_g():
@@ -381,70 +531,51 @@ def main():
         except Exception as e:  # capture unsupported: report, keep the eager number
             epoch_graph = {"error": f"{type(e).__name__}: {e}"[:200]}
 
-    # ---- roofline of the dominant kernel (per launch, this rank) --------------------------
-    S = plan.num_segments
-    E_loc = plan.num_edges
-    # the layer's transform may be split over several launches (root rows + relation groups,
-    # MPGNN_OPT_OVERLAP): the roofline is per LAYER = the summed durations of its launches
-    layer_calls = args.steps * args.layers
-    seg_avg_ms = seg_ms / max(layer_calls, 1)
-    n_root = plan.num_nodes if world == 1 else (shard[1] - shard[0])
-    flops = 2.0 * (S + n_root) * F * F   # Y = H @ W_r over S segment rows + Y_root = x @ root
-    alg_bytes = 4 * F * (2 * S + 2 * n_root) + 4 * F * F * (plan.num_relations_present + 1)  # A rows in, Y out, W
-    achieved_tf = flops / (seg_avg_ms * 1e-3) / 1e12 if seg_n else None
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_seg_fwd.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("workload") == args.workload and pmc.get("feat") == F and world == 1 and \
-                    pmc.get("kernel", "").startswith("mpgnn::rel_gemm_kernel"):
-                traffic = pmc.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    roofline = {
-        "bound": "mfma", "achieved": round(achieved_tf, 3) if achieved_tf else None, "peak": PEAK_FP32_MFMA,
-        "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_MFMA, 4) if achieved_tf else None,
-        "traffic": traffic,
-        "kernel": ("rel_gemm_kernel (Y = H @ W_r, Y_root = x @ root; W_r slice held in registers; "
-                   "v_mfma_f32_32x32x2_f32)") if F in (64, 128) else
-                  "tile_gemm_kernel (Y = H @ W_r, Y_root = x @ root; persistent LDS-tiled; v_mfma_f32_32x32x2_f32)",
-        "avg_launch_us": round(seg_avg_ms * 1e3, 2), "launches": seg_n,
-        "launches_per_layer": round(seg_n / max(layer_calls, 1), 2),
-        "note": "avg_launch_us = summed duration of one layer's transform launches (root rows + relation "
-                "groups; they run on a second stream beside the segment means, so contention is included)",
-        "alg_flops_per_launch": flops, "alg_bytes_per_launch": alg_bytes,
-        "alg_GBps": round(alg_bytes / (seg_avg_ms * 1e-3) / 1e9, 1) if seg_n else None,
-        "hbm_frac_if_streamed": round(alg_bytes / (seg_avg_ms * 1e-3) / 1e9 / PEAK_HBM, 4) if seg_n else None,
-        "row_kernel_avg_us": round(row_ms / max(row_n, 1) * 1e3, 2),
-    }
-
     result = None
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            if args.workload == "fb15k237":
-                cpu = cpu_baseline(g, net_cpu, args.layers, args.cpu_reps)
+            if single:
+                convs_cpu = list(model_cpu.layers_list[0])
+                cpu = cpu_baseline_single(g, convs_cpu, metapath, edges_per_step, args.cpu_reps)
             else:
-                cpu = cpu_baseline_sampled(g, net_cpu, args.layers, args.cpu_reps)
+                params = {k: v.detach() for k, v in model_cpu.state_dict().items()}
+                if args.workload.startswith("fb15k237"):
+                    cpu = cpu_baseline_full(g, params, args.layers, args.cpu_reps)
+                else:
+                    cpu = cpu_baseline_rel0(g, params, args.layers, args.cpu_reps)
+        if single:
+            what = (f"MPNetm metapath chain (mode A, CustomRGCNConv x{layers}), metapath={metapath}, "
+                    f"F_in=F_hidden={F}")
+        else:
+            what = f"RGCN Net stack forward (mode B), L={layers}, F_in=F_hidden=F_out={F}"
+        if world == 1:
+            par = "single GPU"
+        elif side == "gathered":
+            par = (f"node_2-range shards x{world} (gathered node, edge-balanced; SURVEY 8e): partial sums per rank, "
+                   "one RCCL reduce-scatter per layer + one all-gather (epoch: per-layer all-reduce of the partial "
+                   "output, gradient all-reduces)")
+        else:
+            par = (f"node_1-range shards x{world} (aggregating node, edge-balanced): complete rows per rank, one "
+                   "RCCL all-gather per layer")
         result = {
             "metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": WORKLOADS[args.workload][1],
-            "config": {"workload": WORKLOADS[args.workload][0] + ": RGCN Net stack forward, "
-                                   f"L={args.layers}, F_in=F_hidden=F_out={F}",
+            "config": {"workload": WORKLOADS[args.workload][0] + ": " + what, "mode": args.mode,
                        "graph": {"nodes": g.num_nodes, "relations": g.num_relations, "edges": g.num_edges,
-                                 "segments": S if world == 1 else None},
-                       "parallelism": "single GPU" if world == 1 else
-                       f"row-range shards x{world} (aggregating node, edge-balanced): each rank computes its "
-                       "complete output rows, one RCCL all-gather per layer (epoch: per-layer all-reduce of the "
-                       "disjoint rows, gradient all-reduces)"},
+                                 "edges_per_step": edges_per_step, "segments_layer1": S,
+                                 "multi_edge_segments_layer1": Sm},
+                       "parallelism": par, "shard_side": side if world > 1 else None},
             "graph_replay": graph,
             "epoch_ms": round(epoch_ms, 3) if epoch_ms is not None else None,
             "epoch_graph": epoch_graph,
-            "epoch_def": "main_rgcn.py:458-461 train (fwd+NLL+bwd+Adam) + validation forward",
+            "epoch_def": ("main.py:1121-1134 mpgnn_train + mpgnn_validation" if single else
+                          "main_rgcn.py:458-461 train (fwd+NLL+bwd+Adam) + validation forward"),
+            "first_step_s": round(first_step_s, 3),
             "roofline": roofline,
+            "roofline_kernels": rooflines,
             "hbm_roofline": hbm_roofline,
             "kernels_per_layer": per_layer,
             "cpu_baseline": cpu,

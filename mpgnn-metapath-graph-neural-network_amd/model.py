@@ -136,11 +136,12 @@ class MPNetm(torch.nn.Module):
             for layer_index in range(0, len(self.metapaths[i])):
                 conv = self.layers_list[i][layer_index]
                 rel = self.metapaths[i][layer_index]
+                # F.relu(conv(...)) of model.py:211,214, fused into the layer's output kernel
                 if layer_index == 0:
-                    h = F.relu(conv(layer_index, rel, x, edge_index, edge_type))
+                    h = conv(layer_index, rel, x, edge_index, edge_type, activation="relu")
                     h = self.dropout(h)
                 else:
-                    h = F.relu(conv(layer_index, rel, h, edge_index, edge_type))
+                    h = conv(layer_index, rel, h, edge_index, edge_type, activation="relu")
                     h = self.dropout2(h)
             embeddings.append(h)
         concatenated_embedding = torch.cat(embeddings, dim=1)

@@ -115,8 +115,10 @@ class CustomRGCNConv(torch.nn.Module):
         glorot(self.root)
         zeros(self.bias)
 
-    def forward(self, layer_num, relation, x, edge_index, edge_type=None):
-        """mp_rgcn_layer.py:158 — ``layer_num`` is accepted and unused, as in the reference."""
+    def forward(self, layer_num, relation, x, edge_index, edge_type=None, *, activation=None):
+        """mp_rgcn_layer.py:158 — ``layer_num`` is accepted and unused, as in the reference.
+        ``activation='relu'`` returns ``F.relu(layer(...))`` (MPNetm, model.py:211,214) with the
+        ReLU fused into the layer's output kernel."""
         if isinstance(x, tuple):
             raise NotImplementedError("bipartite (x_l, x_r) input is not supported")
         if x is None or x.dtype == torch.long:
@@ -131,7 +133,8 @@ class CustomRGCNConv(torch.nn.Module):
         if isinstance(relation, Tensor):
             relation = int(relation.item())
         plan = get_plan(edge_index, edge_type, x.size(0), flow=self.flow, device=x.device)
-        out = rgcn_conv(x, self.weight, self.root, self.bias, plan, MODE_SINGLE, relation=int(relation))
+        out = rgcn_conv(x, self.weight, self.root, self.bias, plan, MODE_SINGLE, relation=int(relation),
+                        activation=activation)
         return _squeeze_like_reference(out, self.root is not None)
 
     def __repr__(self) -> str:
