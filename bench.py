@@ -422,7 +422,7 @@ def main():
             torch.cuda.current_stream().wait_stream(s_cap)
             torch.cuda.synchronize()
             cg = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(cg), torch.no_grad():
+            with torch.cuda.graph(cg, stream=s_cap), torch.no_grad():  # the warmed-up stream's workspace
                 step()
             for _ in range(3):
                 cg.replay()
@@ -512,7 +512,7 @@ def main():
             torch.cuda.synchronize()
             cg_e = torch.cuda.CUDAGraph()
             optg.zero_grad(set_to_none=True)
-            with torch.cuda.graph(cg_e):
+            with torch.cuda.graph(cg_e, stream=s_cap):
                 static_loss = epoch_g()
             for _ in range(3):
                 cg_e.replay()

@@ -1007,6 +1007,12 @@ struct RelGemmArgs {
     float* Y;             // rows s - sel_b
     float* Yroot;         // rows i - row_lo
     int sel_b, row_lo, row_hi;
+    // fused mode-SINGLE layer (CAT): node rows i read [x_i | mean_i] against [root; W] (K = 2·F_in);
+    // node_map[i] = 0 (no segment of the relation), s_src + 1 (x row), or s_src (< 0: Hm row)
+    const int* node_map;
+    int m_rows;           // CAT: rows of Hm (indices are clamped to the tables: a bad map cannot fault)
+    const float* bias;    // nullable, CAT epilogue
+    int relu;             // CAT epilogue: fused ReLU
 #ifdef MPGNN_STAMPS
     unsigned long long* stamps;
 #endif
@@ -1040,7 +1046,7 @@ __device__ __forceinline__ void stamp_id_at(unsigned long long* g_stamps) {
 #define stamp_id() ((void)0)
 #endif
 
-template <int KB, bool DGRAD, int NB = 1, int OCC = 2>
+template <int KB, bool DGRAD, int NB = 1, int OCC = 2, bool CAT = false>
 struct RelGemm {
     static constexpr int K = 64 * KB;
     static constexpr int KH = K / 2;
@@ -1113,6 +1119,12 @@ struct RelGemm {
 #pragma unroll
         for (int j = 0; j < WPT; ++j) row[j] = it.r0 + min((tid + j * kThreads) / W4, it.nrows - 1);
         cnt = 1;
+        if constexpr (CAT) {  // a thread's float4 column is fixed (256 % W4 == 0): x half or mean half
+            const bool mh = (tid % W4) >= W4 / 2;
+#pragma unroll
+            for (int j = 0; j < WPT; ++j) row[j] = mh ? a.node_map[row[j]] : row[j] + 1;
+            return;
+        }
         if (!it.root) {
             if constexpr (DGRAD) {
                 cnt = a.s_cnt[it.r0 + min(tid & 31, it.nrows - 1)];
@@ -1125,8 +1137,23 @@ struct RelGemm {
         }
     }
     __device__ static __forceinline__ void issue_rows(const RelGemmArgs& a, int tid, const int (&row)[WPT],
-                                                      float4 (&v)[WPT]) {
+                                                      float4 (&v)[WPT], int& zm) {
         constexpr int W4 = K / 4;
+        if constexpr (CAT) {  // rows of F = K/2 floats: x[v - 1] (v > 0), Hm[-v - 1 - m_lo] (v < 0), 0 (v == 0)
+            constexpr int F = K / 2;
+            const int c4 = ((tid % W4) % (W4 / 2)) * 4;
+            zm = 0;
+#pragma unroll
+            for (int j = 0; j < WPT; ++j) {
+                const int r = row[j];
+                const float* base = r >= 0 ? a.Aroot + (size_t)min(max(r - 1, 0), a.row_hi - 1) * F
+                                           : a.Arel + (size_t)min(max(-r - 1 - a.m_lo, 0), a.m_rows - 1) * F;
+                zm |= (r == 0 ? 1 : 0) << j;
+                v[j] = *reinterpret_cast<const float4*>(base + c4);
+            }
+            return;
+        }
+        zm = 0;
 #pragma unroll
         for (int j = 0; j < WPT; ++j) {
             const int c4 = ((tid + j * kThreads) % W4) * 4;
@@ -1141,18 +1168,26 @@ struct RelGemm {
     }
 
     __device__ static __forceinline__ void commit(const Item& it, int tid, const float4 (&v)[WPT], int cnt, float* A,
-                                                  float* sc) {
+                                                  float* sc, int zm = 0) {
         constexpr int W4 = K / 4;
 #pragma unroll
         for (int j = 0; j < WPT; ++j) {
             const int e = tid + j * kThreads;
             const int r = e / W4;
             *reinterpret_cast<float4*>(A + r * lda + (e % W4) * 4) =
-                r < it.nrows ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+                (r < it.nrows && !((zm >> j) & 1)) ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         // the dgrad row scale as a reciprocal (one IEEE division per row and item here, a multiply
         // per output in the epilogue instead of a 10-instruction division: ≤ 1.5 ulp apart)
         if (tid < 32) sc[tid] = 1.0f / (float)cnt;
+    }
+
+    // CAT: B = [root; W] — lane half 0 takes root's K/2 rows, half 1 W's
+    __device__ static __forceinline__ void load_b_cat(const RelGemmArgs& a, int wave, int lane, float (&b)[KH]) {
+        const int c = lane & 31, h = lane >> 5;
+        const float* p = (h ? a.W : a.Wroot) + col0() + wave * 32 + c;
+#pragma unroll
+        for (int j = 0; j < KH; ++j) b[j] = p[j * N];
     }
 
     // this wave's K × 32 weight slice: lane-half h holds k = h·KH + j, column 32·wave + c
@@ -1200,17 +1235,19 @@ struct RelGemm {
         const ItemTable tab = item_table(a, i_beg, i_end, lane);
         auto get_item = [&](int i) { return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i); };
         Item cur = get_item(i_beg);
+        int zm = 0;
         {
             int crow[WPT];
             gather_idx(a, cur, tid, crow, cnt);
-            issue_rows(a, tid, crow, v);
+            issue_rows(a, tid, crow, v, zm);
         }
         int nrow[WPT];
         int ncnt = 1;
         if (i_beg + 1 < i_end) gather_idx(a, get_item(i_beg + 1), tid, nrow, ncnt);
         float b[KH];
-        load_b(cur.w, wave, lane, b);
-        commit(cur, tid, v, cnt, As, Sc);
+        if constexpr (CAT) load_b_cat(a, wave, lane, b);
+        else load_b(cur.w, wave, lane, b);
+        commit(cur, tid, v, cnt, As, Sc, zm);
 #pragma unroll
         for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(b[j]));
         __syncthreads();
@@ -1218,7 +1255,10 @@ struct RelGemm {
         constexpr int NG = KH / 4;                 // MFMA groups (one A fragment each) per chain
         constexpr int SPG = (16 + NG - 1) / NG;    // previous item's stores per group
         constexpr int kCommitAt = (3 * NG) / 4;    // group after which the next tile is committed
-        constexpr bool kSplit = KB <= 2;           // two accumulation chains (accuracy)
+        constexpr bool kSplit = KB <= 2 || CAT;    // two accumulation chains (accuracy)
+        // CAT epilogue: + bias (this lane's column), fused ReLU
+        float bias_c = 0.0f;
+        if constexpr (CAT) bias_c = a.bias != nullptr ? a.bias[col0() + wave * 32 + c] : 0.0f;
         // this lane's byte offset of output row `row` inside an item's first row (col block + strip)
         const int col_b = (col0() + wave * 32 + c) * 4;
         // the first chain stores through an empty descriptor (every store dropped): the stores
@@ -1238,11 +1278,11 @@ struct RelGemm {
             const bool has_next = i + 1 < i_end;
             const Item nxt = has_next ? get_item(i + 1) : cur;
             if (has_next) {
-                issue_rows(a, tid, nrow, v);
+                issue_rows(a, tid, nrow, v, zm);
                 cnt = ncnt;
                 if (i + 2 < i_end) gather_idx(a, get_item(i + 2), tid, nrow, ncnt);
             }
-            const bool new_w = nxt.w != cur.w;
+            const bool new_w = !CAT && nxt.w != cur.w;
             float bn[kPrefetchB ? KH : 1];
             if constexpr (kPrefetchB) {
                 if (new_w) load_b(nxt.w, wave, lane, bn);
@@ -1269,14 +1309,20 @@ struct RelGemm {
                 for (int u = 0; u < SPG; ++u)
                     if (gi * SPG + u < 16) store_prev(gi * SPG + u);
                 if (gi == kCommitAt - 1 && has_next) {
-                    commit(nxt, tid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32);
+                    commit(nxt, tid, v, cnt, As + (buf ^ 1) * 32 * lda, Sc + (buf ^ 1) * 32, zm);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
             stamp(i - i_beg, 1);
             // this item's outputs become the next chain's stores
 #pragma unroll
-            for (int r = 0; r < 16; ++r) prev[r] = kSplit ? acc[r] + acc2[r] : acc[r];
+            for (int r = 0; r < 16; ++r) {
+                prev[r] = kSplit ? acc[r] + acc2[r] : acc[r];
+                if constexpr (CAT) {
+                    prev[r] = prev[r] + bias_c;
+                    if (a.relu) prev[r] = relu_f(prev[r]);
+                }
+            }
             {
                 float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
                 const int bytes = __builtin_amdgcn_readfirstlane(cur.nrows) * N * 4;
@@ -1330,9 +1376,9 @@ struct RelGemm {
         auto get_item = [&](int i) { return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i); };
         Item cur = get_item(i_beg);
         {
-            int crow[WPT];
+            int crow[WPT], zm_unused;
             gather_idx(a, cur, tid, crow, cnt);
-            issue_rows(a, tid, crow, v);
+            issue_rows(a, tid, crow, v, zm_unused);
         }
         int nrow[WPT];  // gathered rows (+ dgrad scale) of the item after the current one
         int ncnt = 1;
@@ -1354,7 +1400,8 @@ struct RelGemm {
             const Item nxt = has_next ? get_item(i + 1) : cur;
             if (has_next) {  // in flight during this item's MFMAs: rows of the next item, row
                              // numbers of the one after
-                issue_rows(a, tid, nrow, v);
+                int zm_unused;
+                issue_rows(a, tid, nrow, v, zm_unused);
                 cnt = ncnt;
                 if (i + 2 < i_end) gather_idx(a, get_item(i + 2), tid, nrow, ncnt);
             }
@@ -1442,10 +1489,10 @@ struct RelGemm {
     }
 };
 
-template <int KB, bool DGRAD, int NB = 1, int OCC = 2>
+template <int KB, bool DGRAD, int NB = 1, int OCC = 2, bool CAT = false>
 __global__ __launch_bounds__(kThreads, OCC) void rel_gemm_kernel(RelGemmArgs a) {
     extern __shared__ float smem[];
-    RelGemm<KB, DGRAD, NB, OCC>::run(a, smem);
+    RelGemm<KB, DGRAD, NB, OCC, CAT>::run(a, smem);
 }
 
 template <int KB>  // Kp = 64·KB
@@ -2727,7 +2774,7 @@ static RootChunks root_chunks(int64_t lo, int64_t hi) {
 
 // Workspace: forward and backward regions are used by different calls, so they overlap.
 struct WsLayout {
-    size_t y = 0, yroot = 0, hf = 0, pseg = 0, prw = 0;     // forward
+    size_t y = 0, yroot = 0, hf = 0, pseg = 0, prw = 0, nmap = 0;  // forward
     size_t g = 0, groot = 0, h = 0, pdx = 0, p = 0, proot = 0, pb = 0;  // backward
     size_t total = 0;      // max(forward, backward): what mpgnn_rgcn_bwd needs
     size_t fwd_total = 0;  // forward part only (mpgnn_rgcn_fwd / _fwd_act)
@@ -2750,6 +2797,7 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
     w.prw = off; off += align256((mode == MPGNN_MODE_ALL ? std::max({p->rw_l.piece_b.size(), (size_t)p->rw_f.nslots,
                                                                      (size_t)p->rwx_f.nslots})
                                                          : 0) * F_out * sizeof(float));
+    w.nmap = off; off += align256((mode == MPGNN_MODE_SINGLE ? (size_t)p->N : 0) * sizeof(int32_t));
     const size_t fwd = off;
     w.fwd_total = std::max<size_t>(fwd, 256);
     off = 0;
@@ -3055,6 +3103,24 @@ static void launch_final(const FinalArgs& a, int nrows, hipStream_t st) {
 __global__ __launch_bounds__(kThreads) void relu_kernel(float* __restrict__ p, size_t n) {
     for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (size_t)gridDim.x * kThreads)
         p[i] = relu_f(p[i]);
+}
+
+// Node map of one relation's segments for the fused mode-SINGLE layer: map[s_row[s]] =
+// s_src[s] + 1 (x row) or s_src[s] (< 0: compact mean row); nodes without a segment keep 0.
+__global__ __launch_bounds__(kThreads) void node_map_kernel(const int* __restrict__ s_row, const int* __restrict__ s_src,
+                                                            int sel_b, int sel_e, int* __restrict__ map) {
+    const int s = sel_b + (int)(blockIdx.x * kThreads + threadIdx.x);
+    if (s >= sel_e) return;
+    const int v = s_src[s];
+    map[s_row[s]] = v >= 0 ? v + 1 : v;
+}
+
+template <int KB>
+static void launch_rel_gemm_cat(const RelGemmArgs& a, hipStream_t st) {
+    constexpr int lda = 64 * KB + 4;
+    const size_t lds = (size_t)(2 * 32 * lda + 64 + 4) * sizeof(float);
+    const int grid = std::min(a.n_root, cu_count() * 2);
+    hipLaunchKernelGGL((rel_gemm_kernel<KB, false, 1, 2, true>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
 // Fast-path row sums over a flat chunked list: flat_rows_kernel over groups [g_lo, g_hi), then
@@ -3404,6 +3470,52 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     float* Yroot = root ? reinterpret_cast<float*>(ws + w.yroot) : nullptr;
     const bool exact = g_exact_order;
     const bool own_range = row_lo == p->shard_lo && row_hi == p->shard_hi;
+    // Mode SINGLE, unsharded, F_in ∈ {64, 128}, F_out = 128: ONE fused GEMM per layer,
+    //   out[i] = act([x_i | mean_i] @ [root; W] + bias)   (K = 2·F_in; mean_i = 0 without a segment)
+    // — a node has at most one segment of the relation, so the transform, the root term, the
+    // combine and the activation of mp_rgcn_layer.py:245-268 (+ model.py:211,214) need no Y,
+    // Y_root or combine pass.
+    const bool cat = mode == MPGNN_MODE_SINGLE && !exact && g_rel_gemm && root != nullptr &&
+                     (F_in == 64 || F_in == 128) && F_out == 128 && row_lo == 0 && row_hi == p->N &&
+                     p->shard_lo == 0 && p->shard_hi == p->N && p->N <= INT32_MAX - 1;
+    if (cat) {
+        float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
+        {
+            TimedLaunch tl(MPGNN_K_MEAN, strm);
+            st = run_means_multi(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
+            if (st != MPGNN_OK) return st;
+        }
+        int* nmap = reinterpret_cast<int*>(ws + w.nmap);
+        {
+            TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
+            if ((st = hip_check(hipMemsetAsync(nmap, 0, (size_t)p->N * sizeof(int), strm), "memset node map")))
+                return st;
+            if (s.sel_e > s.sel_b) {
+                hipLaunchKernelGGL(node_map_kernel, dim3((s.sel_e - s.sel_b + kThreads - 1) / kThreads), dim3(kThreads),
+                                   0, strm, p->d.s_row, p->d.s_src, s.sel_b, s.sel_e, nmap);
+                if ((st = hip_check(hipGetLastError(), "node_map_kernel launch"))) return st;
+            }
+        }
+        RelGemmArgs r{};
+        r.n_rel = 0;
+        r.n_root = (int)((p->N + 31) / 32);
+        r.Arel = H;
+        r.Aroot = x;
+        r.m_lo = s.m_lo;
+        r.m_rows = std::max(s.m_hi - s.m_lo, 1);
+        r.node_map = nmap;
+        r.W = weight;
+        r.Wroot = root;
+        r.Yroot = out;
+        r.row_lo = 0;
+        r.row_hi = (int)p->N;
+        r.bias = bias;
+        r.relu = act == MPGNN_ACT_RELU;
+        TimedLaunch tl(MPGNN_K_SEG_FWD, strm);
+        if (F_in == 64) launch_rel_gemm_cat<2>(r, strm);
+        else launch_rel_gemm_cat<4>(r, strm);
+        return hip_check(hipGetLastError(), "rel_gemm_kernel (fused mode SINGLE) launch");
+    }
     {
         // 1) Hm[m] = mean(x over multi-edge segment m)  (the saved means when training); a
         //    single-edge segment's mean is its x row, read by the GEMM through s_src

@@ -50,6 +50,10 @@ def _ptr(t):
 # Workspace per (device, stream): calls on one stream run in stream order, so one growing
 # buffer serves them all (and keeps a fixed address for HIP-graph capture).
 _WS: dict = {}
+# Buffers outgrown while a HIP graph was being captured: kernels captured earlier in that graph
+# still read and write them at every replay, so they must outlive the graph (freed by
+# release_workspaces). Outside a capture the smaller buffer is dropped at once.
+_RETIRED: list = []
 
 
 def _workspace(nbytes: int, device: torch.device) -> torch.Tensor:
@@ -58,8 +62,10 @@ def _workspace(nbytes: int, device: torch.device) -> torch.Tensor:
     if ws is None or ws.numel() < nbytes:
         # drop the smaller buffer first: the caching allocator hands its block back in stream
         # order, so the peak is the new size, not old + new (matters at C5: ~58 GB each)
-        _WS.pop(key, None)
-        del ws
+        old = _WS.pop(key, None)
+        if old is not None and torch.cuda.is_current_stream_capturing():
+            _RETIRED.append(old)
+        del ws, old
         ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         _WS[key] = ws
     return ws
@@ -67,8 +73,9 @@ def _workspace(nbytes: int, device: torch.device) -> torch.Tensor:
 
 def release_workspaces() -> None:
     """Drop the cached per-(device, stream) scratch buffers (e.g. after a HIP-graph capture on
-    a side stream); the next call allocates again."""
+    a side stream, once the graph is gone); the next call allocates again."""
     _WS.clear()
+    _RETIRED.clear()
 
 
 def _forward(x, weight, root, bias, plan: GraphPlan, mode: int, relation: int, num_relations: int,

@@ -1,39 +1,25 @@
 #!/usr/bin/env python3
-"""Summarise FETCH_SIZE / WRITE_SIZE passes (rocprofv3 --pmc, kernel-trace only) into
-profiles/pmc_seg_fwd.json: HBM bytes per launch of the forward transform kernel (the bench's
-roofline kernel), corrected as MI355X_MICROARCH.md §HBM prescribes for gfx950 (FETCH_SIZE reports
-half of the read bytes: doubled; WRITE_SIZE exact).
-Usage: pmc_traffic.py <fetch_dir> <write_dir> <out.json> [kernel name prefix]"""
-import csv
-import glob
+"""profiles/r02_pmc_traffic.json — the bench's roofline `traffic`: HBM bytes per launch of each
+forward kernel (role-labelled) from a scripts/pmc_report.py report of the PMC passes
+(FETCH_SIZE ×2 + WRITE_SIZE per MI355X_MICROARCH.md §HBM, separate kernel-trace-only passes).
+usage: pmc_traffic.py <report.json> <workload> <mode> <feat> [out.json]"""
 import json
-import os
 import sys
 
-KERNEL = sys.argv[4] if len(sys.argv) > 4 else "mpgnn::rel_gemm_kernel<2, false>"
-
-
-def avg(root, counter):
-    vals = {}
-    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            name = r.get("Kernel_Name", "").split("(")[0].replace("void ", "")
-            if name.startswith(KERNEL) and r["Counter_Name"] == counter:
-                vals.setdefault(r.get("Dispatch_Id", len(vals)), 0.0)
-                vals[r.get("Dispatch_Id", len(vals))] += float(r["Counter_Value"])
-    return sum(vals.values()) / len(vals), len(vals)
-
-
-fetch_kb, n1 = avg(sys.argv[1], "FETCH_SIZE")
-write_kb, n2 = avg(sys.argv[2], "WRITE_SIZE")
-out = {
-    "workload": "fb15k237", "feat": 128, "kernel": KERNEL,
-    "command": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, kernel-trace only) -- "
-               "python3 scripts/prof_layer.py --iters 20 (one RGCN layer forward, mode ALL)",
-    "dispatches": [n1, n2],
-    "fetch_size_kb_per_launch": round(fetch_kb, 1), "write_size_kb_per_launch": round(write_kb, 1),
-    "hbm_bytes_per_launch": int((2 * fetch_kb + write_kb) * 1024),
-    "correction": "gfx950: FETCH_SIZE x2 (reports half of wide coalesced read bytes), WRITE_SIZE as is",
-}
-json.dump(out, open(sys.argv[3], "w"), indent=1)
-print(json.dumps(out))
+rep = json.load(open(sys.argv[1]))
+workload, mode, feat = sys.argv[2], sys.argv[3], int(sys.argv[4])
+out_path = sys.argv[5] if len(sys.argv) > 5 else "profiles/r02_pmc_traffic.json"
+try:
+    rows = json.load(open(out_path))
+except (OSError, ValueError):
+    rows = []
+rows = [r for r in rows if not (r["workload"] == workload and r["mode"] == mode and r["feat"] == feat)]
+for name, e in rep.items():
+    if "hbm_MB_per_launch" not in e:
+        continue
+    rows.append({"workload": workload, "mode": mode, "feat": feat, "kernel": name,
+                 "hbm_bytes_per_launch": int(e["hbm_MB_per_launch"] * 1e6), "profiled_us": e.get("profiled_us"),
+                 "l2_hit": e.get("l2_hit"), "mfma_util": e.get("mfma_util"),
+                 "source": f"scripts/pmc.sh + scripts/pmc_report.py ({sys.argv[1]})"})
+json.dump(rows, open(out_path, "w"), indent=1)
+print(json.dumps(rows, indent=1))

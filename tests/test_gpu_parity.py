@@ -934,3 +934,123 @@ def test_linear_head_gradients_vs_autograd(n, f, o, bias):
     torch.testing.assert_close(out, ref_out, rtol=1e-4, atol=1e-4)
     for a, b in zip(got, ref):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * max(1.0, float(b.abs().max())))
+
+
+# ------------------------------------------------------------------------------------------
+# mode SINGLE (CustomRGCNConv, the MPGNN metapath layer) at full C2 size and on C5 rows
+# ------------------------------------------------------------------------------------------
+def test_mode_single_full_size_c2_fwd_bwd():
+    """BASELINE.json configs[1] (N = 100 k, R = 16, 128-d), CustomRGCNConv over relation 1 on the
+    whole graph — the fused layer GEMM ([x | mean] @ [root; W] + bias, one launch) — forward and
+    every gradient against the oracle (mp_rgcn_layer.py:225-271) in fp32 and the float64 truth."""
+    g = data.config_graph("C2")
+    N = g.num_nodes
+    gen = torch.Generator().manual_seed(21)
+    W = (torch.rand(128, 128, generator=gen) - 0.5) * 0.2
+    root = (torch.rand(128, 128, generator=gen) - 0.5) * 0.2
+    bias = torch.rand(128, generator=gen) - 0.5
+    gout = torch.randn(N, 128, generator=gen)
+    r32, r64 = oracle_layer2(g.x, g.edge_index, g.edge_type, W, root, bias, gout, mode=MODE_SINGLE, rel=1)
+    plan = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, N)
+    xg = g.x.to(DEV).requires_grad_(True)
+    Wg, rg, bg = (p.to(DEV).requires_grad_(True) for p in (W, root, bias))
+    out = rgcn_conv(xg, Wg, rg, bg, plan, MODE_SINGLE, relation=1)
+    out.backward(gout.to(DEV))
+    close_all({"out": out, "dx": xg.grad, "dW": Wg.grad, "droot": rg.grad, "dbias": bg.grad}, r32, r64, "C2 single ")
+
+
+@pytest.mark.parametrize("f_in", [64, 128])
+def test_fused_single_layer_absent_relation_and_relu(f_in):
+    """The fused mode-SINGLE GEMM with an absent relation (every node row is [x_i | 0]) and with
+    the ReLU epilogue: x @ root + bias, and relu(layer) of the oracle."""
+    g = data.synthetic_graph(900, 3, 8, feat_dim=f_in, seed=3 + f_in)
+    torch.manual_seed(4)
+    conv = mpgnn_amd.CustomRGCNConv(f_in, 128, 1, flow="target_to_source")
+    with torch.no_grad():
+        conv.bias.uniform_(-0.5, 0.5)
+    W, root, bias = (p.detach().clone() for p in (conv.weight, conv.root, conv.bias))
+    conv = conv.to(DEV)
+    ei, et, xg = g.edge_index.to(DEV), g.edge_type.to(DEV), g.x.to(DEV)
+    out = conv(0, 7, xg, ei, et)
+    rel_close(out, g.x @ root + bias, what="absent out", ref64=g.x.double() @ root.double() + bias.double())
+    for rel in (0, 2):
+        r32, r64 = oracle_layer2(g.x, g.edge_index, g.edge_type, W, root, bias, None, mode=MODE_SINGLE, rel=rel)
+        out = conv(0, rel, xg, ei, et, activation="relu")
+        rel_close(out, torch.relu(r32["out"]), what="fused relu out", ref64=torch.relu(r64["out"]))
+
+
+def test_mode_single_c5_full_size_sampled_rows():
+    """BASELINE.json configs[4] (N = 2 M, 64 relations, 256-d) mode SINGLE over relation 2 on the
+    whole graph; checked on 256 sampled rows against the oracle CustomRGCNConv arithmetic
+    (mean over the row's relation-2 edges @ W + x @ root + bias) and the float64 truth."""
+    g = data.config_graph("C5")
+    N, F = g.num_nodes, g.x.shape[1]
+    gen = torch.Generator().manual_seed(8)
+    W = (torch.rand(F, F, generator=gen) - 0.5) * 0.1
+    root = (torch.rand(F, F, generator=gen) - 0.5) * 0.1
+    bias = torch.rand(F, generator=gen) - 0.5
+    plan = mpgnn_amd.GraphPlan(g.edge_index, g.edge_type, N)
+    with torch.no_grad():
+        out = rgcn_conv(g.x.to(DEV), W.to(DEV), root.to(DEV), bias.to(DEV), plan, MODE_SINGLE, relation=2).cpu()
+    rows = torch.from_numpy(np.random.default_rng(2).choice(N, 256, replace=False))
+    ei, et = g.edge_index, g.edge_type
+    sel = (et == 2) & torch.isin(ei[0], rows)
+    src, dst = ei[0][sel], ei[1][sel]
+    for dt in (torch.float32, torch.float64):
+        h = torch.zeros(N, F, dtype=dt)
+        h.index_add_(0, src, g.x[dst].to(dt))  # sequential per row, as scatter_add_
+        cnt = torch.bincount(src, minlength=N).clamp(min=1).to(dt)
+        hr = h[rows] / cnt[rows, None]
+        ref = hr @ W.to(dt) + g.x[rows].to(dt) @ root.to(dt) + bias.to(dt)
+        if dt == torch.float32:
+            r32 = ref
+        else:
+            r64 = ref
+    rel_close(out[rows], r32, what="C5 single sampled rows", ref64=r64)
+
+
+def test_graph_captured_training_step_equals_eager():
+    """One MPNetm training step (forward, NLL, backward, Adam) captured as a HIP graph on torch's
+    own capture stream — the layer workspaces grow inside the capture (forward-only, then the
+    backward's size) — replays bit for bit like the same step run eagerly."""
+    g = data.synthetic_graph(3000, 4, 12, feat_dim=64, seed=9)
+    ei, et, x = g.edge_index.to(DEV), g.edge_type.to(DEV), g.x.to(DEV)
+    y = torch.randint(0, 2, (g.num_nodes,), generator=torch.Generator().manual_seed(1)).to(DEV)
+    torch.manual_seed(30)
+    ref = mpgnn_amd.MPNetm(64, 128, 4, 128, 2, 1, [[3, 1, 0]])
+    nets = [mpgnn_amd.MPNetm(64, 128, 4, 128, 2, 1, [[3, 1, 0]]).to(DEV) for _ in range(2)]
+    for n in nets:
+        n.load_state_dict(ref.state_dict())
+        n.eval()  # dropout off: the two runs see the same masks (none)
+    opts = [torch.optim.Adam(n.parameters(), lr=0.01, weight_decay=5e-4, fused=True, capturable=True) for n in nets]
+
+    def train_step(net, opt):
+        out = net(x, ei, et)
+        loss = torch.nn.functional.nll_loss(out, y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    mpgnn_amd.functional.release_workspaces()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm-up (optimizer state, autograd) off the default stream
+        opts[0].zero_grad(set_to_none=True)
+        train_step(nets[0], opts[0])
+    torch.cuda.current_stream().wait_stream(s)
+    opts[1].zero_grad(set_to_none=True)
+    train_step(nets[1], opts[1])
+    torch.cuda.synchronize()
+    cg = torch.cuda.CUDAGraph()
+    opts[0].zero_grad(set_to_none=True)
+    with torch.cuda.graph(cg):
+        train_step(nets[0], opts[0])
+    for _ in range(3):
+        cg.replay()
+        opts[1].zero_grad(set_to_none=True)
+        train_step(nets[1], opts[1])
+    torch.cuda.synchronize()
+    for (k, a), (_, b) in zip(nets[0].state_dict().items(), nets[1].state_dict().items()):
+        assert torch.equal(a, b), k
+    del cg
+    mpgnn_amd.functional.release_workspaces()

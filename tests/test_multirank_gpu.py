@@ -1,0 +1,111 @@
+"""GPU, world_size 2 over gloo on the one GPU: the multi-rank TRAINING path of the HIP layers.
+
+RGCNConv(shard=(lo, hi), group=WORLD) runs _RGCNConvFn with a group: the forward all-reduces
+the ranks' partial outputs, the backward all-reduces grad_x, dW, droot and dbias (functional.py
+_forward / _RGCNConvFn.backward). Two spawned ranks (fresh processes, before any GPU call) run a
+2-layer Net-style stack forward + backward for both partitions (node_2 'gathered', node_1
+'rows') and compare the output and every gradient with the unsharded layers run in the same
+process, at the parity bar of tests/test_gpu_parity.py. Rendezvous on 127.0.0.1."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, side, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import mpgnn_amd
+        from mpgnn_amd import data
+        from tests.test_gpu_parity import max_rel_err
+        dev = torch.device("cuda", 0)
+        g = data.synthetic_graph(3000, 6, 14, feat_dim=64, seed=4)
+        ei, et = g.edge_index.to(dev), g.edge_type.to(dev)
+        torch.manual_seed(30)
+        conv1 = mpgnn_amd.RGCNConv(64, 128, 6, flow="target_to_source")
+        conv2 = mpgnn_amd.RGCNConv(128, 128, 6, flow="target_to_source")
+        with torch.no_grad():
+            for c in (conv1, conv2):
+                c.bias.uniform_(-0.3, 0.3)
+        twins = []
+        for _ in range(2):
+            a = mpgnn_amd.RGCNConv(64, 128, 6, flow="target_to_source")
+            b = mpgnn_amd.RGCNConv(128, 128, 6, flow="target_to_source")
+            a.load_state_dict(conv1.state_dict())
+            b.load_state_dict(conv2.state_dict())
+            twins.append((a.to(dev), b.to(dev)))
+        gout = torch.randn(g.num_nodes, 128, generator=torch.Generator().manual_seed(5)).to(dev)
+        ranges = mpgnn_amd.distributed.shard_ranges(g.edge_index, g.num_nodes, world, side=side)
+        shard = ranges[rank]
+        res = []
+        for k, (c1, c2) in enumerate(twins):
+            x = g.x.to(dev).requires_grad_(True)
+            if k == 0:  # sharded, per-layer all-reduce inside the autograd function
+                h = c1(x, ei, et, shard=shard, group=dist.group.WORLD, activation="relu", shard_side=side)
+                out = c2(h, ei, et, shard=shard, group=dist.group.WORLD, shard_side=side)
+            else:
+                h = c1(x, ei, et, activation="relu")
+                out = c2(h, ei, et)
+            out.backward(gout)
+            torch.cuda.synchronize()
+            res.append([out.detach(), x.grad] + [p.grad for p in (c1.weight, c1.root, c1.bias, c2.weight, c2.root,
+                                                                    c2.bias)])
+        # float64 truth (CPU oracle, ReLU mask of the unsharded GPU run at kinks): the sharded
+        # result must be as close to it as the unsharded one (x2), or within 1e-4 of it
+        from oracle import rgcn_oracle as orc
+        from tests.test_gpu_parity import kink_act
+        x64 = g.x.double().requires_grad_(True)
+        ps = [p.detach().cpu().double().requires_grad_(True) for p in (conv1.weight, conv1.root, conv1.bias,
+                                                                         conv2.weight, conv2.root, conv2.bias)]
+        pre = orc.rgcn_forward(x64, g.edge_index, g.edge_type, *ps[:3])
+        h_gpu = twins[1][0](g.x.to(dev), ei, et)  # unsharded layer-1 pre-activation
+        act = kink_act([h_gpu.detach()])
+        out64 = orc.rgcn_forward(act(0, pre), g.edge_index, g.edge_type, *ps[3:])
+        out64.backward(gout.cpu().double())
+        truth = [out64.detach(), x64.grad] + [p.grad for p in ps]
+        names = ["out", "dx", "dW1", "droot1", "dbias1", "dW2", "droot2", "dbias2"]
+        errs = {}
+        for n, a, b, t64 in zip(names, res[0], res[1], truth):
+            errs[n] = (max_rel_err(a, b), max_rel_err(a, t64), max_rel_err(b, t64))
+        q.put((rank, errs, None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report to the parent, never hang it
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("side", ["gathered", "rows"])
+def test_two_rank_training_path_matches_unsharded(side):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, side, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    for rank, errs, tb in results:
+        assert tb is None, f"rank {rank}:\n{tb}"
+        for name, (e, e_sh64, e_un64) in errs.items():
+            # cross-rank partial sums change the fp32 summation order (SURVEY 8e parity: 1e-4
+            # elementwise, decided against the float64 truth where the two fp32 orders differ)
+            assert e <= 1e-4 or e_sh64 <= max(1e-4, 2 * e_un64), (side, rank, name, e, e_sh64, e_un64)
