@@ -1046,7 +1046,7 @@ __device__ __forceinline__ void stamp_id_at(unsigned long long* g_stamps) {
 #define stamp_id() ((void)0)
 #endif
 
-template <int KB, bool DGRAD, int NB = 1, int OCC = 2, bool CAT = false>
+template <int KB, bool DGRAD, int NB = 1, int OCC = 2, bool CAT = false, bool PIPE = true>
 struct RelGemm {
     static constexpr int K = 64 * KB;
     static constexpr int KH = K / 2;
@@ -1055,7 +1055,9 @@ struct RelGemm {
     __device__ static __forceinline__ int col0() { return NB > 1 ? (int)blockIdx.y * 128 : 0; }
     // the next relation run's weight slice prefetched into a second register set (K = 256: two
     // slices would not fit; three workgroups per CU: neither)
-    static constexpr bool kPrefetchB = KB <= 2 && OCC <= 2;
+    // pipelined dgrad (the forward's cross-item loop) keeps the previous item's outputs in 16 more
+    // registers: its weight slice is reloaded after the chain on a relation change instead
+    static constexpr bool kPrefetchB = KB <= 2 && OCC <= 2 && !(DGRAD && PIPE);
     static constexpr int lda = K + 4;
     static constexpr int WPT = 32 * (K / 4) / kThreads;  // float4 of an A tile per thread
 
@@ -1217,7 +1219,7 @@ struct RelGemm {
     // buffer three quarters into item i's chain (its rows were issued at the top of item i).
     __device__ static void run_fwd(const RelGemmArgs& a, float* smem) {
         float* As = smem;                 // [2][32][lda]
-        float* Sc = smem + 2 * 32 * lda;  // commit's (unused) row scales
+        float* Sc = smem + 2 * 32 * lda;  // [2][32] dgrad row scales (forward: unused)
         const int tid = threadIdx.x;
         const int lane = tid & 63, c = lane & 31, h = lane >> 5;
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1318,6 +1320,9 @@ struct RelGemm {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 prev[r] = kSplit ? acc[r] + acc2[r] : acc[r];
+                if constexpr (DGRAD) {  // row scale 1/cnt of relation rows (reciprocal, see commit)
+                    if (!cur.root) prev[r] = prev[r] * Sc[buf * 32 + (r & 3) + 8 * (r >> 2) + 4 * h];
+                }
                 if constexpr (CAT) {
                     prev[r] = prev[r] + bias_c;
                     if (a.relu) prev[r] = relu_f(prev[r]);
@@ -1347,7 +1352,7 @@ struct RelGemm {
     }
 
     __device__ static void run(const RelGemmArgs& a, float* smem) {
-        if constexpr (!DGRAD) {
+        if constexpr (!DGRAD || PIPE) {
             run_fwd(a, smem);
             return;
         }
@@ -1489,10 +1494,10 @@ struct RelGemm {
     }
 };
 
-template <int KB, bool DGRAD, int NB = 1, int OCC = 2, bool CAT = false>
+template <int KB, bool DGRAD, int NB = 1, int OCC = 2, bool CAT = false, bool PIPE = true>
 __global__ __launch_bounds__(kThreads, OCC) void rel_gemm_kernel(RelGemmArgs a) {
     extern __shared__ float smem[];
-    RelGemm<KB, DGRAD, NB, OCC, CAT>::run(a, smem);
+    RelGemm<KB, DGRAD, NB, OCC, CAT, PIPE>::run(a, smem);
 }
 
 template <int KB>  // Kp = 64·KB
@@ -2637,15 +2642,8 @@ static void launch_rel_gemm_wide(const RelGemmArgs& a, hipStream_t st) {
     const size_t lds = (size_t)(2 * 32 * lda + 64 + 4) * sizeof(float);
     const int n_items = a.n_rel + a.n_root;
     const int grid = std::min(n_items, std::max(1, cu_count() * 2 / NB));
-    hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD, NB>), dim3(grid, NB), dim3(kThreads), lds, st, a);
-}
-
-static int rel_occ() {  // experiment switch: workgroups per CU of the B-stationary GEMM
-    static int v = [] {
-        const char* e = std::getenv("MPGNN_REL_OCC");
-        return e ? std::max(2, std::min(3, std::atoi(e))) : 2;
-    }();
-    return v;
+    // K = 256 dgrad: the pipelined loop's extra registers would spill (128 for the B slice)
+    hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD, NB, 2, false, !DGRAD>), dim3(grid, NB), dim3(kThreads), lds, st, a);
 }
 
 template <int KB, bool DGRAD>
@@ -2653,12 +2651,8 @@ static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
     constexpr int lda = 64 * KB + 4;
     const size_t lds = (size_t)(2 * 32 * lda + 64 + 4 + (DGRAD ? 4 * 16 * 64 : 0)) * sizeof(float);
     const int n_items = a.n_rel + a.n_root;
-    const int occ = rel_occ();
-    const int grid = std::min(n_items, cu_count() * occ);
-    if (occ == 3)
-        hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD, 1, 3>), dim3(grid), dim3(kThreads), lds, st, a);
-    else
-        hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
+    const int grid = std::min(n_items, cu_count() * 2);  // two workgroups per CU
+    hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
 static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, hipStream_t st) {
