@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <limits>
 #include <new>
 #include <string>
@@ -289,6 +290,7 @@ static void build_flat(const std::vector<int32_t>& run_ptr, const std::vector<in
                 }
             }
             close_group(local ? 1 : 0);
+            if (local) L.max_pieces = std::max(L.max_pieces, k);
             cs = e;
         }
         const int32_t pe = run_ptr[cuts[ci + 1]];
@@ -395,6 +397,7 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
         return rel_d[ea] == rel_d[eb] && n1[ea] == n1[eb];
     });
     const int64_t G = (int64_t)gstart.size() - 1;
+    tm.mark("  segment run starts");
     std::vector<int32_t> seg_id(G), edge_off(G);  // kept: local edge count, then offsets
     parallel_for(G, [&](int64_t g) {
         int32_t c = 0;
@@ -406,6 +409,7 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
         edge_off[g] = c;
         seg_id[g] = c > 0 ? 1 : 0;
     });
+    tm.mark("  segment local counts");
     const int64_t S_loc = exclusive_scan(seg_id);
     const int64_t E_loc = exclusive_scan(edge_off);
     p->e_col.assign(E_loc, 0);
@@ -415,6 +419,7 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
     p->s_cnt.assign(S_loc, 0);
     p->s_ptr.assign(S_loc + 1, (int32_t)E_loc);
     std::vector<int32_t> seg_of_edge(E_loc);  // segment id of each local edge (relation-major order)
+    std::vector<int32_t> seg_d(S_loc);        // dense relation of each kept segment (ascending)
     parallel_for(G, [&](int64_t g) {
         const int32_t a0 = gstart[g], a1 = gstart[g + 1];
         const int32_t next_off = g + 1 < G ? edge_off[g + 1] : (int32_t)E_loc;
@@ -433,17 +438,18 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
             }
         }
         p->s_row[sid] = (int32_t)n1[e0];
+        seg_d[sid] = rel_d[e0];
         p->s_rel[sid] = p->rel_val32[rel_d[e0]];
         p->s_cnt[sid] = a1 - a0;  // GLOBAL count of (row, relation)
         p->s_ptr[sid] = edge_off[g];
     });
-    for (int64_t g = 0; g < G; ++g) {  // kept segments per dense relation
-        const int32_t next_off = g + 1 < G ? edge_off[g + 1] : (int32_t)E_loc;
-        if (next_off != edge_off[g]) p->rel_seg_ptr[rel_d[by_rel_row[gstart[g]]] + 1]++;
-    }
+    tm.mark("  segment fill");
     p->E = E_loc;
     p->S = S_loc;
-    for (int64_t d = 0; d < R; ++d) p->rel_seg_ptr[d + 1] += p->rel_seg_ptr[d];
+    // kept segments per dense relation: segments are relation-major, so the range of relation d
+    // starts at the first segment whose dense relation is >= d
+    for (int64_t d = 0; d <= R; ++d)
+        p->rel_seg_ptr[d] = (int32_t)(std::lower_bound(seg_d.begin(), seg_d.end(), (int32_t)d) - seg_d.begin());
     for (int64_t d = 0; d < R; ++d)
         p->rel_edge_ptr[d + 1] = p->s_ptr[p->rel_seg_ptr[d + 1]];
     tm.mark("segments");
@@ -487,11 +493,6 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
     }
     tm.mark("multi-edge segments");
 
-    // dense relation of each segment (segments are relation-major)
-    std::vector<int32_t> seg_d(p->S);
-    parallel_for(R, [&](int64_t d) {
-        for (int32_t s = p->rel_seg_ptr[d]; s < p->rel_seg_ptr[d + 1]; ++s) seg_d[s] = (int32_t)d;
-    });
 
     // ---- row-major segment order (node_1, relation) -------------------------------------
     {
@@ -503,98 +504,102 @@ static int32_t build(const int64_t* ei, const int64_t* et, int64_t E, int64_t N,
     }
 
     tm.mark("row-major order");
-    // ---- transposed orders for grad_x ---------------------------------------------------
-    {
-        std::vector<int32_t> edges(p->E);
-        parallel_for(p->E, [&](int64_t k) { edges[k] = (int32_t)k; });
-        std::vector<int32_t> by_col;  // (node_2, relation, node_1, edge)
-        counting_sort(edges, N, [&](int32_t k) { return (int64_t)p->e_col[k]; }, by_col, &p->t_ptr);
-        p->t_seg.resize(p->E);
-        parallel_for(p->E, [&](int64_t q) { p->t_seg[q] = seg_of_edge[by_col[q]]; });
-        // edges are relation-major, so an edge's dense relation follows from its position
-        std::vector<int32_t> edge_d(p->E);
-        parallel_for(R, [&](int64_t d) {
-            for (int32_t k = p->rel_edge_ptr[d]; k < p->rel_edge_ptr[d + 1]; ++k) edge_d[k] = (int32_t)d;
+    const std::vector<int32_t> node_cuts{0, (int32_t)N};
+    // augmented lists: own rows [lo, hi) get a trailing extra-row entry
+    auto augment = [&](const std::vector<int32_t>& ptr, const std::vector<int32_t>& val, FlatHost& F,
+                       std::vector<int32_t>& out_val, int32_t chunk) {
+        std::vector<int32_t> xptr(N + 1, 0);
+        parallel_for(N, [&](int64_t i) { xptr[i] = ptr[i] + (int32_t)std::clamp<int64_t>(i, lo, hi) - (int32_t)lo; });
+        xptr[N] = ptr[N] + (int32_t)(hi - lo);
+        out_val.assign(xptr[N], 0);
+        parallel_for(N, [&](int64_t i) {
+            int32_t w = xptr[i];
+            for (int32_t q = ptr[i]; q < ptr[i + 1]; ++q) out_val[w++] = val[q];
+            if (i >= lo && i < hi) out_val[w] = -(int32_t)(i - lo) - 1;
         });
-        std::vector<int32_t> by_rel_col;  // (relation, node_2, node_1, edge)
-        counting_sort(by_col, R, [&](int32_t k) { return (int64_t)edge_d[k]; }, by_rel_col, nullptr);
-        p->ta_col.resize(p->E);
-        p->ta_seg.resize(p->E);
-        parallel_for(p->E, [&](int64_t q) {
-            p->ta_col[q] = p->e_col[by_rel_col[q]];
-            p->ta_seg[q] = seg_of_edge[by_rel_col[q]];
-        });
-    }
-
-    tm.mark("transposed orders");
-    // ---- ragged two-level lists (bounded serial work per wave) ---------------------------
-    build_ragged(p->s_ptr, p->seg_l);
-    build_ragged(p->t_ptr, p->t_l);
-    build_ragged(p->rw_ptr, p->rw_l);
-    resolve_ragged(p->seg_l, p->e_col);
-    resolve_ragged(p->t_l, p->t_seg);
-    resolve_ragged(p->rw_l, p->rw_seg);
-    tm.mark("ragged lists");
-    {
+        build_flat(xptr, node_cuts, F, chunk);
+    };
+    // The backward-only tables (transposed orders, grad_x lists) are independent of the forward
+    // ones from here on: built on a second host thread beside them (C5: ~2x shorter plan build).
+    std::exception_ptr bwd_error;
+    std::thread bwd_thread([&] {
+        try {
+            // ---- transposed orders for grad_x -------------------------------------------
+            std::vector<int32_t> edges(p->E);
+            parallel_for(p->E, [&](int64_t k) { edges[k] = (int32_t)k; });
+            std::vector<int32_t> by_col;  // (node_2, relation, node_1, edge)
+            counting_sort(edges, N, [&](int32_t k) { return (int64_t)p->e_col[k]; }, by_col, &p->t_ptr);
+            p->t_seg.resize(p->E);
+            parallel_for(p->E, [&](int64_t q) { p->t_seg[q] = seg_of_edge[by_col[q]]; });
+            // edges are relation-major, so an edge's dense relation follows from its position
+            std::vector<int32_t> edge_d(p->E);
+            parallel_for(R, [&](int64_t d) {
+                for (int32_t k = p->rel_edge_ptr[d]; k < p->rel_edge_ptr[d + 1]; ++k) edge_d[k] = (int32_t)d;
+            });
+            std::vector<int32_t> by_rel_col;  // (relation, node_2, node_1, edge)
+            counting_sort(by_col, R, [&](int32_t k) { return (int64_t)edge_d[k]; }, by_rel_col, nullptr);
+            p->ta_col.resize(p->E);
+            p->ta_seg.resize(p->E);
+            parallel_for(p->E, [&](int64_t q) {
+                p->ta_col[q] = p->e_col[by_rel_col[q]];
+                p->ta_seg[q] = seg_of_edge[by_rel_col[q]];
+            });
+            // ragged + flat grad_x lists
+            build_ragged(p->t_ptr, p->t_l);
+            resolve_ragged(p->t_l, p->t_seg);
+            build_flat(p->t_ptr, node_cuts, p->t_f);
+            augment(p->t_ptr, p->t_seg, p->tx_f, p->tx_val, kFlatChunk);
+            // runs of equal (relation, node_2) in ta order (mode SINGLE grad_x)
+            const std::vector<int32_t> run_ptr = run_starts(p->E, [&](int64_t a, int64_t b) {
+                return edge_d[a] == edge_d[b] && p->ta_col[a] == p->ta_col[b];
+            });
+            const int64_t nruns = (int64_t)run_ptr.size() - 1;
+            std::vector<int32_t> run_key(nruns), run_rel(nruns);
+            parallel_for(nruns, [&](int64_t r) {
+                run_key[r] = p->ta_col[run_ptr[r]];
+                run_rel[r] = edge_d[run_ptr[r]];
+            });
+            build_ragged(run_ptr, p->ta_l);
+            resolve_ragged(p->ta_l, p->ta_seg);
+            const size_t runs = run_key.size();
+            p->ta_key.resize(p->ta_l.ent.size());
+            parallel_for((int64_t)runs, [&](int64_t r) {
+                for (int32_t q = p->ta_l.ent_ptr[r]; q < p->ta_l.ent_ptr[r + 1]; ++q) p->ta_key[q] = run_key[r];
+            });
+            p->rel_ta_ent_ptr.assign(R + 1, 0);
+            p->rel_ta_piece_ptr.assign(R + 1, 0);
+            size_t r = 0;
+            for (int64_t d = 0; d < R; ++d) {
+                p->rel_ta_ent_ptr[d] = p->ta_l.ent_ptr[r];
+                p->rel_ta_piece_ptr[d] = p->ta_l.run_piece_ptr[r];
+                while (r < runs && run_rel[r] == d) ++r;
+            }
+            p->rel_ta_ent_ptr[R] = p->ta_l.ent_ptr[runs];
+            p->rel_ta_piece_ptr[R] = p->ta_l.run_piece_ptr[runs];
+        } catch (...) {
+            bwd_error = std::current_exception();
+        }
+    });
+    try {
+        // ---- forward lists: ragged (exact order) + flat (segments, multi-edge, combine) ----
+        build_ragged(p->s_ptr, p->seg_l);
+        build_ragged(p->rw_ptr, p->rw_l);
+        resolve_ragged(p->seg_l, p->e_col);
+        resolve_ragged(p->rw_l, p->rw_seg);
         // segments over edges, cut at relation boundaries (mode SINGLE selects one relation)
         std::vector<int32_t> seg_cuts(p->rel_seg_ptr.begin(), p->rel_seg_ptr.end());
         build_flat(p->s_ptr, seg_cuts, p->seg_f);
         build_flat(p->m_ptr, p->rel_m_ptr, p->segm_f);  // multi-edge segments, cut at relations
-        const std::vector<int32_t> node_cuts{0, (int32_t)N};
-        build_flat(p->t_ptr, node_cuts, p->t_f);
         build_flat(p->rw_ptr, node_cuts, p->rw_f, kFlatChunkRowMajor);
-        // augmented lists: own rows [lo, hi) get a trailing extra-row entry
-        std::vector<int32_t> xptr(N + 1, 0);
-        auto augment = [&](const std::vector<int32_t>& ptr, const std::vector<int32_t>& val, FlatHost& F,
-                           std::vector<int32_t>& out_val, int32_t chunk) {
-            parallel_for(N, [&](int64_t i) { xptr[i] = ptr[i] + (int32_t)std::clamp<int64_t>(i, lo, hi) - (int32_t)lo; });
-            xptr[N] = ptr[N] + (int32_t)(hi - lo);
-            out_val.assign(xptr[N], 0);
-            parallel_for(N, [&](int64_t i) {
-                int32_t w = xptr[i];
-                for (int32_t q = ptr[i]; q < ptr[i + 1]; ++q) out_val[w++] = val[q];
-                if (i >= lo && i < hi) out_val[w] = -(int32_t)(i - lo) - 1;
-            });
-            build_flat(xptr, node_cuts, F, chunk);
-        };
-        augment(p->t_ptr, p->t_seg, p->tx_f, p->tx_val, kFlatChunk);
         augment(p->rw_ptr, p->rw_seg, p->rwx_f, p->rwx_val, kFlatChunkRowMajor);
+    } catch (...) {
+        bwd_thread.join();
+        throw;
     }
-    tm.mark("flat lists");
-    {
-        // runs of equal (relation, node_2) in ta order
-        std::vector<int32_t> edge_d(p->E);  // dense relation of each position (relation-major)
-        parallel_for(R, [&](int64_t d) {
-            for (int32_t k = p->rel_edge_ptr[d]; k < p->rel_edge_ptr[d + 1]; ++k) edge_d[k] = (int32_t)d;
-        });
-        const std::vector<int32_t> run_ptr = run_starts(p->E, [&](int64_t a, int64_t b) {
-            return edge_d[a] == edge_d[b] && p->ta_col[a] == p->ta_col[b];
-        });
-        const int64_t nruns = (int64_t)run_ptr.size() - 1;
-        std::vector<int32_t> run_key(nruns), run_rel(nruns);
-        parallel_for(nruns, [&](int64_t r) {
-            run_key[r] = p->ta_col[run_ptr[r]];
-            run_rel[r] = edge_d[run_ptr[r]];
-        });
-        build_ragged(run_ptr, p->ta_l);
-        resolve_ragged(p->ta_l, p->ta_seg);
-        const size_t runs = run_key.size();
-        p->ta_key.resize(p->ta_l.ent.size());
-        parallel_for((int64_t)runs, [&](int64_t r) {
-            for (int32_t q = p->ta_l.ent_ptr[r]; q < p->ta_l.ent_ptr[r + 1]; ++q) p->ta_key[q] = run_key[r];
-        });
-        p->rel_ta_ent_ptr.assign(R + 1, 0);
-        p->rel_ta_piece_ptr.assign(R + 1, 0);
-        size_t r = 0;
-        for (int64_t d = 0; d < R; ++d) {
-            p->rel_ta_ent_ptr[d] = p->ta_l.ent_ptr[r];
-            p->rel_ta_piece_ptr[d] = p->ta_l.run_piece_ptr[r];
-            while (r < runs && run_rel[r] == d) ++r;
-        }
-        p->rel_ta_ent_ptr[R] = p->ta_l.ent_ptr[runs];
-        p->rel_ta_piece_ptr[R] = p->ta_l.run_piece_ptr[runs];
-    }
-    tm.mark("ta ragged");
+    tm.mark("forward lists");
+    bwd_thread.join();
+    if (bwd_error) std::rethrow_exception(bwd_error);
+    tm.mark("backward tables (joined)");
     p->rel_seg_piece_ptr.assign(R + 1, 0);
     for (int64_t d = 0; d <= R; ++d) p->rel_seg_piece_ptr[d] = p->seg_l.run_piece_ptr[p->rel_seg_ptr[d]];
 

@@ -60,7 +60,9 @@ constexpr int kFlatChunk = 32;
 // means), so they are cut finer to give the combine launch enough waves: 11.7 → 10.6 µs.
 constexpr int kFlatChunkRowMajor = 16;
 constexpr int kFlatGroup = 4;         // chunks per normal group (= waves per workgroup)
-constexpr int kFlatLongPieces = 16;   // pieces a long group sums in LDS (<= 16 · F floats)
+constexpr int kFlatLongPieces = 16;   // pieces a long group sums in LDS (<= 16 · F floats); more
+                                      // pieces serialise too much in one workgroup (C3 grad_x hubs:
+                                      // 32 -> 49 vs 62 us)
 
 struct FlatHost {
     std::vector<int32_t> chunk_ptr;   // [nch+1] positions
@@ -76,6 +78,7 @@ struct FlatHost {
     std::vector<int32_t> cut_group_ptr;  // [ncuts+1] group range of each forced-cut section
     std::vector<int32_t> cut_split_ptr;  // [ncuts+1] split-row range of each section
     int32_t nslots = 0;
+    int32_t max_pieces = 0;           // largest long group (its LDS slots: max_pieces · F floats)
 };
 
 struct FlatDev {

@@ -1770,7 +1770,7 @@ __device__ __forceinline__ void flat_chunk(const FlatArgs& a, int c, int lane, f
 // piece order and finishes the row (one launch, no finalize for rows of <= 16 pieces).
 template <int V, int T, int U = 16>
 __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float lds_pieces[];  // [kFlatLongPieces][F] (long groups)
+    extern __shared__ __attribute__((aligned(16))) float lds_pieces[];  // [max_pieces][F] (long groups)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int g = a.g_lo + (int)blockIdx.x;
@@ -1793,6 +1793,8 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
         if (c < c1) flat_chunk<V, T, U>(a, c, lane, a.carry, bb);
         return;
     }
+    // a long row's pieces (the same 16 loads in flight as a normal chunk: more would raise the
+    // kernel's register count and cost every group occupancy)
     for (int c = c0 + wave; c < c1; c += kWaves) flat_chunk<V, T, U>(a, c, lane, lds_pieces, bb);
     __syncthreads();
     if (wave != 0) return;
@@ -2349,13 +2351,268 @@ __global__ __launch_bounds__(kThreads, 2) void outer_accum_kernel(OuterArgs a) {
     outer_accum_body<VEC>(a, (int)blockIdx.x);
 }
 
-// The weight-gradient chunks and the root / bias chunks of one backward call in ONE launch:
-// blocks [0, n_a) take `a`, the rest `b` (the root part alone is ~60-110 workgroups, a
-// mostly idle chip for a whole launch).
+// Persistent form of the two-part outer-product launch: workgroup w walks the chunks w, w + G, …
+// of [root chunks (`ra`, ra_n of them) | weight chunks (`wa`)] as ONE stream of 16-row slices —
+// the next slice's rows (and the row indices of the one after) are in flight during the current
+// slice's MFMAs ACROSS chunk boundaries, so no chunk pays a cold prologue; a finished chunk's
+// partial goes out after the next slice is committed (its stores never hold up a commit).
+// Same arithmetic per chunk as outer_accum_body (32-row blocks, block totals in row order).
+struct OuterCursor {
+    int chunk;      // global chunk id: [0, ra_n) root chunks, then weight chunks
+    int sl, ns;     // slice within the chunk, slices of the chunk
+    int p0, p1;     // the chunk's row range
+};
+
 template <bool VEC, int SL>
-__global__ __launch_bounds__(kThreads, 2) void outer_accum2_kernel(OuterArgs a, OuterArgs b, int n_a) {
-    if ((int)blockIdx.x < n_a) outer_accum_body<VEC, SL>(a, (int)blockIdx.x);
-    else outer_accum_body<VEC, SL>(b, (int)blockIdx.x - n_a);
+__global__ __launch_bounds__(kThreads, 2) void outer_persist_kernel(OuterArgs ra, OuterArgs wa, int ra_n, int n_all) {
+    constexpr int OB = (SL / 2) * kOuterLd;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* bufs = smem;  // [2 buffers][A, B][OB]
+    const int G = (int)gridDim.x;
+    if ((int)blockIdx.x >= n_all) return;
+    const int m_base = blockIdx.y * kColTile;
+    const int n_base = blockIdx.z * kColTile;
+    const int M = wa.M, Nn = wa.Nn;  // same widths in both parts
+    const int mcols = min(kColTile, M - m_base);
+    const int ncols = min(kColTile, Nn - n_base);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int c = lane & 31;
+    const int h = lane >> 5;
+
+    // the two parts' fields selected BY VALUE (wave-uniform ternaries stay in SGPRs; a reference
+    // to a kernel-argument struct picked at run time would put both structs in scratch)
+    struct Src {
+        const float *A, *A2, *B;
+        const int *a_idx, *b_idx;
+        int a_off, a2_off;
+    };
+    auto src_of = [&](int chunk) {
+        const bool r = chunk < ra_n;
+        Src x;
+        x.A = r ? ra.A : wa.A;
+        x.A2 = r ? ra.A2 : wa.A2;
+        x.B = r ? ra.B : wa.B;
+        x.a_idx = r ? ra.a_idx : wa.a_idx;
+        x.b_idx = r ? ra.b_idx : wa.b_idx;
+        x.a_off = r ? ra.a_off : wa.a_off;
+        x.a2_off = r ? ra.a2_off : wa.a2_off;
+        return x;
+    };
+    // every chunk holds >= 1 row (relation chunks by construction, root chunks by their count)
+    auto open_chunk = [&](int chunk) {
+        OuterCursor k;
+        k.chunk = chunk;
+        k.sl = 0;
+        int p0 = 0, p1 = 0;
+        if (chunk < ra_n) {  // root chunks: fixed-length row ranges
+            p0 = ra.row_lo + chunk * ra.chunk_rows;
+            p1 = min(ra.row_hi, p0 + ra.chunk_rows);
+        } else if (chunk < n_all) {  // relation-pure weight chunks
+            p0 = ld_uniform(wa.chunk_begin, chunk - ra_n + wa.chunk_off);
+            p1 = ld_uniform(wa.chunk_end, chunk - ra_n + wa.chunk_off);
+        }
+        k.p0 = p0;
+        k.p1 = p1;
+        k.ns = (p1 - p0 + SL - 1) / SL;
+        return k;
+    };
+    auto advance = [&](const OuterCursor& k) {
+        if (k.sl + 1 < k.ns) {
+            OuterCursor n = k;
+            n.sl = k.sl + 1;
+            return n;
+        }
+        return open_chunk(k.chunk + G);
+    };
+    auto valid = [&](const OuterCursor& k) { return k.chunk < n_all && k.ns > 0; };
+
+    constexpr int NS = VEC ? SL * 128 / (4 * kThreads) : SL * 128 / kThreads;
+    float4 va[VEC ? NS : 1], vb[VEC ? NS : 1];
+    float sa[VEC ? 1 : NS], sb[VEC ? 1 : NS];
+    int ai[NS], bi[NS], ai_next[NS], bi_next[NS];
+    auto slot_row = [&](int j) { return VEC ? ((tid + j * kThreads) >> 5) : ((tid + j * kThreads) >> 7); };
+    auto slot_col = [&](int j) { return VEC ? 4 * ((tid + j * kThreads) & 31) : ((tid + j * kThreads) & 127); };
+    auto load_idx = [&](const OuterCursor& k, int (&oa)[NS], int (&ob)[NS]) {
+        const Src a = src_of(k.chunk);
+        const int ps = k.p0 + k.sl * SL;
+        const int last = max(k.p1 - 1, k.p0);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int p = min(ps + slot_row(j), last);
+            ob[j] = a.b_idx != nullptr ? a.b_idx[p] : p;
+            oa[j] = a.a_idx != nullptr ? a.a_idx[p] : p - a.a_off;
+        }
+    };
+    auto issue = [&](const OuterCursor& k) {
+        const Src a = src_of(k.chunk);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const float* ar = ai[j] >= 0 ? a.A + (size_t)ai[j] * M : a.A2 + (size_t)(-ai[j] - 1 - a.a2_off) * M;
+            if constexpr (VEC) {
+                const int ca = min(m_base + slot_col(j), M - 4);
+                const int cb = min(n_base + slot_col(j), Nn - 4);
+                va[j] = *reinterpret_cast<const float4*>(ar + ca);
+                vb[j] = *reinterpret_cast<const float4*>(a.B + (size_t)bi[j] * Nn + cb);
+            } else {
+                const int ca = min(m_base + slot_col(j), M - 1);
+                const int cb = min(n_base + slot_col(j), Nn - 1);
+                sa[j] = ar[ca];
+                sb[j] = a.B[(size_t)bi[j] * Nn + cb];
+            }
+        }
+    };
+    auto commit = [&](const OuterCursor& k, float* buf) {
+        const int nr = min(SL, k.p1 - k.p0 - k.sl * SL);
+        float* Al = buf;
+        float* Bl = buf + OB;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int r = slot_row(j);
+            const int col = slot_col(j);
+            const bool live = r < nr;
+            if constexpr (VEC) {
+                const unsigned ka = (live && col < mcols) ? ~0u : 0u;
+                const unsigned kb = (live && col < ncols) ? ~0u : 0u;
+                auto msk = [](float4 v, unsigned m) {
+                    return make_float4(__uint_as_float(__float_as_uint(v.x) & m), __uint_as_float(__float_as_uint(v.y) & m),
+                                       __uint_as_float(__float_as_uint(v.z) & m), __uint_as_float(__float_as_uint(v.w) & m));
+                };
+                *reinterpret_cast<float4*>(Al + outer_row(r) + col) = msk(va[j], ka);
+                *reinterpret_cast<float4*>(Bl + outer_row(r) + col) = msk(vb[j], kb);
+            } else {
+                Al[outer_row(r) + col] = (live && col < mcols) ? sa[j] : 0.0f;
+                Bl[outer_row(r) + col] = (live && col < ncols) ? sb[j] : 0.0f;
+            }
+        }
+    };
+
+    f32x16 acc[4], tot[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            acc[q][r] = 0.0f;
+            tot[q][r] = 0.0f;
+        }
+    float bsum = 0.0f, bblk = 0.0f;
+
+    OuterCursor cur = open_chunk((int)blockIdx.x);
+    if (!valid(cur)) return;
+    OuterCursor nx = advance(cur);   // rows in flight during cur
+    OuterCursor nn = valid(nx) ? advance(nx) : nx;  // row indices in flight during cur
+    load_idx(cur, ai, bi);
+    if (valid(nx)) load_idx(nx, ai_next, bi_next);
+    issue(cur);
+    commit(cur, bufs);
+    __syncthreads();
+    int buf = 0;
+    while (true) {
+        float* cbuf = bufs + buf * 2 * OB;
+        const bool more = valid(nx);
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                ai[j] = ai_next[j];
+                bi[j] = bi_next[j];
+            }
+            if (valid(nn)) load_idx(nn, ai_next, bi_next);
+            issue(nx);
+        }
+        const bool is_root = cur.chunk < ra_n;
+        const bool do_bsum = is_root && ra.Pb != nullptr && blockIdx.y == 0 && tid < kColTile;
+        const int nr = min(SL, cur.p1 - cur.p0 - cur.sl * SL);
+        if (do_bsum) {
+            const float* Bl = cbuf + OB;
+            float bl[SL];
+#pragma unroll
+            for (int r = 0; r < SL; ++r) bl[r] = Bl[outer_row(r) + tid];
+#pragma unroll
+            for (int r = 0; r < SL; ++r) bblk += bl[r];
+        }
+        const float* Ar = cbuf + outer_row(h) + c;
+        const float* Br = cbuf + OB + outer_row(h) + wave * 32 + c;
+        const int steps = (nr + 1) >> 1;
+        float av[4], bv;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) av[q] = Ar[q * 32];
+        bv = Br[0];
+        for (int t = 0; t < steps; ++t) {
+            float an[4], bn;
+            const int o = (t + 1 < steps ? t + 1 : t) * kOuterLd;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) an[q] = Ar[o + q * 32];
+            bn = Br[o];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv, acc[q], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) av[q] = an[q];
+            bv = bn;
+        }
+        const bool chunk_end = cur.sl + 1 == cur.ns;
+        if (((cur.sl + 1) * SL) % kOuterBlock == 0 || chunk_end) {  // block boundary (uniform)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    tot[q][r] += acc[q][r];
+                    acc[q][r] = 0.0f;
+                }
+            bsum += bblk;
+            bblk = 0.0f;
+        }
+        if (more) commit(nx, bufs + (buf ^ 1) * 2 * OB);  // before the chunk's stores (in-order vmcnt)
+        if (chunk_end) {
+            float* D;
+            float* Db = nullptr;
+            if (is_root) {
+                const int cidx = cur.chunk;
+                D = ra.P + (size_t)cidx * M * Nn;
+                Db = ra.Pb != nullptr ? ra.Pb + (size_t)cidx * Nn : nullptr;
+                if (ra.dst_mode == 3) {
+                    D = ra.dst;
+                    Db = ra.dst_b;
+                }
+            } else {
+                const int cidx = cur.chunk - ra_n;
+                D = wa.P + (size_t)cidx * M * Nn;
+                if (wa.dst_mode == 1 || wa.dst_mode == 2) {
+                    const int di = ld_uniform(wa.chunk_dst, cidx + wa.chunk_off);
+                    if (di >= 0) D = wa.dst + (size_t)(wa.dst_mode == 1 ? di : 0) * M * Nn;
+                }
+            }
+            // laundered lane offsets: otherwise LICM hoists the 64 store offsets out of the chunk
+            // loop and holds them live across it (spills)
+            const int ln = opaque(lane);
+            const int col = n_base + wave * 32 + (ln & 31);
+            const int h4 = 4 * (ln >> 5);
+            if (D != nullptr && wave * 32 < ncols && col < Nn) {
+                float* Dc = D + col;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = m_base + q * 32 + (r & 3) + 8 * (r >> 2) + h4;
+                        if (m < M) Dc[(size_t)m * Nn] = tot[q][r];
+                    }
+            }
+            if (do_bsum && Db != nullptr && tid < ncols) Db[n_base + tid] = bsum;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) tot[q][r] = 0.0f;
+            bsum = 0.0f;
+        }
+        __syncthreads();
+        if (!more) break;
+        cur = nx;
+        nx = nn;
+        nn = valid(nn) ? advance(nn) : nn;
+        buf ^= 1;
+    }
 }
 
 // dst[group g] (elems floats) = Σ_{c in chunks of g, ascending} P[c]
@@ -3082,9 +3339,9 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
 }
 
 template <int V, int T>
-static void launch_flat(const FlatArgs& a, hipStream_t st) {
+static void launch_flat(const FlatArgs& a, int max_pieces, hipStream_t st) {
     const int n = a.g_hi - a.g_lo;
-    const size_t lds = (size_t)kFlatLongPieces * a.F * sizeof(float);
+    const size_t lds = (size_t)max_pieces * a.F * sizeof(float);  // 0 when the list has no long row
     hipLaunchKernelGGL((flat_rows_kernel<V, T>), dim3(n), dim3(kThreads), lds, st, a);
 }
 
@@ -3122,6 +3379,7 @@ static void launch_rel_gemm_cat(const RelGemmArgs& a, hipStream_t st) {
 // mode 1 over every row [r_lo, r_hi) (split and empty rows, extra + bias on own rows).
 struct FlatRun {
     const FlatDev* fd;
+    int max_pieces;       // the list's largest long group (LDS slots)
     int g_lo, g_hi, k_lo, k_hi;
     const int* table;
     int idx_off, filter, flo, fhi;
@@ -3171,7 +3429,7 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
         a.out = f.out;
         a.carry = f.carry;
         a.relu = f.final_mode == 0 ? f.relu : 0;  // mode 1: the finalize adds extra + bias first
-        MPGNN_VT_DISPATCH(V, T, launch_flat, a, strm);
+        MPGNN_VT_DISPATCH(V, T, launch_flat, a, f.max_pieces, strm);
         int32_t st = hip_check(hipGetLastError(), "flat_rows_kernel launch");
         if (st != MPGNN_OK) return st;
     }
@@ -3213,6 +3471,7 @@ static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x
         // flat chunked list; chunks and splits of the relation range [d_lo, d_hi)
         FlatRun f{};
         f.fd = &p->d.seg_f;
+        f.max_pieces = p->seg_f.max_pieces;
         f.g_lo = p->seg_f.cut_group_ptr[s.d_lo];
         f.g_hi = p->seg_f.cut_group_ptr[s.d_hi];
         f.k_lo = p->seg_f.cut_split_ptr[s.d_lo];
@@ -3253,6 +3512,7 @@ static int32_t run_means_multi(const mpgnn_plan* p, const Selection& s, const fl
     if (!exact) {
         FlatRun f{};
         f.fd = &p->d.segm_f;
+        f.max_pieces = p->segm_f.max_pieces;
         f.g_lo = p->segm_f.cut_group_ptr[s.d_lo];
         f.g_hi = p->segm_f.cut_group_ptr[s.d_hi];
         f.k_lo = p->segm_f.cut_split_ptr[s.d_lo];
@@ -3544,6 +3804,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         }
         FlatRun f{};
         f.fd = &p->d.rwx_f;
+        f.max_pieces = p->rwx_f.max_pieces;
         f.g_lo = 0;
         f.g_hi = (int)p->rwx_f.group_ptr.size() - 1;
         f.k_lo = 0;
@@ -3570,6 +3831,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     if (mode == MPGNN_MODE_ALL && !exact) {
         FlatRun f{};
         f.fd = &p->d.rw_f;
+        f.max_pieces = p->rw_f.max_pieces;
         f.g_lo = 0;
         f.g_hi = (int)p->rw_f.group_ptr.size() - 1;
         f.table = p->d.rw_seg;
@@ -3655,6 +3917,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         }
         FlatRun f{};
         f.fd = &p->d.tx_f;
+        f.max_pieces = p->tx_f.max_pieces;
         f.g_lo = 0;
         f.g_hi = (int)p->tx_f.group_ptr.size() - 1;
         f.k_lo = 0;
@@ -3679,6 +3942,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
     } else if (mode == MPGNN_MODE_ALL && !exact) {
         FlatRun f{};
         f.fd = &p->d.t_f;
+        f.max_pieces = p->t_f.max_pieces;
         f.g_lo = 0;
         f.g_hi = (int)p->t_f.group_ptr.size() - 1;
         f.table = p->d.t_seg;
@@ -3964,13 +4228,18 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         TimedLaunch tl(MPGNN_K_OUTER, strm);
         // one launch: root chunks (all full length; the relation chunks of small relations are
         // short) dispatched first so they are not the launch's tail, 16-row LDS slices
-        const dim3 grid2(nch + rc.n, mt, nt);
         const size_t lds16 = (size_t)(4 * (16 / 2) * kOuterLd) * sizeof(float);
-        if (outer_vec)
-            hipLaunchKernelGGL((outer_accum2_kernel<true, 16>), grid2, dim3(kThreads), lds16, strm, orr, ow, rc.n);
-        else
-            hipLaunchKernelGGL((outer_accum2_kernel<false, 16>), grid2, dim3(kThreads), lds16, strm, orr, ow, rc.n);
-        if ((st = hip_check(hipGetLastError(), "outer_accum2_kernel launch")) != MPGNN_OK) return st;
+        {
+            // persistent: two workgroups per CU per column tile pair, root chunks first
+            const int n_all = nch + rc.n;
+            const int gx = std::max(1, std::min(n_all, cu_count() * 2 / std::max(1, mt * nt)));
+            const dim3 gridp(gx, mt, nt);
+            if (outer_vec)
+                hipLaunchKernelGGL((outer_persist_kernel<true, 16>), gridp, dim3(kThreads), lds16, strm, orr, ow, rc.n, n_all);
+            else
+                hipLaunchKernelGGL((outer_persist_kernel<false, 16>), gridp, dim3(kThreads), lds16, strm, orr, ow, rc.n, n_all);
+        }
+        if ((st = hip_check(hipGetLastError(), "outer_persist_kernel launch")) != MPGNN_OK) return st;
     } else {
         if (have_w) {
             TimedLaunch tl(MPGNN_K_OUTER, strm);

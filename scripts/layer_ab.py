@@ -20,7 +20,7 @@ ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--backward", action="store_true")
 ap.add_argument("--label", default="")
 a = ap.parse_args()
-g = data.fb15k237_graph(feat_dim=128) if a.workload == "fb15k237" else data.config_graph(a.workload)
+g = data.config_graph(a.workload)
 dev = torch.device("cuda", 0)
 F = g.x.shape[1]
 torch.manual_seed(10)

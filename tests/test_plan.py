@@ -148,8 +148,8 @@ def test_flat_lists_bit_exact_and_well_formed(case, shard):
     rows, or the 2..16 pieces of one row (long group); rows of more pieces have one global carry
     slot per piece."""
     name, ei, et, N = case
-    if name == "hubs":  # long segments / in-lists: rows of 1, 31, 32, 33, 64, 65, 300, 600 entries
-        rows = [1, 31, 32, 33, 64, 65, 300, 600, 2, 5]
+    if name == "hubs":  # long segments / in-lists: rows of 1, 31, 32, 33, 64, 65, 300, 600, 1100 entries
+        rows = [1, 31, 32, 33, 64, 65, 300, 600, 1100, 2, 5]
         n1 = np.concatenate([np.full(k, i) for i, k in enumerate(rows)])
         n2 = np.concatenate([np.arange(k) % 40 for k in rows])
         ei, et, N = np.stack([n1, n2]), np.zeros(len(n1), np.int64), 40
