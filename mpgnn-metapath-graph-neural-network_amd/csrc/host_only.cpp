@@ -17,3 +17,7 @@ extern "C" int32_t mpgnn_set_option(int32_t option, int64_t value) {
     mpgnn::set_last_error("host-only library: kernel options are not available");
     return MPGNN_ERR_UNSUPPORTED;
 }
+
+// no kernels in the host-only build: the plan's device node maps are not built (the fused
+// mode-SINGLE layer builds a relation's map per call when they are absent)
+int32_t mpgnn::build_rel_node_maps(mpgnn_plan*) { return MPGNN_OK; }

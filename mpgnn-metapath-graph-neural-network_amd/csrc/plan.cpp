@@ -711,6 +711,7 @@ int32_t mpgnn_plan_destroy(mpgnn_plan* p) {
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(p->device);
         (void)hipFree(p->d.block);
+        if (p->d.rel_node_map) (void)hipFree(p->d.rel_node_map);
         (void)hipSetDevice(prev);
     }
     delete p;
@@ -873,7 +874,7 @@ int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
         {&p->d.rwx_f.row_of, &p->rwx_f.row_of}, {&p->d.rwx_f.split_row, &p->rwx_f.split_row},
         {&p->d.rwx_f.split_ptr, &p->rwx_f.split_ptr}, {&p->d.rwx_f.split_slot, &p->rwx_f.split_slot},
         {&p->d.rwx_f.row_split, &p->rwx_f.row_split}, {&p->d.rwx_f.group_ptr, &p->rwx_f.group_ptr}, {&p->d.rwx_f.group_long, &p->rwx_f.group_long}, {&p->d.rwx_val, &p->rwx_val},
-        {&p->d.s_src, &p->s_src}, {&p->d.m_ptr, &p->m_ptr}, {&p->d.em_col, &p->em_col}, {&p->d.m_cnt, &p->m_cnt},
+        {&p->d.rel_seg_ptr, &p->rel_seg_ptr}, {&p->d.s_src, &p->s_src}, {&p->d.m_ptr, &p->m_ptr}, {&p->d.em_col, &p->em_col}, {&p->d.m_cnt, &p->m_cnt},
         {&p->d.segm_f.chunk_ptr, &p->segm_f.chunk_ptr}, {&p->d.segm_f.chunk_info, &p->segm_f.chunk_info},
         {&p->d.segm_f.row_of, &p->segm_f.row_of}, {&p->d.segm_f.split_row, &p->segm_f.split_row},
         {&p->d.segm_f.split_ptr, &p->segm_f.split_ptr}, {&p->d.segm_f.split_slot, &p->segm_f.split_slot},
@@ -910,7 +911,10 @@ int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
     p->d.block = block;
     p->d.block_bytes = total;
     p->device = device;
-    return MPGNN_OK;
+    if (hipSetDevice(device) != hipSuccess) return fail(MPGNN_ERR_HIP, "hipSetDevice failed");
+    const int32_t st = build_rel_node_maps(p);
+    (void)hipSetDevice(prev);
+    return st;
 }
 
 }  // extern "C"

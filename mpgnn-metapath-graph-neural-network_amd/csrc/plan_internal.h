@@ -122,7 +122,13 @@ struct DeviceTables {
     int32_t *s_src = nullptr, *m_ptr = nullptr, *em_col = nullptr, *m_cnt = nullptr;
     FlatDev segm_f;                 // flat chunked list of the multi-edge segments over em_col
     int32_t *tx_val = nullptr, *rwx_val = nullptr;  // their entry values (segment id | -(own row + 1))
-    void* block = nullptr;          // single hipMalloc holding every table above
+    int32_t* rel_seg_ptr = nullptr; // [nrel+1] segment range of each dense relation
+    // mode-SINGLE node maps, one row of N per dense relation + an all-zero row (absent relation):
+    // map[d·N + i] = s_src + 1 (x row) or s_src (< 0: compact mean) of node i's relation-d
+    // segment, 0 without one; built on the device at upload when (R+1)·N·4 <= 1 GiB (else the
+    // fused layer builds the relation's map per call)
+    int32_t* rel_node_map = nullptr;
+    void* block = nullptr;          // single hipMalloc holding every table above (but the maps)
     size_t block_bytes = 0;
 };
 
@@ -188,6 +194,8 @@ struct mpgnn_plan {
 namespace mpgnn {
 
 void set_last_error(const std::string& msg);
+// rgcn_kernels.hip: allocate + fill DeviceTables::rel_node_map (synchronous; upload time)
+int32_t build_rel_node_maps(mpgnn_plan* p);
 extern int g_chunk_rows;     // MPGNN_OPT_CHUNK_ROWS: reduction chunk base length (default kChunkRows)
 extern int g_plan_threads;  // host threads of mpgnn_plan_create (0 = hardware concurrency, ≤ 16)
 

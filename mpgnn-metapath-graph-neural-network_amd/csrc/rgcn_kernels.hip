@@ -3366,6 +3366,49 @@ __global__ __launch_bounds__(kThreads) void node_map_kernel(const int* __restric
     map[s_row[s]] = v >= 0 ? v + 1 : v;
 }
 
+// Every relation's node map at once (plan upload): segment s of dense relation d (binary search
+// of s in rel_seg_ptr) sets map[d·N + s_row[s]].
+__global__ __launch_bounds__(kThreads) void rel_node_map_kernel(const int* __restrict__ rel_seg_ptr, int nrel,
+                                                                const int* __restrict__ s_row,
+                                                                const int* __restrict__ s_src, int S, int64_t N,
+                                                                int* __restrict__ map) {
+    const int s = (int)(blockIdx.x * kThreads + threadIdx.x);
+    if (s >= S) return;
+    int lo = 0, hi = nrel;  // largest d with rel_seg_ptr[d] <= s
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (rel_seg_ptr[mid] <= s) lo = mid;
+        else hi = mid;
+    }
+    const int v = s_src[s];
+    map[(int64_t)lo * N + s_row[s]] = v >= 0 ? v + 1 : v;
+}
+
+int32_t build_rel_node_maps(mpgnn_plan* p) {
+    const size_t rows = (size_t)p->nrel + 1;  // + the all-zero row of an absent relation
+    const size_t bytes = rows * (size_t)p->N * sizeof(int32_t);
+    if (p->N == 0 || bytes > ((size_t)1 << 30)) return MPGNN_OK;  // per-call maps instead
+    void* m = nullptr;
+    if (hipMalloc(&m, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return MPGNN_OK;  // not fatal: per-call maps
+    }
+    int32_t st = hip_check(hipMemset(m, 0, bytes), "memset node maps");
+    if (st == MPGNN_OK && p->S > 0) {
+        hipLaunchKernelGGL(rel_node_map_kernel, dim3((unsigned)((p->S + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                           0, p->d.rel_seg_ptr, (int)p->nrel, p->d.s_row, p->d.s_src, (int)p->S, p->N,
+                           static_cast<int*>(m));
+        st = hip_check(hipGetLastError(), "rel_node_map_kernel launch");
+        if (st == MPGNN_OK) st = hip_check(hipDeviceSynchronize(), "node maps");
+    }
+    if (st != MPGNN_OK) {
+        (void)hipFree(m);
+        return st;
+    }
+    p->d.rel_node_map = static_cast<int32_t*>(m);
+    return MPGNN_OK;
+}
+
 template <int KB>
 static void launch_rel_gemm_cat(const RelGemmArgs& a, hipStream_t st) {
     constexpr int lda = 64 * KB + 4;
@@ -3739,16 +3782,20 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
             st = run_means_multi(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
             if (st != MPGNN_OK) return st;
         }
-        int* nmap = reinterpret_cast<int*>(ws + w.nmap);
-        {
+        const int* nmap;
+        if (p->d.rel_node_map != nullptr) {  // the plan's map of this relation (absent: the zero row)
+            nmap = p->d.rel_node_map + (size_t)(s.d_hi > s.d_lo ? s.d_lo : p->nrel) * (size_t)p->N;
+        } else {
+            int* m = reinterpret_cast<int*>(ws + w.nmap);
             TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
-            if ((st = hip_check(hipMemsetAsync(nmap, 0, (size_t)p->N * sizeof(int), strm), "memset node map")))
+            if ((st = hip_check(hipMemsetAsync(m, 0, (size_t)p->N * sizeof(int), strm), "memset node map")))
                 return st;
             if (s.sel_e > s.sel_b) {
                 hipLaunchKernelGGL(node_map_kernel, dim3((s.sel_e - s.sel_b + kThreads - 1) / kThreads), dim3(kThreads),
-                                   0, strm, p->d.s_row, p->d.s_src, s.sel_b, s.sel_e, nmap);
+                                   0, strm, p->d.s_row, p->d.s_src, s.sel_b, s.sel_e, m);
                 if ((st = hip_check(hipGetLastError(), "node_map_kernel launch"))) return st;
             }
+            nmap = m;
         }
         RelGemmArgs r{};
         r.n_rel = 0;
