@@ -137,7 +137,20 @@ enum mpgnn_shard_side { MPGNN_SHARD_GATHERED = 0, MPGNN_SHARD_ROWS = 1 };
 int32_t mpgnn_plan_create_sharded(const int64_t* edge_index, const int64_t* edge_type, int64_t num_edges,
                                   int64_t num_nodes, int64_t shard_lo, int64_t shard_hi, int32_t side,
                                   mpgnn_plan** out);
+/* The same plan built on the GPU from DEVICE-resident edge arrays (edge_index [2, E] and
+ * edge_type [E], int64, on device `device`), enqueued on `stream` (a hipStream_t; NULL = the
+ * null stream) and synchronised before return: stable radix sorts and prefix sums instead of the
+ * host counting sorts, tables bit-identical to mpgnn_plan_create_sharded's. The tables stay on
+ * the device (the plan counts as uploaded to `device`); mpgnn_plan_export copies them back on
+ * first use. Replaces the per-call boolean compaction of mp_rgcn_layer.py:29-35 (called at :231)
+ * like mpgnn_plan_create, for a graph that already lives on the GPU. */
+int32_t mpgnn_plan_create_device(const int64_t* edge_index, const int64_t* edge_type, int64_t num_edges,
+                                 int64_t num_nodes, int64_t shard_lo, int64_t shard_hi, int32_t side,
+                                 int32_t device, void* stream, mpgnn_plan** out);
 int32_t mpgnn_plan_destroy(mpgnn_plan* plan);
+/* 64-bit fingerprint (FNV-1a) of every table of the plan, exported or internal: equal for plans
+ * built from the same graph by either builder (tests/test_plan_device.py). */
+int32_t mpgnn_plan_digest(const mpgnn_plan* plan, uint64_t* out);
 int32_t mpgnn_plan_get_info(const mpgnn_plan* plan, mpgnn_plan_info* info);
 /* Element count of an exported table, and a copy of it into host memory. */
 int32_t mpgnn_plan_table_size(const mpgnn_plan* plan, int32_t table, int64_t* elems, int32_t* elem_bytes);

@@ -63,7 +63,9 @@ _PI64 = ctypes.POINTER(ctypes.c_int64)
 SIGNATURES = [
     ("mpgnn_plan_create", _I32, [_P, _P, _I64, _I64, _I64, _I64, ctypes.POINTER(_P)]),
     ("mpgnn_plan_create_sharded", _I32, [_P, _P, _I64, _I64, _I64, _I64, _I32, ctypes.POINTER(_P)]),
+    ("mpgnn_plan_create_device", _I32, [_P, _P, _I64, _I64, _I64, _I64, _I32, _I32, _P, ctypes.POINTER(_P)]),
     ("mpgnn_plan_destroy", _I32, [_P]),
+    ("mpgnn_plan_digest", _I32, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("mpgnn_plan_get_info", _I32, [_P, ctypes.POINTER(PlanInfo)]),
     ("mpgnn_plan_table_size", _I32, [_P, _I32, _PI64, ctypes.POINTER(_I32)]),
     ("mpgnn_plan_export", _I32, [_P, _I32, _P, _I64]),

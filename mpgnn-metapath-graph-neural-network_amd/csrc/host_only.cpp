@@ -21,3 +21,13 @@ extern "C" int32_t mpgnn_set_option(int32_t option, int64_t value) {
 // no kernels in the host-only build: the plan's device node maps are not built (the fused
 // mode-SINGLE layer builds a relation's map per call when they are absent)
 int32_t mpgnn::build_rel_node_maps(mpgnn_plan*) { return MPGNN_OK; }
+
+// no device build in the host-only library
+int32_t mpgnn::sync_host_tables(mpgnn_plan*) { return MPGNN_OK; }
+void mpgnn::free_device_plan(mpgnn_plan*) {}
+extern "C" int32_t mpgnn_plan_create_device(const int64_t*, const int64_t*, int64_t, int64_t, int64_t, int64_t, int32_t,
+                                            int32_t, void*, mpgnn_plan** out) {
+    if (out) *out = nullptr;
+    mpgnn::set_last_error("host-only library: no device plan build");
+    return MPGNN_ERR_UNSUPPORTED;
+}

@@ -207,6 +207,8 @@ static void build_ragged(const std::vector<int32_t>& run_ptr, RaggedHost& L) {
     const int64_t n_pc = exclusive_scan(L.run_piece_ptr);
     L.ent_ptr[runs] = (int32_t)n_ent;
     L.run_piece_ptr[runs] = (int32_t)n_pc;
+    L.nent = n_ent;
+    L.npieces = n_pc;
     L.ent.assign(n_ent, 0);
     L.piece_b.assign(n_pc, 0);
     L.piece_e.assign(n_pc, 0);
@@ -303,6 +305,8 @@ static void build_flat(const std::vector<int32_t>& run_ptr, const std::vector<in
         L.cut_split_ptr.push_back((int32_t)L.split_row.size());
     }
     L.nslots = slot;
+    L.ngroups = (int32_t)L.group_ptr.size() - 1;
+    L.nsplit = (int32_t)L.split_row.size();
 }
 
 // Resolved entries: a position p becomes idx[p] (what the gather loads), a piece reference
@@ -706,11 +710,12 @@ int32_t mpgnn_plan_create_sharded(const int64_t* edge_index, const int64_t* edge
 
 int32_t mpgnn_plan_destroy(mpgnn_plan* p) {
     if (!p) return MPGNN_OK;
-    if (p->d.block) {
+    if (p->d.block || p->device_built) {
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(p->device);
-        (void)hipFree(p->d.block);
+        if (p->d.block) (void)hipFree(p->d.block);
+        free_device_plan(p);
         if (p->d.rel_node_map) (void)hipFree(p->d.rel_node_map);
         (void)hipSetDevice(prev);
     }
@@ -791,6 +796,7 @@ static const void* table_ptr(const mpgnn_plan* p, int32_t t, int64_t* n, int32_t
 
 int32_t mpgnn_plan_table_size(const mpgnn_plan* p, int32_t table, int64_t* elems, int32_t* elem_bytes) {
     if (!p || !elems || !elem_bytes) return fail(MPGNN_ERR_ARG, "NULL argument");
+    if (int32_t st = sync_host_tables(const_cast<mpgnn_plan*>(p)); st != MPGNN_OK) return st;
     table_ptr(p, table, elems, elem_bytes);
     if (*elems < 0) return fail(MPGNN_ERR_ARG, "unknown table id " + std::to_string(table));
     return MPGNN_OK;
@@ -798,6 +804,7 @@ int32_t mpgnn_plan_table_size(const mpgnn_plan* p, int32_t table, int64_t* elems
 
 int32_t mpgnn_plan_export(const mpgnn_plan* p, int32_t table, void* dst, int64_t capacity) {
     if (!p) return fail(MPGNN_ERR_ARG, "NULL plan");
+    if (int32_t st = sync_host_tables(const_cast<mpgnn_plan*>(p)); st != MPGNN_OK) return st;
     int64_t n = 0;
     int32_t eb = 0;
     const void* src = table_ptr(p, table, &n, &eb);
@@ -807,6 +814,43 @@ int32_t mpgnn_plan_export(const mpgnn_plan* p, int32_t table, void* dst, int64_t
         if (!dst) return fail(MPGNN_ERR_ARG, "NULL destination");
         std::memcpy(dst, src, (size_t)(n * eb));
     }
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_plan_digest(const mpgnn_plan* cp, uint64_t* out) {
+    if (!cp || !out) return fail(MPGNN_ERR_ARG, "NULL argument");
+    mpgnn_plan* p = const_cast<mpgnn_plan*>(cp);
+    if (int32_t st = sync_host_tables(p); st != MPGNN_OK) return st;
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over 32-bit words, sizes included
+    auto word = [&](uint64_t w) { h = (h ^ w) * 1099511628211ull; };
+    auto vec = [&](const std::vector<int32_t>& v) {
+        word(v.size());
+        for (int32_t x : v) word((uint32_t)x);
+    };
+    for (int64_t v : {p->N, p->E_in, p->E, p->S, p->nrel, p->shard_lo, p->shard_hi}) word((uint64_t)v);
+    for (int64_t v : p->rel_values) word((uint64_t)v);
+    for (uint8_t v : p->rel_invalid) word(v);
+    for (const std::vector<int32_t>* v :
+         {&p->rel_seg_ptr, &p->rel_edge_ptr, &p->rel_tile_ptr, &p->rel_t32_ptr, &p->rel_chunk_ptr, &p->e_col, &p->e_id,
+          &p->s_ptr, &p->s_row, &p->s_rel, &p->s_cnt, &p->s_pos, &p->rw_ptr, &p->rw_seg, &p->t_ptr, &p->t_seg, &p->ta_col,
+          &p->ta_seg, &p->tile_begin, &p->tile_end, &p->t32_begin, &p->t32_end, &p->t32_cost, &p->chunk_begin,
+          &p->chunk_end, &p->rel_val32, &p->chunk_dst, &p->s_src, &p->m_ptr, &p->em_col, &p->m_cnt, &p->rel_m_ptr,
+          &p->tx_val, &p->rwx_val, &p->ta_key, &p->rel_ta_ent_ptr, &p->rel_seg_piece_ptr, &p->rel_ta_piece_ptr})
+        vec(*v);
+    for (const RaggedHost* L : {&p->seg_l, &p->t_l, &p->ta_l, &p->rw_l}) {
+        for (const std::vector<int32_t>* v : {&L->ent, &L->ent_ptr, &L->piece_b, &L->piece_e, &L->res, &L->run_piece_ptr})
+            vec(*v);
+        word((uint64_t)L->nent);
+        word((uint64_t)L->npieces);
+    }
+    for (const FlatHost* L : {&p->seg_f, &p->t_f, &p->rw_f, &p->tx_f, &p->rwx_f, &p->segm_f}) {
+        for (const std::vector<int32_t>* v : {&L->chunk_ptr, &L->chunk_info, &L->row_of, &L->group_ptr, &L->group_long,
+                                              &L->split_row, &L->split_ptr, &L->split_slot, &L->row_split,
+                                              &L->cut_group_ptr, &L->cut_split_ptr})
+            vec(*v);
+        for (int32_t v : {L->nslots, L->max_pieces, L->ngroups, L->nsplit}) word((uint32_t)v);
+    }
+    *out = h;
     return MPGNN_OK;
 }
 
@@ -823,7 +867,7 @@ int32_t mpgnn_plan_select(const mpgnn_plan* p, int32_t mode, int64_t relation, i
 
 int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
     if (!p) return fail(MPGNN_ERR_ARG, "NULL plan");
-    if (p->d.block) {
+    if (p->d.block || p->device_built) {
         if (p->device == device) return MPGNN_OK;
         return fail(MPGNN_ERR_ARG, "plan already uploaded to another device");
     }

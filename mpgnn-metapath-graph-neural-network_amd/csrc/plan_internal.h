@@ -3,6 +3,7 @@
 #pragma once
 
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -43,6 +44,7 @@ struct RaggedHost {
     std::vector<int32_t> ent, ent_ptr, piece_b, piece_e;
     std::vector<int32_t> res;            // [entries] idx[position] | -(piece+1)
     std::vector<int32_t> run_piece_ptr;  // [runs+1] first piece of each run
+    int64_t nent = 0, npieces = 0;       // sizes (a device-built plan keeps the vectors on the device)
 };
 
 // Flat chunked list (flat_rows_kernel): the positions of a list whose consecutive runs are
@@ -79,6 +81,7 @@ struct FlatHost {
     std::vector<int32_t> cut_split_ptr;  // [ncuts+1] split-row range of each section
     int32_t nslots = 0;
     int32_t max_pieces = 0;           // largest long group (its LDS slots: max_pieces · F floats)
+    int32_t ngroups = 0, nsplit = 0;  // sizes (a device-built plan keeps the vectors on the device)
 };
 
 struct FlatDev {
@@ -189,6 +192,18 @@ struct mpgnn_plan {
 
     int device = -1;
     mpgnn::DeviceTables d;
+
+    // plans built on the device (plan_device.hip): every table is its own allocation and the big
+    // ones reach their host vector only when exported (sync_host_tables)
+    bool device_built = false;
+    struct DevTable {
+        std::vector<int32_t>* host;
+        const int32_t* dev;
+        int64_t n;
+    };
+    std::vector<DevTable> dev_tables;
+    std::vector<void*> dev_allocs;
+    std::once_flag host_once;
 };
 
 namespace mpgnn {
@@ -196,6 +211,9 @@ namespace mpgnn {
 void set_last_error(const std::string& msg);
 // rgcn_kernels.hip: allocate + fill DeviceTables::rel_node_map (synchronous; upload time)
 int32_t build_rel_node_maps(mpgnn_plan* p);
+// plan_device.hip: copy a device-built plan's tables into its host vectors (once); free its tables
+int32_t sync_host_tables(mpgnn_plan* p);
+void free_device_plan(mpgnn_plan* p);
 extern int g_chunk_rows;     // MPGNN_OPT_CHUNK_ROWS: reduction chunk base length (default kChunkRows)
 extern int g_plan_threads;  // host threads of mpgnn_plan_create (0 = hardware concurrency, ≤ 16)
 

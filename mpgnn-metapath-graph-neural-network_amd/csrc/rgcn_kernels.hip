@@ -3045,7 +3045,7 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
     // piece partials (exact-order / mode SINGLE lists) or flat-list carry slots
     const size_t seg_slots = std::max({(size_t)(s.sp_hi - s.sp_lo), (size_t)p->seg_f.nslots, (size_t)p->segm_f.nslots});
     w.pseg = off; off += align256(seg_slots * fmax * sizeof(float));
-    w.prw = off; off += align256((mode == MPGNN_MODE_ALL ? std::max({p->rw_l.piece_b.size(), (size_t)p->rw_f.nslots,
+    w.prw = off; off += align256((mode == MPGNN_MODE_ALL ? std::max({(size_t)p->rw_l.npieces, (size_t)p->rw_f.nslots,
                                                                      (size_t)p->rwx_f.nslots})
                                                          : 0) * F_out * sizeof(float));
     w.nmap = off; off += align256((mode == MPGNN_MODE_SINGLE ? (size_t)p->N : 0) * sizeof(int32_t));
@@ -3053,7 +3053,7 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
     w.fwd_total = std::max<size_t>(fwd, 256);
     off = 0;
     const size_t dx_pieces = (mode == MPGNN_MODE_ALL)
-                                 ? std::max({p->t_l.piece_b.size(), (size_t)p->t_f.nslots, (size_t)p->tx_f.nslots})
+                                 ? std::max({(size_t)p->t_l.npieces, (size_t)p->t_f.nslots, (size_t)p->tx_f.nslots})
                                  : (size_t)(s.tap_hi - s.tap_lo);
     w.g = off; off += align256(S_sel * F_in * sizeof(float));
     w.groot = off; off += align256(rows * F_in * sizeof(float));
@@ -3068,7 +3068,7 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
 
 static int32_t check_common(const mpgnn_plan* p, int F_in, int F_out) {
     if (!p) return arg_error("NULL plan");
-    if (!p->d.block) {
+    if (!p->d.block && !p->device_built) {
         set_last_error("plan is not on a device: call mpgnn_plan_upload first");
         return MPGNN_ERR_NOT_ON_DEVICE;
     }
@@ -3853,9 +3853,9 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         f.fd = &p->d.rwx_f;
         f.max_pieces = p->rwx_f.max_pieces;
         f.g_lo = 0;
-        f.g_hi = (int)p->rwx_f.group_ptr.size() - 1;
+        f.g_hi = p->rwx_f.ngroups;
         f.k_lo = 0;
-        f.k_hi = (int)p->rwx_f.split_row.size();
+        f.k_hi = p->rwx_f.nsplit;
         f.table = p->d.rwx_val;
         f.idx_off = s.sel_b;
         f.filter = !s.all_segments;
@@ -3880,7 +3880,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         f.fd = &p->d.rw_f;
         f.max_pieces = p->rw_f.max_pieces;
         f.g_lo = 0;
-        f.g_hi = (int)p->rw_f.group_ptr.size() - 1;
+        f.g_hi = p->rw_f.ngroups;
         f.table = p->d.rw_seg;
         f.idx_off = s.sel_b;
         f.filter = !s.all_segments;
@@ -3904,7 +3904,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         return run_flat(f, strm);
     }
     if (mode == MPGNN_MODE_ALL) {
-        const bool ragged = !exact && !p->rw_l.piece_b.empty();
+        const bool ragged = !exact && p->rw_l.npieces > 0;
         a.list_kind = 0;
         a.ptr = ragged ? p->d.rw_ent_ptr : p->d.rw_ptr;
         a.g.ent = ragged ? p->d.rw_ent : nullptr;
@@ -3914,7 +3914,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         a.g.filter = !s.all_segments;
         a.g.flo = s.sel_b;
         a.g.fhi = s.sel_e;
-        if (ragged) k_hi = (int)p->rw_l.piece_b.size();
+        if (ragged) k_hi = (int)(size_t)p->rw_l.npieces;
     } else {
         a.list_kind = 1;  // at most one segment per row: no pieces
         a.keys = p->d.s_row;
@@ -3966,9 +3966,9 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         f.fd = &p->d.tx_f;
         f.max_pieces = p->tx_f.max_pieces;
         f.g_lo = 0;
-        f.g_hi = (int)p->tx_f.group_ptr.size() - 1;
+        f.g_hi = p->tx_f.ngroups;
         f.k_lo = 0;
-        f.k_hi = (int)p->tx_f.split_row.size();
+        f.k_hi = p->tx_f.nsplit;
         f.table = p->d.tx_val;
         f.idx_off = s.sel_b;
         f.filter = !s.all_segments;
@@ -3991,7 +3991,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         f.fd = &p->d.t_f;
         f.max_pieces = p->t_f.max_pieces;
         f.g_lo = 0;
-        f.g_hi = (int)p->t_f.group_ptr.size() - 1;
+        f.g_hi = p->t_f.ngroups;
         f.table = p->d.t_seg;
         f.idx_off = s.sel_b;
         f.filter = !s.all_segments;
@@ -4013,7 +4013,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         st = run_flat(f, strm);
         if (st != MPGNN_OK) return st;
     } else if (mode == MPGNN_MODE_ALL) {
-        const bool ragged = !exact && !p->t_l.piece_b.empty() && s.sel_e > s.sel_b;
+        const bool ragged = !exact && p->t_l.npieces > 0 && s.sel_e > s.sel_b;
         a.list_kind = 0;
         a.ptr = ragged ? p->d.t_ent_ptr : p->d.t_ptr;
         a.g.ent = ragged ? p->d.t_ent : nullptr;
@@ -4025,7 +4025,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         if (ragged) {
             pb = p->d.t_pb;
             pe = p->d.t_pe;
-            k_hi = (int)p->t_l.piece_b.size();
+            k_hi = (int)(size_t)p->t_l.npieces;
         }
     } else {
         a.list_kind = 1;
@@ -4060,7 +4060,7 @@ static void mean_bwd_layout(const mpgnn_plan* p, int32_t mode, const Selection& 
     const size_t S_sel = (size_t)(s.sel_e - s.sel_b);
     const size_t seg_slots = std::max((size_t)(s.sp_hi - s.sp_lo), (size_t)p->seg_f.nslots);
     const size_t dx_pieces = (mode == MPGNN_MODE_ALL)
-                                 ? std::max({p->t_l.piece_b.size(), (size_t)p->t_f.nslots, (size_t)p->tx_f.nslots})
+                                 ? std::max({(size_t)p->t_l.npieces, (size_t)p->t_f.nslots, (size_t)p->tx_f.nslots})
                                  : (size_t)(s.tap_hi - s.tap_lo);
     *off_pdx = align256(S_sel * F * sizeof(float));
     *total = std::max<size_t>(*off_pdx + align256(std::max(dx_pieces, seg_slots) * F * sizeof(float)), 256);

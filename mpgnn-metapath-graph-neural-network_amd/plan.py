@@ -8,6 +8,7 @@ Replaces the per-call, per-relation compaction ``edge_index[:, edge_type == r]``
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 import weakref
 from collections import OrderedDict
@@ -26,18 +27,29 @@ class GraphPlan:
 
     def __init__(self, edge_index: torch.Tensor, edge_type: torch.Tensor, num_nodes: int,
                  shard: tuple[int, int] | None = None, flow: str = "target_to_source",
-                 shard_side: str = "gathered"):
+                 shard_side: str = "gathered", build: str = "auto"):
+        """build: "host" (csrc/plan.cpp, multi-threaded counting sorts), "device" (csrc/
+        plan_device.hip, radix sorts on the GPU holding the graph; the plan is then resident on
+        that device) or "auto" = "device" when edge_index is a CUDA tensor (MPGNN_PLAN_BUILD=host
+        forces the host build). Both give bit-identical tables."""
         if flow not in FLOWS:
             raise ValueError(f"Expected 'flow' to be either {FLOWS} (got '{flow}')")
         if edge_index.dim() != 2 or edge_index.size(0) != 2:
             raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
         if edge_type.dim() != 1 or edge_type.numel() != edge_index.size(1):
             raise ValueError("edge_type must be [E] matching edge_index")
-        ei = edge_index.detach().to("cpu", torch.int64)
+        if build not in ("auto", "host", "device"):
+            raise ValueError(f"build must be 'auto', 'host' or 'device', got {build!r}")
+        on_device = build == "device" or (build == "auto" and edge_index.is_cuda
+                                          and os.environ.get("MPGNN_PLAN_BUILD", "") != "host")
+        dev = None
+        if on_device:
+            dev = edge_index.device if edge_index.is_cuda else torch.device("cuda", torch.cuda.current_device())
+        ei = edge_index.detach().to(dev if on_device else "cpu", torch.int64)
         if flow == "source_to_target":  # aggregate into edge_index[1]: swap the roles
             ei = ei.flip(0)
         ei = ei.contiguous()
-        et = edge_type.detach().to("cpu", torch.int64).contiguous()
+        et = edge_type.detach().to(dev if on_device else "cpu", torch.int64).contiguous()
         self.num_nodes = int(num_nodes)
         self.flow = flow
         lo, hi = shard if shard is not None else (0, self.num_nodes)
@@ -46,13 +58,24 @@ class GraphPlan:
             raise ValueError(f"shard_side must be one of {tuple(_lib.SHARD_SIDES)}")
         self.shard_side = shard_side
         handle = ctypes.c_void_p()
-        check(lib.mpgnn_plan_create_sharded(ei.data_ptr() if ei.numel() else None,
-                                            et.data_ptr() if et.numel() else None,
-                                            et.numel(), self.num_nodes, self.shard[0], self.shard[1],
-                                            _lib.SHARD_SIDES[shard_side], ctypes.byref(handle)),
-              "mpgnn_plan_create")
-        self._h = handle
         self._device = None
+        if on_device:
+            # returns after the build has finished on the stream: ei / et may be freed after it
+            check(lib.mpgnn_plan_create_device(ei.data_ptr() if ei.numel() else None,
+                                               et.data_ptr() if et.numel() else None,
+                                               et.numel(), self.num_nodes, self.shard[0], self.shard[1],
+                                               _lib.SHARD_SIDES[shard_side], dev.index,
+                                               ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream),
+                                               ctypes.byref(handle)),
+                  "mpgnn_plan_create_device")
+            self._device = dev.index
+        else:
+            check(lib.mpgnn_plan_create_sharded(ei.data_ptr() if ei.numel() else None,
+                                                et.data_ptr() if et.numel() else None,
+                                                et.numel(), self.num_nodes, self.shard[0], self.shard[1],
+                                                _lib.SHARD_SIDES[shard_side], ctypes.byref(handle)),
+                  "mpgnn_plan_create")
+        self._h = handle
         self._lock = threading.Lock()
         self._sel_cache: dict = {}
         self._ws_cache: dict = {}
@@ -117,6 +140,12 @@ class GraphPlan:
         check(lib.mpgnn_plan_export(self._h, tid, out.ctypes.data if out.size else None,
                                     out.nbytes), "mpgnn_plan_export")
         return out
+
+    def digest(self) -> int:
+        """Fingerprint of every plan table (equal for both builders on the same graph)."""
+        out = ctypes.c_uint64()
+        check(lib.mpgnn_plan_digest(self._h, ctypes.byref(out)), "mpgnn_plan_digest")
+        return int(out.value)
 
     def hsave_rows(self, mode: int, relation: int, num_relations: int) -> int:
         """Rows of the saved means of a layer call: its multi-edge segments (the single-edge
