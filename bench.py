@@ -334,7 +334,8 @@ def main():
     _lib.lib.mpgnn_timing_enable(0)
     kinds = {"mean": "segment means (flat_rows_kernel over the multi-edge segments)",
              "seg_fwd": "transform GEMM (rel_gemm_kernel)",
-             "row_fwd": "combine / output (flat_rows_kernel or gather_rows_kernel)",
+             "row_fwd": ("combine / output (single_combine_kernel: node -> segment map, one streaming pass)"
+                         if single else "combine / output (flat_rows_kernel over the augmented row-major list)"),
              "final": "split-row finalize", "piece": "ordered pieces"}
     per_layer = {}
     for kind, label in kinds.items():
@@ -381,7 +382,8 @@ def main():
         else:
             ach = work / (us * 1e-6) / 1e9
             peak, unit = PEAK_HBM, "GB/s"
-        kname = {"seg_fwd": "rel_gemm_kernel", "mean": "flat_rows_kernel", "row_fwd": "flat_rows_kernel"}[kind]
+        kname = {"seg_fwd": "rel_gemm_kernel", "mean": "flat_rows_kernel",
+                 "row_fwd": "single_combine_kernel" if single else "flat_rows_kernel"}[kind]
         rooflines.append({"kind": kind, "kernel": kname, "bound": bound, "achieved": round(ach, 2), "peak": peak,
                           "unit": unit, "frac": round(ach / peak, 4), "us_per_layer": us,
                           "share_of_layer": None, "algorithmic": model_txt,
@@ -574,6 +576,10 @@ def main():
             "epoch_def": ("main.py:1121-1134 mpgnn_train + mpgnn_validation" if single else
                           "main_rgcn.py:458-461 train (fwd+NLL+bwd+Adam) + validation forward"),
             "first_step_s": round(first_step_s, 3),
+            "first_step_def": ("graph plan built on the GPU from the resident edge tensors "
+                               "(mpgnn_plan_create_device) + first forward"
+                               if os.environ.get("MPGNN_PLAN_BUILD", "") != "host" else
+                               "host plan build + upload + first forward"),
             "roofline": roofline,
             "roofline_kernels": rooflines,
             "hbm_roofline": hbm_roofline,

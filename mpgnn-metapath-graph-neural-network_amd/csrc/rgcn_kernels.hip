@@ -3366,6 +3366,41 @@ __global__ __launch_bounds__(kThreads) void node_map_kernel(const int* __restric
     map[s_row[s]] = v >= 0 ? v + 1 : v;
 }
 
+// Mode-SINGLE combine for the widths the fused layer does not take (F % 4 == 0): a node has at
+// most one segment of the relation, so out[i] = act((0 + Y[seg(i)] + Yroot[i]) + bias) streams
+// row by row through a per-call node -> segment map (seg_map_kernel) — the same sums, in the same
+// order, as the gather_rows path it replaces (a binary search of s_row per row, then a separate
+// ReLU pass over the output): C5 single, F = 256, 2 M rows.
+__global__ __launch_bounds__(kThreads) void seg_map_kernel(const int* __restrict__ s_row, int sel_b, int sel_e,
+                                                           int* __restrict__ map) {
+    const int s = sel_b + (int)(blockIdx.x * kThreads + threadIdx.x);
+    if (s < sel_e) map[s_row[s]] = s - sel_b;
+}
+
+__global__ __launch_bounds__(kThreads) void single_combine_kernel(const float* __restrict__ Y, const float* __restrict__ Yroot,
+                                                                  const float* __restrict__ bias,
+                                                                  const int* __restrict__ map, int N, int F, int lo,
+                                                                  int hi, int relu, float* __restrict__ out) {
+    const int F4 = F >> 2;
+    const size_t n = (size_t)N * F4;
+    const bool own_terms = Yroot != nullptr || bias != nullptr;
+    for (size_t t = (size_t)blockIdx.x * kThreads + threadIdx.x; t < n; t += (size_t)gridDim.x * kThreads) {
+        const int i = (int)(t / F4);
+        const int c = (int)(t - (size_t)i * F4) * 4;
+        const int m = map[i];
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m >= 0) v = f4_add(v, *reinterpret_cast<const float4*>(Y + (size_t)m * F + c));
+        if (own_terms && i >= lo && i < hi) {
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 ex = Yroot ? *reinterpret_cast<const float4*>(Yroot + (size_t)(i - lo) * F + c) : z;
+            const float4 bb = bias ? *reinterpret_cast<const float4*>(bias + c) : z;
+            v = f4_add(f4_add(v, ex), bb);
+        }
+        if (relu) v = make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
+        *reinterpret_cast<float4*>(out + (size_t)i * F + c) = v;
+    }
+}
+
 // Every relation's node map at once (plan upload): segment s of dense relation d (binary search
 // of s in rel_seg_ptr) sets map[d·N + s_row[s]].
 __global__ __launch_bounds__(kThreads) void rel_node_map_kernel(const int* __restrict__ rel_seg_ptr, int nrel,
@@ -3915,6 +3950,18 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         a.g.flo = s.sel_b;
         a.g.fhi = s.sel_e;
         if (ragged) k_hi = (int)(size_t)p->rw_l.npieces;
+    } else if (!exact && F_out % 4 == 0 && p->N > 0) {
+        int* m = reinterpret_cast<int*>(ws + w.nmap);
+        TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
+        if ((st = hip_check(hipMemsetAsync(m, 0xFF, (size_t)p->N * sizeof(int), strm), "memset segment map"))) return st;
+        if (s.sel_e > s.sel_b)
+            hipLaunchKernelGGL(seg_map_kernel, dim3((s.sel_e - s.sel_b + kThreads - 1) / kThreads), dim3(kThreads), 0, strm,
+                               p->d.s_row, (int)s.sel_b, (int)s.sel_e, m);
+        const size_t n4 = (size_t)p->N * (F_out / 4);
+        hipLaunchKernelGGL(single_combine_kernel, dim3((unsigned)std::min<size_t>((n4 + kThreads - 1) / kThreads, 1u << 20)),
+                           dim3(kThreads), 0, strm, Y, Yroot, bias, m, (int)p->N, F_out, (int)row_lo, (int)row_hi,
+                           act == MPGNN_ACT_RELU ? 1 : 0, out);
+        return hip_check(hipGetLastError(), "single_combine_kernel launch");
     } else {
         a.list_kind = 1;  // at most one segment per row: no pieces
         a.keys = p->d.s_row;
