@@ -332,10 +332,14 @@ def main():
             step()
     torch.cuda.synchronize()
     _lib.lib.mpgnn_timing_enable(0)
+    # mode SINGLE at F = 256 (rgcn_kernels.hip root_epi): root items finish the segment-less rows
+    root_epi = bool(single and F == 256 and world == 1)
     kinds = {"mean": "segment means (flat_rows_kernel over the multi-edge segments)",
              "seg_fwd": "transform GEMM (rel_gemm_kernel)",
-             "row_fwd": ("combine / output (single_combine_kernel: node -> segment map, one streaming pass)"
-                         if single else "combine / output (flat_rows_kernel over the augmented row-major list)"),
+             "row_fwd": (("rows with a segment: single_fix_kernel (the root items' epilogue finished the others)"
+                          if root_epi else "combine / output (single_combine_kernel: node -> segment map, one "
+                          "streaming pass)") if single else
+                         "combine / output (flat_rows_kernel over the augmented row-major list)"),
              "final": "split-row finalize", "piece": "ordered pieces"}
     per_layer = {}
     for kind, label in kinds.items():
@@ -368,8 +372,10 @@ def main():
                     "(x @ root)"),
         "mean": ("hbm", Em * (4.0 * F + 4) + Sm * (4.0 * F + 8), "Em·(4F + 4) gathered x rows + col ids of the "
                  "multi-edge segments, Sm·(4F + 8) mean rows written + counts / pointers"),
-        "row_fwd": ("hbm", (S + n_rows) * (4.0 * F + 4) + n_rows * 4.0 * F, "(S + N)·(4F + 4) Y / Y_root rows + ids "
-                    "gathered, N·4F output rows written"),
+        "row_fwd": (("hbm", S * (12.0 * F + 4), "S·(12F + 4): Y rows + s_row read, the segment rows of out read "
+                     "and written") if root_epi else
+                    ("hbm", (S + n_rows) * (4.0 * F + 4) + n_rows * 4.0 * F, "(S + N)·(4F + 4) Y / Y_root rows + ids "
+                     "gathered, N·4F output rows written")),
     }
     rooflines = []
     for kind, (bound, work, model_txt) in model_costs.items():
@@ -383,7 +389,8 @@ def main():
             ach = work / (us * 1e-6) / 1e9
             peak, unit = PEAK_HBM, "GB/s"
         kname = {"seg_fwd": "rel_gemm_kernel", "mean": "flat_rows_kernel",
-                 "row_fwd": "single_combine_kernel" if single else "flat_rows_kernel"}[kind]
+                 "row_fwd": ("single_fix_kernel" if root_epi else "single_combine_kernel") if single
+                 else "flat_rows_kernel"}[kind]
         rooflines.append({"kind": kind, "kernel": kname, "bound": bound, "achieved": round(ach, 2), "peak": peak,
                           "unit": unit, "frac": round(ach / peak, 4), "us_per_layer": us,
                           "share_of_layer": None, "algorithmic": model_txt,

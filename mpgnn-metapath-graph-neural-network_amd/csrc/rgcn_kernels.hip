@@ -1008,7 +1008,9 @@ struct RelGemmArgs {
     float* Yroot;         // rows i - row_lo
     int sel_b, row_lo, row_hi;
     // fused mode-SINGLE layer (CAT): node rows i read [x_i | mean_i] against [root; W] (K = 2·F_in);
-    // node_map[i] = 0 (no segment of the relation), s_src + 1 (x row), or s_src (< 0: Hm row)
+    // node_map[i] = 0 (no segment of the relation), s_src + 1 (x row), or s_src (< 0: Hm row).
+    // Forward, not CAT (mode-SINGLE root epilogue): root rows i with node_map[i] == 0 are final —
+    // act((0 + x_i @ root) + bias); the others stay x_i @ root for single_fix_kernel
     const int* node_map;
     int m_rows;           // CAT: rows of Hm (indices are clamped to the tables: a bad map cannot fault)
     const float* bias;    // nullable, CAT epilogue
@@ -1046,7 +1048,10 @@ __device__ __forceinline__ void stamp_id_at(unsigned long long* g_stamps) {
 #define stamp_id() ((void)0)
 #endif
 
-template <int KB, bool DGRAD, int NB = 1, int OCC = 2, bool CAT = false, bool PIPE = true>
+// REPI: the mode-SINGLE root epilogue (RelGemmArgs::node_map, forward only) — its own
+// instantiation over ROOT items only (n_rel == 0: no gathered rows, no weight changes), launched
+// after the relation items' normal kernel; the mode-ALL kernels carry none of its registers
+template <int KB, bool DGRAD, int NB = 1, int OCC = 2, bool CAT = false, bool PIPE = true, bool REPI = false>
 struct RelGemm {
     static constexpr int K = 64 * KB;
     static constexpr int KH = K / 2;
@@ -1068,6 +1073,13 @@ struct RelGemm {
 
     __device__ static __forceinline__ Item item(const RelGemmArgs& a, int i) {
         Item it;
+        if constexpr (REPI) {  // root items only
+            it.root = 1;
+            it.r0 = a.row_lo + i * 32;
+            it.nrows = min(32, a.row_hi - it.r0);
+            it.w = a.Wroot;
+            return it;
+        }
         it.root = i >= a.n_rel;
         if (!it.root) {
             it.r0 = ld_uniform(a.t_begin, a.t_lo + i);
@@ -1121,6 +1133,9 @@ struct RelGemm {
 #pragma unroll
         for (int j = 0; j < WPT; ++j) row[j] = it.r0 + min((tid + j * kThreads) / W4, it.nrows - 1);
         cnt = 1;
+        if constexpr (REPI) {  // root epilogue: this lane's row of the item has a segment?
+            if (it.root) cnt = a.node_map[it.r0 + min(tid & 31, it.nrows - 1)];
+        }
         if constexpr (CAT) {  // a thread's float4 column is fixed (256 % W4 == 0): x half or mean half
             const bool mh = (tid % W4) >= W4 / 2;
 #pragma unroll
@@ -1180,8 +1195,16 @@ struct RelGemm {
                 (r < it.nrows && !((zm >> j) & 1)) ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         // the dgrad row scale as a reciprocal (one IEEE division per row and item here, a multiply
-        // per output in the epilogue instead of a 10-instruction division: ≤ 1.5 ulp apart)
-        if (tid < 32) sc[tid] = 1.0f / (float)cnt;
+        // per output in the epilogue instead of a 10-instruction division: ≤ 1.5 ulp apart);
+        // REPI: one word, bit k = row k of the item has a segment of the relation (wave 0's lanes k
+        // loaded row k's flag); read back as a wave-uniform value, so the epilogue's 16 flags cost
+        // no vector registers
+        if constexpr (REPI) {
+            const unsigned long long bm = __ballot(cnt != 0);
+            if (tid == 0) reinterpret_cast<unsigned*>(sc)[0] = (unsigned)bm;
+        } else {
+            if (tid < 32) sc[tid] = 1.0f / (float)cnt;
+        }
     }
 
     // CAT: B = [root; W] — lane half 0 takes root's K/2 rows, half 1 W's
@@ -1234,8 +1257,11 @@ struct RelGemm {
         stamp_id();
         float4 v[WPT];
         int cnt;
-        const ItemTable tab = item_table(a, i_beg, i_end, lane);
-        auto get_item = [&](int i) { return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i); };
+        const ItemTable tab = REPI ? ItemTable{} : item_table(a, i_beg, i_end, lane);
+        auto get_item = [&](int i) {
+            if constexpr (REPI) return item(a, i);
+            return i - i_beg < 64 ? item_at(a, tab, i - i_beg) : item(a, i);
+        };
         Item cur = get_item(i_beg);
         int zm = 0;
         {
@@ -1260,7 +1286,7 @@ struct RelGemm {
         constexpr bool kSplit = KB <= 2 || CAT;    // two accumulation chains (accuracy)
         // CAT epilogue: + bias (this lane's column), fused ReLU
         float bias_c = 0.0f;
-        if constexpr (CAT) bias_c = a.bias != nullptr ? a.bias[col0() + wave * 32 + c] : 0.0f;
+        if constexpr (CAT || REPI) bias_c = a.bias != nullptr ? a.bias[col0() + wave * 32 + c] : 0.0f;
         // this lane's byte offset of output row `row` inside an item's first row (col block + strip)
         const int col_b = (col0() + wave * 32 + c) * 4;
         // the first chain stores through an empty descriptor (every store dropped): the stores
@@ -1284,7 +1310,7 @@ struct RelGemm {
                 cnt = ncnt;
                 if (i + 2 < i_end) gather_idx(a, get_item(i + 2), tid, nrow, ncnt);
             }
-            const bool new_w = !CAT && nxt.w != cur.w;
+            const bool new_w = !CAT && !REPI && nxt.w != cur.w;
             float bn[kPrefetchB ? KH : 1];
             if constexpr (kPrefetchB) {
                 if (new_w) load_b(nxt.w, wave, lane, bn);
@@ -1317,6 +1343,8 @@ struct RelGemm {
             }
             stamp(i - i_beg, 1);
             // this item's outputs become the next chain's stores
+            unsigned emask = 0;
+            if constexpr (REPI) emask = __builtin_amdgcn_readfirstlane(reinterpret_cast<const unsigned*>(Sc)[buf * 32]);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 prev[r] = kSplit ? acc[r] + acc2[r] : acc[r];
@@ -1326,6 +1354,12 @@ struct RelGemm {
                 if constexpr (CAT) {
                     prev[r] = prev[r] + bias_c;
                     if (a.relu) prev[r] = relu_f(prev[r]);
+                }
+                if constexpr (REPI) {  // a row without a segment: (0 + x_i @ root) + bias, act
+                    if (cur.root && !((emask >> ((r & 3) + 8 * (r >> 2) + 4 * h)) & 1u)) {
+                        const float e = (0.0f + prev[r]) + bias_c;
+                        prev[r] = a.relu ? relu_f(e) : e;
+                    }
                 }
             }
             {
@@ -1494,10 +1528,10 @@ struct RelGemm {
     }
 };
 
-template <int KB, bool DGRAD, int NB = 1, int OCC = 2, bool CAT = false, bool PIPE = true>
+template <int KB, bool DGRAD, int NB = 1, int OCC = 2, bool CAT = false, bool PIPE = true, bool REPI = false>
 __global__ __launch_bounds__(kThreads, OCC) void rel_gemm_kernel(RelGemmArgs a) {
     extern __shared__ float smem[];
-    RelGemm<KB, DGRAD, NB, OCC, CAT, PIPE>::run(a, smem);
+    RelGemm<KB, DGRAD, NB, OCC, CAT, PIPE, REPI>::run(a, smem);
 }
 
 template <int KB>  // Kp = 64·KB
@@ -2900,6 +2934,19 @@ static void launch_rel_gemm_wide(const RelGemmArgs& a, hipStream_t st) {
     const int n_items = a.n_rel + a.n_root;
     const int grid = std::min(n_items, std::max(1, cu_count() * 2 / NB));
     // K = 256 dgrad: the pipelined loop's extra registers would spill (128 for the B slice)
+    if (!DGRAD && a.node_map != nullptr) {  // relation items, then root items with the root epilogue
+        RelGemmArgs rel = a, rt = a;
+        rel.n_root = 0;
+        rel.node_map = nullptr;
+        rt.n_rel = 0;
+        if (rel.n_rel > 0)
+            hipLaunchKernelGGL((rel_gemm_kernel<KB, false, NB, 2, false, true>),
+                               dim3(std::min(rel.n_rel, std::max(1, cu_count() * 2 / NB)), NB), dim3(kThreads), lds, st, rel);
+        if (rt.n_root > 0)
+            hipLaunchKernelGGL((rel_gemm_kernel<KB, false, NB, 2, false, true, true>),
+                               dim3(std::min(rt.n_root, std::max(1, cu_count() * 2 / NB)), NB), dim3(kThreads), lds, st, rt);
+        return;
+    }
     hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD, NB, 2, false, !DGRAD>), dim3(grid, NB), dim3(kThreads), lds, st, a);
 }
 
@@ -2909,6 +2956,19 @@ static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
     const size_t lds = (size_t)(2 * 32 * lda + 64 + 4 + (DGRAD ? 4 * 16 * 64 : 0)) * sizeof(float);
     const int n_items = a.n_rel + a.n_root;
     const int grid = std::min(n_items, cu_count() * 2);  // two workgroups per CU
+    if (!DGRAD && a.node_map != nullptr) {  // relation items, then root items with the root epilogue
+        RelGemmArgs rel = a, rt = a;
+        rel.n_root = 0;
+        rel.node_map = nullptr;
+        rt.n_rel = 0;
+        if (rel.n_rel > 0)
+            hipLaunchKernelGGL((rel_gemm_kernel<KB, false>), dim3(std::min(rel.n_rel, cu_count() * 2)), dim3(kThreads), lds, st,
+                               rel);
+        if (rt.n_root > 0)
+            hipLaunchKernelGGL((rel_gemm_kernel<KB, false, 1, 2, false, true, true>), dim3(std::min(rt.n_root, cu_count() * 2)),
+                               dim3(kThreads), lds, st, rt);
+        return;
+    }
     hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
@@ -3092,7 +3152,8 @@ static void clamp_rows(const mpgnn_plan* p, int64_t* lo, int64_t* hi) {
 static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, int gather_kind, const float* src,
                        int K, const float* W, const float* Wroot, int trans, int N, float* Y, float* Yroot,
                        int64_t row_lo, int64_t row_hi, float* H, float* Pseg, bool exact, int kind,
-                       hipStream_t strm, const float* Hsrc = nullptr) {
+                       hipStream_t strm, const float* Hsrc = nullptr, const int* root_map = nullptr,
+                       const float* root_bias = nullptr, int root_relu = 0) {
     const int m_lo = s.m_lo;
     const int n_rel = s.t_hi - s.t_lo;
     const int n_root = (Wroot != nullptr) ? (int)((row_hi - row_lo + kTileRows - 1) / kTileRows) : 0;
@@ -3140,6 +3201,11 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         r.sel_b = s.sel_b;
         r.row_lo = (int)row_lo;
         r.row_hi = (int)row_hi;
+        if (gather_kind != 1 && root_map != nullptr) {  // mode-SINGLE root epilogue (see RelGemmArgs)
+            r.node_map = root_map;
+            r.bias = root_bias;
+            r.relu = root_relu;
+        }
 #ifdef MPGNN_STAMPS
         r.stamps = gather_kind == 1 ? nullptr : g_stamps_host;
 #endif
@@ -3398,6 +3464,26 @@ __global__ __launch_bounds__(kThreads) void single_combine_kernel(const float* _
         }
         if (relu) v = make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
         *reinterpret_cast<float4*>(out + (size_t)i * F + c) = v;
+    }
+}
+
+// After the root epilogue (RelGemmArgs::node_map, not CAT): the rows WITH a segment of the
+// relation, out[s_row[s]] = act(((0 + Y[s]) + x_i @ root) + bias) — the combine's order.
+__global__ __launch_bounds__(kThreads) void single_fix_kernel(const float* __restrict__ Y, const int* __restrict__ s_row,
+                                                              int sel_b, int sel_e, const float* __restrict__ bias,
+                                                              int F, int relu, float* __restrict__ out) {
+    const int F4 = F >> 2;
+    const size_t n = (size_t)(sel_e - sel_b) * F4;
+    for (size_t t = (size_t)blockIdx.x * kThreads + threadIdx.x; t < n; t += (size_t)gridDim.x * kThreads) {
+        const int k = (int)(t / F4);
+        const int c = (int)(t - (size_t)k * F4) * 4;
+        const int i = s_row[sel_b + k];
+        float4* o = reinterpret_cast<float4*>(out + (size_t)i * F + c);
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 v = f4_add(f4_add(z, *reinterpret_cast<const float4*>(Y + (size_t)k * F + c)), *o);
+        v = f4_add(v, bias ? *reinterpret_cast<const float4*>(bias + c) : z);
+        if (relu) v = make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
+        *o = v;
     }
 }
 
@@ -3810,6 +3896,51 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     const bool cat = mode == MPGNN_MODE_SINGLE && !exact && g_rel_gemm && root != nullptr &&
                      (F_in == 64 || F_in == 128) && F_out == 128 && row_lo == 0 && row_hi == p->N &&
                      p->shard_lo == 0 && p->shard_hi == p->N && p->N <= INT32_MAX - 1;
+    // the relation's node map: the plan's (absent relation: its zero row), else built per call
+    auto relation_node_map = [&](const int** nmap) -> int32_t {
+        if (p->d.rel_node_map != nullptr) {
+            *nmap = p->d.rel_node_map + (size_t)(s.d_hi > s.d_lo ? s.d_lo : p->nrel) * (size_t)p->N;
+            return MPGNN_OK;
+        }
+        int* m = reinterpret_cast<int*>(ws + w.nmap);
+        TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
+        int32_t e = hip_check(hipMemsetAsync(m, 0, (size_t)p->N * sizeof(int), strm), "memset node map");
+        if (e != MPGNN_OK) return e;
+        if (s.sel_e > s.sel_b) {
+            hipLaunchKernelGGL(node_map_kernel, dim3((s.sel_e - s.sel_b + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                               strm, p->d.s_row, p->d.s_src, s.sel_b, s.sel_e, m);
+            if ((e = hip_check(hipGetLastError(), "node_map_kernel launch")) != MPGNN_OK) return e;
+        }
+        *nmap = m;
+        return MPGNN_OK;
+    };
+    // Mode SINGLE, F_in = F_out = 256 (the wide B-stationary GEMM; K = 512 of the fused layer would
+    // not fit the weight slice in registers), unsharded: the root items' epilogue finishes every
+    // row without a segment of the relation — act((0 + x_i @ root) + bias) straight into out (87 %
+    // of C5's rows) — and single_fix_kernel adds Y to the rows with one: no Y_root buffer, no
+    // combine pass over all N rows.
+    const bool root_epi = mode == MPGNN_MODE_SINGLE && !exact && g_rel_gemm && g_rel_wide && root != nullptr &&
+                          F_in == 256 && F_out == 256 && row_lo == 0 && row_hi == p->N && p->shard_lo == 0 &&
+                          p->shard_hi == p->N && p->N <= INT32_MAX - 1;
+    if (root_epi) {
+        float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
+        {
+            TimedLaunch tl(MPGNN_K_MEAN, strm);
+            st = run_means_multi(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
+            if (st != MPGNN_OK) return st;
+        }
+        const int* nmap = nullptr;
+        if ((st = relation_node_map(&nmap)) != MPGNN_OK) return st;
+        st = run_seg(p, mode, s, 2, x, F_in, weight, root, 0, F_out, Y, out, row_lo, row_hi, nullptr, nullptr, true,
+                     MPGNN_K_SEG_FWD, strm, H, nmap, bias, act == MPGNN_ACT_RELU ? 1 : 0);
+        if (st != MPGNN_OK || s.sel_e <= s.sel_b) return st;
+        TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
+        const size_t n4 = (size_t)(s.sel_e - s.sel_b) * (F_out / 4);
+        hipLaunchKernelGGL(single_fix_kernel, dim3((unsigned)std::min<size_t>((n4 + kThreads - 1) / kThreads, 1u << 20)),
+                           dim3(kThreads), 0, strm, Y, p->d.s_row, (int)s.sel_b, (int)s.sel_e, bias, F_out,
+                           act == MPGNN_ACT_RELU ? 1 : 0, out);
+        return hip_check(hipGetLastError(), "single_fix_kernel launch");
+    }
     if (cat) {
         float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
         {
@@ -3817,21 +3948,8 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
             st = run_means_multi(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
             if (st != MPGNN_OK) return st;
         }
-        const int* nmap;
-        if (p->d.rel_node_map != nullptr) {  // the plan's map of this relation (absent: the zero row)
-            nmap = p->d.rel_node_map + (size_t)(s.d_hi > s.d_lo ? s.d_lo : p->nrel) * (size_t)p->N;
-        } else {
-            int* m = reinterpret_cast<int*>(ws + w.nmap);
-            TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
-            if ((st = hip_check(hipMemsetAsync(m, 0, (size_t)p->N * sizeof(int), strm), "memset node map")))
-                return st;
-            if (s.sel_e > s.sel_b) {
-                hipLaunchKernelGGL(node_map_kernel, dim3((s.sel_e - s.sel_b + kThreads - 1) / kThreads), dim3(kThreads),
-                                   0, strm, p->d.s_row, p->d.s_src, s.sel_b, s.sel_e, m);
-                if ((st = hip_check(hipGetLastError(), "node_map_kernel launch"))) return st;
-            }
-            nmap = m;
-        }
+        const int* nmap = nullptr;
+        if ((st = relation_node_map(&nmap)) != MPGNN_OK) return st;
         RelGemmArgs r{};
         r.n_rel = 0;
         r.n_root = (int)((p->N + 31) / 32);

@@ -1054,3 +1054,40 @@ def test_graph_captured_training_step_equals_eager():
         assert torch.equal(a, b), k
     del cg
     mpgnn_amd.functional.release_workspaces()
+
+
+@pytest.mark.parametrize("act", [None, "relu"])
+def test_mode_single_256_root_epilogue_fwd_bwd(act):
+    """Mode SINGLE at F_in = F_out = 256 (C5's width): the wide GEMM finishes the rows without a
+    segment of the relation in its root epilogue ((0 + x_i @ root) + bias, ReLU) and
+    single_fix_kernel adds Y to the rows with one. Whole-graph forward and every gradient against
+    the oracle CustomRGCNConv (fp32 and the float64 truth), present and absent relations, a
+    700-edge hub segment."""
+    g = data.synthetic_graph(6000, 4, 12, feat_dim=256, seed=17)
+    hub = torch.stack([torch.full((700,), 5), torch.arange(700) % 6000])
+    ei = torch.cat([g.edge_index, hub], 1)
+    et = torch.cat([g.edge_type, torch.full((700,), 1)])
+    N = g.num_nodes
+    gen = torch.Generator().manual_seed(23)
+    W = (torch.rand(256, 256, generator=gen) - 0.5) * 0.1
+    root = (torch.rand(256, 256, generator=gen) - 0.5) * 0.1
+    bias = torch.rand(256, generator=gen) - 0.5
+    gout = torch.randn(N, 256, generator=gen)
+    plan = mpgnn_amd.GraphPlan(ei.to(DEV), et.to(DEV), N)
+    for rel in (1, 3, 9):  # 9: absent relation
+        xg = g.x.to(DEV).requires_grad_(True)
+        Wg, rg, bg = (p.to(DEV).requires_grad_(True) for p in (W, root, bias))
+        out = rgcn_conv(xg, Wg, rg, bg, plan, MODE_SINGLE, relation=rel, activation=act)
+        out.backward(gout.to(DEV))
+        got = {"out": out, "dx": xg.grad, "dW": Wg.grad, "droot": rg.grad, "dbias": bg.grad}
+        relu = kink_act([out]) if act == "relu" else None  # ReLU kinks follow the GPU's mask
+        refs = {}
+        for dt in (torch.float32, torch.float64):
+            xr, Wr, rr, br = (t.detach().to(dt).requires_grad_(True) for t in (g.x, W, root, bias))
+            o = orc.custom_rgcn_forward(xr, ei, et, rel, Wr, rr, br)
+            if relu is not None:
+                o = relu(0, o)
+            o.backward(gout.to(dt))
+            refs[dt] = {"out": o.detach(), "dx": xr.grad, "dW": Wr.grad, "droot": rr.grad, "dbias": br.grad}
+        for k in got:
+            rel_close(got[k], refs[torch.float32][k], what=f"256 single rel {rel} {act} {k}", ref64=refs[torch.float64][k])
