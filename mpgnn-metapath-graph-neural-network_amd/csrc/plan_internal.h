@@ -27,10 +27,10 @@ inline int32_t item_cost(int64_t edges) {
 }
 // Relation-pure reduction chunks for the weight gradient (outer_accum_kernel): at most this
 // many segments, balanced within a relation (bounds the longest workgroup's MFMA chain).
-// 192 with 16-row slices (MPGNN_OPT_OUTER_SLICE): FB15K backward outer + slab reduce 61.7 ->
-// 54.5 us per layer vs 256 / 32-row slices (128: 56.0; 512 leaves the outer launch too few
-// workgroups: 88 us); scripts/chunk_ab.py
-constexpr int kChunkRows = 192;
+// 256 with the persistent 32-row-slice kernel (outer_persist_kernel): survey-recipe C3 outer +
+// slab reduce 128.4 -> 120 us per layer (224: 135, 288: 129, 320: 137, 384: 135; 128: 136);
+// scripts/layer_ab.py --chunk-rows, profiles/r02_chunk_rows_ab.jsonl
+constexpr int kChunkRows = 256;
 constexpr int64_t kChunkTarget = 4096;  // reduction chunks per graph (chunk length grows past kChunkRows)
 // Ragged lists: a run (segment / gathered row) longer than this many entries is cut into
 // ordered pieces of at most kPieceEntries, summed by piece_sum_kernel; consumers then add the

@@ -1,11 +1,9 @@
-# A/B probe runs on the GPU box: per-kernel µs of one C3 layer's training step, env switches
+# A/B probe runs on the GPU box: per-kernel µs of one C3 layer's training step (backward
+# weight-gradient chunk length sweep)
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for w in fb15k237; do
-  timeout -k 10 120 python scripts/layer_ab.py --workload $w --backward --label "$w-bwd" >> gpurun_out/ab.jsonl
-  MPGNN_OUTER_SL32=1 timeout -k 10 120 python scripts/layer_ab.py --workload $w --backward --label "$w-bwd-sl32" >> gpurun_out/ab.jsonl
-  timeout -k 10 120 python scripts/layer_ab.py --workload $w --backward --label "$w-bwd" >> gpurun_out/ab.jsonl
-  MPGNN_OUTER_SL32=1 timeout -k 10 120 python scripts/layer_ab.py --workload $w --backward --label "$w-bwd-sl32" >> gpurun_out/ab.jsonl
+for cr in 224 256 288 320 256 224; do
+  timeout -k 10 120 python scripts/layer_ab.py --workload fb15k237 --backward --chunk-rows $cr --label "bwd-cr$cr" >> gpurun_out/ab.jsonl
 done
 cat gpurun_out/ab.jsonl

@@ -19,7 +19,10 @@ ap.add_argument("--workload", default="fb15k237")
 ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--backward", action="store_true")
 ap.add_argument("--label", default="")
+ap.add_argument("--chunk-rows", type=int, default=0, help="MPGNN_OPT_CHUNK_ROWS (0: default)")
 a = ap.parse_args()
+if a.chunk_rows:
+    _lib.check(_lib.lib.mpgnn_set_option(20, a.chunk_rows))
 g = data.config_graph(a.workload)
 dev = torch.device("cuda", 0)
 F = g.x.shape[1]
@@ -53,6 +56,7 @@ for _ in range(a.iters):
 torch.cuda.synchronize()
 _lib.lib.mpgnn_timing_enable(0)
 res = {"label": a.label, "workload": a.workload, "env": {k: v for k, v in os.environ.items() if k.startswith("MPGNN_")},
+       "chunk_rows": a.chunk_rows,
        "wall_us_per_iter": round(wall, 2)}
 for kind in _lib.KERNEL_KINDS:
     ms, n = _lib.kernel_timing(kind)
