@@ -2572,20 +2572,22 @@ __global__ __launch_bounds__(kThreads, 2) void outer_persist_kernel(OuterArgs ra
 #pragma unroll
         for (int q = 0; q < 4; ++q) av[q] = Ar[q * 32];
         bv = Br[0];
-        for (int t = 0; t < steps; ++t) {
+        // one k-step as a lambda, no scheduling barriers: the code the compiler makes of this form
+        // interleaves the next step's LDS reads with the MFMAs best (C3 103.4 -> 99.9 us, C2
+        // 407 -> 396 us per layer vs the grouped, barrier-fenced plain loop; same arithmetic)
+        auto kstep = [&](int t) {
             float an[4], bn;
             const int o = (t + 1 < steps ? t + 1 : t) * kOuterLd;
 #pragma unroll
             for (int q = 0; q < 4; ++q) an[q] = Ar[o + q * 32];
             bn = Br[o];
-            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv, acc[q], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < 4; ++q) av[q] = an[q];
             bv = bn;
-        }
+        };
+        for (int t = 0; t < steps; ++t) kstep(t);
         const bool chunk_end = cur.sl + 1 == cur.ns;
         if (((cur.sl + 1) * SL) % kOuterBlock == 0 || chunk_end) {  // block boundary (uniform)
 #pragma unroll
