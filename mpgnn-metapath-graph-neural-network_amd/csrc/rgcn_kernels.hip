@@ -3449,43 +3449,49 @@ __global__ __launch_bounds__(kThreads) void single_combine_kernel(const float* _
                                                                   const float* __restrict__ bias,
                                                                   const int* __restrict__ map, int N, int F, int lo,
                                                                   int hi, int relu, float* __restrict__ out) {
+    // one wave per row, lanes over its float4 columns (no index division)
     const int F4 = F >> 2;
-    const size_t n = (size_t)N * F4;
+    const int lane = threadIdx.x & 63;
     const bool own_terms = Yroot != nullptr || bias != nullptr;
-    for (size_t t = (size_t)blockIdx.x * kThreads + threadIdx.x; t < n; t += (size_t)gridDim.x * kThreads) {
-        const int i = (int)(t / F4);
-        const int c = (int)(t - (size_t)i * F4) * 4;
+    for (int i = (int)blockIdx.x * kWaves + (int)(threadIdx.x >> 6); i < N; i += (int)gridDim.x * kWaves) {
         const int m = map[i];
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (m >= 0) v = f4_add(v, *reinterpret_cast<const float4*>(Y + (size_t)m * F + c));
-        if (own_terms && i >= lo && i < hi) {
-            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 ex = Yroot ? *reinterpret_cast<const float4*>(Yroot + (size_t)(i - lo) * F + c) : z;
-            const float4 bb = bias ? *reinterpret_cast<const float4*>(bias + c) : z;
-            v = f4_add(f4_add(v, ex), bb);
+        const bool own = own_terms && i >= lo && i < hi;
+        for (int c4 = lane; c4 < F4; c4 += 64) {
+            const int c = 4 * c4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (m >= 0) v = f4_add(v, *reinterpret_cast<const float4*>(Y + (size_t)m * F + c));
+            if (own) {
+                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 ex = Yroot ? *reinterpret_cast<const float4*>(Yroot + (size_t)(i - lo) * F + c) : z;
+                const float4 bb = bias ? *reinterpret_cast<const float4*>(bias + c) : z;
+                v = f4_add(f4_add(v, ex), bb);
+            }
+            if (relu) v = make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
+            *reinterpret_cast<float4*>(out + (size_t)i * F + c) = v;
         }
-        if (relu) v = make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
-        *reinterpret_cast<float4*>(out + (size_t)i * F + c) = v;
     }
 }
 
 // After the root epilogue (RelGemmArgs::node_map, not CAT): the rows WITH a segment of the
-// relation, out[s_row[s]] = act(((0 + Y[s]) + x_i @ root) + bias) — the combine's order.
+// relation, out[s_row[s]] = act(((0 + Y[s]) + x_i @ root) + bias) — the combine's order. One wave
+// per segment row.
 __global__ __launch_bounds__(kThreads) void single_fix_kernel(const float* __restrict__ Y, const int* __restrict__ s_row,
                                                               int sel_b, int sel_e, const float* __restrict__ bias,
                                                               int F, int relu, float* __restrict__ out) {
     const int F4 = F >> 2;
-    const size_t n = (size_t)(sel_e - sel_b) * F4;
-    for (size_t t = (size_t)blockIdx.x * kThreads + threadIdx.x; t < n; t += (size_t)gridDim.x * kThreads) {
-        const int k = (int)(t / F4);
-        const int c = (int)(t - (size_t)k * F4) * 4;
+    const int lane = threadIdx.x & 63;
+    const int n = sel_e - sel_b;
+    for (int k = (int)blockIdx.x * kWaves + (int)(threadIdx.x >> 6); k < n; k += (int)gridDim.x * kWaves) {
         const int i = s_row[sel_b + k];
-        float4* o = reinterpret_cast<float4*>(out + (size_t)i * F + c);
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        float4 v = f4_add(f4_add(z, *reinterpret_cast<const float4*>(Y + (size_t)k * F + c)), *o);
-        v = f4_add(v, bias ? *reinterpret_cast<const float4*>(bias + c) : z);
-        if (relu) v = make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
-        *o = v;
+        for (int c4 = lane; c4 < F4; c4 += 64) {
+            const int c = 4 * c4;
+            float4* o = reinterpret_cast<float4*>(out + (size_t)i * F + c);
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 v = f4_add(f4_add(z, *reinterpret_cast<const float4*>(Y + (size_t)k * F + c)), *o);
+            v = f4_add(v, bias ? *reinterpret_cast<const float4*>(bias + c) : z);
+            if (relu) v = make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
+            *o = v;
+        }
     }
 }
 
@@ -3937,8 +3943,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
                      MPGNN_K_SEG_FWD, strm, H, nmap, bias, act == MPGNN_ACT_RELU ? 1 : 0);
         if (st != MPGNN_OK || s.sel_e <= s.sel_b) return st;
         TimedLaunch tl(MPGNN_K_ROW_FWD, strm);
-        const size_t n4 = (size_t)(s.sel_e - s.sel_b) * (F_out / 4);
-        hipLaunchKernelGGL(single_fix_kernel, dim3((unsigned)std::min<size_t>((n4 + kThreads - 1) / kThreads, 1u << 20)),
+        hipLaunchKernelGGL(single_fix_kernel, dim3((unsigned)std::min<int64_t>((s.sel_e - s.sel_b + kWaves - 1) / kWaves, 1 << 20)),
                            dim3(kThreads), 0, strm, Y, p->d.s_row, (int)s.sel_b, (int)s.sel_e, bias, F_out,
                            act == MPGNN_ACT_RELU ? 1 : 0, out);
         return hip_check(hipGetLastError(), "single_fix_kernel launch");
@@ -4077,8 +4082,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         if (s.sel_e > s.sel_b)
             hipLaunchKernelGGL(seg_map_kernel, dim3((s.sel_e - s.sel_b + kThreads - 1) / kThreads), dim3(kThreads), 0, strm,
                                p->d.s_row, (int)s.sel_b, (int)s.sel_e, m);
-        const size_t n4 = (size_t)p->N * (F_out / 4);
-        hipLaunchKernelGGL(single_combine_kernel, dim3((unsigned)std::min<size_t>((n4 + kThreads - 1) / kThreads, 1u << 20)),
+        hipLaunchKernelGGL(single_combine_kernel, dim3((unsigned)std::min<int64_t>((p->N + kWaves - 1) / kWaves, 1 << 20)),
                            dim3(kThreads), 0, strm, Y, Yroot, bias, m, (int)p->N, F_out, (int)row_lo, (int)row_hi,
                            act == MPGNN_ACT_RELU ? 1 : 0, out);
         return hip_check(hipGetLastError(), "single_combine_kernel launch");

@@ -1091,3 +1091,25 @@ def test_mode_single_256_root_epilogue_fwd_bwd(act):
             refs[dt] = {"out": o.detach(), "dx": xr.grad, "dW": Wr.grad, "droot": rr.grad, "dbias": br.grad}
         for k in got:
             rel_close(got[k], refs[torch.float32][k], what=f"256 single rel {rel} {act} {k}", ref64=refs[torch.float64][k])
+
+
+@pytest.mark.parametrize("f_in,f_out", [(96, 64), (128, 256), (64, 36), (32, 6)])
+def test_mode_single_streaming_combine_widths(f_in, f_out):
+    """Mode SINGLE at widths neither the fused layer nor the root epilogue takes: the transform,
+    then single_combine_kernel (one wave per row through the node -> segment map; F_out % 4 != 0
+    keeps the gather-rows combine) — forward with ReLU against the oracle."""
+    g = data.synthetic_graph(3000, 3, 9, feat_dim=f_in, seed=31 + f_in)
+    gen = torch.Generator().manual_seed(f_out)
+    W = (torch.rand(f_in, f_out, generator=gen) - 0.5) * 0.2
+    root = (torch.rand(f_in, f_out, generator=gen) - 0.5) * 0.2
+    bias = torch.rand(f_out, generator=gen) - 0.5
+    plan = mpgnn_amd.GraphPlan(g.edge_index.to(DEV), g.edge_type.to(DEV), g.num_nodes)
+    for rel in (0, 2, 7):  # 7: absent
+        with torch.no_grad():
+            out = rgcn_conv(g.x.to(DEV), W.to(DEV), root.to(DEV), bias.to(DEV), plan, MODE_SINGLE, relation=rel,
+                            activation="relu")
+        act = kink_act([out])
+        r32 = act(0, orc.custom_rgcn_forward(g.x, g.edge_index, g.edge_type, rel, W, root, bias))
+        r64 = act(0, orc.custom_rgcn_forward(g.x.double(), g.edge_index, g.edge_type, rel, W.double(), root.double(),
+                                             bias.double()))
+        rel_close(out, r32, what=f"single combine {f_in}x{f_out} rel {rel}", ref64=r64)
