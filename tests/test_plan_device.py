@@ -105,3 +105,27 @@ def test_device_plan_c2_full_and_layer_parity():
         del os.environ["MPGNN_PLAN_BUILD"]
         mpgnn_amd.plan_cache.clear()
     assert torch.equal(y_dev, y_host)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_device_plan_random_graphs(seed):
+    """Random shapes: node counts from 1 to 5000, empty / tiny / long rows, duplicate edges,
+    sparse and negative relation ids, shards on either side — the device build equals the host
+    build on every table (digest)."""
+    rng = np.random.default_rng(1000 + seed)
+    N = int(rng.choice([1, 2, 7, 64, 333, 5000]))
+    E = int(rng.choice([0, 1, 5, 100, 3000, 20000]))
+    R = int(rng.integers(1, 12))
+    rel_ids = rng.choice(np.array([-9, -1, 0, 1, 2, 3, 5, 8, 13, 1000, 2**35], np.int64), size=R, replace=False)
+    hub = int(rng.integers(0, N))
+    n1 = np.where(rng.random(E) < 0.2, hub, rng.integers(0, N, E))      # a hub row: long segments
+    n2 = np.where(rng.random(E) < 0.2, hub, rng.integers(0, N, E))      # and a hub column: long in-lists
+    et = rel_ids[rng.integers(0, R, E)]
+    if E and rng.random() < 0.3:
+        n1[rng.integers(0, E)] = N + 3                                   # an invalid edge
+    side = "rows" if rng.random() < 0.5 else "gathered"
+    lo = int(rng.integers(0, N + 1))
+    hi = int(rng.integers(lo, N + 1))
+    for shard in ((0, N), (lo, hi)):
+        host, devp = both(np.stack([n1, n2]), et, N, shard[0], shard[1], side)
+        assert devp.digest() == host.digest(), (seed, shard, side)
