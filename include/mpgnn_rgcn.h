@@ -272,12 +272,14 @@ enum mpgnn_option {
     MPGNN_OPT_REL_WIDE = 19,     /* 1 (default): the B-stationary GEMM also takes F_in = F_out = 256 (two 128-column
                                     blocks); 0: tile_gemm_kernel there */
     MPGNN_OPT_CHUNK_ROWS = 20    /* backward weight-gradient reduction chunks: base length in rows (multiple of 32,
-                                    32..1024, default 192) of the root chunks and of the relation chunks of plans
+                                    32..1024, default 256) of the root chunks and of the relation chunks of plans
                                     created afterwards; same results up to fp32 summation order of the slabs */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };
 int32_t mpgnn_set_option(int32_t option, int64_t value);
+/* Current value of an option (tests save and restore the shipped defaults around overrides). */
+int32_t mpgnn_get_option(int32_t option, int64_t* value);
 
 /* --- graph file reader --------------------------------------------------------------
  * link.dat (`node_1 \t relation \t node_2`, one edge per line) → the tensors of

@@ -89,6 +89,7 @@ SIGNATURES = [
     ("mpgnn_linear_wgrad_workspace_bytes", _I32, [_I64, _I32, _I32, _PI64]),
     ("mpgnn_linear_wgrad", _I32, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P]),
     ("mpgnn_set_option", _I32, [_I32, _I64]),
+    ("mpgnn_get_option", _I32, [_I32, _PI64]),
     ("mpgnn_timing_enable", _I32, [_I32]),
     ("mpgnn_debug_occupancy", _I32, [_I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
     ("mpgnn_timing_reset", _I32, []),
@@ -157,6 +158,17 @@ def kernel_timing(kind: str) -> tuple[float, int]:
     ms, n = ctypes.c_double(), ctypes.c_int64()
     check(lib.mpgnn_timing_query(KERNEL_KINDS[kind], ctypes.byref(ms), ctypes.byref(n)), "mpgnn_timing_query")
     return float(ms.value), int(n.value)
+
+
+def get_option(option: int) -> int:
+    """Current value of an ``enum mpgnn_option`` switch."""
+    v = ctypes.c_int64()
+    check(lib.mpgnn_get_option(int(option), ctypes.byref(v)), "mpgnn_get_option")
+    return int(v.value)
+
+
+def set_option(option: int, value: int) -> None:
+    check(lib.mpgnn_set_option(int(option), int(value)), "mpgnn_set_option")
 
 
 def set_exact_order(on: bool) -> None:

@@ -18,9 +18,18 @@ extern "C" int32_t mpgnn_set_option(int32_t option, int64_t value) {
     return MPGNN_ERR_UNSUPPORTED;
 }
 
+extern "C" int32_t mpgnn_get_option(int32_t option, int64_t* value) {
+    if (option == MPGNN_OPT_PLAN_THREADS && value) {
+        *value = mpgnn::g_plan_threads;
+        return MPGNN_OK;
+    }
+    mpgnn::set_last_error("host-only library: kernel options are not available");
+    return MPGNN_ERR_UNSUPPORTED;
+}
+
 // no kernels in the host-only build: the plan's device node maps are not built (the fused
 // mode-SINGLE layer builds a relation's map per call when they are absent)
-int32_t mpgnn::build_rel_node_maps(mpgnn_plan*) { return MPGNN_OK; }
+int32_t mpgnn::build_rel_node_maps(mpgnn_plan*, void*) { return MPGNN_OK; }
 
 // no device build in the host-only library
 int32_t mpgnn::sync_host_tables(mpgnn_plan*) { return MPGNN_OK; }

@@ -130,16 +130,30 @@ inline bool parse_double(const char*& s, const char* e, double& v) {
     return s >= e || is_blank(*s);
 }
 
-// Number of fields of one line (whitespace separated), 0 for a blank line.
+// node.dat / label.dat fields as pandas.read_csv(sep='\t') cuts them: on every single '\t' (a
+// trailing '\r' dropped), so an empty field ('1\t\t3', a trailing tab) is a field of its own
+// (NaN) and a space never separates fields. 0 for a blank line.
+inline const char* strip_cr(const char* b, const char* e) { return (e > b && e[-1] == '\r') ? e - 1 : e; }
+
 inline int64_t count_fields(const char* b, const char* e) {
-    int64_t n = 0;
-    while (b < e) {
-        while (b < e && is_blank(*b)) ++b;
-        if (b >= e) break;
-        ++n;
-        while (b < e && !is_blank(*b)) ++b;
-    }
+    if (!line_has_data(b, e)) return 0;
+    e = strip_cr(b, e);
+    int64_t n = 1;
+    for (; b < e; ++b) n += *b == '\t';
     return n;
+}
+
+// One tab-separated field [b, e): surrounding spaces ignored (pandas' float parser skips them),
+// empty -> NaN, otherwise it must be one number.
+inline bool parse_field(const char* b, const char* e, double& v) {
+    while (b < e && (*b == ' ' || *b == '\r')) ++b;
+    while (e > b && (e[-1] == ' ' || e[-1] == '\r')) --e;
+    if (b == e) {
+        v = std::numeric_limits<double>::quiet_NaN();
+        return true;
+    }
+    const char* s = b;
+    return parse_double(s, e, v) && s == e;
 }
 
 int parse_threads(size_t bytes) {
@@ -310,22 +324,20 @@ int32_t mpgnn_tsv_parse_f64(const char* path, double* out, int64_t rows, int64_t
                 const char* le = nl ? nl : e;
                 if (line_has_data(b, le)) {
                     const char* s = b;
+                    const char* lend = strip_cr(b, le);
                     double* row = out + r * cols;
                     int64_t c = 0;
-                    for (; c < cols; ++c) {
-                        while (s < le && is_blank(*s)) ++s;
-                        if (s >= le) break;
-                        if (!parse_double(s, le, row[c])) {
+                    for (;; ++c) {
+                        const char* fe = (const char*)memchr(s, '\t', (size_t)(lend - s));
+                        if (!fe) fe = lend;
+                        if (c >= cols || !parse_field(s, fe, row[c])) {  // more fields than cols / not a number
                             bad[t] = r;
                             return;
                         }
+                        if (fe == lend) break;
+                        s = fe + 1;
                     }
-                    while (s < le && is_blank(*s)) ++s;
-                    if (s != le) {  // more fields than cols
-                        bad[t] = r;
-                        return;
-                    }
-                    for (; c < cols; ++c) row[c] = nan;  // ragged row: pandas fills NaN
+                    for (++c; c < cols; ++c) row[c] = nan;  // ragged row: pandas fills NaN
                     ++r;
                 }
                 b = le + 1;

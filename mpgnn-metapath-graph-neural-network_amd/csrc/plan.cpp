@@ -955,10 +955,7 @@ int32_t mpgnn_plan_upload(mpgnn_plan* p, int32_t device) {
     p->d.block = block;
     p->d.block_bytes = total;
     p->device = device;
-    if (hipSetDevice(device) != hipSuccess) return fail(MPGNN_ERR_HIP, "hipSetDevice failed");
-    const int32_t st = build_rel_node_maps(p);
-    (void)hipSetDevice(prev);
-    return st;
+    return MPGNN_OK;  // the mode-SINGLE node maps are built on first use (build_rel_node_maps)
 }
 
 }  // extern "C"

@@ -1060,8 +1060,8 @@ void Builder::build_all(const int64_t* ei, const int64_t* et, int64_t E, int64_t
 // device-built plan.
 int32_t sync_host_tables(mpgnn_plan* p) {
     if (!p->device_built) return MPGNN_OK;
-    int32_t st = MPGNN_OK;
     std::call_once(p->host_once, [&] {
+        int32_t st = MPGNN_OK;
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(p->device);
@@ -1074,8 +1074,10 @@ int32_t sync_host_tables(mpgnn_plan* p) {
             }
         }
         (void)hipSetDevice(prev);
+        p->host_sync_status = st;  // every later call reports the same outcome (no half-filled OK)
     });
-    return st;
+    if (p->host_sync_status != MPGNN_OK) set_last_error("a device-built plan's tables could not be copied to the host");
+    return p->host_sync_status;
 }
 
 void free_device_plan(mpgnn_plan* p) {
@@ -1137,12 +1139,13 @@ extern "C" int32_t mpgnn_plan_create_device(const int64_t* edge_index, const int
     } catch (const std::bad_alloc&) {
         st = MPGNN_ERR_ALLOC;
         set_last_error("host allocation failed while building the plan");
+    } catch (const std::exception& e) {  // e.g. length_error from a vector resize: never cross the C ABI
+        st = MPGNN_ERR_ALLOC;
+        set_last_error(std::string("device plan build: ") + e.what());
     }
-    if (st == MPGNN_OK) st = build_rel_node_maps(p);
     (void)hipSetDevice(prev);
     if (st != MPGNN_OK) {
         free_device_plan(p);
-        if (p->d.rel_node_map) (void)hipFree(p->d.rel_node_map);
         delete p;
         return st;
     }

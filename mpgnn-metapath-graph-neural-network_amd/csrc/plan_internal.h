@@ -2,6 +2,7 @@
 // launchers (rgcn_kernels.hip). Not part of the public ABI (include/mpgnn_rgcn.h).
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <mutex>
 #include <string>
@@ -128,8 +129,9 @@ struct DeviceTables {
     int32_t* rel_seg_ptr = nullptr; // [nrel+1] segment range of each dense relation
     // mode-SINGLE node maps, one row of N per dense relation + an all-zero row (absent relation):
     // map[d·N + i] = s_src + 1 (x row) or s_src (< 0: compact mean) of node i's relation-d
-    // segment, 0 without one; built on the device at upload when (R+1)·N·4 <= 1 GiB (else the
-    // fused layer builds the relation's map per call)
+    // segment, 0 without one; built on the device at the first unsharded mode-SINGLE call when
+    // (R+1)·N·4 <= 1 GiB (else, and inside a graph capture, the layer builds the relation's map
+    // per call). Mode-ALL and sharded plans never allocate them.
     int32_t* rel_node_map = nullptr;
     void* block = nullptr;          // single hipMalloc holding every table above (but the maps)
     size_t block_bytes = 0;
@@ -204,13 +206,19 @@ struct mpgnn_plan {
     std::vector<DevTable> dev_tables;
     std::vector<void*> dev_allocs;
     std::once_flag host_once;
+    int32_t host_sync_status = MPGNN_OK;  // outcome of the once-only host copy (sync_host_tables)
+    // mode-SINGLE node maps (DeviceTables::rel_node_map): built lazily by the first unsharded
+    // fused mode-SINGLE call that is not being graph-captured; tried once per plan
+    mutable std::mutex node_map_mu;
+    mutable std::atomic<bool> node_maps_tried{false};
 };
 
 namespace mpgnn {
 
 void set_last_error(const std::string& msg);
-// rgcn_kernels.hip: allocate + fill DeviceTables::rel_node_map (synchronous; upload time)
-int32_t build_rel_node_maps(mpgnn_plan* p);
+// rgcn_kernels.hip: allocate + fill DeviceTables::rel_node_map on `stream` (synchronised before
+// return; first unsharded mode-SINGLE use of the plan, never during a graph capture)
+int32_t build_rel_node_maps(mpgnn_plan* p, void* stream);
 // plan_device.hip: copy a device-built plan's tables into its host vectors (once); free its tables
 int32_t sync_host_tables(mpgnn_plan* p);
 void free_device_plan(mpgnn_plan* p);

@@ -3513,23 +3513,25 @@ __global__ __launch_bounds__(kThreads) void rel_node_map_kernel(const int* __res
     map[(int64_t)lo * N + s_row[s]] = v >= 0 ? v + 1 : v;
 }
 
-int32_t build_rel_node_maps(mpgnn_plan* p) {
+int32_t build_rel_node_maps(mpgnn_plan* p, void* stream) {
     const size_t rows = (size_t)p->nrel + 1;  // + the all-zero row of an absent relation
     const size_t bytes = rows * (size_t)p->N * sizeof(int32_t);
     if (p->N == 0 || bytes > ((size_t)1 << 30)) return MPGNN_OK;  // per-call maps instead
+    hipStream_t strm = static_cast<hipStream_t>(stream);
     void* m = nullptr;
     if (hipMalloc(&m, bytes) != hipSuccess) {
         (void)hipGetLastError();
         return MPGNN_OK;  // not fatal: per-call maps
     }
-    int32_t st = hip_check(hipMemset(m, 0, bytes), "memset node maps");
+    int32_t st = hip_check(hipMemsetAsync(m, 0, bytes, strm), "memset node maps");
     if (st == MPGNN_OK && p->S > 0) {
         hipLaunchKernelGGL(rel_node_map_kernel, dim3((unsigned)((p->S + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                           0, p->d.rel_seg_ptr, (int)p->nrel, p->d.s_row, p->d.s_src, (int)p->S, p->N,
+                           strm, p->d.rel_seg_ptr, (int)p->nrel, p->d.s_row, p->d.s_src, (int)p->S, p->N,
                            static_cast<int*>(m));
         st = hip_check(hipGetLastError(), "rel_node_map_kernel launch");
-        if (st == MPGNN_OK) st = hip_check(hipDeviceSynchronize(), "node maps");
     }
+    // published only once complete: calls on other streams may read it right after
+    if (st == MPGNN_OK) st = hip_check(hipStreamSynchronize(strm), "node maps");
     if (st != MPGNN_OK) {
         (void)hipFree(m);
         return st;
@@ -3799,6 +3801,23 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
     }
 }
 
+int32_t mpgnn_get_option(int32_t option, int64_t* value) {
+    if (!value) return arg_error("NULL value");
+    switch (option) {
+        case MPGNN_OPT_EXACT_ORDER: *value = g_exact_order ? 1 : 0; return MPGNN_OK;
+        case MPGNN_OPT_TIMING_MASK: {
+            std::lock_guard<std::mutex> lk(g_timing_mu);
+            *value = g_timing_mask;
+            return MPGNN_OK;
+        }
+        case MPGNN_OPT_REL_GEMM: *value = g_rel_gemm ? 1 : 0; return MPGNN_OK;
+        case MPGNN_OPT_PLAN_THREADS: *value = g_plan_threads; return MPGNN_OK;
+        case MPGNN_OPT_REL_WIDE: *value = g_rel_wide ? 1 : 0; return MPGNN_OK;
+        case MPGNN_OPT_CHUNK_ROWS: *value = g_chunk_rows; return MPGNN_OK;
+        default: return arg_error("unknown option " + std::to_string(option));
+    }
+}
+
 int32_t mpgnn_rel_mean_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R,
                            const float* x, int32_t F, float* h, void* stream) {
     int32_t st = check_common(p, F, 1);
@@ -3906,6 +3925,17 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
                      p->shard_lo == 0 && p->shard_hi == p->N && p->N <= INT32_MAX - 1;
     // the relation's node map: the plan's (absent relation: its zero row), else built per call
     auto relation_node_map = [&](const int** nmap) -> int32_t {
+        if (!p->node_maps_tried) {  // first unsharded fused mode-SINGLE call: every relation's map
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            if (hipStreamIsCapturing(strm, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+                std::lock_guard<std::mutex> lk(p->node_map_mu);
+                if (!p->node_maps_tried) {
+                    const int32_t e = build_rel_node_maps(const_cast<mpgnn_plan*>(p), strm);
+                    p->node_maps_tried = true;
+                    if (e != MPGNN_OK) return e;
+                }
+            }
+        }
         if (p->d.rel_node_map != nullptr) {
             *nmap = p->d.rel_node_map + (size_t)(s.d_hi > s.d_lo ? s.d_lo : p->nrel) * (size_t)p->N;
             return MPGNN_OK;

@@ -6,7 +6,9 @@ ranges are balanced by edge count. Every rank produces a partial output for ALL 
 (normalised by the GLOBAL per-(node_1, relation) counts, kept in the plan), adds x @ root +
 bias only for rows in its own range, and one all-reduce (RCCL over xGMI with the "nccl"
 backend) per layer sums the partials. Backward: grad_x rows are local to the owner of the
-range, dW / droot / dbias are partial sums — all reduced by all-reduce.
+range — one all-gather of the owned rows (``gather_owned_rows``); dW / droot / dbias are
+partial sums — one bucketed asynchronous all-reduce per layer once all its uses have been
+accumulated (``ShardGradReducer``), overlapped with the earlier layers' backward.
 
 This replaces the reference's mpi4py object fan-out (main.py:1193-1459), which replicated the
 whole graph on every rank and parallelised only over candidate relations/metapaths.
@@ -17,7 +19,7 @@ import numpy as np
 import torch
 
 __all__ = ["shard_ranges", "edge_balanced_ranges", "rank_slice", "metapath_fanout", "best_metapaths",
-           "sharded_stack_forward"]
+           "sharded_stack_forward", "ShardGradReducer", "gather_owned_rows", "group_ranges"]
 
 
 def edge_balanced_ranges(gathered: np.ndarray | torch.Tensor, num_nodes: int, world: int) -> list[tuple[int, int]]:
@@ -97,11 +99,149 @@ def best_metapaths(scores: dict, k: int = 3) -> dict:
 # ---------------------------------------------------------------------------------------
 # inference stack with reduce-scatter between layers
 # ---------------------------------------------------------------------------------------
+_PAD_CACHE: dict = {}
+
+
 def _padded_index(ranges: list[tuple[int, int]], device) -> tuple[torch.Tensor, int]:
-    """Row i of range k goes to padded slot k·m + (i - lo_k), m = the largest range."""
+    """Row i of range k goes to padded slot k·m + (i - lo_k), m = the largest range (cached per
+    (ranges, device): the index is rebuilt and uploaded once, not per layer call)."""
+    key = (tuple(tuple(r) for r in ranges), str(device))
+    hit = _PAD_CACHE.get(key)
+    if hit is not None:
+        return hit
     m = max(hi - lo for lo, hi in ranges)
     idx = torch.cat([torch.arange(lo, hi, dtype=torch.int64) - lo + k * m for k, (lo, hi) in enumerate(ranges)])
-    return idx.to(device), m
+    _PAD_CACHE[key] = (idx.to(device), m)
+    return _PAD_CACHE[key]
+
+
+_RANGES_CACHE: dict = {}
+
+
+def group_ranges(shard: tuple[int, int], group=None) -> list[tuple[int, int]]:
+    """Every rank's shard range, gathered once per (group, own range) — a collective on first
+    use (all ranks reach it at the same layer call), cached afterwards."""
+    import torch.distributed as dist
+    key = (id(group), tuple(shard))
+    hit = _RANGES_CACHE.get(key)
+    if hit is not None:
+        return hit
+    world = dist.get_world_size(group)
+    got = [None] * world
+    dist.all_gather_object(got, (int(shard[0]), int(shard[1])), group=group)
+    _RANGES_CACHE[key] = [tuple(r) for r in got]
+    return _RANGES_CACHE[key]
+
+
+def gather_owned_rows(g: torch.Tensor, shard: tuple[int, int], group=None) -> torch.Tensor:
+    """Assemble a [N, F] tensor of which each rank holds only its own rows [lo_k, hi_k) — the
+    grad_x of a node_2-range shard (a rank's edges gather only node_2 rows of its range and its
+    root term only touches its own rows, so every other row of its partial grad_x is zero). One
+    all-gather of the padded row slabs moves N·F·4·(W-1)/W bytes per rank: half of the all-reduce
+    of the full partials it replaces."""
+    import torch.distributed as dist
+    ranges = group_ranges(shard, group)
+    world = len(ranges)
+    idx, m = _padded_index(ranges, g.device)
+    lo, hi = shard
+    f = g.shape[1]
+    slab = g.new_empty(m, f)
+    slab[:hi - lo] = g[lo:hi]  # the padding rows are never read back
+    full = g.new_empty(world * m, f)
+    dist.all_gather_into_tensor(full, slab, group=group)
+    return full.index_select(0, idx)
+
+
+class ShardGradReducer:
+    """Bucketed, overlapped all-reduce of one sharded layer's parameter gradients (SURVEY §8e:
+    "partial dW_r, droot and dbias go through an all-reduce once per step, bucketed").
+
+    The layer's ``weight`` / ``root`` / ``bias`` gradients live as views of ONE flat buffer
+    (installed as ``param.grad`` before the backward; autograd accumulates into them in place).
+    A layer applied several times per forward (``Net.conv2``, model.py:146, shared by layers
+    1..L-1) accumulates all its uses locally first: once every use has been accumulated (a
+    post-accumulate-grad hook counts them against the uses counted in the forward), ONE
+    asynchronous all-reduce of the flat buffer is issued, so it runs behind the backward of the
+    earlier layers; the end-of-backward callback makes the stream wait for it before the
+    optimizer reads the gradients. Summing the partial sums of all uses before the reduction is
+    the same linear combination as reducing each use (the reference reduces nothing: it runs on
+    one process)."""
+
+    _pending: list = []  # reducers touched by the running backward (one end-of-backward callback)
+
+    def __init__(self, params, group):
+        self.params = [p for p in params if p is not None]
+        self.group = group
+        self.flat = None
+        self.uses = 0
+        self.hits = {}
+        self.work = None
+        self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
+
+    def _install(self):
+        """Make every param.grad a view of the flat buffer (zeroed where it had no gradient)."""
+        ps = [p for p in self.params if p.requires_grad]
+        total = sum(p.numel() for p in ps)
+        dev = ps[0].device
+        if self.flat is None or self.flat.numel() != total or self.flat.device != dev:
+            self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+            views_ok = False
+        else:
+            views_ok = True
+        off = 0
+        for p in ps:
+            v = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+            g = p.grad
+            if g is not None and views_ok and g.data_ptr() == v.data_ptr():
+                continue  # already our view (zero_grad(set_to_none=False) zeroed it in place)
+            if g is None:
+                v.zero_()
+            else:
+                v.copy_(g)
+            p.grad = v
+
+    def note_use(self):
+        """Called by the layer's forward when autograd will run through it."""
+        self._install()  # no-op while param.grad is still our view
+        if self.uses == 0:
+            self.hits = {id(p): 0 for p in self.params if p.requires_grad}
+        self.uses += 1
+
+    def _launch(self):
+        import torch.distributed as dist
+        self.work = dist.all_reduce(self.flat, group=self.group, async_op=True)
+
+    def _hook(self, p):
+        if id(p) not in self.hits:
+            return
+        if not ShardGradReducer._pending:
+            torch.autograd.Variable._execution_engine.queue_callback(ShardGradReducer._finish_all)
+        if self not in ShardGradReducer._pending:
+            ShardGradReducer._pending.append(self)
+        self.hits[id(p)] += 1
+        if self.work is None and self.uses and all(h >= self.uses for h in self.hits.values()):
+            self._launch()  # every use accumulated: reduce now, behind the earlier layers' backward
+
+    @staticmethod
+    def _finish_all():
+        """End of the backward: reduce what has not been (a use count left stale by a forward
+        that was never backpropagated), then make the stream wait for every reduction (NCCL:
+        no host block) before the optimizer reads the gradients. Same order on every rank."""
+        pending, ShardGradReducer._pending = ShardGradReducer._pending, []
+        for r in pending:
+            if r.work is None:
+                r._launch()
+        for r in pending:
+            r.work.wait()
+            r.work = None
+            r.uses = 0
+            r.hits = {k: 0 for k in r.hits}
+
+    def remove(self):
+        for h in self._handles:
+            h.remove()
+        self._handles = []
 
 
 def sharded_stack_forward(convs, x: torch.Tensor, edge_index: torch.Tensor, edge_type: torch.Tensor,

@@ -11,7 +11,9 @@
 ``segment_means`` — the mean aggregation alone (bit-exact vs PyG propagate, no grad).
 
 With ``group`` set (dst-range sharding) the partial outputs of the ranks are
-summed by an all-reduce (RCCL over xGMI for the "nccl" backend) and so are the gradients.
+summed by an all-reduce (RCCL over xGMI for the "nccl" backend); grad_x of a node_2 shard is
+all-gathered from the owners of the rows, the parameter gradients are all-reduced as one bucket
+(by ``distributed.ShardGradReducer`` behind the earlier layers' backward, for nn.RGCNConv).
 """
 from __future__ import annotations
 
@@ -116,13 +118,14 @@ def _forward(x, weight, root, bias, plan: GraphPlan, mode: int, relation: int, n
 class _RGCNConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, root, bias, plan: GraphPlan, mode: int, relation: int,
-                num_relations: int, row_lo: int, row_hi: int, group, act: int):
+                num_relations: int, row_lo: int, row_hi: int, group, act: int, params_reduced: bool):
         out, x, weight, root, h_save = _forward(x, weight, root, bias, plan, mode, relation, num_relations,
                                                 row_lo, row_hi, group, ctx.needs_input_grad[1], act)
         ctx.plan = plan
         ctx.mode, ctx.relation, ctx.num_relations = mode, relation, num_relations
         ctx.rows = (row_lo, row_hi)
         ctx.group = group
+        ctx.params_reduced = params_reduced
         ctx.has_root, ctx.has_bias = root is not None, bias is not None
         ctx.act = act
         ctx.save_for_backward(x, weight, root, h_save, out if act == ACT_RELU else None)
@@ -144,9 +147,19 @@ class _RGCNConvFn(torch.autograd.Function):
         f_out = weight.shape[-1]
         nx, nw, nr, nb = ctx.needs_input_grad[:4]
         gx = torch.empty_like(x) if nx else None
-        gw = torch.empty_like(weight) if nw else None
-        gr = torch.empty_like(root) if (nr and root is not None) else None
-        gb = torch.empty(f_out, dtype=torch.float32, device=x.device) if (nb and ctx.has_bias) else None
+        want = [nw, nr and root is not None, nb and ctx.has_bias]
+        shapes = [weight.shape, root.shape if root is not None else None, (f_out,)]
+        flat = None
+        if ctx.group is not None and not ctx.params_reduced and any(want):
+            # direct functional caller with a group: dW / droot / dbias written into ONE flat
+            # buffer, reduced by one all-reduce (nn.RGCNConv hands this to ShardGradReducer)
+            sizes = [int(torch.Size(s).numel()) if w else 0 for w, s in zip(want, shapes)]
+            flat = torch.empty(sum(sizes), dtype=torch.float32, device=x.device)
+            offs = [0, sizes[0], sizes[0] + sizes[1]]
+            gw, gr, gb = (flat[o:o + n].view(s) if w else None for w, s, o, n in zip(want, shapes, offs, sizes))
+        else:
+            gw, gr, gb = (torch.empty(s, dtype=torch.float32, device=x.device) if w else None
+                          for w, s in zip(want, shapes))
         ws = _workspace(plan.workspace_bytes(ctx.mode, ctx.relation, ctx.num_relations, f_in, f_out,
                                              *ctx.rows), x.device)
         check(lib.mpgnn_rgcn_bwd(plan.handle, ctx.mode, int(ctx.relation), int(ctx.num_relations),
@@ -154,19 +167,27 @@ class _RGCNConvFn(torch.autograd.Function):
                                  grad_out.data_ptr(), ctx.rows[0], ctx.rows[1], _ptr(gx), _ptr(gw),
                                  _ptr(gr), _ptr(gb), ws.data_ptr(), _stream(x)), "mpgnn_rgcn_bwd")
         if ctx.group is not None:
-            for g in (gx, gw, gr, gb):
-                if g is not None:
-                    dist.all_reduce(g, group=ctx.group)
-        return gx, gw, gr, gb, None, None, None, None, None, None, None, None
+            if gx is not None:
+                if plan.shard_side == "gathered":
+                    # non-zero only on this rank's node_2 rows: all-gather them (half the bytes)
+                    from .distributed import gather_owned_rows
+                    gx = gather_owned_rows(gx, plan.shard, ctx.group)
+                else:  # node_1 shards gather from every row: partial sums everywhere
+                    dist.all_reduce(gx, group=ctx.group)
+            if flat is not None:
+                dist.all_reduce(flat, group=ctx.group)
+        return gx, gw, gr, gb, None, None, None, None, None, None, None, None, None
 
 
 def rgcn_conv(x: torch.Tensor, weight: torch.Tensor, root, bias, plan: GraphPlan, mode: int,
               relation: int = -1, num_relations: int = 0, row_range=None, group=None,
-              activation=None) -> torch.Tensor:
+              activation=None, params_reduced: bool = False) -> torch.Tensor:
     """One relational conv layer on the GPU (see module docstring).
 
     ``activation='relu'`` returns ``F.relu(layer(x))`` (model.py:144,146): fused into the
-    combine epilogue when the layer is unsharded, applied after the all-reduce otherwise."""
+    combine epilogue when the layer is unsharded, applied after the all-reduce otherwise.
+    ``params_reduced``: with a ``group``, the caller reduces the parameter gradients itself
+    (``distributed.ShardGradReducer``); otherwise the backward all-reduces them (one bucket)."""
     if activation not in (None, "relu"):
         raise ValueError(f"activation must be None or 'relu', got {activation!r}")
     lo, hi = row_range if row_range is not None else (0, plan.num_nodes)
@@ -181,7 +202,7 @@ def rgcn_conv(x: torch.Tensor, weight: torch.Tensor, root, bias, plan: GraphPlan
                        int(lo), int(hi), group, False, act)[0]
     else:
         out = _RGCNConvFn.apply(x, weight, root, bias, plan, int(mode), int(relation),
-                                int(num_relations), int(lo), int(hi), group, act)
+                                int(num_relations), int(lo), int(hi), group, act, bool(params_reduced))
     if activation == "relu" and not fuse:
         out = torch.relu(out)
     return out

@@ -92,9 +92,23 @@ class RGCNConv(torch.nn.Module):
         plan = get_plan(edge_index, edge_type, x.size(0), flow=self.flow, shard=shard, device=x.device,
                         shard_side=shard_side)
         row_range = shard if shard is not None else None
+        reduced = False
+        if group is not None and torch.is_grad_enabled() and \
+                any(p is not None and p.requires_grad for p in (self.weight, self.root, self.bias)):
+            # partial dW / droot / dbias: one bucketed async all-reduce once every use of this
+            # layer in the step has been accumulated (Net shares conv2 across layers 1..L-1)
+            red = self.__dict__.get("_grad_reducer")
+            if red is None or red.group is not group:
+                if red is not None:
+                    red.remove()
+                from .distributed import ShardGradReducer
+                red = ShardGradReducer((self.weight, self.root, self.bias), group)
+                self.__dict__["_grad_reducer"] = red
+            red.note_use()
+            reduced = True
         return rgcn_conv(x, self.weight, self.root, self.bias, plan, MODE_ALL,
                          num_relations=self.num_relations, row_range=row_range, group=group,
-                         activation=activation)
+                         activation=activation, params_reduced=reduced)
 
     def __repr__(self) -> str:
         return (f"{self.__class__.__name__}({self.in_channels}, "

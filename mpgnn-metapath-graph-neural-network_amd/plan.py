@@ -27,11 +27,14 @@ class GraphPlan:
 
     def __init__(self, edge_index: torch.Tensor, edge_type: torch.Tensor, num_nodes: int,
                  shard: tuple[int, int] | None = None, flow: str = "target_to_source",
-                 shard_side: str = "gathered", build: str = "auto"):
+                 shard_side: str = "gathered", build: str = "auto", device=None):
         """build: "host" (csrc/plan.cpp, multi-threaded counting sorts), "device" (csrc/
-        plan_device.hip, radix sorts on the GPU holding the graph; the plan is then resident on
-        that device) or "auto" = "device" when edge_index is a CUDA tensor (MPGNN_PLAN_BUILD=host
-        forces the host build). Both give bit-identical tables."""
+        plan_device.hip, radix sorts on the GPU; the plan is then resident on that device) or
+        "auto" = "device" when edge_index is a CUDA tensor (MPGNN_PLAN_BUILD=host forces the host
+        build). Both give bit-identical tables. ``device``: the GPU the plan must live on (the
+        features' device; default: edge_index's) — the edge tensors are copied there for the
+        build. If the device build runs out of memory outside PyTorch's caching allocator
+        ("auto" only), the plan is built on the host and uploaded instead."""
         if flow not in FLOWS:
             raise ValueError(f"Expected 'flow' to be either {FLOWS} (got '{flow}')")
         if edge_index.dim() != 2 or edge_index.size(0) != 2:
@@ -44,7 +47,12 @@ class GraphPlan:
                                           and os.environ.get("MPGNN_PLAN_BUILD", "") != "host")
         dev = None
         if on_device:
-            dev = edge_index.device if edge_index.is_cuda else torch.device("cuda", torch.cuda.current_device())
+            if device is not None and torch.device(device).type == "cuda":
+                dev = torch.device(device)
+                if dev.index is None:
+                    dev = torch.device("cuda", torch.cuda.current_device())
+            else:
+                dev = edge_index.device if edge_index.is_cuda else torch.device("cuda", torch.cuda.current_device())
         ei = edge_index.detach().to(dev if on_device else "cpu", torch.int64)
         if flow == "source_to_target":  # aggregate into edge_index[1]: swap the roles
             ei = ei.flip(0)
@@ -61,15 +69,21 @@ class GraphPlan:
         self._device = None
         if on_device:
             # returns after the build has finished on the stream: ei / et may be freed after it
-            check(lib.mpgnn_plan_create_device(ei.data_ptr() if ei.numel() else None,
-                                               et.data_ptr() if et.numel() else None,
-                                               et.numel(), self.num_nodes, self.shard[0], self.shard[1],
-                                               _lib.SHARD_SIDES[shard_side], dev.index,
-                                               ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream),
-                                               ctypes.byref(handle)),
-                  "mpgnn_plan_create_device")
-            self._device = dev.index
-        else:
+            st = lib.mpgnn_plan_create_device(ei.data_ptr() if ei.numel() else None,
+                                              et.data_ptr() if et.numel() else None,
+                                              et.numel(), self.num_nodes, self.shard[0], self.shard[1],
+                                              _lib.SHARD_SIDES[shard_side], dev.index,
+                                              ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream),
+                                              ctypes.byref(handle))
+            if st == _lib.MPGNN_ERR_ALLOC and build == "auto":
+                # the builder's scratch is raw hipMalloc: with PyTorch's cache holding the device,
+                # fall back to the host build (uploaded below by to_device)
+                on_device = False
+                ei, et = ei.cpu(), et.cpu()
+            else:
+                check(st, "mpgnn_plan_create_device")
+                self._device = dev.index
+        if not on_device:
             check(lib.mpgnn_plan_create_sharded(ei.data_ptr() if ei.numel() else None,
                                                 et.data_ptr() if et.numel() else None,
                                                 et.numel(), self.num_nodes, self.shard[0], self.shard[1],
@@ -195,7 +209,8 @@ class _PlanCache:
                     self._d.move_to_end(key)
                     return plan.to_device(device) if device is not None else plan
                 del self._d[key]
-        plan = GraphPlan(edge_index, edge_type, num_nodes, shard=shard, flow=flow, shard_side=shard_side)
+        plan = GraphPlan(edge_index, edge_type, num_nodes, shard=shard, flow=flow, shard_side=shard_side,
+                         device=device)
         if device is not None:
             plan.to_device(device)
         with self._lock:

@@ -28,6 +28,26 @@ def pytest_sessionfinish(session, exitstatus):
     _parity_report.dump()
 
 
+_OPTIONS = (0, 3, 5, 11, 19, 20)  # enum mpgnn_option switches a test may override
+_DEFAULTS: dict = {}
+
+
+@pytest.fixture(autouse=True)
+def _restore_library_options():
+    """Every test starts from the SHIPPED option values (read once, before any test changed
+    them) and a test that overrides one cannot leak it into the rest of the session."""
+    from mpgnn_amd import _lib
+    if not _DEFAULTS:
+        for o in _OPTIONS:
+            try:
+                _DEFAULTS[o] = _lib.get_option(o)
+            except (NotImplementedError, RuntimeError):  # host-only sanitizer library: no kernel options
+                pass
+    yield
+    for o, v in _DEFAULTS.items():
+        _lib.set_option(o, v)
+
+
 @pytest.fixture(scope="session")
 def golden():
     import numpy as np

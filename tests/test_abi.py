@@ -78,8 +78,13 @@ def test_withdrawn_option_is_refused():
     for opt in (1, 2, 4, 6, 7, 8, 9, 10, 12, 13, 14, 15, 16, 17, 18, 21, 22, 23):
         assert lib.mpgnn_set_option(opt, 0) == _lib.MPGNN_ERR_ARG
         assert b"withdrawn" in lib.mpgnn_last_error()
-    assert lib.mpgnn_set_option(20, 192) == 0
+    shipped = _lib.get_option(20)
+    assert shipped == 256  # the header's documented default chunk length
+    assert lib.mpgnn_set_option(20, 192) == 0 and _lib.get_option(20) == 192
+    assert lib.mpgnn_set_option(20, shipped) == 0
     assert lib.mpgnn_set_option(11, 0) == 0
+    with pytest.raises(ValueError):
+        _lib.get_option(1)
 
 
 def test_workspace_bytes_is_host_computable():

@@ -100,6 +100,95 @@ def test_dst_sharded_allreduce_matches_unsharded(name):
 
 
 # ------------------------------------------------------------------------------------------
+# training-path communication: bucketed async gradient all-reduce + owned-row all-gather
+# ------------------------------------------------------------------------------------------
+def _reducer_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.set_num_threads(1)
+        from mpgnn_amd.distributed import ShardGradReducer, gather_owned_rows, shard_ranges
+        msgs = []
+        gen = torch.Generator().manual_seed(5)
+        F = 6
+        W0, r0, b0 = torch.randn(3, F, F, generator=gen), torch.randn(F, F, generator=gen), torch.randn(F, generator=gen)
+        xs = [torch.randn(10, F, generator=gen) for _ in range(world)]  # rank k's partial input
+
+        class Layer(torch.nn.Module):  # a sharded layer: a partial result per rank
+            def __init__(self, reduce):
+                super().__init__()
+                self.weight = torch.nn.Parameter(W0.clone())
+                self.root = torch.nn.Parameter(r0.clone())
+                self.bias = torch.nn.Parameter(b0.clone())
+                self.red = ShardGradReducer((self.weight, self.root, self.bias), dist.group.WORLD) if reduce else None
+
+            def forward(self, h):
+                if self.red is not None and torch.is_grad_enabled():
+                    self.red.note_use()
+                return torch.tanh(h @ self.weight.sum(0) + h @ self.root * (rank + 1) + self.bias)
+
+        def run(layer, iters, stale=False, set_to_none=True):
+            grads = []
+            for it in range(iters):
+                layer.zero_grad(set_to_none=set_to_none)
+                if stale and it == 0:
+                    layer(xs[rank])  # grad-enabled forward never backpropagated (stale use count)
+                out = layer(layer(xs[rank]))  # two uses per step (Net.conv2 is shared, model.py:146)
+                (out * (it + 1)).sum().backward()
+                grads.append([p.grad.clone() for p in (layer.weight, layer.root, layer.bias)])
+            return grads
+
+        plain = run(Layer(False), 2)
+        for gs in plain:  # expected: the sum over ranks of the local gradients
+            for g_ in gs:
+                dist.all_reduce(g_)
+        for name, kw in (("set_to_none", {}), ("zero_in_place", {"set_to_none": False}),
+                         ("stale_use", {"stale": True})):
+            got = run(Layer(True), 2, **kw)
+            for it, (a, b) in enumerate(zip(got, plain)):
+                for pa, pb, pn in zip(a, b, ("weight", "root", "bias")):
+                    if not torch.allclose(pa, pb, rtol=1e-6, atol=1e-6):
+                        msgs.append(f"{name} iter {it} {pn}: {float((pa - pb).abs().max()):.3e}")
+        # all-gather of owned rows: rank k contributes rows [lo_k, hi_k) only
+        ei = torch.randint(0, 37, (2, 300), generator=torch.Generator().manual_seed(2))
+        ranges = shard_ranges(ei, 37, world)
+        full = torch.randn(37, 4, generator=torch.Generator().manual_seed(3))
+        mine = torch.full_like(full, float("nan"))
+        lo, hi = ranges[rank]
+        mine[lo:hi] = full[lo:hi]
+        got = gather_owned_rows(mine, ranges[rank], dist.group.WORLD)
+        if not torch.equal(got, full):
+            msgs.append("gather_owned_rows differs")
+        q.put((rank, not msgs, msgs))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, False, [traceback.format_exc()]))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_grad_reducer_and_owned_row_gather(world):
+    """ShardGradReducer: parameter gradients of a layer used twice per step end up as the sum
+    over ranks of the local gradients (one async all-reduce per layer), across zero_grad styles
+    and after a forward that was never backpropagated; gather_owned_rows assembles the owners'
+    rows exactly."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reducer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, msgs in res:
+        assert ok, (rank, msgs)
+
+
+# ------------------------------------------------------------------------------------------
 # metapath-candidate fan-out (SURVEY §8f #3, main.py:1430-1452): replicas only
 # ------------------------------------------------------------------------------------------
 def _fake_train(data, input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, metapaths, **kw):

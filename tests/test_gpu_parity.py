@@ -773,14 +773,17 @@ def test_chunk_rows_option_moves_only_slab_boundaries(mode):
         return [t.grad.clone() for t in [xg] + ps]
 
     r32, r64 = oracle_layer2(g.x, g.edge_index, g.edge_type, W, root, bias, gout.cpu(), mode=mode, rel=3)
+    shipped = _lib.get_option(20)
+    assert shipped == 256
     try:
-        for rows in (192, 64, 512):
-            _lib.check(_lib.lib.mpgnn_set_option(20, rows))
+        for rows in (shipped, 192, 64, 512):  # the shipped default first
+            _lib.set_option(20, rows)
             plan_cache.clear()
             got = run()
             close_all(dict(zip(("dx", "dW", "droot", "dbias"), got)), r32, r64, f"chunk rows {rows} ")
     finally:
-        _lib.lib.mpgnn_set_option(20, 192)
+        _lib.set_option(20, shipped)
+        plan_cache.clear()
 
 
 @pytest.mark.parametrize("name,mode,rel", [("C1", MODE_ALL, -1), ("C1", MODE_SINGLE, 1), ("fb15k237", MODE_ALL, -1),

@@ -102,16 +102,18 @@ def test_tsv_reader_edge_cases(tmp_path):
     p = str(tmp_path / "n.dat")
     _write(p, "")
     assert data.read_tsv_numeric(p).shape == (0, 0)
-    # ragged rows pad with NaN (pandas read_csv), floats / exponents / signs, CRLF, blank lines
-    _write(p, "0\t1.5\t-2e3\r\n\n1\t+4\n2 0.25 7\t\n")
+    # ragged rows pad with NaN (pandas read_csv), floats / exponents / signs, CRLF, blank lines,
+    # an empty middle field and a trailing tab (NaN fields in place: the split is on single tabs,
+    # as read_csv(sep='\t') of main.py:140-147 cuts them), spaces around a number
+    _write(p, "0\t1.5\t-2e3\t\r\n\n1\t\t+4\n2\t 0.25 \t7\t\n")
     a = data.read_tsv_numeric(p)
-    assert a.shape == (3, 3)
-    assert np.array_equal(a[:, :2], [[0, 1.5], [1, 4], [2, 0.25]])
-    assert a[0, 2] == -2000 and np.isnan(a[1, 2]) and a[2, 2] == 7
+    assert a.shape == (3, 4)
+    assert a[0, 2] == -2000 and np.isnan(a[1, 1]) and a[1, 2] == 4 and a[2, 1] == 0.25 and a[2, 2] == 7
+    assert np.isnan(a[:, 3]).all()
     import pandas as pd
-    ref = pd.read_csv(p, sep=r"\s+", header=None).to_numpy(dtype=np.float64)
+    ref = pd.read_csv(p, sep="\t", header=None).to_numpy(dtype=np.float64)
     assert np.array_equal(np.isnan(a), np.isnan(ref)) and np.array_equal(np.nan_to_num(a), np.nan_to_num(ref))
-    for bad in ("0\tred\n", "1\t2x\n"):
+    for bad in ("0\tred\n", "1\t2x\n", "1\t2 3\n"):  # a space never separates fields
         _write(p, bad)
         with pytest.raises(ValueError):
             data.read_tsv_numeric(p)

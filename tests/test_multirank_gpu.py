@@ -90,22 +90,131 @@ def _worker(rank, world, port, side, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("side", ["gathered", "rows"])
-def test_two_rank_training_path_matches_unsharded(side):
+def _run_ranks(target, world, *args, timeout=240):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, side, q)) for r in range(2)]
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
     for p in procs:
         p.start()
-    results = [q.get(timeout=240) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
+    try:
+        results = [q.get(timeout=timeout) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return sorted(results, key=lambda r: r[0])
+
+
+@pytest.mark.parametrize("side", ["gathered", "rows"])
+def test_two_rank_training_path_matches_unsharded(side):
+    results = _run_ranks(_worker, 2, side)
     for rank, errs, tb in results:
         assert tb is None, f"rank {rank}:\n{tb}"
         for name, (e, e_sh64, e_un64) in errs.items():
             # cross-rank partial sums change the fp32 summation order (SURVEY 8e parity: 1e-4
             # elementwise, decided against the float64 truth where the two fp32 orders differ)
             assert e <= 1e-4 or e_sh64 <= max(1e-4, 2 * e_un64), (side, rank, name, e, e_sh64, e_un64)
+
+
+# ------------------------------------------------------------------------------------------
+# the path `bench.py --gpus N` times: sharded_stack_forward with the HIP RGCNConv layers on C3
+# ------------------------------------------------------------------------------------------
+def _stack_worker(rank, world, port, side, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import mpgnn_amd
+        from mpgnn_amd import data
+        from mpgnn_amd.distributed import shard_ranges, sharded_stack_forward
+        from tests.test_gpu_parity import max_rel_err, kink_act
+        from oracle import rgcn_oracle as orc
+        dev = torch.device("cuda", 0)
+        g = data.fb15k237_graph(feat_dim=128, seed=0, recipe="survey")  # C3, bench.py's headline graph
+        x, ei, et = g.x.to(dev), g.edge_index.to(dev), g.edge_type.to(dev)
+        torch.manual_seed(10)
+        net = mpgnn_amd.Net(128, 128, g.num_relations, 128, 2, 3).to(dev)
+        with torch.no_grad():
+            for c in (net.conv1, net.conv2):
+                c.bias.uniform_(-0.3, 0.3)
+        convs = [net.conv1, net.conv2, net.conv2]
+        ranges = shard_ranges(g.edge_index, g.num_nodes, world, side=side)
+        with torch.no_grad():
+            out = sharded_stack_forward(convs, x, ei, et, ranges, dist.group.WORLD, shard_side=side)
+            h, acts = x, []
+            for c in convs:
+                h = c(h, ei, et, activation="relu")
+                acts.append(h)
+            torch.cuda.synchronize()
+        e = max_rel_err(out, h)
+        norm = float((out - h).double().norm() / h.double().norm())
+        e_sh64 = e_un64 = None
+        if rank == 0 and e > 1e-4:
+            # float64 truth: the CPU oracle's loop in float64, ReLU following the unsharded GPU
+            # mask at kinks (only needed when the two fp32 orders differ beyond the bar)
+            act = kink_act(acts)
+            t64 = g.x.double()
+            with torch.no_grad():
+                for k, c in enumerate(convs):
+                    t64 = act(k, orc.rgcn_forward(t64, g.edge_index, g.edge_type, c.weight.detach().cpu().double(),
+                                                  c.root.detach().cpu().double(), c.bias.detach().cpu().double()))
+            e_sh64, e_un64 = max_rel_err(out, t64), max_rel_err(h, t64)
+        q.put((rank, (e, e_sh64, e_un64, norm), None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # report to the parent, never hang it
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("side", ["gathered", "rows"])
+def test_two_rank_sharded_stack_c3_matches_unsharded(side):
+    """bench.py --gpus N's timed step (distributed.sharded_stack_forward: per-layer reduce-scatter
+    of partial sums, or all-gather of rows) with the real HIP RGCNConv layers on the C3 graph,
+    against the unsharded 3-layer stack at the suite's elementwise bar."""
+    for rank, errs, tb in _run_ranks(_stack_worker, 2, side, timeout=400):
+        assert tb is None, f"rank {rank}:\n{tb}"
+        e, e_sh64, e_un64, norm = errs
+        assert norm <= 1e-5, (side, rank, norm)  # normwise ||sharded - unsharded|| / ||unsharded||
+        if rank == 0:
+            assert e <= 1e-4 or e_sh64 <= max(1e-4, 2 * e_un64), (side, rank, e, e_sh64, e_un64)
+
+
+def _bench_worker(rank, world, port, q):
+    import contextlib
+    import io
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    try:
+        os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                           "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world), "MPGNN_BENCH_REHEARSE": "1"})
+        sys.argv = ["bench.py", "--gpus", str(world), "--steps", "3", "--warmup", "1", "--epoch-steps", "2",
+                    "--no-cpu-baseline"]
+        import bench
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            bench.main()
+        lines = [ln for ln in buf.getvalue().splitlines() if ln.startswith("{")]
+        q.put((rank, [json.loads(ln) for ln in lines], None))
+    except BaseException:  # SystemExit included
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_bench_two_rank_rehearsal_prints_one_line():
+    """bench.main() under the N = 2 launch (env RANK / WORLD_SIZE, both ranks on the one GPU over
+    gloo): rank 0 prints exactly one parseable JSON line with n_gpus 2, rank 1 prints none."""
+    res = _run_ranks(_bench_worker, 2, timeout=600)
+    for rank, lines, tb in res:
+        assert tb is None, f"rank {rank}:\n{tb}"
+    assert len(res[0][1]) == 1 and res[1][1] == [], res
+    line = res[0][1][0]
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["epoch_ms"] > 0, line
+    assert line["config"]["shard_side"] == "gathered" and line["scaling"] == "strong"
