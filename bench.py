@@ -77,8 +77,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="fb15k237", choices=list(WORKLOADS))
-    ap.add_argument("--mode", default="all", choices=["all", "single"],
-                    help="all = RGCN Net (mode B, main_rgcn.py); single = MPNetm metapath chain (mode A, main.py)")
+    ap.add_argument("--mode", default="all", choices=["all", "single", "score"],
+                    help="all = RGCN Net (mode B, main_rgcn.py); single = MPNetm metapath chain (mode A, main.py); "
+                         "score = the metapath score function (model.py:26-125, main.py:727-760)")
+    ap.add_argument("--relation", type=int, default=None, help="mode score: relation scored (default: the largest)")
     ap.add_argument("--metapath", default=None,
                     help="mode single: comma-separated relations, one per layer (default C2 '1,0', C5 '2,1,0', "
                          "FB15K the three most frequent relations)")
@@ -320,6 +322,130 @@ def time_drop_in_loop(single, g, x, ei, et, F, layers, metapath, epochs, shard_k
             "note": "(t(1+K) - t(1)) / K of the drop-in loop call, host syncs included; synthetic 2-class labels"}
 
 
+def bench_score(args):
+    """Mode score: the metapath score function of the reference's search loop —
+    ``score_relation_parallel`` (main.py:727-760): edge dictionary of one relation, then 100
+    epochs of train() (model.py:74-89 forward = per-source argmax of the destination weights,
+    MSE, backward, Adam, clamp). One STEP = one train() epoch of the drop-in (GPU kernels
+    mpgnn_score_argmax / _bwd + torch's MSE / fused Adam / clamp). value = edges scored per
+    second = E_r · steps / time (every edge of the relation whose source is in the mask is read
+    once per epoch by the argmax). Single GPU (candidate relations are independent: replicas).
+    roofline: mpgnn_score_argmax (memset + kernel) per launch, HIP events on the launch stream,
+    against HBM with its algorithmic bytes. cpu_baseline: the oracle's reference-style loop
+    (oracle/score_oracle.py, the Python dict loop of model.py:82-87) on a bounded number of epochs."""
+    import random as _random
+    from mpgnn_amd import score as sc
+    rank, world, local, group = setup_dist(args.gpus)
+    if world > 1:
+        raise SystemExit("--mode score shards nothing (candidate relations are replicas)")
+    dev = torch.device("cuda", local)
+    if args.workload.startswith("fb15k237"):
+        g = data.fb15k237_graph(feat_dim=4, seed=0, recipe="relcond" if args.workload == "fb15k237_relcond" else "survey")
+    else:
+        g = data.config_graph(args.workload)
+    N = g.num_nodes
+    counts = torch.bincount(g.edge_type, minlength=g.num_relations)
+    rel = int(torch.argmax(counts)) if args.relation is None else int(args.relation)
+    y = torch.randint(0, 2, (N,), generator=torch.Generator().manual_seed(0))
+
+    class D:
+        pass
+    d = D()
+    d.x = torch.zeros(N, 2)
+    d.edge_index, d.edge_type, d.num_nodes = g.edge_index.to(dev), g.edge_type.to(dev), N
+    d.labels = y.unsqueeze(-1)
+    mask = torch.unique(g.edge_index[0][g.edge_type == rel]).tolist()  # first-iteration mask (main.py:734-735)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ed, dd = sc.create_edge_dictionary(d, rel, mask, BAGS=False, dataset="synthetic")
+    _random.seed(0)
+    w0 = sc.initialize_weights(d, dd, BAGS=False)
+    torch.manual_seed(77)
+    model = sc.get_model(w0, 2).to(dev)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t0
+    opt = sc.get_optimizer(model)
+    crit, crit_node = sc.get_loss(), sc.get_loss_per_node()
+    E_r = ed.num_entries
+
+    def step():
+        return sc.train(d, ed, model, opt, crit, mask, crit_node, [], w0, None, BAGS=False, dataset="synthetic")
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()[0]
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = elapsed * 1e3 / args.steps
+    # the argmax kernel alone, HIP events on the launch stream (torch's current stream)
+    w = model.input.weights.detach()
+    reps = 200
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.no_grad():
+        for _ in range(5):
+            sc.score_argmax(w, ed)
+        ev0.record()
+        for _ in range(reps):
+            sc.score_argmax(w, ed)
+        ev1.record()
+    torch.cuda.synchronize()
+    k_us = ev0.elapsed_time(ev1) * 1e3 / reps
+    K = len(ed)
+    alg = E_r * 8.0 + K * (4 + 8 + 12) + N * 4.0
+    roofline = {"bound": "hbm", "achieved": round(alg / (k_us * 1e-6) / 1e9, 2), "peak": PEAK_HBM, "unit": "GB/s",
+                "frac": round(alg / (k_us * 1e-6) / 1e9 / PEAK_HBM, 5), "traffic": None,
+                "kernel": "score_argmax_kernel (+ max_weights memset)", "avg_launch_us": round(k_us, 3),
+                "algorithmic": "E_r·(4 dst id + 4 weight) + K·(4 key + 8 ptr + 12 outputs) + N·4 max_weights",
+                "note": "tiny launch (K sources, E_r edges): bound by launch latency, not HBM"}
+    # the whole score_relation_parallel (dictionary build + weights + 100 epochs + final loss.item)
+    _random.seed(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sc.score_relation_parallel(d, rel, [], 2, "synthetic")
+    srp_s = time.perf_counter() - t0
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import score_oracle as so
+        with _cpu_threads():
+            ei_c, et_c = g.edge_index, g.edge_type
+            ed_o, dd_o = so.create_edge_dictionary(ei_c, et_c, rel, mask, d.labels, "synthetic")
+            w_o = so.initialize_weights(N, dd_o, _random.Random(0))
+            torch.manual_seed(77)
+            m_o = so.Score(w_o, "synthetic", 2)
+            o_o = torch.optim.Adam(m_o.parameters(), lr=0.1)
+            so.train(m_o, o_o, ed_o, N, d.labels, mask, "synthetic")  # warm-up
+            times = []
+            for _ in range(max(2, min(args.cpu_reps, 5))):
+                t1 = time.perf_counter()
+                so.train(m_o, o_o, ed_o, N, d.labels, mask, "synthetic")
+                times.append(time.perf_counter() - t1)
+        med = _median(times)
+        cpu = {"value": E_r / med, "unit": "edges/s", "cores": usable_cpus()[0], "kind": "port", **host_info(),
+               "sample": f"{len(times)} epochs (after 1 warm-up) of the oracle's reference-style train() "
+                         f"(oracle/score_oracle.py: the per-source Python loop of model.py:82-87, MSE, Adam, clamp), "
+                         f"relation {rel} ({E_r} edges, {K} sources); median {med * 1e3:.1f} ms per epoch"}
+    result = {
+        "metric": "score-function edges scored/sec (main.py:727-760 epochs)", "value": round(E_r * args.steps / elapsed, 1),
+        "unit": "edges/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": WORKLOADS[args.workload][1].split(",")[0] + "; 2-class synthetic labels, seed-0 random weights",
+        "config": {"workload": f"{WORKLOADS[args.workload][0]}: score function, relation {rel} (the largest), "
+                               f"first-iteration mask (all {K} sources)", "mode": "score",
+                   "graph": {"nodes": N, "edges_relation": E_r, "sources": K}},
+        "epoch_def": "one train() of main.py:641-673 (non-bag): argmax forward, MSE, backward, Adam(lr 0.1), clamp",
+        "score_relation_parallel_s": round(srp_s, 4),
+        "setup_s": round(setup_s, 4),
+        "final_loss": round(float(loss.item()), 6),
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(result), flush=True)
+    return result
+
+
 def pmc_traffic(workload, mode, feat, kernel_prefix):
     """HBM bytes per launch of `kernel_prefix` from the committed PMC summary, or None."""
     path = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
@@ -336,6 +462,8 @@ def pmc_traffic(workload, mode, feat, kernel_prefix):
 
 def main():
     args = parse()
+    if args.mode == "score":
+        return bench_score(args)
     rank, world, local, group = setup_dist(args.gpus)
     dev = torch.device("cuda", local)
     if args.workload.startswith("fb15k237"):

@@ -256,6 +256,30 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
                        float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
                        void* workspace, void* stream);
 
+/* --- score function --------------------------------------------------------
+ * The metapath-candidate score of the reference, OutputLayer.forward non-bag branch
+ * (model.py:74-89) as trained by train() / score_relation_parallel (main.py:641-673, 727-760).
+ * The edge dictionary of one relation (create_edge_dictionary, main.py:387-424) is a CSR in
+ * dictionary order: source keys[k] (int32 node ids, k = 0..num_keys-1, mask order), its
+ * destinations dst[key_ptr[k] .. key_ptr[k+1]) in edge-file order (every key has >= 1).
+ * All pointers are DEVICE pointers; weights / max_weights / grad_* are fp32 [num_nodes].
+ *
+ * mpgnn_score_argmax: max_weights = 0, then for every key k: arg_pos[k] = the position p of the
+ * FIRST maximum of weights[dst[p]] (torch.argmax: NaN counts as the maximum), max_node[k] =
+ * dst[arg_pos[k]], max_weights[keys[k]] = weights[max_node[k]] (bit-identical to model.py:85-87).
+ * Replaces the per-source Python loop of model.py:82-87. */
+int32_t mpgnn_score_argmax(const float* weights, int64_t num_nodes, const int32_t* keys, const int32_t* key_ptr,
+                           const int32_t* dst, int64_t num_keys, float* max_weights, int32_t* arg_pos,
+                           int32_t* max_node, void* stream);
+/* Backward of mpgnn_score_argmax (autograd of model.py:87 `max_weights[source] = weights[max_node]`):
+ * grad_weights[n] = Σ grad_max[keys[k]] over the keys whose argmax edge points at n, added in
+ * DESCENDING k (the order autograd unwinds the reference's CopySlices chain), 0 where none.
+ * (in_ptr [num_nodes+1], in_pos, in_key) list, per destination node n, every (edge position p,
+ * key k) of the dictionary with dst[p] == n, sorted by k descending — built once per dictionary. */
+int32_t mpgnn_score_argmax_bwd(const float* grad_max, int64_t num_nodes, const int32_t* keys, const int32_t* arg_pos,
+                               const int32_t* in_ptr, const int32_t* in_pos, const int32_t* in_key,
+                               float* grad_weights, void* stream);
+
 /* --- options ----------------------------------------------------------------------------
  * MPGNN_OPT_EXACT_ORDER = 1: every gather-sum adds its entries strictly in the reference's
  * sequential order (no ordered-piece split of long runs). Default 0: runs longer than 32

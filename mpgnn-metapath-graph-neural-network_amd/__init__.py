@@ -8,6 +8,8 @@ francescoferrini/MPGNN-Metapath-Graph-Neural-Network.
   plan.GraphPlan                 one-time sorted segment tables of a graph (cached)
   data, distributed              graph inputs (C1-C5, native link.dat reader) and dst-range sharding
   main, main_rgcn, metrics       training / evaluation loops of main.py and main_rgcn.py
+  score.Score / score_relation_parallel   the metapath score function (model.py:26-125,
+                                 main.py:387-760) on the GPU: segment argmax kernels
 
 The directory name is not a Python identifier; import it as ``mpgnn_amd`` (repo-root shim).
 """
@@ -17,6 +19,7 @@ from .model import MPNetm, Net
 from .mp_rgcn_layer import CustomRGCNConv, masked_edge_index
 from .nn import CustomFastRGCNConv, FastRGCNConv, RGCNConv
 from . import data, distributed, metrics  # noqa: E402
+from . import score  # noqa: E402  (score function, model.py:26-125 / main.py:387-760)
 from . import main, main_rgcn  # noqa: E402  (training-loop drop-ins, main.py / main_rgcn.py)
 from .plan import GraphPlan, get_plan, plan_cache
 

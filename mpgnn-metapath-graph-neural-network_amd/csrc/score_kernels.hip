@@ -1,0 +1,123 @@
+// score_kernels.hip — gfx950 kernels of the metapath score function.
+//
+// Reference: OutputLayer.forward, non-bag branch (model.py:74-89), driven by train()
+// (main.py:641-673) inside score_relation_parallel (main.py:727-760), 100 epochs per candidate
+// relation. For every source node of the edge dictionary (create_edge_dictionary,
+// main.py:387-424: {source: [destinations of one relation]}) the reference runs a Python loop:
+//     max_node = dsts[torch.argmax(weights[dsts])];  max_weights[source] = weights[max_node]
+// and autograd sends d max_weights[source] back to weights[max_node], the contributions of the
+// sources accumulated in REVERSE dictionary order (the CopySlices chain is unwound last source
+// first). Here the dictionary is a CSR in dictionary order (keys, key_ptr, dst) and one thread
+// scans one source's destinations; the backward walks, per destination node, a static list of
+// the (source, edge) pairs that can select it, sorted by source rank descending, and adds the
+// gradient of each pair that IS its source's argmax — the reference's order, no atomics.
+//
+// Both kernels move a few bytes per edge (index + weight gather) and are latency / HBM bound;
+// they replace O(E) Python-level tensor ops per epoch.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "plan_internal.h"
+
+namespace mpgnn {
+namespace {
+
+constexpr int kScoreThreads = 256;
+
+int32_t hip_status(hipError_t e, const char* what) {
+    if (e == hipSuccess) return MPGNN_OK;
+    set_last_error(std::string(what) + ": " + hipGetErrorString(e));
+    return MPGNN_ERR_HIP;
+}
+
+int32_t arg_fail(const char* msg) {
+    set_last_error(msg);
+    return MPGNN_ERR_ARG;
+}
+
+// torch.argmax over a float vector (ATen's reduction): the first index of the maximum, a NaN
+// counting as larger than every number (the first NaN wins).
+__device__ __forceinline__ bool takes_over(float best, float v) {
+    return !__builtin_isnan(best) && (__builtin_isnan(v) || v > best);
+}
+
+__global__ __launch_bounds__(kScoreThreads) void score_argmax_kernel(
+        const float* __restrict__ w, const int32_t* __restrict__ keys, const int32_t* __restrict__ key_ptr,
+        const int32_t* __restrict__ dst, int32_t K, float* __restrict__ max_w, int32_t* __restrict__ arg_pos,
+        int32_t* __restrict__ max_node) {
+    const int32_t k = (int32_t)(blockIdx.x * kScoreThreads + threadIdx.x);
+    if (k >= K) return;
+    const int32_t b = key_ptr[k], e = key_ptr[k + 1];
+    int32_t bp = b;
+    int32_t bn = dst[b];
+    float bv = w[bn];
+    for (int32_t p = b + 1; p < e; ++p) {
+        const int32_t n = dst[p];
+        const float v = w[n];
+        if (takes_over(bv, v)) {
+            bv = v;
+            bp = p;
+            bn = n;
+        }
+    }
+    arg_pos[k] = bp;
+    max_node[k] = bn;
+    max_w[keys[k]] = bv;  // == weights[max_node], the same bits
+}
+
+__global__ __launch_bounds__(kScoreThreads) void score_scatter_kernel(
+        const float* __restrict__ grad_max, const int32_t* __restrict__ keys, const int32_t* __restrict__ arg_pos,
+        const int32_t* __restrict__ in_ptr, const int32_t* __restrict__ in_pos, const int32_t* __restrict__ in_key,
+        int64_t N, float* __restrict__ grad_w) {
+    const int64_t n = (int64_t)blockIdx.x * kScoreThreads + threadIdx.x;
+    if (n >= N) return;
+    const int32_t b = in_ptr[n], e = in_ptr[n + 1];
+    float acc = 0.0f;
+    bool any = false;
+    for (int32_t j = b; j < e; ++j) {  // sources by rank, descending: the reference's order
+        const int32_t k = in_key[j];
+        if (arg_pos[k] == in_pos[j]) {
+            const float g = grad_max[keys[k]];
+            acc = any ? acc + g : g;
+            any = true;
+        }
+    }
+    grad_w[n] = acc;
+}
+
+}  // namespace
+}  // namespace mpgnn
+
+using namespace mpgnn;
+
+extern "C" int32_t mpgnn_score_argmax(const float* weights, int64_t num_nodes, const int32_t* keys,
+                                      const int32_t* key_ptr, const int32_t* dst, int64_t num_keys,
+                                      float* max_weights, int32_t* arg_pos, int32_t* max_node, void* stream) {
+    if (num_nodes < 0 || num_keys < 0 || num_keys >= (int64_t)INT32_MAX) return arg_fail("mpgnn_score_argmax: bad sizes");
+    if (num_nodes == 0) return MPGNN_OK;
+    if (!weights || !max_weights) return arg_fail("mpgnn_score_argmax: NULL weights / max_weights");
+    if (num_keys > 0 && (!keys || !key_ptr || !dst || !arg_pos || !max_node))
+        return arg_fail("mpgnn_score_argmax: NULL dictionary / output");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    int32_t st = hip_status(hipMemsetAsync(max_weights, 0, (size_t)num_nodes * sizeof(float), strm),
+                            "memset max_weights");
+    if (st != MPGNN_OK || num_keys == 0) return st;
+    const unsigned grid = (unsigned)((num_keys + kScoreThreads - 1) / kScoreThreads);
+    hipLaunchKernelGGL(score_argmax_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, weights, keys, key_ptr, dst,
+                       (int32_t)num_keys, max_weights, arg_pos, max_node);
+    return hip_status(hipGetLastError(), "score_argmax_kernel launch");
+}
+
+extern "C" int32_t mpgnn_score_argmax_bwd(const float* grad_max, int64_t num_nodes, const int32_t* keys,
+                                          const int32_t* arg_pos, const int32_t* in_ptr, const int32_t* in_pos,
+                                          const int32_t* in_key, float* grad_weights, void* stream) {
+    if (num_nodes < 0) return arg_fail("mpgnn_score_argmax_bwd: bad sizes");
+    if (num_nodes == 0) return MPGNN_OK;
+    if (!grad_max || !in_ptr || !grad_weights) return arg_fail("mpgnn_score_argmax_bwd: NULL argument");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    const unsigned grid = (unsigned)((num_nodes + kScoreThreads - 1) / kScoreThreads);
+    hipLaunchKernelGGL(score_scatter_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, grad_max, keys, arg_pos,
+                       in_ptr, in_pos, in_key, num_nodes, grad_weights);
+    return hip_status(hipGetLastError(), "score_scatter_kernel launch");
+}

@@ -6,7 +6,8 @@ node slices (``linear``: same forward, same parameters, blocked summation order)
 order and a seeded initialisation are identical to the reference, so ``state_dict``s load
 either way. ``MPNet`` (model.py:153-176) is not provided: it calls its convs with 4 arguments
 where CustomRGCNConv.forward needs 5 (mp_rgcn_layer.py:158) and cannot run in the reference.
-The score-function classes (model.py:12-125) are outside the hot path.
+The score-function classes (model.py:26-125: InputLayer, OutputLayer, Score) are the GPU ones of
+``score`` (segment-argmax kernels), re-exported here under the reference's names.
 """
 from __future__ import annotations
 
@@ -18,8 +19,9 @@ import torch.nn.functional as F
 
 from .mp_rgcn_layer import CustomRGCNConv
 from .nn import RGCNConv
+from .score import InputLayer, OutputLayer, Score  # noqa: F401  (model.py:26-125)
 
-__all__ = ["Net", "MPNetm", "linear"]
+__all__ = ["Net", "MPNetm", "linear", "InputLayer", "OutputLayer", "Score"]
 
 
 class _SplitKLinear(torch.autograd.Function):

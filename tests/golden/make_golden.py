@@ -255,6 +255,106 @@ def make_mpnetm_golden(model):
     np.savez_compressed(os.path.join(HERE, "mpnetm_synthetic.npz"), **out)
 
 
+SCORE_FUNCS = ("masked_edge_index", "create_edge_dictionary", "initialize_weights", "get_model", "get_optimizer",
+               "get_loss", "get_loss_per_node", "train", "score_relation_parallel")
+
+
+def reference_main_functions(model):
+    """The reference main.py cannot be imported (mpi4py, seaborn, mlxtend, imblearn and utils.py
+    are absent), so its score-function definitions are compiled straight from /root/reference/
+    main.py (ast: only the named top-level functions, unchanged) into a namespace holding what
+    main.py's own imports give them (``from model import *``, random, ...). Nothing of the
+    reference is written into this repository; only the outputs below are."""
+    import ast
+    import random
+    src = open(os.path.join(REF, "main.py")).read()
+    tree = ast.parse(src)
+    keep = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in SCORE_FUNCS]
+    assert {n.name for n in keep} == set(SCORE_FUNCS), {n.name for n in keep}
+    ns = dict(vars(model))
+    ns.update({"random": random, "COMPLEX": "synthetic"})
+    exec(compile(ast.Module(body=keep, type_ignores=[]), os.path.join(REF, "main.py"), "exec"), ns)
+    return ns
+
+
+def make_score_golden(model):
+    """Score function (model.py:26-125) trained by the reference's own score_relation_parallel
+    path (main.py:727-760: create_edge_dictionary :387-438, initialize_weights :479-497, train
+    :641-673) on the planted synthetic graph (KAT L3): per epoch the loss and every source's
+    argmax destination, plus the final parameters. Two cases:
+      rel1_synth   relation 1, dataset 'synthetic' (labels indexed by node), all sources of
+                   the relation (the first-iteration mask: sorted unique node_1)
+      rel0_mask    relation 0, dataset 'fb15k-237' (labels per mask position), a shuffled mask
+                   with one duplicate and nodes without an edge of the relation."""
+    import random
+    ns = reference_main_functions(model)
+    kat = np.load(os.path.join(HERE, "kat_synthetic.npz"))
+    link, node, label = kat["L3_link"], kat["L3_node"], kat["L3_label"]
+    edge_index = torch.tensor(np.stack([link[:, 0], link[:, 2]]))
+    edge_type = torch.tensor(link[:, 1])
+    x = torch.from_numpy(node[:, 1:].astype(np.float32))
+    N = x.size(0)
+    lab = torch.zeros(N, dtype=torch.int64)
+    lab[torch.from_numpy(label[:, 0])] = torch.from_numpy(label[:, 1])
+    out = {"edge_index": edge_index.numpy(), "edge_type": edge_type.numpy(), "x": x.numpy(), "labels": lab.numpy()}
+    epochs = 100
+    for tag, rel, dataset in (("rel1_synth", 1, "synthetic"), ("rel0_mask", 0, "fb15k-237")):
+        data = model.Data()
+        data.x, data.edge_index, data.edge_type, data.num_nodes = x, edge_index, edge_type, N
+        if dataset == "synthetic":
+            mask = torch.unique(edge_index[0][edge_type == rel]).tolist()
+            data.labels = lab.unsqueeze(-1)
+        else:
+            srcs = torch.unique(edge_index[0][edge_type == rel]).tolist()
+            g = np.random.default_rng(7)
+            mask = [int(v) for v in g.permutation(srcs)[: len(srcs) // 2]]
+            absent = sorted(set(range(N)) - set(srcs))[:5]
+            mask = mask[:10] + [absent[0]] + mask[10:] + [mask[3]] + absent[1:]
+            data.labels = lab[torch.tensor(mask)].unsqueeze(-1)  # per mask position
+        ed, dd = ns["create_edge_dictionary"](data, rel, mask, BAGS=False, dataset=dataset)
+        random.seed(1000 + rel)
+        weights = ns["initialize_weights"](data, dd, BAGS=False)
+        for k in range(N):  # the reference leaves non-destination entries uninitialised
+            if k not in dd:
+                weights[k] = 0.0
+        w0 = weights.clone()
+        torch.manual_seed(77)
+        mod = ns["get_model"](weights, x.size(1))
+        opt = ns["get_optimizer"](mod)
+        crit, crit_node = ns["get_loss"](), ns["get_loss_per_node"]()
+        losses, argmax = [], []
+        keys = list(ed.keys())
+        for _ in range(epochs):
+            loss, best, _, _, _ = ns["train"](data, ed, mod, opt, crit, mask, crit_node, [], weights, torch.tensor(0),
+                                              BAGS=False, bags_to_predict=None, bags_to_predict_labels=None,
+                                              dataset=dataset)
+            losses.append(loss.item())
+            argmax.append([best[k] for k in keys])
+        out[f"{tag}_relation"] = np.int64(rel)
+        out[f"{tag}_mask"] = np.array(mask, dtype=np.int64)
+        out[f"{tag}_mask_labels"] = data.labels.numpy()
+        out[f"{tag}_keys"] = np.array(keys, dtype=np.int64)
+        out[f"{tag}_key_ptr"] = np.cumsum([0] + [len(ed[k]) for k in keys]).astype(np.int64)
+        out[f"{tag}_dst"] = np.array(sum((ed[k] for k in keys), []), dtype=np.int64)
+        out[f"{tag}_dd_keys"] = np.array(list(dd.keys()), dtype=np.int64)
+        out[f"{tag}_dd_min"] = np.array([min(v) for v in dd.values()], dtype=np.float64)
+        out[f"{tag}_dd_len"] = np.array([len(v) for v in dd.values()], dtype=np.int64)
+        out[f"{tag}_w0"] = w0.numpy()
+        out[f"{tag}_loss"] = np.array(losses)
+        out[f"{tag}_argmax"] = np.array(argmax, dtype=np.int32)
+        out[f"{tag}_w_final"] = mod.input.weights.detach().numpy()[:, 0]
+        out[f"{tag}_lin_final"] = mod.output.LinearLayerAttri.weight.detach().numpy()
+        torch.manual_seed(77)
+        out[f"{tag}_lin0"] = torch.nn.Linear(x.size(1), 1, bias=False).weight.detach().numpy()
+        # the same run through score_relation_parallel itself (its returned loss)
+        random.seed(1000 + rel)
+        torch.manual_seed(77)
+        ret = ns["score_relation_parallel"](data, rel, list(mask) if dataset != "synthetic" else [], x.size(1),
+                                            dataset=dataset)
+        out[f"{tag}_srp_loss"] = np.float64(ret[1])
+    np.savez_compressed(os.path.join(HERE, "score_synthetic.npz"), **out)
+
+
 def make_fb15k_triples():
     """FB15K-237 dev+test triples as entity/relation indices (entities.txt / relations.txt
     order). train.tsv is missing from the reference (.MISSING_LARGE_BLOBS:7); the bench's
@@ -286,6 +386,7 @@ def main():
     make_kat()
     make_layer_goldens(layer)
     make_mpnetm_golden(model)
+    make_score_golden(model)
     make_fb15k_triples()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):

@@ -1,0 +1,237 @@
+"""The metapath score function: model.py:26-125 + main.py:387-760, non-bag path.
+
+CPU: the oracle restatement (oracle/score_oracle.py) against the goldens produced by the
+reference's own functions (tests/golden/score_synthetic.npz, make_golden.make_score_golden):
+edge / destination dictionaries, initial weights, the per-epoch loss and argmax of all 100
+epochs, the final parameters; the host side of the drop-in (destination dictionary, weight
+initialisation) against the same goldens.
+
+GPU (through the C ABI, mpgnn_score_argmax / _bwd): the device-built dictionary bit-exact
+against the goldens; the forward (argmax node, max weight) BIT-EXACT against the oracle on
+C1 / KAT / C3 graphs with ties, NaNs and empty sources; the backward bit-exact against autograd
+through the oracle's loop (the reference's reverse accumulation order); the 100-epoch training
+trajectory against the reference's (same argmax at every epoch, loss and weights within 1e-5).
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import score_oracle as so
+
+DEV = "cuda"
+
+
+def _golden(golden):
+    return golden("score_synthetic.npz")
+
+
+def _graph(g):
+    return torch.from_numpy(g["edge_index"]), torch.from_numpy(g["edge_type"]), torch.from_numpy(g["x"])
+
+
+CASES = [("rel1_synth", "synthetic"), ("rel0_mask", "fb15k-237")]
+
+
+def _oracle_run(g, tag, dataset, epochs=100):
+    ei, et, x = _graph(g)
+    N = x.size(0)
+    rel = int(g[f"{tag}_relation"])
+    mask = g[f"{tag}_mask"].tolist()
+    labels = torch.from_numpy(g[f"{tag}_mask_labels"])
+    ed, dd = so.create_edge_dictionary(ei, et, rel, mask, labels, dataset)
+    w0 = so.initialize_weights(N, dd, random.Random(1000 + rel))
+    torch.manual_seed(77)
+    model = so.Score(w0.clone(), dataset, x.size(1))
+    opt = torch.optim.Adam(model.parameters(), lr=0.1)
+    trace = []
+    for _ in range(epochs):
+        loss, best, _, _ = so.train(model, opt, ed, N, labels, mask, dataset)
+        trace.append((loss.item(), [best[k] for k in ed]))
+    return ed, dd, w0, model, trace
+
+
+# ------------------------------------------------------------------------------------------
+# CPU: oracle vs the reference's own outputs
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("tag,dataset", CASES)
+def test_oracle_matches_reference_score_training(golden, tag, dataset):
+    g = _golden(golden)
+    ed, dd, w0, model, trace = _oracle_run(g, tag, dataset)
+    keys = list(ed.keys())
+    assert keys == g[f"{tag}_keys"].tolist()
+    assert np.array_equal(np.cumsum([0] + [len(ed[k]) for k in keys]), g[f"{tag}_key_ptr"])
+    assert sum((ed[k] for k in keys), []) == g[f"{tag}_dst"].tolist()
+    assert list(dd.keys()) == g[f"{tag}_dd_keys"].tolist()
+    assert [min(v) for v in dd.values()] == g[f"{tag}_dd_min"].tolist()
+    assert np.array_equal(w0.numpy(), g[f"{tag}_w0"])
+    losses = np.array([t[0] for t in trace])
+    assert np.array_equal(losses, g[f"{tag}_loss"]), np.abs(losses - g[f"{tag}_loss"]).max()
+    assert np.array_equal(np.array([t[1] for t in trace]), g[f"{tag}_argmax"])
+    assert np.array_equal(model.input.weights.detach().numpy()[:, 0], g[f"{tag}_w_final"])
+    assert float(g[f"{tag}_srp_loss"]) == losses[-1]  # the reference's score_relation_parallel itself
+
+
+def test_oracle_forward_argmax_semantics():
+    """torch.argmax as model.py:85 uses it: first maximum, NaN is the maximum."""
+    w = torch.tensor([0.5, 1.0, 1.0, float("nan"), 0.2, float("nan"), 1.0]).unsqueeze(-1)
+    d = {0: [0, 1, 2], 1: [4, 3, 5], 2: [6, 1], 3: [4]}
+    mw, best = so.score_forward(w, 7, d)
+    assert best == {0: 1, 1: 3, 2: 6, 3: 4}
+    assert mw[0, 0] == 1.0 and torch.isnan(mw[1, 0]) and mw[3, 0] == 0.2 and mw[4, 0] == 0.0
+
+
+def test_destination_dictionary_and_weight_init_match_reference(golden):
+    """Host side of the drop-in: DestinationDictionary (keys in first-appearance order, minimum
+    label per key) and initialize_weights' random stream, against the reference's outputs."""
+    from mpgnn_amd.score import DestinationDictionary, initialize_weights
+    g = _golden(golden)
+    ei, et, x = _graph(g)
+    for tag, dataset in CASES:
+        rel = int(g[f"{tag}_relation"])
+        mask = g[f"{tag}_mask"].tolist()
+        labels = torch.from_numpy(g[f"{tag}_mask_labels"]).reshape(-1)
+        sel = (et == rel).numpy()
+        src, dst = ei[0].numpy()[sel], ei[1].numpy()[sel]
+        first = {}
+        for i, s in enumerate(mask):
+            first.setdefault(s, i)
+        keep = np.array([s in first for s in src], dtype=bool)
+        lab = labels.numpy()
+        per_edge = lab[src[keep]] if dataset == "synthetic" else lab[[first[s] for s in src[keep]]]
+        dd = DestinationDictionary(dst[keep], per_edge.astype(np.float64), True)
+        assert dd.keys_arr.tolist() == g[f"{tag}_dd_keys"].tolist()
+        assert dd.min_labels().tolist() == g[f"{tag}_dd_min"].tolist()
+        assert [len(dd[k]) for k in dd] == g[f"{tag}_dd_len"].tolist()
+
+        class D:
+            num_nodes = x.size(0)
+        w = initialize_weights(D, dd, False, rng=random.Random(1000 + rel))
+        assert np.array_equal(w.numpy(), g[f"{tag}_w0"])
+
+
+# ------------------------------------------------------------------------------------------
+# GPU: the HIP kernels through the C ABI
+# ------------------------------------------------------------------------------------------
+def _graphs():
+    from mpgnn_amd import data
+    out = []
+    g = data.config_graph("C1")
+    out.append(("C1", g.edge_index, g.edge_type, g.num_nodes))
+    g = data.fb15k237_graph(feat_dim=4, seed=0, recipe="survey")
+    out.append(("C3", g.edge_index, g.edge_type, g.num_nodes))
+    return out
+
+
+def _tied_weights(n, seed):
+    """Few distinct values (many ties), exact 0 / 1 (the clamp bounds), a few NaNs."""
+    gen = torch.Generator().manual_seed(seed)
+    w = torch.randint(0, 6, (n,), generator=gen).float() / 5.0
+    w[torch.randint(0, n, (max(1, n // 500),), generator=gen)] = float("nan")
+    return w
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [0, 1])
+def test_score_argmax_forward_backward_bit_exact(case):
+    from mpgnn_amd.score import build_edge_dictionary, score_argmax
+    name, ei, et, N = _graphs()[case]
+    rels = torch.unique(et).tolist()
+    rels = rels[:3] + rels[-2:] if len(rels) > 5 else rels
+    for rel in rels:
+        srcs = torch.unique(ei[0][et == rel]).tolist()
+        rng = np.random.default_rng(rel)
+        # a shuffled subset + a node without an edge of the relation + a duplicate
+        mask = [int(v) for v in rng.permutation(srcs)[: max(1, (3 * len(srcs)) // 4)]]
+        mask = mask + [mask[0]] + [N - 1]
+        ed_ref, _ = so.create_edge_dictionary(ei, et, rel, mask, torch.zeros(len(mask), 1), "fb15k-237")
+        ed, _ = build_edge_dictionary(ei.to(DEV), et.to(DEV), rel, mask, num_nodes=N)
+        assert list(ed.keys()) == list(ed_ref.keys()), (name, rel)
+        assert all(ed[k] == ed_ref[k] for k in list(ed_ref)[:200]), (name, rel)
+        w = _tied_weights(N, rel + 1)
+        wr = w.clone().unsqueeze(-1).requires_grad_(True)
+        mw_ref, best_ref = so.score_forward(wr, N, ed_ref)
+        wg = w.to(DEV).unsqueeze(-1).requires_grad_(True)
+        mw, mn = score_argmax(wg, ed)
+        assert mn.cpu().tolist() == [best_ref[k] for k in ed_ref], (name, rel)
+        assert torch.equal(torch.isnan(mw.detach().cpu()), torch.isnan(mw_ref.detach()))
+        assert torch.equal(torch.nan_to_num(mw.detach().cpu(), 7.0), torch.nan_to_num(mw_ref.detach(), 7.0))
+        gout = torch.randn(N, 1, generator=torch.Generator().manual_seed(rel))
+        mw_ref.backward(gout)
+        mw.backward(gout.to(DEV))
+        assert torch.equal(wg.grad.cpu(), wr.grad), (name, rel, float((wg.grad.cpu() - wr.grad).abs().max()))
+
+
+@pytest.mark.gpu
+def test_score_argmax_empty_and_plain_dict_input():
+    from mpgnn_amd.score import OutputLayer, build_edge_dictionary, score_argmax
+    ei = torch.tensor([[0, 0, 2], [1, 2, 1]])
+    et = torch.tensor([0, 0, 1])
+    ed, _ = build_edge_dictionary(ei.to(DEV), et.to(DEV), 5, [0, 1, 2], num_nodes=3)  # absent relation
+    assert len(ed) == 0
+    w = torch.rand(3, 1, device=DEV, requires_grad=True)
+    mw, mn = score_argmax(w, ed)
+    assert torch.equal(mw.cpu(), torch.zeros(3, 1)) and mn.numel() == 0
+    mw.sum().backward()
+    assert torch.equal(w.grad.cpu(), torch.zeros(3, 1))
+    out = OutputLayer(2).to(DEV)
+
+    class D:
+        num_nodes = 3
+    w2 = torch.tensor([[0.1], [0.7], [0.7]], device=DEV)
+    mw2, best, _ = out(w2, D, {0: [2, 1]}, False, None, None)  # the reference's own dict type
+    assert dict(best) == {0: 2} and float(mw2[0, 0]) == pytest.approx(0.7)
+    with pytest.raises(IndexError):
+        build_edge_dictionary(ei.to(DEV), et.to(DEV), 0, [0], num_nodes=2)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        score_argmax(w.detach().cpu(), ed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag,dataset", CASES)
+def test_score_training_tracks_reference(golden, tag, dataset):
+    """The drop-in train() (GPU kernels, fused Adam) over the reference's 100 epochs: the
+    dictionaries bit-exact, the argmax of every source identical at every epoch, the loss and
+    the final weights within 1e-5 of the reference's (Adam's fp32 arithmetic is torch's GPU
+    kernel, not the CPU one)."""
+    from mpgnn_amd import score as sc
+    g = _golden(golden)
+    ei, et, x = _graph(g)
+    rel = int(g[f"{tag}_relation"])
+    mask = g[f"{tag}_mask"].tolist()
+
+    class Data:
+        pass
+    d = Data()
+    d.x, d.edge_index, d.edge_type, d.num_nodes = x, ei.to(DEV), et.to(DEV), x.size(0)
+    d.labels = torch.from_numpy(g[f"{tag}_mask_labels"])
+    ed, dd = sc.create_edge_dictionary(d, rel, mask, BAGS=False, dataset=dataset)
+    assert list(ed.keys()) == g[f"{tag}_keys"].tolist()
+    assert ed.dst_t.cpu().tolist() == g[f"{tag}_dst"].tolist()
+    assert ed.key_ptr_t.cpu().tolist() == g[f"{tag}_key_ptr"].tolist()
+    w0 = sc.initialize_weights(d, dd, False, rng=random.Random(1000 + rel))
+    assert np.array_equal(w0.numpy(), g[f"{tag}_w0"])
+    torch.manual_seed(77)
+    model = sc.get_model(w0, x.size(1)).to(DEV)
+    assert np.array_equal(model.output.LinearLayerAttri.weight.detach().cpu().numpy(), g[f"{tag}_lin0"])
+    opt = sc.get_optimizer(model)
+    crit, crit_node = sc.get_loss(), sc.get_loss_per_node()
+    losses, first_diff = [], None
+    for ep in range(100):
+        loss, best, lpn, _, pred = sc.train(d, ed, model, opt, crit, mask, crit_node, [], w0, torch.tensor(0),
+                                            BAGS=False, dataset=dataset)
+        losses.append(loss.item())
+        got = best.values_tensor().cpu().numpy()
+        if first_diff is None and not np.array_equal(got, g[f"{tag}_argmax"][ep]):
+            first_diff = ep
+    assert first_diff is None, f"argmax differs from the reference at epoch {first_diff}"
+    ref = g[f"{tag}_loss"]
+    assert np.allclose(losses, ref, rtol=1e-5, atol=1e-7), np.abs(np.array(losses) - ref).max()
+    wf = model.input.weights.detach().cpu().numpy()[:, 0]
+    assert np.allclose(wf, g[f"{tag}_w_final"], rtol=1e-5, atol=1e-6)
+    # the drop-in score_relation_parallel itself
+    random.seed(1000 + rel)
+    torch.manual_seed(77)
+    r, final, ed2, _ = sc.score_relation_parallel(d, rel, mask if dataset != "synthetic" else [], x.size(1), dataset)
+    assert r == rel and final == pytest.approx(float(g[f"{tag}_srp_loss"]), rel=1e-5, abs=1e-7)
