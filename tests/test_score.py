@@ -66,13 +66,13 @@ def test_oracle_matches_reference_score_training(golden, tag, dataset):
     assert list(dd.keys()) == g[f"{tag}_dd_keys"].tolist()
     assert [min(v) for v in dd.values()] == g[f"{tag}_dd_min"].tolist()
     assert np.array_equal(w0.numpy(), g[f"{tag}_w0"])
-    # the loss is an fp32 mean whose summation order follows the host's SIMD width / threads (the
-    # goldens were made on another CPU): within 1e-6; it feeds nothing back (d mean / d p is
-    # elementwise), so the argmax and the weights are exact
+    # the goldens were made on another CPU: the fp32 mean's summation order and Adam's vectorised
+    # arithmetic (FMA contraction) follow the host's SIMD width, so the loss and the weights agree
+    # to a few ulps (1e-6) while the argmax of every source at every epoch is identical
     losses = np.array([t[0] for t in trace])
     assert np.allclose(losses, g[f"{tag}_loss"], rtol=1e-6, atol=0), np.abs(losses - g[f"{tag}_loss"]).max()
     assert np.array_equal(np.array([t[1] for t in trace]), g[f"{tag}_argmax"])
-    assert np.array_equal(model.input.weights.detach().numpy()[:, 0], g[f"{tag}_w_final"])
+    assert np.allclose(model.input.weights.detach().numpy()[:, 0], g[f"{tag}_w_final"], rtol=1e-6, atol=1e-7)
     # the reference's score_relation_parallel itself returned the same final loss
     assert float(g[f"{tag}_srp_loss"]) == pytest.approx(losses[-1], rel=1e-6)
 
