@@ -1534,6 +1534,215 @@ __global__ __launch_bounds__(kThreads, OCC) void rel_gemm_kernel(RelGemmArgs a) 
     RelGemm<KB, DGRAD, NB, OCC, CAT, PIPE, REPI>::run(a, smem);
 }
 
+// ----------------------------------------------------------------------------------------
+// rel_gemm_bf3_kernel — rel_gemm_kernel's B-stationary persistent GEMM (same items, gathers,
+// cross-item pipeline, outputs) on the bf16 matrix cores: v_mfma_f32_32x32x16_bf16 runs 16× the
+// FLOP/clk of v_mfma_f32_32x32x2_f32 (MI355X_MICROARCH.md §Matrix cores). Every fp32 operand is
+// split EXACTLY into three bf16 pieces, a = a0 + a1 + a2 (round-to-nearest: |a1| ≤ 2^-9|a|,
+// |a2| ≤ 2^-18|a|; each bf16 × bf16 product is exact in fp32) and the six products down to
+// 2^-18 relative are accumulated:
+//     hi += a0·b0        lo += a2·b0 + a1·b1 + a0·b2 + a1·b0 + a0·b1        out = hi + lo
+// (dropped: a1·b2, a2·b1 ≤ 2^-27, a2·b2). 6 MFMAs of 32 cycles per 16 k instead of 8 of 64:
+// 2.67× the fp32-MFMA rate. Accuracy: the hardware adds each instruction's 16 products before
+// rounding into the accumulator (scripts/mfma_bf16_probe.hip), and the small terms sum in their
+// own accumulator, so the result is at least as close to the float64 truth as the fp32 fmaf
+// chain of rel_gemm_kernel (tests/test_gpu_parity.py holds it to the same bars).
+//
+// Registers: the wave's K × 32 weight slice as 3 × K/16 bf16x8 fragments (K = 128: 96 VGPRs,
+// lane-half h holds k ∈ [16s + 8h, 16s + 8h + 8) of k-step s, column 32·wave + (lane & 31)).
+// LDS: the A tile as three bf16 planes [32][K + 8] (double-buffered; the 16-B pad makes the
+// fragment reads ds_read_b128-conflict-free), split once by the committing thread.
+// ----------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3_bf16(float a, __bf16& h0, __bf16& h1, __bf16& h2) {
+    h0 = (__bf16)a;               // v_cvt_pk_bf16_f32: round to nearest even
+    const float r1 = a - (float)h0;  // exact
+    h1 = (__bf16)r1;
+    const float r2 = r1 - (float)h1;  // exact, ≤ 8 significant bits: h2 == r2
+    h2 = (__bf16)r2;
+}
+
+template <int KB, bool DGRAD>
+struct RelGemmBf3 {
+    using Base = RelGemm<KB, DGRAD>;
+    static constexpr int K = 64 * KB;
+    static constexpr int N = 128;
+    static constexpr int NS = K / 16;              // k-steps of 16
+    static constexpr int LDAB = K + 8;             // bf16 row stride of an A plane
+    static constexpr int PLANE = 32 * LDAB;        // bf16 per plane
+    static constexpr int WPT = Base::WPT;          // float4 of an A tile per thread
+    using Item = typename Base::Item;
+    using ItemTable = typename Base::ItemTable;
+
+    static constexpr size_t lds_bytes() { return (size_t)2 * 3 * PLANE * 2 + 2 * 32 * sizeof(float) + 64; }
+
+    __device__ static __forceinline__ void commit(const Item& it, int tid, const float4 (&v)[WPT], int cnt,
+                                                  __bf16* A, float* sc) {
+        constexpr int W4 = K / 4;
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+            const int e = tid + j * kThreads;
+            const int r = e / W4;
+            const float4 x = r < it.nrows ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            __bf16 p0[4], p1[4], p2[4];
+            split3_bf16(x.x, p0[0], p1[0], p2[0]);
+            split3_bf16(x.y, p0[1], p1[1], p2[1]);
+            split3_bf16(x.z, p0[2], p1[2], p2[2]);
+            split3_bf16(x.w, p0[3], p1[3], p2[3]);
+            __bf16* d = A + r * LDAB + (e % W4) * 4;
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<bf16x4*>(d) = bf16x4{p0[0], p0[1], p0[2], p0[3]};
+            *reinterpret_cast<bf16x4*>(d + PLANE) = bf16x4{p1[0], p1[1], p1[2], p1[3]};
+            *reinterpret_cast<bf16x4*>(d + 2 * PLANE) = bf16x4{p2[0], p2[1], p2[2], p2[3]};
+        }
+        if (tid < 32) sc[tid] = 1.0f / (float)cnt;
+    }
+
+    // the wave's weight slice as bf16 pieces: b[s][p][j] = piece p of B(16s + 8h + j, 32·wave + c)
+    __device__ static __forceinline__ void load_b(const float* w, int wave, int lane, bf16x8 (&b)[NS][3]) {
+        const int c = lane & 31, h = lane >> 5;
+        float f[NS][8];
+        if constexpr (!DGRAD) {
+            const float* p = w + (size_t)(8 * h) * N + wave * 32 + c;
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) f[s][j] = p[(16 * s + j) * N];
+        } else {  // B(k, n) = W[n][k]: 8 consecutive floats of row n = 32·wave + c
+            const float* p = w + (size_t)(wave * 32 + c) * K + 8 * h;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const float4 t0 = *reinterpret_cast<const float4*>(p + 16 * s);
+                const float4 t1 = *reinterpret_cast<const float4*>(p + 16 * s + 4);
+                f[s][0] = t0.x; f[s][1] = t0.y; f[s][2] = t0.z; f[s][3] = t0.w;
+                f[s][4] = t1.x; f[s][5] = t1.y; f[s][6] = t1.z; f[s][7] = t1.w;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                __bf16 h0, h1, h2;
+                split3_bf16(f[s][j], h0, h1, h2);
+                b[s][0][j] = h0;
+                b[s][1][j] = h1;
+                b[s][2][j] = h2;
+            }
+    }
+
+    __device__ static void run(const RelGemmArgs& a, __bf16* smem) {
+        __bf16* As = smem;                                            // [2][3 planes][32][LDAB]
+        float* Sc = reinterpret_cast<float*>(smem + 2 * 3 * PLANE);  // [2][32] dgrad row scales
+        const int tid = threadIdx.x;
+        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int n_items = a.n_rel + a.n_root;
+        const int G = (int)gridDim.x;
+        const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
+        const int rng = g * q + min(g, rem) + ((int)blockIdx.x >> 3);
+        const int i_beg = (int)((long long)rng * n_items / G);
+        const int i_end = (int)((long long)(rng + 1) * n_items / G);
+        if (i_beg >= i_end) return;
+
+        float4 v[WPT];
+        int cnt;
+        const ItemTable tab = Base::item_table(a, i_beg, i_end, lane);
+        auto get_item = [&](int i) { return i - i_beg < 64 ? Base::item_at(a, tab, i - i_beg) : Base::item(a, i); };
+        Item cur = get_item(i_beg);
+        int zm = 0;
+        {
+            int crow[WPT];
+            Base::gather_idx(a, cur, tid, crow, cnt);
+            Base::issue_rows(a, tid, crow, v, zm);
+        }
+        int nrow[WPT];
+        int ncnt = 1;
+        if (i_beg + 1 < i_end) Base::gather_idx(a, get_item(i_beg + 1), tid, nrow, ncnt);
+        bf16x8 b[NS][3];
+        load_b(cur.w, wave, lane, b);
+        commit(cur, tid, v, cnt, As, Sc);
+        __syncthreads();
+
+        constexpr int SPG = (16 + NS - 1) / NS;  // previous item's stores per k-step
+        constexpr int kCommitAt = (3 * NS) / 4;  // k-step after which the next tile is committed
+        const int col_b = (wave * 32 + c) * 4;
+        float prev[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) prev[r] = 0.0f;
+        __amdgpu_buffer_rsrc_t prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.Y, (short)0, 0, 0x00020000);
+        auto store_prev = [&](int r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(prev[r]), prev_rsrc, row * (N * 4) + col_b, 0, 0);
+        };
+        int buf = 0;
+        for (int i = i_beg; i < i_end; ++i) {
+            const bool has_next = i + 1 < i_end;
+            const Item nxt = has_next ? get_item(i + 1) : cur;
+            if (has_next) {
+                Base::issue_rows(a, tid, nrow, v, zm);
+                cnt = ncnt;
+                if (i + 2 < i_end) Base::gather_idx(a, get_item(i + 2), tid, nrow, ncnt);
+            }
+            const bool new_w = nxt.w != cur.w;
+            const __bf16* Ab = As + buf * 3 * PLANE + c * LDAB + 8 * h;
+            f32x16 hi, lo;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                hi[r] = 0.0f;
+                lo[r] = 0.0f;
+            }
+            bf16x8 f0 = *reinterpret_cast<const bf16x8*>(Ab);
+            bf16x8 f1 = *reinterpret_cast<const bf16x8*>(Ab + PLANE);
+            bf16x8 f2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * PLANE);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const bf16x8 a0 = f0, a1 = f1, a2 = f2;
+                if (s + 1 < NS) {
+                    f0 = *reinterpret_cast<const bf16x8*>(Ab + 16 * (s + 1));
+                    f1 = *reinterpret_cast<const bf16x8*>(Ab + PLANE + 16 * (s + 1));
+                    f2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * PLANE + 16 * (s + 1));
+                }
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[s][0], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][1], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][2], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][0], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][1], lo, 0, 0, 0);
+                hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][0], hi, 0, 0, 0);
+#pragma unroll
+                for (int u = 0; u < SPG; ++u)
+                    if (s * SPG + u < 16) store_prev(s * SPG + u);
+                if (s == kCommitAt - 1 && has_next) commit(nxt, tid, v, cnt, As + (buf ^ 1) * 3 * PLANE, Sc + (buf ^ 1) * 32);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                prev[r] = hi[r] + lo[r];
+                if constexpr (DGRAD) {  // row scale 1/cnt of relation rows
+                    if (!cur.root) prev[r] = prev[r] * Sc[buf * 32 + (r & 3) + 8 * (r >> 2) + 4 * h];
+                }
+            }
+            {
+                float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
+                const int bytes = __builtin_amdgcn_readfirstlane(cur.nrows) * N * 4;
+                prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(Yt, (short)0, bytes, 0x00020000);
+            }
+            if (new_w) load_b(nxt.w, wave, lane, b);  // after the chain: the slice registers are free
+            __syncthreads();
+            cur = nxt;
+            buf ^= 1;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) store_prev(r);
+    }
+};
+
+template <int KB, bool DGRAD>
+__global__ __launch_bounds__(kThreads, 2) void rel_gemm_bf3_kernel(RelGemmArgs a) {
+    extern __shared__ __bf16 smem_bf[];
+    RelGemmBf3<KB, DGRAD>::run(a, smem_bf);
+}
+
 template <int KB>  // Kp = 64·KB
 __global__ __launch_bounds__(kThreads, 2) void tile_gemm_kernel(TileGemmArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -2974,7 +3183,26 @@ static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
+static bool g_gemm_bf3 = true;  // MPGNN_OPT_GEMM_BF3: K ∈ {64, 128}, N = 128 on the bf16 matrix cores (3-way split)
+
+template <int KB, bool DGRAD>
+static void launch_rel_gemm_bf3(const RelGemmArgs& a, hipStream_t st) {
+    const size_t lds = RelGemmBf3<KB, DGRAD>::lds_bytes();
+    const int grid = std::min(a.n_rel + a.n_root, cu_count() * 2);  // two workgroups per CU
+    hipLaunchKernelGGL((rel_gemm_bf3_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
+}
+
 static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, hipStream_t st) {
+    if (g_gemm_bf3 && (K == 64 || K == 128) && a.node_map == nullptr) {
+        if (K == 64) {
+            if (dgrad) launch_rel_gemm_bf3<1, true>(a, st);
+            else launch_rel_gemm_bf3<1, false>(a, st);
+        } else {
+            if (dgrad) launch_rel_gemm_bf3<2, true>(a, st);
+            else launch_rel_gemm_bf3<2, false>(a, st);
+        }
+        return;
+    }
     if (K == 256) {  // F_in = F_out = 256 (C5): two 128-column blocks, K = 256
         if (dgrad) launch_rel_gemm_wide<4, true, 2>(a, st);
         else launch_rel_gemm_wide<4, false, 2>(a, st);
@@ -3790,6 +4018,9 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
         case MPGNN_OPT_REL_WIDE:
             g_rel_wide = value != 0;
             return MPGNN_OK;
+        case MPGNN_OPT_GEMM_BF3:
+            g_gemm_bf3 = value != 0;
+            return MPGNN_OK;
         case MPGNN_OPT_CHUNK_ROWS:
             if (value < 32 || value > 1024 || value % 32 != 0)
                 return arg_error("MPGNN_OPT_CHUNK_ROWS must be 32..1024, a multiple of 32");
@@ -3814,6 +4045,7 @@ int32_t mpgnn_get_option(int32_t option, int64_t* value) {
         case MPGNN_OPT_PLAN_THREADS: *value = g_plan_threads; return MPGNN_OK;
         case MPGNN_OPT_REL_WIDE: *value = g_rel_wide ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_CHUNK_ROWS: *value = g_chunk_rows; return MPGNN_OK;
+        case MPGNN_OPT_GEMM_BF3: *value = g_gemm_bf3 ? 1 : 0; return MPGNN_OK;
         default: return arg_error("unknown option " + std::to_string(option));
     }
 }
