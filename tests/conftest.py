@@ -23,6 +23,14 @@ def pytest_collection_modifyitems(config, items):
             item.add_marker(skip)
 
 
+def pytest_sessionstart(session):
+    # MPGNN_GEMM_BF3=0|1: run the suite on the fp32-MFMA or the bf16-split GEMMs (A/B of accuracy)
+    v = os.environ.get("MPGNN_GEMM_BF3")
+    if v is not None:
+        from mpgnn_amd import _lib
+        _lib.set_option(24, int(v))
+
+
 def pytest_sessionfinish(session, exitstatus):
     from tests import _parity_report
     _parity_report.dump()

@@ -57,20 +57,26 @@ def _worker(rank, world, port, name, q):
         Ws, rs, bs = (t.detach().clone().requires_grad_(True) for t in (W, root, bias))
         ref = orc.rgcn_forward(xs, g.edge_index, g.edge_type, Ws, rs, bs)
         ref.backward(gout)
+        # float64 truth (decides elements where the two fp32 summation orders differ)
+        x64 = g.x.double().requires_grad_(True)
+        W64, r64, b64 = (t.detach().double().requires_grad_(True) for t in (W, root, bias))
+        ref64 = orc.rgcn_forward(x64, g.edge_index, g.edge_type, W64, r64, b64)
+        ref64.backward(gout.double())
         ok = True
         msgs = []
+        from tests._bars import passes
 
-        def close(a, b, what):
+        def close(a, b, t, what):
             nonlocal ok
-            scale = float(b.abs().max())
-            err = float((a - b).abs().max())
-            if err > 1e-5 * scale + 1e-6:
+            good, msg = passes(a, b, t)
+            if not good:
                 ok = False
-                msgs.append(f"{what}: err {err:.3e} scale {scale:.3e}")
+                msgs.append(f"{what}: {msg}")
 
-        close(out, ref.detach(), "out")
-        for a, b, w in zip(grads, [xs.grad, Ws.grad, rs.grad, bs.grad], ["dx", "dW", "droot", "dbias"]):
-            close(a, b, w)
+        close(out, ref.detach(), ref64.detach(), "out")
+        for a, b, t, w in zip(grads, [xs.grad, Ws.grad, rs.grad, bs.grad], [x64.grad, W64.grad, r64.grad, b64.grad],
+                              ["dx", "dW", "droot", "dbias"]):
+            close(a, b, t, w)
         # the local edge sets partition the graph
         n_local = torch.tensor([plan.num_edges])
         dist.all_reduce(n_local)
@@ -79,8 +85,9 @@ def _worker(rank, world, port, name, q):
             msgs.append(f"edges {int(n_local)} != {g.num_edges}")
         q.put((rank, ok, msgs))
         dist.destroy_process_group()
-    except Exception as e:  # report instead of hanging the parent
-        q.put((rank, False, [repr(e)]))
+    except Exception:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, False, [traceback.format_exc()]))
 
 
 @pytest.mark.parametrize("name", ["small", "C1"])
@@ -286,14 +293,17 @@ def _stack_worker(rank, world, port, q, side="gathered"):
         convs = [make_conv(*p) for p in layers]
         out = mpgnn_amd.distributed.sharded_stack_forward(convs, g.x, g.edge_index, g.edge_type, ranges,
                                                           shard_side=side)
-        ref = g.x
+        ref, ref64 = g.x, g.x.double()
         for W, root, bias in layers:
             ref = torch.relu(orc.rgcn_forward(ref, g.edge_index, g.edge_type, W, root, bias))
-        err = float((out - ref).abs().max())
-        q.put((rank, err, float(ref.abs().max())))
+            ref64 = torch.relu(orc.rgcn_forward(ref64, g.edge_index, g.edge_type, W.double(), root.double(),
+                                                bias.double()))
+        from tests._bars import passes
+        q.put((rank,) + passes(out, ref, ref64))
         dist.destroy_process_group()
-    except Exception as e:  # pragma: no cover
-        q.put((rank, None, repr(e)))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
 
 
 @pytest.mark.parametrize("world,side", [(2, "gathered"), (3, "gathered"), (2, "rows"), (3, "rows")])
@@ -309,6 +319,6 @@ def test_sharded_stack_reduce_scatter_matches_unsharded(world, side):
     res = [q.get(timeout=180) for _ in procs]
     for p in procs:
         p.join(timeout=60)
-    for rank, err, scale in res:
-        assert err is not None, scale
-        assert err <= 1e-4 * scale + 1e-6, (rank, err, scale)
+    for rank, ok, msg in res:
+        assert ok is not None, msg
+        assert ok, (rank, msg)  # the suite's elementwise + normwise bar (tests/_bars.py)

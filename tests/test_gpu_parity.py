@@ -46,18 +46,7 @@ FLOOR = 1e-3
 MODEL_CPU_FACTOR = 4.0
 
 
-def max_rel_err(got, ref, floor=FLOOR) -> float:
-    """max_e |got - ref| / max(|ref_e|, floor·max|ref|)  (0 for empty / all-zero ref and got)."""
-    got = got.detach().double().cpu()
-    ref = ref.detach().double().cpu()
-    assert got.shape == ref.shape, (got.shape, ref.shape)
-    if ref.numel() == 0:
-        return 0.0
-    err = (got - ref).abs()
-    scale = float(ref.abs().max())
-    if scale == 0.0:
-        return float("inf") if float(err.max()) > 0 else 0.0
-    return float((err / ref.abs().clamp_min(floor * scale)).max())
+from tests._bars import max_rel_err, normwise_err  # noqa: E402  (the suite's bar, shared)
 
 
 def rel_close(got, ref, tol=TOL, what="", ref64=None, cpu_factor=2.0):
@@ -68,15 +57,20 @@ def rel_close(got, ref, tol=TOL, what="", ref64=None, cpu_factor=2.0):
     assert got_f.shape == ref_f.shape, (what, got_f.shape, ref_f.shape)
     assert bool(torch.isfinite(got_f).all()) == bool(torch.isfinite(ref_f).all()), (what, "non-finite values differ")
     e = max_rel_err(got_f, ref_f)
+    # normwise relative error ||gpu - ref|| / ||ref|| — the north star's "1e-4 rel" read as a norm:
+    # held to the same 1e-4 for every check, beside the elementwise bar
+    nw = normwise_err(got_f, ref_f)
+    assert nw <= tol, f"{what}: normwise rel err {nw:.3e} > {tol:.0e}"
     if ref64 is None:
-        record(what, e, tol)
+        record(what, e, tol, normwise=nw)
         assert e <= tol, f"{what}: max elementwise rel err {e:.3e} > {tol:.0e} (no float64 truth given)"
         return e
     ref64 = ref64.detach().double().cpu()
     e_gpu = max_rel_err(got_f, ref64)
     e_cpu = max_rel_err(ref_f, ref64)
     bar = max(tol, cpu_factor * e_cpu)
-    record(what, e, tol, e_gpu64=e_gpu, e_cpu64=e_cpu, cpu_factor=cpu_factor)
+    record(what, e, tol, normwise=nw, e_gpu64=e_gpu, e_cpu64=e_cpu, cpu_factor=cpu_factor,
+           normwise_gpu64=normwise_err(got_f, ref64), normwise_cpu64=normwise_err(ref_f, ref64))
     assert e <= tol or e_gpu <= bar, (f"{what}: gpu vs fp32 reference {e:.3e} > {tol:.0e} and vs float64 truth "
                                       f"gpu {e_gpu:.3e}, reference fp32 path {e_cpu:.3e} (bar {bar:.3e})")
     return e
@@ -934,9 +928,17 @@ def test_linear_head_gradients_vs_autograd(n, f, o, bias):
     ref_out = torch.nn.functional.linear(x, layer.weight, layer.bias)
     ref_out.backward(go)
     ref = [x.grad, layer.weight.grad] + ([layer.bias.grad] if bias else [])
-    torch.testing.assert_close(out, ref_out, rtol=1e-4, atol=1e-4)
-    for a, b in zip(got, ref):
-        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * max(1.0, float(b.abs().max())))
+    # the float64 truth of the same products (the suite's elementwise bar, decided against it
+    # where the two fp32 summation orders differ at a cancellation)
+    x64 = x.detach().cpu().double().requires_grad_(True)
+    w64 = layer.weight.detach().cpu().double().requires_grad_(True)
+    b64 = layer.bias.detach().cpu().double().requires_grad_(True) if bias else None
+    o64 = torch.nn.functional.linear(x64, w64, b64)
+    o64.backward(go.cpu().double())
+    t64 = [x64.grad, w64.grad] + ([b64.grad] if bias else [])
+    rel_close(out, ref_out, what=f"linear {n}x{f}->{o} out", ref64=o64.detach())
+    for a, b, t, nm in zip(got, ref, t64, ("dx", "dW", "dbias")):
+        rel_close(a, b, what=f"linear {n}x{f}->{o} {nm}", ref64=t)
 
 
 # ------------------------------------------------------------------------------------------
