@@ -54,6 +54,7 @@ from mpgnn_amd.distributed import shard_ranges, sharded_stack_forward  # noqa: E
 
 METRIC = "edges aggregated/sec + epoch time, FB15K-237 128-d at 1/2/4/8 MI355X"
 PEAK_FP32_MFMA = 157.3  # TFLOP/s dense (MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32)
+PEAK_BF16_MFMA = 2516.6  # TFLOP/s dense = 16 x the f32 rate (v_mfma_f32_32x32x16_bf16, 32 cycles, MI355X_MICROARCH.md)
 PEAK_HBM = 8000.0       # GB/s spec
 
 WORKLOADS = {
@@ -450,11 +451,12 @@ def bench_score(args):
 
 def pmc_traffic(workload, mode, feat, kernel_prefix):
     """HBM bytes per launch of `kernel_prefix` from the committed PMC summary, or None."""
-    path = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
-    try:
-        rows = json.load(open(path))
-    except (OSError, ValueError):
-        return None
+    rows = []
+    for rnd in ("r03", "r02"):  # the newest round's PMC summary first
+        try:
+            rows += json.load(open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic.json")))
+        except (OSError, ValueError):
+            pass
     for r in rows:
         if r.get("workload") == workload and r.get("mode") == mode and r.get("feat") == feat and \
                 r.get("kernel", "").startswith(kernel_prefix):
@@ -607,24 +609,37 @@ def main():
                     ("hbm", (S + n_rows) * (4.0 * F + 4) + n_rows * 4.0 * F, "(S + N)·(4F + 4) Y / Y_root rows + ids "
                      "gathered, N·4F output rows written")),
     }
+    bf3 = args.gemm == "bf3" and not single and F in (64, 128)  # rel_gemm_bf3_kernel runs the transform
     rooflines = []
     for kind, (bound, work, model_txt) in model_costs.items():
         if kind not in per_layer:
             continue
         us = per_layer[kind]["us_per_layer"]
-        if bound == "mfma":
+        extra = {}
+        if bound == "mfma" and bf3:
+            # the transform on the bf16 matrix cores: 6 bf16 MFMA products per fp32 product (exact
+            # 3-way operand split) — priced against the dense bf16 peak with the flops it issues
+            ach = 6.0 * work / (us * 1e-6) / 1e12
+            peak, unit = PEAK_BF16_MFMA, "TFLOP/s"
+            fp32_eq = work / (us * 1e-6) / 1e12
+            extra = {"hw_flops_per_launch": 6.0 * work, "fp32_equivalent_TFLOPs": round(fp32_eq, 2),
+                     "frac_of_fp32_mfma_peak": round(fp32_eq / PEAK_FP32_MFMA, 4),
+                     "path": "v_mfma_f32_32x32x16_bf16, fp32 operands split a = a0 + a1 + a2 (bf16, exact), "
+                             "6 products (a0b0 | a2b0 + a1b1 + a0b2 + a1b0 + a0b1), fp32 accumulation"}
+        elif bound == "mfma":
             ach = work / (us * 1e-6) / 1e12
             peak, unit = PEAK_FP32_MFMA, "TFLOP/s"
+            extra = {"path": "v_mfma_f32_32x32x2_f32"}
         else:
             ach = work / (us * 1e-6) / 1e9
             peak, unit = PEAK_HBM, "GB/s"
-        kname = {"seg_fwd": "rel_gemm_kernel", "mean": "flat_rows_kernel",
+        kname = {"seg_fwd": "rel_gemm_bf3_kernel" if bf3 else "rel_gemm_kernel", "mean": "flat_rows_kernel",
                  "row_fwd": ("single_fix_kernel" if root_epi else "single_combine_kernel") if single
                  else "flat_rows_kernel"}[kind]
         rooflines.append({"kind": kind, "kernel": kname, "bound": bound, "achieved": round(ach, 2), "peak": peak,
                           "unit": unit, "frac": round(ach / peak, 4), "us_per_layer": us,
                           "share_of_layer": None, "algorithmic": model_txt,
-                          ("alg_flops_per_launch" if bound == "mfma" else "alg_bytes_per_launch"): work})
+                          ("alg_flops_per_launch" if bound == "mfma" else "alg_bytes_per_launch"): work, **extra})
     total_us = sum(v["us_per_layer"] for v in per_layer.values())
     for r in rooflines:
         r["share_of_layer"] = round(r["us_per_layer"] / total_us, 3) if total_us else None
@@ -635,11 +650,12 @@ def main():
         traffic = pmc_traffic(args.workload, mode_tag, F, "mpgnn::" + dom["kernel"]) if world == 1 else None
         roofline = {"bound": dom["bound"], "achieved": dom["achieved"], "peak": dom["peak"], "unit": dom["unit"],
                     "frac": dom["frac"], "traffic": traffic, "kernel": dom["kernel"], "kind": dom["kind"],
+                    **{k: dom[k] for k in ("fp32_equivalent_TFLOPs", "frac_of_fp32_mfma_peak", "path") if k in dom},
                     "avg_launch_us": dom["us_per_layer"], "share_of_layer": dom["share_of_layer"],
                     "algorithmic": dom["algorithmic"],
                     "note": "dominant kernel of the forward layer by the per-kernel HIP-event pass (events on the "
                             "launch stream, one pair per launch; the headline timed region has none); traffic = "
-                            "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/r02_pmc_traffic.json)"}
+                            "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/r03_pmc_traffic.json, r02 for kernels not re-profiled)"}
         # SURVEY 8d whole-step HBM roofline of the aggregation (kept beside the kernel roofline)
     b_edge = 4 * F + 4
     hbm_roofline = {"bound": "hbm", "bytes_per_edge": b_edge,

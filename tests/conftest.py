@@ -23,14 +23,6 @@ def pytest_collection_modifyitems(config, items):
             item.add_marker(skip)
 
 
-def pytest_sessionstart(session):
-    # MPGNN_GEMM_BF3=0|1: run the suite on the fp32-MFMA or the bf16-split GEMMs (A/B of accuracy)
-    v = os.environ.get("MPGNN_GEMM_BF3")
-    if v is not None:
-        from mpgnn_amd import _lib
-        _lib.set_option(24, int(v))
-
-
 def pytest_sessionfinish(session, exitstatus):
     from tests import _parity_report
     _parity_report.dump()
@@ -46,6 +38,10 @@ def _restore_library_options():
     them) and a test that overrides one cannot leak it into the rest of the session."""
     from mpgnn_amd import _lib
     if not _DEFAULTS:
+        # MPGNN_GEMM_BF3=0|1: the whole session on the fp32-MFMA or the bf16-split GEMMs (A/B)
+        v = os.environ.get("MPGNN_GEMM_BF3")
+        if v is not None:
+            _lib.set_option(24, int(v))
         for o in _OPTIONS:
             try:
                 _DEFAULTS[o] = _lib.get_option(o)
