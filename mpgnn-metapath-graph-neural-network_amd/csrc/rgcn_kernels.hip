@@ -1645,23 +1645,33 @@ struct RelGemmBf3 {
         const int i_end = (int)((long long)(rng + 1) * n_items / G);
         if (i_beg >= i_end) return;
 
-        float4 v[WPT];
-        int cnt;
+        // A rows are gathered TWO items ahead (the bf16 chain of an item is 2.67x shorter than the
+        // fp32 one: one item of lead left the commit waiting on the gathers): rows of item i+1
+        // sit in one register set (committed three quarters into item i's chain), rows of item
+        // i+2 are issued into the other at the top of item i, and the row numbers of item i+3
+        // are loaded then. The two sets swap roles every item (the loop body is instantiated
+        // twice), so no register copy waits on loads in flight.
         const ItemTable tab = Base::item_table(a, i_beg, i_end, lane);
         auto get_item = [&](int i) { return i - i_beg < 64 ? Base::item_at(a, tab, i - i_beg) : Base::item(a, i); };
         Item cur = get_item(i_beg);
-        int zm = 0;
+        float4 va[WPT], vb[WPT];
+        int cnta = 1, cntb = 1, zm = 0;
         {
-            int crow[WPT];
-            Base::gather_idx(a, cur, tid, crow, cnt);
-            Base::issue_rows(a, tid, crow, v, zm);
+            int crow[WPT], c0;
+            Base::gather_idx(a, cur, tid, crow, c0);
+            Base::issue_rows(a, tid, crow, va, zm);
+            commit(cur, tid, va, c0, As, Sc);
         }
         int nrow[WPT];
         int ncnt = 1;
-        if (i_beg + 1 < i_end) Base::gather_idx(a, get_item(i_beg + 1), tid, nrow, ncnt);
+        if (i_beg + 1 < i_end) {
+            int r1[WPT];
+            Base::gather_idx(a, get_item(i_beg + 1), tid, r1, cnta);
+            Base::issue_rows(a, tid, r1, va, zm);
+        }
+        if (i_beg + 2 < i_end) Base::gather_idx(a, get_item(i_beg + 2), tid, nrow, ncnt);
         bf16x8 b[NS][3];
         load_b(cur.w, wave, lane, b);
-        commit(cur, tid, v, cnt, As, Sc);
         __syncthreads();
 
         constexpr int SPG = (16 + NS - 1) / NS;  // previous item's stores per k-step
@@ -1676,13 +1686,15 @@ struct RelGemmBf3 {
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(prev[r]), prev_rsrc, row * (N * 4) + col_b, 0, 0);
         };
         int buf = 0;
-        for (int i = i_beg; i < i_end; ++i) {
+        // item i: vc = rows of item i+1 (committed in this item), vn = receives rows of item i+2
+        auto step = [&](int i, float4 (&vc)[WPT], int& cntc, float4 (&vn)[WPT], int& cntn) {
             const bool has_next = i + 1 < i_end;
             const Item nxt = has_next ? get_item(i + 1) : cur;
-            if (has_next) {
-                Base::issue_rows(a, tid, nrow, v, zm);
-                cnt = ncnt;
-                if (i + 2 < i_end) Base::gather_idx(a, get_item(i + 2), tid, nrow, ncnt);
+            if (i + 2 < i_end) {
+                int zn;
+                Base::issue_rows(a, tid, nrow, vn, zn);
+                cntn = ncnt;
+                if (i + 3 < i_end) Base::gather_idx(a, get_item(i + 3), tid, nrow, ncnt);
             }
             const bool new_w = nxt.w != cur.w;
             const __bf16* Ab = As + buf * 3 * PLANE + c * LDAB + 8 * h;
@@ -1712,7 +1724,7 @@ struct RelGemmBf3 {
 #pragma unroll
                 for (int u = 0; u < SPG; ++u)
                     if (s * SPG + u < 16) store_prev(s * SPG + u);
-                if (s == kCommitAt - 1 && has_next) commit(nxt, tid, v, cnt, As + (buf ^ 1) * 3 * PLANE, Sc + (buf ^ 1) * 32);
+                if (s == kCommitAt - 1 && has_next) commit(nxt, tid, vc, cntc, As + (buf ^ 1) * 3 * PLANE, Sc + (buf ^ 1) * 32);
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
@@ -1731,6 +1743,10 @@ struct RelGemmBf3 {
             __syncthreads();
             cur = nxt;
             buf ^= 1;
+        };
+        for (int i = i_beg; i < i_end; i += 2) {
+            step(i, va, cnta, vb, cntb);
+            if (i + 1 < i_end) step(i + 1, vb, cntb, va, cnta);
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) store_prev(r);
