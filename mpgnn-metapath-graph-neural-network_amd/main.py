@@ -16,7 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from . import data as _data
-from .metrics import class_weight_balanced, f1_macro_many
+from .metrics import class_weight_balanced, confusion_counts_many, f1_from_counts, f1_macro_many
 from .model import MPNetm
 # score function helpers of main.py:387-760 (non-bag path, GPU kernels): same names
 from .score import (create_edge_dictionary, get_loss, get_loss_per_node, get_model, get_optimizer,  # noqa: F401
@@ -124,10 +124,8 @@ def take_rows(out: torch.Tensor, idx):
     return out[idx]
 
 
-def mpgnn_train(model, optimizer, data):
-    """main.py:1055-1082: full-batch forward, unweighted NLL on train_idx, backward, step.
-    Returns (float loss, balanced class weights) like the reference (the weights are
-    computed there but not applied, main.py:1065)."""
+def _train_step(model, optimizer, data):
+    """mpgnn_train's body with the loss left on the device (no host sync)."""
     model.train()
     optimizer.zero_grad()
     out = model(data.x, data.edge_index, data.edge_type)
@@ -135,7 +133,26 @@ def mpgnn_train(model, optimizer, data):
     loss = F.nll_loss(take_rows(out, data.train_idx).squeeze(-1), data.train_y)
     loss.backward()
     optimizer.step()
-    return float(loss.detach()), weights
+    return loss.detach(), weights
+
+
+def mpgnn_train(model, optimizer, data):
+    """main.py:1055-1082: full-batch forward, unweighted NLL on train_idx, backward, step.
+    Returns (float loss, balanced class weights) like the reference (the weights are
+    computed there but not applied, main.py:1065)."""
+    loss, weights = _train_step(model, optimizer, data)
+    return float(loss), weights
+
+
+@torch.no_grad()
+def _val_counts(model, data):
+    """mpgnn_validation's work on the device: (val loss, [2, 3, C] train / val confusion counts)."""
+    model.eval()
+    pred = model(data.x, data.edge_index, data.edge_type)
+    loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
+    c = _num_classes(pred)
+    return loss_val, confusion_counts_many([(torch.argmax(pred[data.train_idx], 1), data.train_y),
+                                            (torch.argmax(pred[data.val_idx], 1), data.val_y)], c)
 
 
 @torch.no_grad()
@@ -165,16 +182,15 @@ def _fit(data_mpgnn, input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, 
     model = MPNetm(input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, len(metapaths), metapaths)
     model = model.to(data_mpgnn.x.device)
     optimizer = _adam(model)
-    best_micro = 0.
-    best_model = model
+    best_model = model  # the reference keeps a reference, not a copy (main.py:1125)
     class_weight = None
-    f1_valt_macro = 0.
+    vcounts = None
+    # every epoch trains and scores the validation split on the device; only the last epoch's
+    # score is read by the host (its best-score test only re-assigns the same model object)
     for _epoch in range(1, epochs + 1):
-        _loss, class_weight = mpgnn_train(model, optimizer, data_mpgnn)
-        _train_acc, f1_val_macro, f1_valt_macro, _loss_val = mpgnn_validation(model, data_mpgnn, class_weight)
-        if f1_val_macro > best_micro:
-            best_micro = f1_val_macro
-            best_model = model  # the reference keeps a reference, not a copy (main.py:1125)
+        _loss, class_weight = _train_step(model, optimizer, data_mpgnn)
+        _loss_val, vcounts = _val_counts(model, data_mpgnn)
+    f1_valt_macro = f1_from_counts(vcounts)[1] if vcounts is not None else 0.
     return model, best_model, class_weight, f1_valt_macro
 
 

@@ -16,7 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from .main import _adam, _one_hot_colours, Data, get_edge_index_and_type_no_reverse, load_files, load_graph, take_rows  # noqa: F401
-from .metrics import class_weight_balanced, f1_macro_many
+from .metrics import class_weight_balanced, class_weight_tensor, confusion_counts_many, f1_from_counts, f1_macro_many
 from .model import Net
 
 __all__ = ["Data", "get_node_features", "mpgnn_train", "mpgnn_validation", "mpgnn_test", "mpgnn_parallel_multiple", "EPOCHS"]
@@ -35,18 +35,46 @@ def _forward(model, data):
     return model(data.x, data.edge_index, data.edge_type, **kw)
 
 
-def mpgnn_train(model, optimizer, data):
-    """main_rgcn.py:369-393: forward, NLL on train_idx weighted by the balanced class weights
-    (main_rgcn.py:376-380), backward, step → (float loss, weights)."""
+def _train_step(model, optimizer, data):
+    """The body of mpgnn_train with the loss left on the device (no host sync)."""
     model.train()
     optimizer.zero_grad()
     out = _forward(model, data)
     weights = class_weight_balanced(data.train_y)
-    weights_tensor = torch.tensor(weights, dtype=torch.float, device=out.device)
+    weights_tensor = class_weight_tensor(data.train_y, out.device)
     loss = F.nll_loss(take_rows(out, data.train_idx).squeeze(-1), data.train_y, weight=weights_tensor)
     loss.backward()
     optimizer.step()
-    return float(loss.detach()), weights
+    return loss.detach(), weights
+
+
+def mpgnn_train(model, optimizer, data):
+    """main_rgcn.py:369-393: forward, NLL on train_idx weighted by the balanced class weights
+    (main_rgcn.py:376-380), backward, step → (float loss, weights)."""
+    loss, weights = _train_step(model, optimizer, data)
+    return float(loss), weights
+
+
+@torch.no_grad()
+def _val_counts(model, data):
+    """mpgnn_validation's work, kept on the device: (val loss, [2, 3, C] confusion counts of the
+    train and validation predictions)."""
+    model.eval()
+    pred = _forward(model, data)
+    loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
+    c = int(pred.shape[1])
+    counts = confusion_counts_many([(torch.argmax(pred[data.train_idx], 1), data.train_y),
+                                    (torch.argmax(pred[data.val_idx], 1), data.val_y)], c)
+    return loss_val, counts
+
+
+@torch.no_grad()
+def _test_counts(model, data):
+    model.eval()
+    pred = _forward(model, data)
+    loss_test = F.nll_loss(pred[data.test_idx].squeeze(-1), data.test_y)
+    counts = confusion_counts_many([(torch.argmax(pred[data.test_idx], 1), data.test_y)], int(pred.shape[1]))
+    return loss_test, counts
 
 
 @torch.no_grad()
@@ -80,18 +108,21 @@ def mpgnn_parallel_multiple(data_mpgnn, input_dim, hidden_dim, num_rel, output_d
     model = Net(input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, metapath_length)
     model = model.to(data_mpgnn.x.device)
     optimizer = _adam(model)
-    best_micro = 0.
     best_model = model
     class_weight = None
+    # Every epoch runs what the reference runs (train, validation forward + scores, test forward
+    # + score) but leaves the scalars on the device: the host reads them only where the loop
+    # prints (every 10th epoch). best_model is the trained model object itself in the
+    # reference (main_rgcn.py:465-466 keeps a reference, not a copy), so its per-epoch
+    # best-score test changes nothing and needs no host read.
     for epoch in range(1, epochs + 1):
-        loss, class_weight = mpgnn_train(model, optimizer, data_mpgnn)
-        train_acc, f1_val_micro, f1_val_macro, loss_val = mpgnn_validation(model, data_mpgnn, class_weight)
-        test_loss, f1_micro_test = mpgnn_test(model, data_mpgnn, class_weight)
-        if f1_val_macro > best_micro:
-            best_micro = f1_val_macro
-            best_model = model
+        loss, class_weight = _train_step(model, optimizer, data_mpgnn)
+        loss_val, vcounts = _val_counts(model, data_mpgnn)
+        test_loss, tcounts = _test_counts(model, data_mpgnn)
         if verbose and epoch % 10 == 0:
-            print(epoch, "train loss %0.3f" % loss, "validation loss %0.3f" % loss_val,
+            train_acc, f1_val_micro = f1_from_counts(vcounts)
+            (f1_micro_test,) = f1_from_counts(tcounts)
+            print(epoch, "train loss %0.3f" % float(loss), "validation loss %0.3f" % loss_val,
                   "train micro: %0.3f" % train_acc, "validation micro: %0.3f" % f1_val_micro,
                   "test micro: %0.3f" % f1_micro_test)
     test_loss, f1_micro_test = mpgnn_test(best_model, data_mpgnn, class_weight)

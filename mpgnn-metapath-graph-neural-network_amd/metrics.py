@@ -16,7 +16,8 @@ import weakref
 import numpy as np
 import torch
 
-__all__ = ["f1_macro", "f1_macro_many", "class_weight_balanced"]
+__all__ = ["f1_macro", "f1_macro_many", "confusion_counts_many", "f1_from_counts", "class_weight_balanced",
+           "class_weight_tensor"]
 
 
 def _confusion_counts(pred: torch.Tensor, y: torch.Tensor, num_classes: int) -> torch.Tensor:
@@ -47,6 +48,18 @@ def f1_macro_many(pairs: list[tuple[torch.Tensor, torch.Tensor]], num_classes: i
     return [_finish(c) for c in counts]
 
 
+def confusion_counts_many(pairs: list[tuple[torch.Tensor, torch.Tensor]], num_classes: int) -> torch.Tensor:
+    """[len(pairs), 3, C] int64 confusion counts, left on the device (no host sync); finish
+    with ``f1_from_counts``."""
+    return torch.stack([_confusion_counts(p, y, num_classes) for p, y in pairs])
+
+
+def f1_from_counts(counts) -> list[float]:
+    """Macro F1 of each [3, C] count block (a device tensor is copied to the host here)."""
+    c = counts.cpu().numpy() if torch.is_tensor(counts) else np.asarray(counts)
+    return [_finish(x) for x in c]
+
+
 def f1_macro(pred: torch.Tensor, y: torch.Tensor, num_classes: int) -> float:
     """``sklearn.metrics.f1_score(pred, y, average='macro')`` (symmetric in its arguments)."""
     return f1_macro_many([(pred, y)], num_classes)[0]
@@ -56,6 +69,21 @@ def f1_macro(pred: torch.Tensor, y: torch.Tensor, num_classes: int) -> float:
 # OBJECT (a weakref that dies with it), not its address: a new label tensor landing at a
 # freed address must not hit a stale entry.
 _CW_LAST: list = [None, -1, None]
+
+
+_CWT_LAST: list = [None, -1, None, None]
+
+
+def class_weight_tensor(y: torch.Tensor, device) -> torch.Tensor:
+    """``torch.tensor(class_weight_balanced(y), dtype=float)`` on ``device`` (main_rgcn.py:376-379),
+    cached for the same label tensor (object and version): the per-epoch host-to-device copy of
+    the reference (a blocking copy) happens once."""
+    ref, ver, dev, t = _CWT_LAST
+    if ref is not None and ref() is y and ver == y._version and dev == str(device):
+        return t
+    t = torch.tensor(class_weight_balanced(y), dtype=torch.float, device=device)
+    _CWT_LAST[:] = [weakref.ref(y), y._version, str(device), t]
+    return t
 
 
 def class_weight_balanced(y: torch.Tensor) -> np.ndarray:
