@@ -2876,6 +2876,250 @@ __global__ __launch_bounds__(kThreads, 2) void outer_persist_kernel(OuterArgs ra
     }
 }
 
+// ----------------------------------------------------------------------------------------
+// outer_bf3_kernel — outer_persist_kernel's persistent chunk stream (same chunks, cursors,
+// destinations, bias column sums) for M = Nn = 128 on the bf16 matrix cores with the exact
+// three-way operand split of rel_gemm_bf3_kernel:  D[m][n] += Σ_p A[p][m] · B[p][n].
+// The K dimension of v_mfma_f32_32x32x16_bf16 runs over the chunk's ROWS, so both operands are
+// read "down a column": a slice of 16 rows is staged TRANSPOSED in LDS as three bf16 planes per
+// matrix, [128 columns][16 rows + 8 pad] (48-B column stride: the 16-B fragment reads and the
+// 16-B plane writes are bank-conflict-free). Thread t stages column t & 127 of rows
+// 8·(t >> 7) .. +8 of both matrices: the rows of a wave are uniform, so their bases come from
+// readlane (SGPRs) and every load is a coalesced 256-B row piece. Rows are fetched two slices
+// ahead (two register sets alternating roles), row indices three. Wave w owns output columns
+// [32w, 32w + 32) and all 128 m: 4 blocks × (hi, lo) accumulators; per 16 rows 24 MFMAs.
+// ----------------------------------------------------------------------------------------
+constexpr int kOb3Ld = 24;                  // bf16 per plane column: 16 rows + 8 pad
+constexpr int kOb3Plane = 128 * kOb3Ld;     // bf16 per plane
+constexpr size_t kOb3Lds = (size_t)2 * 6 * kOb3Plane * 2 + 256 * sizeof(float);  // 2 buffers × 6 planes + bias exchange
+
+__global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, OuterArgs wa, int ra_n, int n_all) {
+    constexpr int SL = 16;
+    extern __shared__ __attribute__((aligned(16))) __bf16 ob3_smem[];
+    __bf16* planes = ob3_smem;                                          // [2][A0 A1 A2 B0 B1 B2][128][24]
+    float* bx = reinterpret_cast<float*>(ob3_smem + 2 * 6 * kOb3Plane);  // [256] bias exchange
+    const int G = (int)gridDim.x;
+    if ((int)blockIdx.x >= n_all) return;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int c = lane & 31;
+    const int h = lane >> 5;
+    const int col = tid & 127;                                         // staged column
+    const int half = __builtin_amdgcn_readfirstlane(tid >> 7);         // staged rows 8·half .. +8 (uniform)
+
+    struct Src {
+        const float *A, *A2, *B;
+        const int *a_idx, *b_idx;
+        int a_off, a2_off;
+    };
+    auto src_of = [&](int chunk) {
+        const bool r = chunk < ra_n;
+        Src x;
+        x.A = r ? ra.A : wa.A;
+        x.A2 = r ? ra.A2 : wa.A2;
+        x.B = r ? ra.B : wa.B;
+        x.a_idx = r ? ra.a_idx : wa.a_idx;
+        x.b_idx = r ? ra.b_idx : wa.b_idx;
+        x.a_off = r ? ra.a_off : wa.a_off;
+        x.a2_off = r ? ra.a2_off : wa.a2_off;
+        return x;
+    };
+    auto open_chunk = [&](int chunk) {
+        OuterCursor k;
+        k.chunk = chunk;
+        k.sl = 0;
+        int p0 = 0, p1 = 0;
+        if (chunk < ra_n) {
+            p0 = ra.row_lo + chunk * ra.chunk_rows;
+            p1 = min(ra.row_hi, p0 + ra.chunk_rows);
+        } else if (chunk < n_all) {
+            p0 = ld_uniform(wa.chunk_begin, chunk - ra_n + wa.chunk_off);
+            p1 = ld_uniform(wa.chunk_end, chunk - ra_n + wa.chunk_off);
+        }
+        k.p0 = p0;
+        k.p1 = p1;
+        k.ns = (p1 - p0 + SL - 1) / SL;
+        return k;
+    };
+    auto advance = [&](const OuterCursor& k) {
+        if (k.sl + 1 < k.ns) {
+            OuterCursor n = k;
+            n.sl = k.sl + 1;
+            return n;
+        }
+        return open_chunk(k.chunk + G);
+    };
+    auto valid = [&](const OuterCursor& k) { return k.chunk < n_all && k.ns > 0; };
+
+    // row indices of a slice: lanes 0..7 of the wave hold those of its 8 staged rows
+    auto load_idx = [&](const OuterCursor& k, int& ia, int& ib) {
+        const Src a = src_of(k.chunk);
+        const int p = min(k.p0 + k.sl * SL + 8 * half + (lane & 7), max(k.p1 - 1, k.p0));
+        ib = a.b_idx != nullptr ? a.b_idx[p] : p;
+        ia = a.a_idx != nullptr ? a.a_idx[p] : p - a.a_off;
+    };
+    // rows of a slice into registers (row bases uniform: readlane of the index lanes)
+    auto issue = [&](const OuterCursor& k, int ia, int ib, float (&va)[8], float (&vb)[8]) {
+        const Src a = src_of(k.chunk);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int ra_ = __builtin_amdgcn_readlane(ia, j);
+            const int rb_ = __builtin_amdgcn_readlane(ib, j);
+            const float* arow = ra_ >= 0 ? a.A + (size_t)ra_ * 128 : a.A2 + (size_t)(-ra_ - 1 - a.a2_off) * 128;
+            va[j] = arow[col];
+            vb[j] = a.B[(size_t)rb_ * 128 + col];
+        }
+    };
+    // split + transposed store of one staged slice; rows past the chunk's end are zeros
+    auto commit = [&](const OuterCursor& k, const float (&va)[8], const float (&vb)[8], __bf16* buf) {
+        const int nr = min(SL, k.p1 - k.p0 - k.sl * SL) - 8 * half;  // live rows of this half (uniform)
+        bf16x8 pa[3], pb[3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float xa = j < nr ? va[j] : 0.0f;
+            const float xb = j < nr ? vb[j] : 0.0f;
+            __bf16 a0, a1, a2, b0, b1, b2;
+            split3_bf16(xa, a0, a1, a2);
+            split3_bf16(xb, b0, b1, b2);
+            pa[0][j] = a0; pa[1][j] = a1; pa[2][j] = a2;
+            pb[0][j] = b0; pb[1][j] = b1; pb[2][j] = b2;
+        }
+        __bf16* d = buf + col * kOb3Ld + 8 * half;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            *reinterpret_cast<bf16x8*>(d + q * kOb3Plane) = pa[q];
+            *reinterpret_cast<bf16x8*>(d + (3 + q) * kOb3Plane) = pb[q];
+        }
+    };
+
+    f32x16 hi[4], lo[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            hi[q][r] = 0.0f;
+            lo[q][r] = 0.0f;
+        }
+    float bpart = 0.0f;  // this thread's share of its column's bias sum (root chunks)
+
+    OuterCursor cur = open_chunk((int)blockIdx.x);
+    if (!valid(cur)) return;
+    OuterCursor c1 = advance(cur);                 // rows in set X during cur
+    OuterCursor c2 = valid(c1) ? advance(c1) : c1;  // rows issued into set Y during cur
+    OuterCursor c3 = valid(c2) ? advance(c2) : c2;  // indices loaded during cur
+    float xa[8], xb[8], ya[8], yb[8];
+    int ia, ib, ja = 0, jb = 0;
+    load_idx(cur, ia, ib);
+    issue(cur, ia, ib, xa, xb);
+    commit(cur, xa, xb, planes);
+    if (valid(c1)) {
+        load_idx(c1, ia, ib);
+        issue(c1, ia, ib, xa, xb);
+    }
+    if (valid(c2)) load_idx(c2, ja, jb);
+    __syncthreads();
+    int buf = 0;
+    // one slice: vn receives the rows of c2, vc (rows of c1) is committed after the MFMAs
+    auto step = [&](float (&vca)[8], float (&vcb)[8], float (&vna)[8], float (&vnb)[8]) -> bool {
+        const bool more = valid(c1);
+        if (valid(c2)) {
+            issue(c2, ja, jb, vna, vnb);
+            if (valid(c3)) load_idx(c3, ja, jb);
+        }
+        const bool is_root = cur.chunk < ra_n;
+        const __bf16* cb = planes + buf * 6 * kOb3Plane;
+        // B fragment (this wave's 32 columns) and per m-block A fragments, 6 products each
+        const __bf16* Bf = cb + 3 * kOb3Plane + (wave * 32 + c) * kOb3Ld + 8 * h;
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(Bf);
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(Bf + kOb3Plane);
+        const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(Bf + 2 * kOb3Plane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const __bf16* Af = cb + (q * 32 + c) * kOb3Ld + 8 * h;
+            const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Af);
+            const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Af + kOb3Plane);
+            const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(Af + 2 * kOb3Plane);
+            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, lo[q], 0, 0, 0);
+            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, lo[q], 0, 0, 0);
+            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, lo[q], 0, 0, 0);
+            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, lo[q], 0, 0, 0);
+            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, lo[q], 0, 0, 0);
+            hi[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, hi[q], 0, 0, 0);
+        }
+        if (is_root && ra.Pb != nullptr) {  // bias: the column sum of dout over the chunk's rows
+            const int nr = min(SL, cur.p1 - cur.p0 - cur.sl * SL) - 8 * half;
+            // this thread's column over its 8 rows of cur's slice, rebuilt exactly from the three
+            // pieces in LDS ((b0 + b1) + b2 == b: the partial sums of the split are representable)
+            const __bf16* bc = cb + 3 * kOb3Plane + col * kOb3Ld + 8 * half;
+            const bf16x8 q0 = *reinterpret_cast<const bf16x8*>(bc);
+            const bf16x8 q1 = *reinterpret_cast<const bf16x8*>(bc + kOb3Plane);
+            const bf16x8 q2 = *reinterpret_cast<const bf16x8*>(bc + 2 * kOb3Plane);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < nr) bpart += ((float)q0[j] + (float)q1[j]) + (float)q2[j];
+        }
+        const bool chunk_end = cur.sl + 1 == cur.ns;
+        if (more) commit(c1, vca, vcb, planes + (buf ^ 1) * 6 * kOb3Plane);
+        if (chunk_end) {
+            float* D;
+            float* Db = nullptr;
+            if (is_root) {
+                const int cidx = cur.chunk;
+                D = ra.P + (size_t)cidx * 128 * 128;
+                Db = ra.Pb != nullptr ? ra.Pb + (size_t)cidx * 128 : nullptr;
+                if (ra.dst_mode == 3) {
+                    D = ra.dst;
+                    Db = ra.dst_b;
+                }
+            } else {
+                const int cidx = cur.chunk - ra_n;
+                D = wa.P + (size_t)cidx * 128 * 128;
+                if (wa.dst_mode == 1 || wa.dst_mode == 2) {
+                    const int di = ld_uniform(wa.chunk_dst, cidx + wa.chunk_off);
+                    if (di >= 0) D = wa.dst + (size_t)(wa.dst_mode == 1 ? di : 0) * 128 * 128;
+                }
+            }
+            const int ln = opaque(lane);
+            const int ocol = wave * 32 + (ln & 31);
+            const int h4 = 4 * (ln >> 5);
+            if (D != nullptr) {  // (a bias-only root part has no weight destination)
+                float* Dc = D + ocol;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = q * 32 + (r & 3) + 8 * (r >> 2) + h4;
+                        Dc[(size_t)m * 128] = hi[q][r] + lo[q][r];
+                    }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    hi[q][r] = 0.0f;
+                    lo[q][r] = 0.0f;
+                }
+            if (is_root && ra.Pb != nullptr) {  // the two row-halves of each column, in order
+                bx[tid] = bpart;
+                bpart = 0.0f;
+                __syncthreads();
+                if (tid < 128 && Db != nullptr) Db[tid] = bx[tid] + bx[tid + 128];
+            }
+        }
+        __syncthreads();
+        if (!more) return false;
+        cur = c1;
+        c1 = c2;
+        c2 = c3;
+        c3 = valid(c3) ? advance(c3) : c3;
+        buf ^= 1;
+        return true;
+    };
+    while (step(xa, xb, ya, yb) && step(ya, yb, xa, xb)) {
+    }
+}
+
 // dst[group g] (elems floats) = Σ_{c in chunks of g, ascending} P[c]
 struct ReduceArgs {
     const float* P;
@@ -4720,7 +4964,14 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
         }
     }
     const int root_y = grad_root ? mt : 1;
-    if (have_w && have_root && root_y == mt) {
+    if (have_w && have_root && root_y == mt && g_gemm_bf3 && F_in == 128 && F_out == 128) {
+        // F_in = F_out = 128: the bf16-split persistent kernel (outer_bf3_kernel)
+        TimedLaunch tl(MPGNN_K_OUTER, strm);
+        const int n_all = nch + rc.n;
+        const int gx = std::max(1, std::min(n_all, cu_count() * 2));
+        hipLaunchKernelGGL(outer_bf3_kernel, dim3(gx), dim3(kThreads), kOb3Lds, strm, orr, ow, rc.n, n_all);
+        if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel launch")) != MPGNN_OK) return st;
+    } else if (have_w && have_root && root_y == mt) {
         TimedLaunch tl(MPGNN_K_OUTER, strm);
         // one launch: root chunks (all full length; the relation chunks of small relations are
         // short) dispatched first so they are not the launch's tail, 16-row LDS slices

@@ -111,6 +111,51 @@ def _adam(model):
     return torch.optim.Adam(params, lr=0.01, weight_decay=0.0005, fused=fused)
 
 
+def _adam_graphable(model):
+    """``_adam`` for a captured epoch: fused and capturable (the step counter on the device);
+    the same update rule."""
+    params = list(model.parameters())
+    return torch.optim.Adam(params, lr=0.01, weight_decay=0.0005, fused=True, capturable=True)
+
+
+def _graphs_enabled(data) -> bool:
+    import os
+    return (os.environ.get("MPGNN_LOOP_GRAPH", "1") != "0" and torch.cuda.is_available() and data.x.is_cuda
+            and not getattr(data, "shard_kw", None))
+
+
+def _epochs(epoch_fn, epochs: int, use_graph: bool, warmup: int = 3):
+    """Run ``epoch_fn`` ``epochs`` times, yielding (epoch, outputs). With ``use_graph`` the first
+    ``warmup`` epochs run eagerly on a side stream, then ONE epoch is captured as a HIP graph
+    (nothing executes during the capture) and replayed for the remaining epochs: every epoch
+    still runs every kernel of the reference's epoch, the host only issues one launch per
+    epoch. Falls back to eager epochs if the capture fails."""
+    if not use_graph or epochs <= warmup:
+        for e in range(1, epochs + 1):
+            yield e, epoch_fn()
+        return
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for e in range(1, warmup + 1):
+            out = epoch_fn()
+            yield e, out
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(graph, stream=side):
+            static = epoch_fn()
+    except Exception:  # capture unsupported here: the remaining epochs run eagerly
+        graph = None
+        torch.cuda.synchronize()
+    for e in range(warmup + 1, epochs + 1):
+        if graph is None:
+            yield e, epoch_fn()
+        else:
+            graph.replay()
+            yield e, static
+
+
 def _num_classes(out: torch.Tensor) -> int:
     return int(out.shape[1]) if out.dim() > 1 else 1
 
@@ -181,15 +226,22 @@ def mpgnn_test(model, data, class_weight):
 def _fit(data_mpgnn, input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, metapaths, epochs):
     model = MPNetm(input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, len(metapaths), metapaths)
     model = model.to(data_mpgnn.x.device)
-    optimizer = _adam(model)
+    optimizer = None if _graphs_enabled(data_mpgnn) else _adam(model)
     best_model = model  # the reference keeps a reference, not a copy (main.py:1125)
-    class_weight = None
+    use_graph = _graphs_enabled(data_mpgnn)
+    if use_graph:
+        optimizer = _adam_graphable(model)
+    class_weight = class_weight_balanced(data_mpgnn.train_y)
     vcounts = None
+
     # every epoch trains and scores the validation split on the device; only the last epoch's
     # score is read by the host (its best-score test only re-assigns the same model object)
-    for _epoch in range(1, epochs + 1):
-        _loss, class_weight = _train_step(model, optimizer, data_mpgnn)
-        _loss_val, vcounts = _val_counts(model, data_mpgnn)
+    def epoch():
+        loss, _ = _train_step(model, optimizer, data_mpgnn)
+        return (loss,) + _val_counts(model, data_mpgnn)
+
+    for _epoch, (_loss, _loss_val, vcounts) in _epochs(epoch, epochs, use_graph):
+        pass
     f1_valt_macro = f1_from_counts(vcounts)[1] if vcounts is not None else 0.
     return model, best_model, class_weight, f1_valt_macro
 

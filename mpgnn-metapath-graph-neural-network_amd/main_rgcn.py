@@ -15,7 +15,8 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-from .main import _adam, _one_hot_colours, Data, get_edge_index_and_type_no_reverse, load_files, load_graph, take_rows  # noqa: F401
+from .main import (_adam, _adam_graphable, _epochs, _graphs_enabled, _one_hot_colours, Data,  # noqa: F401
+                   get_edge_index_and_type_no_reverse, load_files, load_graph, take_rows)
 from .metrics import class_weight_balanced, class_weight_tensor, confusion_counts_many, f1_from_counts, f1_macro_many
 from .model import Net
 
@@ -107,18 +108,21 @@ def mpgnn_parallel_multiple(data_mpgnn, input_dim, hidden_dim, num_rel, output_d
     as in the reference)."""
     model = Net(input_dim, hidden_dim, num_rel, output_dim, ll_output_dim, metapath_length)
     model = model.to(data_mpgnn.x.device)
-    optimizer = _adam(model)
+    use_graph = _graphs_enabled(data_mpgnn)
+    optimizer = _adam_graphable(model) if use_graph else _adam(model)
     best_model = model
-    class_weight = None
+    class_weight = class_weight_balanced(data_mpgnn.train_y)
     # Every epoch runs what the reference runs (train, validation forward + scores, test forward
     # + score) but leaves the scalars on the device: the host reads them only where the loop
     # prints (every 10th epoch). best_model is the trained model object itself in the
     # reference (main_rgcn.py:465-466 keeps a reference, not a copy), so its per-epoch
     # best-score test changes nothing and needs no host read.
-    for epoch in range(1, epochs + 1):
-        loss, class_weight = _train_step(model, optimizer, data_mpgnn)
-        loss_val, vcounts = _val_counts(model, data_mpgnn)
-        test_loss, tcounts = _test_counts(model, data_mpgnn)
+    # (one HIP graph per epoch after three eager ones: main._epochs)
+    def epoch_fn():
+        loss, _ = _train_step(model, optimizer, data_mpgnn)
+        return (loss,) + _val_counts(model, data_mpgnn) + _test_counts(model, data_mpgnn)
+
+    for epoch, (loss, loss_val, vcounts, test_loss, tcounts) in _epochs(epoch_fn, epochs, use_graph):
         if verbose and epoch % 10 == 0:
             train_acc, f1_val_micro = f1_from_counts(vcounts)
             (f1_micro_test,) = f1_from_counts(tcounts)

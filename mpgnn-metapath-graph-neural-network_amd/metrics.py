@@ -20,14 +20,24 @@ __all__ = ["f1_macro", "f1_macro_many", "confusion_counts_many", "f1_from_counts
            "class_weight_tensor"]
 
 
+def _count(v: torch.Tensor, bins: int) -> torch.Tensor:
+    """bincount of values in [0, bins) (integer scatter-add: exact, and no host read of the
+    maximum — torch.bincount's size query — so it can run inside a HIP-graph capture)."""
+    out = torch.zeros(bins, dtype=torch.int64, device=v.device)
+    return out.scatter_add_(0, v, torch.ones_like(v))
+
+
 def _confusion_counts(pred: torch.Tensor, y: torch.Tensor, num_classes: int) -> torch.Tensor:
-    """[3, C] int64: (count of each label in pred, in y, agreeing positions per label)."""
+    """[3, C] int64: (count of each label in pred, in y, agreeing positions per label). Labels
+    outside [0, C) fall in an overflow bin (nll_loss rejects them before this runs)."""
     pred = pred.reshape(-1).to(torch.int64)
     y = y.reshape(-1).to(device=pred.device, dtype=torch.int64)
-    hit = torch.where(pred == y, y, torch.full_like(y, num_classes))  # misses → overflow bin
-    return torch.stack([torch.bincount(pred, minlength=num_classes)[:num_classes],
-                        torch.bincount(y, minlength=num_classes)[:num_classes],
-                        torch.bincount(hit, minlength=num_classes + 1)[:num_classes]])
+    c = num_classes
+    over = torch.full_like(y, c)
+    pred_c = torch.where((pred >= 0) & (pred < c), pred, over)
+    y_c = torch.where((y >= 0) & (y < c), y, over)
+    hit = torch.where(pred_c == y_c, y_c, over)  # misses → overflow bin
+    return torch.stack([_count(pred_c, c + 1)[:c], _count(y_c, c + 1)[:c], _count(hit, c + 1)[:c]])
 
 
 def _finish(counts: np.ndarray) -> float:

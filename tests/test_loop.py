@@ -314,3 +314,21 @@ def test_metapath_fanout_single_rank_trains_each_candidate(golden):
     best = mdist.best_metapaths(scores, k=1)
     assert scores[str(planted)] == max(scores.values()), scores
     assert list(best) == [str(planted)] or scores[list(best)[0]] == scores[str(planted)]
+
+
+@pytest.mark.gpu
+def test_rgcn_loop_graph_replay_equals_eager(capsys, monkeypatch):
+    """mpgnn_parallel_multiple (main_rgcn.py:452-472) replays one captured HIP graph per epoch
+    after three eager ones (main._epochs): Net has no dropout, so the replayed epochs compute
+    exactly what the eager loop computes — the printed losses / scores and the returned test F1
+    are identical with MPGNN_LOOP_GRAPH=0 and =1."""
+    g = data.config_graph("C1")
+    d = _task(g).to(DEV)
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MPGNN_LOOP_GRAPH", flag)
+        torch.manual_seed(30)
+        f1 = main_rgcn.mpgnn_parallel_multiple(d, 128, 64, g.num_relations, 64, 3, 2, epochs=30)
+        outs.append((f1, capsys.readouterr().out))
+    assert outs[0] == outs[1], outs
+    assert outs[0][1].count("train loss") == 3
