@@ -309,7 +309,7 @@ def time_drop_in_loop(single, g, x, ei, et, F, layers, metapath, epochs, shard_k
         torch.cuda.synchronize()
         return time.perf_counter() - t0, score
 
-    run(2)  # warm-up (plan cached, allocator and kernels warm)
+    run(6)  # warm-up: plan cached, allocator and kernels warm, one graph capture done (graph pool)
     # the loops run their first 3 epochs eagerly and replay one captured epoch after that
     # (main._epochs): t(6 + K) - t(6) holds K steady-state epochs, the capture cancels
     t1, _ = timed(6)
