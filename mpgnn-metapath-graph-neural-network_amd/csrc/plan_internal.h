@@ -59,9 +59,10 @@ struct RaggedHost {
 //     split chunks: their partials go to global carry slots that finalize_rows_kernel adds in
 //     chunk order.
 constexpr int kFlatChunk = 32;
-// The row-major (combine) lists have few positions (S + N ≈ 63 k at C3 vs E = 310 k for the
-// means), so they are cut finer to give the combine launch enough waves: 11.7 → 10.6 µs.
-constexpr int kFlatChunkRowMajor = 16;
+// The row-major (combine) lists: measured on the C3 survey graph (S + N = 222 k positions,
+// ~15 per row) with the bf16-split GEMM, 16 / 32 / 48 / 64 positions per chunk: combine
+// 26.7 / 22.7 / 23.2 / 24.5 µs (round 2 chose 16 on the 63 k-position graph of round 1)
+constexpr int kFlatChunkRowMajor = 32;
 constexpr int kFlatGroup = 4;         // chunks per normal group (= waves per workgroup)
 constexpr int kFlatLongPieces = 16;   // pieces a long group sums in LDS (<= 16 · F floats); more
                                       // pieces serialise too much in one workgroup (C3 grad_x hubs:

@@ -14,7 +14,7 @@ import numpy as np
 
 TILE_ROWS = 64
 FLAT_CHUNK = 32
-FLAT_CHUNK_ROW_MAJOR = 16  # the row-major (combine) list (plan_internal.h kFlatChunkRowMajor)
+FLAT_CHUNK_ROW_MAJOR = 32  # the row-major (combine) list (plan_internal.h kFlatChunkRowMajor)
 FLAT_GROUP = 4             # chunks per normal workgroup group (kFlatGroup)
 FLAT_LONG_PIECES = 16      # pieces of a run one workgroup sums in LDS (kFlatLongPieces)
 

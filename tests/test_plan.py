@@ -143,7 +143,7 @@ def test_plan_cache_reuses_and_invalidates():
 @pytest.mark.parametrize("shard", [None, (0.3, 0.7)])
 def test_flat_lists_bit_exact_and_well_formed(case, shard):
     """Flat chunked lists (fast-path row sums) == the numpy restatement, and well formed:
-    chunks of 1..32 (16) positions covering every position once, cut at row ends; a row longer
+    chunks of 1..32 positions covering every position once, cut at row ends; a row longer
     than a chunk is cut into pieces holding only that row; groups of <= 4 chunks of complete
     rows, or the 2..16 pieces of one row (long group); rows of more pieces have one global carry
     slot per piece."""
@@ -160,7 +160,7 @@ def test_flat_lists_bit_exact_and_well_formed(case, shard):
     for tname in FLAT:
         got = plan.table(tname)
         assert np.array_equal(got, ref[tname]), tname
-    for l, run_ptr, chunk in (("seg", ref["s_ptr"], 32), ("t", ref["t_ptr"], 32), ("rw", ref["rw_ptr"], 16),
+    for l, run_ptr, chunk in (("seg", ref["s_ptr"], 32), ("t", ref["t_ptr"], 32), ("rw", ref["rw_ptr"], 32),
                               ("segm", ref["m_ptr"], 32)):
         cp = plan.table(f"{l}_f_chunk_ptr")
         sizes = np.diff(cp)
