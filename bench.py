@@ -570,7 +570,9 @@ def main():
     # mode SINGLE at F = 256 (rgcn_kernels.hip root_epi): root items finish the segment-less rows
     root_epi = bool(single and F == 256 and world == 1)
     kinds = {"mean": "segment means (flat_rows_kernel over the multi-edge segments)",
-             "seg_fwd": "transform GEMM (rel_gemm_kernel)",
+             "seg_fwd": ("split-K transform GEMM of the whole layer (single_bf3_kernel)"
+                         if single and args.gemm == "bf3" and F in (64, 128) and world == 1 else
+                         "transform GEMM (rel_gemm_bf3_kernel / rel_gemm_kernel)"),
              "row_fwd": (("rows with a segment: single_fix_kernel (the root items' epilogue finished the others)"
                           if root_epi else "combine / output (single_combine_kernel: node -> segment map, one "
                           "streaming pass)") if single else
@@ -612,7 +614,9 @@ def main():
                     ("hbm", (S + n_rows) * (4.0 * F + 4) + n_rows * 4.0 * F, "(S + N)·(4F + 4) Y / Y_root rows + ids "
                      "gathered, N·4F output rows written")),
     }
-    bf3 = args.gemm == "bf3" and not single and F in (64, 128)  # rel_gemm_bf3_kernel runs the transform
+    # the transform on the bf16-split matrix cores: rel_gemm_bf3_kernel (mode ALL), mode SINGLE
+    # unsharded: single_bf3_kernel (split-K: x @ root and mean @ W halves, one launch per layer)
+    bf3 = args.gemm == "bf3" and F in (64, 128) and (not single or world == 1)
     rooflines = []
     for kind, (bound, work, model_txt) in model_costs.items():
         if kind not in per_layer:
@@ -636,7 +640,8 @@ def main():
         else:
             ach = work / (us * 1e-6) / 1e9
             peak, unit = PEAK_HBM, "GB/s"
-        kname = {"seg_fwd": "rel_gemm_bf3_kernel" if bf3 else "rel_gemm_kernel", "mean": "flat_rows_kernel",
+        seg_name = "single_bf3_kernel" if bf3 and single else "rel_gemm_bf3_kernel" if bf3 else "rel_gemm_kernel"
+        kname = {"seg_fwd": seg_name, "mean": "flat_rows_kernel",
                  "row_fwd": ("single_fix_kernel" if root_epi else "single_combine_kernel") if single
                  else "flat_rows_kernel"}[kind]
         rooflines.append({"kind": kind, "kernel": kname, "bound": bound, "achieved": round(ach, 2), "peak": peak,

@@ -1759,6 +1759,187 @@ __global__ __launch_bounds__(kThreads, 2) void rel_gemm_bf3_kernel(RelGemmArgs a
     RelGemmBf3<KB, DGRAD>::run(a, smem_bf);
 }
 
+// ----------------------------------------------------------------------------------------
+// single_bf3_kernel — the whole unsharded mode-SINGLE layer (CustomRGCNConv over one relation,
+// mp_rgcn_layer.py:231-268, + the model's ReLU) in one launch on the bf16 matrix cores:
+//     out[i] = act((mean_i @ W + x_i @ root) + bias)      mean_i = 0 without a segment
+// in the reference's association (out = h @ W; out += x @ root; out += bias). A node has at
+// most one segment of the relation, so a 32-row item of node rows needs no combine. The
+// workgroup's eight waves split K: waves 0-3 hold the root slice and multiply the item's x
+// rows, waves 4-7 hold the W slice and multiply its mean rows (node_map: x row, compact mean
+// Hm row, or none), each over 32 columns with rel_gemm_bf3_kernel's exact three-piece split
+// (six products, fp32 accumulation); the mean half hands its tile to the x half through LDS,
+// which adds, finishes and stores. Persistent over items; the rows of item i+1 are gathered
+// during item i, their node_map entries one item earlier still.
+//   C3 (455 items of 32 rows): one item per workgroup is latency, not MFMA, bound — the split
+//   halves each wave's chain and the bf16 pieces cut it 2.67x against the fp32 K = 256 chain.
+// ----------------------------------------------------------------------------------------
+struct SingleBf3Args {
+    const float* x;       // [N][K]
+    const float* H;       // compact means, row m - m_lo
+    const int* node_map;  // [N]: s_src + 1 (x row), s_src (< 0: Hm row), 0 (no segment)
+    int m_lo, m_rows, N;
+    const float* W;       // [K][128]
+    const float* root;    // [K][128]
+    const float* bias;    // nullable [128]
+    int relu;
+    float* out;           // [N][128]
+};
+
+constexpr int kSingleThreads = 512;
+
+template <int KB>
+struct SingleBf3 {
+    using Gemm = RelGemmBf3<KB, false>;
+    static constexpr int K = 64 * KB, N = 128, NS = K / 16, LDAB = K + 8, PLANE = 32 * LDAB;
+    static constexpr int W4 = K / 4;              // float4 per row
+    static constexpr int WPT = 32 * W4 / 256;     // float4 per thread of a half
+    static constexpr int LDO = N + 4;             // fp32 row stride of the exchanged tile
+    static constexpr size_t lds_bytes() { return (size_t)6 * PLANE * 2 + (size_t)32 * LDO * sizeof(float); }
+
+    // per-thread state of one item: thread t of a half holds float4 (t + 256 j) of its 32 x K tile
+    struct Rows {
+        int mp[WPT];
+        float4 v[WPT];
+    };
+    // the mean half's node_map entries of item it
+    __device__ static __forceinline__ void load_map(const SingleBf3Args& a, int it, bool mh, int t, Rows& q) {
+        if (mh) {
+#pragma unroll
+            for (int j = 0; j < WPT; ++j) q.mp[j] = a.node_map[min(it * 32 + (t + j * 256) / W4, a.N - 1)];
+        }
+    }
+    // x rows (x half) or mean rows (mean half: x row, compact mean row, or zeros) of item it;
+    // indices are clamped into the tables: a bad map cannot fault
+    __device__ static __forceinline__ void issue(const SingleBf3Args& a, int it, bool mh, int t, Rows& q) {
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+            const int e = t + j * 256;
+            const int row = min(it * 32 + e / W4, a.N - 1);
+            const int c4 = (e % W4) * 4;
+            const float* base;
+            bool zero = false;
+            if (!mh) {
+                base = a.x + (size_t)row * K;
+            } else {
+                const int m = q.mp[j];
+                zero = m == 0;
+                base = m > 0 ? a.x + (size_t)min(m - 1, a.N - 1) * K
+                             : a.H + (size_t)min(max(-m - 1 - a.m_lo, 0), max(a.m_rows - 1, 0)) * K;
+                if (zero) base = a.x;
+            }
+            q.v[j] = *reinterpret_cast<const float4*>(base + c4);
+            if (zero) q.v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    // the half's tile as three bf16 planes (rows past N: zeros)
+    __device__ static __forceinline__ void commit(const SingleBf3Args& a, int it, bool mh, int t, const Rows& q,
+                                                  __bf16* smem) {
+        __bf16* P = smem + (mh ? 3 * PLANE : 0);
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+            const int e = t + j * 256;
+            const int r = e / W4;
+            const float4 xv = it * 32 + r < a.N ? q.v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            __bf16 p0[4], p1[4], p2[4];
+            split3_bf16(xv.x, p0[0], p1[0], p2[0]);
+            split3_bf16(xv.y, p0[1], p1[1], p2[1]);
+            split3_bf16(xv.z, p0[2], p1[2], p2[2]);
+            split3_bf16(xv.w, p0[3], p1[3], p2[3]);
+            __bf16* d = P + r * LDAB + (e % W4) * 4;
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<bf16x4*>(d) = bf16x4{p0[0], p0[1], p0[2], p0[3]};
+            *reinterpret_cast<bf16x4*>(d + PLANE) = bf16x4{p1[0], p1[1], p1[2], p1[3]};
+            *reinterpret_cast<bf16x4*>(d + 2 * PLANE) = bf16x4{p2[0], p2[1], p2[2], p2[3]};
+        }
+    }
+    // the wave's 32 x 32 product of its half's tile (committed, barrier passed) with its slice
+    __device__ static __forceinline__ f32x16 chain(bool mh, int c, int h, const __bf16* smem, const bf16x8 (&b)[NS][3]) {
+        const __bf16* Ab = smem + (mh ? 3 * PLANE : 0) + c * LDAB + 8 * h;
+        f32x16 hi, lo;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            hi[r] = 0.0f;
+            lo[r] = 0.0f;
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Ab + 16 * s);
+            const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Ab + PLANE + 16 * s);
+            const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * PLANE + 16 * s);
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[s][0], lo, 0, 0, 0);
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][1], lo, 0, 0, 0);
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][2], lo, 0, 0, 0);
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][0], lo, 0, 0, 0);
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][1], lo, 0, 0, 0);
+            hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][0], hi, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) hi[r] = hi[r] + lo[r];
+        return hi;
+    }
+    // mean half: its tile into LDS (before a barrier); x half (after it): (mean@W + x@root) + bias, act, store
+    __device__ static __forceinline__ void put_mean(int col, int h, const f32x16& acc, __bf16* smem) {
+        float* Ot = reinterpret_cast<float*>(smem + 6 * PLANE);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Ot[((r & 3) + 8 * (r >> 2) + 4 * h) * LDO + col] = acc[r];
+    }
+    __device__ static __forceinline__ void finish(const SingleBf3Args& a, int it, int col, int h, float bcol,
+                                                  const f32x16& acc, const __bf16* smem) {
+        const float* Ot = reinterpret_cast<const float*>(smem + 6 * PLANE);
+        const int r0 = it * 32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            float o = (Ot[row * LDO + col] + acc[r]) + bcol;
+            if (a.relu) o = relu_f(o);
+            if (r0 + row < a.N) a.out[(size_t)(r0 + row) * N + col] = o;
+        }
+    }
+};
+
+template <int KB>
+__global__ __launch_bounds__(kSingleThreads, 1) void single_bf3_kernel(SingleBf3Args a) {
+    using S = SingleBf3<KB>;
+    extern __shared__ __bf16 smem_bf[];
+    const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool mh = wave >= 4;  // wave-uniform: the mean half
+    const int t = tid & 255;    // thread within its half
+    const int wq = wave & 3;    // column block of the wave
+    const int n_items = (a.N + 31) / 32;
+    const int G = (int)gridDim.x;
+    const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
+    const int rng = g * q + min(g, rem) + ((int)blockIdx.x >> 3);  // consecutive items on one XCD
+    const int i_beg = (int)((long long)rng * n_items / G);
+    const int i_end = (int)((long long)(rng + 1) * n_items / G);
+    if (i_beg >= i_end) return;
+
+    typename S::Rows rows;
+    S::load_map(a, i_beg, mh, t, rows);
+    S::issue(a, i_beg, mh, t, rows);
+    if (i_beg + 1 < i_end) S::load_map(a, i_beg + 1, mh, t, rows);
+    bf16x8 b[S::NS][3];
+    S::Gemm::load_b(mh ? a.W : a.root, wq, lane, b);
+    S::commit(a, i_beg, mh, t, rows, smem_bf);
+    if (i_beg + 1 < i_end) S::issue(a, i_beg + 1, mh, t, rows);
+    if (i_beg + 2 < i_end) S::load_map(a, i_beg + 2, mh, t, rows);
+    const int col = wq * 32 + c;
+    const float bcol = a.bias != nullptr ? a.bias[col] : 0.0f;
+    __syncthreads();
+
+    for (int i = i_beg; i < i_end; ++i) {
+        const f32x16 acc = S::chain(mh, c, h, smem_bf, b);
+        if (mh) S::put_mean(col, h, acc, smem_bf);
+        __syncthreads();  // the mean tile is in LDS; both A tiles are free
+        if (!mh) S::finish(a, i, col, h, bcol, acc, smem_bf);
+        if (i + 1 < i_end) S::commit(a, i + 1, mh, t, rows, smem_bf);
+        if (i + 2 < i_end) S::issue(a, i + 2, mh, t, rows);
+        if (i + 3 < i_end) S::load_map(a, i + 3, mh, t, rows);
+        __syncthreads();  // the next item's A tiles are in LDS; the mean tile is free
+    }
+}
+
 template <int KB>  // Kp = 64·KB
 __global__ __launch_bounds__(kThreads, 2) void tile_gemm_kernel(TileGemmArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -2098,10 +2279,9 @@ struct FinalArgs {
     int relu;              // fused activation after the bias
 };
 
+// one wave, work index w (mode 0: split row k0 + w; mode 1: row r_lo + w)
 template <int V, int T>
-__global__ __launch_bounds__(kThreads) void finalize_rows_kernel(FinalArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int w = (int)blockIdx.x * kWaves + (int)(threadIdx.x >> 6);
+__device__ __forceinline__ void finalize_row(const FinalArgs& a, int w, int lane) {
     const int F = a.F;
     int row, k;
     if (a.mode == 0) {
@@ -2176,6 +2356,12 @@ __global__ __launch_bounds__(kThreads) void finalize_rows_kernel(FinalArgs a) {
         }
     }
 }
+
+template <int V, int T>
+__global__ __launch_bounds__(kThreads) void finalize_rows_kernel(FinalArgs a) {
+    finalize_row<V, T>(a, (int)blockIdx.x * kWaves + (int)(threadIdx.x >> 6), (int)(threadIdx.x & 63));
+}
+
 
 // ----------------------------------------------------------------------------------------
 // gather_rows_kernel — the row-sum / segment-mean gather for F % 4 == 0 (any summation
@@ -4472,13 +4658,40 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     }
     if (cat) {
         float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
+        const int* nmap = nullptr;
+        if ((st = relation_node_map(&nmap)) != MPGNN_OK) return st;
+        if (g_gemm_bf3) {  // split-K layer on the bf16 matrix cores
+            SingleBf3Args sa{};
+            sa.x = x;
+            sa.H = H;
+            sa.node_map = nmap;
+            sa.m_lo = s.m_lo;
+            sa.m_rows = std::max(s.m_hi - s.m_lo, 1);
+            sa.N = (int)p->N;
+            sa.W = weight;
+            sa.root = root;
+            sa.bias = bias;
+            sa.relu = act == MPGNN_ACT_RELU;
+            sa.out = out;
+            const int n_gi = (int)((p->N + 31) / 32);
+            {
+                TimedLaunch tl(MPGNN_K_MEAN, strm);
+                st = run_means_multi(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
+                if (st != MPGNN_OK) return st;
+            }
+            const int grid = (int)std::min<int64_t>(n_gi, cu_count());
+            TimedLaunch tl(MPGNN_K_SEG_FWD, strm);
+            if (F_in == 64)
+                hipLaunchKernelGGL(single_bf3_kernel<1>, dim3(grid), dim3(kSingleThreads), SingleBf3<1>::lds_bytes(), strm, sa);
+            else
+                hipLaunchKernelGGL(single_bf3_kernel<2>, dim3(grid), dim3(kSingleThreads), SingleBf3<2>::lds_bytes(), strm, sa);
+            return hip_check(hipGetLastError(), "single_bf3_kernel launch");
+        }
         {
             TimedLaunch tl(MPGNN_K_MEAN, strm);
             st = run_means_multi(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
             if (st != MPGNN_OK) return st;
         }
-        const int* nmap = nullptr;
-        if ((st = relation_node_map(&nmap)) != MPGNN_OK) return st;
         RelGemmArgs r{};
         r.n_rel = 0;
         r.n_root = (int)((p->N + 31) / 32);

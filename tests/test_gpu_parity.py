@@ -965,9 +965,13 @@ def test_mode_single_full_size_c2_fwd_bwd():
 
 
 @pytest.mark.parametrize("f_in", [64, 128])
-def test_fused_single_layer_absent_relation_and_relu(f_in):
-    """The fused mode-SINGLE GEMM with an absent relation (every node row is [x_i | 0]) and with
-    the ReLU epilogue: x @ root + bias, and relu(layer) of the oracle."""
+@pytest.mark.parametrize("bf3", [1, 0])
+def test_fused_single_layer_absent_relation_and_relu(f_in, bf3):
+    """The fused mode-SINGLE layer with an absent relation (every node row is [x_i | 0]) and with
+    the ReLU epilogue: x @ root + bias, and relu(layer) of the oracle — on the split-K bf16
+    kernel (single_bf3_kernel, MPGNN_OPT_GEMM_BF3 = 1) and on the fp32 K = 2·F_in GEMM."""
+    from mpgnn_amd import _lib
+    _lib.set_option(24, bf3)
     g = data.synthetic_graph(900, 3, 8, feat_dim=f_in, seed=3 + f_in)
     torch.manual_seed(4)
     conv = mpgnn_amd.CustomRGCNConv(f_in, 128, 1, flow="target_to_source")
