@@ -28,8 +28,11 @@ cpu_baseline threads: the affinity mask capped by the cgroup CPU quota (both rec
 
 roofline: the kernel with the largest share of the forward layer (per-kernel HIP-event pass on
 the launch stream; rocprofv3 summary in profiles/), against its own bound — the transform GEMM
-(rel_gemm_kernel, fp32 MFMA, 2·(S+N)·F_in·F_out FLOPs per launch) or the gathers (segment means /
-combine, HBM 8 TB/s, SURVEY §8d bytes). Every forward kernel kind is listed in roofline_kernels.
+(rel_gemm_bf3_kernel / single_bf3_kernel on the bf16 matrix cores: 6 bf16 products per fp32
+product of 2·(S+N)·F_in·F_out, priced against the dense bf16 peak, the fp32-equivalent rate
+beside it; --gemm fp32: rel_gemm_kernel against the fp32 MFMA peak) or the gathers (segment
+means / combine, HBM 8 TB/s, SURVEY §8d bytes). Every forward kernel kind is listed in
+roofline_kernels.
 traffic: HBM bytes per launch from the rocprofv3 PMC passes committed under profiles/ (FETCH_SIZE
 ×2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), or null when no pass matches the workload.
 cpu_baseline: the CPU oracle (PyG-2.3.1 loop semantics, same ATen ops) on this host.
@@ -386,17 +389,37 @@ def bench_score(args):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     ms = elapsed * 1e3 / args.steps
-    # the argmax kernel alone, HIP events on the launch stream (torch's current stream)
+    # the argmax launch alone (max_weights memset + kernel): 50 calls captured as one HIP graph
+    # and replayed between HIP events, so the GPU time is measured, not the host's issue rate
+    # of the per-call Python work (eager: ~47 us per call, the kernel a few)
     w = model.input.weights.detach()
-    reps = 200
+    reps, per_graph = 200, 50
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    k_how = "graph"
     with torch.no_grad():
-        for _ in range(5):
-            sc.score_argmax(w, ed)
-        ev0.record()
-        for _ in range(reps):
-            sc.score_argmax(w, ed)
-        ev1.record()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(5):
+                sc.score_argmax(w, ed)
+        torch.cuda.current_stream().wait_stream(side)
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for _ in range(per_graph):
+                    sc.score_argmax(w, ed)
+            graph.replay()
+            ev0.record()
+            for _ in range(reps // per_graph):
+                graph.replay()
+            ev1.record()
+        except RuntimeError:  # capture refused: eager calls (host-bound upper bound)
+            k_how = "eager"
+            torch.cuda.synchronize()
+            ev0.record()
+            for _ in range(reps):
+                sc.score_argmax(w, ed)
+            ev1.record()
     torch.cuda.synchronize()
     k_us = ev0.elapsed_time(ev1) * 1e3 / reps
     K = len(ed)
@@ -405,6 +428,7 @@ def bench_score(args):
                 "frac": round(alg / (k_us * 1e-6) / 1e9 / PEAK_HBM, 5), "traffic": None,
                 "kernel": "score_argmax_kernel (+ max_weights memset)", "avg_launch_us": round(k_us, 3),
                 "algorithmic": "E_r·(4 dst id + 4 weight) + K·(4 key + 8 ptr + 12 outputs) + N·4 max_weights",
+                "timing": f"HIP events around {reps} launches ({'replays of a HIP graph of ' + str(per_graph) + ' calls' if k_how == 'graph' else 'eager calls'})",
                 "note": "tiny launch (K sources, E_r edges): bound by launch latency, not HBM"}
     # the whole score_relation_parallel (dictionary build + weights + 100 epochs + final loss.item)
     _random.seed(0)

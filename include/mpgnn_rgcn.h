@@ -193,8 +193,8 @@ int32_t mpgnn_relu_bwd(const float* grad_out, const float* act_out, int64_t n, f
 /* Weight / bias gradient of the wrappers' Linear heads over all N node rows (Net.lin,
  * model.py:147; MPNetm.fc1/fc2, model.py:224-226): grad_weight[o][f] = Σ_i grad_out[i][o]·x[i][f],
  * grad_bias[o] = Σ_i grad_out[i][o] (nullable), row-sliced partials summed in a fixed order
- * (deterministic). x [N,F], grad_out [N,O], grad_weight [O,F] row-major fp32; F <= 256 and
- * O <= 32·(256/F). Scratch: mpgnn_linear_wgrad_workspace_bytes. Replaces autograd's
+ * (deterministic). x [N,F], grad_out [N,O], grad_weight [O,F] row-major fp32; F <= 256, any O
+ * (blocks of 32·(256/F) outputs per pass). Scratch: mpgnn_linear_wgrad_workspace_bytes. Replaces autograd's
  * grad_outᵀ @ x of F.linear (a serial-K library GEMM at K = N). */
 int32_t mpgnn_linear_wgrad_workspace_bytes(int64_t N, int32_t F, int32_t O, int64_t* bytes);
 int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int32_t F, int32_t O, float* grad_weight,

@@ -3399,13 +3399,14 @@ __global__ __launch_bounds__(kThreads) void relu_bwd_kernel(const float* g, cons
 // :224-226): gw[o][f] = Σ_i g[i][o]·x[i][f], gb[o] = Σ_i g[i][o]. Stage 1: workgroup p sums
 // its row slice into partial P[p][o][0..F] (column F = the bias); thread t owns column
 // f = t % F and outputs o ≡ t / F (mod 256 / F) — the g loads are wave-uniform. Stage 2 sums
-// the partials in a fixed order (deterministic, no atomics).
+// the partials in a fixed order (deterministic, no atomics). Heads with more outputs than one
+// pass holds (O > 32·256/F, e.g. MPNetm.fc1 128 -> 128) run in output blocks [o_lo, o_lo + O).
 constexpr int kLinAcc = 32;  // outputs per thread (O ≤ kLinAcc · 256 / F)
 constexpr int kLinRows = 8;  // rows per load batch
 constexpr int kLinRowsPerPart = 64;
 __global__ __launch_bounds__(kThreads) void linear_wgrad_part_kernel(const float* __restrict__ x,
-                                                                     const float* __restrict__ g, int N, int F, int O,
-                                                                     int rows, float* __restrict__ P) {
+                                                                     const float* __restrict__ g, int ldg, int N, int F,
+                                                                     int O, int rows, float* __restrict__ P) {
     const int tid = threadIdx.x;
     const int G = kThreads / F;
     const int f = tid % F, grp = tid / F;
@@ -3426,7 +3427,7 @@ __global__ __launch_bounds__(kThreads) void linear_wgrad_part_kernel(const float
             if (o < O) {
                 float gv[kLinRows];
 #pragma unroll
-                for (int u = 0; u < kLinRows; ++u) gv[u] = i0 + u < r1 ? g[(size_t)(i0 + u) * O + o] : 0.0f;
+                for (int u = 0; u < kLinRows; ++u) gv[u] = i0 + u < r1 ? g[(size_t)(i0 + u) * ldg + o] : 0.0f;
 #pragma unroll
                 for (int u = 0; u < kLinRows; ++u) {
                     acc[k] = __builtin_fmaf(gv[u], xv[u], acc[k]);
@@ -4412,18 +4413,20 @@ static int linear_parts(int64_t N) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(4096, (N + kLinRowsPerPart - 1) / kLinRowsPerPart));
 }
 
+static int linear_block(int F) { return kLinAcc * (kThreads / F); }  // outputs per pass
+
 int32_t mpgnn_linear_wgrad_workspace_bytes(int64_t N, int32_t F, int32_t O, int64_t* bytes) {
     if (!bytes) return arg_error("NULL bytes");
     if (N < 0 || F <= 0 || O <= 0) return arg_error("bad N, F or O");
-    *bytes = (int64_t)linear_parts(N) * O * (F + 1) * (int64_t)sizeof(float);
+    if (F > kThreads) return arg_error("mpgnn_linear_wgrad: needs F <= 256");
+    *bytes = (int64_t)linear_parts(N) * std::min(O, linear_block(F)) * (F + 1) * (int64_t)sizeof(float);
     return MPGNN_OK;
 }
 
 int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int32_t F, int32_t O, float* grad_weight,
                            float* grad_bias, void* workspace, void* stream) {
     if (N < 0 || F <= 0 || O <= 0) return arg_error("bad N, F or O");
-    if (F > kThreads || (int64_t)O > (int64_t)kLinAcc * (kThreads / F))
-        return arg_error("mpgnn_linear_wgrad: needs F <= 256 and O <= 32 * (256 / F)");
+    if (F > kThreads) return arg_error("mpgnn_linear_wgrad: needs F <= 256");
     if (N > INT32_MAX) return arg_error("N too large");
     if (!grad_weight || !workspace || (N > 0 && (!x || !grad_out))) return arg_error("NULL pointer");
     hipStream_t strm = static_cast<hipStream_t>(stream);
@@ -4435,13 +4438,19 @@ int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int
         if (st == MPGNN_OK && grad_bias) st = hip_check(hipMemsetAsync(grad_bias, 0, (size_t)O * sizeof(float), strm), "memset");
         return st;
     }
-    hipLaunchKernelGGL(linear_wgrad_part_kernel, dim3(parts), dim3(kThreads), 0, strm, x, grad_out, (int)N, F, O, rows, P);
-    int32_t st = hip_check(hipGetLastError(), "linear_wgrad_part_kernel launch");
-    if (st != MPGNN_OK) return st;
-    const int elems = O * (F + 1);
-    hipLaunchKernelGGL(linear_wgrad_sum_kernel, dim3((elems + kWaves - 1) / kWaves), dim3(kThreads), 0, strm, P, parts,
-                       F, O, grad_weight, grad_bias);
-    return hip_check(hipGetLastError(), "linear_wgrad_sum_kernel launch");
+    // output blocks in order; the partials buffer is reused (stream order)
+    for (int o_lo = 0; o_lo < O; o_lo += linear_block(F)) {
+        const int Ob = std::min(O - o_lo, linear_block(F));
+        hipLaunchKernelGGL(linear_wgrad_part_kernel, dim3(parts), dim3(kThreads), 0, strm, x, grad_out + o_lo, O, (int)N,
+                           F, Ob, rows, P);
+        int32_t st = hip_check(hipGetLastError(), "linear_wgrad_part_kernel launch");
+        if (st != MPGNN_OK) return st;
+        const int elems = Ob * (F + 1);
+        hipLaunchKernelGGL(linear_wgrad_sum_kernel, dim3((elems + kWaves - 1) / kWaves), dim3(kThreads), 0, strm, P,
+                           parts, F, Ob, grad_weight + (size_t)o_lo * F, grad_bias ? grad_bias + o_lo : nullptr);
+        if ((st = hip_check(hipGetLastError(), "linear_wgrad_sum_kernel launch")) != MPGNN_OK) return st;
+    }
+    return MPGNN_OK;
 }
 
 int32_t mpgnn_set_option(int32_t option, int64_t value) {

@@ -19,6 +19,7 @@ branch (model.py:45-72, score_relation_bags_*) is not on this path and raises.
 """
 from __future__ import annotations
 
+import os
 import random
 from collections.abc import Mapping
 
@@ -445,10 +446,22 @@ def score_relation_parallel(data, relation, source_nodes, features_dim, dataset,
                                                                      dataset=dataset)
     weights = initialize_weights(data, destination_dictionary, BAGS=False)
     model = get_model(weights, features_dim).to(edge_dictionary.device)
-    optimizer = get_optimizer(model)
     criterion, criterion_per_node = get_loss(), get_loss_per_node()
+    # the 100 epochs replay one captured HIP graph after three eager ones (main._epochs: every
+    # kernel of every epoch still runs; the host issues one launch per epoch instead of ~25)
+    from .main import _epochs
+    use_graph = os.environ.get("MPGNN_LOOP_GRAPH", "1") != "0" and edge_dictionary.device.type == "cuda"
+    if use_graph:  # Adam(lr 0.1) of main.py:521-522, fused and capturable: the same update
+        optimizer = torch.optim.Adam(list(model.parameters()), lr=0.1, fused=True, capturable=True)
+    else:
+        optimizer = get_optimizer(model)
+    grad_mask = torch.tensor(0)
+
+    def epoch():
+        return train(data, edge_dictionary, model, optimizer, criterion, source_nodes, criterion_per_node,
+                     [], weights, grad_mask, BAGS=False, dataset=dataset)[0]
+
     loss = None
-    for _ in range(epochs):
-        loss, _, _, _, _ = train(data, edge_dictionary, model, optimizer, criterion, source_nodes, criterion_per_node,
-                                 [], weights, torch.tensor(0), BAGS=False, dataset=dataset)
+    for _, loss in _epochs(epoch, epochs, use_graph):
+        pass
     return relation, loss.item(), edge_dictionary, destination_dictionary

@@ -720,10 +720,12 @@ def test_c2_layer_backward_long_reduction_chunks():
                "dbias": convg.bias.grad}, r32, r64, "C2 ")
 
 
-@pytest.mark.parametrize("n,f_in,f_out", [(14541, 128, 2), (1000, 128, 64), (300, 64, 3)])
+@pytest.mark.parametrize("n,f_in,f_out", [(14541, 128, 2), (1000, 128, 64), (300, 64, 3), (14541, 128, 128),
+                                         (2000, 256, 200)])
 def test_split_k_linear_matches_nn_linear(n, f_in, f_out):
     """model.linear: forward bit-identical to nn.Linear; grad_weight (sliced over rows) and
-    grad_bias / grad_input within fp32 rounding of autograd's."""
+    grad_bias / grad_input within fp32 rounding of autograd's — also for heads wider than one
+    pass of mpgnn_linear_wgrad (MPNetm.fc1 128 -> 128: two output blocks; 256 -> 200: seven)."""
     from mpgnn_amd.model import linear
     torch.manual_seed(0)
     lin = torch.nn.Linear(f_in, f_out).to(DEV)

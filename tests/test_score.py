@@ -12,6 +12,7 @@ C1 / KAT / C3 graphs with ties, NaNs and empty sources; the backward bit-exact a
 through the oracle's loop (the reference's reverse accumulation order); the 100-epoch training
 trajectory against the reference's (same argmax at every epoch, loss and weights within 1e-5).
 """
+import os
 import random
 
 import numpy as np
@@ -125,6 +126,15 @@ def _graphs():
     out.append(("C1", g.edge_index, g.edge_type, g.num_nodes))
     g = data.fb15k237_graph(feat_dim=4, seed=0, recipe="survey")
     out.append(("C3", g.edge_index, g.edge_type, g.num_nodes))
+    # hubs wider than a wave: source 3 -> 300 destinations (argmax across lanes and rounds);
+    # destination 7 <- 190 sources (its in-list spans three 64-pair rounds)
+    gen = torch.Generator().manual_seed(5)
+    n = 500
+    src = torch.cat([torch.full((300,), 3), torch.arange(10, 200), torch.randint(0, n, (400,), generator=gen)])
+    dst = torch.cat([torch.randperm(n, generator=gen)[:300], torch.full((190,), 7),
+                     torch.randint(0, n, (400,), generator=gen)])
+    et = torch.cat([torch.zeros(490, dtype=torch.int64), torch.randint(0, 2, (400,), generator=gen)])
+    out.append(("hubs", torch.stack([src, dst]), et, n))
     return out
 
 
@@ -137,7 +147,7 @@ def _tied_weights(n, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", [0, 1])
+@pytest.mark.parametrize("case", [0, 1, 2])
 def test_score_argmax_forward_backward_bit_exact(case):
     from mpgnn_amd.score import build_edge_dictionary, score_argmax
     name, ei, et, N = _graphs()[case]
@@ -234,8 +244,18 @@ def test_score_training_tracks_reference(golden, tag, dataset):
     assert np.allclose(losses, ref, rtol=1e-5, atol=1e-7), np.abs(np.array(losses) - ref).max()
     wf = model.input.weights.detach().cpu().numpy()[:, 0]
     assert np.allclose(wf, g[f"{tag}_w_final"], rtol=1e-5, atol=1e-6)
-    # the drop-in score_relation_parallel itself
-    random.seed(1000 + rel)
-    torch.manual_seed(77)
-    r, final, ed2, _ = sc.score_relation_parallel(d, rel, mask if dataset != "synthetic" else [], x.size(1), dataset)
-    assert r == rel and final == pytest.approx(float(g[f"{tag}_srp_loss"]), rel=1e-5, abs=1e-7)
+    # the drop-in score_relation_parallel itself: eager, and replaying one captured HIP graph
+    # per epoch after three eager ones (the default) — the same kernels, the same final loss
+    finals = []
+    for flag in ("0", "1"):
+        os.environ["MPGNN_LOOP_GRAPH"] = flag
+        try:
+            random.seed(1000 + rel)
+            torch.manual_seed(77)
+            r, final, ed2, _ = sc.score_relation_parallel(d, rel, mask if dataset != "synthetic" else [], x.size(1),
+                                                          dataset)
+        finally:
+            os.environ.pop("MPGNN_LOOP_GRAPH", None)
+        assert r == rel and final == pytest.approx(float(g[f"{tag}_srp_loss"]), rel=1e-5, abs=1e-7)
+        finals.append(final)
+    assert finals[0] == finals[1], finals
