@@ -1683,7 +1683,9 @@ struct RelGemmBf3 {
         __amdgpu_buffer_rsrc_t prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.Y, (short)0, 0, 0x00020000);
         auto store_prev = [&](int r) {
             const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(prev[r]), prev_rsrc, row * (N * 4) + col_b, 0, 0);
+            // cache policy sc1 (aux bit 4): measured 49.8 -> 48.7 us at C3, the combine unchanged
+            // (nt, aux bit 1, cost the combine 22.8 -> 28.3 us: Y left the MALL)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(prev[r]), prev_rsrc, row * (N * 4) + col_b, 0, 16);
         };
         int buf = 0;
         // item i: vc = rows of item i+1 (committed in this item), vn = receives rows of item i+2
@@ -5021,6 +5023,11 @@ int32_t mpgnn_rel_mean_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, 
 }
 
 
+static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const float* x, int32_t F_in, int32_t F_out,
+                          const float* h_save, const float* grad_out, float* grad_weight, float* grad_root,
+                          float* grad_bias, const Selection& s, const WsLayout& w, const RootChunks& rc, char* ws,
+                          hipStream_t strm);
+
 int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
                        int32_t F_in, const float* weight, const float* root, int32_t F_out,
                        const float* h_save, const float* grad_out, int64_t row_lo, int64_t row_hi,
@@ -5037,20 +5044,36 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
     const WsLayout w = ws_layout(p, mode, s, F_in, F_out, row_lo, row_hi, rc);
     char* ws = static_cast<char*>(workspace);
     if (!ws) return arg_error("NULL workspace");
-    const size_t wsize = (size_t)F_in * F_out;
     const bool exact = g_exact_order;
 
+    const bool want_x = grad_x != nullptr && p->N > 0;
+    const bool want_p = grad_weight != nullptr || grad_root != nullptr || grad_bias != nullptr;
     // ---- grad_x = Σ_r A_rᵀ ((dout @ W_rᵀ) / cnt) + dout @ rootᵀ ----------------------
-    if (grad_x != nullptr && p->N > 0) {
+    auto grad_x_part = [&](hipStream_t strm) -> int32_t {
         float* G = reinterpret_cast<float*>(ws + w.g);
         float* Groot = root ? reinterpret_cast<float*>(ws + w.groot) : nullptr;
-        st = run_seg(p, mode, s, 1, grad_out, F_out, weight, root, 1, F_in, G, Groot, row_lo, row_hi, nullptr,
-                     nullptr, true, MPGNN_K_SEG_DGRAD, strm);
-        if (st != MPGNN_OK) return st;
-        st = run_grad_x(p, mode, s, G, Groot, F_in, row_lo, row_hi, grad_x, reinterpret_cast<float*>(ws + w.pdx),
-                        exact, strm);
-        if (st != MPGNN_OK) return st;
-    }
+        int32_t e = run_seg(p, mode, s, 1, grad_out, F_out, weight, root, 1, F_in, G, Groot, row_lo, row_hi, nullptr,
+                            nullptr, true, MPGNN_K_SEG_DGRAD, strm);
+        if (e != MPGNN_OK) return e;
+        return run_grad_x(p, mode, s, G, Groot, F_in, row_lo, row_hi, grad_x, reinterpret_cast<float*>(ws + w.pdx),
+                          exact, strm);
+    };
+    // (the two halves on two streams — parameter gradients on a side stream forked from and
+    // joined into the caller's — measured slower: C3 epoch 1.163 -> 1.207 ms; not kept)
+    if (want_x && (st = grad_x_part(strm)) != MPGNN_OK) return st;
+    if (want_p) st = bwd_params(p, mode, R, x, F_in, F_out, h_save, grad_out, grad_weight, grad_root, grad_bias, s, w,
+                                rc, ws, strm);
+    return st;
+}
+
+// the parameter gradients of mpgnn_rgcn_bwd (dW / droot / dbias outer products + slab reduce)
+static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const float* x, int32_t F_in, int32_t F_out,
+                          const float* h_save, const float* grad_out, float* grad_weight, float* grad_root,
+                          float* grad_bias, const Selection& s, const WsLayout& w, const RootChunks& rc, char* ws,
+                          hipStream_t strm) {
+    int32_t st = MPGNN_OK;
+    const size_t wsize = (size_t)F_in * F_out;
+    const bool exact = g_exact_order;
     const int mt = (F_in + kColTile - 1) / kColTile;
     const int nt = (F_out + kColTile - 1) / kColTile;
     const size_t outer_lds = (size_t)(4 * kOuterBuf) * sizeof(float);

@@ -28,8 +28,20 @@ from .plan import GraphPlan
 __all__ = ["rgcn_conv", "segment_means", "MODE_SINGLE", "MODE_ALL"]
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _stream_of(device: torch.device) -> int:
+    """Raw handle of torch's current stream on ``device`` (the C accessor: ~0.2 µs against ~5 µs
+    for ``torch.cuda.current_stream(...).cuda_stream``, which builds a Stream object — this runs
+    a few times per layer call, so it shows in the host-bound small-graph epochs)."""
+    if _raw_stream is not None:
+        return _raw_stream(device.index if device.index is not None else torch.cuda.current_device())
+    return torch.cuda.current_stream(device).cuda_stream
+
+
 def _stream(t: torch.Tensor) -> int:
-    return torch.cuda.current_stream(t.device).cuda_stream
+    return _stream_of(t.device)
 
 
 def _dev(t: torch.Tensor, name: str) -> torch.Tensor:
@@ -59,7 +71,7 @@ _RETIRED: list = []
 
 
 def _workspace(nbytes: int, device: torch.device) -> torch.Tensor:
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    key = (device.index, _stream_of(device))
     ws = _WS.get(key)
     if ws is None or ws.numel() < nbytes:
         # drop the smaller buffer first: the caching allocator hands its block back in stream

@@ -40,7 +40,8 @@ COMPLEX = "fb15k-237"  # main.py:1484 (stored by Score, unused by the non-bag fo
 
 
 def _stream(device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    from .functional import _stream_of
+    return _stream_of(torch.device(device))
 
 
 def _ptr(t):
