@@ -72,6 +72,25 @@ __device__ __forceinline__ void vstore(float* p, const float (&v)[V]) {
     }
 }
 
+// vstore through a buffer resource over a wave-uniform base with the sc1 cache policy (aux bit
+// 4) — the row outputs of the gather-sum kernels (segment means: 17.4 -> 16.8 µs at C3) and of
+// the bf16 GEMMs leave this way
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <int V>
+__device__ __forceinline__ void vstore_sc1(float* base, int off, const float (&v)[V]) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+    if constexpr (V == 4) {
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])}, r, off * 4,
+            0, 16);
+    } else if constexpr (V == 2) {
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(v[0]), __float_as_uint(v[1])}, r, off * 4, 0, 16);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[0]), r, off * 4, 0, 16);
+    }
+}
+
 // ReLU with torch's semantics (clamp_min(x, 0)): x < 0 → 0, NaN and -0.0 pass through, so a
 // diverging run still shows NaN (fmaxf(NaN, 0) would return 0).
 __device__ __forceinline__ float relu_f(float v) { return v < 0.0f ? 0.0f : v; }
@@ -2128,7 +2147,7 @@ __device__ __forceinline__ void flat_finish_store(const FlatArgs& a, int rr, flo
                 if (addb) o[k] = o[k] + bb[t][k];
                 if (a.relu) o[k] = relu_f(o[k]);
             }
-            vstore<V>(dst + col, o);
+            vstore_sc1<V>(dst, col, o);
         }
     }
 }
