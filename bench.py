@@ -97,6 +97,8 @@ def parse():
                     help="epochs of the drop-in training loop timed (0 skips; default 20 C3, 5 C2, 2 C5)")
     ap.add_argument("--gemm", default="bf3", choices=["bf3", "fp32"],
                     help="transform / dgrad GEMM: bf3 = bf16 matrix cores, 3-way exact split (default); fp32 = fp32 MFMA")
+    ap.add_argument("--chunk-rows", type=int, default=None,
+                    help="backward weight-gradient reduction chunk length (MPGNN_OPT_CHUNK_ROWS; default: the library's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed CPU repetitions (median), after 2 warm-ups")
     a = ap.parse_args()
@@ -494,6 +496,8 @@ def pmc_traffic(workload, mode, feat, kernel_prefix):
 def main():
     args = parse()
     _lib.set_option(24, 1 if args.gemm == "bf3" else 0)  # MPGNN_OPT_GEMM_BF3
+    if args.chunk_rows is not None:
+        _lib.set_option(20, args.chunk_rows)  # MPGNN_OPT_CHUNK_ROWS (before the plan is built)
     if args.mode == "score":
         return bench_score(args)
     rank, world, local, group = setup_dist(args.gpus)
