@@ -99,6 +99,8 @@ def parse():
                     help="transform / dgrad GEMM: bf3 = bf16 matrix cores, 3-way exact split (default); fp32 = fp32 MFMA")
     ap.add_argument("--chunk-rows", type=int, default=None,
                     help="backward weight-gradient reduction chunk length (MPGNN_OPT_CHUNK_ROWS; default: the library's)")
+    ap.add_argument("--bwd-fused", type=int, default=1, choices=[0, 1],
+                    help="backward at F = 128: dgrad + dW in one launch (MPGNN_OPT_BWD_FUSED); 0 for A/B")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed CPU repetitions (median), after 2 warm-ups")
     a = ap.parse_args()
@@ -498,6 +500,7 @@ def pmc_traffic(workload, mode, feat, kernel_prefix):
 def main():
     args = parse()
     _lib.set_option(24, 1 if args.gemm == "bf3" else 0)  # MPGNN_OPT_GEMM_BF3
+    _lib.set_option(25, args.bwd_fused)  # MPGNN_OPT_BWD_FUSED
     if args.chunk_rows is not None:
         _lib.set_option(20, args.chunk_rows)  # MPGNN_OPT_CHUNK_ROWS (before the plan is built)
     if args.mode == "score":

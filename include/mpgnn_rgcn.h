@@ -298,10 +298,13 @@ enum mpgnn_option {
     MPGNN_OPT_CHUNK_ROWS = 20,   /* backward weight-gradient reduction chunks: base length in rows (multiple of 32,
                                     32..1024, default 256) of the root chunks and of the relation chunks of plans
                                     created afterwards; same results up to fp32 summation order of the slabs */
-    MPGNN_OPT_GEMM_BF3 = 24      /* 1 (default): the transform / dgrad GEMMs (K in {64,128}, N = 128) on the bf16
+    MPGNN_OPT_GEMM_BF3 = 24,     /* 1 (default): the transform / dgrad GEMMs (K in {64,128}, N = 128) on the bf16
                                     matrix cores with each fp32 operand split exactly into three bf16 pieces (six
                                     products, fp32 accumulation: fp32-level accuracy at 2.67x the fp32-MFMA rate);
                                     0: the fp32-MFMA kernel (v_mfma_f32_32x32x2_f32) */
+    MPGNN_OPT_BWD_FUSED = 25     /* 1 (default): mpgnn_rgcn_bwd at F_in = F_out = 128 (bf16-split GEMMs) runs
+                                    dgrad and dW / droot / dbias in one launch that gathers dout once;
+                                    0: the dgrad launch + the chunked dW launch */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

@@ -717,6 +717,7 @@ int32_t mpgnn_plan_destroy(mpgnn_plan* p) {
         if (p->d.block) (void)hipFree(p->d.block);
         free_device_plan(p);
         if (p->d.rel_node_map) (void)hipFree(p->d.rel_node_map);
+        for (auto& kv : p->bw_slabs) (void)hipFree(kv.second.dev);
         (void)hipSetDevice(prev);
     }
     delete p;

@@ -3,7 +3,9 @@
 #pragma once
 
 #include <atomic>
+#include <array>
 #include <cstdint>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -212,6 +214,15 @@ struct mpgnn_plan {
     // fused mode-SINGLE call that is not being graph-captured; tried once per plan
     mutable std::mutex node_map_mu;
     mutable std::atomic<bool> node_maps_tried{false};
+    // bwd_bf3_kernel's slab layout per (selection, row range, grid): the first slab of every
+    // workgroup and the slab range of every dense relation, on the device (made outside graph
+    // captures by the first backward call of that shape; freed with the plan)
+    struct BwSlabs {
+        int* dev = nullptr;  // [G] first slab per workgroup, then [nrel + 1] relation slab ranges
+        int n_slabs = 0, root_lo = 0;
+    };
+    mutable std::mutex bw_mu;
+    mutable std::map<std::array<int64_t, 8>, BwSlabs> bw_slabs;
 };
 
 namespace mpgnn {

@@ -3327,6 +3327,286 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
     }
 }
 
+// ----------------------------------------------------------------------------------------
+// bwd_bf3_kernel — the GEMM work of a layer's backward at F_in = F_out = 128 in ONE persistent
+// launch over rel_gemm's items (32-row relation tiles, then 32-node root items), both products
+// that read dout on the bf16 matrix cores with the exact three-way split:
+//   dgrad   G[seg] = (dout[node_1] @ W_rᵀ) / cnt,  G_root = dout @ rootᵀ      (waves 0-3)
+//   dW      dW_r += Σ_rows A_rowᵀ dout_row, droot += x_iᵀ dout_i, dbias += Σ dout_i   (waves 4-7)
+// The item's dout rows are gathered ONCE (waves 0-3) and committed both row-major (dgrad's A
+// operand) and transposed (dW's B operand: K = the item's rows); waves 4-7 gather its A rows
+// (x row or compact mean through s_src; x rows for root items) into transposed planes. dW
+// accumulates in registers over a workgroup's run of items of one weight and leaves as one
+// slab per run; the host knows every workgroup's item range, so the slabs of one weight are
+// contiguous and reduce_slabs3_kernel sums them in order (deterministic). Replaces the dgrad
+// launch, outer_bf3_kernel's second gather of dout + its 256-row chunk slabs.
+// Waves 0-3 and 4-7 run separate loops (disjoint register sets) with the same two barriers
+// per item; the rows of item i+1 are in flight during item i, their indices one item earlier.
+// ----------------------------------------------------------------------------------------
+constexpr int kBwThreads = 512;
+constexpr int kBwLdt = 40;                     // transposed plane column: 32 rows + 8 pad (bf16, 80 B)
+constexpr int kBwTPlane = 128 * kBwLdt;        // bf16 per transposed plane
+constexpr int kBwLdab = 136;                   // row-major plane row: K + 8 (bf16)
+constexpr int kBwRPlane = 32 * kBwLdab;        // bf16 per row-major plane
+constexpr size_t kBwLds = (size_t)(3 * kBwRPlane + 6 * kBwTPlane) * 2 + (32 + 256) * sizeof(float);
+
+struct BwdArgs {
+    RelGemmArgs g;         // items + dgrad operands (DGRAD use: Aroot = dout, W / Wroot transposed);
+                           // g.Y == nullptr: no grad_x wanted (no dgrad chain)
+    const float* x;        // [N][128] layer input: A rows of dW
+    const float* Hm;       // saved compact means (row m - g.m_lo)
+    float* slabs;          // [n_slabs][128][128]
+    float* bslabs;         // [n_slabs][128] bias partials (root runs)
+    const int* wg_slab0;   // [G] first slab of each workgroup
+};
+
+__device__ __forceinline__ void bw_range(int n_items, int& i_beg, int& i_end) {
+    const int G = (int)gridDim.x;
+    const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
+    const int rng = g * q + min(g, rem) + ((int)blockIdx.x >> 3);  // consecutive items on one XCD
+    i_beg = (int)((long long)rng * n_items / G);
+    i_end = (int)((long long)(rng + 1) * n_items / G);
+}
+
+// waves 0-3: dout rows of every item (both layouts) and, with g.Y, the dgrad products
+__device__ __forceinline__ void bw_dgrad_half(const BwdArgs& A, int i_beg, int i_end, __bf16* Rp, __bf16* Dt,
+                                              float* Sc) {
+    using Bs = RelGemm<2, true>;
+    using Ds = RelGemmBf3<2, true>;
+    using Item = Bs::Item;
+    constexpr int N = 128, NS = 8, WPT = Bs::WPT, W4 = 32;
+    const RelGemmArgs& a = A.g;
+    const int t = threadIdx.x;  // 0..255
+    const int lane = t & 63, c = lane & 31, h = lane >> 5;
+    const int wq = __builtin_amdgcn_readfirstlane(t >> 6);
+    const bool want_dx = a.Y != nullptr;
+    Item cur = Bs::item(a, i_beg);
+    int row[WPT], cnt = 1, nrow[WPT], ncnt = 1, zm;
+    float4 v[WPT];
+    Bs::gather_idx(a, cur, t, row, cnt);
+    Bs::issue_rows(a, t, row, v, zm);
+    if (i_beg + 1 < i_end) Bs::gather_idx(a, Bs::item(a, i_beg + 1), t, nrow, ncnt);
+    bf16x8 b[NS][3];
+    const float* wcur = nullptr;
+    const int col_b = (wq * 32 + c) * 4;
+    for (int i = i_beg; i < i_end; ++i) {
+        // commit: split once, store row-major (dgrad A) and transposed (dW B); rows past the item: 0
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+            const int e = t + j * 256;
+            const int r = e / W4, c4 = (e % W4) * 4;
+            const float4 xv = r < cur.nrows ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            __bf16 p0[4], p1[4], p2[4];
+            split3_bf16(xv.x, p0[0], p1[0], p2[0]);
+            split3_bf16(xv.y, p0[1], p1[1], p2[1]);
+            split3_bf16(xv.z, p0[2], p1[2], p2[2]);
+            split3_bf16(xv.w, p0[3], p1[3], p2[3]);
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            __bf16* d = Rp + r * kBwLdab + c4;
+            *reinterpret_cast<bf16x4*>(d) = bf16x4{p0[0], p0[1], p0[2], p0[3]};
+            *reinterpret_cast<bf16x4*>(d + kBwRPlane) = bf16x4{p1[0], p1[1], p1[2], p1[3]};
+            *reinterpret_cast<bf16x4*>(d + 2 * kBwRPlane) = bf16x4{p2[0], p2[1], p2[2], p2[3]};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __bf16* dt = Dt + (c4 + q) * kBwLdt + r;
+                dt[0] = p0[q];
+                dt[kBwTPlane] = p1[q];
+                dt[2 * kBwTPlane] = p2[q];
+            }
+        }
+        if (t < 32) Sc[t] = 1.0f / (float)cnt;
+        if (want_dx && cur.w != wcur) {  // the item's weight slice (relation change)
+            Ds::load_b(cur.w, wq, lane, b);
+            wcur = cur.w;
+        }
+        const bool has_next = i + 1 < i_end;
+        const Item nxt = has_next ? Bs::item(a, i + 1) : cur;
+        if (has_next) {
+            Bs::issue_rows(a, t, nrow, v, zm);
+            cnt = ncnt;
+            if (i + 2 < i_end) Bs::gather_idx(a, Bs::item(a, i + 2), t, nrow, ncnt);
+        }
+        __syncthreads();  // (1) the item's planes are in LDS
+        if (want_dx) {
+            const __bf16* Ab = Rp + c * kBwLdab + 8 * h;
+            f32x16 hi, lo;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                hi[r] = 0.0f;
+                lo[r] = 0.0f;
+            }
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Ab + 16 * s);
+                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Ab + kBwRPlane + 16 * s);
+                const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * kBwRPlane + 16 * s);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[s][0], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][1], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][2], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][0], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][1], lo, 0, 0, 0);
+                hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][0], hi, 0, 0, 0);
+            }
+            float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
+            const int bytes = __builtin_amdgcn_readfirstlane(cur.nrows) * N * 4;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Yt, (short)0, bytes, 0x00020000);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+                float o = hi[r] + lo[r];
+                if (!cur.root) o = o * Sc[rr];
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), rs, rr * (N * 4) + col_b, 0, 16);
+            }
+        }
+        __syncthreads();  // (2) planes free for the next commit
+        cur = nxt;
+    }
+}
+
+// waves 4-7: A rows of every item (transposed) and the dW / droot / dbias products
+__device__ __forceinline__ void bw_dw_half(const BwdArgs& A, int i_beg, int i_end, const __bf16* Dt, __bf16* Xt,
+                                           float* bx) {
+    using Bs = RelGemm<2, true>;
+    using Item = Bs::Item;
+    const RelGemmArgs& a = A.g;
+    const int t = threadIdx.x - 256;  // 0..255
+    const int lane = t & 63, c = lane & 31, h = lane >> 5;
+    const int wq = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int col = t & 127;
+    const int hf = __builtin_amdgcn_readfirstlane(t >> 7);  // staged rows 8·hf + 16u .. +8 (u = 0, 1)
+    // lanes 0..7 of the wave: A-row index of staged row 8·hf + 16u + lane (x row >= 0, else Hm row)
+    auto load_idx = [&](const Item& it, int (&ia)[2]) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k = min(8 * hf + 16 * u + (lane & 7), it.nrows - 1);
+            ia[u] = it.root ? it.r0 + k : a.s_src[it.r0 + k];
+        }
+    };
+    auto issue = [&](const int (&ia)[2], float (&xv)[2][8]) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int rw = __builtin_amdgcn_readlane(ia[u], j);
+                const float* base = rw >= 0 ? A.x + (size_t)rw * 128 : A.Hm + (size_t)(-rw - 1 - a.m_lo) * 128;
+                xv[u][j] = base[col];
+            }
+    };
+    Item cur = Bs::item(a, i_beg);
+    int ia[2], nia[2] = {0, 0};
+    float xv[2][8];
+    load_idx(cur, ia);
+    issue(ia, xv);
+    if (i_beg + 1 < i_end) load_idx(Bs::item(a, i_beg + 1), nia);
+    f32x16 hi[4], lo[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            hi[q][r] = 0.0f;
+            lo[q][r] = 0.0f;
+        }
+    float bpart = 0.0f;
+    int slab = A.wg_slab0[blockIdx.x];
+    int pending_b = -1;  // bias slab whose two halves wait in bx for the barrier
+    for (int i = i_beg; i < i_end; ++i) {
+        if (pending_b >= 0) {  // after barrier (2) of the previous item
+            if (t < 128) A.bslabs[(size_t)pending_b * 128 + col] = bx[t] + bx[t + 128];
+            pending_b = -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int nr = min(8, cur.nrows - (8 * hf + 16 * u));  // live rows of this group (uniform)
+            bf16x8 pa[3];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                __bf16 a0, a1, a2;
+                split3_bf16(j < nr ? xv[u][j] : 0.0f, a0, a1, a2);
+                pa[0][j] = a0;
+                pa[1][j] = a1;
+                pa[2][j] = a2;
+            }
+            __bf16* d = Xt + col * kBwLdt + 8 * hf + 16 * u;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x8*>(d + p * kBwTPlane) = pa[p];
+        }
+        const bool has_next = i + 1 < i_end;
+        const Item nxt = has_next ? Bs::item(a, i + 1) : cur;
+        if (has_next) {
+            issue(nia, xv);
+            if (i + 2 < i_end) load_idx(Bs::item(a, i + 2), nia);
+        }
+        __syncthreads();  // (1)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const __bf16* Bf = Dt + (wq * 32 + c) * kBwLdt + 16 * s + 8 * h;
+            const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(Bf);
+            const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(Bf + kBwTPlane);
+            const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(Bf + 2 * kBwTPlane);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const __bf16* Af = Xt + (q * 32 + c) * kBwLdt + 16 * s + 8 * h;
+                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Af);
+                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Af + kBwTPlane);
+                const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(Af + 2 * kBwTPlane);
+                lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, lo[q], 0, 0, 0);
+                lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, lo[q], 0, 0, 0);
+                lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, lo[q], 0, 0, 0);
+                lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, lo[q], 0, 0, 0);
+                lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, lo[q], 0, 0, 0);
+                hi[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, hi[q], 0, 0, 0);
+            }
+        }
+        if (cur.root) {  // dbias: this thread's column of dout over its staged rows, rebuilt exactly
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const __bf16* bc = Dt + col * kBwLdt + 8 * hf + 16 * u;
+                const bf16x8 q0 = *reinterpret_cast<const bf16x8*>(bc);
+                const bf16x8 q1 = *reinterpret_cast<const bf16x8*>(bc + kBwTPlane);
+                const bf16x8 q2 = *reinterpret_cast<const bf16x8*>(bc + 2 * kBwTPlane);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bpart += ((float)q0[j] + (float)q1[j]) + (float)q2[j];
+            }
+        }
+        if (!has_next || nxt.w != cur.w) {  // the run ends: its slab
+            float* D = A.slabs + (size_t)slab * 128 * 128;
+            const int ocol = wq * 32 + c;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = q * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    D[(size_t)m * 128 + ocol] = hi[q][r] + lo[q][r];
+                    hi[q][r] = 0.0f;
+                    lo[q][r] = 0.0f;
+                }
+            if (cur.root) {
+                bx[t] = bpart;
+                bpart = 0.0f;
+                pending_b = slab;
+            }
+            ++slab;
+        }
+        __syncthreads();  // (2)
+        cur = nxt;
+    }
+    if (pending_b >= 0 && t < 128) A.bslabs[(size_t)pending_b * 128 + col] = bx[t] + bx[t + 128];
+}
+
+__global__ __launch_bounds__(kBwThreads, 1) void bwd_bf3_kernel(BwdArgs A) {
+    extern __shared__ __attribute__((aligned(16))) __bf16 bw_smem[];
+    __bf16* Rp = bw_smem;
+    __bf16* Dt = Rp + 3 * kBwRPlane;
+    __bf16* Xt = Dt + 3 * kBwTPlane;
+    float* Sc = reinterpret_cast<float*>(Xt + 3 * kBwTPlane);
+    float* bx = Sc + 32;
+    int i_beg, i_end;
+    bw_range(A.g.n_rel + A.g.n_root, i_beg, i_end);
+    if (i_beg >= i_end) return;
+    if (threadIdx.x < 256) bw_dgrad_half(A, i_beg, i_end, Rp, Dt, Sc);
+    else bw_dw_half(A, i_beg, i_end, Dt, Xt, bx);
+}
+
 // dst[group g] (elems floats) = Σ_{c in chunks of g, ascending} P[c]
 struct ReduceArgs {
     const float* P;
@@ -3652,6 +3932,7 @@ static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
 }
 
 static bool g_gemm_bf3 = true;  // MPGNN_OPT_GEMM_BF3: K ∈ {64, 128}, N = 128 on the bf16 matrix cores (3-way split)
+static bool g_bwd_fused = true;  // MPGNN_OPT_BWD_FUSED: see bwd_bf3_kernel
 
 template <int KB, bool DGRAD>
 static void launch_rel_gemm_bf3(const RelGemmArgs& a, hipStream_t st) {
@@ -3785,6 +4066,7 @@ static RootChunks root_chunks(int64_t lo, int64_t hi) {
 struct WsLayout {
     size_t y = 0, yroot = 0, hf = 0, pseg = 0, prw = 0, nmap = 0;  // forward
     size_t g = 0, groot = 0, h = 0, pdx = 0, p = 0, proot = 0, pb = 0;  // backward
+    size_t bw = 0, bwb = 0;  // bwd_bf3_kernel slabs (F_in = F_out = 128)
     size_t total = 0;      // max(forward, backward): what mpgnn_rgcn_bwd needs
     size_t fwd_total = 0;  // forward part only (mpgnn_rgcn_fwd / _fwd_act)
 };
@@ -3820,6 +4102,11 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
     w.p = off; off += align256((size_t)(s.c_hi - s.c_lo) * F_in * F_out * sizeof(float));
     w.proot = off; off += align256((size_t)rc.n * F_in * F_out * sizeof(float));
     w.pb = off; off += align256((size_t)rc.n * F_out * sizeof(float));
+    if (F_in == 128 && F_out == 128) {  // bwd_bf3_kernel: one slab per (workgroup, weight run)
+        const size_t ns = (size_t)cu_count() + (size_t)std::max<int64_t>(s.d_hi - s.d_lo, 0) + 2;
+        w.bw = off; off += align256(ns * F_in * F_out * sizeof(float));
+        w.bwb = off; off += align256(ns * F_out * sizeof(float));
+    }
     w.total = std::max<size_t>(std::max(fwd, off), 256);
     return w;
 }
@@ -4497,6 +4784,9 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
         case MPGNN_OPT_GEMM_BF3:
             g_gemm_bf3 = value != 0;
             return MPGNN_OK;
+        case MPGNN_OPT_BWD_FUSED:
+            g_bwd_fused = value != 0;
+            return MPGNN_OK;
         case MPGNN_OPT_CHUNK_ROWS:
             if (value < 32 || value > 1024 || value % 32 != 0)
                 return arg_error("MPGNN_OPT_CHUNK_ROWS must be 32..1024, a multiple of 32");
@@ -4522,6 +4812,7 @@ int32_t mpgnn_get_option(int32_t option, int64_t* value) {
         case MPGNN_OPT_REL_WIDE: *value = g_rel_wide ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_CHUNK_ROWS: *value = g_chunk_rows; return MPGNN_OK;
         case MPGNN_OPT_GEMM_BF3: *value = g_gemm_bf3 ? 1 : 0; return MPGNN_OK;
+        case MPGNN_OPT_BWD_FUSED: *value = g_bwd_fused ? 1 : 0; return MPGNN_OK;
         default: return arg_error("unknown option " + std::to_string(option));
     }
 }
@@ -5047,6 +5338,174 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
                           float* grad_bias, const Selection& s, const WsLayout& w, const RootChunks& rc, char* ws,
                           hipStream_t strm);
 
+
+// The backward at F_in = F_out = 128 through bwd_bf3_kernel (dgrad + dW / droot / dbias in one
+// launch) + reduce_slabs3_kernel + grad_x. Returns MPGNN_ERR_UNSUPPORTED (nothing launched) when
+// its slab layout is not cached and cannot be made now (graph capture): the caller falls back.
+static int32_t bwd_fused(const mpgnn_plan* p, int32_t mode, int32_t R, const float* x, const float* weight,
+                         const float* root, const float* h_save, const float* grad_out, int64_t row_lo, int64_t row_hi,
+                         float* grad_x, float* grad_weight, float* grad_root, float* grad_bias, const Selection& s,
+                         const WsLayout& w, char* ws, hipStream_t strm) {
+    const int n_rel = s.t32_hi - s.t32_lo;
+    const int n_root = (int)((row_hi - row_lo + 31) / 32);
+    const int n_items = n_rel + n_root;
+    if (n_root == 0) return MPGNN_ERR_UNSUPPORTED;
+    const int G = std::min(n_items, cu_count());
+    // one workgroup per CU walks its items with the next item's rows in flight: few items per
+    // workgroup (C3 mode SINGLE: 3) it saves the second launch and gather (epoch 0.74 -> 0.69 ms);
+    // at C3 mode ALL (29 items per workgroup) the two launches at two workgroups per CU are
+    // faster (epoch 1.17 vs 1.30 ms) — measured, the split point is conservative
+    if (n_items > 4 * cu_count()) return MPGNN_ERR_UNSUPPORTED;
+    const int64_t nd = s.d_hi - s.d_lo;
+    // ---- slab layout (host: every workgroup's item range, runs of one weight) ----
+    const std::array<int64_t, 8> key{mode, s.t32_lo, s.t32_hi, s.d_lo, s.d_hi, row_lo, row_hi, G};
+    mpgnn_plan::BwSlabs lay;
+    {
+        std::lock_guard<std::mutex> lk(p->bw_mu);
+        auto it = p->bw_slabs.find(key);
+        if (it != p->bw_slabs.end()) {
+            lay = it->second;
+        } else {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            if (hipStreamIsCapturing(strm, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+                return MPGNN_ERR_UNSUPPORTED;
+            std::vector<int> wkey(n_items);
+            for (int i = 0; i < n_items; ++i) {
+                if (i >= n_rel) {
+                    wkey[i] = -1;  // root
+                } else if (mode != MPGNN_MODE_ALL) {
+                    wkey[i] = 0;   // one weight
+                } else {
+                    const int t = s.t32_lo + i;
+                    wkey[i] = (int)(std::upper_bound(p->rel_t32_ptr.begin(), p->rel_t32_ptr.end(), t) -
+                                    p->rel_t32_ptr.begin()) - 1;
+                }
+            }
+            // workgroup blockIdx g holds the rng(g)-th consecutive item range (bw_range); slabs are
+            // numbered in item order, so each weight's slabs are contiguous (relations, then root)
+            std::vector<int> tab((size_t)G + (size_t)p->nrel + 1, 0), skey, perm(G);
+            for (int g = 0; g < G; ++g) {
+                const int gx = g & 7, q = G >> 3, rem = G & 7;
+                perm[gx * q + std::min(gx, rem) + (g >> 3)] = g;
+            }
+            int ns = 0;
+            for (int rg = 0; rg < G; ++rg) {
+                const int ib = (int)((long long)rg * n_items / G), ie = (int)((long long)(rg + 1) * n_items / G);
+                tab[perm[rg]] = ns;
+                for (int i = ib; i < ie; ++i)
+                    if (i == ib || wkey[i] != wkey[i - 1]) {
+                        skey.push_back(wkey[i]);
+                        ++ns;
+                    }
+            }
+            int root_lo = ns;
+            for (int k = 0; k < ns; ++k)
+                if (skey[k] < 0) {
+                    root_lo = k;
+                    break;
+                }
+            // relation slab ranges, indexed by absolute dense relation (reduce_slabs_body's gptr)
+            int* rp = tab.data() + G;
+            int k = 0;
+            for (int64_t d = 0; d <= p->nrel; ++d) {
+                while (k < root_lo && skey[k] < d) ++k;
+                rp[d] = k;
+            }
+            int* dev = nullptr;
+            if (hipMalloc(&dev, tab.size() * sizeof(int)) != hipSuccess) {
+                (void)hipGetLastError();
+                return MPGNN_ERR_UNSUPPORTED;
+            }
+            if (hipMemcpy(dev, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+                (void)hipGetLastError();
+                (void)hipFree(dev);
+                return MPGNN_ERR_UNSUPPORTED;
+            }
+            lay.dev = dev;
+            lay.n_slabs = ns;
+            lay.root_lo = root_lo;
+            p->bw_slabs[key] = lay;
+        }
+    }
+    if ((size_t)lay.n_slabs * 128 * 128 * sizeof(float) > w.bwb - w.bw) return MPGNN_ERR_UNSUPPORTED;
+    float* slabs = reinterpret_cast<float*>(ws + w.bw);
+    float* bslabs = reinterpret_cast<float*>(ws + w.bwb);
+    int32_t st = MPGNN_OK;
+    if (mode == MPGNN_MODE_ALL && nd != (int64_t)R) {  // weight ids without a relation of the plan: zeros
+        if ((st = hip_check(hipMemsetAsync(grad_weight, 0, (size_t)std::max(R, 0) * 128 * 128 * sizeof(float), strm),
+                            "memset grad_weight")) != MPGNN_OK)
+            return st;
+    }
+    BwdArgs A{};
+    RelGemmArgs& r = A.g;
+    r.t_begin = p->d.t32_begin;
+    r.t_end = p->d.t32_end;
+    r.t_lo = s.t32_lo;
+    r.n_rel = n_rel;
+    r.n_root = n_root;
+    r.Aroot = grad_out;
+    r.s_src = p->d.s_src;
+    r.m_lo = s.m_lo;
+    r.s_row = p->d.s_row;
+    r.s_cnt = p->d.s_cnt;
+    r.s_rel = p->d.s_rel;
+    r.W = weight;
+    r.w_per_rel = (mode == MPGNN_MODE_ALL);
+    r.Wroot = root;
+    r.Y = grad_x != nullptr ? reinterpret_cast<float*>(ws + w.g) : nullptr;
+    r.Yroot = grad_x != nullptr ? reinterpret_cast<float*>(ws + w.groot) : nullptr;
+    r.sel_b = s.sel_b;
+    r.row_lo = (int)row_lo;
+    r.row_hi = (int)row_hi;
+    A.x = x;
+    A.Hm = h_save;
+    A.slabs = slabs;
+    A.bslabs = bslabs;
+    A.wg_slab0 = lay.dev;
+    {
+        TimedLaunch tl(MPGNN_K_OUTER, strm);
+        hipLaunchKernelGGL(bwd_bf3_kernel, dim3(G), dim3(kBwThreads), kBwLds, strm, A);
+        if ((st = hip_check(hipGetLastError(), "bwd_bf3_kernel launch")) != MPGNN_OK) return st;
+    }
+    {
+        ReduceArgs r3[3] = {};
+        int gx[3] = {0, 0, 0};
+        // weights: mode ALL one group per selected dense relation (its contiguous slab range),
+        // mode SINGLE one group (every relation slab)
+        r3[0].P = slabs;
+        r3[0].elems = 128 * 128;
+        r3[0].dst = grad_weight;
+        if (mode == MPGNN_MODE_ALL) {
+            r3[0].gptr = lay.dev + G;
+            r3[0].g_base = (int)s.d_lo;
+            r3[0].gdst = p->d.rel_val32;
+            gx[0] = (int)nd;
+        } else {
+            r3[0].nchunks = lay.root_lo;
+            gx[0] = 1;
+        }
+        r3[1].P = slabs + (size_t)lay.root_lo * 128 * 128;
+        r3[1].elems = 128 * 128;
+        r3[1].nchunks = lay.n_slabs - lay.root_lo;
+        r3[1].dst = grad_root;
+        gx[1] = grad_root != nullptr ? 1 : 0;
+        r3[2].P = bslabs + (size_t)lay.root_lo * 128;
+        r3[2].elems = 128;
+        r3[2].nchunks = lay.n_slabs - lay.root_lo;
+        r3[2].dst = grad_bias;
+        gx[2] = grad_bias != nullptr ? 1 : 0;
+        ZeroList zl{};
+        TimedLaunch tl(MPGNN_K_REDUCE, strm);
+        hipLaunchKernelGGL(reduce_slabs3_kernel, dim3(gx[0] + gx[1] + gx[2], (128 * 128 + kThreads - 1) / kThreads),
+                           dim3(kThreads), 0, strm, r3[0], r3[1], r3[2], gx[0], gx[1], gx[2], zl);
+        if ((st = hip_check(hipGetLastError(), "reduce_slabs3_kernel launch")) != MPGNN_OK) return st;
+    }
+    if (grad_x != nullptr)
+        st = run_grad_x(p, mode, s, reinterpret_cast<float*>(ws + w.g), reinterpret_cast<float*>(ws + w.groot), 128,
+                        row_lo, row_hi, grad_x, reinterpret_cast<float*>(ws + w.pdx), false, strm);
+    return st;
+}
+
 int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
                        int32_t F_in, const float* weight, const float* root, int32_t F_out,
                        const float* h_save, const float* grad_out, int64_t row_lo, int64_t row_hi,
@@ -5067,6 +5526,14 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
 
     const bool want_x = grad_x != nullptr && p->N > 0;
     const bool want_p = grad_weight != nullptr || grad_root != nullptr || grad_bias != nullptr;
+    if (g_bwd_fused && g_gemm_bf3 && g_rel_gemm && !exact && F_in == 128 && F_out == 128 && p->N > 0 && x != nullptr &&
+        root != nullptr && grad_weight != nullptr && grad_root != nullptr && (h_save != nullptr || s.m_hi == s.m_lo) &&
+        p->N <= INT32_MAX - 1) {
+        st = bwd_fused(p, mode, R, x, weight, root, h_save, grad_out, row_lo, row_hi, want_x ? grad_x : nullptr,
+                       grad_weight, grad_root, grad_bias, s, w, ws, strm);
+        if (st != MPGNN_ERR_UNSUPPORTED) return st;
+        st = MPGNN_OK;
+    }
     // ---- grad_x = Σ_r A_rᵀ ((dout @ W_rᵀ) / cnt) + dout @ rootᵀ ----------------------
     auto grad_x_part = [&](hipStream_t strm) -> int32_t {
         float* G = reinterpret_cast<float*>(ws + w.g);
