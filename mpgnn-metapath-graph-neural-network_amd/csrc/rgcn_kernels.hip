@@ -3368,7 +3368,9 @@ __device__ __forceinline__ void bw_range(int n_items, int& i_beg, int& i_end) {
     i_end = (int)((long long)(rng + 1) * n_items / G);
 }
 
-// waves 0-3: dout rows of every item (both layouts) and, with g.Y, the dgrad products
+// waves 0-3: dout rows of every item (both layouts) and, with g.Y, the dgrad products. Rows
+// are gathered two items ahead (two register sets alternating roles), row indices three; the
+// next item's weight slice is loaded after the chain (the registers are free then).
 __device__ __forceinline__ void bw_dgrad_half(const BwdArgs& A, int i_beg, int i_end, __bf16* Rp, __bf16* Dt,
                                               float* Sc) {
     using Bs = RelGemm<2, true>;
@@ -3380,22 +3382,30 @@ __device__ __forceinline__ void bw_dgrad_half(const BwdArgs& A, int i_beg, int i
     const int lane = t & 63, c = lane & 31, h = lane >> 5;
     const int wq = __builtin_amdgcn_readfirstlane(t >> 6);
     const bool want_dx = a.Y != nullptr;
-    Item cur = Bs::item(a, i_beg);
-    int row[WPT], cnt = 1, nrow[WPT], ncnt = 1, zm;
-    float4 v[WPT];
-    Bs::gather_idx(a, cur, t, row, cnt);
-    Bs::issue_rows(a, t, row, v, zm);
-    if (i_beg + 1 < i_end) Bs::gather_idx(a, Bs::item(a, i_beg + 1), t, nrow, ncnt);
-    bf16x8 b[NS][3];
-    const float* wcur = nullptr;
     const int col_b = (wq * 32 + c) * 4;
-    for (int i = i_beg; i < i_end; ++i) {
-        // commit: split once, store row-major (dgrad A) and transposed (dW B); rows past the item: 0
+    Item cur = Bs::item(a, i_beg);
+    float4 va[WPT], vb[WPT];
+    int cnta = 1, cntb = 1, nrow[WPT], ncnt = 1, zm;
+    {
+        int r0[WPT];
+        Bs::gather_idx(a, cur, t, r0, cnta);
+        Bs::issue_rows(a, t, r0, va, zm);
+    }
+    if (i_beg + 1 < i_end) {
+        int r1[WPT];
+        Bs::gather_idx(a, Bs::item(a, i_beg + 1), t, r1, cntb);
+        Bs::issue_rows(a, t, r1, vb, zm);
+    }
+    if (i_beg + 2 < i_end) Bs::gather_idx(a, Bs::item(a, i_beg + 2), t, nrow, ncnt);
+    bf16x8 b[NS][3];
+    if (want_dx) Ds::load_b(cur.w, wq, lane, b);
+    // item i: vc / cntc hold its rows; after the commit they receive item i+2's
+    auto step = [&](int i, float4 (&vc)[WPT], int& cntc) {
 #pragma unroll
-        for (int j = 0; j < WPT; ++j) {
+        for (int j = 0; j < WPT; ++j) {  // commit: split once, row-major (dgrad A) + transposed (dW B)
             const int e = t + j * 256;
             const int r = e / W4, c4 = (e % W4) * 4;
-            const float4 xv = r < cur.nrows ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 xv = r < cur.nrows ? vc[j] : make_float4(0.f, 0.f, 0.f, 0.f);
             __bf16 p0[4], p1[4], p2[4];
             split3_bf16(xv.x, p0[0], p1[0], p2[0]);
             split3_bf16(xv.y, p0[1], p1[1], p2[1]);
@@ -3414,18 +3424,15 @@ __device__ __forceinline__ void bw_dgrad_half(const BwdArgs& A, int i_beg, int i
                 dt[2 * kBwTPlane] = p2[q];
             }
         }
-        if (t < 32) Sc[t] = 1.0f / (float)cnt;
-        if (want_dx && cur.w != wcur) {  // the item's weight slice (relation change)
-            Ds::load_b(cur.w, wq, lane, b);
-            wcur = cur.w;
+        if (t < 32) Sc[t] = 1.0f / (float)cntc;
+        if (i + 2 < i_end) {
+            int zn;
+            Bs::issue_rows(a, t, nrow, vc, zn);
+            cntc = ncnt;
+            if (i + 3 < i_end) Bs::gather_idx(a, Bs::item(a, i + 3), t, nrow, ncnt);
         }
         const bool has_next = i + 1 < i_end;
         const Item nxt = has_next ? Bs::item(a, i + 1) : cur;
-        if (has_next) {
-            Bs::issue_rows(a, t, nrow, v, zm);
-            cnt = ncnt;
-            if (i + 2 < i_end) Bs::gather_idx(a, Bs::item(a, i + 2), t, nrow, ncnt);
-        }
         __syncthreads();  // (1) the item's planes are in LDS
         if (want_dx) {
             const __bf16* Ab = Rp + c * kBwLdab + 8 * h;
@@ -3436,16 +3443,16 @@ __device__ __forceinline__ void bw_dgrad_half(const BwdArgs& A, int i_beg, int i
                 lo[r] = 0.0f;
             }
 #pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Ab + 16 * s);
-                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Ab + kBwRPlane + 16 * s);
-                const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * kBwRPlane + 16 * s);
-                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[s][0], lo, 0, 0, 0);
-                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][1], lo, 0, 0, 0);
-                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][2], lo, 0, 0, 0);
-                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][0], lo, 0, 0, 0);
-                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][1], lo, 0, 0, 0);
-                hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][0], hi, 0, 0, 0);
+            for (int s2 = 0; s2 < NS; ++s2) {
+                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Ab + 16 * s2);
+                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Ab + kBwRPlane + 16 * s2);
+                const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * kBwRPlane + 16 * s2);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[s2][0], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s2][1], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s2][2], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s2][0], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s2][1], lo, 0, 0, 0);
+                hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s2][0], hi, 0, 0, 0);
             }
             float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
             const int bytes = __builtin_amdgcn_readfirstlane(cur.nrows) * N * 4;
@@ -3457,13 +3464,19 @@ __device__ __forceinline__ void bw_dgrad_half(const BwdArgs& A, int i_beg, int i
                 if (!cur.root) o = o * Sc[rr];
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), rs, rr * (N * 4) + col_b, 0, 16);
             }
+            if (has_next && nxt.w != cur.w) Ds::load_b(nxt.w, wq, lane, b);  // after the chain
         }
         __syncthreads();  // (2) planes free for the next commit
         cur = nxt;
+    };
+    for (int i = i_beg; i < i_end; i += 2) {
+        step(i, va, cnta);
+        if (i + 1 < i_end) step(i + 1, vb, cntb);
     }
 }
 
-// waves 4-7: A rows of every item (transposed) and the dW / droot / dbias products
+// waves 4-7: A rows of every item (transposed) and the dW / droot / dbias products; rows two
+// items ahead like the other half
 __device__ __forceinline__ void bw_dw_half(const BwdArgs& A, int i_beg, int i_end, const __bf16* Dt, __bf16* Xt,
                                            float* bx) {
     using Bs = RelGemm<2, true>;
@@ -3493,11 +3506,19 @@ __device__ __forceinline__ void bw_dw_half(const BwdArgs& A, int i_beg, int i_en
             }
     };
     Item cur = Bs::item(a, i_beg);
-    int ia[2], nia[2] = {0, 0};
-    float xv[2][8];
-    load_idx(cur, ia);
-    issue(ia, xv);
-    if (i_beg + 1 < i_end) load_idx(Bs::item(a, i_beg + 1), nia);
+    int nia[2] = {0, 0};
+    float xa[2][8], xb[2][8];
+    {
+        int ia[2];
+        load_idx(cur, ia);
+        issue(ia, xa);
+    }
+    if (i_beg + 1 < i_end) {
+        int ia[2];
+        load_idx(Bs::item(a, i_beg + 1), ia);
+        issue(ia, xb);
+    }
+    if (i_beg + 2 < i_end) load_idx(Bs::item(a, i_beg + 2), nia);
     f32x16 hi[4], lo[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -3509,7 +3530,7 @@ __device__ __forceinline__ void bw_dw_half(const BwdArgs& A, int i_beg, int i_en
     float bpart = 0.0f;
     int slab = A.wg_slab0[blockIdx.x];
     int pending_b = -1;  // bias slab whose two halves wait in bx for the barrier
-    for (int i = i_beg; i < i_end; ++i) {
+    auto step = [&](int i, float (&xv)[2][8]) {
         if (pending_b >= 0) {  // after barrier (2) of the previous item
             if (t < 128) A.bslabs[(size_t)pending_b * 128 + col] = bx[t] + bx[t + 128];
             pending_b = -1;
@@ -3530,22 +3551,22 @@ __device__ __forceinline__ void bw_dw_half(const BwdArgs& A, int i_beg, int i_en
 #pragma unroll
             for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x8*>(d + p * kBwTPlane) = pa[p];
         }
+        if (i + 2 < i_end) {
+            issue(nia, xv);
+            if (i + 3 < i_end) load_idx(Bs::item(a, i + 3), nia);
+        }
         const bool has_next = i + 1 < i_end;
         const Item nxt = has_next ? Bs::item(a, i + 1) : cur;
-        if (has_next) {
-            issue(nia, xv);
-            if (i + 2 < i_end) load_idx(Bs::item(a, i + 2), nia);
-        }
         __syncthreads();  // (1)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const __bf16* Bf = Dt + (wq * 32 + c) * kBwLdt + 16 * s + 8 * h;
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const __bf16* Bf = Dt + (wq * 32 + c) * kBwLdt + 16 * s2 + 8 * h;
             const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(Bf);
             const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(Bf + kBwTPlane);
             const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(Bf + 2 * kBwTPlane);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const __bf16* Af = Xt + (q * 32 + c) * kBwLdt + 16 * s + 8 * h;
+                const __bf16* Af = Xt + (q * 32 + c) * kBwLdt + 16 * s2 + 8 * h;
                 const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Af);
                 const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Af + kBwTPlane);
                 const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(Af + 2 * kBwTPlane);
@@ -3589,6 +3610,10 @@ __device__ __forceinline__ void bw_dw_half(const BwdArgs& A, int i_beg, int i_en
         }
         __syncthreads();  // (2)
         cur = nxt;
+    };
+    for (int i = i_beg; i < i_end; i += 2) {
+        step(i, xa);
+        if (i + 1 < i_end) step(i + 1, xb);
     }
     if (pending_b >= 0 && t < 128) A.bslabs[(size_t)pending_b * 128 + col] = bx[t] + bx[t + 128];
 }
