@@ -32,10 +32,9 @@ class _SplitKLinear(torch.autograd.Function):
     with K = N, which the BLAS library tiles into a handful of long serial-K workgroups (66 µs
     for O = 2 at C3, 6 % of the epoch). Here K is cut into slices of ≤ 1024 rows: one batched
     GEMM over the slices + a sum over them — the same products in fp32, summed in a different
-    (blocked) order; for F ≤ 256 and the heads' shapes the C ABI's ``mpgnn_linear_wgrad`` does it
-    in two launches per block of 32·256/F outputs, bias gradient included (MPNetm.fc1 128 -> 128
-    at C3: 4 launches, where the batched library GEMM took 60 µs). Forward and grad_input are
-    exactly the autograd ones (``F.linear``, ``mm``)."""
+    (blocked) order; for F ≤ 256 and O ≤ 32·256/F the C ABI's ``mpgnn_linear_wgrad`` does it in
+    two launches, bias gradient included. Forward and grad_input are exactly the autograd ones
+    (``F.linear``, ``mm``)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -50,10 +49,10 @@ class _SplitKLinear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = g.mm(weight)
         f, o = x.shape[1], g.shape[1]
-        # the HIP pair is scalar-FMA work (N·F·O): for the heads' usual shapes (O ≤ 32·256/F, or a
-        # small N·F·O such as MPNetm.fc1 128 -> 128 at C3) it beats the library's serial-K GEMM; a
-        # wide head over millions of rows (C5 fc1 256 -> 256 at N = 2 M) goes to the batched GEMM
-        small = o <= 32 * (256 // max(f, 1)) or x.shape[0] * f * o <= (1 << 28)
+        # the HIP pair is scalar-FMA work (N·F·O): for the heads with few outputs (O ≤ 32·256/F:
+        # Net.lin, MPNetm.fc2) it beats the library's serial-K GEMM; wider heads (MPNetm.fc1
+        # 128 -> 128: 2 x 52 µs here against one 60 µs batched GEMM at C3) take the batched GEMM
+        small = o <= 32 * (256 // max(f, 1))
         if ctx.needs_input_grad[1] and f <= 256 and small and x.dtype == g.dtype == torch.float32:
             # one HIP kernel pair (row-sliced partials + ordered slice sum, bias in the same pass)
             # instead of pad + batched GEMM + two reductions (~8 launches)

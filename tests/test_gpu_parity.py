@@ -767,12 +767,35 @@ def test_c2_layer_backward_long_reduction_chunks():
                "dbias": convg.bias.grad}, r32, r64, "C2 ")
 
 
+@pytest.mark.parametrize("n,f,o", [(14541, 128, 128), (2000, 256, 200), (777, 96, 70)])
+def test_linear_wgrad_abi_output_blocks(n, f, o):
+    """mpgnn_linear_wgrad for heads wider than one pass (O > 32·256/F: output blocks of
+    32·256/F, the partials buffer reused in stream order): weight and bias gradient against the
+    float64 truth at the suite's bar."""
+    import ctypes
+    from mpgnn_amd import _lib
+    gen = torch.Generator().manual_seed(n + o)
+    x = torch.randn(n, f, generator=gen)
+    g = torch.randn(n, o, generator=gen)
+    xd, gd = x.to(DEV), g.to(DEV)
+    nb = ctypes.c_int64()
+    _lib.check(_lib.lib.mpgnn_linear_wgrad_workspace_bytes(n, f, o, ctypes.byref(nb)))
+    ws = torch.empty(int(nb.value), dtype=torch.uint8, device=DEV)
+    gw = torch.empty(o, f, device=DEV)
+    gb = torch.empty(o, device=DEV)
+    _lib.check(_lib.lib.mpgnn_linear_wgrad(xd.data_ptr(), gd.data_ptr(), n, f, o, gw.data_ptr(), gb.data_ptr(),
+                                           ws.data_ptr(), torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    rel_close(gw, g.t() @ x, what=f"linear_wgrad {n}x{f}->{o} dW", ref64=g.double().t() @ x.double())
+    rel_close(gb, g.sum(0), what=f"linear_wgrad {n}x{f}->{o} db", ref64=g.double().sum(0))
+
+
 @pytest.mark.parametrize("n,f_in,f_out", [(14541, 128, 2), (1000, 128, 64), (300, 64, 3), (14541, 128, 128),
                                          (2000, 256, 200)])
 def test_split_k_linear_matches_nn_linear(n, f_in, f_out):
     """model.linear: forward bit-identical to nn.Linear; grad_weight (sliced over rows) and
-    grad_bias / grad_input within fp32 rounding of autograd's — also for heads wider than one
-    pass of mpgnn_linear_wgrad (MPNetm.fc1 128 -> 128: two output blocks; 256 -> 200: seven)."""
+    grad_bias / grad_input within fp32 rounding of autograd's (wide heads such as MPNetm.fc1
+    128 -> 128 take the batched-GEMM slicing, the narrow ones the C ABI pair)."""
     from mpgnn_amd.model import linear
     torch.manual_seed(0)
     lin = torch.nn.Linear(f_in, f_out).to(DEV)
