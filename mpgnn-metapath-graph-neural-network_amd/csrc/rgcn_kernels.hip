@@ -2611,6 +2611,7 @@ struct OuterArgs {
     float* dst;              // direct destination (see dst_mode)
     float* Pb;               // nullable: [nchunks][Nn] column sums of B (bias grad)
     float* dst_b;            // direct bias destination when dst_mode == 3
+    int bias_of_a;           // outer_bf3_kernel root chunks: Pb = column sums of A instead (M == 128)
 };
 
 constexpr int kOuterLd = 288;                        // one row pair: 128 + 32 pad + 128
@@ -3258,7 +3259,7 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
             const int nr = min(SL, cur.p1 - cur.p0 - cur.sl * SL) - 8 * half;
             // this thread's column over its 8 rows of cur's slice, rebuilt exactly from the three
             // pieces in LDS ((b0 + b1) + b2 == b: the partial sums of the split are representable)
-            const __bf16* bc = cb + 3 * kOb3Plane + col * kOb3Ld + 8 * half;
+            const __bf16* bc = cb + (ra.bias_of_a ? 0 : 3 * kOb3Plane) + col * kOb3Ld + 8 * half;
             const bf16x8 q0 = *reinterpret_cast<const bf16x8*>(bc);
             const bf16x8 q1 = *reinterpret_cast<const bf16x8*>(bc + kOb3Plane);
             const bf16x8 q2 = *reinterpret_cast<const bf16x8*>(bc + 2 * kOb3Plane);
@@ -4748,11 +4749,26 @@ static int linear_parts(int64_t N) {
 
 static int linear_block(int F) { return kLinAcc * (kThreads / F); }  // outputs per pass
 
+// F = O = 128 (MPNetm.fc1 of one 128-wide metapath, model.py:224): gw = gᵀ x is a 128 × 128
+// outer-product sum over N rows — outer_bf3_kernel's root-chunk stream with A = grad_out,
+// B = x and the bias column sums taken from A (bias_of_a), row chunks of >= 64 rows (about two
+// per CU), then the ordered slab sum (reduce_slabs3_kernel). The scalar pair below needs 2 × ~50 µs
+// for this width at C3 (two output blocks), the library's sliced GEMM ~45-60 µs.
+static bool linear_bf3(int64_t N, int32_t F, int32_t O) { return g_gemm_bf3 && F == 128 && O == 128 && N > 0; }
+static int linear_bf3_chunk(int64_t N) {
+    const int64_t per = (N + 2 * (int64_t)cu_count() - 1) / (2 * (int64_t)cu_count());
+    return (int)std::max<int64_t>(64, (per + 15) / 16 * 16);
+}
+
 int32_t mpgnn_linear_wgrad_workspace_bytes(int64_t N, int32_t F, int32_t O, int64_t* bytes) {
     if (!bytes) return arg_error("NULL bytes");
     if (N < 0 || F <= 0 || O <= 0) return arg_error("bad N, F or O");
     if (F > kThreads) return arg_error("mpgnn_linear_wgrad: needs F <= 256");
     *bytes = (int64_t)linear_parts(N) * std::min(O, linear_block(F)) * (F + 1) * (int64_t)sizeof(float);
+    if (linear_bf3(N, F, O)) {
+        const int64_t nch = (N + linear_bf3_chunk(N) - 1) / linear_bf3_chunk(N);
+        *bytes = std::max<int64_t>(*bytes, nch * (128 * 128 + 128) * (int64_t)sizeof(float));
+    }
     return MPGNN_OK;
 }
 
@@ -4770,6 +4786,43 @@ int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int
         int32_t st = hip_check(hipMemsetAsync(grad_weight, 0, (size_t)O * F * sizeof(float), strm), "memset");
         if (st == MPGNN_OK && grad_bias) st = hip_check(hipMemsetAsync(grad_bias, 0, (size_t)O * sizeof(float), strm), "memset");
         return st;
+    }
+    if (linear_bf3(N, F, O)) {
+        const int chunk = linear_bf3_chunk(N);
+        const int nch = (int)((N + chunk - 1) / chunk);
+        float* Pb = P + (size_t)nch * 128 * 128;
+        OuterArgs orr{};
+        orr.row_lo = 0;
+        orr.row_hi = (int)N;
+        orr.chunk_rows = chunk;
+        orr.dst_mode = nch == 1 ? 3 : 0;
+        orr.A = grad_out;  // D[o][f] = Σ_i g[i][o] · x[i][f]
+        orr.M = 128;
+        orr.B = x;
+        orr.Nn = 128;
+        orr.P = P;
+        orr.dst = grad_weight;
+        orr.Pb = grad_bias ? Pb : nullptr;
+        orr.dst_b = grad_bias;
+        orr.bias_of_a = 1;
+        OuterArgs none{};
+        hipLaunchKernelGGL(outer_bf3_kernel, dim3(std::min(nch, cu_count() * 2)), dim3(kThreads), kOb3Lds, strm, orr,
+                           none, nch, nch);
+        int32_t st = hip_check(hipGetLastError(), "outer_bf3_kernel (linear) launch");
+        if (st != MPGNN_OK || nch == 1) return st;
+        ReduceArgs rw{}, rb{};
+        rw.P = P;
+        rw.elems = 128 * 128;
+        rw.nchunks = nch;
+        rw.dst = grad_weight;
+        rb.P = Pb;
+        rb.elems = 128;
+        rb.nchunks = nch;
+        rb.dst = grad_bias;
+        const int nb = grad_bias ? 1 : 0;
+        hipLaunchKernelGGL(reduce_slabs3_kernel, dim3(1 + nb, (128 * 128 + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                           strm, rw, rb, ReduceArgs{}, 1, nb, 0, ZeroList{});
+        return hip_check(hipGetLastError(), "reduce_slabs3_kernel (linear) launch");
     }
     // output blocks in order; the partials buffer is reused (stream order)
     for (int o_lo = 0; o_lo < O; o_lo += linear_block(F)) {

@@ -50,9 +50,10 @@ class _SplitKLinear(torch.autograd.Function):
             gx = g.mm(weight)
         f, o = x.shape[1], g.shape[1]
         # the HIP pair is scalar-FMA work (N·F·O): for the heads with few outputs (O ≤ 32·256/F:
-        # Net.lin, MPNetm.fc2) it beats the library's serial-K GEMM; wider heads (MPNetm.fc1
-        # 128 -> 128: 2 x 52 µs here against one 60 µs batched GEMM at C3) take the batched GEMM
-        small = o <= 32 * (256 // max(f, 1))
+        # Net.lin, MPNetm.fc2) it beats the library's serial-K GEMM; F = O = 128 (MPNetm.fc1 of
+        # one metapath) runs on the bf16-split matrix cores behind the same entry point; other
+        # wide heads take the batched GEMM
+        small = o <= 32 * (256 // max(f, 1)) or (f == 128 and o == 128)
         if ctx.needs_input_grad[1] and f <= 256 and small and x.dtype == g.dtype == torch.float32:
             # one HIP kernel pair (row-sliced partials + ordered slice sum, bias in the same pass)
             # instead of pad + batched GEMM + two reductions (~8 launches)

@@ -767,7 +767,8 @@ def test_c2_layer_backward_long_reduction_chunks():
                "dbias": convg.bias.grad}, r32, r64, "C2 ")
 
 
-@pytest.mark.parametrize("n,f,o", [(14541, 128, 128), (2000, 256, 200), (777, 96, 70)])
+@pytest.mark.parametrize("n,f,o", [(14541, 128, 128), (2000, 256, 200), (777, 96, 70), (1, 128, 128),
+                                   (64, 128, 128), (200003, 128, 128)])
 def test_linear_wgrad_abi_output_blocks(n, f, o):
     """mpgnn_linear_wgrad for heads wider than one pass (O > 32·256/F: output blocks of
     32·256/F, the partials buffer reused in stream order): weight and bias gradient against the
@@ -982,7 +983,8 @@ def test_relu_bwd_matches_threshold_backward(n, offset):
 
 
 @pytest.mark.parametrize("n,f,o,bias", [(14541, 128, 2, True), (1000, 128, 64, True), (5, 256, 32, False),
-                                        (3000, 64, 128, True), (700, 512, 4, True)])
+                                        (3000, 64, 128, True), (700, 512, 4, True), (14541, 128, 128, True),
+                                        (50, 128, 128, True), (70001, 128, 128, False)])
 def test_linear_head_gradients_vs_autograd(n, f, o, bias):
     """model.linear (the wrappers' heads, model.py:147 / :224-226): forward and all gradients vs
     plain autograd of F.linear, 1e-4 — the C-ABI mpgnn_linear_wgrad path (F <= 256) and the
