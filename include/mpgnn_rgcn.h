@@ -256,6 +256,20 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
                        float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
                        void* workspace, void* stream);
 
+/* mpgnn_rgcn_bwd with the parameter gradients ACCUMULATED: grad_weight / grad_root / grad_bias
+ * (all three required) receive dst + this call's gradient, computed exactly as mpgnn_rgcn_bwd's
+ * and added once per element (the value autograd's gradient accumulation of a parameter used
+ * twice produces: Net applies the same conv2 for layers 1..L-1, model.py:144-146). grad_x is
+ * written as by mpgnn_rgcn_bwd. Mode ALL, F_in = F_out = 128 on the bf16-split path only;
+ * MPGNN_ERR_UNSUPPORTED otherwise, with nothing launched. */
+int32_t mpgnn_rgcn_bwd_accumulate(const mpgnn_plan* plan, int32_t mode, int64_t relation,
+                                  int32_t num_relations, const float* x, int32_t F_in,
+                                  const float* weight, const float* root, int32_t F_out,
+                                  const float* h_save, const float* grad_out,
+                                  int64_t row_lo, int64_t row_hi,
+                                  float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
+                                  void* workspace, void* stream);
+
 /* --- score function --------------------------------------------------------
  * The metapath-candidate score of the reference, OutputLayer.forward non-bag branch
  * (model.py:74-89) as trained by train() / score_relation_parallel (main.py:641-673, 727-760).

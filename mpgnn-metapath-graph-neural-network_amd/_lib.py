@@ -85,6 +85,8 @@ SIGNATURES = [
     ("mpgnn_rgcn_fwd_act", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _P, _I32, _P, _P, _P, _I32, _P]),
     ("mpgnn_rgcn_bwd", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _I32, _P, _P, _I64, _I64,
                               _P, _P, _P, _P, _P, _P]),
+    ("mpgnn_rgcn_bwd_accumulate", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _I32, _P, _P, _I64, _I64,
+                                         _P, _P, _P, _P, _P, _P]),
     ("mpgnn_relu_bwd", _I32, [_P, _P, _I64, _P, _P]),
     ("mpgnn_linear_wgrad_workspace_bytes", _I32, [_I64, _I32, _I32, _PI64]),
     ("mpgnn_linear_wgrad", _I32, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P]),

@@ -2427,12 +2427,11 @@ __device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
     return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
-template <int S, bool EXTRA>
+template <int S, bool EXTRA, int KR = 4>  // KR: rows per sub-wave (1 for the 32-entry pieces)
 __global__ __launch_bounds__(kThreads) void gather_rows_kernel(GatherRowsArgs a) {
     constexpr int G = 64 / S;    // rows per load instruction
-    constexpr int KR = 4;        // rows per sub-wave
     constexpr int RPW = KR * G;  // rows per wave
-    constexpr int U = 16;        // row loads in flight per lane
+    constexpr int U = KR == 1 ? S : 16;  // row loads in flight per lane (a whole piece when KR = 1)
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int sub = lane / S;
@@ -2612,6 +2611,7 @@ struct OuterArgs {
     float* Pb;               // nullable: [nchunks][Nn] column sums of B (bias grad)
     float* dst_b;            // direct bias destination when dst_mode == 3
     int bias_of_a;           // outer_bf3_kernel root chunks: Pb = column sums of A instead (M == 128)
+    int acc;                 // outer_bf3_kernel: direct destinations get dst + D (mpgnn_rgcn_bwd_accumulate)
 };
 
 constexpr int kOuterLd = 288;                        // one row pair: 128 + 32 pad + 128
@@ -3272,6 +3272,7 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
         if (chunk_end) {
             float* D;
             float* Db = nullptr;
+            bool add = false;  // a final destination of an accumulating call: dst + D
             if (is_root) {
                 const int cidx = cur.chunk;
                 D = ra.P + (size_t)cidx * 128 * 128;
@@ -3279,13 +3280,17 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
                 if (ra.dst_mode == 3) {
                     D = ra.dst;
                     Db = ra.dst_b;
+                    add = ra.acc != 0;
                 }
             } else {
                 const int cidx = cur.chunk - ra_n;
                 D = wa.P + (size_t)cidx * 128 * 128;
                 if (wa.dst_mode == 1 || wa.dst_mode == 2) {
                     const int di = ld_uniform(wa.chunk_dst, cidx + wa.chunk_off);
-                    if (di >= 0) D = wa.dst + (size_t)(wa.dst_mode == 1 ? di : 0) * 128 * 128;
+                    if (di >= 0) {
+                        D = wa.dst + (size_t)(wa.dst_mode == 1 ? di : 0) * 128 * 128;
+                        add = wa.acc != 0;
+                    }
                 }
             }
             const int ln = opaque(lane);
@@ -3298,7 +3303,8 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int m = q * 32 + (r & 3) + 8 * (r >> 2) + h4;
-                        Dc[(size_t)m * 128] = hi[q][r] + lo[q][r];
+                        const float v = hi[q][r] + lo[q][r];
+                        Dc[(size_t)m * 128] = add ? Dc[(size_t)m * 128] + v : v;
                     }
             }
 #pragma unroll
@@ -3312,7 +3318,10 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
                 bx[tid] = bpart;
                 bpart = 0.0f;
                 __syncthreads();
-                if (tid < 128 && Db != nullptr) Db[tid] = bx[tid] + bx[tid + 128];
+                if (tid < 128 && Db != nullptr) {
+                    const float v = bx[tid] + bx[tid + 128];
+                    Db[tid] = add ? Db[tid] + v : v;
+                }
             }
         }
         __syncthreads();
@@ -3644,6 +3653,7 @@ struct ReduceArgs {
     int g_base;          // group index offset into gptr / gdst
     float* dst;
     int skip_single;     // groups of exactly one chunk were written directly: skip them
+    int acc;             // dst = dst + Σ (mpgnn_rgcn_bwd_accumulate)
 };
 
 __device__ __forceinline__ void reduce_slabs_body(const ReduceArgs& a, const int g) {
@@ -3673,7 +3683,8 @@ __device__ __forceinline__ void reduce_slabs_body(const ReduceArgs& a, const int
         s += v[0];
     }
     const int d = a.gdst != nullptr ? a.gdst[a.g_base + g] : g;
-    a.dst[(size_t)d * a.elems + e] = s;
+    float* dp = a.dst + (size_t)d * a.elems + e;
+    *dp = a.acc ? *dp + s : s;
 }
 
 
@@ -4311,22 +4322,31 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
     return hip_check(hipGetLastError(), "seg_tile_kernel launch");
 }
 
-template <int S>
-static void launch_gather_rows_s(const GatherRowsArgs& a, hipStream_t st) {
-    constexpr int rows_per_block = kWaves * 4 * (64 / S);
+template <int S, int KR>
+static void launch_gather_rows_k(const GatherRowsArgs& a, hipStream_t st) {
+    constexpr int rows_per_block = kWaves * KR * (64 / S);
     const int rows = a.N - a.r_begin;
     const dim3 grid((rows + rows_per_block - 1) / rows_per_block);
     if (a.extra != nullptr || a.bias != nullptr)
-        hipLaunchKernelGGL((gather_rows_kernel<S, true>), grid, dim3(kThreads), 0, st, a);
+        hipLaunchKernelGGL((gather_rows_kernel<S, true, KR>), grid, dim3(kThreads), 0, st, a);
     else
-        hipLaunchKernelGGL((gather_rows_kernel<S, false>), grid, dim3(kThreads), 0, st, a);
+        hipLaunchKernelGGL((gather_rows_kernel<S, false, KR>), grid, dim3(kThreads), 0, st, a);
 }
 
-static void launch_gather_rows(const GatherRowsArgs& a, hipStream_t st) {
-    if (a.F <= 32) launch_gather_rows_s<8>(a, st);
-    else if (a.F <= 64) launch_gather_rows_s<16>(a, st);
-    else if (a.F <= 128) launch_gather_rows_s<32>(a, st);
-    else launch_gather_rows_s<64>(a, st);
+// pieces (<= kPieceEntries entries each): one per sub-wave, all its entries in flight at once
+// (C3 mode-SINGLE grad_x, 70 pieces: four pieces chained per sub-wave took 26 us); rows: four
+// per sub-wave, their entries concatenated (rows average a few entries)
+template <int S>
+static void launch_gather_rows_s(const GatherRowsArgs& a, hipStream_t st, bool pieces) {
+    if (pieces) launch_gather_rows_k<S, 1>(a, st);
+    else launch_gather_rows_k<S, 4>(a, st);
+}
+
+static void launch_gather_rows(const GatherRowsArgs& a, hipStream_t st, bool pieces = false) {
+    if (a.F <= 32) launch_gather_rows_s<8>(a, st, pieces);
+    else if (a.F <= 64) launch_gather_rows_s<16>(a, st, pieces);
+    else if (a.F <= 128) launch_gather_rows_s<32>(a, st, pieces);
+    else launch_gather_rows_s<64>(a, st, pieces);
 }
 
 // Ordered row sums out[i] = Σ list(i) + extra + bias, with the pieces of long rows first.
@@ -4357,7 +4377,7 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
             ga.out_off = k_lo;
             ga.dummy = a.g.dummy;
             TimedLaunch tl(MPGNN_K_PIECE, strm);
-            launch_gather_rows(ga, strm);
+            launch_gather_rows(ga, strm, true);
         } else {
             PieceArgs pa{};
             pa.pb = pb;
@@ -5414,7 +5434,7 @@ int32_t mpgnn_rel_mean_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, 
 static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const float* x, int32_t F_in, int32_t F_out,
                           const float* h_save, const float* grad_out, float* grad_weight, float* grad_root,
                           float* grad_bias, const Selection& s, const WsLayout& w, const RootChunks& rc, char* ws,
-                          hipStream_t strm);
+                          hipStream_t strm, bool acc);
 
 
 // The backward at F_in = F_out = 128 through bwd_bf3_kernel (dgrad + dW / droot / dbias in one
@@ -5584,11 +5604,11 @@ static int32_t bwd_fused(const mpgnn_plan* p, int32_t mode, int32_t R, const flo
     return st;
 }
 
-int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
-                       int32_t F_in, const float* weight, const float* root, int32_t F_out,
-                       const float* h_save, const float* grad_out, int64_t row_lo, int64_t row_hi,
-                       float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
-                       void* workspace, void* stream) {
+static int32_t rgcn_bwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
+                             int32_t F_in, const float* weight, const float* root, int32_t F_out,
+                             const float* h_save, const float* grad_out, int64_t row_lo, int64_t row_hi,
+                             float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
+                             void* workspace, void* stream, bool acc) {
     int32_t st = check_common(p, F_in, F_out);
     if (st != MPGNN_OK) return st;
     Selection s;
@@ -5604,7 +5624,15 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
 
     const bool want_x = grad_x != nullptr && p->N > 0;
     const bool want_p = grad_weight != nullptr || grad_root != nullptr || grad_bias != nullptr;
-    if (g_bwd_fused && g_gemm_bf3 && g_rel_gemm && !exact && F_in == 128 && F_out == 128 && p->N > 0 && x != nullptr &&
+    if (acc) {
+        // accumulating parameter gradients: the mode-ALL F = 128 path (outer_bf3_kernel + the
+        // ordered slab sum) only, decided before anything is launched
+        const int nch = s.c_hi - s.c_lo;
+        if (mode != MPGNN_MODE_ALL || !g_gemm_bf3 || F_in != 128 || F_out != 128 || !grad_weight || !grad_root ||
+            !grad_bias || nch <= 0 || rc.n <= 0 || !x)
+            return MPGNN_ERR_UNSUPPORTED;
+    }
+    if (!acc && g_bwd_fused && g_gemm_bf3 && g_rel_gemm && !exact && F_in == 128 && F_out == 128 && p->N > 0 && x != nullptr &&
         root != nullptr && grad_weight != nullptr && grad_root != nullptr && (h_save != nullptr || s.m_hi == s.m_lo) &&
         p->N <= INT32_MAX - 1) {
         st = bwd_fused(p, mode, R, x, weight, root, h_save, grad_out, row_lo, row_hi, want_x ? grad_x : nullptr,
@@ -5626,15 +5654,33 @@ int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int3
     // joined into the caller's — measured slower: C3 epoch 1.163 -> 1.207 ms; not kept)
     if (want_x && (st = grad_x_part(strm)) != MPGNN_OK) return st;
     if (want_p) st = bwd_params(p, mode, R, x, F_in, F_out, h_save, grad_out, grad_weight, grad_root, grad_bias, s, w,
-                                rc, ws, strm);
+                                rc, ws, strm, acc);
     return st;
+}
+
+int32_t mpgnn_rgcn_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
+                       int32_t F_in, const float* weight, const float* root, int32_t F_out,
+                       const float* h_save, const float* grad_out, int64_t row_lo, int64_t row_hi,
+                       float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
+                       void* workspace, void* stream) {
+    return rgcn_bwd_impl(p, mode, relation, R, x, F_in, weight, root, F_out, h_save, grad_out, row_lo, row_hi, grad_x,
+                         grad_weight, grad_root, grad_bias, workspace, stream, false);
+}
+
+int32_t mpgnn_rgcn_bwd_accumulate(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
+                                  int32_t F_in, const float* weight, const float* root, int32_t F_out,
+                                  const float* h_save, const float* grad_out, int64_t row_lo, int64_t row_hi,
+                                  float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
+                                  void* workspace, void* stream) {
+    return rgcn_bwd_impl(p, mode, relation, R, x, F_in, weight, root, F_out, h_save, grad_out, row_lo, row_hi, grad_x,
+                         grad_weight, grad_root, grad_bias, workspace, stream, true);
 }
 
 // the parameter gradients of mpgnn_rgcn_bwd (dW / droot / dbias outer products + slab reduce)
 static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const float* x, int32_t F_in, int32_t F_out,
                           const float* h_save, const float* grad_out, float* grad_weight, float* grad_root,
                           float* grad_bias, const Selection& s, const WsLayout& w, const RootChunks& rc, char* ws,
-                          hipStream_t strm) {
+                          hipStream_t strm, bool acc) {
     int32_t st = MPGNN_OK;
     const size_t wsize = (size_t)F_in * F_out;
     const bool exact = g_exact_order;
@@ -5664,7 +5710,8 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
         const size_t wbytes = (mode == MPGNN_MODE_ALL ? (size_t)std::max(R, 0) : 1) * wsize * sizeof(float);
         // every weight index with a segment range is written (directly or by the slab reduce,
         // zeros for an empty range); only indices absent from the plan need the memset
-        const bool all_written = (mode == MPGNN_MODE_ALL) ? (s.d_hi - s.d_lo) == (int64_t)R : (s.c_hi > s.c_lo);
+        // (accumulating: absent relation ids keep their gradient)
+        const bool all_written = acc || ((mode == MPGNN_MODE_ALL) ? (s.d_hi - s.d_lo) == (int64_t)R : (s.c_hi > s.c_lo));
         if (!all_written && mode == MPGNN_MODE_ALL && (int64_t)R - (s.d_hi - s.d_lo) <= kMaxZeroIds) {
             // the few absent relation ids are zeroed by the reduce launch
             zl.dst = grad_weight;
@@ -5707,12 +5754,14 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
             ow.P = P;
             ow.dst = grad_weight;
             ow.Pb = nullptr;
+            ow.acc = acc ? 1 : 0;
             have_w = true;
             ReduceArgs r{};
             r.P = P;
             r.elems = (int)wsize;
             r.dst = grad_weight;
             r.skip_single = 1;
+            r.acc = acc ? 1 : 0;
             const int ey = (int)((wsize + kThreads - 1) / kThreads);
             if (mode == MPGNN_MODE_ALL) {
                 r.gptr = p->d.rel_chunk_ptr;
@@ -5753,6 +5802,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
             orr.dst = grad_root;
             orr.Pb = grad_bias ? Pb : nullptr;
             orr.dst_b = grad_bias;
+            orr.acc = acc ? 1 : 0;
             have_root = true;
             if (rc.n > 1 && grad_root) {
                 ReduceArgs r{};
@@ -5760,6 +5810,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
                 r.elems = (int)wsize;
                 r.nchunks = rc.n;
                 r.dst = grad_root;
+                r.acc = acc ? 1 : 0;
                 reduces.push_back({r, 1, (int)((wsize + kThreads - 1) / kThreads)});
             }
             if (rc.n > 1 && grad_bias) {
@@ -5768,12 +5819,15 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
                 r.elems = F_out;
                 r.nchunks = rc.n;
                 r.dst = grad_bias;
+                r.acc = acc ? 1 : 0;
                 reduces.push_back({r, 1, (F_out + kThreads - 1) / kThreads});
             }
         }
     }
     const int root_y = grad_root ? mt : 1;
-    if (have_w && have_root && root_y == mt && g_gemm_bf3 && F_in == 128 && F_out == 128) {
+    const bool bf3 = have_w && have_root && root_y == mt && g_gemm_bf3 && F_in == 128 && F_out == 128;
+    if (acc && !bf3) return MPGNN_ERR_UNSUPPORTED;  // (excluded by rgcn_bwd_impl's check)
+    if (bf3) {
         // F_in = F_out = 128: the bf16-split persistent kernel (outer_bf3_kernel)
         TimedLaunch tl(MPGNN_K_OUTER, strm);
         const int n_all = nch + rc.n;

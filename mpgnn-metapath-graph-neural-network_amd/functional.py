@@ -22,7 +22,7 @@ import ctypes
 import torch
 import torch.distributed as dist
 
-from ._lib import ACT_NONE, ACT_RELU, MODE_ALL, MODE_SINGLE, check, lib
+from ._lib import ACT_NONE, ACT_RELU, MODE_ALL, MODE_SINGLE, MPGNN_ERR_UNSUPPORTED, check, lib
 from .plan import GraphPlan
 
 __all__ = ["rgcn_conv", "segment_means", "MODE_SINGLE", "MODE_ALL"]
@@ -127,10 +127,25 @@ def _forward(x, weight, root, bias, plan: GraphPlan, mode: int, relation: int, n
     return out, x, weight, root, h_save
 
 
+class GradStash:
+    """Parameter gradients of a layer applied several times in one forward (Net's conv2 for
+    layers 1..L-1, model.py:144-146), summed inside the backward kernels instead of by autograd's
+    gradient accumulation (one [R, F, F] add per extra use). Each use carries a role: ``"first"``
+    (the LAST use in forward order, whose backward runs first: fresh gradients, kept here),
+    ``"mid"`` (added to them) and ``"final"`` (the first use: added, then handed to autograd);
+    the other uses hand autograd no parameter gradient. The sums are autograd's: dst + new,
+    in backward order."""
+    __slots__ = ("bufs",)
+
+    def __init__(self):
+        self.bufs = None
+
+
 class _RGCNConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, root, bias, plan: GraphPlan, mode: int, relation: int,
-                num_relations: int, row_lo: int, row_hi: int, group, act: int, params_reduced: bool):
+                num_relations: int, row_lo: int, row_hi: int, group, act: int, params_reduced: bool,
+                stash=None):
         out, x, weight, root, h_save = _forward(x, weight, root, bias, plan, mode, relation, num_relations,
                                                 row_lo, row_hi, group, ctx.needs_input_grad[1], act)
         ctx.plan = plan
@@ -140,6 +155,7 @@ class _RGCNConvFn(torch.autograd.Function):
         ctx.params_reduced = params_reduced
         ctx.has_root, ctx.has_bias = root is not None, bias is not None
         ctx.act = act
+        ctx.stash = stash
         ctx.save_for_backward(x, weight, root, h_save, out if act == ACT_RELU else None)
         return out
 
@@ -159,6 +175,8 @@ class _RGCNConvFn(torch.autograd.Function):
         f_out = weight.shape[-1]
         nx, nw, nr, nb = ctx.needs_input_grad[:4]
         gx = torch.empty_like(x) if nx else None
+        if ctx.stash is not None and ctx.group is None and nw and nr and nb and root is not None and ctx.has_bias:
+            return _shared_backward(ctx, plan, x, weight, root, h_save, grad_out, gx)
         want = [nw, nr and root is not None, nb and ctx.has_bias]
         shapes = [weight.shape, root.shape if root is not None else None, (f_out,)]
         flat = None
@@ -188,18 +206,51 @@ class _RGCNConvFn(torch.autograd.Function):
                     dist.all_reduce(gx, group=ctx.group)
             if flat is not None:
                 dist.all_reduce(flat, group=ctx.group)
-        return gx, gw, gr, gb, None, None, None, None, None, None, None, None, None
+        return gx, gw, gr, gb, None, None, None, None, None, None, None, None, None, None
+
+
+def _shared_backward(ctx, plan, x, weight, root, h_save, grad_out, gx):
+    """_RGCNConvFn.backward of one use of a shared layer (GradStash)."""
+    stash, role = ctx.stash
+    N, f_in = x.shape
+    f_out = weight.shape[-1]
+    ws = _workspace(plan.workspace_bytes(ctx.mode, ctx.relation, ctx.num_relations, f_in, f_out, *ctx.rows), x.device)
+    args_head = (plan.handle, ctx.mode, int(ctx.relation), int(ctx.num_relations), x.data_ptr(), f_in,
+                 weight.data_ptr(), root.data_ptr(), f_out, _ptr(h_save), grad_out.data_ptr(), ctx.rows[0],
+                 ctx.rows[1], _ptr(gx))
+    if role == "first" or stash.bufs is None:
+        bufs = tuple(torch.empty(sh, dtype=torch.float32, device=x.device) for sh in (weight.shape, root.shape, (f_out,)))
+        check(lib.mpgnn_rgcn_bwd(*args_head, *(b.data_ptr() for b in bufs), ws.data_ptr(), _stream(x)),
+              "mpgnn_rgcn_bwd")
+        stash.bufs = bufs
+    else:
+        bufs = stash.bufs
+        st = lib.mpgnn_rgcn_bwd_accumulate(*args_head, *(b.data_ptr() for b in bufs), ws.data_ptr(), _stream(x))
+        if st == MPGNN_ERR_UNSUPPORTED:  # other widths / modes: fresh gradients, then autograd's add
+            new = tuple(torch.empty_like(b) for b in bufs)
+            check(lib.mpgnn_rgcn_bwd(*args_head, *(b.data_ptr() for b in new), ws.data_ptr(), _stream(x)),
+                  "mpgnn_rgcn_bwd")
+            for b, n in zip(bufs, new):
+                b.add_(n)
+        else:
+            check(st, "mpgnn_rgcn_bwd_accumulate")
+    none = (None,) * 10
+    if role == "final":
+        stash.bufs = None
+        return (gx,) + bufs + none
+    return (gx, None, None, None) + none
 
 
 def rgcn_conv(x: torch.Tensor, weight: torch.Tensor, root, bias, plan: GraphPlan, mode: int,
               relation: int = -1, num_relations: int = 0, row_range=None, group=None,
-              activation=None, params_reduced: bool = False) -> torch.Tensor:
+              activation=None, params_reduced: bool = False, grad_stash=None) -> torch.Tensor:
     """One relational conv layer on the GPU (see module docstring).
 
     ``activation='relu'`` returns ``F.relu(layer(x))`` (model.py:144,146): fused into the
     combine epilogue when the layer is unsharded, applied after the all-reduce otherwise.
     ``params_reduced``: with a ``group``, the caller reduces the parameter gradients itself
-    (``distributed.ShardGradReducer``); otherwise the backward all-reduces them (one bucket)."""
+    (``distributed.ShardGradReducer``); otherwise the backward all-reduces them (one bucket).
+    ``grad_stash``: ``(GradStash, role)`` for a layer applied several times (see GradStash)."""
     if activation not in (None, "relu"):
         raise ValueError(f"activation must be None or 'relu', got {activation!r}")
     lo, hi = row_range if row_range is not None else (0, plan.num_nodes)
@@ -214,7 +265,8 @@ def rgcn_conv(x: torch.Tensor, weight: torch.Tensor, root, bias, plan: GraphPlan
                        int(lo), int(hi), group, False, act)[0]
     else:
         out = _RGCNConvFn.apply(x, weight, root, bias, plan, int(mode), int(relation),
-                                int(num_relations), int(lo), int(hi), group, act, bool(params_reduced))
+                                int(num_relations), int(lo), int(hi), group, act, bool(params_reduced),
+                                grad_stash if group is None else None)
     if activation == "relu" and not fuse:
         out = torch.relu(out)
     return out

@@ -18,6 +18,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .mp_rgcn_layer import CustomRGCNConv
+from .functional import GradStash
 from .nn import RGCNConv
 from .score import InputLayer, OutputLayer, Score  # noqa: F401  (model.py:26-125)
 
@@ -123,10 +124,20 @@ class Net(_FastTrainToggle, torch.nn.Module):
         self.LinearLayer = torch.nn.Linear(output_dim, ll_output_dim)
 
     def forward(self, x, edge_index, edge_type, *, shard=None, group=None, shard_side="gathered"):
+        last = self.metapath_length - 1
+        stash = None
+        if last >= 2 and shard is None and group is None and x.is_cuda and torch.is_grad_enabled() and \
+                all(p.requires_grad for p in (self.conv2.weight, self.conv2.root, self.conv2.bias)):
+            # conv2's gradients over its uses summed inside the backward kernels (GradStash)
+            stash = GradStash()
         for layer_index in range(0, self.metapath_length):
             conv = self.conv1 if layer_index == 0 else self.conv2
+            kw = {}
+            if stash is not None and layer_index >= 1:
+                kw["_grad_stash"] = (stash, "first" if layer_index == last else "final" if layer_index == 1 else "mid")
             # F.relu(conv(...)) of model.py:144,146, fused into the layer's combine kernel
-            x = conv(x, edge_index, edge_type, shard=shard, group=group, activation="relu", shard_side=shard_side)
+            x = conv(x, edge_index, edge_type, shard=shard, group=group, activation="relu", shard_side=shard_side,
+                     **kw)
         x = linear(self.LinearLayer, x)
         return F.log_softmax(x, dim=1)
 

@@ -72,7 +72,7 @@ class RGCNConv(torch.nn.Module):
         zeros(self.bias)
 
     def forward(self, x, edge_index, edge_type=None, *, shard=None, group=None, activation=None,
-                shard_side="gathered"):
+                shard_side="gathered", _grad_stash=None):
         """``shard=(lo, hi)`` + ``group``: this rank owns the edges whose gathered node lies in
         [lo, hi) (dst-range sharding; ``shard_side="rows"``: whose aggregating
         node lies in it, the rank's output rows then being complete); outputs are all-reduced.
@@ -108,7 +108,8 @@ class RGCNConv(torch.nn.Module):
             reduced = True
         return rgcn_conv(x, self.weight, self.root, self.bias, plan, MODE_ALL,
                          num_relations=self.num_relations, row_range=row_range, group=group,
-                         activation=activation, params_reduced=reduced)
+                         activation=activation, params_reduced=reduced,
+                         grad_stash=_grad_stash if shard is None else None)
 
     def __repr__(self) -> str:
         return (f"{self.__class__.__name__}({self.in_channels}, "
