@@ -5631,6 +5631,13 @@ static int32_t rgcn_bwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         if (mode != MPGNN_MODE_ALL || !g_gemm_bf3 || F_in != 128 || F_out != 128 || !grad_weight || !grad_root ||
             !grad_bias || nch <= 0 || rc.n <= 0 || !x)
             return MPGNN_ERR_UNSUPPORTED;
+        // where mpgnn_rgcn_bwd takes the one-launch bwd_fused path (few items per CU) its
+        // gradients are summed in another order: refused, so that the caller's fallback (fresh
+        // gradients + one add) stays bit-identical to autograd's accumulation of that path
+        const int64_t items = (int64_t)(s.t32_hi - s.t32_lo) + (row_hi - row_lo + 31) / 32;
+        if (g_bwd_fused && g_rel_gemm && !exact && root && (h_save != nullptr || s.m_hi == s.m_lo) &&
+            p->N <= INT32_MAX - 1 && row_hi > row_lo && items <= 4 * (int64_t)cu_count())
+            return MPGNN_ERR_UNSUPPORTED;
     }
     if (!acc && g_bwd_fused && g_gemm_bf3 && g_rel_gemm && !exact && F_in == 128 && F_out == 128 && p->N > 0 && x != nullptr &&
         root != nullptr && grad_weight != nullptr && grad_root != nullptr && (h_save != nullptr || s.m_hi == s.m_lo) &&

@@ -12,6 +12,7 @@ The score-function classes (model.py:26-125: InputLayer, OutputLayer, Score) are
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -113,6 +114,10 @@ class _FastTrainToggle:
         return self
 
 
+# MPGNN_GRAD_STASH=0: Net's shared conv2 gradients summed by autograd (A/B switch; same values)
+_GRAD_STASH = os.environ.get("MPGNN_GRAD_STASH", "1") != "0"
+
+
 class Net(_FastTrainToggle, torch.nn.Module):
     """RGCN baseline (model.py:132-149): conv1, then the SAME conv2 for layers 1..L-1."""
 
@@ -126,7 +131,7 @@ class Net(_FastTrainToggle, torch.nn.Module):
     def forward(self, x, edge_index, edge_type, *, shard=None, group=None, shard_side="gathered"):
         last = self.metapath_length - 1
         stash = None
-        if last >= 2 and shard is None and group is None and x.is_cuda and torch.is_grad_enabled() and \
+        if last >= 2 and _GRAD_STASH and shard is None and group is None and x.is_cuda and torch.is_grad_enabled() and \
                 all(p.requires_grad for p in (self.conv2.weight, self.conv2.root, self.conv2.bias)):
             # conv2's gradients over its uses summed inside the backward kernels (GradStash)
             stash = GradStash()
