@@ -2611,7 +2611,6 @@ struct OuterArgs {
     float* Pb;               // nullable: [nchunks][Nn] column sums of B (bias grad)
     float* dst_b;            // direct bias destination when dst_mode == 3
     int bias_of_a;           // outer_bf3_kernel root chunks: Pb = column sums of A instead (M == 128)
-    int acc;                 // outer_bf3_kernel: direct destinations get dst + D (mpgnn_rgcn_bwd_accumulate)
 };
 
 constexpr int kOuterLd = 288;                        // one row pair: 128 + 32 pad + 128
@@ -3272,7 +3271,6 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
         if (chunk_end) {
             float* D;
             float* Db = nullptr;
-            bool add = false;  // a final destination of an accumulating call: dst + D
             if (is_root) {
                 const int cidx = cur.chunk;
                 D = ra.P + (size_t)cidx * 128 * 128;
@@ -3280,17 +3278,13 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
                 if (ra.dst_mode == 3) {
                     D = ra.dst;
                     Db = ra.dst_b;
-                    add = ra.acc != 0;
                 }
             } else {
                 const int cidx = cur.chunk - ra_n;
                 D = wa.P + (size_t)cidx * 128 * 128;
                 if (wa.dst_mode == 1 || wa.dst_mode == 2) {
                     const int di = ld_uniform(wa.chunk_dst, cidx + wa.chunk_off);
-                    if (di >= 0) {
-                        D = wa.dst + (size_t)(wa.dst_mode == 1 ? di : 0) * 128 * 128;
-                        add = wa.acc != 0;
-                    }
+                    if (di >= 0) D = wa.dst + (size_t)(wa.dst_mode == 1 ? di : 0) * 128 * 128;
                 }
             }
             const int ln = opaque(lane);
@@ -3303,8 +3297,7 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int m = q * 32 + (r & 3) + 8 * (r >> 2) + h4;
-                        const float v = hi[q][r] + lo[q][r];
-                        Dc[(size_t)m * 128] = add ? Dc[(size_t)m * 128] + v : v;
+                        Dc[(size_t)m * 128] = hi[q][r] + lo[q][r];
                     }
             }
 #pragma unroll
@@ -3318,10 +3311,7 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
                 bx[tid] = bpart;
                 bpart = 0.0f;
                 __syncthreads();
-                if (tid < 128 && Db != nullptr) {
-                    const float v = bx[tid] + bx[tid + 128];
-                    Db[tid] = add ? Db[tid] + v : v;
-                }
+                if (tid < 128 && Db != nullptr) Db[tid] = bx[tid] + bx[tid + 128];
             }
         }
         __syncthreads();
@@ -5748,7 +5738,9 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
             ow.chunk_end = p->d.chunk_end;
             ow.chunk_dst = p->d.chunk_dst;
             ow.chunk_off = s.c_lo;
-            ow.dst_mode = mode == MPGNN_MODE_ALL ? 1 : 2;
+            // accumulating: every chunk to a slab, the reduce adds dst + Σ (the MFMA kernel's
+            // epilogue stays store-only: a read-modify-write there cost 9 us per launch)
+            ow.dst_mode = acc ? 0 : (mode == MPGNN_MODE_ALL ? 1 : 2);
             ow.A = x;  // segment s: x[s_src[s]] or Hm[-s_src[s] - 1 - m_lo]
             ow.a_idx = p->d.s_src;
             ow.A2 = H;
@@ -5761,13 +5753,12 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
             ow.P = P;
             ow.dst = grad_weight;
             ow.Pb = nullptr;
-            ow.acc = acc ? 1 : 0;
             have_w = true;
             ReduceArgs r{};
             r.P = P;
             r.elems = (int)wsize;
             r.dst = grad_weight;
-            r.skip_single = 1;
+            r.skip_single = acc ? 0 : 1;
             r.acc = acc ? 1 : 0;
             const int ey = (int)((wsize + kThreads - 1) / kThreads);
             if (mode == MPGNN_MODE_ALL) {
@@ -5798,7 +5789,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
             orr.row_lo = rc.rows_lo;
             orr.row_hi = rc.rows_hi;
             orr.chunk_rows = rc.chunk;
-            orr.dst_mode = rc.n == 1 ? 3 : 0;
+            orr.dst_mode = (rc.n == 1 && !acc) ? 3 : 0;
             orr.A = x;
             orr.M = F_in;
             orr.a_off = 0;
@@ -5809,9 +5800,8 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
             orr.dst = grad_root;
             orr.Pb = grad_bias ? Pb : nullptr;
             orr.dst_b = grad_bias;
-            orr.acc = acc ? 1 : 0;
             have_root = true;
-            if (rc.n > 1 && grad_root) {
+            if ((rc.n > 1 || acc) && grad_root) {
                 ReduceArgs r{};
                 r.P = P;
                 r.elems = (int)wsize;
@@ -5820,7 +5810,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
                 r.acc = acc ? 1 : 0;
                 reduces.push_back({r, 1, (int)((wsize + kThreads - 1) / kThreads)});
             }
-            if (rc.n > 1 && grad_bias) {
+            if ((rc.n > 1 || acc) && grad_bias) {
                 ReduceArgs r{};
                 r.P = Pb;
                 r.elems = F_out;
