@@ -122,11 +122,14 @@ def setup_dist(n):
     # rehearsal of the N > 1 flow on a one-GPU box: every rank on device 0 over gloo
     # (MPGNN_BENCH_REHEARSE=1); the numbers of such a run are not a measurement
     rehearse = os.environ.get("MPGNN_BENCH_REHEARSE") == "1"
+    # MPGNN_BENCH_FORCE_DIST=1: the sharded path through a real process group even at N = 1
+    # (RCCL with one rank: every collective runs, each an identity) — the world-1 RCCL test
+    force = os.environ.get("MPGNN_BENCH_FORCE_DIST") == "1"
     if rehearse:
         local = 0
     torch.cuda.set_device(local)
     group = None
-    if world > 1:
+    if world > 1 or force:
         if rehearse:
             dist.init_process_group("gloo")
         else:
@@ -506,6 +509,7 @@ def main():
     if args.mode == "score":
         return bench_score(args)
     rank, world, local, group = setup_dist(args.gpus)
+    sharded = group is not None
     dev = torch.device("cuda", local)
     if args.workload.startswith("fb15k237"):
         g = data.fb15k237_graph(feat_dim=args.feat, seed=0,
@@ -519,7 +523,7 @@ def main():
     single = args.mode == "single"
     shard = ranges = None
     side = args.shard_side
-    if world > 1:
+    if sharded:
         ranges = shard_ranges(g.edge_index, g.num_nodes, world, side=side)
         shard = ranges[rank]
     torch.manual_seed(10)  # main_rgcn.py:31 / main.py:31-style seeding of the init
@@ -539,7 +543,7 @@ def main():
         model = model.to(dev).eval()
         convs = list(model.layers_list[0])
         edges_per_step = int(sum(int(rel_counts[r]) for r in metapath))
-        if world > 1:
+        if sharded:
             raise SystemExit("--mode single shards nothing (MPGNN candidates are replicas: distributed.metapath_fanout)")
 
         def step():
@@ -558,7 +562,7 @@ def main():
         layers = args.layers
 
         def step():
-            if world > 1:  # partial sums per rank, reduce-scatter per layer (or all-gather of rows)
+            if sharded:  # partial sums per rank, reduce-scatter per layer (or all-gather of rows)
                 return sharded_stack_forward(convs, x, ei, et, ranges, group, shard_side=side)
             h = x
             for conv in convs:
@@ -601,10 +605,10 @@ def main():
     torch.cuda.synchronize()
     _lib.lib.mpgnn_timing_enable(0)
     # mode SINGLE at F = 256 (rgcn_kernels.hip root_epi): root items finish the segment-less rows
-    root_epi = bool(single and F == 256 and world == 1)
+    root_epi = bool(single and F == 256 and not sharded)
     kinds = {"mean": "segment means (flat_rows_kernel over the multi-edge segments)",
              "seg_fwd": ("split-K transform GEMM of the whole layer (single_bf3_kernel)"
-                         if single and args.gemm == "bf3" and F in (64, 128) and world == 1 else
+                         if single and args.gemm == "bf3" and F in (64, 128) and not sharded else
                          "transform GEMM (rel_gemm_bf3_kernel / rel_gemm_kernel)"),
              "row_fwd": (("rows with a segment: single_fix_kernel (the root items' epilogue finished the others)"
                           if root_epi else "combine / output (single_combine_kernel: node -> segment map, one "
@@ -635,7 +639,7 @@ def main():
     d_lo = int(torch.searchsorted(torch.from_numpy(plan.table("rel_seg_ptr")).to(torch.int64), seg_b).item())
     m_lo = int(rel_m[d_lo]) if len(rel_m) else 0
     Em = int(m_ptr[m_lo + Sm] - m_ptr[m_lo]) if Sm else 0
-    n_rows = plan.num_nodes if world == 1 else (shard[1] - shard[0])
+    n_rows = plan.num_nodes if not sharded else (shard[1] - shard[0])
     E_layer = (edges_per_step // layers) if not single else int(rel_counts[metapath[0]])
     model_costs = {
         "seg_fwd": ("mfma", 2.0 * (S + n_rows) * F * F, "2·(S + N)·F_in·F_out: segment rows (mean @ W_r) + node rows "
@@ -649,7 +653,7 @@ def main():
     }
     # the transform on the bf16-split matrix cores: rel_gemm_bf3_kernel (mode ALL), mode SINGLE
     # unsharded: single_bf3_kernel (split-K: x @ root and mean @ W halves, one launch per layer)
-    bf3 = args.gemm == "bf3" and F in (64, 128) and (not single or world == 1)
+    bf3 = args.gemm == "bf3" and F in (64, 128) and (not single or not sharded)
     rooflines = []
     for kind, (bound, work, model_txt) in model_costs.items():
         if kind not in per_layer:
@@ -688,7 +692,7 @@ def main():
     roofline = None
     if dom is not None:
         mode_tag = "single" if single else "all"
-        traffic = pmc_traffic(args.workload, mode_tag, F, "mpgnn::" + dom["kernel"]) if world == 1 else None
+        traffic = pmc_traffic(args.workload, mode_tag, F, "mpgnn::" + dom["kernel"]) if not sharded else None
         roofline = {"bound": dom["bound"], "achieved": dom["achieved"], "peak": dom["peak"], "unit": dom["unit"],
                     "frac": dom["frac"], "traffic": traffic, "kernel": dom["kernel"], "kind": dom["kind"],
                     **{k: dom[k] for k in ("fp32_equivalent_TFLOPs", "frac_of_fp32_mfma_peak", "path") if k in dom},
@@ -708,7 +712,7 @@ def main():
 
     # ---- the same step replayed as one HIP graph (launch overhead removed) ---------------
     graph = None
-    if world == 1:
+    if not sharded:
         try:
             s_cap = torch.cuda.Stream()
             s_cap.wait_stream(torch.cuda.current_stream())
@@ -778,7 +782,7 @@ def main():
 
     # ---- the same epoch captured once as a HIP graph (host issue removed) -------------------
     epoch_graph = None
-    if args.epoch_steps > 0 and world == 1:
+    if args.epoch_steps > 0 and not sharded:
         try:
             if single:
                 netg = mpgnn_amd.MPNetm(F, F, g.num_relations, F, 2, 1, [metapath]).to(dev)
@@ -830,14 +834,14 @@ def main():
     # ---- the reference's whole epoch, through the drop-in loops ------------------------------
     loop = None
     if args.loop_epochs > 0:
-        shard_kw = dict(shard=shard, group=group, shard_side=side) if world > 1 else None
+        shard_kw = dict(shard=shard, group=group, shard_side=side) if sharded else None
         loop = time_drop_in_loop(single, g, x, ei, et, F, args.layers, metapath if single else None,
                                  args.loop_epochs, shard_kw, dev, group)
 
     result = None
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if not sharded and not args.no_cpu_baseline:
             with _cpu_threads():
                 if single:
                     convs_cpu = list(model_cpu.layers_list[0])
@@ -853,7 +857,7 @@ def main():
                     f"F_in=F_hidden={F}")
         else:
             what = f"RGCN Net stack forward (mode B), L={layers}, F_in=F_hidden=F_out={F}"
-        if world == 1:
+        if not sharded:
             par = "single GPU"
         elif side == "gathered":
             par = (f"node_2-range shards x{world} (gathered node, edge-balanced; SURVEY 8e): partial sums per rank, "
@@ -871,7 +875,7 @@ def main():
                        "graph": {"nodes": g.num_nodes, "relations": g.num_relations, "edges": g.num_edges,
                                  "edges_per_step": edges_per_step, "segments_layer1": S,
                                  "multi_edge_segments_layer1": Sm},
-                       "parallelism": par, "shard_side": side if world > 1 else None},
+                       "parallelism": par, "shard_side": side if sharded else None},
             "graph_replay": graph,
             "epoch_ms": round(epoch_ms, 3) if epoch_ms is not None else None,
             "epoch_graph": epoch_graph,

@@ -294,6 +294,36 @@ int32_t mpgnn_score_argmax_bwd(const float* grad_max, int64_t num_nodes, const i
                                const int32_t* in_ptr, const int32_t* in_pos, const int32_t* in_key,
                                float* grad_weights, void* stream);
 
+/* Bag branch of the score (OutputLayer.forward with BAGS=True, model.py:45-72; trained by
+ * train(BAGS=True) / score_relation_bags_parallel, main.py:641-673, 853-917; replaces the
+ * per-bag, per-source Python loop). Bags are a CSR over their member source nodes: bag i holds
+ * mem_node[bag_ptr[i] .. bag_ptr[i+1]) in bag order, mem_key[m] = the dictionary key index of
+ * member m (-1 if it is no key: skipped, model.py:59). feat is fp32 [num_nodes, feat_dim]
+ * (data.x), lin_weight fp32 [feat_dim] (LinearLayerAttri.weight[0]).
+ * mpgnn_score_bag_argmax, per bag in member order: s_m = Σ_j feat[node][j]·lin[j] (feature
+ * order, no FMA contraction), mem_pos[m] = the position p of the FIRST maximum of
+ * weights[dst[p]]·s_m (torch.argmax), mem_max[m] = dst[p], mem_v[m] = weights[mem_max[m]]·s_m;
+ * the bag's pick is the first member whose v is strictly larger than the running maximum
+ * (starting at -10): bag_mem[i] = that member (-1: none), max_weights[i] = its v (0: none),
+ * bag_w[i] = weights[its max node]. Members that are no key leave their mem_* entries unwritten. */
+int32_t mpgnn_score_bag_argmax(const float* weights, const float* feat, int32_t feat_dim, const float* lin_weight,
+                               const int32_t* bag_ptr, const int32_t* mem_node, const int32_t* mem_key,
+                               int64_t num_bags, const int32_t* key_ptr, const int32_t* dst, float* max_weights,
+                               int32_t* bag_mem, float* bag_w, float* mem_s, float* mem_v, int32_t* mem_pos,
+                               int32_t* mem_max, void* stream);
+/* Backward of mpgnn_score_bag_argmax (autograd of model.py:64,70): grad_weights[n] = Σ
+ * grad_max[i]·s_{pick(i)} over the bags whose pick points at n, added in DESCENDING bag order
+ * (0 where none); grad_lin[j] = Σ_{bags i with a pick, descending} feat[node_i][j]·(grad_max[i]·
+ * bag_w[i]). (in_ptr [num_nodes+1], in_bag, in_mem, in_pos): per destination node n, every (bag,
+ * member, edge position) candidate with dst[position] == n, bags descending — built once per
+ * (bags, dictionary). grad_lin may be NULL (not wanted). */
+int32_t mpgnn_score_bag_argmax_bwd(const float* grad_max, int64_t num_bags, const int32_t* bag_mem,
+                                   const float* bag_w, const int32_t* mem_node, const float* mem_s,
+                                   const int32_t* mem_pos, const float* feat, int32_t feat_dim,
+                                   int64_t num_nodes, const int32_t* in_ptr, const int32_t* in_bag,
+                                   const int32_t* in_mem, const int32_t* in_pos, float* grad_weights,
+                                   float* grad_lin, void* stream);
+
 /* --- options ----------------------------------------------------------------------------
  * MPGNN_OPT_EXACT_ORDER = 1: every gather-sum adds its entries strictly in the reference's
  * sequential order (no ordered-piece split of long runs). Default 0: runs longer than 32

@@ -125,6 +125,157 @@ __global__ __launch_bounds__(kScoreThreads) void score_scatter_kernel(
     if (lane == 0) grad_w[n] = acc;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Bag branch (model.py:45-72), trained by train(BAGS=True) inside score_relation_bags_parallel
+// (main.py:641-673, 853-917). Bags are lists of source nodes; per bag, per member source in the
+// dictionary (in bag order): s = LinearLayerAttri(feat[source]) (a dot over the F features),
+// the FIRST argmax of weights[dst] * s over the source's destinations, v = weights[max] * s; the
+// bag keeps the first member whose v is STRICTLY larger than the running maximum (-10 at the
+// start), max_weights[bag] = v. One wave per bag walks its members in order; each member's
+// argmax is the wave-parallel first-argmax of score_argmax_kernel over the products.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float dot_seq(const float* __restrict__ f, const float* __restrict__ wl, int F) {
+    // F.linear of one feature row: products added in feature order, no contraction into FMAs
+    // (exact for the one-hot colour features of the reference's datasets)
+    float acc = 0.0f;
+    for (int j = 0; j < F; ++j) acc = __fadd_rn(acc, __fmul_rn(f[j], wl[j]));
+    return acc;
+}
+
+__global__ __launch_bounds__(kScoreThreads) void score_bag_argmax_kernel(
+        const float* __restrict__ w, const float* __restrict__ feat, int32_t F, const float* __restrict__ wlin,
+        const int32_t* __restrict__ bag_ptr, const int32_t* __restrict__ mem_node, const int32_t* __restrict__ mem_key,
+        const int32_t* __restrict__ key_ptr, const int32_t* __restrict__ dst, int32_t B, float* __restrict__ max_w,
+        int32_t* __restrict__ bag_mem, float* __restrict__ bag_w, float* __restrict__ mem_s, float* __restrict__ mem_v,
+        int32_t* __restrict__ mem_pos, int32_t* __restrict__ mem_max) {
+    const int lane = threadIdx.x & 63;
+    const int32_t i = (int32_t)(blockIdx.x * kScoreWaves + (threadIdx.x >> 6));
+    if (i >= B) return;
+    const int32_t mb = bag_ptr[i], me = bag_ptr[i + 1];
+    float cur = -10.0f;   // max_weight_for_current_bag (model.py:57)
+    float out_v = 0.0f, out_w = 0.0f;
+    int32_t out_m = -1;
+    for (int32_t m = mb; m < me; ++m) {
+        const int32_t k = mem_key[m];
+        if (k < 0) continue;  // `if source_node in node_dict` (model.py:59)
+        const float s = dot_seq(feat + (size_t)mem_node[m] * F, wlin, F);
+        const int32_t b = key_ptr[k], e = key_ptr[k + 1];
+        float bv = 0.0f;
+        int32_t bp = INT32_MAX, bn = 0;
+        for (int32_t p = b + lane; p < e; p += 64) {
+            const int32_t n = dst[p];
+            const float v = __fmul_rn(w[n], s);  // weights_of_source *= lin(feat) (model.py:60-61)
+            if (bp == INT32_MAX || takes_over(bv, v)) {
+                bv = v;
+                bp = p;
+                bn = n;
+            }
+        }
+#pragma unroll
+        for (int sh = 32; sh >= 1; sh >>= 1) {
+            const float ov = __shfl_xor(bv, sh);
+            const int32_t op = __shfl_xor(bp, sh), on = __shfl_xor(bn, sh);
+            bool take;
+            if (op == INT32_MAX) take = false;
+            else if (bp == INT32_MAX) take = true;
+            else if (takes_over(bv, ov)) take = true;
+            else if (takes_over(ov, bv)) take = false;
+            else take = op < bp;
+            if (take) {
+                bv = ov;
+                bp = op;
+                bn = on;
+            }
+        }
+        // bv == weights[max_node] * lin(feat[source]) (model.py:64): the same product, the same bits
+        if (lane == 0) {
+            mem_s[m] = s;
+            mem_v[m] = bv;
+            mem_pos[m] = bp;
+            mem_max[m] = bn;
+        }
+        if (bv > cur) {  // strict: the first member with the largest v keeps the bag (model.py:67-70)
+            cur = bv;
+            out_v = bv;
+            out_m = m;
+            out_w = w[bn];
+        }
+    }
+    if (lane == 0) {
+        max_w[i] = out_v;   // 0 when no member is in the dictionary (torch.zeros, model.py:48)
+        bag_mem[i] = out_m;
+        bag_w[i] = out_w;
+    }
+}
+
+// d weights: one wave per destination node n walks its static candidate list — every (bag i,
+// member m, edge position p) with dst[p] == n, bags DESCENDING — and adds g_i · s_m for the
+// entries that are their bag's final pick (member m and m's argmax position p): autograd
+// unwinds the reference's max_weights[i] = v CopySlices chain last bag first (overwritten picks
+// of a bag contribute exact zeros).
+__global__ __launch_bounds__(kScoreThreads) void score_bag_scatter_kernel(
+        const float* __restrict__ g, const int32_t* __restrict__ bag_mem, const int32_t* __restrict__ mem_pos,
+        const float* __restrict__ mem_s, const int32_t* __restrict__ in_ptr, const int32_t* __restrict__ in_bag,
+        const int32_t* __restrict__ in_mem, const int32_t* __restrict__ in_pos, int64_t N, float* __restrict__ grad_w) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n = (int64_t)blockIdx.x * kScoreWaves + (threadIdx.x >> 6);
+    if (n >= N) return;
+    const int32_t b = in_ptr[n], e = in_ptr[n + 1];
+    float acc = 0.0f;
+    bool any = false;
+    for (int32_t j0 = b; j0 < e; j0 += 64) {
+        const int32_t j = j0 + lane;
+        bool match = false;
+        float c = 0.0f;
+        if (j < e) {
+            const int32_t i = in_bag[j], m = in_mem[j];
+            match = bag_mem[i] == m && mem_pos[m] == in_pos[j];
+            if (match) c = __fmul_rn(g[i], mem_s[m]);
+        }
+        unsigned long long mask = __ballot(match);
+        while (mask) {
+            const int l = __builtin_ctzll(mask);
+            const float cv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, c), l));
+            acc = any ? __fadd_rn(acc, cv) : cv;
+            any = true;
+            mask &= mask - 1;
+        }
+    }
+    if (lane == 0) grad_w[n] = acc;
+}
+
+// d LinearLayerAttri.weight[j] = Σ_{bags i descending} feat[source_i][j] · (g_i · weights[max_i]):
+// one wave per feature column; lanes form 64 bags' terms at once, lane order is then folded
+// serially (the reference's accumulation order).
+__global__ __launch_bounds__(64) void score_bag_lin_kernel(
+        const float* __restrict__ g, const int32_t* __restrict__ bag_mem, const float* __restrict__ bag_w,
+        const int32_t* __restrict__ mem_node, const float* __restrict__ feat, int32_t F, int32_t B,
+        float* __restrict__ grad_lin) {
+    const int lane = threadIdx.x;
+    const int32_t j = blockIdx.x;
+    float acc = 0.0f;
+    bool any = false;
+    for (int32_t i0 = B - 1; i0 >= 0; i0 -= 64) {
+        const int32_t i = i0 - lane;  // lane 0 holds the highest bag of the chunk
+        bool has = false;
+        float c = 0.0f;
+        if (i >= 0) {
+            const int32_t m = bag_mem[i];
+            has = m >= 0;
+            if (has) c = __fmul_rn(feat[(size_t)mem_node[m] * F + j], __fmul_rn(g[i], bag_w[i]));
+        }
+        unsigned long long mask = __ballot(has);
+        while (mask) {
+            const int l = __builtin_ctzll(mask);
+            const float cv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, c), l));
+            acc = any ? __fadd_rn(acc, cv) : cv;
+            any = true;
+            mask &= mask - 1;
+        }
+    }
+    if (lane == 0) grad_lin[j] = acc;
+}
+
 }  // namespace
 }  // namespace mpgnn
 
@@ -159,4 +310,49 @@ extern "C" int32_t mpgnn_score_argmax_bwd(const float* grad_max, int64_t num_nod
     hipLaunchKernelGGL(score_scatter_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, grad_max, keys, arg_pos,
                        in_ptr, in_pos, in_key, num_nodes, grad_weights);
     return hip_status(hipGetLastError(), "score_scatter_kernel launch");
+}
+
+extern "C" int32_t mpgnn_score_bag_argmax(const float* weights, const float* feat, int32_t feat_dim, const float* lin_weight,
+                                          const int32_t* bag_ptr, const int32_t* mem_node, const int32_t* mem_key,
+                                          int64_t num_bags, const int32_t* key_ptr, const int32_t* dst, float* max_weights,
+                                          int32_t* bag_mem, float* bag_w, float* mem_s, float* mem_v, int32_t* mem_pos,
+                                          int32_t* mem_max, void* stream) {
+    if (num_bags < 0 || num_bags >= (int64_t)INT32_MAX || feat_dim < 0) return arg_fail("mpgnn_score_bag_argmax: bad sizes");
+    if (num_bags == 0) return MPGNN_OK;
+    if (!weights || !bag_ptr || !mem_node || !mem_key || !max_weights || !bag_mem || !bag_w || !mem_s || !mem_v ||
+        !mem_pos || !mem_max || (feat_dim > 0 && (!feat || !lin_weight)))
+        return arg_fail("mpgnn_score_bag_argmax: NULL argument");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    const unsigned grid = (unsigned)((num_bags + kScoreWaves - 1) / kScoreWaves);
+    hipLaunchKernelGGL(score_bag_argmax_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, weights, feat, feat_dim,
+                       lin_weight, bag_ptr, mem_node, mem_key, key_ptr, dst, (int32_t)num_bags, max_weights, bag_mem,
+                       bag_w, mem_s, mem_v, mem_pos, mem_max);
+    return hip_status(hipGetLastError(), "score_bag_argmax_kernel launch");
+}
+
+extern "C" int32_t mpgnn_score_bag_argmax_bwd(const float* grad_max, int64_t num_bags, const int32_t* bag_mem,
+                                              const float* bag_w, const int32_t* mem_node, const float* mem_s,
+                                              const int32_t* mem_pos, const float* feat, int32_t feat_dim,
+                                              int64_t num_nodes, const int32_t* in_ptr, const int32_t* in_bag,
+                                              const int32_t* in_mem, const int32_t* in_pos, float* grad_weights,
+                                              float* grad_lin, void* stream) {
+    if (num_bags < 0 || num_bags >= (int64_t)INT32_MAX || num_nodes < 0 || feat_dim < 0)
+        return arg_fail("mpgnn_score_bag_argmax_bwd: bad sizes");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    if (num_nodes > 0) {
+        if (!in_ptr || !grad_weights) return arg_fail("mpgnn_score_bag_argmax_bwd: NULL candidate list / output");
+        const unsigned grid = (unsigned)((num_nodes + kScoreWaves - 1) / kScoreWaves);
+        hipLaunchKernelGGL(score_bag_scatter_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, grad_max, bag_mem,
+                           mem_pos, mem_s, in_ptr, in_bag, in_mem, in_pos, num_nodes, grad_weights);
+        int32_t st = hip_status(hipGetLastError(), "score_bag_scatter_kernel launch");
+        if (st != MPGNN_OK) return st;
+    }
+    if (feat_dim > 0 && grad_lin) {
+        if (num_bags == 0) return hip_status(hipMemsetAsync(grad_lin, 0, (size_t)feat_dim * sizeof(float), strm),
+                                             "memset grad_lin");
+        hipLaunchKernelGGL(score_bag_lin_kernel, dim3((unsigned)feat_dim), dim3(64), 0, strm, grad_max, bag_mem, bag_w,
+                           mem_node, feat, feat_dim, (int32_t)num_bags, grad_lin);
+        return hip_status(hipGetLastError(), "score_bag_lin_kernel launch");
+    }
+    return MPGNN_OK;
 }

@@ -7,8 +7,9 @@ ranges are balanced by edge count. Every rank produces a partial output for ALL 
 bias only for rows in its own range, and one all-reduce (RCCL over xGMI with the "nccl"
 backend) per layer sums the partials. Backward: grad_x rows are local to the owner of the
 range — one all-gather of the owned rows (``gather_owned_rows``); dW / droot / dbias are
-partial sums — one bucketed asynchronous all-reduce per layer once all its uses have been
-accumulated (``ShardGradReducer``), overlapped with the earlier layers' backward.
+partial sums — each use's partials are deposited in one flat bucket per layer and reduced by
+one asynchronous all-reduce once every use of the step has been deposited
+(``ShardGradReducer``), overlapped with the earlier layers' backward.
 
 This replaces the reference's mpi4py object fan-out (main.py:1193-1459), which replicated the
 whole graph on every rank and parallelised only over candidate relations/metapaths.
@@ -152,20 +153,41 @@ def gather_owned_rows(g: torch.Tensor, shard: tuple[int, int], group=None) -> to
     return full.index_select(0, idx)
 
 
+class _GradTap(torch.autograd.Function):
+    """Identity on a sharded layer's parameters whose backward hands the rank-local partial
+    gradients of this use to the layer's ShardGradReducer instead of to autograd's leaf
+    accumulation (it returns no gradient for the parameters themselves)."""
+
+    @staticmethod
+    def forward(ctx, reducer, *params):
+        ctx.reducer = reducer
+        return tuple(p.view_as(p) for p in params)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        ctx.reducer._deposit(grads)
+        return (None,) + (None,) * len(grads)
+
+
 class ShardGradReducer:
     """Bucketed, overlapped all-reduce of one sharded layer's parameter gradients (SURVEY §8e:
     "partial dW_r, droot and dbias go through an all-reduce once per step, bucketed").
 
-    The layer's ``weight`` / ``root`` / ``bias`` gradients live as views of ONE flat buffer
-    (installed as ``param.grad`` before the backward; autograd accumulates into them in place).
-    A layer applied several times per forward (``Net.conv2``, model.py:146, shared by layers
-    1..L-1) accumulates all its uses locally first: once every use has been accumulated (a
-    post-accumulate-grad hook counts them against the uses counted in the forward), ONE
-    asynchronous all-reduce of the flat buffer is issued, so it runs behind the backward of the
-    earlier layers; the end-of-backward callback makes the stream wait for it before the
-    optimizer reads the gradients. Summing the partial sums of all uses before the reduction is
-    the same linear combination as reducing each use (the reference reduces nothing: it runs on
-    one process)."""
+    Every grad-enabled forward of the layer passes its parameters through ``tap`` (an identity
+    autograd node). The tap's backward receives this use's RANK-LOCAL partial dW / droot / dbias
+    and adds them into ONE flat buffer owned by the reducer (the first use of a backward
+    overwrites it) — autograd never accumulates partials into ``param.grad``. A layer applied
+    several times per forward (``Net.conv2``, model.py:146, shared by layers 1..L-1) has one tap
+    per use: once every tap of the step has deposited, ONE asynchronous all-reduce of the flat
+    buffer is issued, so it runs behind the backward of the earlier layers. The end-of-backward
+    callback launches what is still pending (a tap whose forward was never backpropagated),
+    makes the stream wait for the reductions (NCCL: no host block) and ADDS the reduced sums to
+    ``param.grad`` (or sets it when None): with no ``zero_grad`` between two backward passes the
+    gradients accumulate as G1 + G2, as autograd's own accumulation does.
+
+    Not supported (raises rather than returning partial sums): ``torch.autograd.grad`` with the
+    sharded layer's parameters as inputs — the tap hands autograd no parameter gradient, so
+    autograd reports them unused."""
 
     _pending: list = []  # reducers touched by the running backward (one end-of-backward callback)
 
@@ -173,61 +195,57 @@ class ShardGradReducer:
         self.params = [p for p in params if p is not None]
         self.group = group
         self.flat = None
-        self.uses = 0
-        self.hits = {}
+        self.taps = 0       # grad-enabled forwards since the last reduction
+        self.deposits = 0   # tap backwards since the last reduction
         self.work = None
-        self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
 
-    def _install(self):
-        """Make every param.grad a view of the flat buffer (zeroed where it had no gradient)."""
+    def tap(self, *params):
+        """The layer's parameters for one grad-enabled forward (None entries pass through)."""
+        live = [p for p in params if p is not None and p.requires_grad]
+        if not live:
+            return params
+        self.taps += 1
+        out = iter(_GradTap.apply(self, *live))
+        return tuple(next(out) if (p is not None and p.requires_grad) else p for p in params)
+
+    def _layout(self):
         ps = [p for p in self.params if p.requires_grad]
         total = sum(p.numel() for p in ps)
-        dev = ps[0].device
-        if self.flat is None or self.flat.numel() != total or self.flat.device != dev:
-            self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
-            views_ok = False
-        else:
-            views_ok = True
-        off = 0
+        if self.flat is None or self.flat.numel() != total or self.flat.device != ps[0].device:
+            self.flat = torch.zeros(total, dtype=torch.float32, device=ps[0].device)
+        views, off = [], 0
         for p in ps:
-            v = self.flat[off:off + p.numel()].view_as(p)
+            views.append((p, self.flat[off:off + p.numel()].view_as(p)))
             off += p.numel()
-            g = p.grad
-            if g is not None and views_ok and g.data_ptr() == v.data_ptr():
-                continue  # already our view (zero_grad(set_to_none=False) zeroed it in place)
-            if g is None:
-                v.zero_()
-            else:
-                v.copy_(g)
-            p.grad = v
+        return views
 
-    def note_use(self):
-        """Called by the layer's forward when autograd will run through it."""
-        self._install()  # no-op while param.grad is still our view
-        if self.uses == 0:
-            self.hits = {id(p): 0 for p in self.params if p.requires_grad}
-        self.uses += 1
+    def _deposit(self, grads):
+        if not ShardGradReducer._pending:
+            torch.autograd.Variable._execution_engine.queue_callback(ShardGradReducer._finish_all)
+        if self not in ShardGradReducer._pending:
+            ShardGradReducer._pending.append(self)
+        views = self._layout()
+        first = self.deposits == 0
+        for (p, v), g in zip(views, grads):
+            if g is None:
+                if first:
+                    v.zero_()
+            elif first:
+                v.copy_(g)
+            else:
+                v.add_(g)
+        self.deposits += 1
+        if self.work is None and self.deposits >= self.taps:
+            self._launch()  # every use deposited: reduce now, behind the earlier layers' backward
 
     def _launch(self):
         import torch.distributed as dist
         self.work = dist.all_reduce(self.flat, group=self.group, async_op=True)
 
-    def _hook(self, p):
-        if id(p) not in self.hits:
-            return
-        if not ShardGradReducer._pending:
-            torch.autograd.Variable._execution_engine.queue_callback(ShardGradReducer._finish_all)
-        if self not in ShardGradReducer._pending:
-            ShardGradReducer._pending.append(self)
-        self.hits[id(p)] += 1
-        if self.work is None and self.uses and all(h >= self.uses for h in self.hits.values()):
-            self._launch()  # every use accumulated: reduce now, behind the earlier layers' backward
-
     @staticmethod
     def _finish_all():
-        """End of the backward: reduce what has not been (a use count left stale by a forward
-        that was never backpropagated), then make the stream wait for every reduction (NCCL:
-        no host block) before the optimizer reads the gradients. Same order on every rank."""
+        """End of the backward: reduce what has not been, make the stream wait for every
+        reduction, then add the sums into param.grad. Same order on every rank."""
         pending, ShardGradReducer._pending = ShardGradReducer._pending, []
         for r in pending:
             if r.work is None:
@@ -235,13 +253,16 @@ class ShardGradReducer:
         for r in pending:
             r.work.wait()
             r.work = None
-            r.uses = 0
-            r.hits = {k: 0 for k in r.hits}
+            for p, v in r._layout():
+                if p.grad is None:
+                    p.grad = v.clone()
+                else:
+                    p.grad.add_(v)
+            r.taps = 0
+            r.deposits = 0
 
     def remove(self):
-        for h in self._handles:
-            h.remove()
-        self._handles = []
+        """Kept for callers of the hook-based reducer: nothing is registered on the params."""
 
 
 def sharded_stack_forward(convs, x: torch.Tensor, edge_index: torch.Tensor, edge_type: torch.Tensor,

@@ -62,34 +62,52 @@ def _ptr(t):
 
 
 # Workspace per (device, stream): calls on one stream run in stream order, so one growing
-# buffer serves them all (and keeps a fixed address for HIP-graph capture).
+# buffer serves them all (and keeps a fixed address for HIP-graph capture). Entry: [buffer,
+# captured] — ``captured`` once a kernel using the buffer was recorded into a HIP graph.
 _WS: dict = {}
-# Buffers outgrown while a HIP graph was being captured: kernels captured earlier in that graph
-# still read and write them at every replay, so they must outlive the graph (freed by
-# release_workspaces). Outside a capture the smaller buffer is dropped at once.
-_RETIRED: list = []
+# Buffers outgrown after (or while) a HIP graph captured them: the graph's kernels read and
+# write them at every replay, so they must outlive the graph — they are kept per stream key
+# until ``release_workspaces`` drops that key (the loops do when their graph is gone).
+# A buffer no graph ever captured is dropped at once when outgrown.
+_RETIRED: dict = {}
 
 
 def _workspace(nbytes: int, device: torch.device) -> torch.Tensor:
     key = (device.index, _stream_of(device))
-    ws = _WS.get(key)
-    if ws is None or ws.numel() < nbytes:
-        # drop the smaller buffer first: the caching allocator hands its block back in stream
-        # order, so the peak is the new size, not old + new (matters at C5: ~58 GB each)
+    ent = _WS.get(key)
+    capturing = torch.cuda.is_current_stream_capturing()
+    if ent is None or ent[0].numel() < nbytes:
+        # drop the smaller buffer first when no graph holds it: the caching allocator hands its
+        # block back in stream order, so the peak is the new size, not old + new
         old = _WS.pop(key, None)
-        if old is not None and torch.cuda.is_current_stream_capturing():
-            _RETIRED.append(old)
-        del ws, old
-        ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
-        _WS[key] = ws
-    return ws
+        if old is not None and (old[1] or capturing):
+            _RETIRED.setdefault(key, []).append(old[0])
+        del ent, old
+        ent = [torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device), False]
+        _WS[key] = ent
+    if capturing:
+        ent[1] = True
+    return ent[0]
 
 
-def release_workspaces() -> None:
-    """Drop the cached per-(device, stream) scratch buffers (e.g. after a HIP-graph capture on
-    a side stream, once the graph is gone); the next call allocates again."""
-    _WS.clear()
-    _RETIRED.clear()
+def release_workspaces(stream=None) -> None:
+    """Drop the cached scratch buffers — every one, or those of one ``torch.cuda.Stream`` —
+    once no HIP graph that captured them will be replayed again; the next call allocates anew.
+    The caller orders later work after the graph's last replay (the loops make the released
+    stream wait for the current one)."""
+    if stream is None:
+        _WS.clear()
+        _RETIRED.clear()
+        return
+    for key in [k for k in _WS if k[1] == stream.cuda_stream]:
+        del _WS[key]
+    for key in [k for k in _RETIRED if k[1] == stream.cuda_stream]:
+        del _RETIRED[key]
+
+
+def workspace_bytes_cached() -> int:
+    """Bytes held by the scratch-buffer cache (live and retired), for leak checks."""
+    return sum(e[0].numel() for e in _WS.values()) + sum(t.numel() for ts in _RETIRED.values() for t in ts)
 
 
 def _forward(x, weight, root, bias, plan: GraphPlan, mode: int, relation: int, num_relations: int,

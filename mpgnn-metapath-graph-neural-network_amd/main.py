@@ -124,6 +124,21 @@ def _graphs_enabled(data) -> bool:
             and not getattr(data, "shard_kw", None))
 
 
+_LOOP_STREAMS: dict = {}
+
+
+def _loop_stream() -> torch.cuda.Stream:
+    """The side stream the loops warm up and capture on: ONE per device for the process. torch
+    keeps a BLAS workspace per (handle, stream) for the process lifetime (~76 MiB each for the
+    Linear heads' GEMMs on this image), so a fresh stream per loop call would leave one behind
+    per call."""
+    dev = torch.cuda.current_device()
+    st = _LOOP_STREAMS.get(dev)
+    if st is None:
+        st = _LOOP_STREAMS[dev] = torch.cuda.Stream()
+    return st
+
+
 def _epochs(epoch_fn, epochs: int, use_graph: bool, warmup: int = 3):
     """Run ``epoch_fn`` ``epochs`` times, yielding (epoch, outputs). With ``use_graph`` the first
     ``warmup`` epochs run eagerly on a side stream, then ONE epoch is captured as a HIP graph
@@ -134,26 +149,35 @@ def _epochs(epoch_fn, epochs: int, use_graph: bool, warmup: int = 3):
         for e in range(1, epochs + 1):
             yield e, epoch_fn()
         return
-    side = torch.cuda.Stream()
+    from .functional import release_workspaces
+    side = _loop_stream()
     side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
-        for e in range(1, warmup + 1):
-            out = epoch_fn()
-            yield e, out
-    torch.cuda.current_stream().wait_stream(side)
-    graph = torch.cuda.CUDAGraph()
+    graph = None
     try:
-        with torch.cuda.graph(graph, stream=side):
-            static = epoch_fn()
-    except Exception:  # capture unsupported here: the remaining epochs run eagerly
+        with torch.cuda.stream(side):
+            for e in range(1, warmup + 1):
+                out = epoch_fn()
+                yield e, out
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(graph, stream=side):
+                static = epoch_fn()
+        except Exception:  # capture unsupported here: the remaining epochs run eagerly
+            graph = None
+            torch.cuda.synchronize()
+        for e in range(warmup + 1, epochs + 1):
+            if graph is None:
+                yield e, epoch_fn()
+            else:
+                graph.replay()
+                yield e, static
+    finally:
+        # the loop owns its side stream's scratch buffers: once its graph is gone they are
+        # released (the next loop's work on the stream is ordered after the last replay)
         graph = None
-        torch.cuda.synchronize()
-    for e in range(warmup + 1, epochs + 1):
-        if graph is None:
-            yield e, epoch_fn()
-        else:
-            graph.replay()
-            yield e, static
+        side.wait_stream(torch.cuda.current_stream())
+        release_workspaces(side)
 
 
 def _num_classes(out: torch.Tensor) -> int:

@@ -93,20 +93,20 @@ class RGCNConv(torch.nn.Module):
                         shard_side=shard_side)
         row_range = shard if shard is not None else None
         reduced = False
+        weight, root, bias = self.weight, self.root, self.bias
         if group is not None and torch.is_grad_enabled() and \
-                any(p is not None and p.requires_grad for p in (self.weight, self.root, self.bias)):
-            # partial dW / droot / dbias: one bucketed async all-reduce once every use of this
-            # layer in the step has been accumulated (Net shares conv2 across layers 1..L-1)
+                any(p is not None and p.requires_grad for p in (weight, root, bias)):
+            # partial dW / droot / dbias of this use go to the layer's reducer (not to .grad):
+            # one bucketed async all-reduce once every use of the step has been deposited
+            # (Net shares conv2 across layers 1..L-1), then added to .grad
             red = self.__dict__.get("_grad_reducer")
             if red is None or red.group is not group:
-                if red is not None:
-                    red.remove()
                 from .distributed import ShardGradReducer
-                red = ShardGradReducer((self.weight, self.root, self.bias), group)
+                red = ShardGradReducer((weight, root, bias), group)
                 self.__dict__["_grad_reducer"] = red
-            red.note_use()
+            weight, root, bias = red.tap(weight, root, bias)
             reduced = True
-        return rgcn_conv(x, self.weight, self.root, self.bias, plan, MODE_ALL,
+        return rgcn_conv(x, weight, root, bias, plan, MODE_ALL,
                          num_relations=self.num_relations, row_range=row_range, group=group,
                          activation=activation, params_reduced=reduced,
                          grad_stash=_grad_stash if shard is None else None)

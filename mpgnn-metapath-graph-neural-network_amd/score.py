@@ -14,8 +14,13 @@ per destination, the gradients of the sources that picked it, added in the order
 unwinds the reference's ``max_weights[source] = weights[max_node]`` chain). The per-epoch
 ``{source: max_node}`` results are returned as lazy Mappings (no host sync until read).
 
-Scope: the non-bag branch (model.py:74-89) that ``score_relation_parallel`` trains. The bag
-branch (model.py:45-72, score_relation_bags_*) is not on this path and raises.
+The bag branch (model.py:45-72) that ``score_relation_bags_parallel`` (main.py:853-917) trains
+in the metapath-extension rounds is the same on the GPU: the bags (lists of source nodes) are a
+device CSR (``BagSet``), the forward ONE kernel (``mpgnn_score_bag_argmax``: one wave per bag
+walks its members in bag order, each member's first argmax of ``weights[dst] · lin(feat[src])``
+wave-parallel, the strict ``>`` pick of the reference), the backward ONE pair of kernels
+(``mpgnn_score_bag_argmax_bwd``: d weights per destination and d LinearLayerAttri per feature,
+added in the order autograd unwinds the reference's chain — bags descending).
 """
 from __future__ import annotations
 
@@ -32,9 +37,12 @@ from ._lib import check, lib
 __all__ = ["EdgeDictionary", "DestinationDictionary", "ArgmaxDict", "build_edge_dictionary", "score_argmax",
            "InputLayer", "OutputLayer", "Score", "create_edge_dictionary", "initialize_weights", "get_model",
            "get_optimizer", "get_loss", "get_loss_per_node", "train", "score_relation_parallel", "EPOCHS",
-           "FIRST_MASK_DATASETS"]
+           "FIRST_MASK_DATASETS", "BagSet", "BagDestinationDictionary", "score_bag_argmax", "create_bags",
+           "clean_bags_for_relation_type", "reinitialize_weights", "retrieve_destinations_low_loss",
+           "score_relation_bags_parallel", "BAG_EPOCHS"]
 
 EPOCHS = 100  # main.py:755
+BAG_EPOCHS = 50  # main.py:888
 FIRST_MASK_DATASETS = ("IMDB", "ACM", "DBLP", "fb15k-237")  # main.py:653: data.labels is per mask position
 COMPLEX = "fb15k-237"  # main.py:1484 (stored by Score, unused by the non-bag forward)
 
@@ -306,9 +314,14 @@ class OutputLayer(nn.Module):
         self.LinearLayerAttri = nn.Linear(features_dim, 1, bias=False)
 
     def forward(self, weights, data, node_dict, BAGS, COMPLEX, feat):
-        if BAGS:
-            raise NotImplementedError("the bag branch of OutputLayer.forward (model.py:45-72) is not on the "
-                                      "GPU score path; score_relation_parallel uses the non-bag branch")
+        if BAGS:  # model.py:45-72: per bag the best member pick (HIP kernels, see score_bag_argmax)
+            num_nodes = int(data.num_nodes)
+            ed = _edge_dictionary_of(node_dict, num_nodes, weights.device)
+            bs = _bag_set_of(data.bags, ed)
+            if feat is None:
+                feat = _features_of(data, weights.device)
+            max_weights, bag_mem, mem_v, mem_max = score_bag_argmax(weights, self.LinearLayerAttri.weight, feat, bs)
+            return max_weights, BagPickDict(bs, bag_mem, mem_max), SourceValueDict(bs, mem_v)
         num_nodes = int(data.num_nodes)
         ed = _edge_dictionary_of(node_dict, num_nodes, weights.device)
         max_weights, max_node = score_argmax(weights, ed)
@@ -334,17 +347,21 @@ class Score(nn.Module):
 
     def forward(self, data, node_dict, BAGS):
         x = self.input()
-        # the reference converts data.x to a CPU FloatTensor (model.py:116) for the bag branch only
-        return self.output(x, data, node_dict, BAGS, self.COMPLEX, None)
+        # data.x as float32 (model.py:116), read by the bag branch only: kept on the GPU
+        feat = _features_of(data, x.device) if BAGS else None
+        return self.output(x, data, node_dict, BAGS, self.COMPLEX, feat)
 
 
 # ---------------------------------------------------------------------------------------------
 # main.py helpers
 # ---------------------------------------------------------------------------------------------
 def create_edge_dictionary(data, relation, source_nodes_mask, BAGS, dataset="synthetic"):
-    """main.py:387-424 (BAGS=False): (EdgeDictionary, DestinationDictionary) built on the GPU."""
+    """main.py:387-438: (EdgeDictionary, DestinationDictionary) built on the GPU; with BAGS the
+    second dictionary is {destination: [labels of the bags of its sources]} (:426-438)."""
     if BAGS:
-        raise NotImplementedError("create_edge_dictionary(BAGS=True) (main.py:426-438) is not on the GPU score path")
+        ed, _ = build_edge_dictionary(data.edge_index, data.edge_type, relation, source_nodes_mask, None, dataset,
+                                      num_nodes=int(data.num_nodes))
+        return ed, BagDestinationDictionary(data, relation)
     return build_edge_dictionary(data.edge_index, data.edge_type, relation, source_nodes_mask, data.labels, dataset,
                                  num_nodes=int(data.num_nodes))
 
@@ -356,7 +373,7 @@ def initialize_weights(data, destination_dictionary, BAGS, rng=None):
     leaves them uninitialised; the argmax never reads them)."""
     rng = rng or random
     weights = torch.zeros(int(data.num_nodes))
-    if isinstance(destination_dictionary, DestinationDictionary):
+    if isinstance(destination_dictionary, (DestinationDictionary, BagDestinationDictionary)):
         keys, mins = destination_dictionary.keys_arr, destination_dictionary.min_labels()
     else:
         keys = np.array(list(destination_dictionary.keys()), dtype=np.int64)
@@ -400,7 +417,9 @@ def train(data, edge_dictionary, model, optimizer, criterion, source_nodes_mask,
     {source: max_node}, predictions). No host sync (the dicts are lazy, the loss a device
     tensor). ``data.labels`` may live on the CPU: it is moved once and cached on ``data``."""
     if BAGS:
-        raise NotImplementedError("train(BAGS=True) (main.py:644-649) is not on the GPU score path")
+        return _train_bags(data, edge_dictionary, model, optimizer, criterion, criterion_per_node,
+                           destination_nodes_with_freezed_weights, previous_weights, grad_mask, bags_to_predict,
+                           bags_to_predict_labels)
     model.train()
     optimizer.zero_grad()
     predictions, max_destination_node_for_bag, max_destination_node_for_source = model(data, edge_dictionary, BAGS)
@@ -426,13 +445,42 @@ def train(data, edge_dictionary, model, optimizer, criterion, source_nodes_mask,
     if destination_nodes_with_freezed_weights:  # main.py:663-664
         model.input.weights.grad = model.input.weights.grad * grad_mask.to(dev)
     optimizer.step()
-    with torch.no_grad():  # main.py:667-672
+    _clamp_and_restore(model, destination_nodes_with_freezed_weights, previous_weights)
+    return loss, max_destination_node_for_source, loss_per_node, max_destination_node_for_bag, predictions
+
+
+def _clamp_and_restore(model, frozen, previous_weights):
+    """main.py:667-672: both parameters clamped to [0, 1], frozen destinations reset to
+    ``previous_weights`` (a no-op when previous_weights IS the parameter's storage, as in
+    score_relation_bags_parallel: InputLayer wraps the weights tensor it is given)."""
+    with torch.no_grad():
         model.input.weights.clamp_(min=0.0, max=1.0)
         model.output.LinearLayerAttri.weight.clamp_(min=0.0, max=1.0)
-        if destination_nodes_with_freezed_weights:
-            idx = torch.as_tensor(list(destination_nodes_with_freezed_weights), dtype=torch.int64, device=dev)
-            model.input.weights[idx] = previous_weights.reshape(-1, 1).to(dev)[idx].to(torch.float32)
-    return loss, max_destination_node_for_source, loss_per_node, max_destination_node_for_bag, predictions
+        if frozen:
+            dev = model.input.weights.device
+            idx = _device_cached(("frozen_idx", tuple(int(v) for v in frozen)), dev,
+                                 lambda: torch.as_tensor([int(v) for v in frozen], dtype=torch.int64))
+            prev = previous_weights.reshape(-1, 1)
+            if prev.device != dev:
+                prev = _device_cached(("prev", id(previous_weights), previous_weights._version), dev,
+                                      lambda: previous_weights.reshape(-1, 1).to(torch.float32), keep=previous_weights)
+            model.input.weights[idx] = prev[idx].to(torch.float32)
+
+
+_DEV_CACHE: dict = {}
+
+
+def _device_cached(key, dev, make, keep=None):
+    """A host-built tensor copied to ``dev`` once per key (the loops call train() under HIP-graph
+    capture, where a fresh host-to-device copy must not be recorded); ``keep`` pins the object
+    whose id is part of the key."""
+    k = (key, str(dev))
+    hit = _DEV_CACHE.get(k)
+    if hit is None:
+        if len(_DEV_CACHE) > 256:
+            _DEV_CACHE.clear()
+        hit = _DEV_CACHE[k] = (make().to(dev), keep)
+    return hit[0]
 
 
 def score_relation_parallel(data, relation, source_nodes, features_dim, dataset, epochs: int = EPOCHS):
@@ -466,3 +514,443 @@ def score_relation_parallel(data, relation, source_nodes, features_dim, dataset,
     for _, loss in _epochs(epoch, epochs, use_graph):
         pass
     return relation, loss.item(), edge_dictionary, destination_dictionary
+
+
+# ---------------------------------------------------------------------------------------------
+# bag branch: model.py:45-72; main.py:426-438, 498-512, 530-592, 641-673, 853-917
+# ---------------------------------------------------------------------------------------------
+class BagDestinationDictionary(Mapping):
+    """``{destination: [labels of the bags holding one of its sources]}`` (main.py:426-438):
+    over the relation's edges in file order whose source lies in some bag of ``data.bags``, the
+    labels of that source's bags (bag order) are appended to the destination's list; keys in
+    first-appearance order. Built with numpy; ``min_labels()`` feeds initialize_weights."""
+
+    def __init__(self, data, relation):
+        ei = data.edge_index.cpu().numpy() if torch.is_tensor(data.edge_index) else np.asarray(data.edge_index)
+        et = data.edge_type.cpu().numpy() if torch.is_tensor(data.edge_type) else np.asarray(data.edge_type)
+        sel = et == int(relation)
+        src, dst = ei[0][sel].astype(np.int64), ei[1][sel].astype(np.int64)
+        labels = data.bag_labels.reshape(-1).cpu().numpy().astype(np.float64) if len(data.bags) else np.zeros(0)
+        per_node = {}  # node -> labels of its bags, bag order (main.py:428-432)
+        for i, bag in enumerate(data.bags):
+            for node in bag:
+                per_node.setdefault(int(node), []).append(float(labels[i]))
+        keep = np.fromiter((int(v) in per_node for v in src), dtype=bool, count=src.size)
+        self._src, self._dst = src[keep], dst[keep]
+        self._per_node = per_node
+        uniq, first = np.unique(self._dst, return_index=True)
+        order = np.argsort(first, kind="stable")
+        self.keys_arr = uniq[order]
+        node_min = {n: min(v) for n, v in per_node.items()}
+        mins = {}
+        for s_, d_ in zip(self._src.tolist(), self._dst.tolist()):
+            m = node_min[s_]
+            if d_ not in mins or m < mins[d_]:
+                mins[d_] = m
+        self._min = np.array([mins[int(k)] for k in self.keys_arr], dtype=np.float64)
+        self._pos = None
+
+    def min_labels(self) -> np.ndarray:
+        return self._min
+
+    def __getitem__(self, dst):
+        d = int(dst)
+        if d not in self:
+            raise KeyError(dst)
+        out = []
+        for s_ in self._src[self._dst == d].tolist():
+            out.extend(self._per_node[s_])
+        return out
+
+    def __contains__(self, dst):
+        if self._pos is None:
+            self._pos = {int(k): i for i, k in enumerate(self.keys_arr)}
+        try:
+            return int(dst) in self._pos
+        except (TypeError, ValueError):
+            return False
+
+    def __iter__(self):
+        return iter(self.keys_arr.tolist())
+
+    def __len__(self):
+        return int(self.keys_arr.size)
+
+
+class BagSet:
+    """Bags (lists of source nodes, data.bags) against one EdgeDictionary, on the device:
+    ``bag_ptr`` [B+1] / ``mem_node`` [M] the CSR of members in bag order, ``mem_key`` [M] each
+    member's dictionary key index (-1: not a key, skipped as model.py:59 does), and the backward's
+    candidate lists — per destination node n every (bag, member, edge position) that can pick n,
+    bags descending (``in_ptr`` [N+1], ``in_bag``, ``in_mem``, ``in_pos``). Integer work, once per
+    (bags, dictionary)."""
+
+    def __init__(self, bags, ed: EdgeDictionary):
+        self.bags = bags
+        self.ed = ed
+        dev = ed.device
+        N = ed.num_nodes
+        lens = np.fromiter((len(b) for b in bags), dtype=np.int64, count=len(bags))
+        B = int(lens.size)
+        self.num_bags = B
+        nodes = np.fromiter((int(n) for b in bags for n in b), dtype=np.int64, count=int(lens.sum()))
+        ptr = np.zeros(B + 1, dtype=np.int64)
+        np.cumsum(lens, out=ptr[1:])
+        i32 = torch.int32
+        self.bag_ptr = torch.from_numpy(ptr).to(dev, i32)
+        nodes_d = torch.from_numpy(nodes).to(dev)
+        self.mem_node = nodes_d.clamp(0, max(N - 1, 0)).to(i32)
+        K = len(ed)
+        key_of = torch.full((max(N, 1),), -1, dtype=torch.int64, device=dev)
+        if K:
+            key_of[ed.keys_t.long()] = torch.arange(K, device=dev)
+        valid = (nodes_d >= 0) & (nodes_d < N)
+        mk = torch.where(valid, key_of[nodes_d.clamp(0, max(N - 1, 0))], torch.full_like(nodes_d, -1))
+        self.mem_key = mk.to(i32)
+        m_idx = torch.nonzero(mk >= 0).reshape(-1)
+        k = mk[m_idx]
+        kp = ed.key_ptr_t.long()
+        deg = (kp[k + 1] - kp[k]) if k.numel() else k
+        total = int(deg.sum()) if k.numel() else 0
+        if total:
+            m_rep = torch.repeat_interleave(m_idx, deg)
+            starts = torch.repeat_interleave(kp[k], deg)
+            offs = torch.arange(total, device=dev) - torch.repeat_interleave(torch.cumsum(deg, 0) - deg, deg)
+            pos = starts + offs
+            node = ed.dst_t.long()[pos]
+            bag_of_mem = torch.repeat_interleave(torch.arange(B, device=dev), torch.from_numpy(lens).to(dev))
+            bag = bag_of_mem[m_rep]
+            order = torch.argsort(node * max(B, 1) + (B - 1 - bag), stable=True)
+            in_ptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(torch.bincount(node, minlength=N), 0, out=in_ptr[1:])
+            self.in_ptr, self.in_bag = in_ptr.to(i32), bag[order].to(i32)
+            self.in_mem, self.in_pos = m_rep[order].to(i32), pos[order].to(i32)
+        else:
+            self.in_ptr = torch.zeros(N + 1, dtype=i32, device=dev)
+            self.in_bag = self.in_mem = self.in_pos = torch.zeros(0, dtype=i32, device=dev)
+        self._strs = None
+
+    @property
+    def num_members(self) -> int:
+        return int(self.mem_node.numel())
+
+    def bag_strs(self):
+        """str(bag) of every bag, the reference's dictionary keys (model.py:69)."""
+        if self._strs is None:
+            self._strs = [str(b) for b in self.bags]
+        return self._strs
+
+
+def _bag_set_of(bags, ed: EdgeDictionary) -> BagSet:
+    cache = ed.__dict__.setdefault("_bag_sets", {})
+    hit = cache.get(id(bags))
+    if hit is None or hit.bags is not bags or hit.num_bags != len(bags):
+        if len(cache) > 8:
+            cache.clear()
+        hit = cache[id(bags)] = BagSet(bags, ed)
+    return hit
+
+
+def _features_of(data, dev):
+    """data.x as float32 on ``dev`` (model.py:116 ``data.x.type(torch.FloatTensor)``), cached
+    on ``data`` per source tensor."""
+    owner = data.__dict__.get("_data", data)  # a _BagsView caches on the data it wraps
+    x = owner.x
+    hit = getattr(owner, "_x_f32_dev", None)
+    if hit is None or hit[0] is not x or hit[1].device != torch.device(dev):
+        hit = (x, x.to(dev, torch.float32).contiguous())
+        try:
+            owner._x_f32_dev = hit
+        except AttributeError:
+            pass
+    return hit[1]
+
+
+class _ScoreBagArgmaxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, weights, lin_weight, feat, bs: BagSet):
+        dev = weights.device
+        B, M = bs.num_bags, bs.num_members
+        w = weights.contiguous()
+        lw = lin_weight.detach().reshape(-1).contiguous()
+        f = feat.contiguous()
+        F = int(f.shape[1]) if f.dim() == 2 else 0
+        max_w = torch.zeros(B, 1, dtype=torch.float32, device=dev)
+        bag_mem = torch.empty(B, dtype=torch.int32, device=dev)
+        bag_w = torch.empty(B, dtype=torch.float32, device=dev)
+        mem_s = torch.empty(M, dtype=torch.float32, device=dev)
+        mem_v = torch.empty(M, dtype=torch.float32, device=dev)
+        mem_pos = torch.empty(M, dtype=torch.int32, device=dev)
+        mem_max = torch.empty(M, dtype=torch.int32, device=dev)
+        ed = bs.ed
+        check(lib.mpgnn_score_bag_argmax(w.data_ptr(), _ptr(f), F, _ptr(lw), bs.bag_ptr.data_ptr(), _ptr(bs.mem_node),
+                                         _ptr(bs.mem_key), B, _ptr(ed.key_ptr_t), _ptr(ed.dst_t), _ptr(max_w),
+                                         _ptr(bag_mem), _ptr(bag_w), _ptr(mem_s), _ptr(mem_v), _ptr(mem_pos),
+                                         _ptr(mem_max), _stream(dev)), "mpgnn_score_bag_argmax")
+        ctx.bs, ctx.F, ctx.lin_shape = bs, F, lin_weight.shape
+        ctx.save_for_backward(bag_mem, bag_w, mem_s, mem_pos, f)
+        ctx.mark_non_differentiable(bag_mem, mem_v, mem_max)
+        return max_w, bag_mem, mem_v, mem_max
+
+    @staticmethod
+    def backward(ctx, g_max, _g1, _g2, _g3):
+        bag_mem, bag_w, mem_s, mem_pos, f = ctx.saved_tensors
+        bs = ctx.bs
+        g = g_max.contiguous().float().reshape(-1)
+        dev = g.device
+        want_w, want_l = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        gw = torch.empty(bs.ed.num_nodes, 1, dtype=torch.float32, device=dev) if want_w else None
+        gl = torch.empty(ctx.lin_shape, dtype=torch.float32, device=dev) if want_l else None
+        check(lib.mpgnn_score_bag_argmax_bwd(_ptr(g), bs.num_bags, _ptr(bag_mem), _ptr(bag_w), _ptr(bs.mem_node),
+                                             _ptr(mem_s), _ptr(mem_pos), _ptr(f), ctx.F if want_l else 0,
+                                             bs.ed.num_nodes if want_w else 0, _ptr(bs.in_ptr), _ptr(bs.in_bag),
+                                             _ptr(bs.in_mem), _ptr(bs.in_pos), _ptr(gw), _ptr(gl), _stream(dev)),
+              "mpgnn_score_bag_argmax_bwd")
+        return gw, gl, None, None
+
+
+def score_bag_argmax(weights: torch.Tensor, lin_weight: torch.Tensor, feat: torch.Tensor, bs: BagSet):
+    """model.py:45-72 for every bag at once: (max_weights [B, 1], bag_mem [B] (the picked member,
+    -1: none), mem_v [M] (weights[max] · lin(feat[source]) per member), mem_max [M] (its argmax
+    destination)); differentiable w.r.t. ``weights`` [N, 1] and ``lin_weight`` [1, F]."""
+    if not weights.is_cuda:
+        raise RuntimeError("mpgnn_amd: the score function runs only as HIP kernels on a ROCm GPU "
+                           "(there is no CPU fallback); move the weights to 'cuda'")
+    if weights.dtype != torch.float32 or weights.numel() != bs.ed.num_nodes:
+        raise ValueError(f"weights must be float32 with {bs.ed.num_nodes} entries, got {weights.dtype} "
+                         f"{tuple(weights.shape)}")
+    if feat.dim() != 2 or feat.shape[0] != bs.ed.num_nodes or lin_weight.numel() != feat.shape[1]:
+        raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied (features {tuple(feat.shape)}, "
+                           f"LinearLayerAttri {tuple(lin_weight.shape)})")
+    return _ScoreBagArgmaxFn.apply(weights, lin_weight, feat.to(torch.float32), bs)
+
+
+class BagPickDict(Mapping):
+    """``{str(bag): max_node}`` of one forward (model.py:69), read lazily from the device: bags in
+    order, a bag without a pick has no entry, a bag whose string repeats an earlier one
+    overwrites its value in place — the reference dict's contents and order."""
+
+    def __init__(self, bs: BagSet, bag_mem: torch.Tensor, mem_max: torch.Tensor):
+        self._bs, self._bm, self._mm = bs, bag_mem, mem_max
+        self._host = None
+
+    def _load(self):
+        if self._host is None:
+            bm = self._bm.cpu().numpy()
+            mm = self._mm.cpu().numpy()
+            d = {}
+            for s_, m in zip(self._bs.bag_strs(), bm.tolist()):
+                if m >= 0:
+                    d[s_] = int(mm[m])
+            self._host = d
+        return self._host
+
+    def __getitem__(self, k):
+        return self._load()[k]
+
+    def __iter__(self):
+        return iter(self._load())
+
+    def __len__(self):
+        return len(self._load())
+
+
+class SourceValueDict(Mapping):
+    """``{source: weights[max_node] · lin(feat[source])}`` (model.py:64) of one forward: keys in
+    first-visit order over the bags' members that are dictionary keys, values 1-element tensors
+    like the reference's (``.item()`` reads them)."""
+
+    def __init__(self, bs: BagSet, mem_v: torch.Tensor):
+        self._bs, self._v = bs, mem_v
+        self._host = None
+
+    def _load(self):
+        if self._host is None:
+            v = self._v.cpu().numpy()
+            keys = self._bs.mem_key.cpu().numpy()
+            nodes = [int(n) for b in self._bs.bags for n in b]
+            d = {}
+            for m, (n, k) in enumerate(zip(nodes, keys.tolist())):
+                if k >= 0:
+                    d[n] = float(v[m])
+            self._host = d
+        return self._host
+
+    def __getitem__(self, k):
+        return torch.tensor([self._load()[k]], dtype=torch.float32)
+
+    def __iter__(self):
+        return iter(self._load())
+
+    def __len__(self):
+        return len(self._load())
+
+    def floats(self) -> dict:
+        """The values as Python floats (no tensor per entry)."""
+        return dict(self._load())
+
+
+class _BagsView:
+    """``data.clone()`` with ``bags`` replaced (main.py:645-646) without copying the graph."""
+
+    def __init__(self, data, bags):
+        self.__dict__["_data"] = data
+        self.__dict__["bags"] = bags
+
+    def __getattr__(self, name):
+        return getattr(self.__dict__["_data"], name)
+
+
+def _train_bags(data, edge_dictionary, model, optimizer, criterion, criterion_per_node, frozen, previous_weights,
+                grad_mask, bags, bag_labels):
+    """main.py:641-673 with BAGS=True: MSE of the bag picks against the bag labels, backward,
+    gradient mask when destinations are frozen, Adam step, clamps, frozen restore."""
+    model.train()
+    optimizer.zero_grad()
+    predictions, by_bag, by_source = model(_BagsView(data, bags), edge_dictionary, True)
+    dev = predictions.device
+    labels = _device_cached(("bag_labels", id(bag_labels), bag_labels._version), dev,
+                            lambda: bag_labels.to(torch.float32), keep=bag_labels)
+    loss = criterion(predictions, labels)
+    loss_per_node = criterion_per_node(predictions.detach(), labels)
+    loss.backward()
+    if frozen:  # main.py:663-664
+        gm = _device_cached(("grad_mask", id(grad_mask), grad_mask._version), dev,
+                            lambda: grad_mask.to(torch.float32), keep=grad_mask)
+        model.input.weights.grad = model.input.weights.grad * gm
+    optimizer.step()
+    _clamp_and_restore(model, frozen, previous_weights)
+    return loss, by_source, loss_per_node, by_bag, predictions
+
+
+def create_bags(edg_dictionary, dest_dictionary, data):
+    """main.py:545-575: for every source, its destinations whose labels are all > 0.9 make one
+    bag (label 1); every other destination is a singleton bag (label 0, once); repeated bags
+    dropped (first kept). Sets ``data.bags`` / ``data.bag_labels`` [B, 1]."""
+    bag, labels = [], []
+    singles = set()
+    for key in edg_dictionary.keys():
+        group = []
+        for value in edg_dictionary[key]:
+            if min(dest_dictionary[value]) > 0.9:
+                group.append(value)
+            elif value not in singles:
+                singles.add(value)
+                bag.append([value])
+                labels.append(0)
+        if group:
+            bag.append(group)
+            labels.append(1)
+    seen = set()
+    new_bag, new_labels = [], []
+    for b, lab in zip(bag, labels):
+        t = tuple(b)
+        if t not in seen:
+            seen.add(t)
+            new_bag.append(b)
+            new_labels.append(lab)
+    data.bags = list(new_bag)
+    data.bag_labels = torch.Tensor(new_labels).unsqueeze(-1)
+
+
+def clean_bags_for_relation_type(data, edge_dictionary):
+    """main.py:577-592: every bag reduced to its members that are dictionary keys; emptied bags
+    dropped with their labels. Returns (bags, labels [B, 1])."""
+    keys = set(edge_dictionary.keys())
+    keep, keep_labels = [], []
+    for c, b in enumerate(data.bags):
+        tmp = [node for node in b if node in keys]
+        if tmp:
+            keep.append(tmp)
+            keep_labels.append(data.bag_labels[c])
+    return keep, torch.Tensor(keep_labels).unsqueeze(-1)
+
+
+def reinitialize_weights(data, destination_dictionary, previous_weights, destination_nodes_with_freezed_weights,
+                         BAGS, rng=None):
+    """main.py:498-512: frozen destinations keep ``previous_weights``, every other destination key
+    gets U(0, 1) from Python's ``random`` (dictionary order); other entries 0 (uninitialised in
+    the reference, never read)."""
+    rng = rng or random
+    weights = torch.zeros(int(data.num_nodes))
+    keys = (destination_dictionary.keys_arr.tolist() if isinstance(destination_dictionary, BagDestinationDictionary)
+            else list(destination_dictionary.keys()))
+    frozen = set(int(v) for v in destination_nodes_with_freezed_weights)
+    prev = previous_weights.detach().reshape(-1).cpu() if frozen else None
+    for key in keys:
+        weights[key] = prev[key] if key in frozen else rng.uniform(0., 1.)
+    return weights
+
+
+def retrieve_destinations_low_loss(max_destination_node_dict, loss_per_node, source_nodes_mask=None):
+    """main.py:530-543: the destinations of the dictionary entries (i-th entry ↔ loss_per_node[i])
+    with loss < 1e-4, first occurrence order."""
+    losses = loss_per_node.detach().reshape(-1).cpu().tolist() if torch.is_tensor(loss_per_node) else \
+        list(loss_per_node)
+    out = []
+    for index, value in enumerate(max_destination_node_dict.values()):
+        if losses[index] < 0.0001 and value not in out:
+            out.append(value)
+    return out
+
+
+def score_relation_bags_parallel(data_object, relation, features_dim, dataset, epochs: int = BAG_EPOCHS,
+                                 trace=None):
+    """main.py:853-917: score one candidate relation against the bags of ``data_object`` —
+    restarts of 50 epochs of train(BAGS=True) until two restarts in a row fail to lower the
+    loss; after an improving restart the destinations of the bags with loss < 1e-4 are frozen
+    (gradient mask 0) for the later restarts, whose weights are re-drawn. Returns (relation,
+    current_loss, model, predictions_for_each_restart, v) like the reference. Each restart's
+    epochs replay one captured HIP graph after three eager ones (main._epochs).
+    ``trace`` (a list) receives (loss, [pick per bag]) of every epoch (one host sync each)."""
+    mask, seen = [], set()
+    for bag in data_object.bags:
+        for elm in bag:
+            if elm not in seen:
+                seen.add(elm)
+                mask.append(elm)
+    edge_dictionary, destination_dictionary = create_edge_dictionary(data_object, relation, mask, BAGS=True,
+                                                                     dataset=dataset)
+    bags, bag_labels = clean_bags_for_relation_type(data_object, edge_dictionary)
+    weights = initialize_weights(data_object, destination_dictionary, BAGS=True)
+    N = int(data_object.num_nodes)
+    grad_mask = torch.ones(len(weights), 1)
+    criterion, criterion_per_node = get_loss(), get_loss_per_node()
+    preds = {}
+    frozen = []
+    v = len(bags) == 1 or (len(bags) > 1 and bag_labels.squeeze().tolist().count(1) == 0)
+    dev = edge_dictionary.device
+    from .main import _epochs
+    use_graph = os.environ.get("MPGNN_LOOP_GRAPH", "1") != "0" and trace is None
+    rest, current_loss, model = 0, 100, None
+    while rest < 2:
+        w_dev = weights.to(dev)
+        model = get_model(w_dev, features_dim).to(dev)  # InputLayer wraps w_dev: the restore reads the live weights
+        optimizer = torch.optim.Adam(list(model.parameters()), lr=0.1, fused=True, capturable=use_graph)
+        frozen_now = list(frozen)
+
+        def epoch():
+            return train(data_object, edge_dictionary, model, optimizer, criterion, mask, criterion_per_node,
+                         frozen_now, w_dev, grad_mask, True, bags_to_predict=bags, bags_to_predict_labels=bag_labels,
+                         dataset=dataset)
+
+        out = None
+        for _, out in _epochs(epoch, epochs, use_graph):
+            if trace is not None:
+                picks = out[3]
+                trace.append((float(out[0].item()), [picks.get(s_, -1) for s_ in [str(b) for b in bags]]))
+        loss, by_source, loss_per_bag, by_bag, _ = out
+        for key, val in by_source.floats().items():
+            preds.setdefault(key, []).append(val)
+        lv = float(loss.item())
+        if lv < current_loss:
+            frozen = retrieve_destinations_low_loss(by_bag, loss_per_bag, mask)
+            current_loss = lv
+            rest = 0
+        else:
+            rest += 1
+        for node in frozen:
+            grad_mask[node] = 0
+        weights = reinitialize_weights(data_object, destination_dictionary, model.input.weights.detach(), frozen,
+                                       BAGS=False)
+    return relation, current_loss, model, preds, v

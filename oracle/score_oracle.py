@@ -151,3 +151,196 @@ def score_relation_parallel(edge_index, edge_type, x, labels, relation, source_n
         if trace is not None:
             trace.append((float(loss.item()), dict(best)))
     return relation, loss.item(), ed, dd, model
+
+
+# ---------------------------------------------------------------------------------------------
+# bag branch (model.py:45-72; main.py:426-438, 543-596, 498-512, 530-543, 641-673, 853-917)
+# ---------------------------------------------------------------------------------------------
+def create_edge_dictionary_bags(edge_index, edge_type, relation, source_nodes_mask, bags, bag_labels):
+    """main.py:387-406 + 426-438 (BAGS=True): the same {source: [destinations]} dictionary, and
+    {destination: [labels of every bag holding one of its sources]} — per edge of the relation
+    (file order) whose source lies in some bag, the labels of that source's bags (bag order)
+    extended onto the destination's list."""
+    ei = masked_edge_index(edge_index, edge_type == relation)
+    src_list, dst_list = ei[0].tolist(), ei[1].tolist()
+    src_set = set(src_list)
+    mask_set = set(source_nodes_mask)
+    edge_dictionary = {}
+    for index in source_nodes_mask:                        # :396-397
+        if index in src_set:
+            edge_dictionary[index] = []
+    for s, d in zip(src_list, dst_list):                   # :399-401
+        if s in mask_set:
+            edge_dictionary[s].append(d)
+    edge_dictionary = {k: v for k, v in edge_dictionary.items() if v}
+    tmp = {}                                               # :428-432
+    for i, bag in enumerate(bags):
+        for node in bag:
+            tmp.setdefault(node, []).append(float(bag_labels[i].item()))
+    dest = {}                                              # :434-437
+    for s, d in zip(src_list, dst_list):
+        if s in tmp:
+            dest.setdefault(d, []).extend(tmp[s])
+    return edge_dictionary, dest
+
+
+def create_bags(edge_dictionary, destination_dictionary):
+    """main.py:545-575: per source, its destinations whose labels are all > 0.9 form one bag
+    (label 1); every other destination is a singleton bag (label 0); duplicates removed
+    (first kept). Returns (bags, bag_labels [B, 1])."""
+    bag, labels = [], []
+    for key in edge_dictionary.keys():
+        lst = []
+        for value in edge_dictionary[key]:
+            if min(destination_dictionary[value]) > 0.9:
+                lst.append(value)
+            elif [value] not in bag:
+                bag.append([value])
+                labels.append(0)
+        if lst:
+            bag.append(lst)
+            labels.append(1)
+    new_bag, new_labels = [], []
+    for b, lab in zip(bag, labels):
+        if b not in new_bag:
+            new_bag.append(b)
+            new_labels.append(lab)
+    return new_bag, torch.Tensor(new_labels).unsqueeze(-1)
+
+
+def clean_bags_for_relation_type(bags, bag_labels, edge_dictionary):
+    """main.py:577-592: each bag reduced to its nodes that are keys of the edge dictionary;
+    emptied bags dropped with their labels."""
+    keep, keep_labels = [], []
+    for c, b in enumerate(bags):
+        tmp = [n for n in b if n in edge_dictionary]
+        if tmp:
+            keep.append(tmp)
+            keep_labels.append(bag_labels[c])
+    return keep, torch.Tensor(keep_labels).unsqueeze(-1)
+
+
+def reinitialize_weights(num_nodes, destination_dictionary, previous_weights, frozen, rng=None):
+    """main.py:498-512: frozen destinations keep ``previous_weights``; every other destination
+    key gets U(0, 1) from Python's ``random`` in dictionary order; other nodes 0 (uninitialised
+    in the reference, never read)."""
+    rng = rng or random
+    weights = torch.zeros(num_nodes)
+    for key in destination_dictionary.keys():
+        if key in frozen:
+            weights[key] = previous_weights[key]
+        else:
+            weights[key] = rng.uniform(0., 1.)
+    return weights
+
+
+def retrieve_destinations_low_loss(max_destination_node_dict, loss_per_node):
+    """main.py:530-543: destinations of the entries (dict order, i-th entry ↔ loss_per_node[i])
+    with loss < 1e-4, first occurrence order."""
+    out = []
+    for index, (_key, value) in enumerate(max_destination_node_dict.items()):
+        if loss_per_node[index] < 0.0001 and value not in out:
+            out.append(value)
+    return out
+
+
+def score_forward_bags(weights, lin, bags, node_dict, feat):
+    """model.py:45-72 restated with the same tensor operations (so autograd unwinds it as the
+    reference's): per bag, per source in the dictionary, ``s = lin(feat[source])``, the first
+    argmax of ``weights[dsts] * s``, ``v = weights[max_node] * s``; the bag keeps the first
+    source whose v is strictly larger than the running maximum (-10 at the start).
+    Returns (max_weights [B, 1], {str(bag): max_node}, {source: v})."""
+    max_weights = torch.zeros(len(bags), 1)
+    by_bag, by_source = {}, {}
+    for i, bag in enumerate(bags):
+        cur = -10
+        for source_node in bag:
+            if source_node in node_dict:
+                w_src = weights[node_dict[source_node]].squeeze(-1)
+                w_src *= lin(feat[source_node])
+                max_node = node_dict[source_node][torch.argmax(w_src).item()]
+                by_source[source_node] = weights[max_node] * lin(feat[source_node])
+                if by_source[source_node] > cur:
+                    cur = by_source[source_node]
+                    by_bag[str(bag)] = max_node
+                    max_weights[i] = by_source[source_node]
+    max_weights.requires_grad_(True)
+    return max_weights, by_bag, by_source
+
+
+def train_bags(model, optimizer, edge_dictionary, bags, bag_labels, feat, frozen, previous_weights, grad_mask):
+    """main.py:641-673 with BAGS=True: MSE(mean) of the bag maxima against the bag labels,
+    backward, gradient mask when weights are frozen, Adam step, clamps, frozen restore.
+    Returns (loss, {source: v}, loss_per_bag, {str(bag): max_node}, predictions)."""
+    model.train()
+    optimizer.zero_grad()
+    pred, by_bag, by_source = score_forward_bags(model.input.weights, model.output.LinearLayerAttri, bags,
+                                                 edge_dictionary, feat)
+    loss = nn.MSELoss(reduction="mean")(pred, bag_labels)
+    loss_per_bag = nn.MSELoss(reduction="none")(pred, bag_labels)
+    loss.backward()
+    if frozen:
+        model.input.weights.grad = model.input.weights.grad * grad_mask
+    optimizer.step()
+    with torch.no_grad():
+        model.input.weights[:] = torch.clamp(model.input.weights, min=0.0, max=1.0)
+        model.output.LinearLayerAttri.weight[:] = torch.clamp(model.output.LinearLayerAttri.weight, min=0.0, max=1.0)
+        if frozen:
+            for idx in range(0, len(model.input.weights[:])):
+                if idx in frozen:
+                    model.input.weights[:][idx] = previous_weights[idx]
+    return loss, by_source, loss_per_bag, by_bag, pred
+
+
+def score_relation_bags_parallel(edge_index, edge_type, x, bags, bag_labels, relation, features_dim,
+                                 rng: random.Random | None = None, epochs: int = 50, trace=None, stop_after=None):
+    """main.py:853-917: restarts of 50 epochs until two restarts in a row fail to lower the
+    loss; after an improving restart the destinations of the bags with loss < 1e-4 are frozen
+    (gradient mask 0) for the next restarts; weights re-drawn per restart. ``trace`` receives
+    per epoch (loss, [max node per bag]) and per restart ('restart', loss, frozen list).
+    Returns (relation, current_loss, model, predictions_for_each_restart, v); ``stop_after`` ends
+    the run after that many train() calls (a prefix of the trajectory, for quick checks) and
+    returns None."""
+    rng = rng or random
+    train_bags._calls = 0
+    num_nodes = x.size(0)
+    mask = []
+    for bag in bags:
+        for elm in bag:
+            if elm not in mask:
+                mask.append(elm)
+    ed, dd = create_edge_dictionary_bags(edge_index, edge_type, relation, mask, bags, bag_labels)
+    cbags, clabels = clean_bags_for_relation_type(bags, bag_labels, ed)
+    weights = initialize_weights(num_nodes, dd, rng)
+    grad_mask = torch.ones(len(weights), 1)
+    feat = x.type(torch.FloatTensor)
+    preds, frozen = {}, []
+    v = len(cbags) == 1 or (len(cbags) > 1 and clabels.squeeze().tolist().count(1) == 0)
+    rest, current_loss, model = 0, 100, None
+    while rest < 2:
+        model = Score(weights, "synthetic", features_dim)
+        optimizer = torch.optim.Adam(model.parameters(), lr=0.1)
+        for _ in range(epochs):
+            loss, by_source, loss_per_bag, by_bag, _ = train_bags(model, optimizer, ed, cbags, clabels, feat, frozen,
+                                                                  weights, grad_mask)
+            if trace is not None:
+                trace.append((float(loss.item()), [by_bag.get(str(b)) for b in cbags]))
+            calls = getattr(train_bags, "_calls", 0) + 1
+            train_bags._calls = calls
+            if stop_after is not None and calls >= stop_after:
+                train_bags._calls = 0
+                return None
+        for key, value in by_source.items():
+            preds.setdefault(key, []).append(value.item())
+        if loss.item() < current_loss:
+            frozen = retrieve_destinations_low_loss(by_bag, loss_per_bag)
+            current_loss = loss.item()
+            rest = 0
+        else:
+            rest += 1
+        for node in frozen:
+            grad_mask[node] = 0
+        if trace is not None:
+            trace.append(("restart", float(loss.item()), list(frozen)))
+        weights = reinitialize_weights(num_nodes, dd, model.input.weights.detach()[:, 0], frozen, rng)
+    return relation, current_loss, model, preds, v

@@ -24,6 +24,10 @@ Outputs (all small):
   layer_all.npz           RGCNConv loop (mode ALL) assembled from reference CustomRGCNConv
                           per-relation transforms, forward + grads, C1 graph
   mpnetm_synthetic.npz    MPNetm(2,64,4,64,2,1,[[1,0]]) seed-30 state_dict + eval logits
+  score_synthetic.npz     score function, non-bag branch (score_relation_parallel)
+  score_bags_synthetic.npz score function, bag branch (score_relation_bags_parallel)
+
+``--only NAME`` runs one generator (e.g. ``--only make_score_bags_golden``).
 """
 from __future__ import annotations
 
@@ -52,6 +56,9 @@ STANDIN = {
             def __init__(self, **kw):
                 for k, v in kw.items():
                     setattr(self, k, v)
+            def clone(self):
+                import copy
+                return copy.copy(self)
     """),
     "torch_geometric/nn/__init__.py": textwrap.dedent("""
         from .conv import MessagePassing
@@ -256,7 +263,9 @@ def make_mpnetm_golden(model):
 
 
 SCORE_FUNCS = ("masked_edge_index", "create_edge_dictionary", "initialize_weights", "get_model", "get_optimizer",
-               "get_loss", "get_loss_per_node", "train", "score_relation_parallel")
+               "get_loss", "get_loss_per_node", "train", "score_relation_parallel", "create_bags",
+               "clean_bags_for_relation_type", "reinitialize_weights", "retrieve_destinations_low_loss",
+               "score_relation_bags_parallel")
 
 
 def reference_main_functions(model):
@@ -355,6 +364,85 @@ def make_score_golden(model):
     np.savez_compressed(os.path.join(HERE, "score_synthetic.npz"), **out)
 
 
+def make_score_bags_golden(model):
+    """Bag branch of the score function (model.py:45-72) driven by the reference's own
+    score_relation_bags_parallel (main.py:853-917: create_edge_dictionary BAGS=True :426-438,
+    clean_bags_for_relation_type :577-592, initialize / reinitialize_weights :479-512, train
+    BAGS=True :641-673, retrieve_destinations_low_loss :530-543) on the planted synthetic graph
+    (KAT L3). The bags come from the reference's create_bags (:545-575) over the dictionaries of
+    a first, non-bag scoring of relation 0 (the search's first step, main.py:1309-1380). Every
+    train() call of the restarts is recorded (loss, max node per bag, loss per bag), with the
+    restart bookkeeping (frozen destinations, the returned current_loss, predictions per source)."""
+    import random
+    ns = reference_main_functions(model)
+    kat = np.load(os.path.join(HERE, "kat_synthetic.npz"))
+    link, node, label = kat["L3_link"], kat["L3_node"], kat["L3_label"]
+    edge_index = torch.tensor(np.stack([link[:, 0], link[:, 2]]))
+    edge_type = torch.tensor(link[:, 1])
+    x = torch.from_numpy(node[:, 1:].astype(np.float32))
+    N = x.size(0)
+    lab = torch.zeros(N, dtype=torch.int64)
+    lab[torch.from_numpy(label[:, 0])] = torch.from_numpy(label[:, 1])
+    data = model.Data()
+    data.x, data.edge_index, data.edge_type, data.num_nodes = x, edge_index, edge_type, N
+    data.labels = lab.unsqueeze(-1)
+    mask = torch.unique(edge_index[0][edge_type == 0]).tolist()
+    ed0, dd0 = ns["create_edge_dictionary"](data, 0, mask, BAGS=False, dataset="synthetic")
+    ns["create_bags"](ed0, dd0, data)
+    bags, bag_labels = data.bags, data.bag_labels
+    out = {"bag_ptr": np.cumsum([0] + [len(b) for b in bags]).astype(np.int64),
+           "bag_nodes": np.array(sum(bags, []), dtype=np.int64), "bag_labels": bag_labels.numpy()}
+    orig_train = ns["train"]
+    for rel in (1, 2, 3, 0):
+        calls = []
+
+        def recording_train(*a, **kw):
+            res = orig_train(*a, **kw)
+            loss, by_source, loss_per_bag, by_bag, pred = res
+            cbags = kw["bags_to_predict"]
+            calls.append((loss.item(), [by_bag.get(str(b), -1) for b in cbags], loss_per_bag.detach().numpy()[:, 0].copy(),
+                          list(a[7])))
+            return res
+        ns["train"] = recording_train
+        random.seed(2000 + rel)
+        torch.manual_seed(88)
+        r, current_loss, mod, preds, v = ns["score_relation_bags_parallel"](data, rel, x.size(1), dataset="synthetic")
+        ns["train"] = orig_train
+        tag = f"bags_rel{rel}"
+        # the cleaned bags of this relation, as train() received them
+        random.seed(2000 + rel)
+        mask_b = []
+        for bag in bags:
+            for elm in bag:
+                if elm not in mask_b:
+                    mask_b.append(elm)
+        edb, ddb = ns["create_edge_dictionary"](data, rel, mask_b, BAGS=True, dataset="synthetic")
+        cb, cl = ns["clean_bags_for_relation_type"](data, edb)
+        out[f"{tag}_cbag_ptr"] = np.cumsum([0] + [len(b) for b in cb]).astype(np.int64)
+        out[f"{tag}_cbag_nodes"] = np.array(sum(cb, []), dtype=np.int64)
+        out[f"{tag}_cbag_labels"] = cl.numpy()
+        keys = list(edb.keys())
+        out[f"{tag}_keys"] = np.array(keys, dtype=np.int64)
+        out[f"{tag}_key_ptr"] = np.cumsum([0] + [len(edb[k]) for k in keys]).astype(np.int64)
+        out[f"{tag}_dst"] = np.array(sum((edb[k] for k in keys), []), dtype=np.int64)
+        out[f"{tag}_dd_keys"] = np.array(list(ddb.keys()), dtype=np.int64)
+        out[f"{tag}_dd_min"] = np.array([min(v_) for v_ in ddb.values()], dtype=np.float64)
+        out[f"{tag}_dd_len"] = np.array([len(v_) for v_ in ddb.values()], dtype=np.int64)
+        out[f"{tag}_loss"] = np.array([c[0] for c in calls])
+        out[f"{tag}_bag_argmax"] = np.array([c[1] for c in calls], dtype=np.int32)
+        out[f"{tag}_loss_per_bag_last"] = np.array([c[2] for c in calls[49::50]])
+        out[f"{tag}_frozen_per_call"] = np.array([len(c[3]) for c in calls], dtype=np.int64)
+        out[f"{tag}_current_loss"] = np.float64(current_loss)
+        out[f"{tag}_v"] = np.bool_(v)
+        pk = list(preds.keys())
+        out[f"{tag}_pred_keys"] = np.array(pk, dtype=np.int64)
+        out[f"{tag}_pred_vals"] = np.array([preds[k] for k in pk], dtype=np.float64)
+        out[f"{tag}_lin_final"] = mod.output.LinearLayerAttri.weight.detach().numpy()
+        wf = mod.input.weights.detach().numpy()[:, 0]
+        out[f"{tag}_w_final_dd"] = wf[np.array(list(ddb.keys()), dtype=np.int64)]
+    np.savez_compressed(os.path.join(HERE, "score_bags_synthetic.npz"), **out)
+
+
 def make_fb15k_triples():
     """FB15K-237 dev+test triples as entity/relation indices (entities.txt / relations.txt
     order). train.tsv is missing from the reference (.MISSING_LARGE_BLOBS:7); the bench's
@@ -383,10 +471,15 @@ def main():
         raise SystemExit("make_golden.py needs /root/reference (survey container only)")
     torch.set_num_threads(1)
     layer, model = import_reference()
+    if "--only" in sys.argv:
+        name = sys.argv[sys.argv.index("--only") + 1]
+        globals()[name](model)
+        return
     make_kat()
     make_layer_goldens(layer)
     make_mpnetm_golden(model)
     make_score_golden(model)
+    make_score_bags_golden(model)
     make_fb15k_triples()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):

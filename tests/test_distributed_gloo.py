@@ -133,14 +133,16 @@ def _reducer_worker(rank, world, port, q):
                 self.red = ShardGradReducer((self.weight, self.root, self.bias), dist.group.WORLD) if reduce else None
 
             def forward(self, h):
+                w, r, b = self.weight, self.root, self.bias
                 if self.red is not None and torch.is_grad_enabled():
-                    self.red.note_use()
-                return torch.tanh(h @ self.weight.sum(0) + h @ self.root * (rank + 1) + self.bias)
+                    w, r, b = self.red.tap(w, r, b)
+                return torch.tanh(h @ w.sum(0) + h @ r * (rank + 1) + b)
 
-        def run(layer, iters, stale=False, set_to_none=True):
+        def run(layer, iters, stale=False, set_to_none=True, accumulate=False):
             grads = []
             for it in range(iters):
-                layer.zero_grad(set_to_none=set_to_none)
+                if not accumulate or it == 0:
+                    layer.zero_grad(set_to_none=set_to_none)
                 if stale and it == 0:
                     layer(xs[rank])  # grad-enabled forward never backpropagated (stale use count)
                 out = layer(layer(xs[rank]))  # two uses per step (Net.conv2 is shared, model.py:146)
@@ -152,13 +154,35 @@ def _reducer_worker(rank, world, port, q):
         for gs in plain:  # expected: the sum over ranks of the local gradients
             for g_ in gs:
                 dist.all_reduce(g_)
-        for name, kw in (("set_to_none", {}), ("zero_in_place", {"set_to_none": False}),
-                         ("stale_use", {"stale": True})):
+        # gradient accumulation (no zero_grad between the backward passes): G1 + G2, each
+        # reduced once — never the already-reduced G1 summed over the ranks again
+        plain_acc = [plain[0], [a + b for a, b in zip(plain[0], plain[1])]]
+        for name, kw, ref in (("set_to_none", {}, plain), ("zero_in_place", {"set_to_none": False}, plain),
+                              ("stale_use", {"stale": True}, plain), ("accumulate", {"accumulate": True}, plain_acc),
+                              ("accumulate_in_place", {"accumulate": True, "set_to_none": False}, plain_acc)):
             got = run(Layer(True), 2, **kw)
-            for it, (a, b) in enumerate(zip(got, plain)):
+            for it, (a, b) in enumerate(zip(got, ref)):
                 for pa, pb, pn in zip(a, b, ("weight", "root", "bias")):
                     if not torch.allclose(pa, pb, rtol=1e-6, atol=1e-6):
                         msgs.append(f"{name} iter {it} {pn}: {float((pa - pb).abs().max()):.3e}")
+        # a later UNSHARDED backward through the same parameters never touches the reducer
+        lay = Layer(True)
+        run(lay, 1)
+        lay.red = None
+        lay.zero_grad()
+        lay(xs[rank]).sum().backward()
+        plain_one = Layer(False)
+        plain_one(xs[rank]).sum().backward()
+        for pa, pb in zip((lay.weight, lay.root, lay.bias), (plain_one.weight, plain_one.root, plain_one.bias)):
+            if not torch.equal(pa.grad, pb.grad):
+                msgs.append("unsharded backward after a sharded one differs")
+        # torch.autograd.grad over tapped parameters fails loudly (never partial sums)
+        lay2 = Layer(True)
+        try:
+            torch.autograd.grad(lay2(xs[rank]).sum(), [lay2.weight])
+            msgs.append("autograd.grad over a sharded layer's parameters did not raise")
+        except RuntimeError:
+            pass
         # all-gather of owned rows: rank k contributes rows [lo_k, hi_k) only
         ei = torch.randint(0, 37, (2, 300), generator=torch.Generator().manual_seed(2))
         ranges = shard_ranges(ei, 37, world)

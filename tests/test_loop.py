@@ -332,3 +332,30 @@ def test_rgcn_loop_graph_replay_equals_eager(capsys, monkeypatch):
         outs.append((f1, capsys.readouterr().out))
     assert outs[0] == outs[1], outs
     assert outs[0][1].count("train loss") == 3
+
+
+@pytest.mark.gpu
+def test_loops_release_their_workspace_between_calls():
+    """Each drop-in loop owns the scratch buffers of its side stream (main._epochs releases
+    them once its HIP graph is gone): calling main.mpgnn_parallel_multiple and
+    main_rgcn.mpgnn_parallel_multiple again and again leaves torch.cuda.memory_allocated and the
+    workspace cache where the first call left them (main.py:1371-1373 trains one model per
+    metapath candidate in one process; a buffer kept per call would grow without bound)."""
+    from mpgnn_amd.functional import workspace_bytes_cached
+    g = data.fb15k237_graph(feat_dim=128, seed=0, recipe="survey")
+    d = _task(g, classes=2).to(DEV)
+    counts = torch.bincount(g.edge_type, minlength=g.num_relations)
+    mp = [int(v) for v in torch.argsort(counts, descending=True, stable=True)[:3]]
+    runs = [lambda: main.mpgnn_parallel_multiple(d, 128, 128, g.num_relations, 128, 2, [mp], epochs=6),
+            lambda: main_rgcn.mpgnn_parallel_multiple(d, 128, 128, g.num_relations, 128, 2, 3, epochs=6,
+                                                      verbose=False)]
+    for run in runs:
+        torch.manual_seed(30)
+        run()  # plan built + cached, default-stream scratch sized
+        torch.cuda.synchronize()
+        base, base_ws = torch.cuda.memory_allocated(), workspace_bytes_cached()
+        for _ in range(3):
+            run()
+            torch.cuda.synchronize()
+            assert torch.cuda.memory_allocated() == base, (torch.cuda.memory_allocated(), base)
+            assert workspace_bytes_cached() == base_ws, (workspace_bytes_cached(), base_ws)
