@@ -609,7 +609,7 @@ def main():
     kinds = {"mean": "segment means (flat_rows_kernel over the multi-edge segments)",
              "seg_fwd": ("split-K transform GEMM of the whole layer (single_bf3_kernel)"
                          if single and args.gemm == "bf3" and F in (64, 128) and not sharded else
-                         "transform GEMM (rel_gemm_bf3_kernel / rel_gemm_kernel)"),
+                         "transform GEMM (rel_gemm_bf3_kernel / rel_gemm_bf3w_kernel at F = 256 / rel_gemm_kernel)"),
              "row_fwd": (("rows with a segment: single_fix_kernel (the root items' epilogue finished the others)"
                           if root_epi else "combine / output (single_combine_kernel: node -> segment map, one "
                           "streaming pass)") if single else
@@ -653,7 +653,8 @@ def main():
     }
     # the transform on the bf16-split matrix cores: rel_gemm_bf3_kernel (mode ALL), mode SINGLE
     # unsharded: single_bf3_kernel (split-K: x @ root and mean @ W halves, one launch per layer)
-    bf3 = args.gemm == "bf3" and F in (64, 128) and (not single or not sharded)
+    # (F = 256, mode ALL: rel_gemm_bf3w_kernel, the split-K form of the same six-product scheme)
+    bf3 = args.gemm == "bf3" and ((F in (64, 128) and (not single or not sharded)) or (F == 256 and not single))
     rooflines = []
     for kind, (bound, work, model_txt) in model_costs.items():
         if kind not in per_layer:
@@ -677,7 +678,8 @@ def main():
         else:
             ach = work / (us * 1e-6) / 1e9
             peak, unit = PEAK_HBM, "GB/s"
-        seg_name = "single_bf3_kernel" if bf3 and single else "rel_gemm_bf3_kernel" if bf3 else "rel_gemm_kernel"
+        seg_name = ("single_bf3_kernel" if bf3 and single else
+                    ("rel_gemm_bf3w_kernel" if F == 256 else "rel_gemm_bf3_kernel") if bf3 else "rel_gemm_kernel")
         kname = {"seg_fwd": seg_name, "mean": "flat_rows_kernel",
                  "row_fwd": ("single_fix_kernel" if root_epi else "single_combine_kernel") if single
                  else "flat_rows_kernel"}[kind]

@@ -1961,6 +1961,293 @@ __global__ __launch_bounds__(kSingleThreads, 1) void single_bf3_kernel(SingleBf3
     }
 }
 
+// ----------------------------------------------------------------------------------------
+// rel_gemm_bf3w_kernel — the K = 256, N = 256 transform (C5: F_in = F_out = 256) and its dgrad
+// on the bf16 matrix cores with the exact three-piece split of the fp32 operands. A wave's
+// K × 32 weight slice in bf16 pieces would take 192 VGPRs at K = 256, so the workgroup's eight
+// waves SPLIT K: waves 0-3 multiply k ∈ [0, 128), waves 4-7 k ∈ [128, 256), each over one
+// 32-column strip of the workgroup's 128 columns (96 VGPRs of slice, as at K = 128). The six
+// products of a k-step go into ONE fp32 accumulator (each MFMA adds its 16 exact products and
+// rounds once: six roundings per 16 k against the fp32 chain's sixteen). The upper half hands its
+// 32 × 128 partial tile to the lower half through LDS (double-buffered), which adds
+// (lower + upper), applies the dgrad row scale, and stores the tile DURING the next item's chain
+// (bounds-checked buffer stores, two per k-step); the next item's A tile is committed to the other
+// LDS buffer three quarters into the chain and the rows of the item after it are issued right
+// then: one barrier per item. The two 128-column blocks of an item are two workgroups eight block
+// ids apart — one XCD, same item range — so the second gather of the A rows hits that XCD's L2.
+// Items, row gathers and outputs as rel_gemm_kernel (RelGemmArgs: relation tiles of segments,
+// then node rows; forward A = x row / compact mean row, dgrad A = dout[node_1] scaled by 1/cnt).
+// ----------------------------------------------------------------------------------------
+template <bool DGRAD>
+struct RelGemmBf3W {
+    static constexpr int K = 256, N = 256, KH = 128, NS = KH / 16, LDAB = KH + 8, PLANE = 32 * LDAB;
+    static constexpr int WPT = 4;                 // float4 per thread: 32 rows × 32 float4 of a K half / 256
+    static constexpr int LDO = 128 + 4;           // fp32 row stride of the exchanged partial tile
+    // [2 buffers][2 halves][3 planes] bf16 + [2][32][LDO] exchange tiles + [3][32] row scales
+    static constexpr size_t lds_bytes() {
+        return (size_t)12 * PLANE * 2 + (size_t)2 * 32 * LDO * sizeof(float) + 3 * 32 * sizeof(float);
+    }
+    struct Item {
+        int r0, nrows, root;
+        const float* w;
+    };
+    // Item descriptors of a 64-item window, lane l holding item base + l (vector loads, read back
+    // with readlane: no dependent scalar loads on the item loop's critical path)
+    struct Tab {
+        int r0, nrows, wrel;  // wrel: weight index, -1 = root
+    };
+    __device__ static __forceinline__ Tab load_tab(const RelGemmArgs& a, int base, int i_end, int lane) {
+        Tab tb;
+        const int i = min(base + lane, i_end - 1);
+        if (i < a.n_rel) {
+            tb.r0 = a.t_begin[a.t_lo + i];
+            tb.nrows = a.t_end[a.t_lo + i] - tb.r0;
+            tb.wrel = a.w_per_rel ? a.s_rel[tb.r0] : 0;
+        } else {
+            tb.r0 = a.row_lo + (i - a.n_rel) * 32;
+            tb.nrows = min(32, a.row_hi - tb.r0);
+            tb.wrel = -1;
+        }
+        return tb;
+    }
+    __device__ static __forceinline__ Item item_at(const RelGemmArgs& a, const Tab& tb, int k) {
+        Item it;
+        it.r0 = readlane(tb.r0, k);
+        it.nrows = readlane(tb.nrows, k);
+        const int wr = readlane(tb.wrel, k);
+        it.root = wr < 0;
+        it.w = it.root ? a.Wroot : a.W + (size_t)wr * K * N;
+        return it;
+    }
+    // source row of each of the thread's WPT tile rows (row t/32 + 8j of the item) and the row's
+    // count (dgrad scale; 1 otherwise)
+    __device__ static __forceinline__ void gather_idx(const RelGemmArgs& a, const Item& it, int t, int (&row)[WPT],
+                                                      int& cnt) {
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) row[j] = it.r0 + min(t / 32 + 8 * j, it.nrows - 1);
+        cnt = 1;
+        if (!it.root) {
+            if constexpr (DGRAD) {
+                cnt = a.s_cnt[it.r0 + min(t & 31, it.nrows - 1)];
+#pragma unroll
+                for (int j = 0; j < WPT; ++j) row[j] = a.s_row[row[j]];
+            } else {
+#pragma unroll
+                for (int j = 0; j < WPT; ++j) row[j] = a.s_src[row[j]];
+            }
+        }
+    }
+    __device__ static __forceinline__ void issue(const RelGemmArgs& a, int kh, int t, const int (&row)[WPT],
+                                                 float4 (&v)[WPT]) {
+        const int c4 = kh * KH + (t & 31) * 4;
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+            const float* base;
+            if constexpr (DGRAD) {
+                base = a.Aroot + (size_t)row[j] * K;
+            } else {
+                base = row[j] >= 0 ? a.Aroot + (size_t)row[j] * K : a.Arel + (size_t)(-row[j] - 1 - a.m_lo) * K;
+            }
+            v[j] = *reinterpret_cast<const float4*>(base + c4);
+        }
+    }
+    __device__ static __forceinline__ void commit(const Item& it, int kh, int t, const float4 (&v)[WPT], int cnt,
+                                                  __bf16* planes, float* sc) {
+        __bf16* P = planes + kh * 3 * PLANE;
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+            const int r = t / 32 + 8 * j;
+            const float4 x = r < it.nrows ? v[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            __bf16 p0[4], p1[4], p2[4];
+            split3_bf16(x.x, p0[0], p1[0], p2[0]);
+            split3_bf16(x.y, p0[1], p1[1], p2[1]);
+            split3_bf16(x.z, p0[2], p1[2], p2[2]);
+            split3_bf16(x.w, p0[3], p1[3], p2[3]);
+            __bf16* d = P + r * LDAB + (t & 31) * 4;
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<bf16x4*>(d) = bf16x4{p0[0], p0[1], p0[2], p0[3]};
+            *reinterpret_cast<bf16x4*>(d + PLANE) = bf16x4{p1[0], p1[1], p1[2], p1[3]};
+            *reinterpret_cast<bf16x4*>(d + 2 * PLANE) = bf16x4{p2[0], p2[1], p2[2], p2[3]};
+        }
+        if (kh == 0 && t < 32) sc[t] = 1.0f / (float)cnt;
+    }
+    // the wave's slice: B(kh·128 + 16s + 8h + j, col) in bf16 pieces
+    __device__ static __forceinline__ void load_b(const float* w, int kh, int col, int h, bf16x8 (&b)[NS][3]) {
+        float f[NS][8];
+        if constexpr (!DGRAD) {
+            const float* p = w + (size_t)(kh * KH + 8 * h) * N + col;
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) f[s][j] = p[(size_t)(16 * s + j) * N];
+        } else {  // B(k, n) = W[n][k]
+            const float* p = w + (size_t)col * K + kh * KH + 8 * h;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const float4 t0 = *reinterpret_cast<const float4*>(p + 16 * s);
+                const float4 t1 = *reinterpret_cast<const float4*>(p + 16 * s + 4);
+                f[s][0] = t0.x; f[s][1] = t0.y; f[s][2] = t0.z; f[s][3] = t0.w;
+                f[s][4] = t1.x; f[s][5] = t1.y; f[s][6] = t1.z; f[s][7] = t1.w;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                __bf16 h0, h1, h2;
+                split3_bf16(f[s][j], h0, h1, h2);
+                b[s][0][j] = h0;
+                b[s][1][j] = h1;
+                b[s][2][j] = h2;
+            }
+    }
+};
+
+template <bool DGRAD>
+__global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
+    using G = RelGemmBf3W<DGRAD>;
+    extern __shared__ __bf16 smem_bf[];
+    __bf16* As = smem_bf;                                                   // [2][2 halves][3][PLANE]
+    float* Ot = reinterpret_cast<float*>(smem_bf + 12 * G::PLANE);         // [2][32][LDO]
+    float* Sc = Ot + 2 * 32 * G::LDO;                                      // [3][32]
+    const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int kh = wave >> 2;   // K half of the wave (uniform)
+    const int wq = wave & 3;    // 32-column strip
+    const int t = tid & 255;    // thread within its half
+    // block b: XCD b & 7; within an XCD, consecutive pairs (cb = 0, 1) share an item range
+    const int Gx = (int)gridDim.x;
+    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+    const int per_xcd = Gx >> 3;                 // launched as a multiple of 16
+    const int cb = slot & 1;
+    const int n_ranges = Gx >> 1;
+    const int rng = xcd * (per_xcd >> 1) + (slot >> 1);
+    const int n_items = a.n_rel + a.n_root;
+    const int i_beg = (int)((long long)rng * n_items / n_ranges);
+    const int i_end = (int)((long long)(rng + 1) * n_items / n_ranges);
+    if (i_beg >= i_end) return;
+    const int col = cb * 128 + wq * 32 + c;
+
+    // item windows: tab_a covers [wb, wb + 64), tab_b the next 64 items (loaded one window ahead)
+    int wb = i_beg;
+    typename G::Tab tab_a = G::load_tab(a, wb, i_end, lane), tab_b = G::load_tab(a, wb + 64, i_end, lane);
+    auto get_item = [&](int i) {
+        return i - wb < 64 ? G::item_at(a, tab_a, i - wb) : G::item_at(a, tab_b, i - wb - 64);
+    };
+    // prologue: item i_beg committed, rows of i_beg+1 in flight, sources of i_beg+2 loaded
+    typename G::Item cur = get_item(i_beg);
+    int row[G::WPT], cnt0 = 1;
+    float4 v[G::WPT];
+    G::gather_idx(a, cur, t, row, cnt0);
+    G::issue(a, kh, t, row, v);
+    bf16x8 b[G::NS][3];
+    G::load_b(cur.w, kh, col, h, b);
+    G::commit(cur, kh, t, v, cnt0, As, Sc + (i_beg % 3) * 32);
+    typename G::Item nxt = cur, nn = cur;
+    int cnt1 = 1, cnt2 = 1;
+    if (i_beg + 1 < i_end) {
+        nxt = get_item(i_beg + 1);
+        G::gather_idx(a, nxt, t, row, cnt1);
+        G::issue(a, kh, t, row, v);
+    }
+    if (i_beg + 2 < i_end) {
+        nn = get_item(i_beg + 2);
+        G::gather_idx(a, nn, t, row, cnt2);
+    }
+    __syncthreads();
+
+    float prev[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) prev[r] = 0.0f;
+    // the lower half's store target: item i-1's rows (bounds: its nrows; none before the first)
+    __amdgpu_buffer_rsrc_t prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.Y, (short)0, 0, 0x00020000);
+    auto store_prev = [&](int r) {
+        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(prev[r]), prev_rsrc, rr * (G::N * 4) + col * 4, 0, 0);
+    };
+    int buf = 0;
+    for (int i = i_beg; i < i_end; ++i) {
+        const bool has_next = i + 1 < i_end;
+        const __bf16* Ab = As + (buf * 2 + kh) * 3 * G::PLANE + c * G::LDAB + 8 * h;
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+        bf16x8 f0 = *reinterpret_cast<const bf16x8*>(Ab);
+        bf16x8 f1 = *reinterpret_cast<const bf16x8*>(Ab + G::PLANE);
+        bf16x8 f2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * G::PLANE);
+#pragma unroll
+        for (int s = 0; s < G::NS; ++s) {
+            const bf16x8 a0 = f0, a1 = f1, a2 = f2;
+            if (s + 1 < G::NS) {
+                f0 = *reinterpret_cast<const bf16x8*>(Ab + 16 * (s + 1));
+                f1 = *reinterpret_cast<const bf16x8*>(Ab + G::PLANE + 16 * (s + 1));
+                f2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * G::PLANE + 16 * (s + 1));
+            }
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[s][0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][0], acc, 0, 0, 0);
+            if (kh == 0) {  // item i-1's tile leaves two rows per k-step
+                store_prev(2 * s);
+                store_prev(2 * s + 1);
+            }
+            if (s == (3 * G::NS) / 4 - 1 && has_next) {
+                G::commit(nxt, kh, t, v, cnt1, As + (buf ^ 1) * 6 * G::PLANE, Sc + ((i + 1) % 3) * 32);
+                if (i + 2 < i_end) G::issue(a, kh, t, row, v);  // item i+2's rows, in flight for a chain
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        float* Oe = Ot + buf * 32 * G::LDO;
+        if (kh == 1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) Oe[((r & 3) + 8 * (r >> 2) + 4 * h) * G::LDO + wq * 32 + c] = acc[r];
+        }
+        if (has_next && nxt.w != cur.w) G::load_b(nxt.w, kh, col, h, b);  // after the chain: registers free
+        const typename G::Item next_item = nxt;
+        if (i + 3 < i_end) {  // sources of item i+3 (row was consumed by the issue above)
+            if (i + 3 - wb >= 64) {  // item i+3 opens the next window: shift, prefetch the one after
+                wb += 64;
+                tab_a = tab_b;
+                tab_b = G::load_tab(a, wb + 64, i_end, lane);
+            }
+            typename G::Item it3 = get_item(i + 3);
+            int c3;
+            G::gather_idx(a, it3, t, row, c3);
+            nxt = nn;
+            cnt1 = cnt2;
+            nn = it3;
+            cnt2 = c3;
+        } else {
+            nxt = nn;
+            cnt1 = cnt2;
+        }
+        __syncthreads();  // upper partial tile of item i in LDS; item i+1's tiles committed
+        if (kh == 0) {
+            const float* sc = Sc + (i % 3) * 32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+                float o = acc[r] + Oe[rr * G::LDO + wq * 32 + c];
+                if constexpr (DGRAD) {
+                    if (!cur.root) o = o * sc[rr];
+                }
+                prev[r] = o;
+            }
+            float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * G::N : a.Y + (size_t)(cur.r0 - a.sel_b) * G::N;
+            const int bytes = __builtin_amdgcn_readfirstlane(cur.nrows) * G::N * 4;
+            prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(Yt, (short)0, bytes, 0x00020000);
+        }
+        cur = next_item;
+        buf ^= 1;
+    }
+    if (kh == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) store_prev(r);
+    }
+}
+
 template <int KB>  // Kp = 64·KB
 __global__ __launch_bounds__(kThreads, 2) void tile_gemm_kernel(TileGemmArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -3968,6 +4255,17 @@ static void launch_rel_gemm_bf3(const RelGemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((rel_gemm_bf3_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
+// K = N = 256: one 512-thread workgroup per CU; column-block pairs on one XCD (grid a multiple of
+// 16: 8 XCDs × pairs), item ranges split over the pairs
+template <bool DGRAD>
+static void launch_rel_gemm_bf3w(const RelGemmArgs& a, hipStream_t st) {
+    const size_t lds = RelGemmBf3W<DGRAD>::lds_bytes();
+    const int n_items = a.n_rel + a.n_root;
+    int pairs = std::min(n_items, cu_count() / 2);
+    pairs = std::max(8, (pairs + 7) / 8 * 8);
+    hipLaunchKernelGGL((rel_gemm_bf3w_kernel<DGRAD>), dim3(2 * pairs), dim3(512), lds, st, a);
+}
+
 static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, hipStream_t st) {
     if (g_gemm_bf3 && (K == 64 || K == 128) && a.node_map == nullptr) {
         if (K == 64) {
@@ -3977,6 +4275,11 @@ static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, hipStream_t
             if (dgrad) launch_rel_gemm_bf3<2, true>(a, st);
             else launch_rel_gemm_bf3<2, false>(a, st);
         }
+        return;
+    }
+    if (g_gemm_bf3 && K == 256 && a.node_map == nullptr) {  // C5: split-K bf16 kernel, two column blocks
+        if (dgrad) launch_rel_gemm_bf3w<true>(a, st);
+        else launch_rel_gemm_bf3w<false>(a, st);
         return;
     }
     if (K == 256) {  // F_in = F_out = 256 (C5): two 128-column blocks, K = 256
@@ -4875,6 +5178,7 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
         case MPGNN_OPT_BWD_FUSED:
             g_bwd_fused = value != 0;
             return MPGNN_OK;
+
         case MPGNN_OPT_CHUNK_ROWS:
             if (value < 32 || value > 1024 || value % 32 != 0)
                 return arg_error("MPGNN_OPT_CHUNK_ROWS must be 32..1024, a multiple of 32");
