@@ -81,9 +81,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="fb15k237", choices=list(WORKLOADS))
-    ap.add_argument("--mode", default="all", choices=["all", "single", "score"],
+    ap.add_argument("--mode", default="all", choices=["all", "single", "score", "score_all"],
                     help="all = RGCN Net (mode B, main_rgcn.py); single = MPNetm metapath chain (mode A, main.py); "
-                         "score = the metapath score function (model.py:26-125, main.py:727-760)")
+                         "score = the metapath score function (model.py:26-125, main.py:727-760); score_all = every "
+                         "relation of the first search round at once (main.py:1309-1330, score_relations_batched)")
     ap.add_argument("--relation", type=int, default=None, help="mode score: relation scored (default: the largest)")
     ap.add_argument("--metapath", default=None,
                     help="mode single: comma-separated relations, one per layer (default C2 '1,0', C5 '2,1,0', "
@@ -485,6 +486,146 @@ def bench_score(args):
     return result
 
 
+def bench_score_all(args):
+    """Mode score_all: the first round of the metapath search —
+    every relation scored by score_relation_parallel (main.py:1309-1330: 100 epochs each, split
+    over MPI ranks) — as ONE batched problem (score.score_relations_batched: per epoch one argmax
+    launch over every relation's dictionary, one gradient scatter, one fused Adam over the stacked
+    [R, N] weights, one clamp; replayed as a HIP graph). One STEP = one epoch of all relations.
+    value = edges scored per second = E (every edge of every relation read by the argmax) ·
+    epochs / time. Beside it: the per-relation drop-in path (score_relation_parallel per
+    relation, its own graph) on a sample of relations, extrapolated; the CPU oracle's per-source
+    Python loop on a bounded sample (2 relations × 3 epochs), extrapolated. roofline: the
+    all-relation argmax launch (mpgnn_score_argmax_multi) per launch, HIP events around 50 graph-
+    captured calls, against HBM with its algorithmic bytes."""
+    import random as _random
+    from mpgnn_amd import score as sc
+    rank, world, local, group = setup_dist(args.gpus)
+    if world > 1:
+        raise SystemExit("--mode score_all shards nothing (one scoring round is one batched problem per GPU)")
+    dev = torch.device("cuda", local)
+    g = data.fb15k237_graph(feat_dim=2, seed=0, recipe="survey") if args.workload.startswith("fb15k237") \
+        else data.config_graph(args.workload)
+    N = g.num_nodes
+    rels = torch.unique(g.edge_type).tolist()
+
+    class D:
+        pass
+    d = D()
+    d.x = torch.zeros(N, 2)
+    d.edge_index, d.edge_type, d.num_nodes = g.edge_index.to(dev), g.edge_type.to(dev), N
+    d.labels = torch.randint(0, 2, (N, 1), generator=torch.Generator().manual_seed(0))
+    epochs = 100  # main.py:755
+    _random.seed(0)
+    torch.manual_seed(77)
+    sc.score_relations_batched(d, rels, 2, "synthetic", epochs=5)  # warm-up: dictionaries, capture path
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(max(1, min(args.steps, 3))):
+        _random.seed(0)
+        torch.manual_seed(77)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = sc.score_relations_batched(d, rels, 2, "synthetic", epochs=epochs)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    total_s = _median(times)
+    E = g.num_edges
+    # per-relation drop-in path on a sample of relations (evenly spaced), extrapolated by edges
+    counts = torch.bincount(g.edge_type).tolist()
+    sample = rels[:: max(1, len(rels) // 12)]
+    _random.seed(0)
+    t0 = time.perf_counter()
+    for r in sample:
+        sc.score_relation_parallel(d, r, [], 2, "synthetic")
+    torch.cuda.synchronize()
+    per_rel_sample_s = time.perf_counter() - t0
+    per_rel_s = per_rel_sample_s * len(rels) / len(sample)
+    # the all-relation argmax launch alone: 50 calls captured once, replayed between HIP events
+    rd = sc.RelationDictionaries(d.edge_index, d.edge_type, rels, N, dev)
+    K = rd.num_keys
+    w = torch.rand(len(rels) * N, device=dev)
+    lab = d.labels.reshape(-1).to(dev).float()
+    alpha = torch.ones(len(rels), device=dev)
+    bufs = [torch.empty(K, dtype=t, device=dev) for t in (torch.int32, torch.int32, torch.float32, torch.float32,
+                                                           torch.float32)]
+
+    def one():
+        _lib.check(_lib.lib.mpgnn_score_argmax_multi(w.data_ptr(), N, rd.keys_t.data_ptr(), rd.key_ptr_t.data_ptr(),
+                                                     rd.dst_t.data_ptr(), rd.key_rel_t.data_ptr(), K, lab.data_ptr(),
+                                                     alpha.data_ptr(), *(b.data_ptr() for b in bufs),
+                                                     torch.cuda.current_stream(dev).cuda_stream))
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            one()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(50):
+            one()
+    graph.replay()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(4):
+        graph.replay()
+    ev1.record()
+    torch.cuda.synchronize()
+    k_us = ev0.elapsed_time(ev1) * 1e3 / 200
+    alg = E * 8.0 + K * (4 + 8 + 4 + 4 + 20)
+    roofline = {"bound": "hbm", "achieved": round(alg / (k_us * 1e-6) / 1e9, 2), "peak": PEAK_HBM, "unit": "GB/s",
+                "frac": round(alg / (k_us * 1e-6) / 1e9 / PEAK_HBM, 5), "traffic": None,
+                "kernel": "score_multi_argmax_kernel", "avg_launch_us": round(k_us, 3),
+                "algorithmic": "E·(4 dst id + 4 weight) + K·(4 key + 8 ptr + 4 relation + 4 label + 20 outputs)",
+                "timing": "HIP events around 200 launches (4 replays of a HIP graph of 50 calls)"}
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import score_oracle as so
+        with _cpu_threads():
+            ei_c, et_c = g.edge_index, g.edge_type
+            t_cpu, e_cpu = 0.0, 0
+            for r in (rels[0], rels[len(rels) // 2]):
+                mask = torch.unique(ei_c[0][et_c == r]).tolist()
+                ed_o, dd_o = so.create_edge_dictionary(ei_c, et_c, r, mask, d.labels, "synthetic")
+                w_o = so.initialize_weights(N, dd_o, _random.Random(0))
+                m_o = so.Score(w_o, "synthetic", 2)
+                o_o = torch.optim.Adam(m_o.parameters(), lr=0.1)
+                t1 = time.perf_counter()
+                for _ in range(3):
+                    so.train(m_o, o_o, ed_o, N, d.labels, mask, "synthetic")
+                t_cpu += time.perf_counter() - t1
+                e_cpu += 3 * int(counts[r])
+        cpu = {"value": e_cpu / t_cpu, "unit": "edges/s", "cores": usable_cpus()[0], "kind": "port", **host_info(),
+               "sample": f"3 epochs of 2 relations ({e_cpu // 3} edges) through the oracle's reference-style train() "
+                         f"(oracle/score_oracle.py, the per-source Python loop of model.py:82-87); "
+                         f"{t_cpu:.2f} s, extrapolated: the full round (237 relations x 100 epochs) "
+                         f"~{E * epochs / (e_cpu / t_cpu):.0f} s"}
+    losses = [r_[1] for r_ in res]
+    result = {
+        "metric": "score-function edges scored/sec, every relation of one search round (main.py:1309-1330)",
+        "value": round(E * epochs / total_s, 1), "unit": "edges/s", "n_gpus": 1, "steps": epochs, "warmup": 5,
+        "ms_per_step": round(total_s * 1e3 / epochs, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": WORKLOADS[args.workload][1].split(",")[0] + "; 2-class synthetic labels, seeded random weights",
+        "config": {"workload": f"{WORKLOADS[args.workload][0]}: all {len(rels)} relations x {epochs} epochs, "
+                               "first-iteration masks (every source of each relation)", "mode": "score_all",
+                   "graph": {"nodes": N, "edges": E, "relations": len(rels), "keys": K}},
+        "epoch_def": "one train() epoch of main.py:641-673 (non-bag) for EVERY relation: argmax forward, MSE, "
+                     "backward, Adam(lr 0.1), clamp",
+        "round_s": round(total_s, 4),
+        "per_relation_path_s": round(per_rel_s, 3),
+        "per_relation_path_def": f"score_relation_parallel per relation (its own HIP-graph loop), {len(sample)} "
+                                 f"relations timed ({per_rel_sample_s:.3f} s), x {len(rels)}/{len(sample)}",
+        "speedup_vs_per_relation": round(per_rel_s / total_s, 2),
+        "losses_finite": int(sum(1 for v in losses if v == v)),
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(result), flush=True)
+    return result
+
+
 def pmc_traffic(workload, mode, feat, kernel_prefix):
     """HBM bytes per launch of `kernel_prefix` from the committed PMC summary, or None."""
     rows = []
@@ -508,6 +649,8 @@ def main():
         _lib.set_option(20, args.chunk_rows)  # MPGNN_OPT_CHUNK_ROWS (before the plan is built)
     if args.mode == "score":
         return bench_score(args)
+    if args.mode == "score_all":
+        return bench_score_all(args)
     rank, world, local, group = setup_dist(args.gpus)
     sharded = group is not None
     dev = torch.device("cuda", local)

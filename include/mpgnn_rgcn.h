@@ -324,6 +324,29 @@ int32_t mpgnn_score_bag_argmax_bwd(const float* grad_max, int64_t num_bags, cons
                                    const int32_t* in_mem, const int32_t* in_pos, float* grad_weights,
                                    float* grad_lin, void* stream);
 
+/* Every candidate relation of one scoring round at once (main.py:1309-1330 runs
+ * score_relation_parallel per relation, 100 epochs each, split over MPI ranks). The relations'
+ * dictionaries form ONE relation-major CSR: key k = (relation key_rel[k] in [0, R), source keys[k]),
+ * destinations dst[key_ptr[k] .. key_ptr[k+1]) in edge order; weights are row-major [R, num_nodes].
+ * mpgnn_score_argmax_multi, per key: arg_pos / max_node as mpgnn_score_argmax over row key_rel[k],
+ * values[k] = weights[key_rel[k]][max_node[k]] (the prediction of source keys[k]),
+ * grad_values[k] = alpha[key_rel[k]] · (values[k] − labels[keys[k]]) — torch's mse_loss_backward
+ * with alpha_r = fp32(2 / K_r) and grad_output 1 — and sq_err[k] = (values[k] − labels[keys[k]])².
+ * mpgnn_score_loss_multi: loss[r] = Σ sq_err over r's keys rel_key_ptr[r] .. rel_key_ptr[r+1] / K_r
+ * (fixed lane-strided order: torch's mean to fp32 rounding). mpgnn_score_argmax_multi_bwd:
+ * grad_weights[0 .. grad_size) = 0, then for every (relation, destination) pair i the ordered sum
+ * (keys DESCENDING) of grad_values of the keys whose argmax edge is one of the pair's candidates
+ * (in_pos / in_key over pair_ptr[i] .. pair_ptr[i+1]) goes to grad_weights[pair_target[i]]. */
+int32_t mpgnn_score_argmax_multi(const float* weights, int64_t num_nodes, const int32_t* keys, const int32_t* key_ptr,
+                                 const int32_t* dst, const int32_t* key_rel, int64_t num_keys, const float* labels,
+                                 const float* alpha, int32_t* arg_pos, int32_t* max_node, float* values,
+                                 float* grad_values, float* sq_err, void* stream);
+int32_t mpgnn_score_loss_multi(const float* sq_err, const int32_t* rel_key_ptr, int64_t num_rel, float* loss,
+                               void* stream);
+int32_t mpgnn_score_argmax_multi_bwd(const float* grad_values, const int32_t* arg_pos, const int32_t* pair_ptr,
+                                     const int64_t* pair_target, const int32_t* in_pos, const int32_t* in_key,
+                                     int64_t num_pairs, int64_t grad_size, float* grad_weights, void* stream);
+
 /* --- options ----------------------------------------------------------------------------
  * MPGNN_OPT_EXACT_ORDER = 1: every gather-sum adds its entries strictly in the reference's
  * sequential order (no ordered-piece split of long runs). Default 0: runs longer than 32

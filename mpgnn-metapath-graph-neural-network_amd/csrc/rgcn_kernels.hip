@@ -2731,16 +2731,46 @@ __global__ __launch_bounds__(kThreads) void gather_rows_kernel(GatherRowsArgs a)
 
     // ---- prologue: row bounds (lane j < RPW: row row0 + j), counts, extra rows, bias -----
     int my_beg = 0, my_end = 0;
-    {
-        const int i = min(row0 + min(lane, RPW - 1), a.N - 1);
-        int b, e;
-        if (a.row_kind == 1) {
-            b = lower_bound_i32(a.keys, a.kb, a.ke, i);
-            e = lower_bound_i32(a.keys, b, a.ke, i + 1);
-        } else {
-            b = a.ptr[i];
-            e = (a.row_kind == 2 ? a.pe : a.ptr + 1)[i];
+    if (a.row_kind == 1) {
+        // sorted keys[kb, ke): the wave finds lower_bound(row0) by a 64-ary search (one probe per
+        // lane per round: ~3 dependent loads instead of a 17-deep binary search per row), then
+        // the bounds of its RPW rows by ballots over the following keys, 64 at a time
+        int l = a.kb, hgh = a.ke;  // wave-uniform; the answer lies in [l, hgh]
+        while (hgh - l > 64) {
+            const int step = (hgh - l + 63) >> 6;
+            const int pj = l + lane * step;
+            const bool pv = pj < hgh;
+            const unsigned long long ge = __ballot(pv && a.keys[min(pj, hgh - 1)] >= row0);
+            const unsigned long long vm = __ballot(pv);
+            if (ge == 0) {
+                l = l + (63 - __builtin_clzll(vm)) * step + 1;  // past the last valid probe
+            } else {
+                const int js = __builtin_ctzll(ge);
+                hgh = l + js * step;
+                if (js > 0) l = l + (js - 1) * step + 1;
+            }
         }
+        int cntv = 0;  // lane j <= RPW: lower_bound(row0 + j) - base
+        const int base = l;
+        for (int q0 = base; q0 < a.ke; q0 += 64) {
+            const int q = q0 + lane;
+            const int kv = q < a.ke ? a.keys[q] : INT_MAX;
+#pragma unroll
+            for (int j = 0; j <= RPW; ++j) {
+                const int cj = __popcll(__ballot(kv < row0 + j));
+                if (lane == j) cntv += cj;
+            }
+            // done once a key of this chunk reaches past the wave's last row (keys are sorted)
+            if (__ballot(kv >= row0 + RPW) != 0) break;
+        }
+        const int b = base + cntv, e = base + __shfl(cntv, min(lane + 1, 63));
+        const bool valid = lane < RPW && row0 + lane < a.N;
+        my_beg = valid ? b : 0;
+        my_end = valid ? e : 0;
+    } else {
+        const int i = min(row0 + min(lane, RPW - 1), a.N - 1);
+        const int b = a.ptr[i];
+        const int e = (a.row_kind == 2 ? a.pe : a.ptr + 1)[i];
         const bool valid = lane < RPW && row0 + lane < a.N;
         my_beg = valid ? b : 0;
         my_end = valid ? e : 0;

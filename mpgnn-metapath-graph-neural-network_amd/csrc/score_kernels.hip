@@ -276,6 +276,123 @@ __global__ __launch_bounds__(64) void score_bag_lin_kernel(
     if (lane == 0) grad_lin[j] = acc;
 }
 
+// ---------------------------------------------------------------------------------------------
+// All candidate relations of one scoring round at once (main.py:1309-1330 scores every relation
+// with its own score_relation_parallel: 100 epochs each, split over MPI ranks). The dictionaries
+// of every relation are ONE relation-major CSR (key k = a (relation, source) pair, destinations in
+// edge order — the graph plan's segment order); relation r's weights are row r of a [R, N] matrix.
+// Per key: the first argmax (score_argmax_kernel's), the prediction v = w[r][max], and the MSE
+// gradient of the relation's mean loss as torch's mse_loss_backward forms it, alpha_r · (v − y)
+// with alpha_r = fp32(2 / K_r), plus the squared error for the loss.
+// ---------------------------------------------------------------------------------------------
+// 8 lanes per key (dictionaries are short: ~1.5 destinations per key at C3; one wave per key left
+// 63 of 64 lanes idle), a key's first argmax by an 8-lane butterfly with the associative first-max
+// operator of score_argmax_kernel
+constexpr int kMultiLanes = 8;
+__global__ __launch_bounds__(kScoreThreads) void score_multi_argmax_kernel(
+        const float* __restrict__ w, int64_t N, const int32_t* __restrict__ keys, const int32_t* __restrict__ key_ptr,
+        const int32_t* __restrict__ dst, const int32_t* __restrict__ key_rel, int32_t K, const float* __restrict__ labels,
+        const float* __restrict__ alpha, int32_t* __restrict__ arg_pos, int32_t* __restrict__ max_node,
+        float* __restrict__ val, float* __restrict__ dval, float* __restrict__ sq) {
+    const int sl = threadIdx.x & (kMultiLanes - 1);
+    const int32_t k = (int32_t)(((size_t)blockIdx.x * kScoreThreads + threadIdx.x) / kMultiLanes);
+    const bool live = k < K;  // every lane stays for the shuffles
+    const int32_t kk = live ? k : K - 1;
+    const int32_t b = key_ptr[kk], e = live ? key_ptr[kk + 1] : b;
+    const int32_t r = key_rel[kk];
+    const float* wr = w + (size_t)r * (size_t)N;
+    float bv = 0.0f;
+    int32_t bp = INT32_MAX, bn = 0;
+    for (int32_t p = b + sl; p < e; p += kMultiLanes) {
+        const int32_t n = dst[p];
+        const float v = wr[n];
+        if (bp == INT32_MAX || takes_over(bv, v)) {
+            bv = v;
+            bp = p;
+            bn = n;
+        }
+    }
+#pragma unroll
+    for (int m = kMultiLanes / 2; m >= 1; m >>= 1) {
+        const float ov = __shfl_xor(bv, m);
+        const int32_t op = __shfl_xor(bp, m), on = __shfl_xor(bn, m);
+        bool take;
+        if (op == INT32_MAX) take = false;
+        else if (bp == INT32_MAX) take = true;
+        else if (takes_over(bv, ov)) take = true;
+        else if (takes_over(ov, bv)) take = false;
+        else take = op < bp;
+        if (take) {
+            bv = ov;
+            bp = op;
+            bn = on;
+        }
+    }
+    if (live && sl == 0) {
+        const float diff = __fsub_rn(bv, labels[keys[k]]);
+        arg_pos[k] = bp;
+        max_node[k] = bn;
+        val[k] = bv;
+        dval[k] = __fmul_rn(alpha[r], diff);  // alpha * (a - b) * grad_output(1)
+        sq[k] = __fmul_rn(diff, diff);
+    }
+}
+
+// loss[r] = Σ sq over relation r's keys / K_r (one wave per relation, a fixed lane-strided order)
+__global__ __launch_bounds__(kScoreThreads) void score_multi_loss_kernel(const float* __restrict__ sq,
+                                                                         const int32_t* __restrict__ rel_key_ptr,
+                                                                         int32_t R, float* __restrict__ loss) {
+    const int lane = threadIdx.x & 63;
+    const int32_t r = (int32_t)(blockIdx.x * kScoreWaves + (threadIdx.x >> 6));
+    if (r >= R) return;
+    const int32_t b = rel_key_ptr[r], e = rel_key_ptr[r + 1];
+    float acc = 0.0f;
+    for (int32_t k = b + lane; k < e; k += 64) acc += sq[k];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
+    if (lane == 0) loss[r] = e > b ? acc / (float)(e - b) : __builtin_nanf("");
+}
+
+// d weights of every relation: 8 lanes per (relation, destination) pair walk the pair's
+// (edge position, key) candidates, keys DESCENDING, adding the gradients of the keys whose argmax
+// is that edge in list order — score_scatter_kernel's order, per relation
+__global__ __launch_bounds__(kScoreThreads) void score_multi_scatter_kernel(
+        const float* __restrict__ dval, const int32_t* __restrict__ arg_pos, const int32_t* __restrict__ pair_ptr,
+        const int64_t* __restrict__ pair_target, const int32_t* __restrict__ in_pos, const int32_t* __restrict__ in_key,
+        int32_t T, float* __restrict__ grad_w) {
+    const int lane = threadIdx.x & 63;
+    const int sl = lane & (kMultiLanes - 1);
+    const int sub0 = lane & ~(kMultiLanes - 1);  // first lane of this pair's group
+    const int32_t pi = (int32_t)(((size_t)blockIdx.x * kScoreThreads + threadIdx.x) / kMultiLanes);
+    const bool live = pi < T;
+    const int32_t b = live ? pair_ptr[pi] : 0, e = live ? pair_ptr[pi + 1] : 0;
+    // rounds: the group's longest list decides (wave-uniform loop over the maximum)
+    int32_t n_rounds = (e - b + kMultiLanes - 1) / kMultiLanes;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) n_rounds = max(n_rounds, __shfl_xor(n_rounds, m));
+    float acc = 0.0f;
+    bool any = false;
+    for (int32_t rd = 0; rd < n_rounds; ++rd) {
+        const int32_t j = b + rd * kMultiLanes + sl;
+        bool match = false;
+        float g = 0.0f;
+        if (j < e) {
+            const int32_t k = in_key[j];
+            match = arg_pos[k] == in_pos[j];
+            if (match) g = dval[k];
+        }
+        unsigned long long mask = (__ballot(match) >> sub0) & ((1ull << kMultiLanes) - 1);
+        while (mask) {  // per group; the groups of a wave iterate together (uniform trip count below)
+            const int l = __builtin_ctzll(mask);
+            const float gv = __shfl(g, sub0 + l);
+            acc = any ? __fadd_rn(acc, gv) : gv;
+            any = true;
+            mask &= mask - 1;
+        }
+    }
+    if (live && sl == 0) grad_w[pair_target[pi]] = acc;
+}
+
 }  // namespace
 }  // namespace mpgnn
 
@@ -355,4 +472,55 @@ extern "C" int32_t mpgnn_score_bag_argmax_bwd(const float* grad_max, int64_t num
         return hip_status(hipGetLastError(), "score_bag_lin_kernel launch");
     }
     return MPGNN_OK;
+}
+
+extern "C" int32_t mpgnn_score_argmax_multi(const float* weights, int64_t num_nodes, const int32_t* keys,
+                                            const int32_t* key_ptr, const int32_t* dst, const int32_t* key_rel,
+                                            int64_t num_keys, const float* labels, const float* alpha, int32_t* arg_pos,
+                                            int32_t* max_node, float* values, float* grad_values, float* sq_err,
+                                            void* stream) {
+    if (num_nodes < 0 || num_keys < 0 || num_keys >= (int64_t)INT32_MAX)
+        return arg_fail("mpgnn_score_argmax_multi: bad sizes");
+    if (num_keys == 0) return MPGNN_OK;
+    if (!weights || !keys || !key_ptr || !dst || !key_rel || !labels || !alpha || !arg_pos || !max_node || !values ||
+        !grad_values || !sq_err)
+        return arg_fail("mpgnn_score_argmax_multi: NULL argument");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    const int64_t per_block = kScoreThreads / kMultiLanes;
+    const unsigned grid = (unsigned)((num_keys + per_block - 1) / per_block);
+    hipLaunchKernelGGL(score_multi_argmax_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, weights, num_nodes, keys,
+                       key_ptr, dst, key_rel, (int32_t)num_keys, labels, alpha, arg_pos, max_node, values, grad_values,
+                       sq_err);
+    return hip_status(hipGetLastError(), "score_multi_argmax_kernel launch");
+}
+
+extern "C" int32_t mpgnn_score_loss_multi(const float* sq_err, const int32_t* rel_key_ptr, int64_t num_rel, float* loss,
+                                          void* stream) {
+    if (num_rel < 0 || num_rel >= (int64_t)INT32_MAX) return arg_fail("mpgnn_score_loss_multi: bad sizes");
+    if (num_rel == 0) return MPGNN_OK;
+    if (!rel_key_ptr || !loss) return arg_fail("mpgnn_score_loss_multi: NULL argument");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    const unsigned grid = (unsigned)((num_rel + kScoreWaves - 1) / kScoreWaves);
+    hipLaunchKernelGGL(score_multi_loss_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, sq_err, rel_key_ptr,
+                       (int32_t)num_rel, loss);
+    return hip_status(hipGetLastError(), "score_multi_loss_kernel launch");
+}
+
+extern "C" int32_t mpgnn_score_argmax_multi_bwd(const float* grad_values, const int32_t* arg_pos,
+                                                const int32_t* pair_ptr, const int64_t* pair_target,
+                                                const int32_t* in_pos, const int32_t* in_key, int64_t num_pairs,
+                                                int64_t grad_size, float* grad_weights, void* stream) {
+    if (num_pairs < 0 || num_pairs >= (int64_t)INT32_MAX || grad_size < 0)
+        return arg_fail("mpgnn_score_argmax_multi_bwd: bad sizes");
+    if (grad_size == 0) return MPGNN_OK;
+    if (!grad_weights || (num_pairs > 0 && (!grad_values || !arg_pos || !pair_ptr || !pair_target || !in_pos || !in_key)))
+        return arg_fail("mpgnn_score_argmax_multi_bwd: NULL argument");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    int32_t st = hip_status(hipMemsetAsync(grad_weights, 0, (size_t)grad_size * sizeof(float), strm), "memset grad");
+    if (st != MPGNN_OK || num_pairs == 0) return st;
+    const int64_t per_block = kScoreThreads / kMultiLanes;
+    const unsigned grid = (unsigned)((num_pairs + per_block - 1) / per_block);
+    hipLaunchKernelGGL(score_multi_scatter_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, grad_values, arg_pos,
+                       pair_ptr, pair_target, in_pos, in_key, (int32_t)num_pairs, grad_weights);
+    return hip_status(hipGetLastError(), "score_multi_scatter_kernel launch");
 }

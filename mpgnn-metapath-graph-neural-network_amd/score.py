@@ -39,7 +39,7 @@ __all__ = ["EdgeDictionary", "DestinationDictionary", "ArgmaxDict", "build_edge_
            "get_optimizer", "get_loss", "get_loss_per_node", "train", "score_relation_parallel", "EPOCHS",
            "FIRST_MASK_DATASETS", "BagSet", "BagDestinationDictionary", "score_bag_argmax", "create_bags",
            "clean_bags_for_relation_type", "reinitialize_weights", "retrieve_destinations_low_loss",
-           "score_relation_bags_parallel", "BAG_EPOCHS"]
+           "score_relation_bags_parallel", "BAG_EPOCHS", "RelationDictionaries", "score_relations_batched"]
 
 EPOCHS = 100  # main.py:755
 BAG_EPOCHS = 50  # main.py:888
@@ -954,3 +954,204 @@ def score_relation_bags_parallel(data_object, relation, features_dim, dataset, e
         weights = reinitialize_weights(data_object, destination_dictionary, model.input.weights.detach(), frozen,
                                        BAGS=False)
     return relation, current_loss, model, preds, v
+
+
+# ---------------------------------------------------------------------------------------------
+# every candidate relation of one scoring round at once (main.py:1309-1330)
+# ---------------------------------------------------------------------------------------------
+class RelationDictionaries:
+    """The edge dictionaries of SEVERAL relations (each: every source of the relation, sorted —
+    the first-iteration mask of main.py:734-735 — with its destinations in edge order) as one
+    relation-major CSR on the device: key k = (relation index key_rel[k], source keys[k]); the
+    graph plan's segment order. Plus the backward's candidate lists per (relation, destination)
+    pair, keys descending (score_scatter_kernel's order), and per-relation key ranges."""
+
+    def __init__(self, edge_index, edge_type, relations, num_nodes, device):
+        dev = torch.device(device)
+        ei, et = edge_index.to(dev), edge_type.to(dev)
+        N = int(num_nodes)
+        rels = torch.as_tensor([int(r) for r in relations], dtype=torch.int64, device=dev)
+        R = int(rels.numel())
+        self.relations = [int(r) for r in relations]
+        self.num_nodes, self.num_relations = N, R
+        # dense index of each edge's relation among `relations` (-1: not scored)
+        srt, order = torch.sort(rels)
+        pos = torch.searchsorted(srt, et)
+        hit = (pos < R) & (srt[pos.clamp(max=max(R - 1, 0))] == et) if R else torch.zeros_like(et, dtype=torch.bool)
+        dense = torch.where(hit, order[pos.clamp(max=max(R - 1, 0))], torch.full_like(et, -1)) if R else \
+            torch.full_like(et, -1)
+        sel = dense >= 0
+        src, dst, d = ei[0][sel], ei[1][sel], dense[sel]
+        if src.numel() and (int(src.min()) < 0 or int(src.max()) >= N or int(dst.min()) < 0 or int(dst.max()) >= N):
+            raise IndexError(f"index out of range: an edge of a scored relation has a node outside [0, {N})")
+        key = d * N + src
+        o = torch.argsort(key, stable=True)  # (relation, source, edge order)
+        key_s, dst_s = key[o], dst[o]
+        uk, counts = torch.unique_consecutive(key_s, return_counts=True)
+        K = int(uk.numel())
+        i32 = torch.int32
+        self.keys_t = (uk % N).to(i32)
+        self.key_rel_t = (uk // N).to(i32)
+        kp = torch.zeros(K + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(counts, 0, out=kp[1:])
+        self.key_ptr_t = kp.to(i32)
+        self.dst_t = dst_s.to(i32)
+        rk = torch.zeros(R + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(torch.bincount(self.key_rel_t.long(), minlength=R), 0, out=rk[1:])
+        self.rel_key_ptr_t = rk.to(i32)
+        self.rel_key_ptr = rk.cpu().numpy()
+        # backward candidates: every (edge position p, key k) by (relation, destination), k descending
+        k_of_p = torch.repeat_interleave(torch.arange(K, device=dev), counts)
+        rel_p = (uk // N)[k_of_p]
+        target = rel_p * N + dst_s
+        comp_order = torch.argsort(target * max(K, 1) + (K - 1 - k_of_p), stable=True)
+        tgt_s = target[comp_order]
+        ut, tcnt = torch.unique_consecutive(tgt_s, return_counts=True)
+        pp = torch.zeros(int(ut.numel()) + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(tcnt, 0, out=pp[1:])
+        self.pair_ptr_t, self.pair_target_t = pp.to(i32), ut.contiguous()
+        self.in_pos_t, self.in_key_t = comp_order.to(i32), k_of_p[comp_order].to(i32)
+        self._src_host = None
+
+    @property
+    def num_keys(self) -> int:
+        return int(self.keys_t.numel())
+
+    def edge_dictionary(self, r: int) -> EdgeDictionary:
+        """Relation index r's dictionary as the per-relation path builds it (EdgeDictionary)."""
+        b, e = int(self.rel_key_ptr[r]), int(self.rel_key_ptr[r + 1])
+        kp = self.key_ptr_t[b:e + 1].long()
+        keys = self.keys_t[b:e]
+        dst = self.dst_t[int(kp[0]):int(kp[-1])] if e > b else self.dst_t[:0]
+        ed, _ = build_edge_dictionary(torch.stack([torch.repeat_interleave(keys.long(), kp[1:] - kp[:-1]),
+                                                   dst.long()]),
+                                      torch.zeros(dst.numel(), dtype=torch.int64, device=dst.device), 0,
+                                      keys.cpu().tolist(), None, num_nodes=self.num_nodes, device=dst.device)
+        return ed
+
+
+def score_relations_batched(data, relations=None, features_dim=2, dataset="synthetic", epochs: int = EPOCHS,
+                            trace=None):
+    """Every candidate relation of the first metapath-search round (main.py:1309-1330: each
+    relation scored by score_relation_parallel, 100 epochs, the relations split over MPI ranks)
+    as ONE problem on the GPU: per epoch one argmax launch over all relations' dictionaries (the
+    relation-major CSR of ``RelationDictionaries``), the MSE gradient fused into it, one scatter
+    launch for the weights' gradients, ONE fused Adam step over the stacked [R, N] weights and
+    one clamp — the same elementwise arithmetic per relation as R separate trainings (Adam and
+    the clamp are elementwise, the argmax / scatter orders are the per-relation kernels').
+    Sources are all nodes with an edge of the relation (the first-iteration mask); labels are per
+    node (dataset 'synthetic', main.py:654-656). Weights drawn relation by relation from Python's
+    ``random`` and the LinearLayerAttri inits from torch's RNG, in the order a sequential loop of
+    score_relation_parallel calls draws them. Returns [(relation, final loss, EdgeDictionary,
+    DestinationDictionary)] in ``relations`` order, like the per-relation function; ``trace``
+    (a list) receives per epoch (losses [R], argmax node per key) with a host sync each."""
+    if dataset != "synthetic":
+        raise NotImplementedError("score_relations_batched: labels per mask position (datasets other than "
+                                  "'synthetic') differ per relation; score those with score_relation_parallel")
+    dev = data.edge_index.device if data.edge_index.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    if relations is None:
+        relations = torch.unique(data.edge_type).tolist()
+    relations = [int(r) for r in relations]
+    N = int(data.num_nodes)
+    rd = RelationDictionaries(data.edge_index, data.edge_type, relations, N, dev)
+    R = rd.num_relations
+    # initial weights of every relation at once (initialize_weights, main.py:479-497): per
+    # relation, its destinations in first-appearance order over its edges (every source is in the
+    # first-iteration mask), weight = |min(labels of its sources) + U(-0.2, 0.2)| with the draws
+    # taken from Python's ``random`` relation after relation — the stream of a sequential loop
+    ei = data.edge_index.cpu().numpy()
+    et = data.edge_type.cpu().numpy()
+    lab_h = data.labels.reshape(-1).cpu().numpy().astype(np.float64)
+    dense = {r: i for i, r in enumerate(relations)}
+    d_of_e = np.array([dense.get(int(v), -1) for v in np.unique(et)], dtype=np.int64)
+    d_e = d_of_e[np.searchsorted(np.unique(et), et)] if et.size else np.zeros(0, dtype=np.int64)
+    keep = d_e >= 0
+    e_idx = np.flatnonzero(keep)
+    e_idx = e_idx[np.argsort(d_e[e_idx], kind="stable")]  # relation-major, file order inside
+    comp = d_e[e_idx] * N + ei[1][e_idx]
+    uniq, first = np.unique(comp, return_index=True)
+    order = np.argsort(first, kind="stable")
+    pair = uniq[order]                                     # (relation, destination), dictionary order
+    srt = np.argsort(comp, kind="stable")
+    starts = np.flatnonzero(np.r_[True, comp[srt][1:] != comp[srt][:-1]]) if comp.size else np.zeros(0, np.int64)
+    mins = (np.minimum.reduceat(lab_h[ei[0][e_idx][srt]], starts) if comp.size else np.zeros(0))[order]
+    draws = np.array([random.uniform(-0.2, 0.2) for _ in range(pair.size)], dtype=np.float64)
+    W0 = torch.zeros(R * N)
+    if pair.size:
+        W0[torch.from_numpy(pair)] = torch.from_numpy(np.abs(mins + draws)).float()
+    for _ in range(R):  # get_model's LinearLayerAttri init per relation (main.py:518-519): torch's RNG stream
+        nn.Linear(features_dim, 1, bias=False)
+    weights = nn.Parameter(W0.to(dev))
+    counts = torch.from_numpy(np.diff(rd.rel_key_ptr)).to(torch.float64)
+    alpha = (2.0 / counts.clamp(min=1)).to(torch.float32).to(dev)  # torch's mse norm, 2 / numel, as fp32
+    labels = data.labels.reshape(-1).to(dev).to(torch.float32)
+    K = rd.num_keys
+    i32 = torch.int32
+    arg_pos = torch.empty(K, dtype=i32, device=dev)
+    max_node = torch.empty(K, dtype=i32, device=dev)
+    val = torch.empty(K, dtype=torch.float32, device=dev)
+    dval = torch.empty(K, dtype=torch.float32, device=dev)
+    sq = torch.empty(K, dtype=torch.float32, device=dev)
+    loss = torch.empty(R, dtype=torch.float32, device=dev)
+    grad = torch.zeros(R * N, dtype=torch.float32, device=dev)
+    use_graph = os.environ.get("MPGNN_LOOP_GRAPH", "1") != "0" and trace is None
+    # capturable in both modes: the step count on the device, the bias corrections formed there —
+    # the arithmetic of score_relation_parallel's graph-replayed Adam
+    opt = torch.optim.Adam([weights], lr=0.1, fused=True, capturable=True)
+
+    def epoch():
+        check(lib.mpgnn_score_argmax_multi(weights.data_ptr(), N, _ptr(rd.keys_t), _ptr(rd.key_ptr_t), _ptr(rd.dst_t),
+                                           _ptr(rd.key_rel_t), K, labels.data_ptr(), alpha.data_ptr(), _ptr(arg_pos),
+                                           _ptr(max_node), _ptr(val), _ptr(dval), _ptr(sq), _stream(dev)),
+              "mpgnn_score_argmax_multi")
+        check(lib.mpgnn_score_loss_multi(_ptr(sq), rd.rel_key_ptr_t.data_ptr(), R, loss.data_ptr(), _stream(dev)),
+              "mpgnn_score_loss_multi")
+        check(lib.mpgnn_score_argmax_multi_bwd(_ptr(dval), _ptr(arg_pos), _ptr(rd.pair_ptr_t), _ptr(rd.pair_target_t),
+                                               _ptr(rd.in_pos_t), _ptr(rd.in_key_t), int(rd.pair_target_t.numel()),
+                                               R * N, grad.data_ptr(), _stream(dev)), "mpgnn_score_argmax_multi_bwd")
+        weights.grad = grad
+        opt.step()
+        with torch.no_grad():
+            weights.clamp_(min=0.0, max=1.0)   # main.py:667-669 (LinearLayerAttri: clamp of its init)
+        return loss
+
+    from .main import _epochs
+    out = None
+    for _, out in _epochs(epoch, epochs, use_graph):
+        if trace is not None:
+            trace.append((out.cpu().numpy().copy(), max_node.cpu().numpy().copy()))
+    final = out.cpu().tolist() if out is not None else [float("nan")] * R
+
+    def dest_dict(rel, ri):
+        b, e = int(rd.rel_key_ptr[ri]), int(rd.rel_key_ptr[ri + 1])
+        return build_edge_dictionary(data.edge_index, data.edge_type, rel, rd.keys_t[b:e].cpu().tolist(), data.labels,
+                                     dataset, num_nodes=N, device=dev)[1]
+    return [(rel, final[ri], _LazyMapping(lambda ri=ri: rd.edge_dictionary(ri)),
+             _LazyMapping(lambda rel=rel, ri=ri: dest_dict(rel, ri))) for ri, rel in enumerate(relations)]
+
+
+class _LazyMapping(Mapping):
+    """A dictionary built on first use (the round's per-relation dictionaries are read only for
+    the relations the search keeps)."""
+
+    def __init__(self, factory):
+        self._factory, self._obj = factory, None
+
+    def get_object(self):
+        if self._obj is None:
+            self._obj = self._factory()
+        return self._obj
+
+    def __getitem__(self, k):
+        return self.get_object()[k]
+
+    def __iter__(self):
+        return iter(self.get_object())
+
+    def __len__(self):
+        return len(self.get_object())
+
+    def __getattr__(self, name):  # EdgeDictionary attributes (dst_t, keys_t, ...)
+        if name.startswith("_"):
+            raise AttributeError(name)
+        return getattr(self.get_object(), name)

@@ -305,21 +305,42 @@ def test_mpnetm_eval_logits_match_reference_golden():
     rel_close(logits, t(g["logits"]), what="logits", ref64=ref64)
 
 
-@pytest.mark.parametrize("name", ["C1", "fb15k237"])
-def test_net_forward_backward_vs_oracle(name):
+@pytest.mark.parametrize("name,hidden,classes", [("C1", 64, 5), ("fb15k237", 64, 5), ("fb15k237", 128, 2)])
+def test_net_forward_backward_vs_oracle(name, hidden, classes, monkeypatch):
+    """Net (model.py:132-149) forward + every parameter gradient against the oracle's net_forward.
+    ("fb15k237", 128, 2) is the bench's headline model, Net(128, 128, 237, 128, 2, 3): its shared
+    conv2 takes the GradStash path (the later uses' gradients summed inside the backward kernels
+    by mpgnn_rgcn_bwd_accumulate, F = 128 only) — the test asserts that path ran."""
     g = data.config_graph(name)
     F = g.x.shape[1]
     torch.manual_seed(10)                                   # main_rgcn.py:31
-    net = mpgnn_amd.Net(F, 64, g.num_relations, 64, 5, 3)
+    net = mpgnn_amd.Net(F, hidden, g.num_relations, hidden, classes, 3)
     sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
-    gout = torch.randn(g.num_nodes, 5, generator=torch.Generator().manual_seed(3))
+    gout = torch.randn(g.num_nodes, classes, generator=torch.Generator().manual_seed(3))
     net = net.to(DEV)
+    import mpgnn_amd.functional as fnl
+    from mpgnn_amd import _lib
+    calls = {"acc": 0}
+
+    class _Count:
+        def __getattr__(self, k):
+            f = getattr(_lib.lib, k)
+            if k != "mpgnn_rgcn_bwd_accumulate":
+                return f
+
+            def wrapped(*a):
+                calls["acc"] += 1
+                return f(*a)
+            return wrapped
+    monkeypatch.setattr(fnl, "lib", _Count())
     acts = []  # the three fused-ReLU layer outputs, in call order
     hooks = [m.register_forward_hook(lambda _m, _i, o: acts.append(o.detach())) for m in (net.conv1, net.conv2)]
     out = net(g.x.to(DEV), g.edge_index.to(DEV), g.edge_type.to(DEV))
     for h in hooks:
         h.remove()
     out.backward(gout.to(DEV))
+    if hidden == 128:
+        assert calls["acc"] == 1, calls  # conv2's second use (backward order) accumulated in-kernel
     act = kink_act(acts)
     res = {}
     for dt in (torch.float32, torch.float64):
@@ -674,16 +695,20 @@ def test_fast_rgcn_conv_matches_per_edge_oracle(f_in, f_out):
     ref = {}
     for dt in (torch.float32, torch.float64):
         xs = g.x.detach().to(dt, copy=True).requires_grad_(True)
-        o = orc.fast_rgcn_forward(xs, g.edge_index, g.edge_type, conv.weight.detach().to(dt),
-                                  conv.root.detach().to(dt), conv.bias.detach().to(dt))
+        ps = [p.detach().to(dt, copy=True).requires_grad_(True) for p in (conv.weight, conv.root, conv.bias)]
+        o = orc.fast_rgcn_forward(xs, g.edge_index, g.edge_type, *ps)
         o.backward(gout.to(dt))
-        ref[dt] = (o.detach(), xs.grad)
+        ref[dt] = (o.detach(), xs.grad, [p.grad for p in ps])
     convg = conv.to(DEV)
     xg = g.x.to(DEV).requires_grad_(True)
     out = convg(xg, g.edge_index.to(DEV), g.edge_type.to(DEV))
     rel_close(out, ref[torch.float32][0], what="fast out", ref64=ref[torch.float64][0])
     out.backward(gout.to(DEV))
     rel_close(xg.grad, ref[torch.float32][1], what="fast dx", ref64=ref[torch.float64][1])
+    # dW (per-edge transform x_j @ W[edge_type], scaled, scattered: mp_rgcn_layer.py:344-357), droot, dbias
+    for name, p, r32, r64 in zip(("dW", "droot", "dbias"), (convg.weight, convg.root, convg.bias),
+                                 ref[torch.float32][2], ref[torch.float64][2]):
+        rel_close(p.grad, r32, what=f"fast {name}", ref64=r64)
 
 
 # ------------------------------------------------------------------------------------------

@@ -259,3 +259,88 @@ def test_score_training_tracks_reference(golden, tag, dataset):
         assert r == rel and final == pytest.approx(float(g[f"{tag}_srp_loss"]), rel=1e-5, abs=1e-7)
         finals.append(final)
     assert finals[0] == finals[1], finals
+
+
+# ------------------------------------------------------------------------------------------
+# every relation of a scoring round at once (main.py:1309-1330) vs the per-relation path
+# ------------------------------------------------------------------------------------------
+def _per_relation_trace(d, rel, features_dim, epochs):
+    """score_relation_parallel's epochs (capturable fused Adam, as its graph-replayed loop),
+    eagerly, recording the loss and the argmax node of every source per epoch."""
+    from mpgnn_amd import score as sc
+    src = d.edge_index[0][d.edge_type == rel]
+    mask = torch.unique(src).tolist()
+    ed, dd = sc.create_edge_dictionary(d, rel, mask, BAGS=False, dataset="synthetic")
+    w0 = sc.initialize_weights(d, dd, BAGS=False)
+    model = sc.get_model(w0, features_dim).to(DEV)
+    opt = torch.optim.Adam(list(model.parameters()), lr=0.1, fused=True, capturable=True)
+    crit, crit_node = sc.get_loss(), sc.get_loss_per_node()
+    out = []
+    for _ in range(epochs):
+        loss, best, _, _, _ = sc.train(d, ed, model, opt, crit, mask, crit_node, [], w0, torch.tensor(0), BAGS=False,
+                                       dataset="synthetic")
+        out.append((loss.item(), best.values_tensor().cpu().numpy().copy()))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", ["kat", "c3"])
+def test_batched_relation_scoring_equals_per_relation_path(golden, graph):
+    """score_relations_batched (one argmax / scatter / Adam / clamp launch per epoch for ALL
+    relations) against the per-relation path run relation by relation from the same random
+    streams: the argmax of every source of every relation identical at every epoch, per-relation
+    losses within 1e-6 (the batched loss sums in a fixed lane order, torch's mean in its own),
+    final losses and dictionaries as score_relation_parallel returns them."""
+    from mpgnn_amd import data as mdata
+    from mpgnn_amd import score as sc
+
+    class D:
+        pass
+    d = D()
+    if graph == "kat":
+        z = golden("kat_synthetic.npz")
+        link, node, label = z["L3_link"], z["L3_node"], z["L3_label"]
+        d.edge_index = torch.from_numpy(np.stack([link[:, 0], link[:, 2]])).to(DEV)
+        d.edge_type = torch.from_numpy(link[:, 1].copy()).to(DEV)
+        d.x = torch.from_numpy(node[:, 1:].astype(np.float32))
+        lab = torch.zeros(node.shape[0], dtype=torch.int64)
+        lab[torch.from_numpy(label[:, 0])] = torch.from_numpy(label[:, 1])
+        rels, epochs = [0, 1, 2, 3], 100
+    else:
+        g = mdata.fb15k237_graph(feat_dim=2, seed=0, recipe="survey")
+        d.edge_index, d.edge_type, d.x = g.edge_index.to(DEV), g.edge_type.to(DEV), g.x
+        lab = torch.randint(0, 2, (g.num_nodes,), generator=torch.Generator().manual_seed(0))
+        rels, epochs = [0, 5, 17, 41, 190, 236, 300], 40  # 300: absent from the graph
+    d.num_nodes = d.x.size(0)
+    d.labels = lab.unsqueeze(-1)
+    random.seed(11)
+    torch.manual_seed(12)
+    trace_b = []
+    res = sc.score_relations_batched(d, rels, 2, "synthetic", epochs=epochs, trace=trace_b)
+    random.seed(11)
+    torch.manual_seed(12)
+    rd = sc.RelationDictionaries(d.edge_index, d.edge_type, rels, d.num_nodes, DEV)
+    for ri, rel in enumerate(rels):
+        b, e = int(rd.rel_key_ptr[ri]), int(rd.rel_key_ptr[ri + 1])
+        if e == b:  # absent relation: nothing to score (the reference's loss over an empty mask is NaN)
+            assert np.isnan(res[ri][1]) and len(res[ri][2]) == 0
+            continue
+        ref = _per_relation_trace(d, rel, 2, epochs)
+        kb = int(rd.rel_key_ptr[ri])
+        kp = rd.key_ptr_t.cpu().numpy()
+        for ep, (l_ref, am_ref) in enumerate(ref):
+            l_b, mn_b = trace_b[ep]
+            assert np.array_equal(mn_b[kb:kb + am_ref.size], am_ref), (graph, rel, ep)
+            assert abs(float(l_b[ri]) - l_ref) <= 1e-6 * max(abs(l_ref), 1e-12) + 1e-9, (graph, rel, ep, l_b[ri], l_ref)
+        r_, loss_, ed_, dd_ = res[ri]
+        assert r_ == rel and abs(loss_ - ref[-1][0]) <= 1e-6 * abs(ref[-1][0]) + 1e-9
+        src = d.edge_index[0][d.edge_type == rel]
+        ed_ref, dd_ref = sc.create_edge_dictionary(d, rel, torch.unique(src).tolist(), BAGS=False, dataset="synthetic")
+        assert list(ed_) == list(ed_ref) and ed_.dst_t.cpu().tolist() == ed_ref.dst_t.cpu().tolist()
+        assert list(dd_) == list(dd_ref)
+    # the default, graph-replayed run returns the same final losses
+    random.seed(11)
+    torch.manual_seed(12)
+    res2 = sc.score_relations_batched(d, rels, 2, "synthetic", epochs=epochs)
+    for a_, b_ in zip(res, res2):
+        assert a_[0] == b_[0] and (a_[1] == b_[1] or (np.isnan(a_[1]) and np.isnan(b_[1])))
