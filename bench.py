@@ -81,7 +81,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="fb15k237", choices=list(WORKLOADS))
-    ap.add_argument("--mode", default="all", choices=["all", "single", "score", "score_all"],
+    ap.add_argument("--mode", default="all", choices=["all", "single", "score", "score_all", "score_bags"],
                     help="all = RGCN Net (mode B, main_rgcn.py); single = MPNetm metapath chain (mode A, main.py); "
                          "score = the metapath score function (model.py:26-125, main.py:727-760); score_all = every "
                          "relation of the first search round at once (main.py:1309-1330, score_relations_batched)")
@@ -626,6 +626,136 @@ def bench_score_all(args):
     return result
 
 
+def bench_score_bags(args):
+    """Mode score_bags (the bag branch): score_relation_bags_parallel (main.py:853-917)
+    — restarts of 50 train(BAGS=True) epochs (model.py:45-72: per bag, per member source, the
+    first argmax of weights · LinearLayerAttri(feat), the strict-max pick) until two restarts fail
+    to lower the loss — for the candidate relation, on bags made by create_bags (main.py:545-575)
+    from a first non-bag scoring of the largest relation. One STEP = one train() epoch. value =
+    edges scored per second = Σ over the bags' member sources of their destination counts ·
+    epochs / time. roofline: mpgnn_score_bag_argmax per launch (HIP events around 50 graph-
+    captured calls) against HBM with its algorithmic bytes. cpu_baseline: the oracle's per-bag
+    Python loop (oracle/score_oracle.py train_bags) on 3 epochs."""
+    import random as _random
+    from mpgnn_amd import score as sc
+    rank, world, local, group = setup_dist(args.gpus)
+    if world > 1:
+        raise SystemExit("--mode score_bags shards nothing (candidate relations are replicas)")
+    dev = torch.device("cuda", local)
+    g = data.fb15k237_graph(feat_dim=2, seed=0, recipe="survey") if args.workload.startswith("fb15k237") \
+        else data.config_graph(args.workload)
+    N = g.num_nodes
+    counts = torch.bincount(g.edge_type, minlength=g.num_relations)
+    order = torch.argsort(counts, descending=True, stable=True).tolist()
+    rel0 = order[0]
+
+    class D:
+        pass
+    d = D()
+    gen = torch.Generator().manual_seed(0)
+    d.x = torch.nn.functional.one_hot(torch.randint(0, 2, (N,), generator=gen), 2).float()  # colour features
+    d.edge_index, d.edge_type, d.num_nodes = g.edge_index.to(dev), g.edge_type.to(dev), N
+    d.labels = torch.randint(0, 2, (N, 1), generator=gen)
+    mask = torch.unique(g.edge_index[0][g.edge_type == rel0]).tolist()
+    ed0, dd0 = sc.create_edge_dictionary(d, rel0, mask, BAGS=False, dataset="synthetic")
+    sc.create_bags(ed0, dd0, d)
+    # the candidate: the relation whose edges start from the most bag members
+    members = torch.tensor(sorted({n for b in d.bags for n in b}))
+    src_in = torch.isin(g.edge_index[0], members)
+    rel = int(torch.argmax(torch.bincount(g.edge_type[src_in], minlength=g.num_relations)))
+    trace = []
+    _random.seed(0)
+    torch.manual_seed(5)
+    sc.score_relation_bags_parallel(d, rel, 2, "synthetic", trace=trace)  # warm-up + epoch count
+    n_epochs = len(trace)
+    times = []
+    for _ in range(max(1, min(args.steps, 3))):
+        _random.seed(0)
+        torch.manual_seed(5)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r_, cur, model, preds, v = sc.score_relation_bags_parallel(d, rel, 2, "synthetic")
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    run_s = _median(times)
+    # the bags / dictionary the epochs ran on, and the edges one epoch reads
+    mask_b = list(dict.fromkeys(n for b in d.bags for n in b))
+    edb, _ = sc.create_edge_dictionary(d, rel, mask_b, BAGS=True, dataset="synthetic")
+    cb, cl = sc.clean_bags_for_relation_type(d, edb)
+    bs = sc.BagSet(cb, edb)
+    kp = edb.key_ptr_t.long()
+    mk = bs.mem_key.long()
+    deg = torch.where(mk >= 0, kp[mk.clamp(min=0) + 1] - kp[mk.clamp(min=0)], torch.zeros_like(mk))
+    edges_epoch = int(deg.sum())
+    w = torch.rand(N, 1, device=dev)
+    lin = torch.rand(1, 2, device=dev)
+    feat = d.x.to(dev)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side), torch.no_grad():
+        for _ in range(3):
+            sc.score_bag_argmax(w, lin, feat, bs)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph), torch.no_grad():
+        for _ in range(50):
+            sc.score_bag_argmax(w, lin, feat, bs)
+    graph.replay()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(4):
+        graph.replay()
+    ev1.record()
+    torch.cuda.synchronize()
+    k_us = ev0.elapsed_time(ev1) * 1e3 / 200
+    B, M = bs.num_bags, bs.num_members
+    alg = edges_epoch * 8.0 + M * (4 + 4 + 8 + 8 + 16) + B * (8 + 12)
+    roofline = {"bound": "hbm", "achieved": round(alg / (k_us * 1e-6) / 1e9, 2), "peak": PEAK_HBM, "unit": "GB/s",
+                "frac": round(alg / (k_us * 1e-6) / 1e9 / PEAK_HBM, 5), "traffic": None,
+                "kernel": "score_bag_argmax_kernel (+ its output allocations)", "avg_launch_us": round(k_us, 3),
+                "algorithmic": "edges·(4 dst + 4 weight) + M·(node, key, key_ptr, feature row, 4 outputs) + B·(ptr, "
+                               "3 outputs)",
+                "timing": "HIP events around 200 calls (4 replays of a HIP graph of 50)",
+                "note": "small launch (B bags, M members): bound by launch latency and the bag-serial member walk"}
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import score_oracle as so
+        with _cpu_threads():
+            ed_o, dd_o = so.create_edge_dictionary_bags(g.edge_index, g.edge_type, rel, mask_b, d.bags, d.bag_labels)
+            cb_o, cl_o = so.clean_bags_for_relation_type(d.bags, d.bag_labels, ed_o)
+            torch.manual_seed(5)
+            m_o = so.Score(so.initialize_weights(N, dd_o, _random.Random(0)), "synthetic", 2)
+            o_o = torch.optim.Adam(m_o.parameters(), lr=0.1)
+            gm = torch.ones(N, 1)
+            t1 = time.perf_counter()
+            for _ in range(3):
+                so.train_bags(m_o, o_o, ed_o, cb_o, cl_o, d.x, [], None, gm)
+            t_cpu = (time.perf_counter() - t1) / 3
+        cpu = {"value": edges_epoch / t_cpu, "unit": "edges/s", "cores": usable_cpus()[0], "kind": "port",
+               **host_info(),
+               "sample": f"3 epochs of train(BAGS=True) through the oracle (oracle/score_oracle.py train_bags: the "
+                         f"per-bag, per-source Python loop of model.py:56-70 + autograd), relation {rel}: "
+                         f"{t_cpu * 1e3:.1f} ms per epoch"}
+    result = {
+        "metric": "bag score edges scored/sec (score_relation_bags_parallel, main.py:853-917)",
+        "value": round(edges_epoch * n_epochs / run_s, 1), "unit": "edges/s", "n_gpus": 1, "steps": n_epochs,
+        "warmup": n_epochs, "ms_per_step": round(run_s * 1e3 / n_epochs, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": WORKLOADS[args.workload][1].split(",")[0] + "; one-hot 2-colour features, 2-class synthetic labels",
+        "config": {"workload": f"{WORKLOADS[args.workload][0]}: bags from create_bags over relation {rel0}'s "
+                               f"dictionaries, candidate relation {rel}", "mode": "score_bags",
+                   "bags": B, "members": M, "edges_per_epoch": edges_epoch, "epochs_run": n_epochs,
+                   "restarts": n_epochs // 50},
+        "epoch_def": "one train(BAGS=True) of main.py:641-673: bag-pick forward, MSE, backward, grad mask, "
+                     "Adam(lr 0.1), clamps",
+        "run_s": round(run_s, 4), "current_loss": cur, "v": bool(v),
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(result), flush=True)
+    return result
+
+
 def pmc_traffic(workload, mode, feat, kernel_prefix):
     """HBM bytes per launch of `kernel_prefix` from the committed PMC summary, or None."""
     rows = []
@@ -651,6 +781,8 @@ def main():
         return bench_score(args)
     if args.mode == "score_all":
         return bench_score_all(args)
+    if args.mode == "score_bags":
+        return bench_score_bags(args)
     rank, world, local, group = setup_dist(args.gpus)
     sharded = group is not None
     dev = torch.device("cuda", local)
