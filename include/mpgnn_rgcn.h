@@ -369,9 +369,11 @@ enum mpgnn_option {
                                     matrix cores with each fp32 operand split exactly into three bf16 pieces (six
                                     products, fp32 accumulation: fp32-level accuracy at 2.67x the fp32-MFMA rate);
                                     0: the fp32-MFMA kernel (v_mfma_f32_32x32x2_f32) */
-    MPGNN_OPT_BWD_FUSED = 25     /* 1 (default): mpgnn_rgcn_bwd at F_in = F_out = 128 (bf16-split GEMMs) runs
+    MPGNN_OPT_BWD_FUSED = 25,    /* 1 (default): mpgnn_rgcn_bwd at F_in = F_out = 128 (bf16-split GEMMs) runs
                                     dgrad and dW / droot / dbias in one launch that gathers dout once;
                                     0: the dgrad launch + the chunked dW launch */
+    MPGNN_OPT_FLAT_WG_PER_CU = 26 /* gather-sum lists (means, combine, grad_x): 0 = one workgroup per list group;
+                                    k > 0 = a persistent grid of k workgroups per CU walking the groups */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

@@ -2521,9 +2521,6 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds_pieces[];  // [max_pieces][F] (long groups)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int g = a.g_lo + (int)blockIdx.x;
-    const int c0 = ld_uniform(a.group_ptr, g), c1 = ld_uniform(a.group_ptr, g + 1);
-    const bool lng = ld_uniform(a.group_long, g) != 0;
     const int F = a.F;
     int colc[T];
 #pragma unroll
@@ -2536,30 +2533,39 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
 #pragma unroll
         for (int k = 0; k < V; ++k) bb[t][k] = has_b ? bb[t][k] : 0.0f;
     }
-    if (!lng) {
-        const int c = c0 + wave;
-        if (c < c1) flat_chunk<V, T, U>(a, c, lane, a.carry, bb);
-        return;
-    }
-    // a long row's pieces (the same 16 loads in flight as a normal chunk: more would raise the
-    // kernel's register count and cost every group occupancy)
-    for (int c = c0 + wave; c < c1; c += kWaves) flat_chunk<V, T, U>(a, c, lane, lds_pieces, bb);
-    __syncthreads();
-    if (wave != 0) return;
-    const int rr = a.row_of[ld_uniform(a.chunk_ptr, c0)];
-    float acc[T][V];
-    zero_acc<V, T>(acc);
-    for (int k = 0; k < c1 - c0; ++k) {  // pieces in order
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-            float v[V];
-            vload<V>(lds_pieces + (size_t)k * F + colc[t], v);
-#pragma unroll
-            for (int q = 0; q < V; ++q) acc[t][q] += v[q];
+    // persistent over groups (grid-stride): the waves stay resident instead of a short-lived
+    // workgroup per group; every wave of a workgroup walks the same groups, so the long groups'
+    // barriers line up
+    for (int g = a.g_lo + (int)blockIdx.x; g < a.g_hi; g += (int)gridDim.x) {
+        const int c0 = ld_uniform(a.group_ptr, g), c1 = ld_uniform(a.group_ptr, g + 1);
+        const bool lng = ld_uniform(a.group_long, g) != 0;
+        if (!lng) {
+            const int c = c0 + wave;
+            if (c < c1) flat_chunk<V, T, U>(a, c, lane, a.carry, bb);
+            continue;
         }
+        // a long row's pieces (the same 16 loads in flight as a normal chunk: more would raise
+        // the kernel's register count and cost every group occupancy)
+        for (int c = c0 + wave; c < c1; c += kWaves) flat_chunk<V, T, U>(a, c, lane, lds_pieces, bb);
+        __syncthreads();
+        if (wave == 0) {
+            const int rr = a.row_of[ld_uniform(a.chunk_ptr, c0)];
+            float acc[T][V];
+            zero_acc<V, T>(acc);
+            for (int k = 0; k < c1 - c0; ++k) {  // pieces in order
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    float v[V];
+                    vload<V>(lds_pieces + (size_t)k * F + colc[t], v);
+#pragma unroll
+                    for (int q = 0; q < V; ++q) acc[t][q] += v[q];
+                }
+            }
+            const bool has_cnt = a.cnt != nullptr;
+            flat_finish_store<V, T>(a, rr, has_cnt ? (float)a.cnt[rr] : 1.0f, has_cnt, bb, acc, lane);
+        }
+        __syncthreads();  // the LDS piece slots are free for the next long group
     }
-    const bool has_cnt = a.cnt != nullptr;
-    flat_finish_store<V, T>(a, rr, has_cnt ? (float)a.cnt[rr] : 1.0f, has_cnt, bb, acc, lane);
 }
 
 // finalize_rows_kernel — one wave per row.
@@ -2928,6 +2934,11 @@ struct OuterArgs {
     float* Pb;               // nullable: [nchunks][Nn] column sums of B (bias grad)
     float* dst_b;            // direct bias destination when dst_mode == 3
     int bias_of_a;           // outer_bf3_kernel root chunks: Pb = column sums of A instead (M == 128)
+    // outer_bf3_kernel on one 128 × 128 quadrant of wider matrices (0 = the 128-wide defaults):
+    // A / B row strides and first columns, D / P row stride, the quadrant's element offset in a
+    // D / P matrix, elements per P slab, per Pb row
+    int lda, ldb, a_col0, b_col0, ldd, d_off, pb_stride;
+    int64_t p_stride;
 };
 
 constexpr int kOuterLd = 288;                        // one row pair: 128 + 32 pad + 128
@@ -3437,12 +3448,16 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
         const int *a_idx, *b_idx;
         int a_off, a2_off;
     };
+    // quadrant geometry (the same for both chunk streams; 0 = the 128-wide defaults)
+    const int lda = ra.lda ? ra.lda : 128, ldb = ra.ldb ? ra.ldb : 128, ldd = ra.ldd ? ra.ldd : 128;
+    const int pb_stride = ra.pb_stride ? ra.pb_stride : 128;
+    const int64_t p_stride = ra.p_stride ? ra.p_stride : 128 * 128;
     auto src_of = [&](int chunk) {
         const bool r = chunk < ra_n;
         Src x;
-        x.A = r ? ra.A : wa.A;
-        x.A2 = r ? ra.A2 : wa.A2;
-        x.B = r ? ra.B : wa.B;
+        x.A = (r ? ra.A : wa.A) + ra.a_col0;
+        x.A2 = (r ? ra.A2 : wa.A2) + ra.a_col0;
+        x.B = (r ? ra.B : wa.B) + ra.b_col0;
         x.a_idx = r ? ra.a_idx : wa.a_idx;
         x.b_idx = r ? ra.b_idx : wa.b_idx;
         x.a_off = r ? ra.a_off : wa.a_off;
@@ -3490,9 +3505,9 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
         for (int j = 0; j < 8; ++j) {
             const int ra_ = __builtin_amdgcn_readlane(ia, j);
             const int rb_ = __builtin_amdgcn_readlane(ib, j);
-            const float* arow = ra_ >= 0 ? a.A + (size_t)ra_ * 128 : a.A2 + (size_t)(-ra_ - 1 - a.a2_off) * 128;
+            const float* arow = ra_ >= 0 ? a.A + (size_t)ra_ * lda : a.A2 + (size_t)(-ra_ - 1 - a.a2_off) * lda;
             va[j] = arow[col];
-            vb[j] = a.B[(size_t)rb_ * 128 + col];
+            vb[j] = a.B[(size_t)rb_ * ldb + col];
         }
     };
     // split + transposed store of one staged slice; rows past the chunk's end are zeros
@@ -3590,18 +3605,18 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
             float* Db = nullptr;
             if (is_root) {
                 const int cidx = cur.chunk;
-                D = ra.P + (size_t)cidx * 128 * 128;
-                Db = ra.Pb != nullptr ? ra.Pb + (size_t)cidx * 128 : nullptr;
+                D = ra.P + (size_t)cidx * p_stride + ra.d_off;
+                Db = ra.Pb != nullptr ? ra.Pb + (size_t)cidx * pb_stride + ra.b_col0 : nullptr;
                 if (ra.dst_mode == 3) {
-                    D = ra.dst;
-                    Db = ra.dst_b;
+                    D = ra.dst != nullptr ? ra.dst + ra.d_off : nullptr;
+                    Db = ra.dst_b != nullptr ? ra.dst_b + ra.b_col0 : nullptr;
                 }
             } else {
                 const int cidx = cur.chunk - ra_n;
-                D = wa.P + (size_t)cidx * 128 * 128;
+                D = wa.P + (size_t)cidx * p_stride + ra.d_off;
                 if (wa.dst_mode == 1 || wa.dst_mode == 2) {
                     const int di = ld_uniform(wa.chunk_dst, cidx + wa.chunk_off);
-                    if (di >= 0) D = wa.dst + (size_t)(wa.dst_mode == 1 ? di : 0) * 128 * 128;
+                    if (di >= 0) D = wa.dst + (size_t)(wa.dst_mode == 1 ? di : 0) * p_stride + ra.d_off;
                 }
             }
             const int ln = opaque(lane);
@@ -3614,7 +3629,7 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int m = q * 32 + (r & 3) + 8 * (r >> 2) + h4;
-                        Dc[(size_t)m * 128] = hi[q][r] + lo[q][r];
+                        Dc[(size_t)m * ldd] = hi[q][r] + lo[q][r];
                     }
             }
 #pragma unroll
@@ -4758,9 +4773,11 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
     return hip_check(hipGetLastError(), "row_sum_kernel launch");
 }
 
+static int g_flat_wg_per_cu = 0;  // MPGNN_OPT_FLAT_WG_PER_CU: persistent grid of flat_rows_kernel (0: a workgroup per group)
 template <int V, int T>
 static void launch_flat(const FlatArgs& a, int max_pieces, hipStream_t st) {
-    const int n = a.g_hi - a.g_lo;
+    const int n_groups = a.g_hi - a.g_lo;
+    const int n = g_flat_wg_per_cu > 0 ? std::min(n_groups, cu_count() * g_flat_wg_per_cu) : n_groups;
     const size_t lds = (size_t)max_pieces * a.F * sizeof(float);  // 0 when the list has no long row
     hipLaunchKernelGGL((flat_rows_kernel<V, T>), dim3(n), dim3(kThreads), lds, st, a);
 }
@@ -5209,6 +5226,10 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
             g_bwd_fused = value != 0;
             return MPGNN_OK;
 
+        case MPGNN_OPT_FLAT_WG_PER_CU:
+            if (value < 0 || value > 64) return arg_error("MPGNN_OPT_FLAT_WG_PER_CU must be 0..64");
+            g_flat_wg_per_cu = (int)value;
+            return MPGNN_OK;
         case MPGNN_OPT_CHUNK_ROWS:
             if (value < 32 || value > 1024 || value % 32 != 0)
                 return arg_error("MPGNN_OPT_CHUNK_ROWS must be 32..1024, a multiple of 32");
@@ -5235,6 +5256,7 @@ int32_t mpgnn_get_option(int32_t option, int64_t* value) {
         case MPGNN_OPT_CHUNK_ROWS: *value = g_chunk_rows; return MPGNN_OK;
         case MPGNN_OPT_GEMM_BF3: *value = g_gemm_bf3 ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_BWD_FUSED: *value = g_bwd_fused ? 1 : 0; return MPGNN_OK;
+        case MPGNN_OPT_FLAT_WG_PER_CU: *value = g_flat_wg_per_cu; return MPGNN_OK;
         default: return arg_error("unknown option " + std::to_string(option));
     }
 }
@@ -6157,8 +6179,35 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
     }
     const int root_y = grad_root ? mt : 1;
     const bool bf3 = have_w && have_root && root_y == mt && g_gemm_bf3 && F_in == 128 && F_out == 128;
+    // F_in = F_out = 256 (C5): the same kernel over the four 128 × 128 quadrants of every dW_r /
+    // droot slab (the bias column sums taken by the two quadrants of the first A half)
+    const bool bf3q = have_w && have_root && root_y == mt && g_gemm_bf3 && F_in == 256 && F_out == 256 && !acc;
     if (acc && !bf3) return MPGNN_ERR_UNSUPPORTED;  // (excluded by rgcn_bwd_impl's check)
-    if (bf3) {
+    if (bf3q) {
+        TimedLaunch tl(MPGNN_K_OUTER, strm);
+        const int n_all = nch + rc.n;
+        const int gx = std::max(1, std::min(n_all, cu_count() * 2));
+        for (int qa = 0; qa < 2; ++qa)
+            for (int qb = 0; qb < 2; ++qb) {
+                OuterArgs rq = orr, wq = ow;
+                for (OuterArgs* o : {&rq, &wq}) {
+                    o->lda = F_in;
+                    o->ldb = F_out;
+                    o->a_col0 = qa * 128;
+                    o->b_col0 = qb * 128;
+                    o->ldd = F_out;
+                    o->d_off = qa * 128 * F_out + qb * 128;
+                    o->p_stride = (int64_t)F_in * F_out;
+                    o->pb_stride = F_out;
+                }
+                if (qa != 0) {  // the bias column sums once per B half
+                    rq.Pb = nullptr;
+                    rq.dst_b = nullptr;
+                }
+                hipLaunchKernelGGL(outer_bf3_kernel, dim3(gx), dim3(kThreads), kOb3Lds, strm, rq, wq, rc.n, n_all);
+                if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel (quadrant) launch")) != MPGNN_OK) return st;
+            }
+    } else if (bf3) {
         // F_in = F_out = 128: the bf16-split persistent kernel (outer_bf3_kernel)
         TimedLaunch tl(MPGNN_K_OUTER, strm);
         const int n_all = nch + rc.n;
