@@ -759,7 +759,7 @@ def bench_score_bags(args):
 def pmc_traffic(workload, mode, feat, kernel_prefix):
     """HBM bytes per launch of `kernel_prefix` from the committed PMC summary, or None."""
     rows = []
-    for rnd in ("r03", "r02"):  # the newest round's PMC summary first
+    for rnd in ("r04", "r03", "r02"):  # the newest round's PMC summary first
         try:
             rows += json.load(open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic.json")))
         except (OSError, ValueError):
@@ -977,7 +977,7 @@ def main():
                     "algorithmic": dom["algorithmic"],
                     "note": "dominant kernel of the forward layer by the per-kernel HIP-event pass (events on the "
                             "launch stream, one pair per launch; the headline timed region has none); traffic = "
-                            "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/r03_pmc_traffic.json, r02 for kernels not re-profiled)"}
+                            "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/r04_pmc_traffic.json; r03 / r02 for kernels not re-profiled)"}
         # SURVEY 8d whole-step HBM roofline of the aggregation (kept beside the kernel roofline)
     b_edge = 4 * F + 4
     hbm_roofline = {"bound": "hbm", "bytes_per_edge": b_edge,

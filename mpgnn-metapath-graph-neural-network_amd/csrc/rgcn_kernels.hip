@@ -91,6 +91,23 @@ __device__ __forceinline__ void vstore_sc1(float* base, int off, const float (&v
     }
 }
 
+// vload through a buffer resource with the sc1 cache policy (bypasses this CU's L1: the partials
+// other workgroups stored sc1 in the same launch, flat_split_arrive)
+template <int V>
+__device__ __forceinline__ void vload_sc1(const float* base, int off, float (&v)[V]) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+    if constexpr (V == 4) {
+        const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, off * 4, 0, 16);
+        v[0] = __uint_as_float(t.x); v[1] = __uint_as_float(t.y); v[2] = __uint_as_float(t.z); v[3] = __uint_as_float(t.w);
+    } else if constexpr (V == 2) {
+        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, off * 4, 0, 16);
+        v[0] = __uint_as_float(t.x); v[1] = __uint_as_float(t.y);
+    } else {
+        v[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off * 4, 0, 16));
+    }
+}
+
 // ReLU with torch's semantics (clamp_min(x, 0)): x < 0 → 0, NaN and -0.0 pass through, so a
 // diverging run still shows NaN (fmaxf(NaN, 0) would return 0).
 __device__ __forceinline__ float relu_f(float v) { return v < 0.0f ? 0.0f : v; }
@@ -2415,6 +2432,14 @@ struct FlatArgs {
     const float* bias;      // nullable: added to complete rows in [lo, hi) after their sum
     int lo, hi;
     int relu;               // fused activation on complete rows (unsharded combine only)
+    // nullable: rows split over > kFlatLongPieces chunks are finished inside the launch — each
+    // piece's partial is stored write-through (sc1), its wave drains and adds 1 to arrive[k]
+    // (agent scope); the wave whose add completes the row sums the row's slots in chunk order
+    // (sc1 loads) and finishes it (finalize_rows_kernel's mode-0 arithmetic, without its launch)
+    unsigned* arrive;       // [nsplit], zero at launch
+    const int* row_split;   // split index per row
+    const int* split_ptr;
+    const int* split_slot;
 };
 
 // The finishing step of a complete row: / cnt (IEEE), + bias on own rows, fused ReLU.
@@ -2437,6 +2462,59 @@ __device__ __forceinline__ void flat_finish_store(const FlatArgs& a, int rr, flo
             vstore_sc1<V>(dst, col, o);
         }
     }
+}
+
+template <int V, int T>
+__device__ __forceinline__ void flat_finish_store(const FlatArgs& a, int rr, float d, bool div, const float (&bb)[T][V],
+                                                  const float (&acc)[T][V], int lane);
+
+// A piece of a row split over more than kFlatLongPieces chunks: store the partial write-through,
+// count it; the last piece's wave adds the row's slots in chunk order (from 0.0f, as
+// finalize_rows_kernel) and finishes the row.  Hand-off: sc1 stores -> this wave's vmcnt(0) ->
+// one lane's agent-scope atomic add; the adder that completes the count reads the slots with
+// sc1 loads only after its add has returned (MI355X_MICROARCH.md § visibility, first row).
+template <int V, int T>
+__device__ __forceinline__ void flat_split_arrive(const FlatArgs& a, int rr, int slot, float d, bool div,
+                                                  const float (&bb)[T][V], const float (&acc)[T][V], int lane) {
+    const int F = a.F;
+    float* dst = a.carry + (size_t)slot * F;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int col = (t * 64 + lane) * V;
+        if (col < F) vstore_sc1<V>(dst, col, acc[t]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int k = ld_uniform(a.row_split, rr);
+    const int s0 = ld_uniform(a.split_ptr, k), s1 = ld_uniform(a.split_ptr, k + 1);
+    unsigned old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(a.arrive + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = (unsigned)readlane((int)old, 0);
+    if (old + 1 != (unsigned)(s1 - s0)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the add
+    int colc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, F - V);
+    float sum[T][V];
+    zero_acc<V, T>(sum);
+    constexpr int SB = (V * T <= 2) ? 32 : 16;
+    for (int sb = s0; sb < s1; sb += SB) {
+        const int my_sl = a.split_slot[min(sb + (lane & (SB - 1)), s1 - 1)];
+        float v[SB][T][V];
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            const float* base = a.carry + (size_t)readlane(my_sl, u) * F;
+#pragma unroll
+            for (int t = 0; t < T; ++t) vload_sc1<V>(base, colc[t], v[u][t]);
+        }
+#pragma unroll
+        for (int u = 0; u < SB; ++u)
+            if (sb + u < s1)
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+#pragma unroll
+                    for (int q = 0; q < V; ++q) sum[t][q] += v[u][t][q];
+    }
+    flat_finish_store<V, T>(a, rr, d, div, bb, sum, lane);
 }
 
 // One wave sums one chunk (<= 32 positions): complete rows are finished and stored; the
@@ -2497,6 +2575,8 @@ __device__ __forceinline__ void flat_chunk(const FlatArgs& a, int c, int lane, f
                     const bool split = (rr == rf && fs) || (rr == rl && ls);
                     if (!split) {
                         flat_finish_store<V, T>(a, rr, (float)readlane(cnt_l, q), has_cnt, bb, acc, lane);
+                    } else if (a.arrive != nullptr && carry == a.carry) {  // piece of a hub row
+                        flat_split_arrive<V, T>(a, rr, slot0, (float)readlane(cnt_l, q), has_cnt, bb, acc, lane);
                     } else {  // a split chunk holds one row: its partial
                         float* dst = carry + (size_t)slot0 * F;
 #pragma unroll
@@ -4473,7 +4553,10 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
     w.g = off; off += align256(S_sel * F_in * sizeof(float));
     w.groot = off; off += align256(rows * F_in * sizeof(float));
     w.h = off; off += align256(Sm_sel * F_in * sizeof(float));
-    w.pdx = off; off += align256(std::max(dx_pieces, seg_slots) * F_in * sizeof(float));
+    // + the grad_x list's split-row counters behind its carry slots (run_grad_x)
+    w.pdx = off;
+    off += align256(std::max(dx_pieces, seg_slots) * F_in * sizeof(float) +
+                    (mode == MPGNN_MODE_ALL ? (size_t)p->tx_f.nsplit * sizeof(unsigned) : 0));
     w.p = off; off += align256((size_t)(s.c_hi - s.c_lo) * F_in * F_out * sizeof(float));
     w.proot = off; off += align256((size_t)rc.n * F_in * F_out * sizeof(float));
     w.pb = off; off += align256((size_t)rc.n * F_out * sizeof(float));
@@ -4773,6 +4856,7 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
     return hip_check(hipGetLastError(), "row_sum_kernel launch");
 }
 
+static bool g_flat_fuse_split = true;  // MPGNN_OPT_FLAT_FUSE_SPLIT: hub rows of grad_x finished in the gather launch
 static int g_flat_wg_per_cu = 0;  // MPGNN_OPT_FLAT_WG_PER_CU: persistent grid of flat_rows_kernel (0: a workgroup per group)
 template <int V, int T>
 static void launch_flat(const FlatArgs& a, int max_pieces, hipStream_t st) {
@@ -4939,6 +5023,7 @@ struct FlatRun {
     const float* bias;
     int lo, hi;
     int relu;             // fused activation (unsharded forward combine)
+    unsigned* arrive;     // mode 0: [nsplit] zeroed piece counters — split rows finished in the launch
 };
 
 static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
@@ -4971,7 +5056,13 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
         }
         a.out = f.out;
         a.carry = f.carry;
-        a.relu = f.final_mode == 0 ? f.relu : 0;  // mode 1: the finalize adds extra + bias first
+        a.relu = f.final_mode == 0 ? f.relu : 0;
+        if (f.final_mode == 0 && f.arrive != nullptr) {
+            a.arrive = f.arrive;
+            a.row_split = f.fd->row_split;
+            a.split_ptr = f.fd->split_ptr;
+            a.split_slot = f.fd->split_slot;
+        }  // mode 1: the finalize adds extra + bias first
         MPGNN_VT_DISPATCH(V, T, launch_flat, a, f.max_pieces, strm);
         int32_t st = hip_check(hipGetLastError(), "flat_rows_kernel launch");
         if (st != MPGNN_OK) return st;
@@ -4999,7 +5090,7 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
     b.dummy = f.out;
     b.relu = f.relu;
     const int nrows = f.final_mode == 0 ? f.k_hi - f.k_lo : f.r_hi - f.r_lo;
-    if (nrows <= 0) return MPGNN_OK;
+    if (nrows <= 0 || (f.final_mode == 0 && f.arrive != nullptr && f.g_hi > f.g_lo)) return MPGNN_OK;
     TimedLaunch tl(MPGNN_K_FINAL, strm);
     MPGNN_VT_DISPATCH(V, T, launch_final, b, nrows, strm);
     return hip_check(hipGetLastError(), "finalize_rows_kernel launch");
@@ -5226,6 +5317,9 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
             g_bwd_fused = value != 0;
             return MPGNN_OK;
 
+        case MPGNN_OPT_FLAT_FUSE_SPLIT:
+            g_flat_fuse_split = value != 0;
+            return MPGNN_OK;
         case MPGNN_OPT_FLAT_WG_PER_CU:
             if (value < 0 || value > 64) return arg_error("MPGNN_OPT_FLAT_WG_PER_CU must be 0..64");
             g_flat_wg_per_cu = (int)value;
@@ -5257,6 +5351,7 @@ int32_t mpgnn_get_option(int32_t option, int64_t* value) {
         case MPGNN_OPT_GEMM_BF3: *value = g_gemm_bf3 ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_BWD_FUSED: *value = g_bwd_fused ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = g_flat_wg_per_cu; return MPGNN_OK;
+        case MPGNN_OPT_FLAT_FUSE_SPLIT: *value = g_flat_fuse_split ? 1 : 0; return MPGNN_OK;
         default: return arg_error("unknown option " + std::to_string(option));
     }
 }
@@ -5655,6 +5750,13 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         f.lo = (int)row_lo;
         f.hi = (int)row_hi;
         TimedLaunch tl(MPGNN_K_ROW_DX, strm);
+        if (g_flat_fuse_split && p->tx_f.nsplit > 0) {
+            // piece counters behind the carry slots (ws_layout reserves them in the pdx region)
+            f.arrive = reinterpret_cast<unsigned*>(Pdx + (size_t)p->tx_f.nslots * F_in);
+            st = hip_check(hipMemsetAsync(f.arrive, 0, (size_t)p->tx_f.nsplit * sizeof(unsigned), strm),
+                           "memset split counters");
+            if (st != MPGNN_OK) return st;
+        }
         st = run_flat(f, strm);
         if (st != MPGNN_OK) return st;
     } else if (mode == MPGNN_MODE_ALL && !exact) {

@@ -185,7 +185,8 @@ class MPNetm(_FastTrainToggle, torch.nn.Module):
                     h = conv(layer_index, rel, h, edge_index, edge_type, activation="relu")
                     h = self.dropout2(h)
             embeddings.append(h)
-        concatenated_embedding = torch.cat(embeddings, dim=1)
+        # torch.cat of ONE embedding (a single metapath) is a copy of it: skipped, same values
+        concatenated_embedding = embeddings[0] if len(embeddings) == 1 else torch.cat(embeddings, dim=1)
         h = F.relu(linear(self.fc1, concatenated_embedding))
         h = linear(self.fc2, h)
         return self.log_softmax(h)

@@ -3,7 +3,7 @@
 # abort or timeout ends the session). Usage: bash scripts/bench_all.sh [quick|full]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out
+OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
 run() {  # name timeout args...
     local name=$1 to=$2; shift 2

@@ -681,6 +681,42 @@ def test_fused_backward_matches_two_launches_and_oracle(mode, rows):
             assert nw <= 1e-5, (k, nw)
 
 
+def test_grad_x_hub_rows_finished_in_launch_equal_finalize():
+    """MPGNN_OPT_FLAT_FUSE_SPLIT: the C3 grad_x rows of more than 16 chunks (hub nodes, up to
+    ~190 pieces) finished by the wave that adds their last piece (write-through partials, an
+    agent-scope piece counter, the slots summed in chunk order) against finalize_rows_kernel
+    after the launch: grad_x bit-identical, repeated calls (the counters must return to zero —
+    a stale count would finish a row early or never), and the oracle's bar."""
+    from mpgnn_amd import _lib
+    g = data.fb15k237_graph(feat_dim=128, seed=0, recipe="survey")
+    N, R = g.num_nodes, g.num_relations
+    indeg = torch.bincount(g.edge_index[1], minlength=N)
+    assert int(indeg.max()) > 16 * 32, "C3 has no hub row of more than 16 chunks"
+    gen = torch.Generator().manual_seed(77)
+    W = (torch.rand((R, 128, 128), generator=gen) - 0.5) * 0.2
+    root = (torch.rand(128, 128, generator=gen) - 0.5) * 0.2
+    bias = torch.rand(128, generator=gen) - 0.5
+    gout = torch.randn(N, 128, generator=gen)
+    plan = mpgnn_amd.GraphPlan(g.edge_index.to(DEV), g.edge_type.to(DEV), N)
+    xg0 = g.x.to(DEV)
+    Wg, rg, bg = (t.to(DEV) for t in (W, root, bias))
+    res = {}
+    for fuse in (1, 0, 1, 1):
+        _lib.set_option(27, fuse)
+        xg = xg0.clone().requires_grad_(True)
+        out = rgcn_conv(xg, Wg, rg, bg, plan, MODE_ALL, num_relations=R)
+        out.backward(gout.to(DEV))
+        torch.cuda.synchronize()
+        if fuse in res:
+            assert torch.equal(xg.grad, res[fuse]), (fuse, "not repeatable")
+        res[fuse] = xg.grad
+    assert torch.equal(res[1], res[0]), "grad_x differs between the in-launch finish and finalize_rows_kernel"
+    hubs = torch.nonzero(indeg > 16 * 32).flatten()
+    r32, r64 = oracle_layer2(g.x, g.edge_index, g.edge_type, W, root, bias, gout, mode=MODE_ALL, rel=None)
+    rel_close(res[1][hubs.to(DEV)], r32["dx"][hubs], what="grad_x hub rows (in-launch finish)", ref64=r64["dx"][hubs])
+    rel_close(res[1], r32["dx"], what="grad_x C3 (in-launch finish)", ref64=r64["dx"])
+
+
 # ------------------------------------------------------------------------------------------
 # CustomFastRGCNConv (A7): transform-then-aggregate semantics on the same kernels
 # ------------------------------------------------------------------------------------------

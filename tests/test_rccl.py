@@ -93,7 +93,7 @@ def _worker(port, q):
         import json
         os.environ["MPGNN_BENCH_FORCE_DIST"] = "1"
         sys.argv = ["bench.py", "--gpus", "1", "--steps", "3", "--warmup", "1", "--epoch-steps", "2",
-                    "--loop-epochs", "2", "--no-cpu-baseline"]
+                    "--loop-epochs", "8", "--no-cpu-baseline"]
         import bench
         bench.setup_dist = (lambda n, _f=bench.setup_dist: (0, 1, 0, group))  # the group is already up
         buf = io.StringIO()
@@ -104,9 +104,15 @@ def _worker(port, q):
             msgs.append(f"bench printed {len(lines)} JSON lines")
         else:
             ln = lines[0]
-            if not (ln["value"] > 0 and ln["epoch_ms"] > 0 and ln["config"]["shard_side"] == "gathered"
-                    and "RCCL" in ln["config"]["parallelism"] and ln["loop_epoch"]["ms"]):
-                msgs.append(f"bench line: {ln}")
+            # the loop leg ran through the group (its ms may be None when t(6 + K) - t(6) is
+            # within the run-to-run noise of so short a timing: that is reported, not a failure)
+            checks = {"value": ln["value"] > 0, "epoch_ms": ln["epoch_ms"] > 0,
+                      "shard_side": ln["config"]["shard_side"] == "gathered",
+                      "parallelism": "RCCL" in ln["config"]["parallelism"],
+                      "loop_epoch": isinstance(ln["loop_epoch"], dict) and "epochs_timed" in ln["loop_epoch"]}
+            bad = [k for k, ok in checks.items() if not ok]
+            if bad:
+                msgs.append(f"bench line fails {bad}: " + str({k: ln.get(k) for k in ("value", "epoch_ms", "loop_epoch")}))
         q.put((msgs, None))
     except BaseException:
         import traceback
