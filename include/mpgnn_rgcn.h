@@ -374,9 +374,12 @@ enum mpgnn_option {
                                     0: the dgrad launch + the chunked dW launch */
     MPGNN_OPT_FLAT_WG_PER_CU = 26, /* gather-sum lists (means, combine, grad_x): 0 = one workgroup per list group;
                                     k > 0 = a persistent grid of k workgroups per CU walking the groups */
-    MPGNN_OPT_FLAT_FUSE_SPLIT = 27 /* 1 (default): grad_x rows split over more than 16 chunks (hub nodes) are
+    MPGNN_OPT_FLAT_FUSE_SPLIT = 27, /* 1 (default): grad_x rows split over more than 16 chunks (hub nodes) are
                                     finished inside the gather-sum launch by the wave adding their last
                                     piece (same sums, same order); 0: finalize_rows_kernel after it */
+    MPGNN_OPT_OUTER_VEC = 28     /* 1 (default): the bf16-split weight-gradient kernel gathers rows 16 B per lane
+                                    and reads its column fragments with transposed LDS reads
+                                    (outer_bf3v_kernel); 0: 4-B column gathers (outer_bf3_kernel) */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

@@ -3740,6 +3740,281 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3_kernel(OuterArgs ra, Ou
 }
 
 // ----------------------------------------------------------------------------------------
+// outer_bf3v_kernel — outer_bf3_kernel (same chunk streams, cursors, destinations, pipeline,
+// six-product split, accumulators, epilogue) with 16-byte row gathers: a slice's 16 rows are
+// staged ROW-major, thread t holding columns 4·(t & 31) .. +3 of rows (t >> 5) and (t >> 5) + 8
+// of both matrices (4 float4 loads per slice instead of 16 dword loads: outer_bf3_kernel issued
+// 2.4x the forward GEMM's vector-memory instructions), and the MFMA fragments, which run down
+// the columns (K = the slice's rows), are read with ds_read_b64_tr_b16 (gfx950's transposed LDS
+// read: a 16-lane group reads 4 rows × 16 columns, lane i receives column i).  Planes
+// [16 rows][160] bf16: the 320-B row stride puts the four rows of a transposed read on disjoint
+// bank quarters (conflict-free).  The bias column sums (root chunks) are taken per thread over
+// its own 4 columns × 2 rows, exact from the three pieces as in outer_bf3_kernel, and the 8
+// row-group partials of each column are added in order at the chunk's end.
+// ----------------------------------------------------------------------------------------
+constexpr int kOvLd = 160;                       // bf16 per staged row: 128 + 32 pad (320 B)
+constexpr int kOvPlane = 16 * kOvLd;             // bf16 per plane (16 rows)
+constexpr size_t kOvLds = (size_t)2 * 6 * kOvPlane * 2 + 8 * 128 * sizeof(float);  // 2 buffers × 6 planes + bias partials
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// 8 consecutive k (rows k0 .. k0 + 8 of a plane) of column `col0 + (lane & 15)` for the lane's
+// 16-lane group: two transposed reads of 4 rows each (lane 4q + p addresses row k0 + q,
+// columns col0 + 4p .. +3)
+__device__ __forceinline__ bf16x8 ov_frag(const __bf16* plane, int k0, int col0, int lane) {
+    const int i = lane & 15;
+    const __bf16* base = plane + (k0 + (i >> 2)) * kOvLd + col0 + 4 * (i & 3);
+    typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 4 * kOvLd));
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel(OuterArgs ra, OuterArgs wa, int ra_n, int n_all) {
+    constexpr int SL = 16;
+    extern __shared__ __attribute__((aligned(16))) __bf16 ov_smem[];
+    __bf16* planes = ov_smem;                                         // [2][A0 A1 A2 B0 B1 B2][16][160]
+    float* bx = reinterpret_cast<float*>(ov_smem + 2 * 6 * kOvPlane);  // [8 row groups][128] bias partials
+    const int G = (int)gridDim.x;
+    if ((int)blockIdx.x >= n_all) return;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int c = lane & 31;
+    const int h = lane >> 5;
+    const int srow = tid >> 5;         // staged rows srow, srow + 8 (0 .. 7: two per wave)
+    const int scol = (tid & 31) * 4;   // staged columns scol .. +3
+
+    struct Src {
+        const float *A, *A2, *B;
+        const int *a_idx, *b_idx;
+        int a_off, a2_off;
+    };
+    const int lda = ra.lda ? ra.lda : 128, ldb = ra.ldb ? ra.ldb : 128, ldd = ra.ldd ? ra.ldd : 128;
+    const int pb_stride = ra.pb_stride ? ra.pb_stride : 128;
+    const int64_t p_stride = ra.p_stride ? ra.p_stride : 128 * 128;
+    auto src_of = [&](int chunk) {
+        const bool r = chunk < ra_n;
+        Src x;
+        x.A = (r ? ra.A : wa.A) + ra.a_col0;
+        x.A2 = (r ? ra.A2 : wa.A2) + ra.a_col0;
+        x.B = (r ? ra.B : wa.B) + ra.b_col0;
+        x.a_idx = r ? ra.a_idx : wa.a_idx;
+        x.b_idx = r ? ra.b_idx : wa.b_idx;
+        x.a_off = r ? ra.a_off : wa.a_off;
+        x.a2_off = r ? ra.a2_off : wa.a2_off;
+        return x;
+    };
+    auto open_chunk = [&](int chunk) {
+        OuterCursor k;
+        k.chunk = chunk;
+        k.sl = 0;
+        int p0 = 0, p1 = 0;
+        if (chunk < ra_n) {
+            p0 = ra.row_lo + chunk * ra.chunk_rows;
+            p1 = min(ra.row_hi, p0 + ra.chunk_rows);
+        } else if (chunk < n_all) {
+            p0 = ld_uniform(wa.chunk_begin, chunk - ra_n + wa.chunk_off);
+            p1 = ld_uniform(wa.chunk_end, chunk - ra_n + wa.chunk_off);
+        }
+        k.p0 = p0;
+        k.p1 = p1;
+        k.ns = (p1 - p0 + SL - 1) / SL;
+        return k;
+    };
+    auto advance = [&](const OuterCursor& k) {
+        if (k.sl + 1 < k.ns) {
+            OuterCursor n = k;
+            n.sl = k.sl + 1;
+            return n;
+        }
+        return open_chunk(k.chunk + G);
+    };
+    auto valid = [&](const OuterCursor& k) { return k.chunk < n_all && k.ns > 0; };
+
+    // row indices of a slice: lanes 0..3 of the wave hold those of its staged rows
+    // 2·wave, 2·wave + 1, 2·wave + 8, 2·wave + 9
+    auto load_idx = [&](const OuterCursor& k, int& ia, int& ib) {
+        const Src a = src_of(k.chunk);
+        const int r = 2 * wave + (lane & 1) + 8 * ((lane >> 1) & 1);
+        const int p = min(k.p0 + k.sl * SL + r, max(k.p1 - 1, k.p0));
+        ib = a.b_idx != nullptr ? a.b_idx[p] : p;
+        ia = a.a_idx != nullptr ? a.a_idx[p] : p - a.a_off;
+    };
+    // this lane's two rows (srow: index lane 0 | 1 by half; srow + 8: lane 2 | 3) as float4
+    auto issue = [&](const OuterCursor& k, int ia, int ib, float4 (&va)[2], float4 (&vb)[2]) {
+        const Src a = src_of(k.chunk);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int a0 = __builtin_amdgcn_readlane(ia, 2 * j), a1 = __builtin_amdgcn_readlane(ia, 2 * j + 1);
+            const int b0 = __builtin_amdgcn_readlane(ib, 2 * j), b1 = __builtin_amdgcn_readlane(ib, 2 * j + 1);
+            const int ra_ = h ? a1 : a0, rb_ = h ? b1 : b0;
+            const float* arow = ra_ >= 0 ? a.A + (size_t)ra_ * lda : a.A2 + (size_t)(-ra_ - 1 - a.a2_off) * lda;
+            va[j] = *reinterpret_cast<const float4*>(arow + scol);
+            vb[j] = *reinterpret_cast<const float4*>(a.B + (size_t)rb_ * ldb + scol);
+        }
+    };
+    // split + row-major store of one staged slice; rows past the chunk's end are zeros
+    auto commit = [&](const OuterCursor& k, const float4 (&va)[2], const float4 (&vb)[2], __bf16* buf) {
+        const int nr = min(SL, k.p1 - k.p0 - k.sl * SL);  // live rows of the slice
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const bool live = srow + 8 * j < nr;
+            const float4 xa = live ? va[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 xb = live ? vb[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float fa[4] = {xa.x, xa.y, xa.z, xa.w}, fb[4] = {xb.x, xb.y, xb.z, xb.w};
+            bf16x4 pa[3], pb[3];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                __bf16 a0, a1, a2, b0, b1, b2;
+                split3_bf16(fa[e], a0, a1, a2);
+                split3_bf16(fb[e], b0, b1, b2);
+                pa[0][e] = a0; pa[1][e] = a1; pa[2][e] = a2;
+                pb[0][e] = b0; pb[1][e] = b1; pb[2][e] = b2;
+            }
+            __bf16* d = buf + (srow + 8 * j) * kOvLd + scol;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                *reinterpret_cast<bf16x4*>(d + q * kOvPlane) = pa[q];
+                *reinterpret_cast<bf16x4*>(d + (3 + q) * kOvPlane) = pb[q];
+            }
+        }
+    };
+
+    f32x16 hi[4], lo[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            hi[q][r] = 0.0f;
+            lo[q][r] = 0.0f;
+        }
+    float bpart[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // this thread's columns over its rows (root chunks)
+
+    OuterCursor cur = open_chunk((int)blockIdx.x);
+    if (!valid(cur)) return;
+    OuterCursor c1 = advance(cur);
+    OuterCursor c2 = valid(c1) ? advance(c1) : c1;
+    OuterCursor c3 = valid(c2) ? advance(c2) : c2;
+    float4 xa[2], xb[2], ya[2], yb[2];
+    int ia, ib, ja = 0, jb = 0;
+    load_idx(cur, ia, ib);
+    issue(cur, ia, ib, xa, xb);
+    commit(cur, xa, xb, planes);
+    if (valid(c1)) {
+        load_idx(c1, ia, ib);
+        issue(c1, ia, ib, xa, xb);
+    }
+    if (valid(c2)) load_idx(c2, ja, jb);
+    __syncthreads();
+    int buf = 0;
+    const int g = lane >> 4;          // 16-lane group of the transposed reads
+    const int kq = 8 * (g >> 1);      // the group's k rows: kq .. kq + 8 (= 8·h)
+    const int mq = 16 * (g & 1);      // the group's 16 columns within a 32-column block
+    auto step = [&](float4 (&vca)[2], float4 (&vcb)[2], float4 (&vna)[2], float4 (&vnb)[2]) -> bool {
+        const bool more = valid(c1);
+        if (valid(c2)) {
+            issue(c2, ja, jb, vna, vnb);
+            if (valid(c3)) load_idx(c3, ja, jb);
+        }
+        const bool is_root = cur.chunk < ra_n;
+        const __bf16* cb = planes + buf * 6 * kOvPlane;
+        const int ncol = wave * 32 + mq;
+        const bf16x8 b0 = ov_frag(cb + 3 * kOvPlane, kq, ncol, lane);
+        const bf16x8 b1 = ov_frag(cb + 4 * kOvPlane, kq, ncol, lane);
+        const bf16x8 b2 = ov_frag(cb + 5 * kOvPlane, kq, ncol, lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bf16x8 a0 = ov_frag(cb, kq, q * 32 + mq, lane);
+            const bf16x8 a1 = ov_frag(cb + kOvPlane, kq, q * 32 + mq, lane);
+            const bf16x8 a2 = ov_frag(cb + 2 * kOvPlane, kq, q * 32 + mq, lane);
+            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, lo[q], 0, 0, 0);
+            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, lo[q], 0, 0, 0);
+            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, lo[q], 0, 0, 0);
+            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, lo[q], 0, 0, 0);
+            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, lo[q], 0, 0, 0);
+            hi[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, hi[q], 0, 0, 0);
+        }
+        if (is_root && ra.Pb != nullptr) {  // bias: column sums over the chunk's rows, exact from the pieces
+            const int nr = min(SL, cur.p1 - cur.p0 - cur.sl * SL);
+            const __bf16* bc = cb + (ra.bias_of_a ? 0 : 3 * kOvPlane) + srow * kOvLd + scol;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x4 q0 = *reinterpret_cast<const bf16x4*>(bc + 8 * j * kOvLd);
+                const bf16x4 q1 = *reinterpret_cast<const bf16x4*>(bc + 8 * j * kOvLd + kOvPlane);
+                const bf16x4 q2 = *reinterpret_cast<const bf16x4*>(bc + 8 * j * kOvLd + 2 * kOvPlane);
+                if (srow + 8 * j < nr)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) bpart[e] += ((float)q0[e] + (float)q1[e]) + (float)q2[e];
+            }
+        }
+        const bool chunk_end = cur.sl + 1 == cur.ns;
+        if (more) commit(c1, vca, vcb, planes + (buf ^ 1) * 6 * kOvPlane);
+        if (chunk_end) {
+            float* D;
+            float* Db = nullptr;
+            if (is_root) {
+                const int cidx = cur.chunk;
+                D = ra.P + (size_t)cidx * p_stride + ra.d_off;
+                Db = ra.Pb != nullptr ? ra.Pb + (size_t)cidx * pb_stride + ra.b_col0 : nullptr;
+                if (ra.dst_mode == 3) {
+                    D = ra.dst != nullptr ? ra.dst + ra.d_off : nullptr;
+                    Db = ra.dst_b != nullptr ? ra.dst_b + ra.b_col0 : nullptr;
+                }
+            } else {
+                const int cidx = cur.chunk - ra_n;
+                D = wa.P + (size_t)cidx * p_stride + ra.d_off;
+                if (wa.dst_mode == 1 || wa.dst_mode == 2) {
+                    const int di = ld_uniform(wa.chunk_dst, cidx + wa.chunk_off);
+                    if (di >= 0) D = wa.dst + (size_t)(wa.dst_mode == 1 ? di : 0) * p_stride + ra.d_off;
+                }
+            }
+            const int ln = opaque(lane);
+            const int ocol = wave * 32 + (ln & 31);
+            const int h4 = 4 * (ln >> 5);
+            if (D != nullptr) {
+                float* Dc = D + ocol;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = q * 32 + (r & 3) + 8 * (r >> 2) + h4;
+                        Dc[(size_t)m * ldd] = hi[q][r] + lo[q][r];
+                    }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    hi[q][r] = 0.0f;
+                    lo[q][r] = 0.0f;
+                }
+            if (is_root && ra.Pb != nullptr) {  // the 8 row groups of each column, in order
+                *reinterpret_cast<float4*>(bx + srow * 128 + scol) = make_float4(bpart[0], bpart[1], bpart[2], bpart[3]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) bpart[e] = 0.0f;
+                __syncthreads();
+                if (tid < 128 && Db != nullptr) {
+                    float t = bx[tid];
+#pragma unroll
+                    for (int r = 1; r < 8; ++r) t += bx[r * 128 + tid];
+                    Db[tid] = t;
+                }
+            }
+        }
+        __syncthreads();
+        if (!more) return false;
+        cur = c1;
+        c1 = c2;
+        c2 = c3;
+        c3 = valid(c3) ? advance(c3) : c3;
+        buf ^= 1;
+        return true;
+    };
+    while (step(xa, xb, ya, yb) && step(ya, yb, xa, xb)) {
+    }
+}
+
+// ----------------------------------------------------------------------------------------
 // bwd_bf3_kernel — the GEMM work of a layer's backward at F_in = F_out = 128 in ONE persistent
 // launch over rel_gemm's items (32-row relation tiles, then 32-node root items), both products
 // that read dout on the bf16 matrix cores with the exact three-way split:
@@ -4856,6 +5131,13 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
     return hip_check(hipGetLastError(), "row_sum_kernel launch");
 }
 
+static bool g_outer_vec = true;  // MPGNN_OPT_OUTER_VEC: outer_bf3v_kernel (16-B gathers, transposed LDS reads)
+static void launch_outer_bf3(dim3 grid, const OuterArgs& r, const OuterArgs& w, int ra_n, int n_all, hipStream_t st) {
+    if (g_outer_vec)
+        hipLaunchKernelGGL(outer_bf3v_kernel, grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
+    else
+        hipLaunchKernelGGL(outer_bf3_kernel, grid, dim3(kThreads), kOb3Lds, st, r, w, ra_n, n_all);
+}
 static bool g_flat_fuse_split = true;  // MPGNN_OPT_FLAT_FUSE_SPLIT: hub rows of grad_x finished in the gather launch
 static int g_flat_wg_per_cu = 0;  // MPGNN_OPT_FLAT_WG_PER_CU: persistent grid of flat_rows_kernel (0: a workgroup per group)
 template <int V, int T>
@@ -5257,8 +5539,7 @@ int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int
         orr.dst_b = grad_bias;
         orr.bias_of_a = 1;
         OuterArgs none{};
-        hipLaunchKernelGGL(outer_bf3_kernel, dim3(std::min(nch, cu_count() * 2)), dim3(kThreads), kOb3Lds, strm, orr,
-                           none, nch, nch);
+        launch_outer_bf3(dim3(std::min(nch, cu_count() * 2)), orr, none, nch, nch, strm);
         int32_t st = hip_check(hipGetLastError(), "outer_bf3_kernel (linear) launch");
         if (st != MPGNN_OK || nch == 1) return st;
         ReduceArgs rw{}, rb{};
@@ -5320,6 +5601,9 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
         case MPGNN_OPT_FLAT_FUSE_SPLIT:
             g_flat_fuse_split = value != 0;
             return MPGNN_OK;
+        case MPGNN_OPT_OUTER_VEC:
+            g_outer_vec = value != 0;
+            return MPGNN_OK;
         case MPGNN_OPT_FLAT_WG_PER_CU:
             if (value < 0 || value > 64) return arg_error("MPGNN_OPT_FLAT_WG_PER_CU must be 0..64");
             g_flat_wg_per_cu = (int)value;
@@ -5352,6 +5636,7 @@ int32_t mpgnn_get_option(int32_t option, int64_t* value) {
         case MPGNN_OPT_BWD_FUSED: *value = g_bwd_fused ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = g_flat_wg_per_cu; return MPGNN_OK;
         case MPGNN_OPT_FLAT_FUSE_SPLIT: *value = g_flat_fuse_split ? 1 : 0; return MPGNN_OK;
+        case MPGNN_OPT_OUTER_VEC: *value = g_outer_vec ? 1 : 0; return MPGNN_OK;
         default: return arg_error("unknown option " + std::to_string(option));
     }
 }
@@ -6306,7 +6591,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
                     rq.Pb = nullptr;
                     rq.dst_b = nullptr;
                 }
-                hipLaunchKernelGGL(outer_bf3_kernel, dim3(gx), dim3(kThreads), kOb3Lds, strm, rq, wq, rc.n, n_all);
+                launch_outer_bf3(dim3(gx), rq, wq, rc.n, n_all, strm);
                 if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel (quadrant) launch")) != MPGNN_OK) return st;
             }
     } else if (bf3) {
@@ -6314,7 +6599,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
         TimedLaunch tl(MPGNN_K_OUTER, strm);
         const int n_all = nch + rc.n;
         const int gx = std::max(1, std::min(n_all, cu_count() * 2));
-        hipLaunchKernelGGL(outer_bf3_kernel, dim3(gx), dim3(kThreads), kOb3Lds, strm, orr, ow, rc.n, n_all);
+        launch_outer_bf3(dim3(gx), orr, ow, rc.n, n_all, strm);
         if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel launch")) != MPGNN_OK) return st;
     } else if (have_w && have_root && root_y == mt) {
         TimedLaunch tl(MPGNN_K_OUTER, strm);
