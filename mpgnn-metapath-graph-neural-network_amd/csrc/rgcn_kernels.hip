@@ -2474,16 +2474,10 @@ __device__ __forceinline__ void flat_finish_store(const FlatArgs& a, int rr, flo
 // one lane's agent-scope atomic add; the adder that completes the count reads the slots with
 // sc1 loads only after its add has returned (MI355X_MICROARCH.md § visibility, first row).
 template <int V, int T>
-__device__ __forceinline__ void flat_split_arrive(const FlatArgs& a, int rr, int slot, float d, bool div,
-                                                  const float (&bb)[T][V], const float (&acc)[T][V], int lane) {
+__device__ __forceinline__ void flat_split_arrive(const FlatArgs& a, int rr, float d, bool div,
+                                                  const float (&bb)[T][V], int lane) {
     const int F = a.F;
-    float* dst = a.carry + (size_t)slot * F;
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-        const int col = (t * 64 + lane) * V;
-        if (col < F) vstore_sc1<V>(dst, col, acc[t]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the piece's sc1 partial has left the wave
     const int k = ld_uniform(a.row_split, rr);
     const int s0 = ld_uniform(a.split_ptr, k), s1 = ld_uniform(a.split_ptr, k + 1);
     unsigned old = 0;
@@ -2496,7 +2490,7 @@ __device__ __forceinline__ void flat_split_arrive(const FlatArgs& a, int rr, int
     for (int t = 0; t < T; ++t) colc[t] = min((t * 64 + lane) * V, F - V);
     float sum[T][V];
     zero_acc<V, T>(sum);
-    constexpr int SB = (V * T <= 2) ? 32 : 16;
+    constexpr int SB = 8;  // slots in flight (rare path: kept small, the chunk loop's registers bound the kernel)
     for (int sb = s0; sb < s1; sb += SB) {
         const int my_sl = a.split_slot[min(sb + (lane & (SB - 1)), s1 - 1)];
         float v[SB][T][V];
@@ -2519,8 +2513,9 @@ __device__ __forceinline__ void flat_split_arrive(const FlatArgs& a, int rr, int
 
 // One wave sums one chunk (<= 32 positions): complete rows are finished and stored; the
 // partial of a split row goes to carry slot `info >> 2` of `carry` (global slots, or the LDS
-// piece slots of a long group).
-template <int V, int T, int U>
+// piece slots of a long group).  With a.arrive, a piece of a > kFlatLongPieces row is counted
+// after the loop (one piece per chunk) and its row finished by the wave that completes it.
+template <int V, int T, int U, bool GLOBAL>
 __device__ __forceinline__ void flat_chunk(const FlatArgs& a, int c, int lane, float* carry, const float (&bb)[T][V]) {
     const int p0 = ld_uniform(a.chunk_ptr, c);
     const int n = ld_uniform(a.chunk_ptr, c + 1) - p0;  // 1 .. kFlatChunk
@@ -2549,6 +2544,8 @@ __device__ __forceinline__ void flat_chunk(const FlatArgs& a, int c, int lane, f
 
     float acc[T][V];
     zero_acc<V, T>(acc);
+    const bool fuse = GLOBAL && a.arrive != nullptr;  // GLOBAL: carry is a.carry (not LDS piece slots)
+    int arr_row = -1;  // the split row this chunk holds a piece of (fuse)
     for (int u0 = 0; u0 < n; u0 += U) {
         float v[U][T][V];
 #pragma unroll
@@ -2575,14 +2572,21 @@ __device__ __forceinline__ void flat_chunk(const FlatArgs& a, int c, int lane, f
                     const bool split = (rr == rf && fs) || (rr == rl && ls);
                     if (!split) {
                         flat_finish_store<V, T>(a, rr, (float)readlane(cnt_l, q), has_cnt, bb, acc, lane);
-                    } else if (a.arrive != nullptr && carry == a.carry) {  // piece of a hub row
-                        flat_split_arrive<V, T>(a, rr, slot0, (float)readlane(cnt_l, q), has_cnt, bb, acc, lane);
                     } else {  // a split chunk holds one row: its partial
                         float* dst = carry + (size_t)slot0 * F;
+                        if (fuse) {  // write-through: another wave may sum it in this launch
 #pragma unroll
-                        for (int t = 0; t < T; ++t) {
-                            const int col = (t * 64 + lane) * V;
-                            if (col < F) vstore<V>(dst + col, acc[t]);
+                            for (int t = 0; t < T; ++t) {
+                                const int col = (t * 64 + lane) * V;
+                                if (col < F) vstore_sc1<V>(dst, col, acc[t]);
+                            }
+                            arr_row = rr;
+                        } else {
+#pragma unroll
+                            for (int t = 0; t < T; ++t) {
+                                const int col = (t * 64 + lane) * V;
+                                if (col < F) vstore<V>(dst + col, acc[t]);
+                            }
                         }
                     }
                     zero_acc<V, T>(acc);
@@ -2591,6 +2595,8 @@ __device__ __forceinline__ void flat_chunk(const FlatArgs& a, int c, int lane, f
         }
         __builtin_amdgcn_sched_barrier(0);
     }
+    if (arr_row >= 0)
+        flat_split_arrive<V, T>(a, arr_row, has_cnt ? (float)a.cnt[arr_row] : 1.0f, has_cnt, bb, lane);
 }
 
 // flat_rows_kernel — one workgroup per group: a normal group's waves take one chunk each; a
@@ -2621,12 +2627,12 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
         const bool lng = ld_uniform(a.group_long, g) != 0;
         if (!lng) {
             const int c = c0 + wave;
-            if (c < c1) flat_chunk<V, T, U>(a, c, lane, a.carry, bb);
+            if (c < c1) flat_chunk<V, T, U, true>(a, c, lane, a.carry, bb);
             continue;
         }
         // a long row's pieces (the same 16 loads in flight as a normal chunk: more would raise
         // the kernel's register count and cost every group occupancy)
-        for (int c = c0 + wave; c < c1; c += kWaves) flat_chunk<V, T, U>(a, c, lane, lds_pieces, bb);
+        for (int c = c0 + wave; c < c1; c += kWaves) flat_chunk<V, T, U, false>(a, c, lane, lds_pieces, bb);
         __syncthreads();
         if (wave == 0) {
             const int rr = a.row_of[ld_uniform(a.chunk_ptr, c0)];

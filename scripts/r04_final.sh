@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/final4
+O=${O:-gpurun_out/final4}
 mkdir -p $O
 if [[ ${SKIP_SUITE:-0} != 1 ]]; then
 MPGNN_PARITY_REPORT=$PWD/$O/parity_report.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 || exit $?
@@ -20,7 +20,5 @@ echo prof done
 OUT=$O/pmc_fwd bash scripts/pmc.sh > $O/pmc_fwd.log 2>&1 || exit $?
 OUT=$O/pmc_bwd ARGS="--iters 10 --backward" bash scripts/pmc.sh > $O/pmc_bwd.log 2>&1 || exit $?
 echo pmc done
-OUT=$O bash scripts/bench_all.sh quick || exit $?
-timeout -k 10 300 python -u bench.py --workload fb15k237_relcond > $O/bench_c3_relcond.log 2>&1 || exit $?
-grep '^{' $O/bench_c3_relcond.log > $O/bench_c3_relcond.json
+OUT=$O bash scripts/bench_all.sh ${BENCH_SET:-full} || exit $?
 echo all done
