@@ -18,15 +18,19 @@ import torch.nn.functional as F
 from . import data as _data
 from .metrics import class_weight_balanced, confusion_counts_many, f1_from_counts, f1_macro_many
 from .model import MPNetm
-# score function helpers of main.py:387-760 (non-bag path, GPU kernels): same names
-from .score import (create_edge_dictionary, get_loss, get_loss_per_node, get_model, get_optimizer,  # noqa: F401
-                    initialize_weights, score_relation_parallel, train)
+# score function helpers of main.py:387-917 (both branches, GPU kernels): same names, plus the
+# batched first-round scoring of every relation (score_relations_batched)
+from .score import (clean_bags_for_relation_type, create_bags, create_edge_dictionary,  # noqa: F401
+                    get_loss, get_loss_per_node, get_model, get_optimizer, initialize_weights,
+                    reinitialize_weights, retrieve_destinations_low_loss, score_relation_bags_parallel,
+                    score_relation_parallel, score_relations_batched, train)
 
 __all__ = ["Data", "load_files", "get_node_features", "get_edge_index_and_type_no_reverse",
            "load_graph", "mpgnn_train", "mpgnn_validation", "mpgnn_test",
            "mpgnn_parallel_multiple", "mpgnn_parallel_multiple_x", "EPOCHS", "create_edge_dictionary",
            "initialize_weights", "get_model", "get_optimizer", "get_loss", "get_loss_per_node", "train",
-           "score_relation_parallel"]
+           "score_relation_parallel", "create_bags", "clean_bags_for_relation_type", "reinitialize_weights",
+           "retrieve_destinations_low_loss", "score_relation_bags_parallel", "score_relations_batched"]
 
 EPOCHS = 999  # ``for epoch in range(1, 1000)`` (main.py:1121, 1144)
 
