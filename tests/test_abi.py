@@ -87,6 +87,24 @@ def test_withdrawn_option_is_refused():
         _lib.get_option(1)
 
 
+def test_round4_switches_default_on_and_round_trip():
+    """The round-4 A/B switches (header enum mpgnn_option): the shipped values are the measured
+    winners — hub rows finished in the gather launch (27), the 16-B-gather weight gradient (28),
+    one workgroup per gather-list group (26 = 0) — and each round-trips through set / get."""
+    from mpgnn_amd import _lib
+    lib = _lib.lib
+    shipped = {26: 0, 27: 1, 28: 1}
+    for opt, v in shipped.items():
+        assert _lib.get_option(opt) == v, (opt, _lib.get_option(opt))
+    try:
+        for opt, v in ((26, 2), (27, 0), (28, 0)):
+            assert lib.mpgnn_set_option(opt, v) == 0 and _lib.get_option(opt) == v
+        assert lib.mpgnn_set_option(26, 65) == _lib.MPGNN_ERR_ARG  # 0..64 workgroups per CU
+    finally:
+        for opt, v in shipped.items():
+            lib.mpgnn_set_option(opt, v)
+
+
 def test_workspace_bytes_is_host_computable():
     import mpgnn_amd
     g = mpgnn_amd.data.config_graph("C1")
