@@ -721,9 +721,11 @@ def test_grad_x_hub_rows_finished_in_launch_equal_finalize():
 def test_weight_gradient_vector_gathers_equal_column_gathers(feat):
     """MPGNN_OPT_OUTER_VEC: outer_bf3v_kernel (16-B row gathers, row-major planes read with
     ds_read_b64_tr_b16) against outer_bf3_kernel (4-B column gathers, transposed planes): the
-    same bf16 pieces reach the matrix cores in the same k order, so dW and droot are
-    bit-identical; dbias sums each column in another (fixed) order: within 1e-6 normwise. C3
-    graph at F = 128; a sampled-relation graph at F = 256 (the four-quadrant launches)."""
+    same bf16 pieces reach the matrix cores, 16 rows per instruction in slice order, so dW and
+    droot agree to the matrix cores' in-instruction rounding (held to 1e-6 normwise; both are
+    held to the oracle's bar elsewhere); dbias sums each column in another fixed order. Each
+    kernel is bitwise repeatable. C3 graph at F = 128; a synthetic graph at F = 256 (the
+    four-quadrant launches)."""
     from mpgnn_amd import _lib
     if feat == 128:
         g = data.fb15k237_graph(feat_dim=128, seed=0, recipe="survey")
@@ -749,7 +751,9 @@ def test_weight_gradient_vector_gathers_equal_column_gathers(feat):
                 assert torch.equal(got[k], res[vec][k]), (vec, k, "not repeatable")
         res[vec] = got
     for k in ("dW", "droot"):
-        assert torch.equal(res[1][k], res[0][k]), f"{k} differs between the two weight-gradient kernels"
+        nwk = normwise_err(res[1][k].cpu(), res[0][k].cpu())
+        record(f"{k} outer_bf3v vs outer_bf3 F={feat}", nwk, 1e-6, normwise=nwk)
+        assert nwk <= 1e-6, (k, nwk)
     nw = normwise_err(res[1]["dbias"].cpu(), res[0]["dbias"].cpu())
     record(f"dbias outer_bf3v vs outer_bf3 F={feat}", nw, 1e-6, normwise=nw)
     assert nw <= 1e-6, nw
