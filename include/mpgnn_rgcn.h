@@ -377,9 +377,13 @@ enum mpgnn_option {
     MPGNN_OPT_FLAT_FUSE_SPLIT = 27, /* 1 (default): grad_x rows split over more than 16 chunks (hub nodes) are
                                     finished inside the gather-sum launch by the wave adding their last
                                     piece (same sums, same order); 0: finalize_rows_kernel after it */
-    MPGNN_OPT_OUTER_VEC = 28     /* 1 (default): the bf16-split weight-gradient kernel gathers rows 16 B per lane
+    MPGNN_OPT_OUTER_VEC = 28,    /* 1 (default): the bf16-split weight-gradient kernel gathers rows 16 B per lane
                                     and reads its column fragments with transposed LDS reads
                                     (outer_bf3v_kernel); 0: 4-B column gathers (outer_bf3_kernel) */
+    MPGNN_OPT_GEMM_SWITCH_COST = 29 /* the bf16-split GEMM's workgroup item ranges (K = 64, 128): 0 = equal item
+                                    counts; c > 0 = ranges balanced by items + (c / 100) per weight run, each
+                                    run paying an exposed weight-slice load (default 250: C3 forward GEMM
+                                    ~53 -> ~48.5 us, dgrad ~58 -> ~54 us; outputs bit-identical) */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

@@ -1051,6 +1051,7 @@ struct RelGemmArgs {
     int m_rows;           // CAT: rows of Hm (indices are clamped to the tables: a bad map cannot fault)
     const float* bias;    // nullable, CAT epilogue
     int relu;             // CAT epilogue: fused ReLU
+    const int* wg_items;  // nullable (rel_gemm_bf3_kernel): [G + 1] first item of each range
 #ifdef MPGNN_STAMPS
     unsigned long long* stamps;
 #endif
@@ -1677,8 +1678,10 @@ struct RelGemmBf3 {
         const int G = (int)gridDim.x;
         const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
         const int rng = g * q + min(g, rem) + ((int)blockIdx.x >> 3);
-        const int i_beg = (int)((long long)rng * n_items / G);
-        const int i_end = (int)((long long)(rng + 1) * n_items / G);
+        // equal item counts, or the host's cost-balanced ranges (a weight switch costs an exposed
+        // slice load: MPGNN_OPT_GEMM_SWITCH_COST)
+        const int i_beg = a.wg_items ? ld_uniform(a.wg_items, rng) : (int)((long long)rng * n_items / G);
+        const int i_end = a.wg_items ? ld_uniform(a.wg_items, rng + 1) : (int)((long long)(rng + 1) * n_items / G);
         if (i_beg >= i_end) return;
 
         // A rows are gathered TWO items ahead (the bf16 chain of an item is 2.67x shorter than the
@@ -4672,6 +4675,52 @@ static void launch_rel_gemm_bf3w(const RelGemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((rel_gemm_bf3w_kernel<DGRAD>), dim3(2 * pairs), dim3(512), lds, st, a);
 }
 
+static int g_gemm_switch_cost = 250;  // MPGNN_OPT_GEMM_SWITCH_COST: percent of an item (0 = equal item counts)
+
+// rel_gemm_bf3_kernel's item ranges balanced by cost = items + c · weight runs (each range pays
+// one exposed weight-slice load per run it holds); cached per plan, made outside captures
+// (nullptr: the kernel's equal split)
+static const int* gemm_ranges(const mpgnn_plan* p, int t_lo, int n_rel, int n_root, int G, hipStream_t st) {
+    if (g_gemm_switch_cost <= 0 || G <= 1) return nullptr;
+    const std::array<int64_t, 5> key{t_lo, n_rel, n_root, G, g_gemm_switch_cost};
+    std::lock_guard<std::mutex> lk(p->bw_mu);
+    auto it = p->gemm_ranges.find(key);
+    if (it != p->gemm_ranges.end()) return it->second;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    const int n = n_rel + n_root;
+    const double c = g_gemm_switch_cost / 100.0;
+    std::vector<double> cum(n + 1, 0.0);
+    int prev_w = -2;
+    for (int i = 0; i < n; ++i) {
+        int w = -1;  // root items
+        if (i < n_rel)
+            w = (int)(std::upper_bound(p->rel_t32_ptr.begin(), p->rel_t32_ptr.end(), t_lo + i) - p->rel_t32_ptr.begin());
+        cum[i + 1] = cum[i] + 1.0 + (w != prev_w ? c : 0.0);
+        prev_w = w;
+    }
+    std::vector<int> tab(G + 1, n);
+    tab[0] = 0;
+    int i = 0;
+    for (int k = 1; k < G; ++k) {
+        const double target = cum[n] * k / G;
+        while (i < n && cum[i] < target) ++i;
+        tab[k] = std::max(tab[k - 1], std::min(i, n));
+    }
+    int* dev = nullptr;
+    if (hipMalloc(&dev, tab.size() * sizeof(int)) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (hipMemcpy(dev, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(dev);
+        return nullptr;
+    }
+    p->gemm_ranges[key] = dev;
+    return dev;
+}
+
 static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, hipStream_t st) {
     if (g_gemm_bf3 && (K == 64 || K == 128) && a.node_map == nullptr) {
         if (K == 64) {
@@ -4933,6 +4982,8 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
 #ifdef MPGNN_STAMPS
         r.stamps = gather_kind == 1 ? nullptr : g_stamps_host;
 #endif
+        if (g_gemm_bf3 && (K == 64 || K == 128) && r.node_map == nullptr)
+            r.wg_items = gemm_ranges(p, r.t_lo, r.n_rel, r.n_root, std::min(r.n_rel + r.n_root, cu_count() * 2), strm);
         TimedLaunch tl(kind, strm);
         launch_rel_gemm(r, K, gather_kind == 1, strm);
         return hip_check(hipGetLastError(), "rel_gemm_kernel launch");
@@ -5610,6 +5661,10 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
         case MPGNN_OPT_OUTER_VEC:
             g_outer_vec = value != 0;
             return MPGNN_OK;
+        case MPGNN_OPT_GEMM_SWITCH_COST:
+            if (value < 0 || value > 10000) return arg_error("MPGNN_OPT_GEMM_SWITCH_COST must be 0..10000 (percent of an item)");
+            g_gemm_switch_cost = (int)value;
+            return MPGNN_OK;
         case MPGNN_OPT_FLAT_WG_PER_CU:
             if (value < 0 || value > 64) return arg_error("MPGNN_OPT_FLAT_WG_PER_CU must be 0..64");
             g_flat_wg_per_cu = (int)value;
@@ -5643,6 +5698,7 @@ int32_t mpgnn_get_option(int32_t option, int64_t* value) {
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = g_flat_wg_per_cu; return MPGNN_OK;
         case MPGNN_OPT_FLAT_FUSE_SPLIT: *value = g_flat_fuse_split ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_OUTER_VEC: *value = g_outer_vec ? 1 : 0; return MPGNN_OK;
+        case MPGNN_OPT_GEMM_SWITCH_COST: *value = g_gemm_switch_cost; return MPGNN_OK;
         default: return arg_error("unknown option " + std::to_string(option));
     }
 }

@@ -759,6 +759,33 @@ def test_weight_gradient_vector_gathers_equal_column_gathers(feat):
     assert nw <= 1e-6, nw
 
 
+def test_gemm_item_ranges_do_not_change_results():
+    """MPGNN_OPT_GEMM_SWITCH_COST: the bf16-split GEMM's workgroup item ranges balanced by
+    items + weight switches (default) against equal item counts — each item's arithmetic is the
+    same wherever it runs, so the layer output and every gradient are bit-identical (C3)."""
+    from mpgnn_amd import _lib
+    g = data.fb15k237_graph(feat_dim=128, seed=0, recipe="survey")
+    N, R = g.num_nodes, g.num_relations
+    gen = torch.Generator().manual_seed(5)
+    W = (torch.rand((R, 128, 128), generator=gen) - 0.5) * 0.2
+    root = (torch.rand(128, 128, generator=gen) - 0.5) * 0.2
+    bias = torch.rand(128, generator=gen) - 0.5
+    gout = torch.randn(N, 128, generator=gen)
+    plan = mpgnn_amd.GraphPlan(g.edge_index.to(DEV), g.edge_type.to(DEV), N)
+    res = {}
+    for cost in (250, 0, 100):
+        _lib.set_option(29, cost)
+        xg = g.x.to(DEV).requires_grad_(True)
+        Wg, rg, bg = (t.to(DEV).requires_grad_(True) for t in (W, root, bias))
+        out = rgcn_conv(xg, Wg, rg, bg, plan, MODE_ALL, num_relations=R)
+        out.backward(gout.to(DEV))
+        torch.cuda.synchronize()
+        res[cost] = [out.detach(), xg.grad, Wg.grad, rg.grad, bg.grad]
+    for cost in (0, 100):
+        for k, a, b in zip(("out", "dx", "dW", "droot", "dbias"), res[cost], res[250]):
+            assert torch.equal(a, b), (cost, k)
+
+
 # ------------------------------------------------------------------------------------------
 # CustomFastRGCNConv (A7): transform-then-aggregate semantics on the same kernels
 # ------------------------------------------------------------------------------------------
