@@ -22,11 +22,12 @@ W = ((torch.rand((R, 128, 128), generator=gen) - 0.5) * 0.2).to(dev)
 root = ((torch.rand((128, 128), generator=gen) - 0.5) * 0.2).to(dev)
 bias = (torch.rand(128, generator=gen) - 0.5).to(dev)
 gout = torch.randn(N, 128, generator=gen).to(dev)
+OPT = int(os.environ.get("AB_OPT", "29"))  # option A/B'd (29: the switch cost)
 costs = [int(v) for v in sys.argv[1:]] or [0, 0, 50, 100]
 ref = None
 for rep in range(3):
     for c in costs:
-        _lib.set_option(29, c)
+        _lib.set_option(OPT, c)
         x = x0.clone().requires_grad_(True)
         Wg, rg, bg = (t.clone().requires_grad_(True) for t in (W, root, bias))
         out = rgcn_conv(x, Wg, rg, bg, plan, 1, num_relations=R)
@@ -51,6 +52,6 @@ for rep in range(3):
         for k in ("seg_fwd", "seg_dgrad"):
             ms, n = _lib.kernel_timing(k)
             res[k] = round(ms * 1e3 / max(n, 1), 2)
-        print(f"cost={c}: {res}", flush=True)
-_lib.set_option(29, 0)
+        print(f"option {OPT}={c}: {res}", flush=True)
+_lib.set_option(29, 250)
 print("done")
