@@ -382,8 +382,14 @@ enum mpgnn_option {
                                     (outer_bf3v_kernel); 0: 4-B column gathers (outer_bf3_kernel) */
     MPGNN_OPT_GEMM_SWITCH_COST = 29 /* the bf16-split GEMM's workgroup item ranges (K = 64, 128): 0 = equal item
                                     counts; c > 0 = ranges balanced by items + (c / 100) per weight run, each
-                                    run paying an exposed weight-slice load (default 250: C3 forward GEMM
-                                    ~53 -> ~48.5 us, dgrad ~58 -> ~54 us; outputs bit-identical) */
+                                    run paying an exposed weight-slice load (default 250: the round-5 A/B with
+                                    per-CU ranges, forward 47.4 -> 45.3 us against 85; outputs bit-identical) */,
+    MPGNN_OPT_GEMM_IL = 30       /* 1 (default): the bf16-split GEMM (K = 64, 128) commits the next item's tile in
+                                    parts scheduled among the MFMAs of the current item's k-steps; 0: the
+                                    round-4 skeleton (whole tile in one k-step); outputs bit-identical */,
+    MPGNN_OPT_GEMM_CU_PAIRS = 31 /* 1 (default): the bf16-split GEMM's item ranges are balanced per CU (the two
+                                    workgroups a CU runs take the halves of one CU range); 0: per workgroup;
+                                    outputs bit-identical */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

@@ -163,6 +163,19 @@ def _load():
 lib = _load()
 
 
+def _env_options() -> None:
+    """MPGNN_OPTS="id=value,..." (A/B scripts): options set once when the library is loaded."""
+    spec = os.environ.get("MPGNN_OPTS", "").strip()
+    for item in filter(None, (t.strip() for t in spec.split(","))):
+        k, _, v = item.partition("=")
+        st = lib.mpgnn_set_option(int(k), int(v))
+        if st != MPGNN_OK:
+            raise ValueError(f"MPGNN_OPTS {item!r}: {lib.mpgnn_last_error().decode(errors='replace')}")
+
+
+_env_options()
+
+
 def kernel_timing(kind: str) -> tuple[float, int]:
     """(total ms, launches) of one kernel kind since mpgnn_timing_reset (syncs its events)."""
     ms, n = ctypes.c_double(), ctypes.c_int64()

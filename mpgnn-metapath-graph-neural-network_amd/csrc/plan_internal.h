@@ -224,9 +224,13 @@ struct mpgnn_plan {
     mutable std::mutex bw_mu;
     mutable std::map<std::array<int64_t, 8>, BwSlabs> bw_slabs;
     // rel_gemm_bf3_kernel's cost-balanced item ranges per (tile range, root items, grid, cost):
-    // [G + 1] first item of each range, on the device (made outside graph captures; freed with
-    // the plan)
-    mutable std::map<std::array<int64_t, 5>, int*> gemm_ranges;
+    // [G + 1] first item of each range, then [items] weight index of each item, on the device
+    // (made outside graph captures, uploaded from the pinned copy; both freed with the plan)
+    struct GemmRanges {
+        int* dev = nullptr;
+        int* host = nullptr;  // pinned
+    };
+    mutable std::map<std::array<int64_t, 5>, GemmRanges> gemm_ranges;
 };
 
 namespace mpgnn {

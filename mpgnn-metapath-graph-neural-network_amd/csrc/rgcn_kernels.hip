@@ -1052,6 +1052,7 @@ struct RelGemmArgs {
     const float* bias;    // nullable, CAT epilogue
     int relu;             // CAT epilogue: fused ReLU
     const int* wg_items;  // nullable (rel_gemm_bf3_kernel): [G + 1] first item of each range
+    int wg_cus;           // > 0 with wg_items: G = 2·wg_cus, ranges 2c and 2c+1 belong to one CU (below)
 #ifdef MPGNN_STAMPS
     unsigned long long* stamps;
 #endif
@@ -1060,11 +1061,13 @@ struct RelGemmArgs {
 #ifdef MPGNN_STAMPS
 // Debug build only (csrc/Makefile `stamps`): per wave and item, shader-clock stamps of the
 // phases of rel_gemm_kernel, written by lane 0 with vector stores (scripts/stamps_gemm.py).
-constexpr int kStampItems = 32, kStampPhases = 6;
+constexpr int kStampItems = 32, kStampPhases = 8;  // row 0: HW_ID, XCC_ID, start, 3 prologue, rt start, rt end
 static unsigned long long* g_stamps_host = nullptr;  // set by mpgnn_debug_stamps_set, passed as an argument
 #define MPGNN_STAMP_PTR a.stamps
 #define stamp(k, ph) stamp_at(a.stamps, k, ph)
 #define stamp_id() stamp_id_at(a.stamps)
+#define stamp_pro(k) stamp_pro_at(a.stamps, k)
+#define stamp_end() stamp_end_at(a.stamps)
 __device__ __forceinline__ void stamp_at(unsigned long long* g_stamps, int k, int ph) {
     if (g_stamps != nullptr && (threadIdx.x & 63) == 0 && k < kStampItems) {
         const size_t w = (size_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
@@ -1078,11 +1081,27 @@ __device__ __forceinline__ void stamp_id_at(unsigned long long* g_stamps) {
         o[0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
         o[1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
         o[2] = __builtin_readcyclecounter();
+        o[6] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+__device__ __forceinline__ void stamp_end_at(unsigned long long* g_stamps) {
+    if (g_stamps != nullptr && (threadIdx.x & 63) == 0) {
+        const size_t w = (size_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+        g_stamps[w * (kStampItems + 1) * kStampPhases + 7] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+// prologue stamps: row 0 slots 3..5 of the wave
+__device__ __forceinline__ void stamp_pro_at(unsigned long long* g_stamps, int k) {
+    if (g_stamps != nullptr && (threadIdx.x & 63) == 0) {
+        const size_t w = (size_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+        g_stamps[w * (kStampItems + 1) * kStampPhases + k] = __builtin_readcyclecounter();
     }
 }
 #else
 #define stamp(k, ph) ((void)0)
 #define stamp_id() ((void)0)
+#define stamp_pro(k) ((void)0)
+#define stamp_end() ((void)0)
 #endif
 
 // REPI: the mode-SINGLE root epilogue (RelGemmArgs::node_map, forward only) — its own
@@ -1592,6 +1611,16 @@ __global__ __launch_bounds__(kThreads, OCC) void rel_gemm_kernel(RelGemmArgs a) 
 // ----------------------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// Workgroup → item range when the host balanced the ranges per CU (gemm_ranges, G = 2·C
+// workgroups on C CUs): blocks b and b + C run on one CU (the dispatcher fills every CU's first
+// slot before any second one — observed on MI355X, speed only, never correctness); the CU's two
+// workgroups take the two halves 2c, 2c + 1 of CU range c, and CU ranges are consecutive on an XCD
+// (blocks b ≡ x mod 8 share XCD x).
+__device__ __forceinline__ int wg_pair_range(int b, int C) {
+    const int cu = b % C, half = b / C;
+    return 2 * ((cu & 7) * (C >> 3) + (cu >> 3)) + half;
+}
+
 __device__ __forceinline__ void split3_bf16(float a, __bf16& h0, __bf16& h1, __bf16& h2) {
     h0 = (__bf16)a;               // v_cvt_pk_bf16_f32: round to nearest even
     const float r1 = a - (float)h0;  // exact
@@ -1637,9 +1666,8 @@ struct RelGemmBf3 {
     }
 
     // the wave's weight slice as bf16 pieces: b[s][p][j] = piece p of B(16s + 8h + j, 32·wave + c)
-    __device__ static __forceinline__ void load_b(const float* w, int wave, int lane, bf16x8 (&b)[NS][3]) {
+    __device__ static __forceinline__ void load_b_raw(const float* w, int wave, int lane, float (&f)[NS][8]) {
         const int c = lane & 31, h = lane >> 5;
-        float f[NS][8];
         if constexpr (!DGRAD) {
             const float* p = w + (size_t)(8 * h) * N + wave * 32 + c;
 #pragma unroll
@@ -1656,6 +1684,8 @@ struct RelGemmBf3 {
                 f[s][4] = t1.x; f[s][5] = t1.y; f[s][6] = t1.z; f[s][7] = t1.w;
             }
         }
+    }
+    __device__ static __forceinline__ void split_b(const float (&f)[NS][8], bf16x8 (&b)[NS][3]) {
 #pragma unroll
         for (int s = 0; s < NS; ++s)
 #pragma unroll
@@ -1667,6 +1697,194 @@ struct RelGemmBf3 {
                 b[s][2][j] = h2;
             }
     }
+    __device__ static __forceinline__ void load_b(const float* w, int wave, int lane, bf16x8 (&b)[NS][3]) {
+        float f[NS][8];
+        load_b_raw(w, wave, lane, f);
+        split_b(f, b);
+    }
+
+    // one float4 of the next item's A tile (thread part j) split into the LDS planes; rows past
+    // nrows are zeros. No branch: the k-step that carries it stays one scheduling region.
+    __device__ static __forceinline__ void commit_part(int j, int tid, int nrows, const float4& v, __bf16* A) {
+        constexpr int W4 = K / 4;
+        const int e = tid + j * kThreads;
+        const int r = e / W4;
+        const float4 x = r < nrows ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+        __bf16 p0[4], p1[4], p2[4];
+        split3_bf16(x.x, p0[0], p1[0], p2[0]);
+        split3_bf16(x.y, p0[1], p1[1], p2[1]);
+        split3_bf16(x.z, p0[2], p1[2], p2[2]);
+        split3_bf16(x.w, p0[3], p1[3], p2[3]);
+        __bf16* d = A + r * LDAB + (e % W4) * 4;
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<bf16x4*>(d) = bf16x4{p0[0], p0[1], p0[2], p0[3]};
+        *reinterpret_cast<bf16x4*>(d + PLANE) = bf16x4{p1[0], p1[1], p1[2], p1[3]};
+        *reinterpret_cast<bf16x4*>(d + 2 * PLANE) = bf16x4{p2[0], p2[1], p2[2], p2[3]};
+    }
+
+    // Interleaved item skeleton (round 5): the same items, gathers, products and stores as run(),
+    // bit-identical outputs, but the next item's tile commit is cut into its WPT float4 parts and
+    // each part is scheduled INSIDE one k-step among that k-step's six MFMAs (sched_group_barrier:
+    // the next k-step's three fragment reads first, then MFMA / VALU / LDS-write / store groups),
+    // and the k-steps carry no branch. run() committed the whole tile in one k-step as ~150 VALU
+    // instructions in a row (waiting on its rows), during which the wave issued no MFMA.
+    __device__ static void run_il(const RelGemmArgs& a, __bf16* smem) {
+        __bf16* As = smem;                                            // [2][3 planes][32][LDAB]
+        float* Sc = reinterpret_cast<float*>(smem + 2 * 3 * PLANE);  // [2][32] dgrad row scales
+        const int tid = threadIdx.x;
+        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int n_items = a.n_rel + a.n_root;
+        const int G = (int)gridDim.x;
+        const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
+        const int rng = a.wg_cus > 0 ? wg_pair_range((int)blockIdx.x, a.wg_cus) : g * q + min(g, rem) + ((int)blockIdx.x >> 3);
+        const int i_beg = a.wg_items ? ld_uniform(a.wg_items, rng) : (int)((long long)rng * n_items / G);
+        const int i_end = a.wg_items ? ld_uniform(a.wg_items, rng + 1) : (int)((long long)(rng + 1) * n_items / G);
+        if (i_beg >= i_end) return;
+        stamp_id();
+
+        // Prologue (round 5): the stamps showed ~10k cycles from the launch to the first item —
+        // six dependent round trips (range, tile rows, s_rel, s_src, rows, then the weight slice).
+        // Now: the item table reads each item's weight index from the range table (no s_rel
+        // hop), the row numbers of the first three items are requested together, the weight
+        // slice is requested beside them and split while the first rows are in flight.
+        ItemTable tab;
+        {
+            const int i = min(i_beg + lane, i_end - 1);
+            if (i < a.n_rel) {
+                tab.r0 = a.t_begin[a.t_lo + i];
+                tab.nrows = a.t_end[a.t_lo + i] - tab.r0;
+                tab.wrel = a.w_per_rel ? (a.wg_items ? a.wg_items[G + 1 + i] : a.s_rel[tab.r0]) : 0;
+            } else {
+                tab.r0 = a.row_lo + (i - a.n_rel) * 32;
+                tab.nrows = min(32, a.row_hi - tab.r0);
+                tab.wrel = -1;
+            }
+        }
+        auto get_item = [&](int i) { return i - i_beg < 64 ? Base::item_at(a, tab, i - i_beg) : Base::item(a, i); };
+        Item cur = get_item(i_beg);
+        float4 va[WPT], vb[WPT];
+        int cnta = 1, cntb = 1, zm = 0;
+        int nrow[WPT];
+        int ncnt = 1;
+        int crow[WPT], c0;
+        int r1[WPT];
+        Base::gather_idx(a, cur, tid, crow, c0);
+        Base::gather_idx(a, get_item(min(i_beg + 1, i_end - 1)), tid, r1, cnta);
+        Base::gather_idx(a, get_item(min(i_beg + 2, i_end - 1)), tid, nrow, ncnt);
+        float wf[NS][8];
+        load_b_raw(cur.w, wave, lane, wf);
+        Base::issue_rows(a, tid, crow, vb, zm);
+        stamp_pro(3);
+        Base::issue_rows(a, tid, r1, va, zm);
+        bf16x8 b[NS][3];
+        split_b(wf, b);
+        stamp_pro(4);
+        commit(cur, tid, vb, c0, As, Sc);
+        stamp_pro(5);
+        __syncthreads();
+
+        constexpr int SPG = (16 + NS - 1) / NS;  // previous item's stores per k-step
+        // store offsets: lane part (column, lane half) in a VGPR, row part (r) a constant soffset
+        const int col_b = (wave * 32 + c) * 4 + h * (4 * N * 4);
+        float prev[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) prev[r] = 0.0f;
+        __amdgpu_buffer_rsrc_t prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.Y, (short)0, 0, 0x00020000);
+        int buf = 0;
+        auto step = [&](int i, float4 (&vc)[WPT], int& cntc, float4 (&vn)[WPT], int& cntn) {
+            stamp(i - i_beg, 0);
+            const bool has_next = i + 1 < i_end;
+            const Item nxt = has_next ? get_item(i + 1) : cur;
+            {  // unconditional (past the range: the last item's rows again), so no register
+               // shuffle waits on these loads at the top of the item
+                int zn;
+                Base::issue_rows(a, tid, nrow, vn, zn);
+                cntn = ncnt;
+                Base::gather_idx(a, get_item(min(i + 3, i_end - 1)), tid, nrow, ncnt);
+            }
+            const bool new_w = nxt.w != cur.w;
+            const int nr = has_next ? nxt.nrows : 0;  // last item: the commit writes zeros nobody reads
+            const __bf16* Ab = As + buf * 3 * PLANE + c * LDAB + 8 * h;
+            __bf16* An = As + (buf ^ 1) * 3 * PLANE;
+            if constexpr (DGRAD) Sc[(buf ^ 1) * 32 + (tid & 31)] = 1.0f / (float)cntc;  // same value per tid & 31
+            f32x16 hi, lo;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                hi[r] = 0.0f;
+                lo[r] = 0.0f;
+            }
+            bf16x8 f0 = *reinterpret_cast<const bf16x8*>(Ab);
+            bf16x8 f1 = *reinterpret_cast<const bf16x8*>(Ab + PLANE);
+            bf16x8 f2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * PLANE);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const bf16x8 a0 = f0, a1 = f1, a2 = f2;
+                if (s + 1 < NS) {
+                    f0 = *reinterpret_cast<const bf16x8*>(Ab + 16 * (s + 1));
+                    f1 = *reinterpret_cast<const bf16x8*>(Ab + PLANE + 16 * (s + 1));
+                    f2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * PLANE + 16 * (s + 1));
+                }
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[s][0], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][1], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][2], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][0], lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][1], lo, 0, 0, 0);
+                hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][0], hi, 0, 0, 0);
+#pragma unroll
+                for (int u = 0; u < SPG; ++u) {
+                    const int r = s * SPG + u;
+                    if (r < 16)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(prev[r]), prev_rsrc, col_b,
+                                                              ((r & 3) + 8 * (r >> 2)) * (N * 4), 16);
+                }
+                // parts of the next tile: part j in k-step 1 + j·NS / WPT
+#pragma unroll
+                for (int j = 0; j < WPT; ++j)
+                    if (s == 1 + (j * NS) / WPT) commit_part(j, tid, nr, vc[j], An);
+                if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // next fragments
+#pragma unroll
+                for (int m = 0; m < 6; ++m) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // VALU
+                    if (m < 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // LDS write
+                    if (m < SPG) __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);  // store
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            stamp(i - i_beg, 1);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                prev[r] = hi[r] + lo[r];
+                if constexpr (DGRAD) {
+                    if (!cur.root) prev[r] = prev[r] * Sc[buf * 32 + (r & 3) + 8 * (r >> 2) + 4 * h];
+                }
+            }
+            {
+                float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
+                const int bytes = __builtin_amdgcn_readfirstlane(cur.nrows) * N * 4;
+                prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(Yt, (short)0, bytes, 0x00020000);
+            }
+            if (new_w) {
+                stamp(i - i_beg, 2);
+                load_b(nxt.w, wave, lane, b);
+            }
+            stamp(i - i_beg, 3);
+            __syncthreads();
+            stamp(i - i_beg, 4);
+            cur = nxt;
+            buf ^= 1;
+        };
+        for (int i = i_beg; i < i_end; i += 2) {
+            step(i, va, cnta, vb, cntb);
+            if (i + 1 < i_end) step(i + 1, vb, cntb, va, cnta);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(prev[r]), prev_rsrc, col_b, ((r & 3) + 8 * (r >> 2)) * (N * 4), 16);
+        stamp_end();
+    }
 
     __device__ static void run(const RelGemmArgs& a, __bf16* smem) {
         __bf16* As = smem;                                            // [2][3 planes][32][LDAB]
@@ -1677,7 +1895,7 @@ struct RelGemmBf3 {
         const int n_items = a.n_rel + a.n_root;
         const int G = (int)gridDim.x;
         const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
-        const int rng = g * q + min(g, rem) + ((int)blockIdx.x >> 3);
+        const int rng = a.wg_cus > 0 ? wg_pair_range((int)blockIdx.x, a.wg_cus) : g * q + min(g, rem) + ((int)blockIdx.x >> 3);
         // equal item counts, or the host's cost-balanced ranges (a weight switch costs an exposed
         // slice load: MPGNN_OPT_GEMM_SWITCH_COST)
         const int i_beg = a.wg_items ? ld_uniform(a.wg_items, rng) : (int)((long long)rng * n_items / G);
@@ -1794,10 +2012,11 @@ struct RelGemmBf3 {
     }
 };
 
-template <int KB, bool DGRAD>
+template <int KB, bool DGRAD, bool IL = false>
 __global__ __launch_bounds__(kThreads, 2) void rel_gemm_bf3_kernel(RelGemmArgs a) {
     extern __shared__ __bf16 smem_bf[];
-    RelGemmBf3<KB, DGRAD>::run(a, smem_bf);
+    if constexpr (IL) RelGemmBf3<KB, DGRAD>::run_il(a, smem_bf);
+    else RelGemmBf3<KB, DGRAD>::run(a, smem_bf);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -4657,11 +4876,14 @@ static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
 static bool g_gemm_bf3 = true;  // MPGNN_OPT_GEMM_BF3: K ∈ {64, 128}, N = 128 on the bf16 matrix cores (3-way split)
 static bool g_bwd_fused = true;  // MPGNN_OPT_BWD_FUSED: see bwd_bf3_kernel
 
+static bool g_gemm_il = true;  // MPGNN_OPT_GEMM_IL: the interleaved item skeleton (RelGemmBf3::run_il)
+
 template <int KB, bool DGRAD>
 static void launch_rel_gemm_bf3(const RelGemmArgs& a, hipStream_t st) {
     const size_t lds = RelGemmBf3<KB, DGRAD>::lds_bytes();
     const int grid = std::min(a.n_rel + a.n_root, cu_count() * 2);  // two workgroups per CU
-    hipLaunchKernelGGL((rel_gemm_bf3_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
+    if (g_gemm_il) hipLaunchKernelGGL((rel_gemm_bf3_kernel<KB, DGRAD, true>), dim3(grid), dim3(kThreads), lds, st, a);
+    else hipLaunchKernelGGL((rel_gemm_bf3_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
 // K = N = 256: one 512-thread workgroup per CU; column-block pairs on one XCD (grid a multiple of
@@ -4676,49 +4898,85 @@ static void launch_rel_gemm_bf3w(const RelGemmArgs& a, hipStream_t st) {
 }
 
 static int g_gemm_switch_cost = 250;  // MPGNN_OPT_GEMM_SWITCH_COST: percent of an item (0 = equal item counts)
+static bool g_gemm_cu_pairs = true;  // MPGNN_OPT_GEMM_CU_PAIRS: ranges balanced per CU (two workgroups each)
 
 // rel_gemm_bf3_kernel's item ranges balanced by cost = items + c · weight runs (each range pays
-// one exposed weight-slice load per run it holds); cached per plan, made outside captures
-// (nullptr: the kernel's equal split)
-static const int* gemm_ranges(const mpgnn_plan* p, int t_lo, int n_rel, int n_root, int G, hipStream_t st) {
+// one exposed weight-slice load per run it holds), followed by every item's weight index (the
+// relation value of its tiles, -1 for root items) so that the kernel's item table needs no
+// dependent s_rel load. Cached per plan; made outside captures (nullptr: the kernel's equal split
+// and s_rel lookups). Uploaded with an asynchronous copy on the caller's stream from a pinned
+// buffer the plan keeps (no device-wide synchronisation, ordered before the kernel reading it).
+static const int* gemm_ranges(const mpgnn_plan* p, int t_lo, int n_rel, int n_root, int G, bool pairs,
+                              hipStream_t st) {
     if (g_gemm_switch_cost <= 0 || G <= 1) return nullptr;
-    const std::array<int64_t, 5> key{t_lo, n_rel, n_root, G, g_gemm_switch_cost};
+    const std::array<int64_t, 5> key{t_lo, n_rel, n_root, G * 2 + (pairs ? 1 : 0), g_gemm_switch_cost};
     std::lock_guard<std::mutex> lk(p->bw_mu);
     auto it = p->gemm_ranges.find(key);
-    if (it != p->gemm_ranges.end()) return it->second;
+    if (it != p->gemm_ranges.end()) return it->second.dev;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
     const int n = n_rel + n_root;
     const double c = g_gemm_switch_cost / 100.0;
     std::vector<double> cum(n + 1, 0.0);
+    std::vector<int> wrel(n, -1);
     int prev_w = -2;
     for (int i = 0; i < n; ++i) {
         int w = -1;  // root items
-        if (i < n_rel)
-            w = (int)(std::upper_bound(p->rel_t32_ptr.begin(), p->rel_t32_ptr.end(), t_lo + i) - p->rel_t32_ptr.begin());
+        if (i < n_rel) {
+            const int d = (int)(std::upper_bound(p->rel_t32_ptr.begin(), p->rel_t32_ptr.end(), t_lo + i) -
+                                p->rel_t32_ptr.begin()) - 1;
+            w = d;
+            wrel[i] = (d >= 0 && d < (int)p->rel_val32.size()) ? p->rel_val32[d] : 0;
+        }
         cum[i + 1] = cum[i] + 1.0 + (w != prev_w ? c : 0.0);
         prev_w = w;
     }
-    std::vector<int> tab(G + 1, n);
+    const size_t words = (size_t)G + 1 + (size_t)n;
+    mpgnn_plan::GemmRanges e;
+    if (hipHostMalloc(reinterpret_cast<void**>(&e.host), words * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    int* tab = e.host;
+    // boundaries of `parts` ranges of [lo, hi) with equal cost (first item whose cost prefix
+    // reaches the target)
+    auto split = [&](int lo, int hi, int parts, int* out) {
+        int i = lo;
+        for (int k = 1; k < parts; ++k) {
+            const double target = cum[lo] + (cum[hi] - cum[lo]) * k / parts;
+            while (i < hi && cum[i] < target) ++i;
+            out[k] = std::max(out[k - 1], std::min(i, hi));
+        }
+    };
     tab[0] = 0;
-    int i = 0;
-    for (int k = 1; k < G; ++k) {
-        const double target = cum[n] * k / G;
-        while (i < n && cum[i] < target) ++i;
-        tab[k] = std::max(tab[k - 1], std::min(i, n));
+    tab[G] = n;
+    if (pairs) {  // CU ranges first, then each CU range in two halves (its two workgroups)
+        std::vector<int> cu(G / 2 + 1, n);
+        cu[0] = 0;
+        split(0, n, G / 2, cu.data());
+        for (int c = 0; c < G / 2; ++c) {
+            tab[2 * c] = cu[c];
+            int two[2] = {cu[c], cu[c]};
+            split(cu[c], cu[c + 1], 2, two);
+            tab[2 * c + 1] = two[1];
+        }
+    } else {
+        split(0, n, G, tab);
     }
-    int* dev = nullptr;
-    if (hipMalloc(&dev, tab.size() * sizeof(int)) != hipSuccess) {
+    std::copy(wrel.begin(), wrel.end(), tab + G + 1);
+    if (hipMalloc(reinterpret_cast<void**>(&e.dev), words * sizeof(int)) != hipSuccess) {
         (void)hipGetLastError();
+        (void)hipHostFree(e.host);
         return nullptr;
     }
-    if (hipMemcpy(dev, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpyAsync(e.dev, e.host, words * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
         (void)hipGetLastError();
-        (void)hipFree(dev);
+        (void)hipFree(e.dev);
+        (void)hipHostFree(e.host);
         return nullptr;
     }
-    p->gemm_ranges[key] = dev;
-    return dev;
+    p->gemm_ranges[key] = e;
+    return e.dev;
 }
 
 static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, hipStream_t st) {
@@ -4982,8 +5240,12 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
 #ifdef MPGNN_STAMPS
         r.stamps = gather_kind == 1 ? nullptr : g_stamps_host;
 #endif
-        if (g_gemm_bf3 && (K == 64 || K == 128) && r.node_map == nullptr)
-            r.wg_items = gemm_ranges(p, r.t_lo, r.n_rel, r.n_root, std::min(r.n_rel + r.n_root, cu_count() * 2), strm);
+        if (g_gemm_bf3 && (K == 64 || K == 128) && r.node_map == nullptr) {
+            const int G = std::min(r.n_rel + r.n_root, cu_count() * 2);
+            const bool pairs = g_gemm_cu_pairs && G == cu_count() * 2 && cu_count() % 8 == 0;
+            r.wg_items = gemm_ranges(p, r.t_lo, r.n_rel, r.n_root, G, pairs, strm);
+            r.wg_cus = (pairs && r.wg_items != nullptr) ? cu_count() : 0;
+        }
         TimedLaunch tl(kind, strm);
         launch_rel_gemm(r, K, gather_kind == 1, strm);
         return hip_check(hipGetLastError(), "rel_gemm_kernel launch");
@@ -5651,6 +5913,12 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
         case MPGNN_OPT_GEMM_BF3:
             g_gemm_bf3 = value != 0;
             return MPGNN_OK;
+        case MPGNN_OPT_GEMM_IL:
+            g_gemm_il = value != 0;
+            return MPGNN_OK;
+        case MPGNN_OPT_GEMM_CU_PAIRS:
+            g_gemm_cu_pairs = value != 0;
+            return MPGNN_OK;
         case MPGNN_OPT_BWD_FUSED:
             g_bwd_fused = value != 0;
             return MPGNN_OK;
@@ -5694,6 +5962,8 @@ int32_t mpgnn_get_option(int32_t option, int64_t* value) {
         case MPGNN_OPT_REL_WIDE: *value = g_rel_wide ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_CHUNK_ROWS: *value = g_chunk_rows; return MPGNN_OK;
         case MPGNN_OPT_GEMM_BF3: *value = g_gemm_bf3 ? 1 : 0; return MPGNN_OK;
+        case MPGNN_OPT_GEMM_IL: *value = g_gemm_il ? 1 : 0; return MPGNN_OK;
+        case MPGNN_OPT_GEMM_CU_PAIRS: *value = g_gemm_cu_pairs ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_BWD_FUSED: *value = g_bwd_fused ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = g_flat_wg_per_cu; return MPGNN_OK;
         case MPGNN_OPT_FLAT_FUSE_SPLIT: *value = g_flat_fuse_split ? 1 : 0; return MPGNN_OK;

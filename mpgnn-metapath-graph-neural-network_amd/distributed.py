@@ -195,8 +195,8 @@ class ShardGradReducer:
         self.params = [p for p in params if p is not None]
         self.group = group
         self.flat = None
-        self.taps = 0       # grad-enabled forwards since the last reduction
-        self.deposits = 0   # tap backwards since the last reduction
+        self.outstanding = 0  # grad-enabled forwards (taps) whose backward has not deposited yet
+        self.deposits = 0     # deposits in the buffer since it was last reduced
         self.work = None
 
     def tap(self, *params):
@@ -204,7 +204,7 @@ class ShardGradReducer:
         live = [p for p in params if p is not None and p.requires_grad]
         if not live:
             return params
-        self.taps += 1
+        self.outstanding += 1
         out = iter(_GradTap.apply(self, *live))
         return tuple(next(out) if (p is not None and p.requires_grad) else p for p in params)
 
@@ -224,6 +224,11 @@ class ShardGradReducer:
             torch.autograd.Variable._execution_engine.queue_callback(ShardGradReducer._finish_all)
         if self not in ShardGradReducer._pending:
             ShardGradReducer._pending.append(self)
+        if self.work is not None:
+            # a reduction of earlier deposits is still reading and writing the buffer (a use that
+            # was not counted: retain_graph=True backward again, or forwards interleaved with
+            # backwards): fold its sums into .grad first, then the buffer starts over
+            self._drain()
         views = self._layout()
         first = self.deposits == 0
         for (p, v), g in zip(views, grads):
@@ -235,31 +240,41 @@ class ShardGradReducer:
             else:
                 v.add_(g)
         self.deposits += 1
-        if self.work is None and self.deposits >= self.taps:
-            self._launch()  # every use deposited: reduce now, behind the earlier layers' backward
+        if self.outstanding > 0:
+            self.outstanding -= 1
+            if self.outstanding == 0:
+                self._launch()  # every counted use deposited: reduce now, behind the earlier layers' backward
 
     def _launch(self):
         import torch.distributed as dist
         self.work = dist.all_reduce(self.flat, group=self.group, async_op=True)
 
+    def _drain(self):
+        """Wait for the in-flight reduction (the stream waits; NCCL: no host block) and add its
+        sums into param.grad (assigned when None); the buffer is free afterwards."""
+        self.work.wait()
+        self.work = None
+        for p, v in self._layout():
+            if p.grad is None:
+                p.grad = v.clone()
+            else:
+                p.grad.add_(v)
+        self.deposits = 0
+
     @staticmethod
     def _finish_all():
         """End of the backward: reduce what has not been, make the stream wait for every
-        reduction, then add the sums into param.grad. Same order on every rank."""
+        reduction, then add the sums into param.grad. Same order on every rank. Uses counted by
+        forwards whose backward did not run in this pass are forgotten: the next backward
+        launches its reduction here, at its end (correct, without the overlap)."""
         pending, ShardGradReducer._pending = ShardGradReducer._pending, []
         for r in pending:
-            if r.work is None:
+            if r.work is None and r.deposits > 0:
                 r._launch()
         for r in pending:
-            r.work.wait()
-            r.work = None
-            for p, v in r._layout():
-                if p.grad is None:
-                    p.grad = v.clone()
-                else:
-                    p.grad.add_(v)
-            r.taps = 0
-            r.deposits = 0
+            if r.work is not None:
+                r._drain()
+            r.outstanding = 0
 
     def remove(self):
         """Kept for callers of the hook-based reducer: nothing is registered on the params."""

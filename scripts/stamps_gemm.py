@@ -17,7 +17,7 @@ import torch  # noqa: E402
 import mpgnn_amd  # noqa: E402
 from mpgnn_amd import _lib, data  # noqa: E402
 
-ITEMS, PH = 32, 6
+ITEMS, PH = 32, 8
 g = data.fb15k237_graph(feat_dim=128)
 dev = torch.device("cuda", 0)
 torch.manual_seed(10)

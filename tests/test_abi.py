@@ -88,17 +88,18 @@ def test_withdrawn_option_is_refused():
 
 
 def test_round4_switches_default_on_and_round_trip():
-    """The round-4 A/B switches (header enum mpgnn_option): the shipped values are the measured
+    """The round-4 / round-5 A/B switches (header enum mpgnn_option): the shipped values are the measured
     winners — hub rows finished in the gather launch (27), the 16-B-gather weight gradient (28),
     one workgroup per gather-list group (26 = 0), GEMM item ranges balanced with a weight switch
-    priced at 2.5 items (29 = 250) — and each round-trips through set / get."""
+    priced at 2.5 items (29 = 250), the interleaved GEMM item skeleton (30) and per-CU item ranges (31)
+    — and each round-trips through set / get."""
     from mpgnn_amd import _lib
     lib = _lib.lib
-    shipped = {26: 0, 27: 1, 28: 1, 29: 250}
+    shipped = {26: 0, 27: 1, 28: 1, 29: 250, 30: 1, 31: 1}
     for opt, v in shipped.items():
         assert _lib.get_option(opt) == v, (opt, _lib.get_option(opt))
     try:
-        for opt, v in ((26, 2), (27, 0), (28, 0), (29, 0)):
+        for opt, v in ((26, 2), (27, 0), (28, 0), (29, 0), (30, 0), (31, 0)):
             assert lib.mpgnn_set_option(opt, v) == 0 and _lib.get_option(opt) == v
         assert lib.mpgnn_set_option(26, 65) == _lib.MPGNN_ERR_ARG  # 0..64 workgroups per CU
     finally:

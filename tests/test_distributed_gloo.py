@@ -165,6 +165,29 @@ def _reducer_worker(rank, world, port, q):
                 for pa, pb, pn in zip(a, b, ("weight", "root", "bias")):
                     if not torch.allclose(pa, pb, rtol=1e-6, atol=1e-6):
                         msgs.append(f"{name} iter {it} {pn}: {float((pa - pb).abs().max()):.3e}")
+        # uses the reducer did not count — retain_graph=True and a second
+        # backward of the same graph; two forwards before their backwards. Each deposit must land
+        # in a buffer no reduction is reading, and every use be reduced exactly once.
+        def twice(layer, retain):
+            layer.zero_grad(set_to_none=True)
+            if retain:
+                out = layer(layer(xs[rank]))
+                out.sum().backward(retain_graph=True)
+                (out * 2).sum().backward()
+            else:
+                out_a = layer(layer(xs[rank]))
+                out_b = layer(layer(xs[rank]))
+                out_a.sum().backward()
+                (out_b * 2).sum().backward()
+            return [p.grad.clone() for p in (layer.weight, layer.root, layer.bias)]
+        for retain in (True, False):
+            ref3 = twice(Layer(False), retain)
+            for g_ in ref3:
+                dist.all_reduce(g_)
+            got3 = twice(Layer(True), retain)
+            for pa, pb, pn in zip(got3, ref3, ("weight", "root", "bias")):
+                if not torch.allclose(pa, pb, rtol=1e-6, atol=1e-6):
+                    msgs.append(f"retain={retain} {pn}: {float((pa - pb).abs().max()):.3e}")
         # a later UNSHARDED backward through the same parameters never touches the reducer
         lay = Layer(True)
         run(lay, 1)
