@@ -393,9 +393,18 @@ enum mpgnn_option {
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };
+/* Process defaults. The kernel switches (every option except TIMING_MASK, PLAN_THREADS and
+ * CHUNK_ROWS) are PER PLAN: a plan copies the defaults when it is created and is changed only by
+ * mpgnn_plan_set_option, so no launch reads process-wide state; mpgnn_set_option of a switch
+ * therefore affects plans created afterwards. TIMING_MASK (profiling) and PLAN_THREADS /
+ * CHUNK_ROWS (plan build parameters, read when a plan is built) stay process-wide. */
 int32_t mpgnn_set_option(int32_t option, int64_t value);
-/* Current value of an option (tests save and restore the shipped defaults around overrides). */
+/* Current default value of an option (tests save and restore the shipped defaults around overrides). */
 int32_t mpgnn_get_option(int32_t option, int64_t* value);
+/* One plan's kernel switch (MPGNN_ERR_ARG for the process-wide options). Not synchronised with
+ * launches on other threads that use the same plan: set switches before using the plan. */
+int32_t mpgnn_plan_set_option(mpgnn_plan* plan, int32_t option, int64_t value);
+int32_t mpgnn_plan_get_option(const mpgnn_plan* plan, int32_t option, int64_t* value);
 
 /* --- graph file reader --------------------------------------------------------------
  * link.dat (`node_1 \t relation \t node_2`, one edge per line) → the tensors of

@@ -99,6 +99,8 @@ SIGNATURES = [
     ("mpgnn_score_bag_argmax_bwd", _I32, [_P, _I64, _P, _P, _P, _P, _P, _P, _I32, _I64, _P, _P, _P, _P, _P, _P,
                                           _P]),
     ("mpgnn_set_option", _I32, [_I32, _I64]),
+    ("mpgnn_plan_set_option", _I32, [_P, _I32, _I64]),
+    ("mpgnn_plan_get_option", _I32, [_P, _I32, _PI64]),
     ("mpgnn_get_option", _I32, [_I32, _PI64]),
     ("mpgnn_timing_enable", _I32, [_I32]),
     ("mpgnn_debug_occupancy", _I32, [_I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
@@ -191,6 +193,8 @@ def get_option(option: int) -> int:
 
 
 def set_option(option: int, value: int) -> None:
+    """The process default of an option: kernel switches apply to plans created afterwards
+    (``GraphPlan.set_option`` changes one plan); see include/mpgnn_rgcn.h."""
     check(lib.mpgnn_set_option(int(option), int(value)), "mpgnn_set_option")
 
 

@@ -27,6 +27,9 @@ extern "C" int32_t mpgnn_get_option(int32_t option, int64_t* value) {
     return MPGNN_ERR_UNSUPPORTED;
 }
 
+// the plans of the host-only build carry the shipped kernel switches (there are no kernels)
+mpgnn::Options mpgnn::default_options() { return mpgnn::Options{}; }
+
 // no kernels in the host-only build: the plan's device node maps are not built (the fused
 // mode-SINGLE layer builds a relation's map per call when they are absent)
 int32_t mpgnn::build_rel_node_maps(mpgnn_plan*, void*) { return MPGNN_OK; }

@@ -694,6 +694,7 @@ int32_t mpgnn_plan_create_sharded(const int64_t* edge_index, const int64_t* edge
     if (shard_hi < shard_lo) shard_hi = shard_lo;
     mpgnn_plan* p = new (std::nothrow) mpgnn_plan();
     if (!p) return fail(MPGNN_ERR_ALLOC, "plan allocation failed");
+    p->opt = mpgnn::default_options();
     try {
         int32_t st = build(edge_index, edge_type, num_edges, num_nodes, shard_lo, shard_hi, side, p);
         if (st != MPGNN_OK) {

@@ -1121,6 +1121,7 @@ extern "C" int32_t mpgnn_plan_create_device(const int64_t* edge_index, const int
         set_last_error("plan allocation failed");
         return MPGNN_ERR_ALLOC;
     }
+    p->opt = mpgnn::default_options();
     int prev = 0;
     if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
         delete p;

@@ -14,6 +14,26 @@
 
 namespace mpgnn {
 
+// Kernel-path switches of ONE plan (header enum mpgnn_option). A plan copies the process
+// defaults (mpgnn_set_option) when it is created; mpgnn_plan_set_option changes that plan only,
+// so every launch is decided by the plan it runs on (no process-wide switch is read on the
+// compute path).
+struct Options {
+    bool exact_order = false;     // MPGNN_OPT_EXACT_ORDER: no ragged pieces anywhere
+    bool rel_gemm = true;         // MPGNN_OPT_REL_GEMM: B-stationary GEMM for K ∈ {64, 128}, N = 128
+    bool rel_wide = true;         // MPGNN_OPT_REL_WIDE: ... also for F_in = F_out = 256 (C5)
+    bool gemm_bf3 = true;         // MPGNN_OPT_GEMM_BF3: the GEMMs on the bf16 matrix cores (3-way split)
+    bool bwd_fused = true;        // MPGNN_OPT_BWD_FUSED: see bwd_bf3_kernel
+    bool flat_fuse_split = true;  // MPGNN_OPT_FLAT_FUSE_SPLIT: hub rows of grad_x finished in the gather launch
+    bool outer_vec = true;        // MPGNN_OPT_OUTER_VEC: outer_bf3v_kernel (16-B gathers, transposed LDS reads)
+    bool gemm_il = true;          // MPGNN_OPT_GEMM_IL: the interleaved GEMM item skeleton
+    bool gemm_cu_pairs = true;    // MPGNN_OPT_GEMM_CU_PAIRS: GEMM item ranges balanced per CU
+    int gemm_switch_cost = 250;   // MPGNN_OPT_GEMM_SWITCH_COST: percent of an item per weight switch
+    int flat_wg_per_cu = 0;       // MPGNN_OPT_FLAT_WG_PER_CU: persistent grid of flat_rows_kernel (0: off)
+};
+// a copy of the process defaults (rgcn_kernels.hip)
+Options default_options();
+
 // Segments are packed into relation-pure tiles of this many rows: one workgroup of the
 // segment-transform kernel owns one tile (rgcn_kernels.hip, seg_tile_kernel).
 constexpr int kTileRows = 64;
@@ -143,6 +163,7 @@ struct DeviceTables {
 }  // namespace mpgnn
 
 struct mpgnn_plan {
+    mpgnn::Options opt;  // this plan's kernel switches (copied from the process defaults at creation)
     int64_t N = 0;
     int64_t E_in = 0;
     int64_t E = 0;  // local edges kept

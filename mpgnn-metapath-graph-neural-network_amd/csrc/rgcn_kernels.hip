@@ -2408,9 +2408,15 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
     for (int i = i_beg; i < i_end; ++i) {
         const bool has_next = i + 1 < i_end;
         const __bf16* Ab = As + (buf * 2 + kh) * 3 * G::PLANE + c * G::LDAB + 8 * h;
-        f32x16 acc;
+        // the small products in their own accumulator (as rel_gemm_bf3_kernel): the a0·b0 chain
+        // rounds once per k-step at the sum's magnitude instead of six times (round 5: C5's
+        // grad_x was 2.2x the fp32 reference path's error off the float64 truth with one)
+        f32x16 acc, hi;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+        for (int r = 0; r < 16; ++r) {
+            acc[r] = 0.0f;
+            hi[r] = 0.0f;
+        }
         bf16x8 f0 = *reinterpret_cast<const bf16x8*>(Ab);
         bf16x8 f1 = *reinterpret_cast<const bf16x8*>(Ab + G::PLANE);
         bf16x8 f2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * G::PLANE);
@@ -2427,7 +2433,7 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][2], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][0], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][0], acc, 0, 0, 0);
+            hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][0], hi, 0, 0, 0);
             if (kh == 0) {  // item i-1's tile leaves two rows per k-step
                 store_prev(2 * s);
                 store_prev(2 * s + 1);
@@ -2438,6 +2444,8 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = hi[r] + acc[r];
         float* Oe = Ot + buf * 32 * G::LDO;
         if (kh == 1) {
 #pragma unroll
@@ -4825,8 +4833,6 @@ static void launch_tile_gemm_kb(const TileGemmArgs& a, hipStream_t st) {
 }
 
 
-static bool g_rel_wide = true;  // MPGNN_OPT_REL_WIDE: B-stationary GEMM also for F_in = F_out = 256 (C5)
-static bool g_rel_gemm = true;  // MPGNN_OPT_REL_GEMM: B-stationary GEMM for K ∈ {64, 128}, N = 128
 
 template <int KB, bool DGRAD, int NB>
 static void launch_rel_gemm_wide(const RelGemmArgs& a, hipStream_t st) {
@@ -4873,16 +4879,20 @@ static void launch_rel_gemm_t(const RelGemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((rel_gemm_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
-static bool g_gemm_bf3 = true;  // MPGNN_OPT_GEMM_BF3: K ∈ {64, 128}, N = 128 on the bf16 matrix cores (3-way split)
-static bool g_bwd_fused = true;  // MPGNN_OPT_BWD_FUSED: see bwd_bf3_kernel
+// process defaults of the per-plan switches (mpgnn_set_option; plans copy them when created)
+static std::mutex g_opt_mu;
+static Options g_defaults;
+Options default_options() {
+    std::lock_guard<std::mutex> lk(g_opt_mu);
+    return g_defaults;
+}
 
-static bool g_gemm_il = true;  // MPGNN_OPT_GEMM_IL: the interleaved item skeleton (RelGemmBf3::run_il)
 
 template <int KB, bool DGRAD>
-static void launch_rel_gemm_bf3(const RelGemmArgs& a, hipStream_t st) {
+static void launch_rel_gemm_bf3(const RelGemmArgs& a, bool il, hipStream_t st) {
     const size_t lds = RelGemmBf3<KB, DGRAD>::lds_bytes();
     const int grid = std::min(a.n_rel + a.n_root, cu_count() * 2);  // two workgroups per CU
-    if (g_gemm_il) hipLaunchKernelGGL((rel_gemm_bf3_kernel<KB, DGRAD, true>), dim3(grid), dim3(kThreads), lds, st, a);
+    if (il) hipLaunchKernelGGL((rel_gemm_bf3_kernel<KB, DGRAD, true>), dim3(grid), dim3(kThreads), lds, st, a);
     else hipLaunchKernelGGL((rel_gemm_bf3_kernel<KB, DGRAD>), dim3(grid), dim3(kThreads), lds, st, a);
 }
 
@@ -4897,8 +4907,6 @@ static void launch_rel_gemm_bf3w(const RelGemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((rel_gemm_bf3w_kernel<DGRAD>), dim3(2 * pairs), dim3(512), lds, st, a);
 }
 
-static int g_gemm_switch_cost = 250;  // MPGNN_OPT_GEMM_SWITCH_COST: percent of an item (0 = equal item counts)
-static bool g_gemm_cu_pairs = true;  // MPGNN_OPT_GEMM_CU_PAIRS: ranges balanced per CU (two workgroups each)
 
 // rel_gemm_bf3_kernel's item ranges balanced by cost = items + c · weight runs (each range pays
 // one exposed weight-slice load per run it holds), followed by every item's weight index (the
@@ -4908,15 +4916,16 @@ static bool g_gemm_cu_pairs = true;  // MPGNN_OPT_GEMM_CU_PAIRS: ranges balanced
 // buffer the plan keeps (no device-wide synchronisation, ordered before the kernel reading it).
 static const int* gemm_ranges(const mpgnn_plan* p, int t_lo, int n_rel, int n_root, int G, bool pairs,
                               hipStream_t st) {
-    if (g_gemm_switch_cost <= 0 || G <= 1) return nullptr;
-    const std::array<int64_t, 5> key{t_lo, n_rel, n_root, G * 2 + (pairs ? 1 : 0), g_gemm_switch_cost};
+    const int cost = p->opt.gemm_switch_cost;
+    if (cost <= 0 || G <= 1) return nullptr;
+    const std::array<int64_t, 5> key{t_lo, n_rel, n_root, G * 2 + (pairs ? 1 : 0), cost};
     std::lock_guard<std::mutex> lk(p->bw_mu);
     auto it = p->gemm_ranges.find(key);
     if (it != p->gemm_ranges.end()) return it->second.dev;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
     const int n = n_rel + n_root;
-    const double c = g_gemm_switch_cost / 100.0;
+    const double c = cost / 100.0;
     std::vector<double> cum(n + 1, 0.0);
     std::vector<int> wrel(n, -1);
     int prev_w = -2;
@@ -4979,18 +4988,18 @@ static const int* gemm_ranges(const mpgnn_plan* p, int t_lo, int n_rel, int n_ro
     return e.dev;
 }
 
-static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, hipStream_t st) {
-    if (g_gemm_bf3 && (K == 64 || K == 128) && a.node_map == nullptr) {
+static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, const Options& o, hipStream_t st) {
+    if (o.gemm_bf3 && (K == 64 || K == 128) && a.node_map == nullptr) {
         if (K == 64) {
-            if (dgrad) launch_rel_gemm_bf3<1, true>(a, st);
-            else launch_rel_gemm_bf3<1, false>(a, st);
+            if (dgrad) launch_rel_gemm_bf3<1, true>(a, o.gemm_il, st);
+            else launch_rel_gemm_bf3<1, false>(a, o.gemm_il, st);
         } else {
-            if (dgrad) launch_rel_gemm_bf3<2, true>(a, st);
-            else launch_rel_gemm_bf3<2, false>(a, st);
+            if (dgrad) launch_rel_gemm_bf3<2, true>(a, o.gemm_il, st);
+            else launch_rel_gemm_bf3<2, false>(a, o.gemm_il, st);
         }
         return;
     }
-    if (g_gemm_bf3 && K == 256 && a.node_map == nullptr) {  // C5: split-K bf16 kernel, two column blocks
+    if (o.gemm_bf3 && K == 256 && a.node_map == nullptr) {  // C5: split-K bf16 kernel, two column blocks
         if (dgrad) launch_rel_gemm_bf3w<true>(a, st);
         else launch_rel_gemm_bf3w<false>(a, st);
         return;
@@ -5034,7 +5043,6 @@ static void launch_piece(const PieceArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((piece_sum_kernel<V, T>), dim3((n + kWaves - 1) / kWaves), dim3(kThreads), 0, st, a);
 }
 
-static bool g_exact_order = false;  // MPGNN_OPT_EXACT_ORDER: no ragged pieces anywhere
 
 struct Selection {
     int64_t d_lo = 0, d_hi = 0;
@@ -5208,7 +5216,7 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
         if (st != MPGNN_OK) return st;
     }
     // B-stationary GEMM (weights in registers per relation run) for the bench shapes
-    if (gather_kind != 0 && W != nullptr && g_rel_gemm && (((K == 64 || K == 128) && N == 128) || (K == 256 && N == 256 && g_rel_wide)) &&
+    if (gather_kind != 0 && W != nullptr && p->opt.rel_gemm && (((K == 64 || K == 128) && N == 128) || (K == 256 && N == 256 && p->opt.rel_wide)) &&
         trans == (gather_kind == 1 ? 1 : 0)) {
         RelGemmArgs r{};
         r.t_begin = p->d.t32_begin;
@@ -5240,14 +5248,14 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
 #ifdef MPGNN_STAMPS
         r.stamps = gather_kind == 1 ? nullptr : g_stamps_host;
 #endif
-        if (g_gemm_bf3 && (K == 64 || K == 128) && r.node_map == nullptr) {
+        if (p->opt.gemm_bf3 && (K == 64 || K == 128) && r.node_map == nullptr) {
             const int G = std::min(r.n_rel + r.n_root, cu_count() * 2);
-            const bool pairs = g_gemm_cu_pairs && G == cu_count() * 2 && cu_count() % 8 == 0;
+            const bool pairs = p->opt.gemm_cu_pairs && G == cu_count() * 2 && cu_count() % 8 == 0;
             r.wg_items = gemm_ranges(p, r.t_lo, r.n_rel, r.n_root, G, pairs, strm);
             r.wg_cus = (pairs && r.wg_items != nullptr) ? cu_count() : 0;
         }
         TimedLaunch tl(kind, strm);
-        launch_rel_gemm(r, K, gather_kind == 1, strm);
+        launch_rel_gemm(r, K, gather_kind == 1, p->opt, strm);
         return hip_check(hipGetLastError(), "rel_gemm_kernel launch");
     }
     // tile_gemm stages A rows as float4 (K % 4 == 0); other widths take seg_tile_kernel
@@ -5450,19 +5458,17 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
     return hip_check(hipGetLastError(), "row_sum_kernel launch");
 }
 
-static bool g_outer_vec = true;  // MPGNN_OPT_OUTER_VEC: outer_bf3v_kernel (16-B gathers, transposed LDS reads)
-static void launch_outer_bf3(dim3 grid, const OuterArgs& r, const OuterArgs& w, int ra_n, int n_all, hipStream_t st) {
-    if (g_outer_vec)
+static void launch_outer_bf3(dim3 grid, const OuterArgs& r, const OuterArgs& w, int ra_n, int n_all, bool vec,
+                             hipStream_t st) {
+    if (vec)
         hipLaunchKernelGGL(outer_bf3v_kernel, grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
     else
         hipLaunchKernelGGL(outer_bf3_kernel, grid, dim3(kThreads), kOb3Lds, st, r, w, ra_n, n_all);
 }
-static bool g_flat_fuse_split = true;  // MPGNN_OPT_FLAT_FUSE_SPLIT: hub rows of grad_x finished in the gather launch
-static int g_flat_wg_per_cu = 0;  // MPGNN_OPT_FLAT_WG_PER_CU: persistent grid of flat_rows_kernel (0: a workgroup per group)
 template <int V, int T>
-static void launch_flat(const FlatArgs& a, int max_pieces, hipStream_t st) {
+static void launch_flat(const FlatArgs& a, int max_pieces, int wg_per_cu, hipStream_t st) {
     const int n_groups = a.g_hi - a.g_lo;
-    const int n = g_flat_wg_per_cu > 0 ? std::min(n_groups, cu_count() * g_flat_wg_per_cu) : n_groups;
+    const int n = wg_per_cu > 0 ? std::min(n_groups, cu_count() * wg_per_cu) : n_groups;
     const size_t lds = (size_t)max_pieces * a.F * sizeof(float);  // 0 when the list has no long row
     hipLaunchKernelGGL((flat_rows_kernel<V, T>), dim3(n), dim3(kThreads), lds, st, a);
 }
@@ -5625,6 +5631,7 @@ struct FlatRun {
     int lo, hi;
     int relu;             // fused activation (unsharded forward combine)
     unsigned* arrive;     // mode 0: [nsplit] zeroed piece counters — split rows finished in the launch
+    int wg_per_cu;        // the plan's MPGNN_OPT_FLAT_WG_PER_CU
 };
 
 static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
@@ -5664,7 +5671,7 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
             a.split_ptr = f.fd->split_ptr;
             a.split_slot = f.fd->split_slot;
         }  // mode 1: the finalize adds extra + bias first
-        MPGNN_VT_DISPATCH(V, T, launch_flat, a, f.max_pieces, strm);
+        MPGNN_VT_DISPATCH(V, T, launch_flat, a, f.max_pieces, f.wg_per_cu, strm);
         int32_t st = hip_check(hipGetLastError(), "flat_rows_kernel launch");
         if (st != MPGNN_OK) return st;
     }
@@ -5705,6 +5712,7 @@ static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x
     if (!exact) {
         // flat chunked list; chunks and splits of the relation range [d_lo, d_hi)
         FlatRun f{};
+        f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.fd = &p->d.seg_f;
         f.max_pieces = p->seg_f.max_pieces;
         f.g_lo = p->seg_f.cut_group_ptr[s.d_lo];
@@ -5746,6 +5754,7 @@ static int32_t run_means_multi(const mpgnn_plan* p, const Selection& s, const fl
     if (s.m_hi == s.m_lo) return MPGNN_OK;
     if (!exact) {
         FlatRun f{};
+        f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.fd = &p->d.segm_f;
         f.max_pieces = p->segm_f.max_pieces;
         f.g_lo = p->segm_f.cut_group_ptr[s.d_lo];
@@ -5806,7 +5815,7 @@ static int linear_block(int F) { return kLinAcc * (kThreads / F); }  // outputs 
 // B = x and the bias column sums taken from A (bias_of_a), row chunks of >= 64 rows (about two
 // per CU), then the ordered slab sum (reduce_slabs3_kernel). The scalar pair below needs 2 × ~50 µs
 // for this width at C3 (two output blocks), the library's sliced GEMM ~45-60 µs.
-static bool linear_bf3(int64_t N, int32_t F, int32_t O) { return g_gemm_bf3 && F == 128 && O == 128 && N > 0; }
+static bool linear_bf3(int64_t N, int32_t F, int32_t O) { return default_options().gemm_bf3 && F == 128 && O == 128 && N > 0; }
 static int linear_bf3_chunk(int64_t N) {
     const int64_t per = (N + 2 * (int64_t)cu_count() - 1) / (2 * (int64_t)cu_count());
     return (int)std::max<int64_t>(64, (per + 15) / 16 * 16);
@@ -5858,7 +5867,7 @@ int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int
         orr.dst_b = grad_bias;
         orr.bias_of_a = 1;
         OuterArgs none{};
-        launch_outer_bf3(dim3(std::min(nch, cu_count() * 2)), orr, none, nch, nch, strm);
+        launch_outer_bf3(dim3(std::min(nch, cu_count() * 2)), orr, none, nch, nch, default_options().outer_vec, strm);
         int32_t st = hip_check(hipGetLastError(), "outer_bf3_kernel (linear) launch");
         if (st != MPGNN_OK || nch == 1) return st;
         ReduceArgs rw{}, rb{};
@@ -5890,52 +5899,62 @@ int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int
     return MPGNN_OK;
 }
 
-int32_t mpgnn_set_option(int32_t option, int64_t value) {
+// The per-plan switches of enum mpgnn_option: set / read one in `o`. MPGNN_ERR_UNSUPPORTED
+// (nothing set) when `option` is not one of them.
+static int32_t set_switch(Options& o, int32_t option, int64_t value) {
     switch (option) {
-        case MPGNN_OPT_EXACT_ORDER:
-            g_exact_order = value != 0;
+        case MPGNN_OPT_EXACT_ORDER: o.exact_order = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_REL_GEMM: o.rel_gemm = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_REL_WIDE: o.rel_wide = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_GEMM_BF3: o.gemm_bf3 = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_GEMM_IL: o.gemm_il = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_GEMM_CU_PAIRS: o.gemm_cu_pairs = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_BWD_FUSED: o.bwd_fused = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_FLAT_FUSE_SPLIT: o.flat_fuse_split = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_OUTER_VEC: o.outer_vec = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_GEMM_SWITCH_COST:
+            if (value < 0 || value > 10000) return arg_error("MPGNN_OPT_GEMM_SWITCH_COST must be 0..10000 (percent of an item)");
+            o.gemm_switch_cost = (int)value;
             return MPGNN_OK;
+        case MPGNN_OPT_FLAT_WG_PER_CU:
+            if (value < 0 || value > 64) return arg_error("MPGNN_OPT_FLAT_WG_PER_CU must be 0..64");
+            o.flat_wg_per_cu = (int)value;
+            return MPGNN_OK;
+        default: return MPGNN_ERR_UNSUPPORTED;
+    }
+}
+static bool get_switch(const Options& o, int32_t option, int64_t* value) {
+    switch (option) {
+        case MPGNN_OPT_EXACT_ORDER: *value = o.exact_order; return true;
+        case MPGNN_OPT_REL_GEMM: *value = o.rel_gemm; return true;
+        case MPGNN_OPT_REL_WIDE: *value = o.rel_wide; return true;
+        case MPGNN_OPT_GEMM_BF3: *value = o.gemm_bf3; return true;
+        case MPGNN_OPT_GEMM_IL: *value = o.gemm_il; return true;
+        case MPGNN_OPT_GEMM_CU_PAIRS: *value = o.gemm_cu_pairs; return true;
+        case MPGNN_OPT_BWD_FUSED: *value = o.bwd_fused; return true;
+        case MPGNN_OPT_FLAT_FUSE_SPLIT: *value = o.flat_fuse_split; return true;
+        case MPGNN_OPT_OUTER_VEC: *value = o.outer_vec; return true;
+        case MPGNN_OPT_GEMM_SWITCH_COST: *value = o.gemm_switch_cost; return true;
+        case MPGNN_OPT_FLAT_WG_PER_CU: *value = o.flat_wg_per_cu; return true;
+        default: return false;
+    }
+}
+
+int32_t mpgnn_set_option(int32_t option, int64_t value) {
+    {
+        std::lock_guard<std::mutex> lk(g_opt_mu);
+        const int32_t st = set_switch(g_defaults, option, value);
+        if (st != MPGNN_ERR_UNSUPPORTED) return st;
+    }
+    switch (option) {
         case MPGNN_OPT_TIMING_MASK: {
             std::lock_guard<std::mutex> lk(g_timing_mu);
             g_timing_mask = value;
             return MPGNN_OK;
         }
-        case MPGNN_OPT_REL_GEMM:
-            g_rel_gemm = value != 0;
-            return MPGNN_OK;
         case MPGNN_OPT_PLAN_THREADS:
             if (value < 0 || value > 256) return arg_error("MPGNN_OPT_PLAN_THREADS must be 0..256");
             g_plan_threads = (int)value;
-            return MPGNN_OK;
-        case MPGNN_OPT_REL_WIDE:
-            g_rel_wide = value != 0;
-            return MPGNN_OK;
-        case MPGNN_OPT_GEMM_BF3:
-            g_gemm_bf3 = value != 0;
-            return MPGNN_OK;
-        case MPGNN_OPT_GEMM_IL:
-            g_gemm_il = value != 0;
-            return MPGNN_OK;
-        case MPGNN_OPT_GEMM_CU_PAIRS:
-            g_gemm_cu_pairs = value != 0;
-            return MPGNN_OK;
-        case MPGNN_OPT_BWD_FUSED:
-            g_bwd_fused = value != 0;
-            return MPGNN_OK;
-
-        case MPGNN_OPT_FLAT_FUSE_SPLIT:
-            g_flat_fuse_split = value != 0;
-            return MPGNN_OK;
-        case MPGNN_OPT_OUTER_VEC:
-            g_outer_vec = value != 0;
-            return MPGNN_OK;
-        case MPGNN_OPT_GEMM_SWITCH_COST:
-            if (value < 0 || value > 10000) return arg_error("MPGNN_OPT_GEMM_SWITCH_COST must be 0..10000 (percent of an item)");
-            g_gemm_switch_cost = (int)value;
-            return MPGNN_OK;
-        case MPGNN_OPT_FLAT_WG_PER_CU:
-            if (value < 0 || value > 64) return arg_error("MPGNN_OPT_FLAT_WG_PER_CU must be 0..64");
-            g_flat_wg_per_cu = (int)value;
             return MPGNN_OK;
         case MPGNN_OPT_CHUNK_ROWS:
             if (value < 32 || value > 1024 || value % 32 != 0)
@@ -5950,27 +5969,35 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
 
 int32_t mpgnn_get_option(int32_t option, int64_t* value) {
     if (!value) return arg_error("NULL value");
+    {
+        std::lock_guard<std::mutex> lk(g_opt_mu);
+        if (get_switch(g_defaults, option, value)) return MPGNN_OK;
+    }
     switch (option) {
-        case MPGNN_OPT_EXACT_ORDER: *value = g_exact_order ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_TIMING_MASK: {
             std::lock_guard<std::mutex> lk(g_timing_mu);
             *value = g_timing_mask;
             return MPGNN_OK;
         }
-        case MPGNN_OPT_REL_GEMM: *value = g_rel_gemm ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_PLAN_THREADS: *value = g_plan_threads; return MPGNN_OK;
-        case MPGNN_OPT_REL_WIDE: *value = g_rel_wide ? 1 : 0; return MPGNN_OK;
         case MPGNN_OPT_CHUNK_ROWS: *value = g_chunk_rows; return MPGNN_OK;
-        case MPGNN_OPT_GEMM_BF3: *value = g_gemm_bf3 ? 1 : 0; return MPGNN_OK;
-        case MPGNN_OPT_GEMM_IL: *value = g_gemm_il ? 1 : 0; return MPGNN_OK;
-        case MPGNN_OPT_GEMM_CU_PAIRS: *value = g_gemm_cu_pairs ? 1 : 0; return MPGNN_OK;
-        case MPGNN_OPT_BWD_FUSED: *value = g_bwd_fused ? 1 : 0; return MPGNN_OK;
-        case MPGNN_OPT_FLAT_WG_PER_CU: *value = g_flat_wg_per_cu; return MPGNN_OK;
-        case MPGNN_OPT_FLAT_FUSE_SPLIT: *value = g_flat_fuse_split ? 1 : 0; return MPGNN_OK;
-        case MPGNN_OPT_OUTER_VEC: *value = g_outer_vec ? 1 : 0; return MPGNN_OK;
-        case MPGNN_OPT_GEMM_SWITCH_COST: *value = g_gemm_switch_cost; return MPGNN_OK;
         default: return arg_error("unknown option " + std::to_string(option));
     }
+}
+
+int32_t mpgnn_plan_set_option(mpgnn_plan* p, int32_t option, int64_t value) {
+    if (!p) return arg_error("NULL plan");
+    const int32_t st = set_switch(p->opt, option, value);
+    if (st == MPGNN_ERR_UNSUPPORTED)
+        return arg_error("option " + std::to_string(option) + " is not a per-plan switch (process-wide or build-time: mpgnn_set_option)");
+    return st;
+}
+
+int32_t mpgnn_plan_get_option(const mpgnn_plan* p, int32_t option, int64_t* value) {
+    if (!p || !value) return arg_error("NULL plan or value");
+    if (!get_switch(p->opt, option, value))
+        return arg_error("option " + std::to_string(option) + " is not a per-plan switch");
+    return MPGNN_OK;
 }
 
 int32_t mpgnn_rel_mean_fwd(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R,
@@ -6068,14 +6095,15 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     char* ws = static_cast<char*>(workspace);
     float* Y = reinterpret_cast<float*>(ws + w.y);
     float* Yroot = root ? reinterpret_cast<float*>(ws + w.yroot) : nullptr;
-    const bool exact = g_exact_order;
+    const Options& o = p->opt;
+    const bool exact = o.exact_order;
     const bool own_range = row_lo == p->shard_lo && row_hi == p->shard_hi;
     // Mode SINGLE, unsharded, F_in ∈ {64, 128}, F_out = 128: ONE fused GEMM per layer,
     //   out[i] = act([x_i | mean_i] @ [root; W] + bias)   (K = 2·F_in; mean_i = 0 without a segment)
     // — a node has at most one segment of the relation, so the transform, the root term, the
     // combine and the activation of mp_rgcn_layer.py:245-268 (+ model.py:211,214) need no Y,
     // Y_root or combine pass.
-    const bool cat = mode == MPGNN_MODE_SINGLE && !exact && g_rel_gemm && root != nullptr &&
+    const bool cat = mode == MPGNN_MODE_SINGLE && !exact && o.rel_gemm && root != nullptr &&
                      (F_in == 64 || F_in == 128) && F_out == 128 && row_lo == 0 && row_hi == p->N &&
                      p->shard_lo == 0 && p->shard_hi == p->N && p->N <= INT32_MAX - 1;
     // the relation's node map: the plan's (absent relation: its zero row), else built per call
@@ -6112,7 +6140,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     // row without a segment of the relation — act((0 + x_i @ root) + bias) straight into out (87 %
     // of C5's rows) — and single_fix_kernel adds Y to the rows with one: no Y_root buffer, no
     // combine pass over all N rows.
-    const bool root_epi = mode == MPGNN_MODE_SINGLE && !exact && g_rel_gemm && g_rel_wide && root != nullptr &&
+    const bool root_epi = mode == MPGNN_MODE_SINGLE && !exact && o.rel_gemm && o.rel_wide && root != nullptr &&
                           F_in == 256 && F_out == 256 && row_lo == 0 && row_hi == p->N && p->shard_lo == 0 &&
                           p->shard_hi == p->N && p->N <= INT32_MAX - 1;
     if (root_epi) {
@@ -6137,7 +6165,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
         const int* nmap = nullptr;
         if ((st = relation_node_map(&nmap)) != MPGNN_OK) return st;
-        if (g_gemm_bf3) {  // split-K layer on the bf16 matrix cores
+        if (o.gemm_bf3) {  // split-K layer on the bf16 matrix cores
             SingleBf3Args sa{};
             sa.x = x;
             sa.H = H;
@@ -6222,6 +6250,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
             if (st != MPGNN_OK) return st;
         }
         FlatRun f{};
+        f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.fd = &p->d.rwx_f;
         f.max_pieces = p->rwx_f.max_pieces;
         f.g_lo = 0;
@@ -6249,6 +6278,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     }
     if (mode == MPGNN_MODE_ALL && !exact) {
         FlatRun f{};
+        f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.fd = &p->d.rw_f;
         f.max_pieces = p->rw_f.max_pieces;
         f.g_lo = 0;
@@ -6346,6 +6376,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
             if (st != MPGNN_OK) return st;
         }
         FlatRun f{};
+        f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.fd = &p->d.tx_f;
         f.max_pieces = p->tx_f.max_pieces;
         f.g_lo = 0;
@@ -6367,7 +6398,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         f.lo = (int)row_lo;
         f.hi = (int)row_hi;
         TimedLaunch tl(MPGNN_K_ROW_DX, strm);
-        if (g_flat_fuse_split && p->tx_f.nsplit > 0) {
+        if (p->opt.flat_fuse_split && p->tx_f.nsplit > 0) {
             // piece counters behind the carry slots (ws_layout reserves them in the pdx region)
             f.arrive = reinterpret_cast<unsigned*>(Pdx + (size_t)p->tx_f.nslots * F_in);
             st = hip_check(hipMemsetAsync(f.arrive, 0, (size_t)p->tx_f.nsplit * sizeof(unsigned), strm),
@@ -6378,6 +6409,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         if (st != MPGNN_OK) return st;
     } else if (mode == MPGNN_MODE_ALL && !exact) {
         FlatRun f{};
+        f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.fd = &p->d.t_f;
         f.max_pieces = p->t_f.max_pieces;
         f.g_lo = 0;
@@ -6492,7 +6524,7 @@ int32_t mpgnn_rel_mean_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, 
     if ((st = hip_check(hipGetLastError(), "scale_rows_kernel launch")) != MPGNN_OK) return st;
     TimedLaunch tl(MPGNN_K_ROW_DX, strm);
     return run_grad_x(p, mode, s, G, nullptr, F, p->shard_lo, p->shard_hi, dx,
-                      reinterpret_cast<float*>(ws + off_pdx), g_exact_order, strm);
+                      reinterpret_cast<float*>(ws + off_pdx), p->opt.exact_order, strm);
 }
 
 
@@ -6685,7 +6717,8 @@ static int32_t rgcn_bwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     const WsLayout w = ws_layout(p, mode, s, F_in, F_out, row_lo, row_hi, rc);
     char* ws = static_cast<char*>(workspace);
     if (!ws) return arg_error("NULL workspace");
-    const bool exact = g_exact_order;
+    const Options& o = p->opt;
+    const bool exact = o.exact_order;
 
     const bool want_x = grad_x != nullptr && p->N > 0;
     const bool want_p = grad_weight != nullptr || grad_root != nullptr || grad_bias != nullptr;
@@ -6693,18 +6726,18 @@ static int32_t rgcn_bwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         // accumulating parameter gradients: the mode-ALL F = 128 path (outer_bf3_kernel + the
         // ordered slab sum) only, decided before anything is launched
         const int nch = s.c_hi - s.c_lo;
-        if (mode != MPGNN_MODE_ALL || !g_gemm_bf3 || F_in != 128 || F_out != 128 || !grad_weight || !grad_root ||
+        if (mode != MPGNN_MODE_ALL || !o.gemm_bf3 || F_in != 128 || F_out != 128 || !grad_weight || !grad_root ||
             !grad_bias || nch <= 0 || rc.n <= 0 || !x)
             return MPGNN_ERR_UNSUPPORTED;
         // where mpgnn_rgcn_bwd takes the one-launch bwd_fused path (few items per CU) its
         // gradients are summed in another order: refused, so that the caller's fallback (fresh
         // gradients + one add) stays bit-identical to autograd's accumulation of that path
         const int64_t items = (int64_t)(s.t32_hi - s.t32_lo) + (row_hi - row_lo + 31) / 32;
-        if (g_bwd_fused && g_rel_gemm && !exact && root && (h_save != nullptr || s.m_hi == s.m_lo) &&
+        if (o.bwd_fused && o.rel_gemm && !exact && root && (h_save != nullptr || s.m_hi == s.m_lo) &&
             p->N <= INT32_MAX - 1 && row_hi > row_lo && items <= 4 * (int64_t)cu_count())
             return MPGNN_ERR_UNSUPPORTED;
     }
-    if (!acc && g_bwd_fused && g_gemm_bf3 && g_rel_gemm && !exact && F_in == 128 && F_out == 128 && p->N > 0 && x != nullptr &&
+    if (!acc && o.bwd_fused && o.gemm_bf3 && o.rel_gemm && !exact && F_in == 128 && F_out == 128 && p->N > 0 && x != nullptr &&
         root != nullptr && grad_weight != nullptr && grad_root != nullptr && (h_save != nullptr || s.m_hi == s.m_lo) &&
         p->N <= INT32_MAX - 1) {
         st = bwd_fused(p, mode, R, x, weight, root, h_save, grad_out, row_lo, row_hi, want_x ? grad_x : nullptr,
@@ -6755,7 +6788,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
                           hipStream_t strm, bool acc) {
     int32_t st = MPGNN_OK;
     const size_t wsize = (size_t)F_in * F_out;
-    const bool exact = g_exact_order;
+    const bool exact = p->opt.exact_order;
     const int mt = (F_in + kColTile - 1) / kColTile;
     const int nt = (F_out + kColTile - 1) / kColTile;
     const size_t outer_lds = (size_t)(4 * kOuterBuf) * sizeof(float);
@@ -6897,10 +6930,10 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
         }
     }
     const int root_y = grad_root ? mt : 1;
-    const bool bf3 = have_w && have_root && root_y == mt && g_gemm_bf3 && F_in == 128 && F_out == 128;
+    const bool bf3 = have_w && have_root && root_y == mt && p->opt.gemm_bf3 && F_in == 128 && F_out == 128;
     // F_in = F_out = 256 (C5): the same kernel over the four 128 × 128 quadrants of every dW_r /
     // droot slab (the bias column sums taken by the two quadrants of the first A half)
-    const bool bf3q = have_w && have_root && root_y == mt && g_gemm_bf3 && F_in == 256 && F_out == 256 && !acc;
+    const bool bf3q = have_w && have_root && root_y == mt && p->opt.gemm_bf3 && F_in == 256 && F_out == 256 && !acc;
     if (acc && !bf3) return MPGNN_ERR_UNSUPPORTED;  // (excluded by rgcn_bwd_impl's check)
     if (bf3q) {
         TimedLaunch tl(MPGNN_K_OUTER, strm);
@@ -6923,7 +6956,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
                     rq.Pb = nullptr;
                     rq.dst_b = nullptr;
                 }
-                launch_outer_bf3(dim3(gx), rq, wq, rc.n, n_all, strm);
+                launch_outer_bf3(dim3(gx), rq, wq, rc.n, n_all, p->opt.outer_vec, strm);
                 if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel (quadrant) launch")) != MPGNN_OK) return st;
             }
     } else if (bf3) {
@@ -6931,7 +6964,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
         TimedLaunch tl(MPGNN_K_OUTER, strm);
         const int n_all = nch + rc.n;
         const int gx = std::max(1, std::min(n_all, cu_count() * 2));
-        launch_outer_bf3(dim3(gx), orr, ow, rc.n, n_all, strm);
+        launch_outer_bf3(dim3(gx), orr, ow, rc.n, n_all, p->opt.outer_vec, strm);
         if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel launch")) != MPGNN_OK) return st;
     } else if (have_w && have_root && root_y == mt) {
         TimedLaunch tl(MPGNN_K_OUTER, strm);

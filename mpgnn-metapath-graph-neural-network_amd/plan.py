@@ -161,6 +161,20 @@ class GraphPlan:
         check(lib.mpgnn_plan_digest(self._h, ctypes.byref(out)), "mpgnn_plan_digest")
         return int(out.value)
 
+    def set_option(self, option: int, value: int) -> None:
+        """This plan's kernel switch (``enum mpgnn_option``; the plan was created with the
+        process defaults of ``_lib.set_option``)."""
+        check(lib.mpgnn_plan_set_option(self._h, int(option), int(value)), "mpgnn_plan_set_option")
+
+    def get_option(self, option: int) -> int:
+        v = ctypes.c_int64()
+        check(lib.mpgnn_plan_get_option(self._h, int(option), ctypes.byref(v)), "mpgnn_plan_get_option")
+        return int(v.value)
+
+    def set_exact_order(self, on: bool) -> None:
+        """MPGNN_OPT_EXACT_ORDER on this plan (see include/mpgnn_rgcn.h)."""
+        self.set_option(_lib.OPT_EXACT_ORDER, 1 if on else 0)
+
     def hsave_rows(self, mode: int, relation: int, num_relations: int) -> int:
         """Rows of the saved means of a layer call: its multi-edge segments (the single-edge
         segments' means are x rows, read through the plan's s_src table)."""

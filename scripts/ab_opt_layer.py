@@ -47,8 +47,19 @@ def run(train):
 
 res = {"workload": a.workload, "opt": a.opt, "values": vals, "default": default}
 outs = {}
-for v in vals:
+plan = mpgnn_amd.get_plan(ei, et, x.shape[0])  # the layer's cached plan: kernel switches are per plan
+
+
+def setopt(v):
     _lib.set_option(a.opt, v)
+    try:
+        plan.set_option(a.opt, v)
+    except ValueError:  # a process-wide option
+        pass
+
+
+for v in vals:
+    setopt(v)
     conv.zero_grad(set_to_none=True)
     outs[v] = run(True)
     torch.cuda.synchronize()
@@ -59,7 +70,7 @@ res["max_abs_diff"] = {n: max(float((outs[vals[0]][k] - outs[v][k]).abs().max())
 timing = {v: [] for v in vals}
 for r in range(a.rounds):
     for v in vals:
-        _lib.set_option(a.opt, v)
+        setopt(v)
         for train in (False, True):
             for _ in range(3):
                 conv.zero_grad(set_to_none=True)
@@ -86,5 +97,5 @@ for r in range(a.rounds):
                 rec[kind] = round(ms * 1e3 / a.iters, 2)
         timing[v].append(rec)
 res["timing"] = {str(v): timing[v] for v in vals}
-_lib.set_option(a.opt, default)
+setopt(default)
 print(json.dumps(res), flush=True)

@@ -50,6 +50,10 @@ def _restore_library_options():
     yield
     for o, v in _DEFAULTS.items():
         _lib.set_option(o, v)
+    # kernel switches are per plan: drop the layer classes' cached plans, which may carry a
+    # switch the test set on them
+    from mpgnn_amd import plan_cache
+    plan_cache.clear()
 
 
 @pytest.fixture(scope="session")

@@ -107,6 +107,38 @@ def test_round4_switches_default_on_and_round_trip():
             lib.mpgnn_set_option(opt, v)
 
 
+def test_kernel_switches_are_per_plan():
+    """VERDICT r4 item 5 / SURVEY §8b ("no global mutable state"): the kernel switches live in
+    each plan. A plan copies the process defaults when it is created; mpgnn_plan_set_option
+    changes that plan only; a later default change reaches plans created after it, not existing
+    ones; the build-time and profiling options are refused on a plan."""
+    import mpgnn_amd
+    from mpgnn_amd import _lib
+    lib = _lib.lib
+    ei = torch.tensor([[0, 1, 2, 2], [1, 2, 0, 1]])
+    et = torch.tensor([0, 1, 0, 1])
+    a = mpgnn_amd.GraphPlan(ei, et, 3, build="host")
+    b = mpgnn_amd.GraphPlan(ei, et, 3, build="host")
+    assert a.get_option(29) == b.get_option(29) == _lib.get_option(29)
+    a.set_option(29, 17)
+    a.set_exact_order(True)
+    assert a.get_option(29) == 17 and a.get_option(0) == 1
+    assert b.get_option(29) == _lib.get_option(29) and b.get_option(0) == 0
+    shipped = _lib.get_option(30)
+    try:
+        _lib.set_option(30, 0)
+        c = mpgnn_amd.GraphPlan(ei, et, 3, build="host")
+        assert c.get_option(30) == 0 and a.get_option(30) == shipped and b.get_option(30) == shipped
+    finally:
+        _lib.set_option(30, shipped)
+    for opt in (3, 11, 20):  # timing mask, plan threads, chunk rows: process-wide
+        assert lib.mpgnn_plan_set_option(a.handle, opt, 1) == _lib.MPGNN_ERR_ARG
+        with pytest.raises(ValueError):
+            a.get_option(opt)
+    with pytest.raises(ValueError):
+        a.set_option(29, -1)
+
+
 def test_workspace_bytes_is_host_computable():
     import mpgnn_amd
     g = mpgnn_amd.data.config_graph("C1")
