@@ -2265,6 +2265,9 @@ struct RelGemmBf3W {
 #pragma unroll
         for (int j = 0; j < WPT; ++j) row[j] = it.r0 + min(t / 32 + 8 * j, it.nrows - 1);
         cnt = 1;
+        if constexpr (!DGRAD) {  // mode-SINGLE root epilogue: does row t & 31 have a segment?
+            if (it.root && a.node_map != nullptr) cnt = a.node_map[it.r0 + min(t & 31, it.nrows - 1)] != 0 ? 1 : 0;
+        }
         if (!it.root) {
             if constexpr (DGRAD) {
                 cnt = a.s_cnt[it.r0 + min(t & 31, it.nrows - 1)];
@@ -2308,7 +2311,7 @@ struct RelGemmBf3W {
             *reinterpret_cast<bf16x4*>(d + PLANE) = bf16x4{p1[0], p1[1], p1[2], p1[3]};
             *reinterpret_cast<bf16x4*>(d + 2 * PLANE) = bf16x4{p2[0], p2[1], p2[2], p2[3]};
         }
-        if (kh == 0 && t < 32) sc[t] = 1.0f / (float)cnt;
+        if (kh == 0 && t < 32) sc[t] = DGRAD ? 1.0f / (float)cnt : (float)cnt;  // forward: root-epilogue flag
     }
     // the wave's slice: B(kh·128 + 16s + 8h + j, col) in bf16 pieces
     __device__ static __forceinline__ void load_b(const float* w, int kh, int col, int h, bf16x8 (&b)[NS][3]) {
@@ -2366,6 +2369,8 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
     const int i_end = (int)((long long)(rng + 1) * n_items / n_ranges);
     if (i_beg >= i_end) return;
     const int col = cb * 128 + wq * 32 + c;
+    const bool root_epi = !DGRAD && a.node_map != nullptr;
+    const float bias_c = (root_epi && a.bias != nullptr) ? a.bias[col] : 0.0f;
 
     // item windows: tab_a covers [wb, wb + 64), tab_b the next 64 items (loaded one window ahead)
     int wb = i_beg;
@@ -2479,6 +2484,14 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
                 float o = acc[r] + Oe[rr * G::LDO + wq * 32 + c];
                 if constexpr (DGRAD) {
                     if (!cur.root) o = o * sc[rr];
+                } else {
+                    // mode-SINGLE root epilogue (RelGemmArgs::node_map): a row without a segment
+                    // of the relation is final, act((0 + x_i @ root) + bias); single_fix_kernel
+                    // finishes the others from x_i @ root
+                    if (root_epi && cur.root && sc[rr] == 0.0f) {
+                        o = (0.0f + o) + bias_c;
+                        if (a.relu) o = relu_f(o);
+                    }
                 }
                 prev[r] = o;
             }
@@ -4999,7 +5012,10 @@ static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, const Optio
         }
         return;
     }
-    if (o.gemm_bf3 && K == 256 && a.node_map == nullptr) {  // C5: split-K bf16 kernel, two column blocks
+    // C5: split-K bf16 kernel, two column blocks; forward with node_map: the mode-SINGLE root
+    // epilogue in the same launch (relation items write Y, root items finish the rows without a
+    // segment, single_fix_kernel the others)
+    if (o.gemm_bf3 && K == 256 && (a.node_map == nullptr || !dgrad)) {
         if (dgrad) launch_rel_gemm_bf3w<true>(a, st);
         else launch_rel_gemm_bf3w<false>(a, st);
         return;
