@@ -389,7 +389,13 @@ enum mpgnn_option {
                                     round-4 skeleton (whole tile in one k-step); outputs bit-identical */,
     MPGNN_OPT_GEMM_CU_PAIRS = 31 /* 1 (default): the bf16-split GEMM's item ranges are balanced per CU (the two
                                     workgroups a CU runs take the halves of one CU range); 0: per workgroup;
-                                    outputs bit-identical */
+                                    outputs bit-identical */,
+    MPGNN_OPT_OUTER_SQ = 32      /* 1: the bf16-split weight gradient (F = 128, and the quadrants at 256) gives each
+                                    wave a 64 x 64 quarter of the slab and schedules the next slice's commit among
+                                    the MFMAs; 0 (default, measured faster at C3: 65.7 vs 68.0 us): 128 x 32
+                                    strips; slabs bit-identical */,
+    MPGNN_OPT_OUTER_RANGES = 33  /* 1 (default): that kernel's workgroups take contiguous chunk ranges balanced by
+                                    16-row slices (per CU); 0: every G-th chunk; slabs bit-identical */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

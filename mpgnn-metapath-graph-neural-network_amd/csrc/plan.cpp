@@ -719,10 +719,11 @@ int32_t mpgnn_plan_destroy(mpgnn_plan* p) {
         free_device_plan(p);
         if (p->d.rel_node_map) (void)hipFree(p->d.rel_node_map);
         for (auto& kv : p->bw_slabs) (void)hipFree(kv.second.dev);
-        for (auto& kv : p->gemm_ranges) {
-            (void)hipFree(kv.second.dev);
-            (void)hipHostFree(kv.second.host);
-        }
+        for (auto* m : {&p->gemm_ranges, &p->outer_ranges})
+            for (auto& kv : *m) {
+                (void)hipFree(kv.second.dev);
+                (void)hipHostFree(kv.second.host);
+            }
         (void)hipSetDevice(prev);
     }
     delete p;

@@ -26,6 +26,8 @@ struct Options {
     bool bwd_fused = true;        // MPGNN_OPT_BWD_FUSED: see bwd_bf3_kernel
     bool flat_fuse_split = true;  // MPGNN_OPT_FLAT_FUSE_SPLIT: hub rows of grad_x finished in the gather launch
     bool outer_vec = true;        // MPGNN_OPT_OUTER_VEC: outer_bf3v_kernel (16-B gathers, transposed LDS reads)
+    bool outer_sq = false;        // MPGNN_OPT_OUTER_SQ: its 64 x 64 wave quarters + interleaved commit (measured slower)
+    bool outer_ranges = true;     // MPGNN_OPT_OUTER_RANGES: its chunks in balanced contiguous ranges per workgroup
     bool gemm_il = true;          // MPGNN_OPT_GEMM_IL: the interleaved GEMM item skeleton
     bool gemm_cu_pairs = true;    // MPGNN_OPT_GEMM_CU_PAIRS: GEMM item ranges balanced per CU
     int gemm_switch_cost = 250;   // MPGNN_OPT_GEMM_SWITCH_COST: percent of an item per weight switch
@@ -252,6 +254,8 @@ struct mpgnn_plan {
         int* host = nullptr;  // pinned
     };
     mutable std::map<std::array<int64_t, 5>, GemmRanges> gemm_ranges;
+    // outer_bf3v_kernel_t's per-workgroup chunk ranges (same ownership as gemm_ranges)
+    mutable std::map<std::array<int64_t, 5>, GemmRanges> outer_ranges;
 };
 
 namespace mpgnn {

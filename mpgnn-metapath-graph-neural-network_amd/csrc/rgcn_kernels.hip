@@ -3268,6 +3268,13 @@ struct OuterArgs {
     // D / P matrix, elements per P slab, per Pb row
     int lda, ldb, a_col0, b_col0, ldd, d_off, pb_stride;
     int64_t p_stride;
+    // outer_bf3v_kernel_t (round 5): nullable [G + 1] first chunk of each workgroup's contiguous
+    // chunk range, balanced by slices (outer_ranges); wg_cus > 0: ranges 2c, 2c + 1 on one CU
+    const int* wg_chunks;
+    int wg_cus;
+#ifdef MPGNN_STAMPS
+    unsigned long long* stamps;  // debug build: per-slice phase stamps (scripts/stamps_outer.py)
+#endif
 };
 
 constexpr int kOuterLd = 288;                        // one row pair: 128 + 32 pad + 128
@@ -3481,6 +3488,7 @@ __global__ __launch_bounds__(kThreads, 2) void outer_accum_kernel(OuterArgs a) {
 // partial goes out after the next slice is committed (its stores never hold up a commit).
 // Same arithmetic per chunk as outer_accum_body (32-row blocks, block totals in row order).
 struct OuterCursor {
+    int pos;        // position in the workgroup's chunk sequence (outer_bf3v_kernel_t; else = chunk)
     int chunk;      // global chunk id: [0, ra_n) root chunks, then weight chunks
     int sl, ns;     // slice within the chunk, slices of the chunk
     int p0, p1;     // the chunk's row range
@@ -4018,13 +4026,29 @@ __device__ __forceinline__ bf16x8 ov_frag(const __bf16* plane, int k0, int col0,
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-__global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel(OuterArgs ra, OuterArgs wa, int ra_n, int n_all) {
+// SQ (round 5, MPGNN_OPT_OUTER_SQ): each wave owns a 64 × 64 quarter of the 128 × 128 slab (2 × 2
+// blocks of 32 × 32: twelve fragments per k-step, 24 transposed reads for 24 MFMAs, against 15
+// fragments / 30 reads for a 128 × 32 strip), and the next slice's commit is scheduled among the
+// MFMAs (branch-free; past the last slice it writes zeros nobody reads). Same products, same
+// per-block accumulators: bit-identical slabs.
+template <bool SQ>
+__global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel_t(OuterArgs ra, OuterArgs wa, int ra_n, int n_all) {
     constexpr int SL = 16;
     extern __shared__ __attribute__((aligned(16))) __bf16 ov_smem[];
     __bf16* planes = ov_smem;                                         // [2][A0 A1 A2 B0 B1 B2][16][160]
     float* bx = reinterpret_cast<float*>(ov_smem + 2 * 6 * kOvPlane);  // [8 row groups][128] bias partials
     const int G = (int)gridDim.x;
-    if ((int)blockIdx.x >= n_all) return;
+    // the workgroup's chunks: its list of the host's window-balanced deal (outer_ranges), or every
+    // G-th chunk. Cursors walk list positions; chunk id = list[position]
+    int c_beg = (int)blockIdx.x, c_end = n_all, c_step = G;
+    const int* clist = nullptr;
+    if (ra.wg_chunks != nullptr) {
+        c_beg = ld_uniform(ra.wg_chunks, (int)blockIdx.x);
+        c_end = ld_uniform(ra.wg_chunks, (int)blockIdx.x + 1);
+        c_step = 1;
+        clist = ra.wg_chunks + G + 1;
+    }
+    if (c_beg >= c_end) return;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
@@ -4053,8 +4077,10 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel(OuterArgs ra, O
         x.a2_off = r ? ra.a2_off : wa.a2_off;
         return x;
     };
-    auto open_chunk = [&](int chunk) {
+    auto open_chunk = [&](int pos) {
         OuterCursor k;
+        k.pos = pos;
+        const int chunk = pos < c_end ? (clist != nullptr ? ld_uniform(clist, pos) : pos) : n_all;
         k.chunk = chunk;
         k.sl = 0;
         int p0 = 0, p1 = 0;
@@ -4076,9 +4102,9 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel(OuterArgs ra, O
             n.sl = k.sl + 1;
             return n;
         }
-        return open_chunk(k.chunk + G);
+        return open_chunk(k.pos + c_step);
     };
-    auto valid = [&](const OuterCursor& k) { return k.chunk < n_all && k.ns > 0; };
+    auto valid = [&](const OuterCursor& k) { return k.pos < c_end && k.ns > 0; };
 
     // row indices of a slice: lanes 0..3 of the wave hold those of its staged rows
     // 2·wave, 2·wave + 1, 2·wave + 8, 2·wave + 9
@@ -4139,8 +4165,12 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel(OuterArgs ra, O
         }
     float bpart[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // this thread's columns over its rows (root chunks)
 
-    OuterCursor cur = open_chunk((int)blockIdx.x);
+    OuterCursor cur = open_chunk(c_beg);
     if (!valid(cur)) return;
+#ifdef MPGNN_STAMPS
+    stamp_id_at(ra.stamps);
+    int nsl = 0;  // slices done (stamped while < kStampItems)
+#endif
     OuterCursor c1 = advance(cur);
     OuterCursor c2 = valid(c1) ? advance(c1) : c1;
     OuterCursor c3 = valid(c2) ? advance(c2) : c2;
@@ -4160,6 +4190,9 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel(OuterArgs ra, O
     const int kq = 8 * (g >> 1);      // the group's k rows: kq .. kq + 8 (= 8·h)
     const int mq = 16 * (g & 1);      // the group's 16 columns within a 32-column block
     auto step = [&](float4 (&vca)[2], float4 (&vcb)[2], float4 (&vna)[2], float4 (&vnb)[2]) -> bool {
+#ifdef MPGNN_STAMPS
+        stamp_at(ra.stamps, nsl, 0);
+#endif
         const bool more = valid(c1);
         if (valid(c2)) {
             issue(c2, ja, jb, vna, vnb);
@@ -4167,21 +4200,59 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel(OuterArgs ra, O
         }
         const bool is_root = cur.chunk < ra_n;
         const __bf16* cb = planes + buf * 6 * kOvPlane;
-        const int ncol = wave * 32 + mq;
-        const bf16x8 b0 = ov_frag(cb + 3 * kOvPlane, kq, ncol, lane);
-        const bf16x8 b1 = ov_frag(cb + 4 * kOvPlane, kq, ncol, lane);
-        const bf16x8 b2 = ov_frag(cb + 5 * kOvPlane, kq, ncol, lane);
+        if constexpr (!SQ) {
+            const int ncol = wave * 32 + mq;
+            const bf16x8 b0 = ov_frag(cb + 3 * kOvPlane, kq, ncol, lane);
+            const bf16x8 b1 = ov_frag(cb + 4 * kOvPlane, kq, ncol, lane);
+            const bf16x8 b2 = ov_frag(cb + 5 * kOvPlane, kq, ncol, lane);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const bf16x8 a0 = ov_frag(cb, kq, q * 32 + mq, lane);
-            const bf16x8 a1 = ov_frag(cb + kOvPlane, kq, q * 32 + mq, lane);
-            const bf16x8 a2 = ov_frag(cb + 2 * kOvPlane, kq, q * 32 + mq, lane);
-            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, lo[q], 0, 0, 0);
-            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, lo[q], 0, 0, 0);
-            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, lo[q], 0, 0, 0);
-            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, lo[q], 0, 0, 0);
-            lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, lo[q], 0, 0, 0);
-            hi[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, hi[q], 0, 0, 0);
+            for (int q = 0; q < 4; ++q) {
+                const bf16x8 a0 = ov_frag(cb, kq, q * 32 + mq, lane);
+                const bf16x8 a1 = ov_frag(cb + kOvPlane, kq, q * 32 + mq, lane);
+                const bf16x8 a2 = ov_frag(cb + 2 * kOvPlane, kq, q * 32 + mq, lane);
+                lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, lo[q], 0, 0, 0);
+                lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, lo[q], 0, 0, 0);
+                lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, lo[q], 0, 0, 0);
+                lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, lo[q], 0, 0, 0);
+                lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, lo[q], 0, 0, 0);
+                hi[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, hi[q], 0, 0, 0);
+            }
+        } else {
+            // wave quarter (mh, nh): blocks q = 2·qm + qn at rows 64·mh + 32·qm, cols 64·nh + 32·qn
+            const int mh = wave >> 1, nh = wave & 1;
+            bf16x8 bq[2][3];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) bq[j][p] = ov_frag(cb + (3 + p) * kOvPlane, kq, 64 * nh + 32 * j + mq, lane);
+            commit(c1, vca, vcb, planes + (buf ^ 1) * 6 * kOvPlane);  // unconditional: zeros past the end
+            __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // the B fragments first
+#pragma unroll
+            for (int qm = 0; qm < 2; ++qm) {
+                bf16x8 a[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) a[p] = ov_frag(cb + p * kOvPlane, kq, 64 * mh + 32 * qm + mq, lane);
+#pragma unroll
+                for (int qn = 0; qn < 2; ++qn) {
+                    const int q = 2 * qm + qn;
+                    const bf16x8* b = bq[qn];
+                    lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], lo[q], 0, 0, 0);
+                    lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], lo[q], 0, 0, 0);
+                    lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], lo[q], 0, 0, 0);
+                    lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], lo[q], 0, 0, 0);
+                    lo[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], lo[q], 0, 0, 0);
+                    hi[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], hi[q], 0, 0, 0);
+                }
+                // this half's A fragments, then its MFMAs with the commit's VALU and LDS writes
+                __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+                for (int m = 0; m < 12; ++m) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+                    if (m < 6) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
         if (is_root && ra.Pb != nullptr) {  // bias: column sums over the chunk's rows, exact from the pieces
             const int nr = min(SL, cur.p1 - cur.p0 - cur.sl * SL);
@@ -4197,7 +4268,13 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel(OuterArgs ra, O
             }
         }
         const bool chunk_end = cur.sl + 1 == cur.ns;
-        if (more) commit(c1, vca, vcb, planes + (buf ^ 1) * 6 * kOvPlane);
+#ifdef MPGNN_STAMPS
+        stamp_at(ra.stamps, nsl, 1);
+#endif
+        if (!SQ && more) commit(c1, vca, vcb, planes + (buf ^ 1) * 6 * kOvPlane);
+#ifdef MPGNN_STAMPS
+        stamp_at(ra.stamps, nsl, 2);
+#endif
         if (chunk_end) {
             float* D;
             float* Db = nullptr;
@@ -4218,17 +4295,29 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel(OuterArgs ra, O
                 }
             }
             const int ln = opaque(lane);
-            const int ocol = wave * 32 + (ln & 31);
             const int h4 = 4 * (ln >> 5);
             if (D != nullptr) {
-                float* Dc = D + ocol;
+                if constexpr (!SQ) {
+                    float* Dc = D + wave * 32 + (ln & 31);
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
+                    for (int q = 0; q < 4; ++q)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int m = q * 32 + (r & 3) + 8 * (r >> 2) + h4;
-                        Dc[(size_t)m * ldd] = hi[q][r] + lo[q][r];
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = q * 32 + (r & 3) + 8 * (r >> 2) + h4;
+                            Dc[(size_t)m * ldd] = hi[q][r] + lo[q][r];
+                        }
+                } else {
+                    const int mh = wave >> 1, nh = wave & 1;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        float* Dc = D + 64 * nh + 32 * (q & 1) + (ln & 31);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = 64 * mh + 32 * (q >> 1) + (r & 3) + 8 * (r >> 2) + h4;
+                            Dc[(size_t)m * ldd] = hi[q][r] + lo[q][r];
+                        }
                     }
+                }
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -4250,7 +4339,16 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel(OuterArgs ra, O
                 }
             }
         }
+#ifdef MPGNN_STAMPS
+        stamp_at(ra.stamps, nsl, 3);
+        if (chunk_end) stamp_at(ra.stamps, nsl, 5);
+#endif
         __syncthreads();
+#ifdef MPGNN_STAMPS
+        stamp_at(ra.stamps, nsl, 4);
+        ++nsl;
+        if (!more) stamp_end_at(ra.stamps);
+#endif
         if (!more) return false;
         cur = c1;
         c1 = c2;
@@ -5001,6 +5099,74 @@ static const int* gemm_ranges(const mpgnn_plan* p, int t_lo, int n_rel, int n_ro
     return e.dev;
 }
 
+// outer_bf3v_kernel_t's chunk lists per workgroup. The chunks are dealt in windows of G
+// consecutive chunks (as round robin: every workgroup works in the same window at a time, so the
+// rows gathered concurrently stay a narrow slice of the relation-major order — contiguous ranges
+// per workgroup measured 10 µs slower at C3: 67.5 -> 77.5), but inside a window the chunks go,
+// largest first, to the workgroups with the least cost so far (cost = 16-row slices + 1 for the
+// chunk-end slab store). Chunks [0, n_root): root chunks (rows row_lo.. in chunk_rows pieces),
+// then the plan's weight chunks [c_lo, c_lo + nch). Table: [G + 1] list offsets, then the lists.
+// Cached per plan, made outside captures (nullptr: the kernel's round robin).
+static const int* outer_ranges(const mpgnn_plan* p, int c_lo, int nch, int row_lo, int row_hi, int chunk_rows,
+                               int n_root, int G, hipStream_t st) {
+    if (G <= 1) return nullptr;
+    const std::array<int64_t, 5> key{c_lo, nch, (int64_t)row_lo * 4096 + chunk_rows, row_hi, G};
+    std::lock_guard<std::mutex> lk(p->bw_mu);
+    auto it = p->outer_ranges.find(key);
+    if (it != p->outer_ranges.end()) return it->second.dev;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    if ((int64_t)p->chunk_begin.size() < (int64_t)c_lo + nch || (int64_t)p->chunk_end.size() < (int64_t)c_lo + nch)
+        return nullptr;
+    const int n = n_root + nch;
+    std::vector<int> cost(n);
+    for (int k = 0; k < n; ++k) {
+        int rows;
+        if (k < n_root) rows = std::min(chunk_rows, row_hi - (row_lo + k * chunk_rows));
+        else rows = p->chunk_end[c_lo + k - n_root] - p->chunk_begin[c_lo + k - n_root];
+        cost[k] = (std::max(rows, 0) + 15) / 16 + 1;
+    }
+    std::vector<std::vector<int>> lists(G);
+    std::vector<int64_t> load(G, 0);
+    std::vector<int> order, wgs(G);
+    for (int w0 = 0; w0 < n; w0 += G) {
+        const int w1 = std::min(n, w0 + G);
+        order.resize(w1 - w0);
+        for (int k = w0; k < w1; ++k) order[k - w0] = k;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+        for (int g = 0; g < G; ++g) wgs[g] = g;
+        std::stable_sort(wgs.begin(), wgs.end(), [&](int a, int b) { return load[a] < load[b]; });
+        for (size_t j = 0; j < order.size(); ++j) {
+            const int g = wgs[j];
+            lists[g].push_back(order[j]);
+            load[g] += cost[order[j]];
+        }
+    }
+    for (auto& l : lists) std::sort(l.begin(), l.end());  // each workgroup walks its chunks in order
+    const size_t words = (size_t)G + 1 + (size_t)n;
+    mpgnn_plan::GemmRanges e;
+    if (hipHostMalloc(reinterpret_cast<void**>(&e.host), words * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    int* tab = e.host;
+    int pos = 0;
+    for (int g = 0; g < G; ++g) {
+        tab[g] = pos;
+        for (int k : lists[g]) tab[G + 1 + pos++] = k;
+    }
+    tab[G] = pos;
+    if (hipMalloc(reinterpret_cast<void**>(&e.dev), words * sizeof(int)) != hipSuccess ||
+        hipMemcpyAsync(e.dev, e.host, words * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
+        (void)hipGetLastError();
+        if (e.dev) (void)hipFree(e.dev);
+        (void)hipHostFree(e.host);
+        return nullptr;
+    }
+    p->outer_ranges[key] = e;
+    return e.dev;
+}
+
 static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, const Options& o, hipStream_t st) {
     if (o.gemm_bf3 && (K == 64 || K == 128) && a.node_map == nullptr) {
         if (K == 64) {
@@ -5474,10 +5640,15 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
     return hip_check(hipGetLastError(), "row_sum_kernel launch");
 }
 
-static void launch_outer_bf3(dim3 grid, const OuterArgs& r, const OuterArgs& w, int ra_n, int n_all, bool vec,
-                             hipStream_t st) {
+static void launch_outer_bf3(dim3 grid, const OuterArgs& r_in, const OuterArgs& w, int ra_n, int n_all, bool vec,
+                             bool sq, hipStream_t st) {
+    OuterArgs r = r_in;
+#ifdef MPGNN_STAMPS
+    r.stamps = g_stamps_host;
+#endif
     if (vec)
-        hipLaunchKernelGGL(outer_bf3v_kernel, grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
+        if (sq) hipLaunchKernelGGL(outer_bf3v_kernel_t<true>, grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
+        else hipLaunchKernelGGL(outer_bf3v_kernel_t<false>, grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
     else
         hipLaunchKernelGGL(outer_bf3_kernel, grid, dim3(kThreads), kOb3Lds, st, r, w, ra_n, n_all);
 }
@@ -5883,7 +6054,7 @@ int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int
         orr.dst_b = grad_bias;
         orr.bias_of_a = 1;
         OuterArgs none{};
-        launch_outer_bf3(dim3(std::min(nch, cu_count() * 2)), orr, none, nch, nch, default_options().outer_vec, strm);
+        launch_outer_bf3(dim3(std::min(nch, cu_count() * 2)), orr, none, nch, nch, default_options().outer_vec, default_options().outer_sq, strm);
         int32_t st = hip_check(hipGetLastError(), "outer_bf3_kernel (linear) launch");
         if (st != MPGNN_OK || nch == 1) return st;
         ReduceArgs rw{}, rb{};
@@ -5928,6 +6099,8 @@ static int32_t set_switch(Options& o, int32_t option, int64_t value) {
         case MPGNN_OPT_BWD_FUSED: o.bwd_fused = value != 0; return MPGNN_OK;
         case MPGNN_OPT_FLAT_FUSE_SPLIT: o.flat_fuse_split = value != 0; return MPGNN_OK;
         case MPGNN_OPT_OUTER_VEC: o.outer_vec = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_OUTER_SQ: o.outer_sq = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_OUTER_RANGES: o.outer_ranges = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_SWITCH_COST:
             if (value < 0 || value > 10000) return arg_error("MPGNN_OPT_GEMM_SWITCH_COST must be 0..10000 (percent of an item)");
             o.gemm_switch_cost = (int)value;
@@ -5950,6 +6123,8 @@ static bool get_switch(const Options& o, int32_t option, int64_t* value) {
         case MPGNN_OPT_BWD_FUSED: *value = o.bwd_fused; return true;
         case MPGNN_OPT_FLAT_FUSE_SPLIT: *value = o.flat_fuse_split; return true;
         case MPGNN_OPT_OUTER_VEC: *value = o.outer_vec; return true;
+        case MPGNN_OPT_OUTER_SQ: *value = o.outer_sq; return true;
+        case MPGNN_OPT_OUTER_RANGES: *value = o.outer_ranges; return true;
         case MPGNN_OPT_GEMM_SWITCH_COST: *value = o.gemm_switch_cost; return true;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = o.flat_wg_per_cu; return true;
         default: return false;
@@ -6951,10 +7126,19 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
     // droot slab (the bias column sums taken by the two quadrants of the first A half)
     const bool bf3q = have_w && have_root && root_y == mt && p->opt.gemm_bf3 && F_in == 256 && F_out == 256 && !acc;
     if (acc && !bf3) return MPGNN_ERR_UNSUPPORTED;  // (excluded by rgcn_bwd_impl's check)
+    // balanced contiguous chunk ranges per workgroup (outer_bf3v_kernel_t only)
+    auto with_ranges = [&](OuterArgs& o, int n_all, int gx) {
+        o.wg_chunks = nullptr;
+        o.wg_cus = 0;
+        if (!p->opt.outer_vec || !p->opt.outer_ranges) return;
+        o.wg_chunks = outer_ranges(p, s.c_lo, nch, rc.rows_lo, rc.rows_hi, rc.chunk, rc.n, gx, strm);
+        (void)n_all;
+    };
     if (bf3q) {
         TimedLaunch tl(MPGNN_K_OUTER, strm);
         const int n_all = nch + rc.n;
         const int gx = std::max(1, std::min(n_all, cu_count() * 2));
+        with_ranges(orr, n_all, gx);
         for (int qa = 0; qa < 2; ++qa)
             for (int qb = 0; qb < 2; ++qb) {
                 OuterArgs rq = orr, wq = ow;
@@ -6972,7 +7156,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
                     rq.Pb = nullptr;
                     rq.dst_b = nullptr;
                 }
-                launch_outer_bf3(dim3(gx), rq, wq, rc.n, n_all, p->opt.outer_vec, strm);
+                launch_outer_bf3(dim3(gx), rq, wq, rc.n, n_all, p->opt.outer_vec, p->opt.outer_sq, strm);
                 if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel (quadrant) launch")) != MPGNN_OK) return st;
             }
     } else if (bf3) {
@@ -6980,7 +7164,8 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
         TimedLaunch tl(MPGNN_K_OUTER, strm);
         const int n_all = nch + rc.n;
         const int gx = std::max(1, std::min(n_all, cu_count() * 2));
-        launch_outer_bf3(dim3(gx), orr, ow, rc.n, n_all, p->opt.outer_vec, strm);
+        with_ranges(orr, n_all, gx);
+        launch_outer_bf3(dim3(gx), orr, ow, rc.n, n_all, p->opt.outer_vec, p->opt.outer_sq, strm);
         if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel launch")) != MPGNN_OK) return st;
     } else if (have_w && have_root && root_y == mt) {
         TimedLaunch tl(MPGNN_K_OUTER, strm);

@@ -134,11 +134,23 @@ __global__ __launch_bounds__(kScoreThreads) void score_scatter_kernel(
 // start), max_weights[bag] = v. One wave per bag walks its members in order; each member's
 // argmax is the wave-parallel first-argmax of score_argmax_kernel over the products.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float dot_seq(const float* __restrict__ f, const float* __restrict__ wl, int F) {
-    // F.linear of one feature row: products added in feature order, no contraction into FMAs
-    // (exact for the one-hot colour features of the reference's datasets)
+// F.linear of one feature row, the same value in every lane of the wave. F <= 32: products added
+// in feature order, no contraction into FMAs — the reference's CPU nn.Linear order at these sizes
+// and exact for the one-hot colour features of its datasets (tests/test_score_bags.py pins the
+// picks bit for bit). Wider rows (dense real features): lane l adds features l, l+64,
+// ... in order, then a fixed xor butterfly — deterministic, one coalesced pass instead of every
+// lane walking all F features; the reference's BLAS order is unknowable, so there the picks are
+// held to the CPU nn.Linear path except at near-ties (tests/test_score_bags.py, dense case).
+__device__ __forceinline__ float dot_row(const float* __restrict__ f, const float* __restrict__ wl, int F, int lane) {
+    if (F <= 32) {
+        float acc = 0.0f;
+        for (int j = 0; j < F; ++j) acc = __fadd_rn(acc, __fmul_rn(f[j], wl[j]));
+        return acc;
+    }
     float acc = 0.0f;
-    for (int j = 0; j < F; ++j) acc = __fadd_rn(acc, __fmul_rn(f[j], wl[j]));
+    for (int j = lane; j < F; j += 64) acc = __fadd_rn(acc, __fmul_rn(f[j], wl[j]));
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) acc = __fadd_rn(acc, __shfl_xor(acc, sh));
     return acc;
 }
 
@@ -158,7 +170,7 @@ __global__ __launch_bounds__(kScoreThreads) void score_bag_argmax_kernel(
     for (int32_t m = mb; m < me; ++m) {
         const int32_t k = mem_key[m];
         if (k < 0) continue;  // `if source_node in node_dict` (model.py:59)
-        const float s = dot_seq(feat + (size_t)mem_node[m] * F, wlin, F);
+        const float s = dot_row(feat + (size_t)mem_node[m] * F, wlin, F, lane);
         const int32_t b = key_ptr[k], e = key_ptr[k + 1];
         float bv = 0.0f;
         int32_t bp = INT32_MAX, bn = 0;

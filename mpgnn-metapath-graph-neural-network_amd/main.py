@@ -129,6 +129,7 @@ def _graphs_enabled(data) -> bool:
 
 
 _LOOP_STREAMS: dict = {}
+_LOOP_ACTIVE: set = set()  # devices whose loop stream a running _epochs generator owns
 
 
 def _loop_stream() -> torch.cuda.Stream:
@@ -149,7 +150,11 @@ def _epochs(epoch_fn, epochs: int, use_graph: bool, warmup: int = 3):
     (nothing executes during the capture) and replayed for the remaining epochs: every epoch
     still runs every kernel of the reference's epoch, the host only issues one launch per
     epoch. Falls back to eager epochs if the capture fails."""
-    if not use_graph or epochs <= warmup:
+    dev = torch.cuda.current_device() if use_graph else None
+    if not use_graph or epochs <= warmup or dev in _LOOP_ACTIVE:
+        # (a loop nested in or interleaved with another on this device runs eagerly: the shared
+        # side stream's scratch buffers belong to the outer loop's captured graph, and releasing
+        # them at this loop's end would free memory that graph still replays into — ADVICE r4)
         for e in range(1, epochs + 1):
             yield e, epoch_fn()
         return
@@ -157,6 +162,7 @@ def _epochs(epoch_fn, epochs: int, use_graph: bool, warmup: int = 3):
     side = _loop_stream()
     side.wait_stream(torch.cuda.current_stream())
     graph = None
+    _LOOP_ACTIVE.add(dev)
     try:
         with torch.cuda.stream(side):
             for e in range(1, warmup + 1):
@@ -182,6 +188,7 @@ def _epochs(epoch_fn, epochs: int, use_graph: bool, warmup: int = 3):
         graph = None
         side.wait_stream(torch.cuda.current_stream())
         release_workspaces(side)
+        _LOOP_ACTIVE.discard(dev)
 
 
 def _num_classes(out: torch.Tensor) -> int:

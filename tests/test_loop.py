@@ -359,3 +359,39 @@ def test_loops_release_their_workspace_between_calls():
             torch.cuda.synchronize()
             assert torch.cuda.memory_allocated() == base, (torch.cuda.memory_allocated(), base)
             assert workspace_bytes_cached() == base_ws, (workspace_bytes_cached(), base_ws)
+
+
+@pytest.mark.gpu
+def test_interleaved_loops_keep_the_outer_graph_valid():
+    """two _epochs loops interleaved on one device. The inner loop must not
+    release the shared side stream's scratch buffers under the outer loop's captured graph — it
+    runs eagerly instead — and the outer loop's replayed epochs still equal the eager ones."""
+    g = data.config_graph("C1")
+    d = _task(g).to(DEV)
+    big = data.synthetic_graph(20000, 5, 12, feat_dim=128, seed=8)
+    xb, eib, etb = big.x.to(DEV), big.edge_index.to(DEV), big.edge_type.to(DEV)
+
+    def make(seed):
+        torch.manual_seed(seed)
+        net = mpgnn_amd.Net(d.x.shape[1], 64, g.num_relations, 64, 3, 3).to(DEV)
+        return net, main._adam_graphable(net)
+
+    def epoch_fn(net, opt):
+        def fn():
+            loss, _ = main._train_step(net, opt, d)
+            return loss
+        return fn
+    net_a, opt_a = make(30)
+    ref_a, ref_opt = make(30)
+    losses_ref = [float(epoch_fn(ref_a, ref_opt)()) for _ in range(8)]
+    gen_a = main._epochs(epoch_fn(net_a, opt_a), 8, True)
+    losses = [float(next(gen_a)[1]) for _ in range(5)]  # 3 eager + capture + 1 replay
+    conv = mpgnn_amd.RGCNConv(128, 128, 5, flow="target_to_source").to(DEV)
+
+    def inner():
+        (conv(xb, eib, etb) ** 2).mean().backward()
+        return torch.zeros(())
+    for _ in main._epochs(inner, 6, True):  # a larger graph on the same device, mid-loop
+        pass
+    losses += [float(v) for _, v in gen_a]
+    assert losses == losses_ref, (losses, losses_ref)
