@@ -759,7 +759,7 @@ def bench_score_bags(args):
 def pmc_traffic(workload, mode, feat, kernel_prefix):
     """HBM bytes per launch of `kernel_prefix` from the committed PMC summary, or None."""
     rows = []
-    for rnd in ("r04", "r03", "r02"):  # the newest round's PMC summary first
+    for rnd in ("r05", "r04", "r03", "r02"):  # the newest round's PMC summary first
         try:
             rows += json.load(open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic.json")))
         except (OSError, ValueError):
@@ -929,7 +929,9 @@ def main():
     # the transform on the bf16-split matrix cores: rel_gemm_bf3_kernel (mode ALL), mode SINGLE
     # unsharded: single_bf3_kernel (split-K: x @ root and mean @ W halves, one launch per layer)
     # (F = 256, mode ALL: rel_gemm_bf3w_kernel, the split-K form of the same six-product scheme)
-    bf3 = args.gemm == "bf3" and ((F in (64, 128) and (not single or not sharded)) or (F == 256 and not single))
+    # (F = 256, mode SINGLE unsharded, round 5: rel_gemm_bf3w_kernel with the root epilogue)
+    bf3 = args.gemm == "bf3" and ((F in (64, 128) and (not single or not sharded)) or
+                                  (F == 256 and (not single or root_epi)))
     rooflines = []
     for kind, (bound, work, model_txt) in model_costs.items():
         if kind not in per_layer:
@@ -953,7 +955,7 @@ def main():
         else:
             ach = work / (us * 1e-6) / 1e9
             peak, unit = PEAK_HBM, "GB/s"
-        seg_name = ("single_bf3_kernel" if bf3 and single else
+        seg_name = ("single_bf3_kernel" if bf3 and single and F != 256 else
                     ("rel_gemm_bf3w_kernel" if F == 256 else "rel_gemm_bf3_kernel") if bf3 else "rel_gemm_kernel")
         kname = {"seg_fwd": seg_name, "mean": "flat_rows_kernel",
                  "row_fwd": ("single_fix_kernel" if root_epi else "single_combine_kernel") if single
@@ -977,7 +979,7 @@ def main():
                     "algorithmic": dom["algorithmic"],
                     "note": "dominant kernel of the forward layer by the per-kernel HIP-event pass (events on the "
                             "launch stream, one pair per launch; the headline timed region has none); traffic = "
-                            "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/r04_pmc_traffic.json; r03 / r02 for kernels not re-profiled)"}
+                            "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/r05_pmc_traffic.json; older rounds for kernels not re-profiled)"}
         # SURVEY 8d whole-step HBM roofline of the aggregation (kept beside the kernel roofline)
     b_edge = 4 * F + 4
     hbm_roofline = {"bound": "hbm", "bytes_per_edge": b_edge,
