@@ -200,6 +200,19 @@ int32_t mpgnn_linear_wgrad_workspace_bytes(int64_t N, int32_t F, int32_t O, int6
 int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int32_t F, int32_t O, float* grad_weight,
                            float* grad_bias, void* workspace, void* stream);
 
+/* Per-epoch scoring of the training loop: replaces mpgnn_validation / mpgnn_test's
+ * torch.argmax(pred[idx], 1) + the per-class counts behind f1_score(..., average='macro')
+ * (main.py:1084-1115; the reference's scikit-learn call on host lists). For each of n_lists
+ * (<= 4) lists l: p_j = argmax over the num_classes scores of row row_idx[l][j] of scores
+ * [rows, num_classes] (first maximum, a NaN wins: torch.argmax), y_j = labels[l][j];
+ * counts[l][0][c] = #{p_j = c}, counts[l][1][c] = #{y_j = c}, counts[l][2][c] = #{p_j = y_j = c}
+ * (int64, [n_lists][3][num_classes]; labels outside [0, num_classes) and rows outside
+ * [0, rows) count in no class). row_idx NULL (or row_idx[l] NULL): rows 0..n[l]-1. Host arrays
+ * of device pointers; one launch. */
+int32_t mpgnn_confusion_counts(const float* scores, int64_t rows, int32_t num_classes, int32_t n_lists,
+                               const int64_t* const* row_idx, const int64_t* const* labels, const int64_t* n,
+                               int64_t* counts, void* stream);
+
 /* Bytes of scratch the fwd/bwd calls need (caller allocates, e.g. torch.empty(uint8)). */
 int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* plan, int32_t mode, int64_t relation,
                                    int32_t num_relations, int32_t F_in, int32_t F_out,
@@ -395,7 +408,10 @@ enum mpgnn_option {
                                     the MFMAs; 0 (default, measured faster at C3: 65.7 vs 68.0 us): 128 x 32
                                     strips; slabs bit-identical */,
     MPGNN_OPT_OUTER_RANGES = 33  /* 1 (default): that kernel's workgroups take contiguous chunk ranges balanced by
-                                    16-row slices (per CU); 0: every G-th chunk; slabs bit-identical */
+                                    16-row slices (per CU); 0: every G-th chunk; slabs bit-identical */,
+    MPGNN_OPT_GEMM_W_IL = 34     /* the K = 256 bf16-split GEMM (F_in = F_out = 256, C5): 1 commits the next item's
+                                    tile in four parts among the k-steps' MFMAs (as GEMM_IL at K = 128); 0
+                                    (default): the whole tile in one k-step; outputs bit-identical */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

@@ -1070,13 +1070,13 @@ static unsigned long long* g_stamps_host = nullptr;  // set by mpgnn_debug_stamp
 #define stamp_end() stamp_end_at(a.stamps)
 __device__ __forceinline__ void stamp_at(unsigned long long* g_stamps, int k, int ph) {
     if (g_stamps != nullptr && (threadIdx.x & 63) == 0 && k < kStampItems) {
-        const size_t w = (size_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+        const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         g_stamps[(w * (kStampItems + 1) + 1 + k) * kStampPhases + ph] = __builtin_readcyclecounter();
     }
 }
 __device__ __forceinline__ void stamp_id_at(unsigned long long* g_stamps) {
     if (g_stamps != nullptr && (threadIdx.x & 63) == 0) {
-        const size_t w = (size_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+        const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         unsigned long long* o = g_stamps + w * (kStampItems + 1) * kStampPhases;
         o[0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
         o[1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
@@ -1086,14 +1086,14 @@ __device__ __forceinline__ void stamp_id_at(unsigned long long* g_stamps) {
 }
 __device__ __forceinline__ void stamp_end_at(unsigned long long* g_stamps) {
     if (g_stamps != nullptr && (threadIdx.x & 63) == 0) {
-        const size_t w = (size_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+        const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         g_stamps[w * (kStampItems + 1) * kStampPhases + 7] = __builtin_amdgcn_s_memrealtime();
     }
 }
 // prologue stamps: row 0 slots 3..5 of the wave
 __device__ __forceinline__ void stamp_pro_at(unsigned long long* g_stamps, int k) {
     if (g_stamps != nullptr && (threadIdx.x & 63) == 0) {
-        const size_t w = (size_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+        const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         g_stamps[w * (kStampItems + 1) * kStampPhases + k] = __builtin_readcyclecounter();
     }
 }
@@ -2313,6 +2313,33 @@ struct RelGemmBf3W {
         }
         if (kh == 0 && t < 32) sc[t] = DGRAD ? 1.0f / (float)cnt : (float)cnt;  // forward: root-epilogue flag
     }
+    // IL: one float4 part of the commit (rows past nrows: zeros) / of the row issue
+    __device__ static __forceinline__ void commit_part(int j, int kh, int t, int nrows, const float4& v, __bf16* planes) {
+        __bf16* P = planes + kh * 3 * PLANE;
+        const int r = t / 32 + 8 * j;
+        const float4 x = r < nrows ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+        __bf16 p0[4], p1[4], p2[4];
+        split3_bf16(x.x, p0[0], p1[0], p2[0]);
+        split3_bf16(x.y, p0[1], p1[1], p2[1]);
+        split3_bf16(x.z, p0[2], p1[2], p2[2]);
+        split3_bf16(x.w, p0[3], p1[3], p2[3]);
+        __bf16* d = P + r * LDAB + (t & 31) * 4;
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<bf16x4*>(d) = bf16x4{p0[0], p0[1], p0[2], p0[3]};
+        *reinterpret_cast<bf16x4*>(d + PLANE) = bf16x4{p1[0], p1[1], p1[2], p1[3]};
+        *reinterpret_cast<bf16x4*>(d + 2 * PLANE) = bf16x4{p2[0], p2[1], p2[2], p2[3]};
+    }
+    __device__ static __forceinline__ void issue_part(const RelGemmArgs& a, int j, int kh, int t, int row, float4& v) {
+        const int c4 = kh * KH + (t & 31) * 4;
+        (void)j;
+        const float* base;
+        if constexpr (DGRAD) {
+            base = a.Aroot + (size_t)row * K;
+        } else {
+            base = row >= 0 ? a.Aroot + (size_t)row * K : a.Arel + (size_t)(-row - 1 - a.m_lo) * K;
+        }
+        v = *reinterpret_cast<const float4*>(base + c4);
+    }
     // the wave's slice: B(kh·128 + 16s + 8h + j, col) in bf16 pieces
     __device__ static __forceinline__ void load_b(const float* w, int kh, int col, int h, bf16x8 (&b)[NS][3]) {
         float f[NS][8];
@@ -2345,7 +2372,12 @@ struct RelGemmBf3W {
     }
 };
 
-template <bool DGRAD>
+// IL (round 5, MPGNN_OPT_GEMM_W_IL; GEMM_IL's skeleton at K = 128): the next item's commit and the row loads of the
+// item after it cut into their four float4 parts, part j committed and re-issued in k-step
+// 2j + 1 among that k-step's MFMAs (sched_group_barrier), the stores of the previous item
+// unconditional (the upper K half's target has no bytes: dropped by the bounds check), so the
+// k-steps carry no branch. Same products, same order: bit-identical outputs.
+template <bool DGRAD, bool IL = false>
 __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
     using G = RelGemmBf3W<DGRAD>;
     extern __shared__ __bf16 smem_bf[];
@@ -2368,6 +2400,7 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
     const int i_beg = (int)((long long)rng * n_items / n_ranges);
     const int i_end = (int)((long long)(rng + 1) * n_items / n_ranges);
     if (i_beg >= i_end) return;
+    stamp_id();
     const int col = cb * 128 + wq * 32 + c;
     const bool root_epi = !DGRAD && a.node_map != nullptr;
     const float bias_c = (root_epi && a.bias != nullptr) ? a.bias[col] : 0.0f;
@@ -2411,6 +2444,7 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
     };
     int buf = 0;
     for (int i = i_beg; i < i_end; ++i) {
+        stamp(i - i_beg, 0);
         const bool has_next = i + 1 < i_end;
         const __bf16* Ab = As + (buf * 2 + kh) * 3 * G::PLANE + c * G::LDAB + 8 * h;
         // the small products in their own accumulator (as rel_gemm_bf3_kernel): the a0·b0 chain
@@ -2439,16 +2473,39 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][0], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][1], acc, 0, 0, 0);
             hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][0], hi, 0, 0, 0);
-            if (kh == 0) {  // item i-1's tile leaves two rows per k-step
-                store_prev(2 * s);
+            if constexpr (!IL) {
+                if (kh == 0) {  // item i-1's tile leaves two rows per k-step
+                    store_prev(2 * s);
+                    store_prev(2 * s + 1);
+                }
+                if (s == (3 * G::NS) / 4 - 1 && has_next) {
+                    G::commit(nxt, kh, t, v, cnt1, As + (buf ^ 1) * 6 * G::PLANE, Sc + ((i + 1) % 3) * 32);
+                    if (i + 2 < i_end) G::issue(a, kh, t, row, v);  // item i+2's rows, in flight for a chain
+                }
+            } else {
+                store_prev(2 * s);  // upper half: zero-byte target, dropped
                 store_prev(2 * s + 1);
-            }
-            if (s == (3 * G::NS) / 4 - 1 && has_next) {
-                G::commit(nxt, kh, t, v, cnt1, As + (buf ^ 1) * 6 * G::PLANE, Sc + ((i + 1) % 3) * 32);
-                if (i + 2 < i_end) G::issue(a, kh, t, row, v);  // item i+2's rows, in flight for a chain
+                if ((s & 1) == 1) {  // part j = s / 2 of item i+1's tile, then item i+2's rows of part j
+                    const int j = s >> 1;
+                    G::commit_part(j, kh, t, has_next ? nxt.nrows : 0, v[j], As + (buf ^ 1) * 6 * G::PLANE);
+                    G::issue_part(a, j, kh, t, row[j], v[j]);
+                }
+                if (s == 1) {
+                    if (kh == 0 && t < 32) Sc[((i + 1) % 3) * 32 + t] = DGRAD ? 1.0f / (float)cnt1 : (float)cnt1;
+                }
+                __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // next fragments
+#pragma unroll
+                for (int m = 0; m < 6; ++m) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+                    if (m < 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                    if (m < 2) __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);
+                    if (m == 2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        stamp(i - i_beg, 1);
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = hi[r] + acc[r];
         float* Oe = Ot + buf * 32 * G::LDO;
@@ -2475,7 +2532,9 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
             nxt = nn;
             cnt1 = cnt2;
         }
+        stamp(i - i_beg, 3);
         __syncthreads();  // upper partial tile of item i in LDS; item i+1's tiles committed
+        stamp(i - i_beg, 4);
         if (kh == 0) {
             const float* sc = Sc + (i % 3) * 32;
 #pragma unroll
@@ -2498,7 +2557,7 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
             float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * G::N : a.Y + (size_t)(cur.r0 - a.sel_b) * G::N;
             const int bytes = __builtin_amdgcn_readfirstlane(cur.nrows) * G::N * 4;
             prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(Yt, (short)0, bytes, 0x00020000);
-        }
+        }  // (the upper half's rsrc keeps 0 bytes: its IL stores are dropped)
         cur = next_item;
         buf ^= 1;
     }
@@ -2506,6 +2565,7 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) store_prev(r);
     }
+    stamp_end();
 }
 
 template <int KB>  // Kp = 64·KB
@@ -5010,12 +5070,13 @@ static void launch_rel_gemm_bf3(const RelGemmArgs& a, bool il, hipStream_t st) {
 // K = N = 256: one 512-thread workgroup per CU; column-block pairs on one XCD (grid a multiple of
 // 16: 8 XCDs × pairs), item ranges split over the pairs
 template <bool DGRAD>
-static void launch_rel_gemm_bf3w(const RelGemmArgs& a, hipStream_t st) {
+static void launch_rel_gemm_bf3w(const RelGemmArgs& a, bool il, hipStream_t st) {
     const size_t lds = RelGemmBf3W<DGRAD>::lds_bytes();
     const int n_items = a.n_rel + a.n_root;
     int pairs = std::min(n_items, cu_count() / 2);
     pairs = std::max(8, (pairs + 7) / 8 * 8);
-    hipLaunchKernelGGL((rel_gemm_bf3w_kernel<DGRAD>), dim3(2 * pairs), dim3(512), lds, st, a);
+    if (il) hipLaunchKernelGGL((rel_gemm_bf3w_kernel<DGRAD, true>), dim3(2 * pairs), dim3(512), lds, st, a);
+    else hipLaunchKernelGGL((rel_gemm_bf3w_kernel<DGRAD, false>), dim3(2 * pairs), dim3(512), lds, st, a);
 }
 
 
@@ -5182,8 +5243,8 @@ static void launch_rel_gemm(const RelGemmArgs& a, int K, bool dgrad, const Optio
     // epilogue in the same launch (relation items write Y, root items finish the rows without a
     // segment, single_fix_kernel the others)
     if (o.gemm_bf3 && K == 256 && (a.node_map == nullptr || !dgrad)) {
-        if (dgrad) launch_rel_gemm_bf3w<true>(a, st);
-        else launch_rel_gemm_bf3w<false>(a, st);
+        if (dgrad) launch_rel_gemm_bf3w<true>(a, o.gemm_w_il, st);
+        else launch_rel_gemm_bf3w<false>(a, o.gemm_w_il, st);
         return;
     }
     if (K == 256) {  // F_in = F_out = 256 (C5): two 128-column blocks, K = 256
@@ -6101,6 +6162,7 @@ static int32_t set_switch(Options& o, int32_t option, int64_t value) {
         case MPGNN_OPT_OUTER_VEC: o.outer_vec = value != 0; return MPGNN_OK;
         case MPGNN_OPT_OUTER_SQ: o.outer_sq = value != 0; return MPGNN_OK;
         case MPGNN_OPT_OUTER_RANGES: o.outer_ranges = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_GEMM_W_IL: o.gemm_w_il = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_SWITCH_COST:
             if (value < 0 || value > 10000) return arg_error("MPGNN_OPT_GEMM_SWITCH_COST must be 0..10000 (percent of an item)");
             o.gemm_switch_cost = (int)value;
@@ -6125,6 +6187,7 @@ static bool get_switch(const Options& o, int32_t option, int64_t* value) {
         case MPGNN_OPT_OUTER_VEC: *value = o.outer_vec; return true;
         case MPGNN_OPT_OUTER_SQ: *value = o.outer_sq; return true;
         case MPGNN_OPT_OUTER_RANGES: *value = o.outer_ranges; return true;
+        case MPGNN_OPT_GEMM_W_IL: *value = o.gemm_w_il; return true;
         case MPGNN_OPT_GEMM_SWITCH_COST: *value = o.gemm_switch_cost; return true;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = o.flat_wg_per_cu; return true;
         default: return false;

@@ -25,6 +25,7 @@ namespace mpgnn {
 namespace {
 
 constexpr int kScoreThreads = 256;
+constexpr int kMaxConfLists = 4;
 
 int32_t hip_status(hipError_t e, const char* what) {
     if (e == hipSuccess) return MPGNN_OK;
@@ -405,6 +406,63 @@ __global__ __launch_bounds__(kScoreThreads) void score_multi_scatter_kernel(
     if (live && sl == 0) grad_w[pair_target[pi]] = acc;
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Per-epoch scoring of the training loop (main.py:1084-1099 mpgnn_validation, main.py:1101-1115
+// mpgnn_test): for each (row index, label) pair list, the argmax of the class scores of every
+// listed row (torch.argmax(pred[idx], 1): first maximum, NaN wins) and the [3, C] confusion
+// counts the macro F1 is finished from (metrics.py): predictions per class, labels per class,
+// agreeing positions per class. Labels outside [0, C) count in no class. One workgroup per list,
+// LDS histograms, integer adds: exact and order-free — one launch instead of the ~45 small
+// torch ops (index, argmax, compare, where, scatter_add, stack) the counts took per epoch.
+// ---------------------------------------------------------------------------------------
+constexpr int kConfThreads = 1024;
+
+struct ConfArgs {
+    const float* scores;
+    int64_t rows;
+    int32_t C;
+    int32_t n_lists;
+    const int64_t* idx[kMaxConfLists];     // nullptr: rows 0..n-1
+    const int64_t* labels[kMaxConfLists];
+    int64_t n[kMaxConfLists];
+    int64_t* out;                          // [n_lists][3][C]
+};
+
+__global__ __launch_bounds__(kConfThreads) void confusion_counts_kernel(ConfArgs a) {
+    extern __shared__ int conf_lds[];  // [3][C + 1]
+    const int C = a.C, L = (int)blockIdx.x;
+    for (int k = threadIdx.x; k < 3 * (C + 1); k += kConfThreads) conf_lds[k] = 0;
+    __syncthreads();
+    const int64_t* idx = a.idx[L];
+    const int64_t* lab = a.labels[L];
+    const int64_t n = a.n[L];
+    for (int64_t j = threadIdx.x; j < n; j += kConfThreads) {
+        const int64_t row = idx ? idx[j] : j;
+        int pc = C;  // a row outside the score matrix predicts no class
+        if (row >= 0 && row < a.rows) {
+            const float* s = a.scores + row * (int64_t)C;
+            float bv = s[0];
+            pc = 0;
+            for (int c = 1; c < C; ++c) {
+                const float v = s[c];
+                if (takes_over(bv, v)) {
+                    bv = v;
+                    pc = c;
+                }
+            }
+        }
+        const int64_t y = lab[j];
+        const int yc = (y >= 0 && y < C) ? (int)y : C;
+        atomicAdd(&conf_lds[pc], 1);
+        atomicAdd(&conf_lds[(C + 1) + yc], 1);
+        atomicAdd(&conf_lds[2 * (C + 1) + (pc == yc ? yc : C)], 1);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < 3 * C; k += kConfThreads)
+        a.out[(int64_t)L * 3 * C + k] = (int64_t)conf_lds[(k / C) * (C + 1) + k % C];
+}
+
 }  // namespace
 }  // namespace mpgnn
 
@@ -535,4 +593,31 @@ extern "C" int32_t mpgnn_score_argmax_multi_bwd(const float* grad_values, const 
     hipLaunchKernelGGL(score_multi_scatter_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, grad_values, arg_pos,
                        pair_ptr, pair_target, in_pos, in_key, (int32_t)num_pairs, grad_weights);
     return hip_status(hipGetLastError(), "score_multi_scatter_kernel launch");
+}
+
+extern "C" int32_t mpgnn_confusion_counts(const float* scores, int64_t rows, int32_t num_classes, int32_t n_lists,
+                                          const int64_t* const* row_idx, const int64_t* const* labels,
+                                          const int64_t* n, int64_t* counts, void* stream) {
+    if (rows < 0 || num_classes <= 0 || num_classes > 8192 || n_lists < 0 || n_lists > kMaxConfLists)
+        return arg_fail("mpgnn_confusion_counts: bad sizes (1 <= num_classes <= 8192, 0 <= n_lists <= 4)");
+    if (n_lists == 0) return MPGNN_OK;
+    if (!counts || !labels || !n) return arg_fail("mpgnn_confusion_counts: NULL argument");
+    ConfArgs a{};
+    a.scores = scores;
+    a.rows = rows;
+    a.C = num_classes;
+    a.n_lists = n_lists;
+    a.out = counts;
+    for (int l = 0; l < n_lists; ++l) {
+        if (n[l] < 0 || n[l] >= (int64_t)INT32_MAX) return arg_fail("mpgnn_confusion_counts: bad list length");
+        a.idx[l] = row_idx ? row_idx[l] : nullptr;
+        if (n[l] > 0 && (!labels[l] || !scores || (!a.idx[l] && n[l] > rows)))
+            return arg_fail("mpgnn_confusion_counts: NULL labels / scores, or an index-free list longer than rows");
+        a.labels[l] = labels[l];
+        a.n[l] = n[l];
+    }
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    const size_t lds = (size_t)3 * (num_classes + 1) * sizeof(int);
+    hipLaunchKernelGGL(confusion_counts_kernel, dim3(n_lists), dim3(kConfThreads), lds, strm, a);
+    return hip_status(hipGetLastError(), "confusion_counts_kernel launch");
 }

@@ -16,7 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from . import data as _data
-from .metrics import class_weight_balanced, confusion_counts_many, f1_from_counts, f1_macro_many
+from .metrics import class_weight_balanced, confusion_counts_rows, f1_from_counts
 from .model import MPNetm
 # score function helpers of main.py:387-917 (both branches, GPU kernels): same names, plus the
 # batched first-round scoring of every relation (score_relations_batched)
@@ -191,10 +191,6 @@ def _epochs(epoch_fn, epochs: int, use_graph: bool, warmup: int = 3):
         _LOOP_ACTIVE.discard(dev)
 
 
-def _num_classes(out: torch.Tensor) -> int:
-    return int(out.shape[1]) if out.dim() > 1 else 1
-
-
 def take_rows(out: torch.Tensor, idx):
     """``out[idx]`` (main.py:1062, main_rgcn.py:380). For a 1-D integer index tensor (the loaders'
     train_idx: unique rows) this is ``index_select``: the same rows, and its backward is one
@@ -230,9 +226,7 @@ def _val_counts(model, data):
     model.eval()
     pred = model(data.x, data.edge_index, data.edge_type)
     loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
-    c = _num_classes(pred)
-    return loss_val, confusion_counts_many([(torch.argmax(pred[data.train_idx], 1), data.train_y),
-                                            (torch.argmax(pred[data.val_idx], 1), data.val_y)], c)
+    return loss_val, confusion_counts_rows(pred, [(data.train_idx, data.train_y), (data.val_idx, data.val_y)])
 
 
 @torch.no_grad()
@@ -242,9 +236,8 @@ def mpgnn_validation(model, data, class_weight):
     model.eval()
     pred = model(data.x, data.edge_index, data.edge_type)
     loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
-    c = _num_classes(pred)
-    f1_train, f1_val = f1_macro_many([(torch.argmax(pred[data.train_idx], 1), data.train_y),
-                                      (torch.argmax(pred[data.val_idx], 1), data.val_y)], c)
+    f1_train, f1_val = f1_from_counts(confusion_counts_rows(pred, [(data.train_idx, data.train_y),
+                                                                     (data.val_idx, data.val_y)]))
     return f1_train, f1_val, f1_val, loss_val
 
 
@@ -254,7 +247,7 @@ def mpgnn_test(model, data, class_weight):
     model.eval()
     pred = model(data.x, data.edge_index, data.edge_type)
     loss_test = F.nll_loss(pred[data.test_idx].squeeze(-1), data.test_y)
-    (f1_test,) = f1_macro_many([(torch.argmax(pred[data.test_idx], 1), data.test_y)], _num_classes(pred))
+    (f1_test,) = f1_from_counts(confusion_counts_rows(pred, [(data.test_idx, data.test_y)]))
     return loss_test, f1_test
 
 

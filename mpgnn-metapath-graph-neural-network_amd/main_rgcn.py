@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 from .main import (_adam, _adam_graphable, _epochs, _graphs_enabled, _one_hot_colours, Data,  # noqa: F401
                    get_edge_index_and_type_no_reverse, load_files, load_graph, take_rows)
-from .metrics import class_weight_balanced, class_weight_tensor, confusion_counts_many, f1_from_counts, f1_macro_many
+from .metrics import class_weight_balanced, class_weight_tensor, confusion_counts_rows, f1_from_counts
 from .model import Net
 
 __all__ = ["Data", "get_node_features", "mpgnn_train", "mpgnn_validation", "mpgnn_test", "mpgnn_parallel_multiple", "EPOCHS"]
@@ -63,9 +63,7 @@ def _val_counts(model, data):
     model.eval()
     pred = _forward(model, data)
     loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
-    c = int(pred.shape[1])
-    counts = confusion_counts_many([(torch.argmax(pred[data.train_idx], 1), data.train_y),
-                                    (torch.argmax(pred[data.val_idx], 1), data.val_y)], c)
+    counts = confusion_counts_rows(pred, [(data.train_idx, data.train_y), (data.val_idx, data.val_y)])
     return loss_val, counts
 
 
@@ -74,7 +72,7 @@ def _test_counts(model, data):
     model.eval()
     pred = _forward(model, data)
     loss_test = F.nll_loss(pred[data.test_idx].squeeze(-1), data.test_y)
-    counts = confusion_counts_many([(torch.argmax(pred[data.test_idx], 1), data.test_y)], int(pred.shape[1]))
+    counts = confusion_counts_rows(pred, [(data.test_idx, data.test_y)])
     return loss_test, counts
 
 
@@ -84,9 +82,8 @@ def mpgnn_validation(model, data, class_weight):
     model.eval()
     pred = _forward(model, data)
     loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
-    c = int(pred.shape[1])
-    f1_train, f1_val = f1_macro_many([(torch.argmax(pred[data.train_idx], 1), data.train_y),
-                                      (torch.argmax(pred[data.val_idx], 1), data.val_y)], c)
+    f1_train, f1_val = f1_from_counts(confusion_counts_rows(pred, [(data.train_idx, data.train_y),
+                                                                     (data.val_idx, data.val_y)]))
     return f1_train, f1_val, f1_val, loss_val
 
 
@@ -96,7 +93,7 @@ def mpgnn_test(model, data, class_weight):
     model.eval()
     pred = _forward(model, data)
     loss_test = F.nll_loss(pred[data.test_idx].squeeze(-1), data.test_y)
-    (f1_test,) = f1_macro_many([(torch.argmax(pred[data.test_idx], 1), data.test_y)], int(pred.shape[1]))
+    (f1_test,) = f1_from_counts(confusion_counts_rows(pred, [(data.test_idx, data.test_y)]))
     return loss_test, f1_test
 
 

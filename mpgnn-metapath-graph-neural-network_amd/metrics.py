@@ -16,8 +16,8 @@ import weakref
 import numpy as np
 import torch
 
-__all__ = ["f1_macro", "f1_macro_many", "confusion_counts_many", "f1_from_counts", "class_weight_balanced",
-           "class_weight_tensor"]
+__all__ = ["f1_macro", "f1_macro_many", "confusion_counts_many", "confusion_counts_rows", "f1_from_counts",
+           "class_weight_balanced", "class_weight_tensor"]
 
 
 def _count(v: torch.Tensor, bins: int) -> torch.Tensor:
@@ -62,6 +62,41 @@ def confusion_counts_many(pairs: list[tuple[torch.Tensor, torch.Tensor]], num_cl
     """[len(pairs), 3, C] int64 confusion counts, left on the device (no host sync); finish
     with ``f1_from_counts``."""
     return torch.stack([_confusion_counts(p, y, num_classes) for p, y in pairs])
+
+
+def confusion_counts_rows(scores: torch.Tensor, lists) -> torch.Tensor:
+    """``confusion_counts_many([(torch.argmax(scores[idx], 1), y) for idx, y in lists], C)`` with
+    C = scores.shape[1]: [len(lists), 3, C] int64 on the device. On the GPU (float32 scores,
+    1-D integer row indices, up to 4 lists) ONE kernel (``mpgnn_confusion_counts``: argmax of
+    each listed row + LDS histograms) instead of ~20 torch ops per list; same counts."""
+    lists = list(lists)
+    ok = (scores.is_cuda and scores.dim() == 2 and scores.dtype == torch.float32 and 0 < len(lists) <= 4
+          and 1 <= scores.shape[1] <= 8192
+          and all(torch.is_tensor(i) and i.dim() == 1 and i.dtype in (torch.int64, torch.int32) and
+                  torch.is_tensor(y) and y.numel() == i.numel() and not y.is_floating_point()
+                  for i, y in lists))
+    if not ok:
+        return confusion_counts_many([(torch.argmax(scores[i], 1), y) for i, y in lists], _num_cols(scores))
+    import ctypes
+    from . import _lib
+    from .functional import _stream
+    dev = scores.device
+    sc = scores.contiguous()
+    c = sc.shape[1]
+    idx = [i.to(device=dev, dtype=torch.int64).contiguous() for i, _ in lists]
+    lab = [y.to(device=dev, dtype=torch.int64).reshape(-1).contiguous() for _, y in lists]
+    n = len(lists)
+    out = torch.empty(n, 3, c, dtype=torch.int64, device=dev)
+    p_idx = (ctypes.c_void_p * n)(*[t.data_ptr() for t in idx])
+    p_lab = (ctypes.c_void_p * n)(*[t.data_ptr() for t in lab])
+    p_n = (ctypes.c_int64 * n)(*[t.numel() for t in idx])
+    _lib.check(_lib.lib.mpgnn_confusion_counts(sc.data_ptr(), sc.shape[0], c, n, p_idx, p_lab, p_n, out.data_ptr(),
+                                               _stream(sc)), "mpgnn_confusion_counts")
+    return out
+
+
+def _num_cols(t: torch.Tensor) -> int:
+    return int(t.shape[1]) if t.dim() > 1 else 1
 
 
 def f1_from_counts(counts) -> list[float]:

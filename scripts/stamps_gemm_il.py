@@ -1,4 +1,5 @@
-"""Phase stamps of the interleaved bf16-split forward GEMM (RelGemmBf3::run_il) on the C3 layer —
+"""Phase stamps of the bf16-split forward GEMMs (RelGemmBf3::run_il at F = 128, rel_gemm_bf3w_kernel
+at F = 256: --workload C5) on one layer —
 debug build only (make -C csrc stamps -> libmpgnn_rgcn_stamps.so, loaded via MPGNN_LIB_PATH).
 Per wave and item: 0 item start | 1 k-loop done | 2 weight switch (stamped only then) | 3 epilogue
 done | 4 barrier passed. Prints phase percentiles, the per-wave span against items and weight
@@ -15,16 +16,34 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import mpgnn_amd  # noqa: E402
 from mpgnn_amd import _lib, data  # noqa: E402
+import argparse  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="fb15k237")
+ap.add_argument("--single", type=int, default=None, help="mode SINGLE over this relation")
+cli = ap.parse_args()
 
 ITEMS, PH = 32, 8
-g = data.fb15k237_graph(feat_dim=128)
+g = data.fb15k237_graph(feat_dim=128) if cli.workload == "fb15k237" else data.config_graph(cli.workload)
 dev = torch.device("cuda", 0)
 torch.manual_seed(10)
-conv = mpgnn_amd.RGCNConv(128, 128, g.num_relations, flow="target_to_source").to(dev)
+F = g.x.shape[1]
+if cli.single is None:
+    conv = mpgnn_amd.RGCNConv(F, F, g.num_relations, flow="target_to_source").to(dev)
+else:
+    conv = mpgnn_amd.CustomRGCNConv(F, F, g.num_relations, flow="target_to_source").to(dev)
 x, ei, et = g.x.to(dev), g.edge_index.to(dev), g.edge_type.to(dev)
+
+
+def fwd():
+    if cli.single is None:
+        return conv(x, ei, et)
+    return conv(0, cli.single, x, ei, et)
+
+
 with torch.no_grad():
     for _ in range(3):
-        conv(x, ei, et)
+        fwd()
 torch.cuda.synchronize()
 nwaves = 256 * 4 * 4
 buf = torch.zeros(nwaves * (ITEMS + 1) * PH, dtype=torch.int64, device=dev)
@@ -32,7 +51,7 @@ fn = _lib.lib.mpgnn_debug_stamps_set
 fn.argtypes = [ctypes.c_void_p]
 assert fn(buf.data_ptr()) == 0
 with torch.no_grad():
-    conv(x, ei, et)
+    fwd()
 torch.cuda.synchronize()
 assert fn(None) == 0
 st = buf.view(nwaves, ITEMS + 1, PH).cpu().numpy()

@@ -28,7 +28,7 @@ def pytest_sessionfinish(session, exitstatus):
     _parity_report.dump()
 
 
-_OPTIONS = (0, 3, 5, 11, 19, 20, 24, 25, 27, 28, 29, 30, 31, 32, 33)  # enum mpgnn_option switches a test may override
+_OPTIONS = (0, 3, 5, 11, 19, 20, 24, 25, 27, 28, 29, 30, 31, 32, 33, 34)  # enum mpgnn_option switches a test may override
 _DEFAULTS: dict = {}
 
 

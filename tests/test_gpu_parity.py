@@ -792,6 +792,47 @@ def test_gemm_item_ranges_do_not_change_results():
             assert torch.equal(a, b), (cost, k)
 
 
+@pytest.mark.parametrize("mode", ["all", "single"])
+def test_k256_gemm_interleaved_commit_bit_identical(mode):
+    """MPGNN_OPT_GEMM_W_IL (34): the K = 256 bf16-split GEMM (F_in = F_out = 256, C5's width) with
+    the next item's tile committed in four parts among the k-steps' MFMAs computes the same
+    products in the same order as the one-k-step commit — forward and dgrad (mode ALL) and the
+    mode-SINGLE forward with its root epilogue, bit-identical; a ragged last node tile (N % 32)
+    and partial relation tiles included."""
+    g = data.synthetic_graph(6007, 7, 10, feat_dim=256, seed=21)
+    N, R = g.num_nodes, g.num_relations
+    gen = torch.Generator().manual_seed(9)
+    single = mode == "single"
+    W = (torch.rand((256, 256) if single else (R, 256, 256), generator=gen) - 0.5) * 0.1
+    root = (torch.rand(256, 256, generator=gen) - 0.5) * 0.1
+    bias = torch.rand(256, generator=gen) - 0.5
+    gout = torch.randn(N, 256, generator=gen)
+    plan = mpgnn_amd.GraphPlan(g.edge_index.to(DEV), g.edge_type.to(DEV), N)
+    res = {}
+    for il in (0, 1, 0):
+        plan.set_option(34, il)
+        xg = g.x.to(DEV).requires_grad_(not single)
+        Wg, rg, bg = (t.to(DEV).requires_grad_(not single) for t in (W, root, bias))
+        if single:
+            with torch.no_grad():
+                out = rgcn_conv(xg, Wg, rg, bg, plan, MODE_SINGLE, relation=3, activation="relu")
+            res[il] = [out]
+        else:
+            out = rgcn_conv(xg, Wg, rg, bg, plan, MODE_ALL, num_relations=R)
+            out.backward(gout.to(DEV))
+            res[il] = [out.detach(), xg.grad, Wg.grad, rg.grad, bg.grad]
+        torch.cuda.synchronize()
+    plan.set_option(34, _lib_default(34))
+    for k, a, b in zip(("out", "dx", "dW", "droot", "dbias"), res[1], res[0]):
+        assert torch.equal(a, b), k
+    assert res[0][0].abs().sum() > 0
+
+
+def _lib_default(opt):
+    from mpgnn_amd import _lib
+    return _lib.get_option(opt)
+
+
 # ------------------------------------------------------------------------------------------
 # CustomFastRGCNConv (A7): transform-then-aggregate semantics on the same kernels
 # ------------------------------------------------------------------------------------------

@@ -153,6 +153,53 @@ def test_f1_macro_identical_to_sklearn(seed):
     assert many == [ref, f1_score(y.tolist(), pred.tolist(), average="macro")]
 
 
+def _rows_case(seed, c, n_rows):
+    """Log-probability-like scores with ties and NaN rows, label lists with out-of-range labels
+    and repeated rows."""
+    g = torch.Generator().manual_seed(seed)
+    s = torch.randn(n_rows, c, generator=g)
+    s[::7] = s[::7].round()  # ties: the first maximum wins
+    s[5::11, c // 2] = float("nan")  # a NaN wins (torch.argmax)
+    if c > 1:
+        s[3::13] = 0.0  # a whole row tied
+    lists = []
+    for k, n in enumerate((n_rows // 2, 1, 0, n_rows + 5)):
+        idx = torch.randint(0, n_rows, (n,), generator=g)
+        y = torch.randint(-1, c + 1, (n,), generator=g)  # -1 and c count in no class
+        lists.append((idx.to(torch.int32) if k == 1 else idx, y))
+    return s, lists
+
+
+@pytest.mark.parametrize("seed,c", [(0, 2), (1, 3), (2, 1), (3, 40)])
+def test_confusion_counts_rows_cpu_equals_argmax_counts(seed, c):
+    s, lists = _rows_case(seed, c, 300)
+    got = metrics.confusion_counts_rows(s, lists)
+    ref = metrics.confusion_counts_many([(torch.argmax(s[i.long()], 1), y) for i, y in lists], c)
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,c", [(0, 2), (1, 3), (2, 1), (3, 40), (4, 700)])
+def test_confusion_counts_rows_kernel_equals_torch(seed, c):
+    """mpgnn_confusion_counts (one launch) = torch.argmax over the listed rows + the per-class
+    counts of metrics.confusion_counts_many, integer-exact; and the macro F1 from them equals
+    scikit-learn's on the same predictions (main.py:1094-1098)."""
+    s, lists = _rows_case(seed, c, 3000)
+    dev = torch.device("cuda", 0)
+    sd = s.to(dev)
+    ld = [(i.to(dev), y.to(dev)) for i, y in lists]
+    got = metrics.confusion_counts_rows(sd, ld)
+    ref = metrics.confusion_counts_many([(torch.argmax(sd[i.long()], 1), y) for i, y in ld], c)
+    assert got.is_cuda and torch.equal(got, ref)
+    pred = torch.argmax(s[lists[0][0]], 1)
+    y = lists[0][1]
+    keep = (y >= 0) & (y < c)
+    if keep.any():
+        assert metrics.f1_from_counts(metrics.confusion_counts_rows(sd, [(ld[0][0][keep.to(dev)],
+                                                                          ld[0][1][keep.to(dev)])]))[0] == \
+            f1_score(pred[keep].tolist(), y[keep].tolist(), average="macro")
+
+
 def test_class_weight_balanced_identical_to_sklearn():
     for seed in range(4):
         y = torch.from_numpy(np.random.default_rng(seed).integers(0, 3 + seed, 97))
