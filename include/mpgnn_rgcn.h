@@ -409,9 +409,11 @@ enum mpgnn_option {
                                     strips; slabs bit-identical */,
     MPGNN_OPT_OUTER_RANGES = 33  /* 1 (default): that kernel's workgroups take contiguous chunk ranges balanced by
                                     16-row slices (per CU); 0: every G-th chunk; slabs bit-identical */,
-    MPGNN_OPT_GEMM_W_IL = 34     /* the K = 256 bf16-split GEMM (F_in = F_out = 256, C5): 1 commits the next item's
-                                    tile in four parts among the k-steps' MFMAs (as GEMM_IL at K = 128); 0
-                                    (default): the whole tile in one k-step; outputs bit-identical */
+    MPGNN_OPT_GEMM_W_IL = 34     /* the K = 256 bf16-split GEMM (F_in = F_out = 256, C5): 1 (default) commits the
+                                    next item's tile in four parts among the k-steps' MFMAs (as GEMM_IL at
+                                    K = 128; round-5 A/B at C5: forward 26.2 -> 23.9 ms, dgrad 25.6 -> 23.2 ms,
+                                    mode SINGLE 2.31 -> 1.87 ms per layer); 0: the whole tile in one k-step;
+                                    outputs bit-identical */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

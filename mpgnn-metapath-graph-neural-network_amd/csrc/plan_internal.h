@@ -27,7 +27,7 @@ struct Options {
     bool flat_fuse_split = true;  // MPGNN_OPT_FLAT_FUSE_SPLIT: hub rows of grad_x finished in the gather launch
     bool outer_vec = true;        // MPGNN_OPT_OUTER_VEC: outer_bf3v_kernel (16-B gathers, transposed LDS reads)
     bool outer_sq = false;        // MPGNN_OPT_OUTER_SQ: its 64 x 64 wave quarters + interleaved commit (measured slower)
-    bool gemm_w_il = false;       // MPGNN_OPT_GEMM_W_IL: the K = 256 GEMM's interleaved commit
+    bool gemm_w_il = true;        // MPGNN_OPT_GEMM_W_IL: the K = 256 GEMM's interleaved commit
     bool outer_ranges = true;     // MPGNN_OPT_OUTER_RANGES: its chunks in balanced contiguous ranges per workgroup
     bool gemm_il = true;          // MPGNN_OPT_GEMM_IL: the interleaved GEMM item skeleton
     bool gemm_cu_pairs = true;    // MPGNN_OPT_GEMM_CU_PAIRS: GEMM item ranges balanced per CU

@@ -2217,6 +2217,8 @@ __global__ __launch_bounds__(kSingleThreads, 1) void single_bf3_kernel(SingleBf3
 // Items, row gathers and outputs as rel_gemm_kernel (RelGemmArgs: relation tiles of segments,
 // then node rows; forward A = x row / compact mean row, dgrad A = dout[node_1] scaled by 1/cnt).
 // ----------------------------------------------------------------------------------------
+__device__ int g_one_i32 = 1;  // RelGemmBf3W::row_val_load's stand-in (never written)
+
 template <bool DGRAD>
 struct RelGemmBf3W {
     static constexpr int K = 256, N = 256, KH = 128, NS = KH / 16, LDAB = KH + 8, PLANE = 32 * LDAB;
@@ -2258,19 +2260,12 @@ struct RelGemmBf3W {
         it.w = it.root ? a.Wroot : a.W + (size_t)wr * K * N;
         return it;
     }
-    // source row of each of the thread's WPT tile rows (row t/32 + 8j of the item) and the row's
-    // count (dgrad scale; 1 otherwise)
-    __device__ static __forceinline__ void gather_idx(const RelGemmArgs& a, const Item& it, int t, int (&row)[WPT],
-                                                      int& cnt) {
+    // source row of each of the thread's WPT tile rows (row t/32 + 8j of the item)
+    __device__ static __forceinline__ void gather_idx(const RelGemmArgs& a, const Item& it, int t, int (&row)[WPT]) {
 #pragma unroll
         for (int j = 0; j < WPT; ++j) row[j] = it.r0 + min(t / 32 + 8 * j, it.nrows - 1);
-        cnt = 1;
-        if constexpr (!DGRAD) {  // mode-SINGLE root epilogue: does row t & 31 have a segment?
-            if (it.root && a.node_map != nullptr) cnt = a.node_map[it.r0 + min(t & 31, it.nrows - 1)] != 0 ? 1 : 0;
-        }
         if (!it.root) {
             if constexpr (DGRAD) {
-                cnt = a.s_cnt[it.r0 + min(t & 31, it.nrows - 1)];
 #pragma unroll
                 for (int j = 0; j < WPT; ++j) row[j] = a.s_row[row[j]];
             } else {
@@ -2293,8 +2288,25 @@ struct RelGemmBf3W {
             v[j] = *reinterpret_cast<const float4*>(base + c4);
         }
     }
-    __device__ static __forceinline__ void commit(const Item& it, int kh, int t, const float4 (&v)[WPT], int cnt,
-                                                  __bf16* planes, float* sc) {
+    // the epilogue's per-row value of tile row t (< 32): dgrad 1 / count of a relation row;
+    // forward with the mode-SINGLE root epilogue: 1 when the node has a segment of the relation,
+    // 0 when its root row is final; 1 otherwise. Issued when the item starts, read before the
+    // item's barrier (a chain later), so the load's latency is off the critical path
+    // (always a load — of g_one_i32 when the item has no such value — so no branch or select
+    // after it makes the compiler wait for the load where it is issued)
+    __device__ static __forceinline__ int row_val_load(const RelGemmArgs& a, const Item& it, int t) {
+        const int r = it.r0 + min(t, it.nrows - 1);
+        const int* p;
+        if constexpr (DGRAD) p = it.root ? &g_one_i32 : a.s_cnt + r;
+        else p = (it.root && a.node_map != nullptr) ? a.node_map + r : &g_one_i32;
+        return *p;
+    }
+    __device__ static __forceinline__ float row_val(int v) {
+        if constexpr (DGRAD) return 1.0f / (float)v;
+        else return v != 0 ? 1.0f : 0.0f;
+    }
+    __device__ static __forceinline__ void commit(const Item& it, int kh, int t, const float4 (&v)[WPT],
+                                                  __bf16* planes) {
         __bf16* P = planes + kh * 3 * PLANE;
 #pragma unroll
         for (int j = 0; j < WPT; ++j) {
@@ -2311,7 +2323,6 @@ struct RelGemmBf3W {
             *reinterpret_cast<bf16x4*>(d + PLANE) = bf16x4{p1[0], p1[1], p1[2], p1[3]};
             *reinterpret_cast<bf16x4*>(d + 2 * PLANE) = bf16x4{p2[0], p2[1], p2[2], p2[3]};
         }
-        if (kh == 0 && t < 32) sc[t] = DGRAD ? 1.0f / (float)cnt : (float)cnt;  // forward: root-epilogue flag
     }
     // IL: one float4 part of the commit (rows past nrows: zeros) / of the row issue
     __device__ static __forceinline__ void commit_part(int j, int kh, int t, int nrows, const float4& v, __bf16* planes) {
@@ -2383,7 +2394,7 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
     extern __shared__ __bf16 smem_bf[];
     __bf16* As = smem_bf;                                                   // [2][2 halves][3][PLANE]
     float* Ot = reinterpret_cast<float*>(smem_bf + 12 * G::PLANE);         // [2][32][LDO]
-    float* Sc = Ot + 2 * 32 * G::LDO;                                      // [3][32]
+    float* Sc = Ot + 2 * 32 * G::LDO;                                      // [2][32]
     const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int kh = wave >> 2;   // K half of the wave (uniform)
@@ -2413,23 +2424,22 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
     };
     // prologue: item i_beg committed, rows of i_beg+1 in flight, sources of i_beg+2 loaded
     typename G::Item cur = get_item(i_beg);
-    int row[G::WPT], cnt0 = 1;
+    int row[G::WPT];
     float4 v[G::WPT];
-    G::gather_idx(a, cur, t, row, cnt0);
+    G::gather_idx(a, cur, t, row);
     G::issue(a, kh, t, row, v);
     bf16x8 b[G::NS][3];
     G::load_b(cur.w, kh, col, h, b);
-    G::commit(cur, kh, t, v, cnt0, As, Sc + (i_beg % 3) * 32);
+    G::commit(cur, kh, t, v, As);
     typename G::Item nxt = cur, nn = cur;
-    int cnt1 = 1, cnt2 = 1;
     if (i_beg + 1 < i_end) {
         nxt = get_item(i_beg + 1);
-        G::gather_idx(a, nxt, t, row, cnt1);
+        G::gather_idx(a, nxt, t, row);
         G::issue(a, kh, t, row, v);
     }
     if (i_beg + 2 < i_end) {
         nn = get_item(i_beg + 2);
-        G::gather_idx(a, nn, t, row, cnt2);
+        G::gather_idx(a, nn, t, row);
     }
     __syncthreads();
 
@@ -2446,6 +2456,8 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
     for (int i = i_beg; i < i_end; ++i) {
         stamp(i - i_beg, 0);
         const bool has_next = i + 1 < i_end;
+        const bool val_lane = kh == 0 && t < 32;
+        const int rv = G::row_val_load(a, cur, t & 31);  // row t & 31's epilogue value, to Sc before the barrier
         const __bf16* Ab = As + (buf * 2 + kh) * 3 * G::PLANE + c * G::LDAB + 8 * h;
         // the small products in their own accumulator (as rel_gemm_bf3_kernel): the a0·b0 chain
         // rounds once per k-step at the sum's magnitude instead of six times (round 5: C5's
@@ -2479,7 +2491,7 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
                     store_prev(2 * s + 1);
                 }
                 if (s == (3 * G::NS) / 4 - 1 && has_next) {
-                    G::commit(nxt, kh, t, v, cnt1, As + (buf ^ 1) * 6 * G::PLANE, Sc + ((i + 1) % 3) * 32);
+                    G::commit(nxt, kh, t, v, As + (buf ^ 1) * 6 * G::PLANE);
                     if (i + 2 < i_end) G::issue(a, kh, t, row, v);  // item i+2's rows, in flight for a chain
                 }
             } else {
@@ -2489,9 +2501,6 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
                     const int j = s >> 1;
                     G::commit_part(j, kh, t, has_next ? nxt.nrows : 0, v[j], As + (buf ^ 1) * 6 * G::PLANE);
                     G::issue_part(a, j, kh, t, row[j], v[j]);
-                }
-                if (s == 1) {
-                    if (kh == 0 && t < 32) Sc[((i + 1) % 3) * 32 + t] = DGRAD ? 1.0f / (float)cnt1 : (float)cnt1;
                 }
                 __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // next fragments
 #pragma unroll
@@ -2522,38 +2531,41 @@ __global__ __launch_bounds__(512, 1) void rel_gemm_bf3w_kernel(RelGemmArgs a) {
                 tab_b = G::load_tab(a, wb + 64, i_end, lane);
             }
             typename G::Item it3 = get_item(i + 3);
-            int c3;
-            G::gather_idx(a, it3, t, row, c3);
+            G::gather_idx(a, it3, t, row);
             nxt = nn;
-            cnt1 = cnt2;
             nn = it3;
-            cnt2 = c3;
         } else {
             nxt = nn;
-            cnt1 = cnt2;
         }
+        if (val_lane) Sc[(i & 1) * 32 + t] = G::row_val(rv);
         stamp(i - i_beg, 3);
         __syncthreads();  // upper partial tile of item i in LDS; item i+1's tiles committed
         stamp(i - i_beg, 4);
         if (kh == 0) {
-            const float* sc = Sc + (i % 3) * 32;
+            // straight-line epilogue: the tile, then the uniform per-item case on all 16 values
+            // (a per-row branch made the compiler wait on each LDS read in turn)
+            const float* sc = Sc + (i & 1) * 32;
+            float o[16];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-                float o = acc[r] + Oe[rr * G::LDO + wq * 32 + c];
-                if constexpr (DGRAD) {
-                    if (!cur.root) o = o * sc[rr];
-                } else {
-                    // mode-SINGLE root epilogue (RelGemmArgs::node_map): a row without a segment
-                    // of the relation is final, act((0 + x_i @ root) + bias); single_fix_kernel
-                    // finishes the others from x_i @ root
-                    if (root_epi && cur.root && sc[rr] == 0.0f) {
-                        o = (0.0f + o) + bias_c;
-                        if (a.relu) o = relu_f(o);
-                    }
+            for (int r = 0; r < 16; ++r) o[r] = acc[r] + Oe[((r & 3) + 8 * (r >> 2) + 4 * h) * G::LDO + wq * 32 + c];
+            if constexpr (DGRAD) {
+                if (!cur.root) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[r] = o[r] * sc[(r & 3) + 8 * (r >> 2) + 4 * h];
                 }
-                prev[r] = o;
+            } else if (root_epi && cur.root) {
+                // mode-SINGLE root epilogue (RelGemmArgs::node_map): a row without a segment of
+                // the relation is final, act((0 + x_i @ root) + bias); single_fix_kernel finishes
+                // the others from x_i @ root
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float f = (0.0f + o[r]) + bias_c;
+                    f = a.relu ? relu_f(f) : f;
+                    o[r] = sc[(r & 3) + 8 * (r >> 2) + 4 * h] == 0.0f ? f : o[r];
+                }
             }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) prev[r] = o[r];
             float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * G::N : a.Y + (size_t)(cur.r0 - a.sel_b) * G::N;
             const int bytes = __builtin_amdgcn_readfirstlane(cur.nrows) * G::N * 4;
             prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(Yt, (short)0, bytes, 0x00020000);

@@ -95,11 +95,11 @@ def test_round4_switches_default_on_and_round_trip():
     — and each round-trips through set / get."""
     from mpgnn_amd import _lib
     lib = _lib.lib
-    shipped = {26: 0, 27: 1, 28: 1, 29: 250, 30: 1, 31: 1, 32: 0, 33: 1, 34: 0}
+    shipped = {26: 0, 27: 1, 28: 1, 29: 250, 30: 1, 31: 1, 32: 0, 33: 1, 34: 1}
     for opt, v in shipped.items():
         assert _lib.get_option(opt) == v, (opt, _lib.get_option(opt))
     try:
-        for opt, v in ((26, 2), (27, 0), (28, 0), (29, 0), (30, 0), (31, 0), (32, 1), (33, 0), (34, 1)):
+        for opt, v in ((26, 2), (27, 0), (28, 0), (29, 0), (30, 0), (31, 0), (32, 1), (33, 0), (34, 0)):
             assert lib.mpgnn_set_option(opt, v) == 0 and _lib.get_option(opt) == v
         assert lib.mpgnn_set_option(26, 65) == _lib.MPGNN_ERR_ARG  # 0..64 workgroups per CU
     finally:
