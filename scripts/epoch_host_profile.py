@@ -20,6 +20,7 @@ ap.add_argument("--workload", default="fb15k237")
 ap.add_argument("--mode", default="single", choices=["single", "all"])
 ap.add_argument("--epochs", type=int, default=20)
 ap.add_argument("--top", type=int, default=40)
+ap.add_argument("--ab-adam", action="store_true", help="alternate torch's fused Adam and main.LeanAdam, 3 rounds")
 a = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -57,6 +58,24 @@ def epoch():
         fwd()
 
 
+if a.ab_adam:
+    params = list(model.parameters())
+    opts = {"torch": torch.optim.Adam(params, lr=0.01, weight_decay=0.0005, fused=True),
+            "lean": mpgnn_amd.main.LeanAdam(params, lr=0.01, weight_decay=0.0005, fused=True)}
+    rec = {k: [] for k in opts}
+    for _ in range(3):
+        for k, o in opts.items():
+            opt = o
+            for _ in range(5):
+                epoch()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.epochs):
+                epoch()
+            torch.cuda.synchronize()
+            rec[k].append(round((time.perf_counter() - t0) * 1e3 / a.epochs, 4))
+    print(json.dumps({"workload": a.workload, "mode": a.mode, "epoch_wall_ms": rec}), flush=True)
+    sys.exit(0)
 for _ in range(5):
     epoch()
 torch.cuda.synchronize()

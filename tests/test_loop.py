@@ -442,3 +442,47 @@ def test_interleaved_loops_keep_the_outer_graph_valid():
         pass
     losses += [float(v) for _, v in gen_a]
     assert losses == losses_ref, (losses, losses_ref)
+
+
+def _lean_case(device, capturable=False):
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(16, 8), torch.nn.ReLU(), torch.nn.Linear(8, 3)).to(device)
+    return m
+
+
+@pytest.mark.parametrize("capturable", [False, pytest.param(True, marks=pytest.mark.gpu)])
+def test_lean_adam_bit_identical_to_torch_fused_adam(capturable):
+    """main.LeanAdam (the loops' optimizer: torch's fused Adam calls issued directly once the
+    state exists) = torch.optim.Adam(fused=True) bit for bit — parameters and state — over
+    several steps, through a missing-gradient step (torch's own path), zero_grad(set_to_none=
+    False), a state_dict reload, and with a step pre-hook that must run once per step."""
+    if capturable and not torch.cuda.is_available():
+        pytest.skip("capturable fused Adam needs the GPU")
+    dev = torch.device("cuda", 0) if capturable else torch.device("cpu")
+    a, b = _lean_case(dev), _lean_case(dev)
+    kw = dict(lr=0.01, weight_decay=5e-4, fused=True, capturable=capturable)
+    oa = torch.optim.Adam(a.parameters(), **kw)
+    ob = main.LeanAdam(b.parameters(), **kw)
+    calls = []
+    ob.register_step_pre_hook(lambda o, ar, k: calls.append(1))
+    x = torch.randn(32, 16, generator=torch.Generator().manual_seed(1)).to(dev)
+    for it in range(7):
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad(set_to_none=(it != 3))
+            m(x).square().mean().backward()
+            if it == 4:
+                m[0].bias.grad = None  # a parameter without a gradient this step
+            o.step()
+        if it == 5:  # reload (a copy: load_state_dict keeps same-device tensors as they are)
+            import copy
+            ob.load_state_dict(copy.deepcopy(oa.state_dict()))
+    assert len(calls) == 7
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.equal(p, q)
+        for k in ("exp_avg", "exp_avg_sq", "step"):
+            assert torch.equal(oa.state[p][k], ob.state[q][k]), k
+
+
+def test_loops_use_lean_adam_on_gpu_params_only():
+    net = torch.nn.Linear(4, 2)
+    assert type(main._adam(net)) is torch.optim.Adam  # CPU parameters: torch's (unfused) Adam
