@@ -4270,6 +4270,9 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel_t(OuterArgs ra,
             issue(c2, ja, jb, vna, vnb);
             if (valid(c3)) load_idx(c3, ja, jb);
         }
+#ifdef MPGNN_STAMPS
+        stamp_at(ra.stamps, nsl, 6);
+#endif
         const bool is_root = cur.chunk < ra_n;
         const __bf16* cb = planes + buf * 6 * kOvPlane;
         if constexpr (!SQ) {

@@ -1,7 +1,7 @@
 """Phase stamps of the bf16-split weight gradient (outer_bf3v_kernel) in the C3 layer backward —
 debug build only (make -C csrc stamps -> libmpgnn_rgcn_stamps.so, loaded via MPGNN_LIB_PATH).
 Per wave and 16-row slice (the first 32 slices of each workgroup): 0 slice start | 1 MFMAs
-issued | 2 next slice committed | 3 chunk-end epilogue done | 5 chunk end (stamped only then) |
+issued | 6 the rows two slices ahead issued | 2 next slice committed | 3 chunk-end epilogue done | 5 chunk end (stamped only then) |
 4 barrier passed; row 0: ids, start, realtime start / end. Cycles of s_memtime."""
 import ctypes
 import json
@@ -45,6 +45,9 @@ valid = (t[:, :, 0] != 0) & (t[:, :, 4] != 0)
 pct = lambda d: {p: int(np.percentile(d, p)) for p in (10, 50, 90, 99)} if np.size(d) else None  # noqa: E731
 res = {"waves": int(used.sum())}
 res["mfma_issue"] = pct((t[:, :, 1] - t[:, :, 0])[valid])
+v6 = valid & (t[:, :, 6] != 0)
+res["rows_issue"] = pct((t[:, :, 6] - t[:, :, 0])[v6])  # slice start -> next rows issued (index wait)
+res["mfma_only"] = pct((t[:, :, 1] - t[:, :, 6])[v6])
 res["commit"] = pct((t[:, :, 2] - t[:, :, 1])[valid])
 ce = valid & (t[:, :, 5] != 0)
 res["chunk_end_frac"] = float(ce.sum() / valid.sum())
