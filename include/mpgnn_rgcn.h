@@ -213,6 +213,18 @@ int32_t mpgnn_confusion_counts(const float* scores, int64_t rows, int32_t num_cl
                                const int64_t* const* row_idx, const int64_t* const* labels, const int64_t* n,
                                int64_t* counts, void* stream);
 
+/* Forward and input gradient of the wrappers' Linear heads (Net.lin model.py:147; MPNetm.fc1 /
+ * fc2 model.py:224-226), replacing F.linear / grad_out @ weight (host-cheap single launches on the
+ * eager epoch's path): out = act(x @ weightᵀ + bias) with x [N,F], weight [O,F], bias [O]
+ * (nullable), act MPGNN_ACT_NONE / _RELU; grad_x = grad_out @ weight ([N,O] @ [O,F]).
+ * Supported: F = O = 128 (bf16-split matrix-core GEMM, fp32-level accuracy) and O <= 8 (F <= 256
+ * for the forward, F % 4 == 0); other shapes return MPGNN_ERR_UNSUPPORTED (the caller keeps the
+ * library GEMM). Pointers 16-byte aligned. */
+int32_t mpgnn_linear_fwd(const float* x, int64_t N, int32_t F, const float* weight, int32_t O, const float* bias,
+                         int32_t act, float* out, void* stream);
+int32_t mpgnn_linear_dgrad(const float* grad_out, int64_t N, int32_t O, const float* weight, int32_t F, float* grad_x,
+                           void* stream);
+
 /* Bytes of scratch the fwd/bwd calls need (caller allocates, e.g. torch.empty(uint8)). */
 int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* plan, int32_t mode, int64_t relation,
                                    int32_t num_relations, int32_t F_in, int32_t F_out,

@@ -90,6 +90,8 @@ SIGNATURES = [
     ("mpgnn_relu_bwd", _I32, [_P, _P, _I64, _P, _P]),
     ("mpgnn_linear_wgrad_workspace_bytes", _I32, [_I64, _I32, _I32, _PI64]),
     ("mpgnn_linear_wgrad", _I32, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P]),
+    ("mpgnn_linear_fwd", _I32, [_P, _I64, _I32, _P, _I32, _P, _I32, _P, _P]),
+    ("mpgnn_linear_dgrad", _I32, [_P, _I64, _I32, _P, _I32, _P, _P]),
     ("mpgnn_score_argmax", _I32, [_P, _I64, _P, _P, _P, _I64, _P, _P, _P, _P]),
     ("mpgnn_score_argmax_bwd", _I32, [_P, _I64, _P, _P, _P, _P, _P, _P, _P]),
     ("mpgnn_score_argmax_multi", _I32, [_P, _I64, _P, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -4832,6 +4832,79 @@ __global__ __launch_bounds__(kThreads) void relu_bwd_kernel(const float* g, cons
     for (int64_t k = i; k < n; k += stride) d[k] = relu_bwd_f(g[k], y[k]);
 }
 
+// The wrappers' Linear heads with few outputs (model.py:147 Net.lin, :226 MPNetm.fc2):
+// out[i][o] = act(Σ_f x[i][f]·W[o][f] + b[o]) for O <= 8, F <= 256 (F % 4 == 0). One wave per row:
+// lane l holds columns 4l..4l+3, the O partial dots are added by a fixed butterfly (deterministic).
+constexpr int kLinSmallO = 8;
+__global__ __launch_bounds__(kThreads) void linear_small_fwd_kernel(const float* __restrict__ x, int N, int F,
+                                                                    const float* __restrict__ W, int O,
+                                                                    const float* __restrict__ bias, int act,
+                                                                    float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int waves = (int)gridDim.x * (kThreads / 64);
+    const int f = 4 * lane;
+    float4 w[kLinSmallO];
+#pragma unroll
+    for (int o = 0; o < kLinSmallO; ++o)
+        w[o] = (o < O && f < F) ? *reinterpret_cast<const float4*>(W + (size_t)o * F + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = (int)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); i < N; i += waves) {
+        const float4 xv = f < F ? *reinterpret_cast<const float4*>(x + (size_t)i * F + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+        float acc[kLinSmallO];
+#pragma unroll
+        for (int o = 0; o < kLinSmallO; ++o) {
+            float t = xv.x * w[o].x;
+            t = fmaf(xv.y, w[o].y, t);
+            t = fmaf(xv.z, w[o].z, t);
+            t = fmaf(xv.w, w[o].w, t);
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m);
+            acc[o] = t;
+        }
+        if (lane < O) {
+            float v = 0.0f;
+#pragma unroll
+            for (int o = 0; o < kLinSmallO; ++o) v = lane == o ? acc[o] : v;
+            v = v + (bias != nullptr ? bias[lane] : 0.0f);
+            out[(size_t)i * O + lane] = act == MPGNN_ACT_RELU ? relu_f(v) : v;
+        }
+    }
+}
+
+// grad of a Linear head's input: gx[i][f] = Σ_o g[i][o]·W[o][f] for O <= 8 (g @ W), float4 columns
+__global__ __launch_bounds__(kThreads) void linear_small_dgrad_kernel(const float* __restrict__ g, int N, int O,
+                                                                      const float* __restrict__ W, int F,
+                                                                      float* __restrict__ gx) {
+    const int F4 = F / 4;
+    const int64_t total = (int64_t)N * F4;
+    for (int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x; e < total; e += (int64_t)gridDim.x * kThreads) {
+        const int i = (int)(e / F4), f = (int)(e % F4) * 4;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int o = 0; o < O; ++o) {
+            const float gv = g[(size_t)i * O + o];
+            const float4 wv = *reinterpret_cast<const float4*>(W + (size_t)o * F + f);
+            acc.x = fmaf(gv, wv.x, acc.x);
+            acc.y = fmaf(gv, wv.y, acc.y);
+            acc.z = fmaf(gv, wv.z, acc.z);
+            acc.w = fmaf(gv, wv.w, acc.w);
+        }
+        *reinterpret_cast<float4*>(gx + (size_t)i * F + f) = acc;
+    }
+}
+
+// y[i][f] = act(y[i][f] + b[f]) in place (the bias / ReLU of a Linear head computed by the GEMM)
+__global__ __launch_bounds__(kThreads) void bias_act_kernel(float* __restrict__ y, int64_t n4, int F4,
+                                                            const float* __restrict__ bias, int act) {
+    for (int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x; e < n4; e += (int64_t)gridDim.x * kThreads) {
+        float4 v = reinterpret_cast<float4*>(y)[e];
+        if (bias != nullptr) {
+            const float4 b = reinterpret_cast<const float4*>(bias)[e % F4];
+            v = make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
+        }
+        if (act == MPGNN_ACT_RELU) v = make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
+        reinterpret_cast<float4*>(y)[e] = v;
+    }
+}
+
 // Linear-layer weight / bias gradient with K = N rows (the wrappers' heads: model.py:147,
 // :224-226): gw[o][f] = Σ_i g[i][o]·x[i][f], gb[o] = Σ_i g[i][o]. Stage 1: workgroup p sums
 // its row slice into partial P[p][o][0..F] (column F = the bias); thread t owns column
@@ -6094,6 +6167,68 @@ int32_t mpgnn_linear_wgrad_workspace_bytes(int64_t N, int32_t F, int32_t O, int6
         *bytes = std::max<int64_t>(*bytes, nch * (128 * 128 + 128) * (int64_t)sizeof(float));
     }
     return MPGNN_OK;
+}
+
+// Linear head forward / input gradient (model.py:147, 224-226): F = O = 128 on the bf16-split GEMM
+// (rel_gemm_bf3_kernel over node rows only: forward with W read transposed as the dgrad does,
+// the input gradient as a plain forward), O <= 8 with a wave per row; others: unsupported.
+static int linear_grid(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)cu_count(), (work + kThreads - 1) / kThreads)); }
+
+static int32_t linear_gemm128(const float* A, int64_t N, const float* W, bool transposed, float* out, hipStream_t strm) {
+    RelGemmArgs a{};
+    a.n_rel = 0;
+    a.n_root = (int)((N + 31) / 32);
+    a.Aroot = A;
+    a.W = W;
+    a.Wroot = W;
+    a.Yroot = out;
+    a.Y = out;
+    a.row_lo = 0;
+    a.row_hi = (int)N;
+    launch_rel_gemm(a, 128, transposed, default_options(), strm);
+    return hip_check(hipGetLastError(), "rel_gemm_bf3_kernel launch (linear)");
+}
+
+int32_t mpgnn_linear_fwd(const float* x, int64_t N, int32_t F, const float* weight, int32_t O, const float* bias,
+                         int32_t act, float* out, void* stream) {
+    if (N < 0 || N > INT32_MAX || F <= 0 || O <= 0) return arg_error("mpgnn_linear_fwd: bad N, F or O");
+    if (act != MPGNN_ACT_NONE && act != MPGNN_ACT_RELU) return arg_error("mpgnn_linear_fwd: bad act");
+    const bool gemm = F == 128 && O == 128 && default_options().gemm_bf3;
+    const bool small = O <= kLinSmallO && F <= 256 && F % 4 == 0;
+    if (!gemm && !small) return MPGNN_ERR_UNSUPPORTED;
+    if (N == 0) return MPGNN_OK;
+    if (!x || !weight || !out) return arg_error("mpgnn_linear_fwd: NULL pointer");
+    if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(weight) | reinterpret_cast<uintptr_t>(out) |
+          reinterpret_cast<uintptr_t>(bias)) & 15) != 0)
+        return arg_error("mpgnn_linear_fwd: pointers must be 16-byte aligned");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    if (gemm) {
+        int32_t st = linear_gemm128(x, N, weight, true, out, strm);
+        if (st != MPGNN_OK || (bias == nullptr && act == MPGNN_ACT_NONE)) return st;
+        const int64_t n4 = N * 128 / 4;
+        hipLaunchKernelGGL(bias_act_kernel, dim3(linear_grid(n4)), dim3(kThreads), 0, strm, out, n4, 32, bias, act);
+        return hip_check(hipGetLastError(), "bias_act_kernel launch");
+    }
+    const int grid = (int)std::min<int64_t>(8 * (int64_t)cu_count(), (N + 3) / 4);
+    hipLaunchKernelGGL(linear_small_fwd_kernel, dim3(grid), dim3(kThreads), 0, strm, x, (int)N, F, weight, O, bias, act, out);
+    return hip_check(hipGetLastError(), "linear_small_fwd_kernel launch");
+}
+
+int32_t mpgnn_linear_dgrad(const float* grad_out, int64_t N, int32_t O, const float* weight, int32_t F, float* grad_x,
+                           void* stream) {
+    if (N < 0 || N > INT32_MAX || F <= 0 || O <= 0) return arg_error("mpgnn_linear_dgrad: bad N, F or O");
+    const bool gemm = F == 128 && O == 128 && default_options().gemm_bf3;
+    const bool small = O <= kLinSmallO && F % 4 == 0;
+    if (!gemm && !small) return MPGNN_ERR_UNSUPPORTED;
+    if (N == 0) return MPGNN_OK;
+    if (!grad_out || !weight || !grad_x) return arg_error("mpgnn_linear_dgrad: NULL pointer");
+    if (((reinterpret_cast<uintptr_t>(grad_out) | reinterpret_cast<uintptr_t>(weight) | reinterpret_cast<uintptr_t>(grad_x)) & 15) != 0)
+        return arg_error("mpgnn_linear_dgrad: pointers must be 16-byte aligned");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    if (gemm) return linear_gemm128(grad_out, N, weight, false, grad_x, strm);
+    hipLaunchKernelGGL(linear_small_dgrad_kernel, dim3(linear_grid(N * (F / 4))), dim3(kThreads), 0, strm, grad_out, (int)N, O,
+                       weight, F, grad_x);
+    return hip_check(hipGetLastError(), "linear_small_dgrad_kernel launch");
 }
 
 int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int32_t F, int32_t O, float* grad_weight,

@@ -39,17 +39,33 @@ class _SplitKLinear(torch.autograd.Function):
     (``F.linear``, ``mm``)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
-        ctx.save_for_backward(x, weight)
+    def forward(ctx, x, weight, bias, relu=False):
         ctx.has_bias = bias is not None
-        return F.linear(x, weight, bias)
+        ctx.relu = relu
+        out = _head_fwd(x, weight, bias, relu)
+        if out is None:  # other shapes: the library GEMM
+            out = F.linear(x, weight, bias)
+            if relu:
+                out = torch.relu(out)
+        ctx.save_for_backward(x, weight, out if relu else None)
+        return out
 
     @staticmethod
     def backward(ctx, g):
-        x, weight = ctx.saved_tensors
+        x, weight, out = ctx.saved_tensors
         gx = gw = gb = None
+        g = g.contiguous()
+        if ctx.relu:  # ReLU fused into the forward: threshold_backward, one launch
+            from . import _lib
+            from .functional import _stream
+            masked = torch.empty_like(out)
+            _lib.check(_lib.lib.mpgnn_relu_bwd(g.data_ptr(), out.data_ptr(), g.numel(), masked.data_ptr(), _stream(g)),
+                       "mpgnn_relu_bwd")
+            g = masked
         if ctx.needs_input_grad[0]:
-            gx = g.mm(weight)
+            gx = _head_dgrad(g, weight)
+            if gx is None:
+                gx = g.mm(weight)
         f, o = x.shape[1], g.shape[1]
         # the HIP pair is scalar-FMA work (N·F·O): for the heads with few outputs (O ≤ 32·256/F:
         # Net.lin, MPNetm.fc2) it beats the library's serial-K GEMM; F = O = 128 (MPNetm.fc1 of
@@ -72,7 +88,7 @@ class _SplitKLinear(torch.autograd.Function):
             _lib.check(_lib.lib.mpgnn_linear_wgrad(xc.data_ptr(), gc.data_ptr(), xc.shape[0], f, o, gw.data_ptr(),
                                                    gb.data_ptr() if want_b else None, ws.data_ptr(), _stream(x)),
                        "mpgnn_linear_wgrad")
-            return gx, gw, gb
+            return gx, gw, gb, None
         if ctx.needs_input_grad[1]:
             n = x.shape[0]
             slices = max(1, min(256, (n + 1023) // 1024))
@@ -86,14 +102,62 @@ class _SplitKLinear(torch.autograd.Function):
                 gw = torch.bmm(gp.view(slices, rows, -1).transpose(1, 2), xp.view(slices, rows, -1)).sum(0)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = g.sum(0)
-        return gx, gw, gb
+        return gx, gw, gb, None
 
 
-def linear(layer: torch.nn.Linear, x: torch.Tensor) -> torch.Tensor:
-    """``layer(x)`` with the split-K weight gradient above (same parameters, same forward)."""
+def _aligned(*ts) -> bool:
+    return all(t is None or (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0)
+               for t in ts)
+
+
+def _head_fwd(x, weight, bias, relu):
+    """act(x @ weightᵀ + bias) through the C ABI's mpgnn_linear_fwd for F = O = 128 (MPNetm.fc1 of a
+    128-wide metapath, model.py:224; the bf16-split GEMM + one bias/ReLU pass): cheap launches
+    where torch's addmm costs ~25 µs of host time (the eager C3 mode-SINGLE epoch is host-bound).
+    The narrow heads (O <= 8) keep torch's forward: the ABI's one-wave-per-row kernel rounds the
+    logits differently and the whole-model gradient check of tests/test_gpu_parity.py
+    (test_adam_training_steps_track_oracle) then lands above its bar on one cancelling bias sum.
+    None: shape or layout not covered."""
+    if x.shape[1] != 128 or weight.shape[0] != 128 or not _aligned(x, weight, bias):
+        return None
+    from . import _lib
+    from .functional import _stream
+    n, f = x.shape
+    o = weight.shape[0]
+    out = torch.empty(n, o, dtype=torch.float32, device=x.device)
+    st = _lib.lib.mpgnn_linear_fwd(x.data_ptr(), n, f, weight.data_ptr(), o, bias.data_ptr() if bias is not None else None,
+                                   _lib.ACT_RELU if relu else _lib.ACT_NONE, out.data_ptr(), _stream(x))
+    if st == _lib.MPGNN_ERR_UNSUPPORTED:
+        return None
+    _lib.check(st, "mpgnn_linear_fwd")
+    return out
+
+
+def _head_dgrad(g, weight):
+    """grad_out @ weight through mpgnn_linear_dgrad (same coverage as _head_fwd), else None."""
+    if not _aligned(g, weight):
+        return None
+    from . import _lib
+    from .functional import _stream
+    n, o = g.shape
+    f = weight.shape[1]
+    gx = torch.empty(n, f, dtype=torch.float32, device=g.device)
+    st = _lib.lib.mpgnn_linear_dgrad(g.data_ptr(), n, o, weight.data_ptr(), f, gx.data_ptr(), _stream(g))
+    if st == _lib.MPGNN_ERR_UNSUPPORTED:
+        return None
+    _lib.check(st, "mpgnn_linear_dgrad")
+    return gx
+
+
+def linear(layer: torch.nn.Linear, x: torch.Tensor, activation=None) -> torch.Tensor:
+    """``layer(x)`` (``F.relu(layer(x))`` with ``activation='relu'``) with the heads' HIP forward /
+    input gradient where covered and the split-K weight gradient above (same parameters)."""
+    if activation not in (None, "relu"):
+        raise ValueError(f"activation must be None or 'relu', got {activation!r}")
     if x.dim() != 2 or not x.is_cuda:
-        return layer(x)
-    return _SplitKLinear.apply(x, layer.weight, layer.bias)
+        out = layer(x)
+        return torch.relu(out) if activation == "relu" else out
+    return _SplitKLinear.apply(x, layer.weight, layer.bias, activation == "relu")
 
 
 class _FastTrainToggle:
@@ -187,6 +251,6 @@ class MPNetm(_FastTrainToggle, torch.nn.Module):
             embeddings.append(h)
         # torch.cat of ONE embedding (a single metapath) is a copy of it: skipped, same values
         concatenated_embedding = embeddings[0] if len(embeddings) == 1 else torch.cat(embeddings, dim=1)
-        h = F.relu(linear(self.fc1, concatenated_embedding))
+        h = linear(self.fc1, concatenated_embedding, activation="relu")  # F.relu(fc1(.)), model.py:225
         h = linear(self.fc2, h)
         return self.log_softmax(h)

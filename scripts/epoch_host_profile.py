@@ -21,6 +21,7 @@ ap.add_argument("--mode", default="single", choices=["single", "all"])
 ap.add_argument("--epochs", type=int, default=20)
 ap.add_argument("--top", type=int, default=40)
 ap.add_argument("--ab-adam", action="store_true", help="alternate torch's fused Adam and main.LeanAdam, 3 rounds")
+ap.add_argument("--ab-heads", action="store_true", help="alternate the Linear heads on the C ABI and on torch, 3 rounds")
 a = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -58,6 +59,26 @@ def epoch():
         fwd()
 
 
+if a.ab_heads:
+    import mpgnn_amd.model as M
+    fwd0, dgrad0 = M._head_fwd, M._head_dgrad
+    modes = {"abi": (fwd0, dgrad0), "torch": (lambda *_: None, lambda *_: None)}
+    opt = mpgnn_amd.main.LeanAdam(list(model.parameters()), lr=0.01, weight_decay=0.0005, fused=True)
+    rec = {k: [] for k in modes}
+    for _ in range(3):
+        for k, (f1, f2) in modes.items():
+            M._head_fwd, M._head_dgrad = f1, f2
+            for _ in range(5):
+                epoch()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.epochs):
+                epoch()
+            torch.cuda.synchronize()
+            rec[k].append(round((time.perf_counter() - t0) * 1e3 / a.epochs, 4))
+    M._head_fwd, M._head_dgrad = fwd0, dgrad0
+    print(json.dumps({"workload": a.workload, "mode": a.mode, "epoch_wall_ms": rec}), flush=True)
+    sys.exit(0)
 if a.ab_adam:
     params = list(model.parameters())
     opts = {"torch": torch.optim.Adam(params, lr=0.01, weight_decay=0.0005, fused=True),

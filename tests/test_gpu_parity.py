@@ -1045,9 +1045,9 @@ def test_linear_wgrad_abi_output_blocks(n, f, o):
 @pytest.mark.parametrize("n,f_in,f_out", [(14541, 128, 2), (1000, 128, 64), (300, 64, 3), (14541, 128, 128),
                                          (2000, 256, 200)])
 def test_split_k_linear_matches_nn_linear(n, f_in, f_out):
-    """model.linear: forward bit-identical to nn.Linear; grad_weight (sliced over rows) and
-    grad_bias / grad_input within fp32 rounding of autograd's (wide heads such as MPNetm.fc1
-    128 -> 128 take the batched-GEMM slicing, the narrow ones the C ABI pair)."""
+    """model.linear: forward (the C ABI's mpgnn_linear_fwd for 128 -> 128 and O <= 8, nn.Linear's
+    GEMM otherwise), grad_weight (sliced over rows) and grad_bias / grad_input within the suite's
+    bar of autograd's, decided against the float64 truth where fp32 orders differ."""
     from mpgnn_amd.model import linear
     torch.manual_seed(0)
     lin = torch.nn.Linear(f_in, f_out).to(DEV)
@@ -1059,10 +1059,10 @@ def test_split_k_linear_matches_nn_linear(n, f_in, f_out):
     x.grad = None
     lin.zero_grad()
     out = linear(lin, x)
-    assert torch.equal(out, ref)
-    out.backward(g)
     # truth: the same products in float64
     x64, g64, w64 = x.detach().double().cpu(), g.double().cpu(), lin.weight.detach().double().cpu()
+    rel_close(out, ref, what="out", ref64=x64 @ w64.t() + lin.bias.detach().double().cpu())
+    out.backward(g)
     truth = [g64 @ w64, g64.t() @ x64, g64.sum(0)]
     for got, want, t64, what in zip([x.grad, lin.weight.grad, lin.bias.grad], ref_grads, truth, ["dx", "dW", "db"]):
         rel_close(got, want, what=what, ref64=t64)
@@ -1264,6 +1264,68 @@ def test_linear_head_gradients_vs_autograd(n, f, o, bias):
     rel_close(out, ref_out, what=f"linear {n}x{f}->{o} out", ref64=o64.detach())
     for a, b, t, nm in zip(got, ref, t64, ("dx", "dW", "dbias")):
         rel_close(a, b, what=f"linear {n}x{f}->{o} {nm}", ref64=t)
+
+
+@pytest.mark.parametrize("n,f,o,bias,relu", [(14541, 128, 2, True, False), (333, 64, 5, False, True),
+                                             (1000, 256, 8, True, True), (7, 4, 1, True, False)])
+def test_linear_small_head_abi_vs_torch(n, f, o, bias, relu):
+    """mpgnn_linear_fwd / mpgnn_linear_dgrad for heads with O <= 8 through the C ABI directly
+    (model.linear keeps torch's forward for them, see model._head_fwd): act(x @ Wᵀ + b) and
+    g @ W against torch at the suite's bar, the float64 truth deciding."""
+    from mpgnn_amd import _lib
+    gen = torch.Generator().manual_seed(21)
+    x = torch.randn(n, f, generator=gen)
+    w = torch.randn(o, f, generator=gen) * 0.1
+    b = torch.randn(o, generator=gen) if bias else None
+    go = torch.randn(n, o, generator=gen)
+    xd, wd, gd = x.to(DEV), w.to(DEV), go.to(DEV)
+    bd = b.to(DEV) if bias else None
+    out = torch.empty(n, o, device=DEV)
+    gx = torch.empty(n, f, device=DEV)
+    _lib.check(_lib.lib.mpgnn_linear_fwd(xd.data_ptr(), n, f, wd.data_ptr(), o, bd.data_ptr() if bias else None,
+                                         _lib.ACT_RELU if relu else _lib.ACT_NONE, out.data_ptr(), None), "fwd")
+    _lib.check(_lib.lib.mpgnn_linear_dgrad(gd.data_ptr(), n, o, wd.data_ptr(), f, gx.data_ptr(), None), "dgrad")
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.linear(xd, wd, bd)
+    ref64 = torch.nn.functional.linear(x.double(), w.double(), b.double() if bias else None)
+    if relu:
+        ref, ref64 = torch.relu(ref), torch.relu(ref64)
+    rel_close(out, ref, what="small head out", ref64=ref64)
+    rel_close(gx, gd @ wd, what="small head dgrad", ref64=go.double() @ w.double())
+
+
+@pytest.mark.parametrize("n,f,o", [(14541, 128, 128), (14541, 128, 2), (333, 64, 5), (1000, 128, 64)])
+def test_linear_head_fused_relu_vs_autograd(n, f, o):
+    """model.linear(..., activation='relu') = F.relu(F.linear(...)) (MPNetm's fc1, model.py:225):
+    the ReLU in the head's launch (mpgnn_linear_fwd / its bias pass) and its backward through
+    mpgnn_relu_bwd, forward and every gradient vs autograd at the suite's bar."""
+    from mpgnn_amd.model import linear
+    gen = torch.Generator().manual_seed(12)
+    layer = torch.nn.Linear(f, o).to(DEV)
+    x = torch.randn(n, f, generator=gen).to(DEV).requires_grad_(True)
+    go = torch.randn(n, o, generator=gen).to(DEV)
+    # no gradient where the pre-activation is within fp32 rounding of 0 (either ReLU mask is right)
+    z64 = torch.nn.functional.linear(x.detach().cpu().double(), layer.weight.detach().cpu().double(),
+                                     layer.bias.detach().cpu().double())
+    go = go * (z64.abs() > 1e-4).to(DEV, torch.float32)
+    out = linear(layer, x, activation="relu")
+    out.backward(go)
+    got = [x.grad.clone(), layer.weight.grad.clone(), layer.bias.grad.clone()]
+    x.grad = None
+    layer.zero_grad(set_to_none=True)
+    ref_out = torch.relu(torch.nn.functional.linear(x, layer.weight, layer.bias))
+    ref_out.backward(go)
+    ref = [x.grad, layer.weight.grad, layer.bias.grad]
+    x64 = x.detach().cpu().double().requires_grad_(True)
+    w64 = layer.weight.detach().cpu().double().requires_grad_(True)
+    b64 = layer.bias.detach().cpu().double().requires_grad_(True)
+    o64 = torch.relu(torch.nn.functional.linear(x64, w64, b64))
+    o64.backward(go.cpu().double())
+    rel_close(out, ref_out, what=f"relu linear {n}x{f}->{o} out", ref64=o64.detach())
+    for a, b, t, nm in zip(got, ref, [x64.grad, w64.grad, b64.grad], ("dx", "dW", "dbias")):
+        rel_close(a, b, what=f"relu linear {n}x{f}->{o} {nm}", ref64=t)
+    with pytest.raises(ValueError):
+        linear(layer, x, activation="gelu")
 
 
 # ------------------------------------------------------------------------------------------
