@@ -26,6 +26,9 @@ from .score import InputLayer, OutputLayer, Score  # noqa: F401  (model.py:26-12
 __all__ = ["Net", "MPNetm", "linear", "InputLayer", "OutputLayer", "Score"]
 
 
+_WGRAD_WS: dict = {}  # (N, F, O) -> mpgnn_linear_wgrad_workspace_bytes
+
+
 class _SplitKLinear(torch.autograd.Function):
     """``F.linear`` whose weight gradient is reduced in slices over the node dimension.
 
@@ -78,10 +81,14 @@ class _SplitKLinear(torch.autograd.Function):
             from . import _lib
             from .functional import _stream, _workspace
             xc, gc = x.contiguous(), g.contiguous()
-            nbytes = ctypes.c_int64()
-            _lib.check(_lib.lib.mpgnn_linear_wgrad_workspace_bytes(xc.shape[0], f, o, ctypes.byref(nbytes)),
-                       "mpgnn_linear_wgrad_workspace_bytes")
-            ws = _workspace(int(nbytes.value), x.device)
+            key = (xc.shape[0], f, o)
+            nb = _WGRAD_WS.get(key)
+            if nb is None:  # the size depends on the shape only: asked once per shape
+                nbytes = ctypes.c_int64()
+                _lib.check(_lib.lib.mpgnn_linear_wgrad_workspace_bytes(xc.shape[0], f, o, ctypes.byref(nbytes)),
+                           "mpgnn_linear_wgrad_workspace_bytes")
+                nb = _WGRAD_WS[key] = int(nbytes.value)
+            ws = _workspace(nb, x.device)
             gw = torch.empty(o, f, dtype=torch.float32, device=x.device)
             want_b = ctx.has_bias and ctx.needs_input_grad[2]
             gb = torch.empty(o, dtype=torch.float32, device=x.device) if want_b else None
