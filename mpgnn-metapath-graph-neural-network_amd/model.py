@@ -125,8 +125,9 @@ def _head_fwd(x, weight, bias, relu):
     logits differently and the whole-model gradient check of tests/test_gpu_parity.py
     (test_adam_training_steps_track_oracle) then lands above its bar on one cancelling bias sum.
     None: shape or layout not covered."""
-    if x.shape[1] != 128 or weight.shape[0] != 128 or not _aligned(x, weight, bias):
-        return None
+    if (x.dim() != 2 or weight.dim() != 2 or x.shape[1] != 128 or tuple(weight.shape) != (128, 128)
+            or (bias is not None and tuple(bias.shape) != (128,)) or not _aligned(x, weight, bias)):
+        return None  # (a shape mismatch is left to F.linear, which raises as the reference does)
     from . import _lib
     from .functional import _stream
     n, f = x.shape
@@ -141,8 +142,8 @@ def _head_fwd(x, weight, bias, relu):
 
 
 def _head_dgrad(g, weight):
-    """grad_out @ weight through mpgnn_linear_dgrad (same coverage as _head_fwd), else None."""
-    if not _aligned(g, weight):
+    """grad_out @ weight through mpgnn_linear_dgrad (F = O = 128, or O <= 8), else None."""
+    if g.dim() != 2 or weight.dim() != 2 or g.shape[1] != weight.shape[0] or not _aligned(g, weight):
         return None
     from . import _lib
     from .functional import _stream
