@@ -1622,6 +1622,12 @@ __device__ __forceinline__ int wg_pair_range(int b, int C) {
 }
 
 __device__ __forceinline__ void split3_bf16(float a, __bf16& h0, __bf16& h1, __bf16& h2) {
+#ifdef MPGNN_PROBE_NOSPLIT  // probe build only (scripts/r05_probe_nosplit.sh): the split's VALU cost
+    h0 = (__bf16)a;
+    h1 = (__bf16)0.0f;
+    h2 = (__bf16)0.0f;
+    return;
+#endif
     h0 = (__bf16)a;               // v_cvt_pk_bf16_f32: round to nearest even
     const float r1 = a - (float)h0;  // exact
     h1 = (__bf16)r1;
