@@ -1036,7 +1036,7 @@ def main():
         model.train()
         opt.zero_grad()
         out = fwd_model()
-        loss = torch.nn.functional.nll_loss(out.index_select(0, train_idx), train_y)
+        loss = mpgnn_amd.metrics.nll_loss_rows(out, train_idx, train_y)
         loss.backward()
         opt.step()
         model.eval()
@@ -1073,7 +1073,7 @@ def main():
             def epoch_g():
                 netg.train()
                 out = netg(x, ei, et)
-                loss = torch.nn.functional.nll_loss(out.index_select(0, train_idx), train_y)
+                loss = mpgnn_amd.metrics.nll_loss_rows(out, train_idx, train_y)
                 loss.backward()
                 optg.step()
                 netg.eval()

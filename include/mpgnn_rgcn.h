@@ -213,6 +213,21 @@ int32_t mpgnn_confusion_counts(const float* scores, int64_t rows, int32_t num_cl
                                const int64_t* const* row_idx, const int64_t* const* labels, const int64_t* n,
                                int64_t* counts, void* stream);
 
+/* The loops' training loss F.nll_loss(out[train_idx], train_y) (main.py:1062-1066, mean
+ * reduction, no class weights) over log-probabilities logp [rows, num_classes]: pairs j with
+ * target[j] == ignore_index are skipped; *total_weight = the kept pairs' count (float);
+ * *loss = -(Σ_j logp[row_idx[j], target[j]] / *total_weight) (NaN when nothing is kept, or when
+ * a kept pair lies outside the matrix). One launch (one workgroup). */
+int32_t mpgnn_nll_rows_fwd(const float* logp, int64_t rows, int32_t num_classes, const int64_t* row_idx,
+                           const int64_t* target, int64_t n, int64_t ignore_index, float* loss, float* total_weight,
+                           void* stream);
+/* Its input gradient: grad_logp[row_idx[j], target[j]] += -(*grad_loss / *total_weight) for every
+ * kept pair inside the matrix (torch's nll_loss backward value, index_select's backward
+ * placement; device scalars). grad_logp [rows, num_classes] must be zeroed by the caller. */
+int32_t mpgnn_nll_rows_bwd(const float* grad_loss, const float* total_weight, int64_t rows, int32_t num_classes,
+                           const int64_t* row_idx, const int64_t* target, int64_t n, int64_t ignore_index,
+                           float* grad_logp, void* stream);
+
 /* Forward and input gradient of the wrappers' Linear heads (Net.lin model.py:147; MPNetm.fc1 /
  * fc2 model.py:224-226), replacing F.linear / grad_out @ weight (host-cheap single launches on the
  * eager epoch's path): out = act(x @ weightᵀ + bias) with x [N,F], weight [O,F], bias [O]

@@ -98,6 +98,8 @@ SIGNATURES = [
     ("mpgnn_score_loss_multi", _I32, [_P, _P, _I64, _P, _P]),
     ("mpgnn_score_argmax_multi_bwd", _I32, [_P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P]),
     ("mpgnn_confusion_counts", _I32, [_P, _I64, _I32, _I32, _P, _P, _P, _P, _P]),
+    ("mpgnn_nll_rows_fwd", _I32, [_P, _I64, _I32, _P, _P, _I64, _I64, _P, _P, _P]),
+    ("mpgnn_nll_rows_bwd", _I32, [_P, _P, _I64, _I32, _P, _P, _I64, _I64, _P, _P]),
     ("mpgnn_score_bag_argmax", _I32, [_P, _P, _I32, _P, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("mpgnn_score_bag_argmax_bwd", _I32, [_P, _I64, _P, _P, _P, _P, _P, _P, _I32, _I64, _P, _P, _P, _P, _P, _P,
                                           _P]),

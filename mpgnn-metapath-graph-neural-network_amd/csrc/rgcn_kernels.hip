@@ -5434,6 +5434,9 @@ static void fill_selection(const mpgnn_plan* p, Selection* s) {
 }
 
 static size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+static size_t align16(size_t b) { return (b + 15) / 16 * 16; }
+// the grad_x list's split-row counters, whole 16-byte words (run_grad_x zeroes them per call)
+static size_t split_counter_bytes(const mpgnn_plan* p) { return align16((size_t)p->tx_f.nsplit * sizeof(unsigned)); }
 
 struct RootChunks {
     int rows_lo = 0, rows_hi = 0, chunk = 256, n = 0;
@@ -5488,8 +5491,8 @@ static WsLayout ws_layout(const mpgnn_plan* p, int32_t mode, const Selection& s,
     w.h = off; off += align256(Sm_sel * F_in * sizeof(float));
     // + the grad_x list's split-row counters behind its carry slots (run_grad_x)
     w.pdx = off;
-    off += align256(std::max(dx_pieces, seg_slots) * F_in * sizeof(float) +
-                    (mode == MPGNN_MODE_ALL ? (size_t)p->tx_f.nsplit * sizeof(unsigned) : 0));
+    off += align256(align16(std::max(dx_pieces, seg_slots) * F_in * sizeof(float)) +
+                    (mode == MPGNN_MODE_ALL ? split_counter_bytes(p) : 0));
     w.p = off; off += align256((size_t)(s.c_hi - s.c_lo) * F_in * F_out * sizeof(float));
     w.proot = off; off += align256((size_t)rc.n * F_in * F_out * sizeof(float));
     w.pb = off; off += align256((size_t)rc.n * F_out * sizeof(float));
@@ -6810,9 +6813,10 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         TimedLaunch tl(MPGNN_K_ROW_DX, strm);
         if (p->opt.flat_fuse_split && p->tx_f.nsplit > 0) {
             // piece counters behind the carry slots (ws_layout reserves them in the pdx region)
-            f.arrive = reinterpret_cast<unsigned*>(Pdx + (size_t)p->tx_f.nslots * F_in);
-            st = hip_check(hipMemsetAsync(f.arrive, 0, (size_t)p->tx_f.nsplit * sizeof(unsigned), strm),
-                           "memset split counters");
+            // 16-byte aligned start and length: one fill launch (a ragged memset is two)
+            f.arrive = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(Pdx) +
+                                                   align16((size_t)p->tx_f.nslots * F_in * sizeof(float)));
+            st = hip_check(hipMemsetAsync(f.arrive, 0, split_counter_bytes(p), strm), "memset split counters");
             if (st != MPGNN_OK) return st;
         }
         st = run_flat(f, strm);

@@ -463,6 +463,69 @@ __global__ __launch_bounds__(kConfThreads) void confusion_counts_kernel(ConfArgs
         a.out[(int64_t)L * 3 * C + k] = (int64_t)conf_lds[(k / C) * (C + 1) + k % C];
 }
 
+// ---------------------------------------------------------------------------------------
+// The training loss of the loops (main.py:1062-1066, ``F.nll_loss(out[train_idx], train_y)``):
+// the mean negative log-probability of each listed (row, target) pair, targets equal to
+// ignore_index skipped. Forward: one workgroup sums the picked entries and counts the kept
+// pairs (total_weight, an exact integer count in float as in torch's kernel); loss = -(sum /
+// total_weight). Backward: grad[row, target] += -(grad_loss / total_weight) — torch's
+// nll_loss backward value, placed where index_select's backward would add it (the caller
+// zeroes grad). Three torch ops and seven launches per epoch become one launch forward and two
+// backward. A pair outside the matrix makes the loss NaN and is skipped by the backward (the
+// host validates the lists once, metrics.nll_loss_rows).
+// ---------------------------------------------------------------------------------------
+constexpr int kNllThreads = 1024;
+
+__global__ __launch_bounds__(kNllThreads) void nll_rows_fwd_kernel(const float* __restrict__ logp, int64_t rows, int C,
+                                                                   const int64_t* __restrict__ idx,
+                                                                   const int64_t* __restrict__ tgt, int64_t n,
+                                                                   int64_t ignore, float* __restrict__ loss,
+                                                                   float* __restrict__ total_weight) {
+    __shared__ float s_sum[kNllThreads / 64], s_w[kNllThreads / 64];
+    float sum = 0.f, w = 0.f;
+    for (int64_t j = threadIdx.x; j < n; j += kNllThreads) {
+        const int64_t t = tgt[j];
+        if (t == ignore) continue;
+        const int64_t r = idx[j];
+        const bool ok = r >= 0 && r < rows && t >= 0 && t < C;
+        sum += ok ? logp[r * C + t] : __builtin_nanf("");
+        w += 1.f;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o);
+        w += __shfl_xor(w, o);
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_sum[wv] = sum;
+        s_w[wv] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float S = 0.f, W = 0.f;
+        for (int k = 0; k < kNllThreads / 64; ++k) {
+            S += s_sum[k];
+            W += s_w[k];
+        }
+        loss[0] = -(S / W);
+        total_weight[0] = W;
+    }
+}
+
+__global__ __launch_bounds__(kScoreThreads) void nll_rows_bwd_kernel(const float* __restrict__ grad_loss,
+                                                                     const float* __restrict__ total_weight,
+                                                                     int64_t rows, int C, const int64_t* __restrict__ idx,
+                                                                     const int64_t* __restrict__ tgt, int64_t n,
+                                                                     int64_t ignore, float* __restrict__ grad) {
+    const int64_t j = (int64_t)blockIdx.x * kScoreThreads + threadIdx.x;
+    if (j >= n) return;
+    const int64_t t = tgt[j];
+    const int64_t r = idx[j];
+    if (t == ignore || r < 0 || r >= rows || t < 0 || t >= C) return;
+    atomicAdd(grad + r * C + t, -(grad_loss[0] / total_weight[0]));  // equal addends: order-free
+}
+
 }  // namespace
 }  // namespace mpgnn
 
@@ -620,4 +683,31 @@ extern "C" int32_t mpgnn_confusion_counts(const float* scores, int64_t rows, int
     const size_t lds = (size_t)3 * (num_classes + 1) * sizeof(int);
     hipLaunchKernelGGL(confusion_counts_kernel, dim3(n_lists), dim3(kConfThreads), lds, strm, a);
     return hip_status(hipGetLastError(), "confusion_counts_kernel launch");
+}
+
+extern "C" int32_t mpgnn_nll_rows_fwd(const float* logp, int64_t rows, int32_t num_classes, const int64_t* row_idx,
+                                      const int64_t* target, int64_t n, int64_t ignore_index, float* loss,
+                                      float* total_weight, void* stream) {
+    if (rows < 0 || num_classes <= 0 || n < 0) return arg_fail("mpgnn_nll_rows_fwd: bad sizes");
+    if (!loss || !total_weight || (n > 0 && (!logp || !row_idx || !target)))
+        return arg_fail("mpgnn_nll_rows_fwd: NULL argument");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(nll_rows_fwd_kernel, dim3(1), dim3(kNllThreads), 0, strm, logp, rows, (int)num_classes, row_idx,
+                       target, n, ignore_index, loss, total_weight);
+    return hip_status(hipGetLastError(), "nll_rows_fwd_kernel launch");
+}
+
+extern "C" int32_t mpgnn_nll_rows_bwd(const float* grad_loss, const float* total_weight, int64_t rows,
+                                      int32_t num_classes, const int64_t* row_idx, const int64_t* target, int64_t n,
+                                      int64_t ignore_index, float* grad_logp, void* stream) {
+    if (rows < 0 || num_classes <= 0 || n < 0 || n / kScoreThreads >= (int64_t)INT32_MAX)
+        return arg_fail("mpgnn_nll_rows_bwd: bad sizes");
+    if (n == 0) return MPGNN_OK;
+    if (!grad_loss || !total_weight || !row_idx || !target || !grad_logp)
+        return arg_fail("mpgnn_nll_rows_bwd: NULL argument");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    const unsigned grid = (unsigned)((n + kScoreThreads - 1) / kScoreThreads);
+    hipLaunchKernelGGL(nll_rows_bwd_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, grad_loss, total_weight, rows,
+                       (int)num_classes, row_idx, target, n, ignore_index, grad_logp);
+    return hip_status(hipGetLastError(), "nll_rows_bwd_kernel launch");
 }

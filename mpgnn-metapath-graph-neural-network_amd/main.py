@@ -13,10 +13,9 @@ from __future__ import annotations
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 from . import data as _data
-from .metrics import class_weight_balanced, confusion_counts_rows, f1_from_counts
+from .metrics import class_weight_balanced, confusion_counts_rows, f1_from_counts, nll_loss_rows
 from .model import MPNetm
 # score function helpers of main.py:387-917 (both branches, GPU kernels): same names, plus the
 # batched first-round scoring of every relation (score_relations_batched)
@@ -278,7 +277,7 @@ def _train_step(model, optimizer, data):
     optimizer.zero_grad()
     out = model(data.x, data.edge_index, data.edge_type)
     weights = class_weight_balanced(data.train_y)
-    loss = F.nll_loss(take_rows(out, data.train_idx).squeeze(-1), data.train_y)
+    loss = nll_loss_rows(out, data.train_idx, data.train_y)
     loss.backward()
     optimizer.step()
     return loss.detach(), weights
@@ -297,7 +296,7 @@ def _val_counts(model, data):
     """mpgnn_validation's work on the device: (val loss, [2, 3, C] train / val confusion counts)."""
     model.eval()
     pred = model(data.x, data.edge_index, data.edge_type)
-    loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
+    loss_val = nll_loss_rows(pred, data.val_idx, data.val_y)
     return loss_val, confusion_counts_rows(pred, [(data.train_idx, data.train_y), (data.val_idx, data.val_y)])
 
 
@@ -307,7 +306,7 @@ def mpgnn_validation(model, data, class_weight):
     the same macro F1, as in the reference."""
     model.eval()
     pred = model(data.x, data.edge_index, data.edge_type)
-    loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
+    loss_val = nll_loss_rows(pred, data.val_idx, data.val_y)
     f1_train, f1_val = f1_from_counts(confusion_counts_rows(pred, [(data.train_idx, data.train_y),
                                                                      (data.val_idx, data.val_y)]))
     return f1_train, f1_val, f1_val, loss_val
@@ -318,7 +317,7 @@ def mpgnn_test(model, data, class_weight):
     """main.py:1101-1115 → (test loss tensor, test macro F1)."""
     model.eval()
     pred = model(data.x, data.edge_index, data.edge_type)
-    loss_test = F.nll_loss(pred[data.test_idx].squeeze(-1), data.test_y)
+    loss_test = nll_loss_rows(pred, data.test_idx, data.test_y)
     (f1_test,) = f1_from_counts(confusion_counts_rows(pred, [(data.test_idx, data.test_y)]))
     return loss_test, f1_test
 

@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 from .main import (_adam, _adam_graphable, _epochs, _graphs_enabled, _one_hot_colours, Data,  # noqa: F401
                    get_edge_index_and_type_no_reverse, load_files, load_graph, take_rows)
-from .metrics import class_weight_balanced, class_weight_tensor, confusion_counts_rows, f1_from_counts
+from .metrics import class_weight_balanced, class_weight_tensor, confusion_counts_rows, f1_from_counts, nll_loss_rows
 from .model import Net
 
 __all__ = ["Data", "get_node_features", "mpgnn_train", "mpgnn_validation", "mpgnn_test", "mpgnn_parallel_multiple", "EPOCHS"]
@@ -62,7 +62,7 @@ def _val_counts(model, data):
     train and validation predictions)."""
     model.eval()
     pred = _forward(model, data)
-    loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
+    loss_val = nll_loss_rows(pred, data.val_idx, data.val_y)
     counts = confusion_counts_rows(pred, [(data.train_idx, data.train_y), (data.val_idx, data.val_y)])
     return loss_val, counts
 
@@ -71,7 +71,7 @@ def _val_counts(model, data):
 def _test_counts(model, data):
     model.eval()
     pred = _forward(model, data)
-    loss_test = F.nll_loss(pred[data.test_idx].squeeze(-1), data.test_y)
+    loss_test = nll_loss_rows(pred, data.test_idx, data.test_y)
     counts = confusion_counts_rows(pred, [(data.test_idx, data.test_y)])
     return loss_test, counts
 
@@ -81,7 +81,7 @@ def mpgnn_validation(model, data, class_weight):
     """main_rgcn.py:395-416 → (f1 train, f1 val, f1 val, val loss tensor)."""
     model.eval()
     pred = _forward(model, data)
-    loss_val = F.nll_loss(pred[data.val_idx].squeeze(-1), data.val_y)
+    loss_val = nll_loss_rows(pred, data.val_idx, data.val_y)
     f1_train, f1_val = f1_from_counts(confusion_counts_rows(pred, [(data.train_idx, data.train_y),
                                                                      (data.val_idx, data.val_y)]))
     return f1_train, f1_val, f1_val, loss_val
@@ -92,7 +92,7 @@ def mpgnn_test(model, data, class_weight):
     """main_rgcn.py:418-432 → (test loss tensor, test macro F1)."""
     model.eval()
     pred = _forward(model, data)
-    loss_test = F.nll_loss(pred[data.test_idx].squeeze(-1), data.test_y)
+    loss_test = nll_loss_rows(pred, data.test_idx, data.test_y)
     (f1_test,) = f1_from_counts(confusion_counts_rows(pred, [(data.test_idx, data.test_y)]))
     return loss_test, f1_test
 

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 __all__ = ["f1_macro", "f1_macro_many", "confusion_counts_many", "confusion_counts_rows", "f1_from_counts",
-           "class_weight_balanced", "class_weight_tensor"]
+           "class_weight_balanced", "class_weight_tensor", "nll_loss_rows"]
 
 
 def _count(v: torch.Tensor, bins: int) -> torch.Tensor:
@@ -93,6 +93,77 @@ def confusion_counts_rows(scores: torch.Tensor, lists) -> torch.Tensor:
     _lib.check(_lib.lib.mpgnn_confusion_counts(sc.data_ptr(), sc.shape[0], c, n, p_idx, p_lab, p_n, out.data_ptr(),
                                                _stream(sc)), "mpgnn_confusion_counts")
     return out
+
+
+class _NllRows(torch.autograd.Function):
+    """mpgnn_nll_rows_fwd / _bwd: the loss in one launch, its input gradient in a zero fill and
+    one scatter launch (torch: index_select, nll_loss and their backward, 7 launches)."""
+
+    @staticmethod
+    def forward(ctx, logp, idx, target):
+        from . import _lib
+        from .functional import _stream
+        loss = torch.empty((), dtype=torch.float32, device=logp.device)
+        tw = torch.empty((), dtype=torch.float32, device=logp.device)
+        _lib.check(_lib.lib.mpgnn_nll_rows_fwd(logp.data_ptr(), logp.shape[0], logp.shape[1], idx.data_ptr(),
+                                               target.data_ptr(), idx.numel(), -100, loss.data_ptr(), tw.data_ptr(),
+                                               _stream(logp)), "mpgnn_nll_rows_fwd")
+        ctx.lists = (idx, target, tw)
+        ctx.shape = tuple(logp.shape)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import _lib
+        from .functional import _stream
+        idx, target, tw = ctx.lists
+        g = g.contiguous()
+        grad = torch.zeros(ctx.shape, dtype=torch.float32, device=g.device)
+        _lib.check(_lib.lib.mpgnn_nll_rows_bwd(g.data_ptr(), tw.data_ptr(), ctx.shape[0], ctx.shape[1], idx.data_ptr(),
+                                               target.data_ptr(), idx.numel(), -100, grad.data_ptr(), _stream(grad)),
+                   "mpgnn_nll_rows_bwd")
+        return grad, None, None
+
+
+# the (row list, target list) pairs last checked in range, by OBJECT (weakrefs) and _version, with
+# the matrix size: the loops pass the same train / val / test lists every epoch, so the one host
+# read of the check happens once per list (and never inside a HIP-graph capture)
+_NLL_OK: list = []
+_NLL_OK_MAX = 4
+
+
+def _nll_lists_valid(idx: torch.Tensor, target: torch.Tensor, rows: int, c: int) -> bool:
+    for ri, vi, rt, vt, shape in _NLL_OK:
+        if ri() is idx and vi == idx._version and rt() is target and vt == target._version and shape == (rows, c):
+            return True
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    ok = bool((((target == -100) | ((target >= 0) & (target < c))).all() &
+               ((idx >= 0) & (idx < rows)).all()).item())
+    if ok:
+        _NLL_OK.insert(0, (weakref.ref(idx), idx._version, weakref.ref(target), target._version, (rows, c)))
+        del _NLL_OK[_NLL_OK_MAX:]
+    return ok
+
+
+def nll_loss_rows(logp: torch.Tensor, idx, target: torch.Tensor) -> torch.Tensor:
+    """``F.nll_loss(logp[idx].squeeze(-1), target)`` — the loops' loss (main.py:1062-1066,
+    1090, 1107; mean over the listed rows, ignore_index -100, no class weights). On the GPU
+    (float32 [rows, C >= 2] log-probabilities, 1-D int64 row and target lists on the same device,
+    lists checked in range once) ``mpgnn_nll_rows_fwd`` / ``_bwd``: the same loss up to the
+    summation order (a few ulp), the same input gradient bit for bit (tests/test_loop.py).
+    Anything else — and lists with an out-of-range entry, so torch raises its own error — runs
+    torch's ops."""
+    fast = (logp.is_cuda and logp.dim() == 2 and logp.dtype == torch.float32 and logp.shape[1] >= 2
+            and torch.is_tensor(idx) and idx.dim() == 1 and idx.dtype == torch.int64 and idx.device == logp.device
+            and torch.is_tensor(target) and target.dim() == 1 and target.dtype == torch.int64
+            and target.device == logp.device and target.numel() == idx.numel()
+            and _nll_lists_valid(idx, target, logp.shape[0], logp.shape[1]))
+    if fast:
+        return _NllRows.apply(logp.contiguous(), idx.contiguous(), target.contiguous())
+    rows = logp.index_select(0, idx.to(logp.device)) if torch.is_tensor(idx) and idx.dim() == 1 and idx.dtype in (
+        torch.int64, torch.int32) else logp[idx]
+    return torch.nn.functional.nll_loss(rows.squeeze(-1), target)
 
 
 def _num_cols(t: torch.Tensor) -> int:

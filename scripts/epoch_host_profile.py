@@ -22,6 +22,7 @@ ap.add_argument("--epochs", type=int, default=20)
 ap.add_argument("--top", type=int, default=40)
 ap.add_argument("--ab-adam", action="store_true", help="alternate torch's fused Adam and main.LeanAdam, 3 rounds")
 ap.add_argument("--ab-heads", action="store_true", help="alternate the Linear heads on the C ABI and on torch, 3 rounds")
+ap.add_argument("--ab-loss", action="store_true", help="alternate metrics.nll_loss_rows and torch's ops, 3 rounds")
 a = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -47,11 +48,18 @@ train_idx = torch.arange(0, g.num_nodes, 3, device=dev)
 train_y = y[train_idx]
 
 
+def torch_loss(out, idx, y):
+    return torch.nn.functional.nll_loss(out.index_select(0, idx), y)
+
+
+LOSS = [mpgnn_amd.metrics.nll_loss_rows]
+
+
 def epoch():
     model.train()
     opt.zero_grad()
     out = fwd()
-    loss = torch.nn.functional.nll_loss(out.index_select(0, train_idx), train_y)
+    loss = LOSS[0](out, train_idx, train_y)
     loss.backward()
     opt.step()
     model.eval()
@@ -59,6 +67,22 @@ def epoch():
         fwd()
 
 
+if a.ab_loss:
+    modes = {"fused": mpgnn_amd.metrics.nll_loss_rows, "torch": torch_loss}
+    rec = {k: [] for k in modes}
+    for _ in range(3):
+        for k, f in modes.items():
+            LOSS[0] = f
+            for _ in range(5):
+                epoch()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.epochs):
+                epoch()
+            torch.cuda.synchronize()
+            rec[k].append(round((time.perf_counter() - t0) * 1e3 / a.epochs, 4))
+    print(json.dumps({"workload": a.workload, "mode": a.mode, "epoch_wall_ms": rec}), flush=True)
+    sys.exit(0)
 if a.ab_heads:
     import mpgnn_amd.model as M
     fwd0, dgrad0 = M._head_fwd, M._head_dgrad

@@ -200,6 +200,77 @@ def test_confusion_counts_rows_kernel_equals_torch(seed, c):
             f1_score(pred[keep].tolist(), y[keep].tolist(), average="macro")
 
 
+def _nll_case(seed, rows, c, n, dup=False, ignore=False):
+    """log_softmax rows (requires grad through the softmax input), a row list (repeated rows when
+    dup) and targets (some ignore_index -100 when ignore)."""
+    g = torch.Generator().manual_seed(seed)
+    h = torch.randn(rows, c, generator=g) * 3
+    idx = torch.randint(0, rows, (n,), generator=g) if dup else torch.randperm(rows, generator=g)[:n]
+    y = torch.randint(0, c, (n,), generator=g)
+    if ignore and n:
+        y[torch.rand(n, generator=g) < 0.2] = -100
+    return h, idx, y
+
+
+def test_nll_loss_rows_cpu_is_torch():
+    h, idx, y = _nll_case(0, 50, 3, 20)
+    logp = torch.log_softmax(h, 1)
+    assert torch.equal(metrics.nll_loss_rows(logp, idx, y), torch.nn.functional.nll_loss(logp[idx], y))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,rows,c,n,dup,ignore", [(0, 14541, 2, 4847, False, False), (1, 3000, 5, 2500, True, True),
+                                                      (2, 70, 2, 0, False, False), (3, 9, 3, 9, False, True),
+                                                      (4, 5000, 40, 4000, True, False)])
+def test_nll_loss_rows_kernel_vs_torch(seed, rows, c, n, dup, ignore):
+    """metrics.nll_loss_rows on the GPU (mpgnn_nll_rows_fwd / _bwd) against torch's
+    F.nll_loss(log_softmax(h)[idx], y) (main.py:1062-1066): the loss within a few ulp (summation
+    order), the gradient of the softmax input bit for bit — repeated rows, ignore_index entries
+    and the empty list (NaN loss, zero gradient) included."""
+    h, idx, y = _nll_case(seed, rows, c, n, dup, ignore)
+    dev = torch.device("cuda", 0)
+    hd, idx_d, y_d = h.to(dev), idx.to(dev), y.to(dev)
+    ha = hd.clone().requires_grad_(True)
+    hb = hd.clone().requires_grad_(True)
+    la = metrics.nll_loss_rows(torch.log_softmax(ha, 1), idx_d, y_d)
+    assert la.grad_fn is not None and "NllRows" in type(la.grad_fn).__name__
+    lb = torch.nn.functional.nll_loss(torch.log_softmax(hb, 1).index_select(0, idx_d), y_d)
+    la.backward()
+    lb.backward()
+    if n == 0 or bool((y == -100).all()):
+        assert torch.isnan(la) and torch.isnan(lb)
+    else:
+        assert torch.allclose(la, lb, rtol=4e-7 * max(1.0, n ** 0.5), atol=0), (float(la), float(lb))
+    assert torch.equal(ha.grad, hb.grad)
+    with torch.no_grad():  # the validation loss: forward only, the same launch
+        lv = metrics.nll_loss_rows(torch.log_softmax(hd, 1), idx_d, y_d)
+        assert torch.equal(lv, la.detach()) or bool(torch.isnan(la))
+
+
+@pytest.mark.gpu
+def test_nll_loss_rows_out_of_range_lists_take_torchs_path():
+    """A row or target outside the matrix fails the one-time list check (the call then runs
+    torch's ops, which raise torch's error, instead of the kernels); ignore_index passes."""
+    dev = torch.device("cuda", 0)
+    logp = torch.log_softmax(torch.randn(10, 3, device=dev), 1)
+    idx = torch.tensor([0, 4, 12], device=dev)
+    y = torch.tensor([0, 1, 2], device=dev)
+    assert not metrics._nll_lists_valid(idx, y, 10, 3)
+    assert not metrics._nll_lists_valid(idx[:2], torch.tensor([0, 3], device=dev), 10, 3)
+    assert metrics._nll_lists_valid(idx[:2], torch.tensor([0, -100], device=dev), 10, 3)
+    assert logp.shape == (10, 3)
+
+
+def test_nll_loss_rows_fallback_raises_torchs_errors():
+    if os.environ.get("MPGNN_LIB_PATH", "").endswith("_asan.so"):
+        pytest.skip("a torch C++ exception aborts under the preloaded sanitizer runtime (test_host_sanitizers)")
+    logp = torch.log_softmax(torch.randn(10, 3), 1)
+    with pytest.raises(IndexError):
+        metrics.nll_loss_rows(logp, torch.tensor([0, 4, 12]), torch.tensor([0, 1, 2]))
+    with pytest.raises(IndexError):
+        metrics.nll_loss_rows(logp, torch.tensor([0, 4]), torch.tensor([0, 3]))
+
+
 def test_class_weight_balanced_identical_to_sklearn():
     for seed in range(4):
         y = torch.from_numpy(np.random.default_rng(seed).integers(0, 3 + seed, 97))
