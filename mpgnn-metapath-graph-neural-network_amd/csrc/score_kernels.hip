@@ -482,14 +482,30 @@ __global__ __launch_bounds__(kNllThreads) void nll_rows_fwd_kernel(const float* 
                                                                    int64_t ignore, float* __restrict__ loss,
                                                                    float* __restrict__ total_weight) {
     __shared__ float s_sum[kNllThreads / 64], s_w[kNllThreads / 64];
+    // kNllBatch pairs per thread in flight: the list loads of a batch, then its matrix loads
+    // (two memory round trips per batch instead of two per pair)
+    constexpr int kNllBatch = 8;
     float sum = 0.f, w = 0.f;
-    for (int64_t j = threadIdx.x; j < n; j += kNllThreads) {
-        const int64_t t = tgt[j];
-        if (t == ignore) continue;
-        const int64_t r = idx[j];
-        const bool ok = r >= 0 && r < rows && t >= 0 && t < C;
-        sum += ok ? logp[r * C + t] : __builtin_nanf("");
-        w += 1.f;
+    for (int64_t j0 = 0; j0 < n; j0 += (int64_t)kNllBatch * kNllThreads) {
+        int64_t r[kNllBatch], t[kNllBatch];
+#pragma unroll
+        for (int u = 0; u < kNllBatch; ++u) {
+            const int64_t j = j0 + (int64_t)u * kNllThreads + threadIdx.x;
+            t[u] = j < n ? tgt[j] : ignore;
+            r[u] = j < n ? idx[j] : 0;
+        }
+        float v[kNllBatch];
+#pragma unroll
+        for (int u = 0; u < kNllBatch; ++u) {
+            const bool ok = r[u] >= 0 && r[u] < rows && t[u] >= 0 && t[u] < C;
+            v[u] = ok ? logp[r[u] * C + t[u]] : __builtin_nanf("");
+        }
+#pragma unroll
+        for (int u = 0; u < kNllBatch; ++u)
+            if (t[u] != ignore) {
+                sum += v[u];
+                w += 1.f;
+            }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {

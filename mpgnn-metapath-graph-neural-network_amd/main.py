@@ -200,6 +200,7 @@ def _graphs_enabled(data) -> bool:
 
 
 _LOOP_STREAMS: dict = {}
+LAST_CAPTURE_ERROR = None  # why _epochs' last failed capture fell back to eager epochs
 _LOOP_ACTIVE: set = set()  # devices whose loop stream a running _epochs generator owns
 
 
@@ -244,7 +245,9 @@ def _epochs(epoch_fn, epochs: int, use_graph: bool, warmup: int = 3):
         try:
             with torch.cuda.graph(graph, stream=side):
                 static = epoch_fn()
-        except Exception:  # capture unsupported here: the remaining epochs run eagerly
+        except Exception as exc:  # capture unsupported here: the remaining epochs run eagerly
+            global LAST_CAPTURE_ERROR
+            LAST_CAPTURE_ERROR = f"{type(exc).__name__}: {exc}"
             graph = None
             torch.cuda.synchronize()
         for e in range(warmup + 1, epochs + 1):
