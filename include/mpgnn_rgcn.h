@@ -213,7 +213,7 @@ int32_t mpgnn_confusion_counts(const float* scores, int64_t rows, int32_t num_cl
                                const int64_t* const* row_idx, const int64_t* const* labels, const int64_t* n,
                                int64_t* counts, void* stream);
 
-/* The loops' training loss F.nll_loss(out[train_idx], train_y) (main.py:1062-1066, mean
+/* The loops' training loss F.nll_loss(out[train_idx], train_y) (main.py:1065, mean
  * reduction, no class weights) over log-probabilities logp [rows, num_classes]: pairs j with
  * target[j] == ignore_index are skipped; *total_weight = the kept pairs' count (float);
  * *loss = -(Σ_j logp[row_idx[j], target[j]] / *total_weight) (NaN when nothing is kept, or when

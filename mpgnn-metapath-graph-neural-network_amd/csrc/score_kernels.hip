@@ -464,7 +464,7 @@ __global__ __launch_bounds__(kConfThreads) void confusion_counts_kernel(ConfArgs
 }
 
 // ---------------------------------------------------------------------------------------
-// The training loss of the loops (main.py:1062-1066, ``F.nll_loss(out[train_idx], train_y)``):
+// The training loss of the loops (main.py:1065, main_rgcn.py:402, 422; ``F.nll_loss(out[train_idx], train_y)``):
 // the mean negative log-probability of each listed (row, target) pair, targets equal to
 // ignore_index skipped. Forward: one workgroup sums the picked entries and counts the kept
 // pairs (total_weight, an exact integer count in float as in torch's kernel); loss = -(sum /

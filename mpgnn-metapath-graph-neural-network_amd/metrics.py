@@ -147,8 +147,8 @@ def _nll_lists_valid(idx: torch.Tensor, target: torch.Tensor, rows: int, c: int)
 
 
 def nll_loss_rows(logp: torch.Tensor, idx, target: torch.Tensor) -> torch.Tensor:
-    """``F.nll_loss(logp[idx].squeeze(-1), target)`` — the loops' loss (main.py:1062-1066,
-    1090, 1107; mean over the listed rows, ignore_index -100, no class weights). On the GPU
+    """``F.nll_loss(logp[idx].squeeze(-1), target)`` — the loops' loss (main.py:1065, 1088,
+    1106, main_rgcn.py:402, 422; mean over the listed rows, ignore_index -100, no class weights). On the GPU
     (float32 [rows, C >= 2] log-probabilities, 1-D int64 row and target lists on the same device,
     lists checked in range once) ``mpgnn_nll_rows_fwd`` / ``_bwd``: the same loss up to the
     summation order (a few ulp), the same input gradient bit for bit (tests/test_loop.py).

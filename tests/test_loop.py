@@ -224,7 +224,7 @@ def test_nll_loss_rows_cpu_is_torch():
                                                       (4, 5000, 40, 4000, True, False)])
 def test_nll_loss_rows_kernel_vs_torch(seed, rows, c, n, dup, ignore):
     """metrics.nll_loss_rows on the GPU (mpgnn_nll_rows_fwd / _bwd) against torch's
-    F.nll_loss(log_softmax(h)[idx], y) (main.py:1062-1066): the loss within a few ulp (summation
+    F.nll_loss(log_softmax(h)[idx], y) (main.py:1065, 1088): the loss within a few ulp (summation
     order), the gradient of the softmax input bit for bit — repeated rows, ignore_index entries
     and the empty list (NaN loss, zero gradient) included."""
     h, idx, y = _nll_case(seed, rows, c, n, dup, ignore)
