@@ -233,7 +233,7 @@ int32_t mpgnn_nll_rows_bwd(const float* grad_loss, const float* total_weight, in
  * eager epoch's path): out = act(x @ weightᵀ + bias) with x [N,F], weight [O,F], bias [O]
  * (nullable), act MPGNN_ACT_NONE / _RELU; grad_x = grad_out @ weight ([N,O] @ [O,F]).
  * Supported: F = O = 128 (bf16-split matrix-core GEMM, fp32-level accuracy) and O <= 8 (F <= 256
- * for the forward, F % 4 == 0); other shapes return MPGNN_ERR_UNSUPPORTED (the caller keeps the
+ * for the forward, F % 4 == 0; the forward's dots summed in float64, rounded once); other shapes return MPGNN_ERR_UNSUPPORTED (the caller keeps the
  * library GEMM). Pointers 16-byte aligned. */
 int32_t mpgnn_linear_fwd(const float* x, int64_t N, int32_t F, const float* weight, int32_t O, const float* bias,
                          int32_t act, float* out, void* stream);

@@ -4840,7 +4840,11 @@ __global__ __launch_bounds__(kThreads) void relu_bwd_kernel(const float* g, cons
 
 // The wrappers' Linear heads with few outputs (model.py:147 Net.lin, :226 MPNetm.fc2):
 // out[i][o] = act(Σ_f x[i][f]·W[o][f] + b[o]) for O <= 8, F <= 256 (F % 4 == 0). One wave per row:
-// lane l holds columns 4l..4l+3, the O partial dots are added by a fixed butterfly (deterministic).
+// lane l holds columns 4l..4l+3. The products are exact in float64 and summed there (the lane's
+// four, then a fixed butterfly, then + b), one rounding to fp32 at the end: the logits are the
+// correctly rounded dot to within float64's error — closer to the exact value than any fp32
+// summation order (the library GEMM's included), so the heads' whole-model gradient checks keep
+// their bars. Deterministic; 8·6·2 shuffles per row are noise at one wave per row.
 constexpr int kLinSmallO = 8;
 __global__ __launch_bounds__(kThreads) void linear_small_fwd_kernel(const float* __restrict__ x, int N, int F,
                                                                     const float* __restrict__ W, int O,
@@ -4853,25 +4857,25 @@ __global__ __launch_bounds__(kThreads) void linear_small_fwd_kernel(const float*
 #pragma unroll
     for (int o = 0; o < kLinSmallO; ++o)
         w[o] = (o < O && f < F) ? *reinterpret_cast<const float4*>(W + (size_t)o * F + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const double b = (bias != nullptr && lane < O) ? (double)bias[lane] : 0.0;
     for (int i = (int)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); i < N; i += waves) {
         const float4 xv = f < F ? *reinterpret_cast<const float4*>(x + (size_t)i * F + f) : make_float4(0.f, 0.f, 0.f, 0.f);
-        float acc[kLinSmallO];
+        double v = 0.0;
 #pragma unroll
         for (int o = 0; o < kLinSmallO; ++o) {
-            float t = xv.x * w[o].x;
-            t = fmaf(xv.y, w[o].y, t);
-            t = fmaf(xv.z, w[o].z, t);
-            t = fmaf(xv.w, w[o].w, t);
+            if (o < O) {  // wave-uniform
+                double t = (double)xv.x * (double)w[o].x;
+                t += (double)xv.y * (double)w[o].y;
+                t += (double)xv.z * (double)w[o].z;
+                t += (double)xv.w * (double)w[o].w;
 #pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m);
-            acc[o] = t;
+                for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m);
+                v = lane == o ? t : v;
+            }
         }
         if (lane < O) {
-            float v = 0.0f;
-#pragma unroll
-            for (int o = 0; o < kLinSmallO; ++o) v = lane == o ? acc[o] : v;
-            v = v + (bias != nullptr ? bias[lane] : 0.0f);
-            out[(size_t)i * O + lane] = act == MPGNN_ACT_RELU ? relu_f(v) : v;
+            const float r = (float)(v + b);
+            out[(size_t)i * O + lane] = act == MPGNN_ACT_RELU ? relu_f(r) : r;
         }
     }
 }

@@ -22,6 +22,8 @@ ap.add_argument("--epochs", type=int, default=20)
 ap.add_argument("--top", type=int, default=40)
 ap.add_argument("--ab-adam", action="store_true", help="alternate torch's fused Adam and main.LeanAdam, 3 rounds")
 ap.add_argument("--ab-heads", action="store_true", help="alternate the Linear heads on the C ABI and on torch, 3 rounds")
+ap.add_argument("--ab-small-fwd", action="store_true",
+                help="alternate the narrow heads' (O <= 8) forward on the C ABI and on torch, 3 rounds")
 ap.add_argument("--ab-loss", action="store_true", help="alternate metrics.nll_loss_rows and torch's ops, 3 rounds")
 a = ap.parse_args()
 
@@ -83,10 +85,12 @@ if a.ab_loss:
             rec[k].append(round((time.perf_counter() - t0) * 1e3 / a.epochs, 4))
     print(json.dumps({"workload": a.workload, "mode": a.mode, "epoch_wall_ms": rec}), flush=True)
     sys.exit(0)
-if a.ab_heads:
+if a.ab_heads or a.ab_small_fwd:
     import mpgnn_amd.model as M
     fwd0, dgrad0 = M._head_fwd, M._head_dgrad
     modes = {"abi": (fwd0, dgrad0), "torch": (lambda *_: None, lambda *_: None)}
+    if a.ab_small_fwd:
+        modes["torch"] = (lambda x, w, b, r: None if w.shape[0] <= 8 else fwd0(x, w, b, r), dgrad0)
     opt = mpgnn_amd.main.LeanAdam(list(model.parameters()), lr=0.01, weight_decay=0.0005, fused=True)
     rec = {k: [] for k in modes}
     for _ in range(3):

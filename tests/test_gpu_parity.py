@@ -1269,9 +1269,10 @@ def test_linear_head_gradients_vs_autograd(n, f, o, bias):
 @pytest.mark.parametrize("n,f,o,bias,relu", [(14541, 128, 2, True, False), (333, 64, 5, False, True),
                                              (1000, 256, 8, True, True), (7, 4, 1, True, False)])
 def test_linear_small_head_abi_vs_torch(n, f, o, bias, relu):
-    """mpgnn_linear_fwd / mpgnn_linear_dgrad for heads with O <= 8 through the C ABI directly
-    (model.linear keeps torch's forward for them, see model._head_fwd): act(x @ Wᵀ + b) and
-    g @ W against torch at the suite's bar, the float64 truth deciding."""
+    """mpgnn_linear_fwd / mpgnn_linear_dgrad for heads with O <= 8 through the C ABI directly:
+    act(x @ Wᵀ + b) and g @ W against torch at the suite's bar, the float64 truth deciding; the
+    forward (float64 sums, one rounding) IS the float64 truth rounded to fp32 but for rare
+    near-half-ulp cases."""
     from mpgnn_amd import _lib
     gen = torch.Generator().manual_seed(21)
     x = torch.randn(n, f, generator=gen)
@@ -1292,6 +1293,8 @@ def test_linear_small_head_abi_vs_torch(n, f, o, bias, relu):
         ref, ref64 = torch.relu(ref), torch.relu(ref64)
     rel_close(out, ref, what="small head out", ref64=ref64)
     rel_close(gx, gd @ wd, what="small head dgrad", ref64=go.double() @ w.double())
+    off = int((out.cpu() != ref64.float()).sum())
+    assert off <= max(1, out.numel() // 10000), (off, out.numel())
 
 
 @pytest.mark.parametrize("n,f,o", [(14541, 128, 128), (14541, 128, 2), (333, 64, 5), (1000, 128, 64)])
