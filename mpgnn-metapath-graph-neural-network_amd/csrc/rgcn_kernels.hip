@@ -4839,43 +4839,52 @@ __global__ __launch_bounds__(kThreads) void relu_bwd_kernel(const float* g, cons
 }
 
 // The wrappers' Linear heads with few outputs (model.py:147 Net.lin, :226 MPNetm.fc2):
-// out[i][o] = act(Σ_f x[i][f]·W[o][f] + b[o]) for O <= 8, F <= 256 (F % 4 == 0). One wave per row:
-// lane l holds columns 4l..4l+3. The products are exact in float64 and summed there (the lane's
-// four, then a fixed butterfly, then + b), one rounding to fp32 at the end: the logits are the
-// correctly rounded dot to within float64's error — closer to the exact value than any fp32
-// summation order (the library GEMM's included), so the heads' whole-model gradient checks keep
-// their bars. Deterministic; 8·6·2 shuffles per row are noise at one wave per row.
+// out[i][o] = act(Σ_f x[i][f]·W[o][f] + b[o]) for O <= 8, F <= 256 (F % 4 == 0). Four rows per
+// wave, 16 lanes per row: lane s of a row holds columns 4s + 64k (k < F/64, rounded up). The
+// products are exact in float64 and summed there (the lane's, then a fixed 16-lane butterfly,
+// then + b), one rounding to fp32 at the end: the logits are the correctly rounded dot to within
+// float64's error — closer to the exact value than any fp32 summation order (the library GEMM's
+// included), so the heads' whole-model gradient checks keep their bars. Deterministic. W (<= 8
+// KB) is re-read per row group from L1.
 constexpr int kLinSmallO = 8;
 __global__ __launch_bounds__(kThreads) void linear_small_fwd_kernel(const float* __restrict__ x, int N, int F,
                                                                     const float* __restrict__ W, int O,
                                                                     const float* __restrict__ bias, int act,
                                                                     float* __restrict__ out) {
     const int lane = threadIdx.x & 63;
-    const int waves = (int)gridDim.x * (kThreads / 64);
-    const int f = 4 * lane;
-    float4 w[kLinSmallO];
+    const int sub = lane & 15, q = lane >> 4;
+    const int groups = (int)gridDim.x * (kThreads / 64);  // 4 rows each
+    const double b = (bias != nullptr && sub < O) ? (double)bias[sub] : 0.0;
+    for (int i0 = ((int)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * 4; i0 < N; i0 += groups * 4) {
+        const int i = i0 + q;
+        float4 xv[4];
 #pragma unroll
-    for (int o = 0; o < kLinSmallO; ++o)
-        w[o] = (o < O && f < F) ? *reinterpret_cast<const float4*>(W + (size_t)o * F + f) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const double b = (bias != nullptr && lane < O) ? (double)bias[lane] : 0.0;
-    for (int i = (int)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); i < N; i += waves) {
-        const float4 xv = f < F ? *reinterpret_cast<const float4*>(x + (size_t)i * F + f) : make_float4(0.f, 0.f, 0.f, 0.f);
-        double v = 0.0;
-#pragma unroll
-        for (int o = 0; o < kLinSmallO; ++o) {
-            if (o < O) {  // wave-uniform
-                double t = (double)xv.x * (double)w[o].x;
-                t += (double)xv.y * (double)w[o].y;
-                t += (double)xv.z * (double)w[o].z;
-                t += (double)xv.w * (double)w[o].w;
-#pragma unroll
-                for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m);
-                v = lane == o ? t : v;
-            }
+        for (int k = 0; k < 4; ++k) {
+            const int f = 4 * sub + 64 * k;
+            xv[k] = (i < N && f < F) ? *reinterpret_cast<const float4*>(x + (size_t)i * F + f)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        if (lane < O) {
+        double v = 0.0;
+        for (int o = 0; o < O; ++o) {  // wave-uniform
+            double t = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int f = 4 * sub + 64 * k;
+                if (f < F) {
+                    const float4 wv = *reinterpret_cast<const float4*>(W + (size_t)o * F + f);
+                    t += (double)xv[k].x * (double)wv.x;
+                    t += (double)xv[k].y * (double)wv.y;
+                    t += (double)xv[k].z * (double)wv.z;
+                    t += (double)xv[k].w * (double)wv.w;
+                }
+            }
+#pragma unroll
+            for (int m = 8; m >= 1; m >>= 1) t += __shfl_xor(t, m);  // within the row's 16 lanes
+            v = sub == o ? t : v;
+        }
+        if (i < N && sub < O) {
             const float r = (float)(v + b);
-            out[(size_t)i * O + lane] = act == MPGNN_ACT_RELU ? relu_f(r) : r;
+            out[(size_t)i * O + sub] = act == MPGNN_ACT_RELU ? relu_f(r) : r;
         }
     }
 }
@@ -6222,7 +6231,7 @@ int32_t mpgnn_linear_fwd(const float* x, int64_t N, int32_t F, const float* weig
         hipLaunchKernelGGL(bias_act_kernel, dim3(linear_grid(n4)), dim3(kThreads), 0, strm, out, n4, 32, bias, act);
         return hip_check(hipGetLastError(), "bias_act_kernel launch");
     }
-    const int grid = (int)std::min<int64_t>(8 * (int64_t)cu_count(), (N + 3) / 4);
+    const int grid = (int)std::min<int64_t>(8 * (int64_t)cu_count(), (N + 15) / 16);  // 16 rows per workgroup
     hipLaunchKernelGGL(linear_small_fwd_kernel, dim3(grid), dim3(kThreads), 0, strm, x, (int)N, F, weight, O, bias, act, out);
     return hip_check(hipGetLastError(), "linear_small_fwd_kernel launch");
 }
