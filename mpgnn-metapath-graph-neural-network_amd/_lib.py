@@ -204,7 +204,8 @@ def set_option(option: int, value: int) -> None:
 
 
 def set_exact_order(on: bool) -> None:
-    """Force reference-sequential summation order everywhere (see include/mpgnn_rgcn.h)."""
+    """Process default of the reference-sequential summation order: applies to plans created
+    afterwards (``GraphPlan.set_exact_order`` switches one existing plan; see include/mpgnn_rgcn.h)."""
     check(lib.mpgnn_set_option(OPT_EXACT_ORDER, 1 if on else 0), "mpgnn_set_option")
 
 

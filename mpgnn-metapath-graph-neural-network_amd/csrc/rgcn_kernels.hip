@@ -5191,8 +5191,8 @@ static void launch_rel_gemm_bf3w(const RelGemmArgs& a, bool il, hipStream_t st) 
 // one exposed weight-slice load per run it holds), followed by every item's weight index (the
 // relation value of its tiles, -1 for root items) so that the kernel's item table needs no
 // dependent s_rel load. Cached per plan; made outside captures (nullptr: the kernel's equal split
-// and s_rel lookups). Uploaded with an asynchronous copy on the caller's stream from a pinned
-// buffer the plan keeps (no device-wide synchronisation, ordered before the kernel reading it).
+// and s_rel lookups). Uploaded on the caller's stream from a pinned buffer the plan keeps and
+// published in the cache only after that stream has drained the copy (once per key).
 static const int* gemm_ranges(const mpgnn_plan* p, int t_lo, int n_rel, int n_root, int G, bool pairs,
                               hipStream_t st) {
     const int cost = p->opt.gemm_switch_cost;
@@ -5257,7 +5257,10 @@ static const int* gemm_ranges(const mpgnn_plan* p, int t_lo, int n_rel, int n_ro
         (void)hipHostFree(e.host);
         return nullptr;
     }
-    if (hipMemcpyAsync(e.dev, e.host, words * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
+    // published only once complete: a later launch on another stream that hits the cache must not
+    // read the table before the copy lands (once per plan and key, outside captures)
+    if (hipMemcpyAsync(e.dev, e.host, words * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
         (void)hipGetLastError();
         (void)hipFree(e.dev);
         (void)hipHostFree(e.host);
@@ -5325,7 +5328,8 @@ static const int* outer_ranges(const mpgnn_plan* p, int c_lo, int nch, int row_l
     }
     tab[G] = pos;
     if (hipMalloc(reinterpret_cast<void**>(&e.dev), words * sizeof(int)) != hipSuccess ||
-        hipMemcpyAsync(e.dev, e.host, words * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
+        hipMemcpyAsync(e.dev, e.host, words * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {  // published only once complete (as gemm_ranges)
         (void)hipGetLastError();
         if (e.dev) (void)hipFree(e.dev);
         (void)hipHostFree(e.host);

@@ -26,6 +26,7 @@ namespace {
 
 constexpr int kScoreThreads = 256;
 constexpr int kMaxConfLists = 4;
+constexpr int kMaxConfClasses = 4096;
 
 int32_t hip_status(hipError_t e, const char* what) {
     if (e == hipSuccess) return MPGNN_OK;
@@ -677,8 +678,10 @@ extern "C" int32_t mpgnn_score_argmax_multi_bwd(const float* grad_values, const 
 extern "C" int32_t mpgnn_confusion_counts(const float* scores, int64_t rows, int32_t num_classes, int32_t n_lists,
                                           const int64_t* const* row_idx, const int64_t* const* labels,
                                           const int64_t* n, int64_t* counts, void* stream) {
-    if (rows < 0 || num_classes <= 0 || num_classes > 8192 || n_lists < 0 || n_lists > kMaxConfLists)
-        return arg_fail("mpgnn_confusion_counts: bad sizes (1 <= num_classes <= 8192, 0 <= n_lists <= 4)");
+    // 3·(C + 1) int32 LDS histograms: C <= 4096 keeps them under the 64 KB a launch gets without
+    // an opt-in attribute
+    if (rows < 0 || num_classes <= 0 || num_classes > kMaxConfClasses || n_lists < 0 || n_lists > kMaxConfLists)
+        return arg_fail("mpgnn_confusion_counts: bad sizes (1 <= num_classes <= 4096, 0 <= n_lists <= 4)");
     if (n_lists == 0) return MPGNN_OK;
     if (!counts || !labels || !n) return arg_fail("mpgnn_confusion_counts: NULL argument");
     ConfArgs a{};

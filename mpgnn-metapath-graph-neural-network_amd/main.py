@@ -152,7 +152,8 @@ class LeanAdam(torch.optim.Adam):
     @torch.no_grad()
     def step(self, closure=None):
         lists = None if closure is not None else self._lean_lists()
-        if lists is None:
+        # AMP: GradScaler sets grad_scale / found_inf on the optimizer; torch's step reads them
+        if lists is None or getattr(self, "grad_scale", None) is not None or getattr(self, "found_inf", None) is not None:
             return self._torch_step(closure)
         params, exp_avgs, exp_avg_sqs, steps = lists
         grads = [p.grad for p in params]

@@ -64,6 +64,25 @@ def confusion_counts_many(pairs: list[tuple[torch.Tensor, torch.Tensor]], num_cl
     return torch.stack([_confusion_counts(p, y, num_classes) for p, y in pairs])
 
 
+_ROWS_OK: list = []  # (weakref(idx), idx._version, rows) of row lists found in range
+
+
+def _rows_valid(idx: torch.Tensor, rows: int) -> bool:
+    """Every entry of ``idx`` in [0, rows), checked once per list object and version (a list with
+    an out-of-range row goes to torch's ops, whose ``scores[idx]`` raises like the reference's
+    ``pred[idx]``). Not checked during a capture (no host read): the torch path runs instead."""
+    for ri, vi, r in _ROWS_OK:
+        if ri() is idx and vi == idx._version and r == rows:
+            return True
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    ok = idx.numel() == 0 or bool(((idx >= 0) & (idx < rows)).all().item())
+    if ok:
+        _ROWS_OK.insert(0, (weakref.ref(idx), idx._version, rows))
+        del _ROWS_OK[16:]
+    return ok
+
+
 def confusion_counts_rows(scores: torch.Tensor, lists) -> torch.Tensor:
     """``confusion_counts_many([(torch.argmax(scores[idx], 1), y) for idx, y in lists], C)`` with
     C = scores.shape[1]: [len(lists), 3, C] int64 on the device. On the GPU (float32 scores,
@@ -71,10 +90,11 @@ def confusion_counts_rows(scores: torch.Tensor, lists) -> torch.Tensor:
     each listed row + LDS histograms) instead of ~20 torch ops per list; same counts."""
     lists = list(lists)
     ok = (scores.is_cuda and scores.dim() == 2 and scores.dtype == torch.float32 and 0 < len(lists) <= 4
-          and 1 <= scores.shape[1] <= 8192
+          and 1 <= scores.shape[1] <= 4096  # the kernel's LDS histograms (mpgnn_confusion_counts)
           and all(torch.is_tensor(i) and i.dim() == 1 and i.dtype in (torch.int64, torch.int32) and
                   torch.is_tensor(y) and y.numel() == i.numel() and not y.is_floating_point()
-                  for i, y in lists))
+                  for i, y in lists)
+          and all(_rows_valid(i, scores.shape[0]) for i, _ in lists))
     if not ok:
         return confusion_counts_many([(torch.argmax(scores[i], 1), y) for i, y in lists], _num_cols(scores))
     import ctypes

@@ -25,7 +25,7 @@ plan = GraphPlan(g.edge_index, g.edge_type, N)
 
 def run(dev, exact=False, fused=True):
     if dev == "cuda":
-        _lib.set_exact_order(exact)
+        plan.set_exact_order(exact)  # the switch is per plan
     p = {k: (v.double() if dev == "cpu" else v.to(dev)).requires_grad_(True) for k, v in sd.items()}
     h = g.x.double() if dev == "cpu" else g.x.to(dev)
     acts = []
