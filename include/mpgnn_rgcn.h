@@ -440,7 +440,12 @@ enum mpgnn_option {
                                     next item's tile in four parts among the k-steps' MFMAs (as GEMM_IL at
                                     K = 128; round-5 A/B at C5: forward 26.2 -> 23.9 ms, dgrad 25.6 -> 23.2 ms,
                                     mode SINGLE 2.31 -> 1.87 ms per layer); 0: the whole tile in one k-step;
-                                    outputs bit-identical */
+                                    outputs bit-identical */,
+    MPGNN_OPT_GEMM_W1 = 35       /* the bf16-split GEMM at K = N = 128 (transform and dgrad): 1 runs
+                                    rel_gemm_w1_kernel (one workgroup per CU, one wave per SIMD, 64-row items,
+                                    the next relation's weight slice prefetched into a second register set);
+                                    0 rel_gemm_bf3_kernel (two workgroups per CU, 32-row items); outputs
+                                    bit-identical */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

@@ -2026,6 +2026,272 @@ __global__ __launch_bounds__(kThreads, 2) void rel_gemm_bf3_kernel(RelGemmArgs a
 }
 
 // ----------------------------------------------------------------------------------------
+// rel_gemm_w1_kernel — the bf16-split GEMM of rel_gemm_bf3_kernel (K = N = 128: the same
+// items' products, the same MFMA instruction, k-step order and six-product order, so the same
+// bits) with ONE workgroup per CU: one wave per SIMD owning the whole 512-entry register file.
+// What that buys over two workgroups of 32-row items:
+//   * 64-row items (two 32-row sub-tiles of one relation, or 64 node rows): one barrier, one
+//     epilogue hand-off and one item-table step per 64 rows, 96 MFMAs per wave per item;
+//   * the next relation's weight slice loaded into a second register set at the top of the item
+//     before the switch (its latency hidden by that item's chain) and split after the chain —
+//     rel_gemm_bf3_kernel's registers held one slice, so each switch exposed a slice load
+//     (stamped: ~85 % of an item);
+//   * half the launch's load storm (256 workgroups fetch their first slice and rows, not 512).
+// Item table (gemm_w1_items, host-built per plan): [G + 1] first item of each workgroup's
+// range (XCD-contiguous ranges, balanced by sub-tiles), then per item {r0, nrows, weight index
+// (-1: root)}. Rows are gathered two items ahead, the next item's tile is committed to the other
+// LDS buffer inside the k-steps (one float4 part per k-step), the previous item's outputs are
+// stored inside the next item's chain — rel_gemm_bf3_kernel's pipeline at twice the rows.
+// ----------------------------------------------------------------------------------------
+template <bool DGRAD>
+struct RelGemmW1 {
+    static constexpr int K = 128;
+    static constexpr int N = 128;
+    static constexpr int NS = K / 16;              // k-steps
+    static constexpr int LDAB = K + 8;             // bf16 row stride of an A plane (conflict-free b128 reads)
+    static constexpr int ROWS = 64;                // rows per item
+    static constexpr int PLANE = ROWS * LDAB;      // bf16 per plane
+    static constexpr int WPT = ROWS * (K / 4) / kThreads;  // 8 float4 of an A tile per thread
+    static constexpr int W4 = K / 4;
+
+    static constexpr size_t lds_bytes() { return (size_t)2 * 3 * PLANE * 2 + 2 * ROWS * sizeof(float); }
+
+    struct Item {
+        int r0, nrows, root;
+        const float* w;
+    };
+    __device__ static __forceinline__ Item item(const RelGemmArgs& a, int i, int G) {
+        const int* t = a.wg_items + G + 1 + 3 * i;
+        Item it;
+        it.r0 = ld_uniform(t, 0);
+        it.nrows = ld_uniform(t, 1);
+        const int wr = ld_uniform(t, 2);
+        it.root = wr < 0;
+        it.w = it.root ? a.Wroot : a.W + (size_t)wr * K * N;
+        return it;
+    }
+    // row of thread part j: (tid >> 5) + 8 j; forward A row = s_src (x row, or compact mean row
+    // -(v+1)), dgrad = dout row s_row (scaled 1 / cnt at the output); root items: the node row
+    __device__ static __forceinline__ void gather_idx(const RelGemmArgs& a, const Item& it, int tid, int (&row)[WPT],
+                                                      int& cnt) {
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) row[j] = it.r0 + min((tid >> 5) + 8 * j, it.nrows - 1);
+        cnt = 1;
+        if (!it.root) {
+            if constexpr (DGRAD) {
+                cnt = a.s_cnt[it.r0 + min(tid & 63, it.nrows - 1)];
+#pragma unroll
+                for (int j = 0; j < WPT; ++j) row[j] = a.s_row[row[j]];
+            } else {
+#pragma unroll
+                for (int j = 0; j < WPT; ++j) row[j] = a.s_src[row[j]];
+            }
+        }
+    }
+    __device__ static __forceinline__ void issue_rows(const RelGemmArgs& a, int tid, const int (&row)[WPT],
+                                                      float4 (&v)[WPT]) {
+        const int c4 = (tid & 31) * 4;
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+            const float* base;
+            if constexpr (DGRAD) base = a.Aroot + (size_t)row[j] * K;
+            else base = row[j] >= 0 ? a.Aroot + (size_t)row[j] * K : a.Arel + (size_t)(-row[j] - 1 - a.m_lo) * K;
+            v[j] = *reinterpret_cast<const float4*>(base + c4);
+        }
+    }
+    __device__ static __forceinline__ void commit_part(int j, int tid, int nrows, const float4& v, __bf16* A) {
+        const int r = (tid >> 5) + 8 * j;
+        const float4 x = r < nrows ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+        __bf16 p0[4], p1[4], p2[4];
+        split3_bf16(x.x, p0[0], p1[0], p2[0]);
+        split3_bf16(x.y, p0[1], p1[1], p2[1]);
+        split3_bf16(x.z, p0[2], p1[2], p2[2]);
+        split3_bf16(x.w, p0[3], p1[3], p2[3]);
+        __bf16* d = A + r * LDAB + (tid & 31) * 4;
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<bf16x4*>(d) = bf16x4{p0[0], p0[1], p0[2], p0[3]};
+        *reinterpret_cast<bf16x4*>(d + PLANE) = bf16x4{p1[0], p1[1], p1[2], p1[3]};
+        *reinterpret_cast<bf16x4*>(d + 2 * PLANE) = bf16x4{p2[0], p2[1], p2[2], p2[3]};
+    }
+    __device__ static __forceinline__ void commit(int tid, int nrows, const float4 (&v)[WPT], __bf16* A) {
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) commit_part(j, tid, nrows, v[j], A);
+    }
+    // the wave's weight slice (raw fp32): f[s][j] = B(16s + 8h + j, 32·wave + c)
+    __device__ static __forceinline__ void load_b_raw(const float* w, int wave, int lane, float (&f)[NS][8]) {
+        RelGemmBf3<2, DGRAD>::load_b_raw(w, wave, lane, f);
+    }
+    __device__ static __forceinline__ void split_b(const float (&f)[NS][8], bf16x8 (&b)[NS][3]) {
+        RelGemmBf3<2, DGRAD>::split_b(f, b);
+    }
+
+    __device__ static void run(const RelGemmArgs& a, __bf16* smem) {
+        __bf16* As = smem;                                            // [2][3 planes][64][LDAB]
+        float* Sc = reinterpret_cast<float*>(smem + 2 * 3 * PLANE);  // [2][64] dgrad row scales
+        const int tid = threadIdx.x;
+        const int lane = tid & 63, c = lane & 31, h = lane >> 5;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int G = (int)gridDim.x;
+        const int rng = ((int)blockIdx.x & 7) * (G >> 3) + ((int)blockIdx.x >> 3);  // XCD-contiguous ranges
+        const int i_beg = ld_uniform(a.wg_items, rng);
+        const int i_end = ld_uniform(a.wg_items, rng + 1);
+        if (i_beg >= i_end) return;
+
+        Item cur = item(a, i_beg, G);
+        float4 va[WPT], vb[WPT];
+        int cnta = 1, cntb = 1;
+        int nrow[WPT];
+        int ncnt = 1;
+        {
+            int crow[WPT], c0, r1[WPT];
+            gather_idx(a, cur, tid, crow, c0);
+            gather_idx(a, item(a, min(i_beg + 1, i_end - 1), G), tid, r1, cnta);
+            gather_idx(a, item(a, min(i_beg + 2, i_end - 1), G), tid, nrow, ncnt);
+            float wf[NS][8];
+            load_b_raw(cur.w, wave, lane, wf);
+            issue_rows(a, tid, crow, vb);
+            issue_rows(a, tid, r1, va);
+            bf16x8 b0[NS][3];
+            split_b(wf, b0);
+            commit(tid, cur.nrows, vb, As);
+            if constexpr (DGRAD) {
+                if (tid < ROWS) Sc[tid] = 1.0f / (float)c0;
+            }
+            __syncthreads();
+            run_items(a, As, Sc, tid, lane, c, h, wave, G, i_beg, i_end, cur, va, vb, cnta, cntb, nrow, ncnt, b0);
+        }
+    }
+
+    __device__ static __forceinline__ void run_items(const RelGemmArgs& a, __bf16* As, float* Sc, int tid, int lane,
+                                                     int c, int h, int wave, int G, int i_beg, int i_end, Item cur,
+                                                     float4 (&va)[WPT], float4 (&vb)[WPT], int& cnta, int& cntb,
+                                                     int (&nrow)[WPT], int& ncnt, bf16x8 (&b)[NS][3]) {
+        constexpr int SPG = (32 + NS - 1) / NS;  // previous item's stores per k-step (2 sub-tiles × 16)
+        const int col_b = (wave * 32 + c) * 4 + h * (4 * N * 4);
+        float prev[2][16];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) prev[u][r] = 0.0f;
+        __amdgpu_buffer_rsrc_t prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.Y, (short)0, 0, 0x00020000);
+        float wf[NS][8];  // the next relation's slice, raw (loaded one item ahead of its first use)
+        int buf = 0;
+        auto step = [&](int i, float4 (&vc)[WPT], int& cntc, float4 (&vn)[WPT], int& cntn) {
+            const bool has_next = i + 1 < i_end;
+            const Item nxt = has_next ? item(a, i + 1, G) : cur;
+            {  // unconditional (past the range: the last item's rows again)
+                issue_rows(a, tid, nrow, vn);
+                cntn = ncnt;
+                gather_idx(a, item(a, min(i + 3, i_end - 1), G), tid, nrow, ncnt);
+            }
+            const bool new_w = nxt.w != cur.w;
+            if (new_w) load_b_raw(nxt.w, wave, lane, wf);
+            const int nr = has_next ? nxt.nrows : 0;
+            const __bf16* Ab = As + buf * 3 * PLANE + c * LDAB + 8 * h;
+            __bf16* An = As + (buf ^ 1) * 3 * PLANE;
+            if constexpr (DGRAD) {
+                if (tid < ROWS) Sc[(buf ^ 1) * ROWS + tid] = 1.0f / (float)cntc;
+            }
+            f32x16 hi0, lo0, hi1, lo1;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                hi0[r] = 0.0f;
+                lo0[r] = 0.0f;
+                hi1[r] = 0.0f;
+                lo1[r] = 0.0f;
+            }
+            bf16x8 f0 = *reinterpret_cast<const bf16x8*>(Ab);
+            bf16x8 f1 = *reinterpret_cast<const bf16x8*>(Ab + PLANE);
+            bf16x8 f2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * PLANE);
+            bf16x8 g0 = *reinterpret_cast<const bf16x8*>(Ab + 32 * LDAB);
+            bf16x8 g1 = *reinterpret_cast<const bf16x8*>(Ab + PLANE + 32 * LDAB);
+            bf16x8 g2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * PLANE + 32 * LDAB);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const bf16x8 a0 = f0, a1 = f1, a2 = f2, e0 = g0, e1 = g1, e2 = g2;
+                if (s + 1 < NS) {
+                    f0 = *reinterpret_cast<const bf16x8*>(Ab + 16 * (s + 1));
+                    f1 = *reinterpret_cast<const bf16x8*>(Ab + PLANE + 16 * (s + 1));
+                    f2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * PLANE + 16 * (s + 1));
+                    g0 = *reinterpret_cast<const bf16x8*>(Ab + 32 * LDAB + 16 * (s + 1));
+                    g1 = *reinterpret_cast<const bf16x8*>(Ab + PLANE + 32 * LDAB + 16 * (s + 1));
+                    g2 = *reinterpret_cast<const bf16x8*>(Ab + 2 * PLANE + 32 * LDAB + 16 * (s + 1));
+                }
+                lo0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[s][0], lo0, 0, 0, 0);
+                lo1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(e2, b[s][0], lo1, 0, 0, 0);
+                lo0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][1], lo0, 0, 0, 0);
+                lo1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(e1, b[s][1], lo1, 0, 0, 0);
+                lo0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][2], lo0, 0, 0, 0);
+                lo1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(e0, b[s][2], lo1, 0, 0, 0);
+                lo0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[s][0], lo0, 0, 0, 0);
+                lo1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(e1, b[s][0], lo1, 0, 0, 0);
+                lo0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][1], lo0, 0, 0, 0);
+                lo1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(e0, b[s][1], lo1, 0, 0, 0);
+                hi0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[s][0], hi0, 0, 0, 0);
+                hi1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(e0, b[s][0], hi1, 0, 0, 0);
+#pragma unroll
+                for (int v = 0; v < SPG; ++v) {
+                    const int q = s * SPG + v;  // 0..31: sub-tile q >> 4, register q & 15
+                    if (q < 32) {
+                        const int u = q >> 4, r = q & 15;
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(prev[u][r]), prev_rsrc, col_b,
+                                                              (32 * u + (r & 3) + 8 * (r >> 2)) * (N * 4), 16);
+                    }
+                }
+                // part j of the next tile in k-step j (WPT == NS)
+                commit_part(s, tid, nr, vc[s], An);
+                if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);  // next fragments
+#pragma unroll
+                for (int m = 0; m < 12; ++m) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);             // one MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);             // VALU
+                    if (m < 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // LDS write
+                    if (m < SPG) __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);  // store
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                prev[0][r] = hi0[r] + lo0[r];
+                prev[1][r] = hi1[r] + lo1[r];
+                if constexpr (DGRAD) {
+                    if (!cur.root) {
+                        prev[0][r] = prev[0][r] * Sc[buf * ROWS + (r & 3) + 8 * (r >> 2) + 4 * h];
+                        prev[1][r] = prev[1][r] * Sc[buf * ROWS + 32 + (r & 3) + 8 * (r >> 2) + 4 * h];
+                    }
+                }
+            }
+            {
+                float* Yt = cur.root ? a.Yroot + (size_t)(cur.r0 - a.row_lo) * N : a.Y + (size_t)(cur.r0 - a.sel_b) * N;
+                const int bytes = __builtin_amdgcn_readfirstlane(cur.nrows) * N * 4;
+                prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(Yt, (short)0, bytes, 0x00020000);
+            }
+            if (new_w) split_b(wf, b);
+            __syncthreads();
+            cur = nxt;
+            buf ^= 1;
+        };
+        for (int i = i_beg; i < i_end; i += 2) {
+            step(i, va, cnta, vb, cntb);
+            if (i + 1 < i_end) step(i + 1, vb, cntb, va, cnta);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(prev[u][r]), prev_rsrc, col_b,
+                                                      (32 * u + (r & 3) + 8 * (r >> 2)) * (N * 4), 16);
+    }
+};
+
+template <bool DGRAD>
+__global__ __launch_bounds__(kThreads, 1) void rel_gemm_w1_kernel(RelGemmArgs a) {
+    extern __shared__ __bf16 smem_bf[];
+    RelGemmW1<DGRAD>::run(a, smem_bf);
+}
+
+// ----------------------------------------------------------------------------------------
 // single_bf3_kernel — the whole unsharded mode-SINGLE layer (CustomRGCNConv over one relation,
 // mp_rgcn_layer.py:231-268, + the model's ReLU) in one launch on the bf16 matrix cores:
 //     out[i] = act((mean_i @ W + x_i @ root) + bias)      mean_i = 0 without a segment
@@ -5270,6 +5536,75 @@ static const int* gemm_ranges(const mpgnn_plan* p, int t_lo, int n_rel, int n_ro
     return e.dev;
 }
 
+// rel_gemm_w1_kernel's item table: the selection's 32-row tiles paired into 64-row items (two
+// consecutive tiles of one relation; a relation's odd last tile alone), then the node rows
+// [row_lo, row_hi) in 64-row root items; G contiguous ranges balanced by cost = sub-tiles + c per
+// weight switch. Layout: [G + 1] first item per range, then {r0, nrows, weight index | -1} per
+// item. Cached per plan like gemm_ranges (made outside captures; nullptr: no table).
+static const int* gemm_w1_items(const mpgnn_plan* p, int t_lo, int n_rel, int row_lo, int row_hi, bool root, int G,
+                                hipStream_t st) {
+    if (G <= 0) return nullptr;
+    const int cost = std::max(p->opt.gemm_switch_cost, 0);
+    const std::array<int64_t, 5> key{t_lo, n_rel, (int64_t)row_lo * 2 + (root ? 1 : 0), -(int64_t)G - 1, (int64_t)row_hi * 1024 + cost};
+    std::lock_guard<std::mutex> lk(p->bw_mu);
+    auto it = p->gemm_ranges.find(key);
+    if (it != p->gemm_ranges.end()) return it->second.dev;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    if ((int64_t)p->t32_begin.size() < (int64_t)t_lo + n_rel) return nullptr;
+    std::vector<int> items;  // r0, nrows, w triplets
+    int d = (int)(std::upper_bound(p->rel_t32_ptr.begin(), p->rel_t32_ptr.end(), t_lo) - p->rel_t32_ptr.begin()) - 1;
+    for (int t = t_lo; t < t_lo + n_rel;) {
+        while (d + 1 < (int)p->rel_t32_ptr.size() && p->rel_t32_ptr[d + 1] <= t) ++d;
+        const int w = (d >= 0 && d < (int)p->rel_val32.size()) ? p->rel_val32[d] : 0;
+        const bool pair = t + 1 < t_lo + n_rel && d + 1 < (int)p->rel_t32_ptr.size() && t + 1 < p->rel_t32_ptr[d + 1];
+        const int r0 = p->t32_begin[t];
+        const int r1 = pair ? p->t32_end[t + 1] : p->t32_end[t];
+        items.push_back(r0);
+        items.push_back(r1 - r0);
+        items.push_back(w);
+        t += pair ? 2 : 1;
+    }
+    if (root)
+        for (int r0 = row_lo; r0 < row_hi; r0 += 64) {
+            items.push_back(r0);
+            items.push_back(std::min(64, row_hi - r0));
+            items.push_back(-1);
+        }
+    const int n = (int)items.size() / 3;
+    std::vector<double> cum(n + 1, 0.0);
+    for (int i = 0; i < n; ++i) {
+        const bool sw = i == 0 || items[3 * i + 2] != items[3 * i - 1];
+        cum[i + 1] = cum[i] + (items[3 * i + 1] > 32 ? 2.0 : 1.0) + (sw ? cost / 100.0 : 0.0);
+    }
+    const size_t words = (size_t)G + 1 + (size_t)n * 3;
+    mpgnn_plan::GemmRanges e;
+    if (hipHostMalloc(reinterpret_cast<void**>(&e.host), words * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    int* tab = e.host;
+    tab[0] = 0;
+    int i = 0;
+    for (int k = 1; k < G; ++k) {
+        const double target = cum[n] * k / G;
+        while (i < n && cum[i] < target) ++i;
+        tab[k] = std::max(tab[k - 1], i);
+    }
+    tab[G] = n;
+    std::copy(items.begin(), items.end(), tab + G + 1);
+    if (hipMalloc(reinterpret_cast<void**>(&e.dev), words * sizeof(int)) != hipSuccess ||
+        hipMemcpyAsync(e.dev, e.host, words * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {  // published only once complete
+        (void)hipGetLastError();
+        if (e.dev) (void)hipFree(e.dev);
+        (void)hipHostFree(e.host);
+        return nullptr;
+    }
+    p->gemm_ranges[key] = e;
+    return e.dev;
+}
+
 // outer_bf3v_kernel_t's chunk lists per workgroup. The chunks are dealt in windows of G
 // consecutive chunks (as round robin: every workgroup works in the same window at a time, so the
 // rows gathered concurrently stay a narrow slice of the relation-major order — contiguous ranges
@@ -5605,6 +5940,19 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
 #ifdef MPGNN_STAMPS
         r.stamps = gather_kind == 1 ? nullptr : g_stamps_host;
 #endif
+        if (p->opt.gemm_bf3 && p->opt.gemm_w1 && K == 128 && r.node_map == nullptr && cu_count() % 8 == 0) {
+            // one workgroup per CU, 64-row items (rel_gemm_w1_kernel)
+            const int G = cu_count();
+            r.wg_items = gemm_w1_items(p, r.t_lo, r.n_rel, r.row_lo, r.row_hi, Wroot != nullptr, G, strm);
+            if (r.wg_items != nullptr) {
+                TimedLaunch tl(kind, strm);
+                if (gather_kind == 1)
+                    hipLaunchKernelGGL(rel_gemm_w1_kernel<true>, dim3(G), dim3(kThreads), RelGemmW1<true>::lds_bytes(), strm, r);
+                else
+                    hipLaunchKernelGGL(rel_gemm_w1_kernel<false>, dim3(G), dim3(kThreads), RelGemmW1<false>::lds_bytes(), strm, r);
+                return hip_check(hipGetLastError(), "rel_gemm_w1_kernel launch");
+            }
+        }
         if (p->opt.gemm_bf3 && (K == 64 || K == 128) && r.node_map == nullptr) {
             const int G = std::min(r.n_rel + r.n_root, cu_count() * 2);
             const bool pairs = p->opt.gemm_cu_pairs && G == cu_count() * 2 && cu_count() % 8 == 0;
@@ -6339,6 +6687,7 @@ static int32_t set_switch(Options& o, int32_t option, int64_t value) {
         case MPGNN_OPT_OUTER_SQ: o.outer_sq = value != 0; return MPGNN_OK;
         case MPGNN_OPT_OUTER_RANGES: o.outer_ranges = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_W_IL: o.gemm_w_il = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_GEMM_W1: o.gemm_w1 = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_SWITCH_COST:
             if (value < 0 || value > 10000) return arg_error("MPGNN_OPT_GEMM_SWITCH_COST must be 0..10000 (percent of an item)");
             o.gemm_switch_cost = (int)value;
@@ -6364,6 +6713,7 @@ static bool get_switch(const Options& o, int32_t option, int64_t* value) {
         case MPGNN_OPT_OUTER_SQ: *value = o.outer_sq; return true;
         case MPGNN_OPT_OUTER_RANGES: *value = o.outer_ranges; return true;
         case MPGNN_OPT_GEMM_W_IL: *value = o.gemm_w_il; return true;
+        case MPGNN_OPT_GEMM_W1: *value = o.gemm_w1; return true;
         case MPGNN_OPT_GEMM_SWITCH_COST: *value = o.gemm_switch_cost; return true;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = o.flat_wg_per_cu; return true;
         default: return false;
