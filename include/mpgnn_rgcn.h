@@ -445,7 +445,10 @@ enum mpgnn_option {
                                     rel_gemm_w1_kernel (one workgroup per CU, one wave per SIMD, 64-row items,
                                     the next relation's weight slice prefetched into a second register set);
                                     0 rel_gemm_bf3_kernel (two workgroups per CU, 32-row items); outputs
-                                    bit-identical */
+                                    bit-identical */,
+    MPGNN_OPT_OUTER_SIDX = 36    /* the bf16-split weight gradient (outer_bf3v_kernel_t): 1 fetches each slice's
+                                    row indices with scalar loads (counted apart from the row loads and slab
+                                    stores); 0 lane vector loads read back by readlane; slabs bit-identical */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

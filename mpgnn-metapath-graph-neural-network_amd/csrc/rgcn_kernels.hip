@@ -4375,7 +4375,13 @@ __device__ __forceinline__ bf16x8 ov_frag(const __bf16* plane, int k0, int col0,
 // fragments / 30 reads for a 128 × 32 strip), and the next slice's commit is scheduled among the
 // MFMAs (branch-free; past the last slice it writes zeros nobody reads). Same products, same
 // per-block accumulators: bit-identical slabs.
-template <bool SQ>
+// SIDX (round 6, MPGNN_OPT_OUTER_SIDX): a slice's four row indices per wave (wave-uniform values)
+// are fetched with scalar loads instead of lane-0..3 vector loads read back by readlane. Scalar
+// loads are counted by lgkmcnt, so the rows' vmcnt waits no longer cover the indices and an index
+// wait no longer covers every row load and slab store issued before it (the stamps put ~1 k of a
+// slice's ~4.5 k cycles in the index wait). Index tables are plan / saved tensors this kernel
+// never writes. Same rows, same products: bit-identical slabs.
+template <bool SQ, bool SIDX = false>
 __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel_t(OuterArgs ra, OuterArgs wa, int ra_n, int n_all) {
     constexpr int SL = 16;
     extern __shared__ __attribute__((aligned(16))) __bf16 ov_smem[];
@@ -4452,20 +4458,39 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel_t(OuterArgs ra,
 
     // row indices of a slice: lanes 0..3 of the wave hold those of its staged rows
     // 2·wave, 2·wave + 1, 2·wave + 8, 2·wave + 9
-    auto load_idx = [&](const OuterCursor& k, int& ia, int& ib) {
+    struct Idx {  // SIDX: the four rows' indices (uniform); else lanes 0..3 of .a[0] / .b[0]
+        int a[4], b[4];
+    };
+    auto load_idx = [&](const OuterCursor& k, Idx& x) {
         const Src a = src_of(k.chunk);
-        const int r = 2 * wave + (lane & 1) + 8 * ((lane >> 1) & 1);
-        const int p = min(k.p0 + k.sl * SL + r, max(k.p1 - 1, k.p0));
-        ib = a.b_idx != nullptr ? a.b_idx[p] : p;
-        ia = a.a_idx != nullptr ? a.a_idx[p] : p - a.a_off;
+        if constexpr (SIDX) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int r = 2 * wave + (q & 1) + 8 * (q >> 1);
+                const int p = min(k.p0 + k.sl * SL + r, max(k.p1 - 1, k.p0));
+                x.b[q] = a.b_idx != nullptr ? ld_uniform(a.b_idx, p) : p;
+                x.a[q] = a.a_idx != nullptr ? ld_uniform(a.a_idx, p) : p - a.a_off;
+            }
+        } else {
+            const int r = 2 * wave + (lane & 1) + 8 * ((lane >> 1) & 1);
+            const int p = min(k.p0 + k.sl * SL + r, max(k.p1 - 1, k.p0));
+            x.b[0] = a.b_idx != nullptr ? a.b_idx[p] : p;
+            x.a[0] = a.a_idx != nullptr ? a.a_idx[p] : p - a.a_off;
+        }
     };
     // this lane's two rows (srow: index lane 0 | 1 by half; srow + 8: lane 2 | 3) as float4
-    auto issue = [&](const OuterCursor& k, int ia, int ib, float4 (&va)[2], float4 (&vb)[2]) {
+    auto issue = [&](const OuterCursor& k, const Idx& x, float4 (&va)[2], float4 (&vb)[2]) {
         const Src a = src_of(k.chunk);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int a0 = __builtin_amdgcn_readlane(ia, 2 * j), a1 = __builtin_amdgcn_readlane(ia, 2 * j + 1);
-            const int b0 = __builtin_amdgcn_readlane(ib, 2 * j), b1 = __builtin_amdgcn_readlane(ib, 2 * j + 1);
+            int a0, a1, b0, b1;
+            if constexpr (SIDX) {
+                a0 = x.a[2 * j]; a1 = x.a[2 * j + 1];
+                b0 = x.b[2 * j]; b1 = x.b[2 * j + 1];
+            } else {
+                a0 = __builtin_amdgcn_readlane(x.a[0], 2 * j); a1 = __builtin_amdgcn_readlane(x.a[0], 2 * j + 1);
+                b0 = __builtin_amdgcn_readlane(x.b[0], 2 * j); b1 = __builtin_amdgcn_readlane(x.b[0], 2 * j + 1);
+            }
             const int ra_ = h ? a1 : a0, rb_ = h ? b1 : b0;
             const float* arow = ra_ >= 0 ? a.A + (size_t)ra_ * lda : a.A2 + (size_t)(-ra_ - 1 - a.a2_off) * lda;
             va[j] = *reinterpret_cast<const float4*>(arow + scol);
@@ -4519,15 +4544,17 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel_t(OuterArgs ra,
     OuterCursor c2 = valid(c1) ? advance(c1) : c1;
     OuterCursor c3 = valid(c2) ? advance(c2) : c2;
     float4 xa[2], xb[2], ya[2], yb[2];
-    int ia, ib, ja = 0, jb = 0;
-    load_idx(cur, ia, ib);
-    issue(cur, ia, ib, xa, xb);
+    Idx ii, jj;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) jj.a[q] = jj.b[q] = 0;
+    load_idx(cur, ii);
+    issue(cur, ii, xa, xb);
     commit(cur, xa, xb, planes);
     if (valid(c1)) {
-        load_idx(c1, ia, ib);
-        issue(c1, ia, ib, xa, xb);
+        load_idx(c1, ii);
+        issue(c1, ii, xa, xb);
     }
-    if (valid(c2)) load_idx(c2, ja, jb);
+    if (valid(c2)) load_idx(c2, jj);
     __syncthreads();
     int buf = 0;
     const int g = lane >> 4;          // 16-lane group of the transposed reads
@@ -4539,8 +4566,8 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel_t(OuterArgs ra,
 #endif
         const bool more = valid(c1);
         if (valid(c2)) {
-            issue(c2, ja, jb, vna, vnb);
-            if (valid(c3)) load_idx(c3, ja, jb);
+            issue(c2, jj, vna, vnb);
+            if (valid(c3)) load_idx(c3, jj);
         }
 #ifdef MPGNN_STAMPS
         stamp_at(ra.stamps, nsl, 6);
@@ -6164,13 +6191,14 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
 }
 
 static void launch_outer_bf3(dim3 grid, const OuterArgs& r_in, const OuterArgs& w, int ra_n, int n_all, bool vec,
-                             bool sq, hipStream_t st) {
+                             bool sq, hipStream_t st, bool sidx = false) {
     OuterArgs r = r_in;
 #ifdef MPGNN_STAMPS
     r.stamps = g_stamps_host;
 #endif
     if (vec)
         if (sq) hipLaunchKernelGGL(outer_bf3v_kernel_t<true>, grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
+        else if (sidx) hipLaunchKernelGGL((outer_bf3v_kernel_t<false, true>), grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
         else hipLaunchKernelGGL(outer_bf3v_kernel_t<false>, grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
     else
         hipLaunchKernelGGL(outer_bf3_kernel, grid, dim3(kThreads), kOb3Lds, st, r, w, ra_n, n_all);
@@ -6688,6 +6716,7 @@ static int32_t set_switch(Options& o, int32_t option, int64_t value) {
         case MPGNN_OPT_OUTER_RANGES: o.outer_ranges = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_W_IL: o.gemm_w_il = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_W1: o.gemm_w1 = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_OUTER_SIDX: o.outer_sidx = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_SWITCH_COST:
             if (value < 0 || value > 10000) return arg_error("MPGNN_OPT_GEMM_SWITCH_COST must be 0..10000 (percent of an item)");
             o.gemm_switch_cost = (int)value;
@@ -6714,6 +6743,7 @@ static bool get_switch(const Options& o, int32_t option, int64_t* value) {
         case MPGNN_OPT_OUTER_RANGES: *value = o.outer_ranges; return true;
         case MPGNN_OPT_GEMM_W_IL: *value = o.gemm_w_il; return true;
         case MPGNN_OPT_GEMM_W1: *value = o.gemm_w1; return true;
+        case MPGNN_OPT_OUTER_SIDX: *value = o.outer_sidx; return true;
         case MPGNN_OPT_GEMM_SWITCH_COST: *value = o.gemm_switch_cost; return true;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = o.flat_wg_per_cu; return true;
         default: return false;
@@ -7001,6 +7031,34 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         // 1) Hm[m] = mean(x over multi-edge segment m)  (the saved means when training); a
         //    single-edge segment's mean is its x row, read by the GEMM through s_src
         float* H = h_save ? h_save : reinterpret_cast<float*>(ws + w.hf);
+#ifdef MPGNN_PROBE_OVERLAP
+        // PROBE BUILD ONLY (scripts/r06_probe_overlap.sh; never the product library): the means on a
+        // side stream CONCURRENT with the whole transform GEMM, which then reads stale Hm rows — WRONG
+        // results. Bounds what running the means beside the GEMM's Hm-free items could save
+        // (VERDICT r5 item 1). MPGNN_PROBE_OVERLAP = 1: means launched first; 2: the GEMM first.
+        {
+            static hipStream_t side = nullptr;
+            static hipEvent_t e0 = nullptr, e1 = nullptr;
+            if (side == nullptr) {
+                (void)hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
+                (void)hipEventCreateWithFlags(&e0, hipEventDisableTiming);
+                (void)hipEventCreateWithFlags(&e1, hipEventDisableTiming);
+            }
+            (void)hipEventRecord(e0, strm);
+            (void)hipStreamWaitEvent(side, e0, 0);
+            if (MPGNN_PROBE_OVERLAP == 1)
+                st = run_means_multi(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, side);
+            if (st != MPGNN_OK) return st;
+            st = run_seg(p, mode, s, 2, x, F_in, weight, root, 0, F_out, Y, Yroot, row_lo, row_hi, nullptr, nullptr,
+                         true, MPGNN_K_SEG_FWD, strm, H);
+            if (st != MPGNN_OK) return st;
+            if (MPGNN_PROBE_OVERLAP == 2)
+                st = run_means_multi(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, side);
+            if (st != MPGNN_OK) return st;
+            (void)hipEventRecord(e1, side);
+            (void)hipStreamWaitEvent(strm, e1, 0);
+        }
+#else
         {
             TimedLaunch tl(MPGNN_K_MEAN, strm);
             st = run_means_multi(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
@@ -7010,6 +7068,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         st = run_seg(p, mode, s, 2, x, F_in, weight, root, 0, F_out, Y, Yroot, row_lo, row_hi, nullptr, nullptr, true,
                      MPGNN_K_SEG_FWD, strm, H);
         if (st != MPGNN_OK) return st;
+#endif
     }
 
     // 2) out[i] = (Σ_{seg of row i, relation order} Y[seg] + Yroot[i]) + bias
@@ -7746,7 +7805,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
                     rq.Pb = nullptr;
                     rq.dst_b = nullptr;
                 }
-                launch_outer_bf3(dim3(gx), rq, wq, rc.n, n_all, p->opt.outer_vec, p->opt.outer_sq, strm);
+                launch_outer_bf3(dim3(gx), rq, wq, rc.n, n_all, p->opt.outer_vec, p->opt.outer_sq, strm, p->opt.outer_sidx);
                 if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel (quadrant) launch")) != MPGNN_OK) return st;
             }
     } else if (bf3) {
@@ -7755,7 +7814,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
         const int n_all = nch + rc.n;
         const int gx = std::max(1, std::min(n_all, cu_count() * 2));
         with_ranges(orr, n_all, gx);
-        launch_outer_bf3(dim3(gx), orr, ow, rc.n, n_all, p->opt.outer_vec, p->opt.outer_sq, strm);
+        launch_outer_bf3(dim3(gx), orr, ow, rc.n, n_all, p->opt.outer_vec, p->opt.outer_sq, strm, p->opt.outer_sidx);
         if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel launch")) != MPGNN_OK) return st;
     } else if (have_w && have_root && root_y == mt) {
         TimedLaunch tl(MPGNN_K_OUTER, strm);

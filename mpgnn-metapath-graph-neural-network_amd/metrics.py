@@ -74,7 +74,7 @@ def _rows_valid(idx: torch.Tensor, rows: int) -> bool:
     for ri, vi, r in _ROWS_OK:
         if ri() is idx and vi == idx._version and r == rows:
             return True
-    if torch.cuda.is_current_stream_capturing():
+    if idx.is_cuda and torch.cuda.is_current_stream_capturing():
         return False
     ok = idx.numel() == 0 or bool(((idx >= 0) & (idx < rows)).all().item())
     if ok:

@@ -20,7 +20,9 @@ mode = sys.argv[2] if len(sys.argv) > 2 else "fwd"
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").strip()
+    # "(anonymous namespace)::" would end the name at its "(": plan_device.hip's once-per-graph
+    # plan-build kernels (k_fill_edges, k_flat_walk, ...) then all read "mpgnn::" (r05 reports)
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
 
 
 def role_labels(rows):

@@ -22,6 +22,7 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--opt", action="append", default=[], help="K=V process default before the plan is built")
 ap.add_argument("--json", default=None)
+ap.add_argument("--no-check", action="store_true", help="skip the graph == eager check (probe libraries)")
 a = ap.parse_args()
 for kv in a.opt:
     k, v = kv.split("=")
@@ -82,7 +83,7 @@ with torch.cuda.graph(graph), torch.no_grad():
     gout = step()
 graph.replay()
 torch.cuda.synchronize()
-assert torch.equal(gout, ref), "graph replay differs from the eager step"
+assert a.no_check or torch.equal(gout, ref), "graph replay differs from the eager step"
 
 
 def replay():

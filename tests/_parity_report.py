@@ -10,8 +10,20 @@ _ROWS: list = []
 
 
 def record(what: str, err: float, tol: float, **extra) -> None:
-    row = {"check": what, "max_rel_err": err, "tol": tol}
+    """One row per check: the pytest node id that made it (PYTEST_CURRENT_TEST: file::test[params]),
+    the label, the errors and the bar; `bar_ratio` = how close the deciding error came to its bar
+    (elementwise vs tol when that passes; else the float64-truth error vs factor x the fp32
+    reference path's own error)."""
+    node = os.environ.get("PYTEST_CURRENT_TEST", "").rsplit(" (", 1)[0]
+    row = {"test": node, "check": what, "max_rel_err": err, "tol": tol}
     row.update(extra)
+    if err <= tol or "e_gpu64" not in extra:
+        row["bar_ratio"] = err / tol if tol > 0 else None
+        row["decided_by"] = "elementwise vs fp32 reference"
+    else:
+        bar = max(tol, extra.get("cpu_factor", 2.0) * extra["e_cpu64"])
+        row["bar_ratio"] = extra["e_gpu64"] / bar if bar > 0 else None
+        row["decided_by"] = "float64 truth vs factor x fp32 reference error"
     _ROWS.append(row)
 
 

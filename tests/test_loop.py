@@ -200,6 +200,33 @@ def test_confusion_counts_rows_kernel_equals_torch(seed, c):
             f1_score(pred[keep].tolist(), y[keep].tolist(), average="macro")
 
 
+def test_confusion_counts_rows_range_check():
+    """a row list with an out-of-range entry fails the one-time check, so the GPU path
+    hands it to torch's ops (whose indexing rejects it like the reference's pred[idx]); a list
+    in range is remembered per object and version."""
+    idx = torch.tensor([0, 4, 9])
+    assert metrics._rows_valid(idx, 10)
+    assert not metrics._rows_valid(torch.tensor([0, 10]), 10)
+    assert not metrics._rows_valid(torch.tensor([-1, 3]), 10)
+    idx[1] = 12  # in-place change: the cached verdict no longer applies
+    assert not metrics._rows_valid(idx, 10)
+    assert metrics._rows_valid(torch.empty(0, dtype=torch.int64), 0)
+
+
+@pytest.mark.gpu
+def test_confusion_counts_rows_wide_classes_take_torch():
+    """C above the kernel's LDS histograms (4096) runs torch's counts (same values) instead of
+    failing the launch."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(6)
+    wide = torch.randn(300, 5000, generator=g).to(dev)
+    idx = torch.randperm(300, generator=g)[:200].to(dev)
+    y = torch.randint(0, 5000, (200,), generator=g).to(dev)
+    got = metrics.confusion_counts_rows(wide, [(idx, y)])
+    ref = metrics.confusion_counts_many([(torch.argmax(wide[idx], 1), y)], 5000)
+    assert torch.equal(got, ref)
+
+
 def _nll_case(seed, rows, c, n, dup=False, ignore=False):
     """log_softmax rows (requires grad through the softmax input), a row list (repeated rows when
     dup) and targets (some ignore_index -100 when ignore)."""
