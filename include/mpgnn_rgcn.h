@@ -446,9 +446,10 @@ enum mpgnn_option {
                                     the next relation's weight slice prefetched into a second register set);
                                     0 rel_gemm_bf3_kernel (two workgroups per CU, 32-row items); outputs
                                     bit-identical */,
-    MPGNN_OPT_OUTER_SIDX = 36    /* the bf16-split weight gradient (outer_bf3v_kernel_t): 1 fetches each slice's
-                                    row indices with scalar loads (counted apart from the row loads and slab
-                                    stores); 0 lane vector loads read back by readlane; slabs bit-identical */
+    MPGNN_OPT_OUTER_VARIANT = 36 /* the bf16-split weight gradient (outer_bf3v_kernel_t) slice pipeline: 0 (default)
+                                    the next-next slice's rows issued before this slice's MFMAs; 1 its row
+                                    indices by scalar loads; 2 its rows issued after this slice's MFMAs; slabs
+                                    bit-identical */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

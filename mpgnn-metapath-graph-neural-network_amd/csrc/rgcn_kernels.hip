@@ -4375,13 +4375,16 @@ __device__ __forceinline__ bf16x8 ov_frag(const __bf16* plane, int k0, int col0,
 // fragments / 30 reads for a 128 × 32 strip), and the next slice's commit is scheduled among the
 // MFMAs (branch-free; past the last slice it writes zeros nobody reads). Same products, same
 // per-block accumulators: bit-identical slabs.
-// SIDX (round 6, MPGNN_OPT_OUTER_SIDX): a slice's four row indices per wave (wave-uniform values)
-// are fetched with scalar loads instead of lane-0..3 vector loads read back by readlane. Scalar
-// loads are counted by lgkmcnt, so the rows' vmcnt waits no longer cover the indices and an index
-// wait no longer covers every row load and slab store issued before it (the stamps put ~1 k of a
-// slice's ~4.5 k cycles in the index wait). Index tables are plan / saved tensors this kernel
-// never writes. Same rows, same products: bit-identical slabs.
-template <bool SQ, bool SIDX = false>
+// VAR (round 6, MPGNN_OPT_OUTER_VARIANT; same rows, same products: bit-identical slabs):
+//   1 (SIDX) a slice's four row indices per wave (wave-uniform values) are fetched with scalar loads
+//     instead of lane-0..3 vector loads read back by readlane: counted by lgkmcnt, so an index wait
+//     no longer covers the row loads and slab stores issued before it (measured slower: 64 -> 69 µs,
+//     each scalar wait drains the wave's LDS operations too);
+//   2 (LATE) the rows of the slice two ahead are issued AFTER this slice's fragment reads and MFMAs,
+//     not before them: the vector-memory wait that the index of that slice implies (it covers the
+//     rows of the next slice, issued one slice earlier) then falls behind the MFMAs already queued
+//     instead of in front of them (the stamps put ~1 k of a slice's ~4.5 k cycles there).
+template <bool SQ, int VAR = 0>
 __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel_t(OuterArgs ra, OuterArgs wa, int ra_n, int n_all) {
     constexpr int SL = 16;
     extern __shared__ __attribute__((aligned(16))) __bf16 ov_smem[];
@@ -4458,6 +4461,7 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel_t(OuterArgs ra,
 
     // row indices of a slice: lanes 0..3 of the wave hold those of its staged rows
     // 2·wave, 2·wave + 1, 2·wave + 8, 2·wave + 9
+    constexpr bool SIDX = VAR == 1;
     struct Idx {  // SIDX: the four rows' indices (uniform); else lanes 0..3 of .a[0] / .b[0]
         int a[4], b[4];
     };
@@ -4565,7 +4569,7 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel_t(OuterArgs ra,
         stamp_at(ra.stamps, nsl, 0);
 #endif
         const bool more = valid(c1);
-        if (valid(c2)) {
+        if (VAR != 2 && valid(c2)) {
             issue(c2, jj, vna, vnb);
             if (valid(c3)) load_idx(c3, jj);
         }
@@ -4645,6 +4649,10 @@ __global__ __launch_bounds__(kThreads, 2) void outer_bf3v_kernel_t(OuterArgs ra,
 #ifdef MPGNN_STAMPS
         stamp_at(ra.stamps, nsl, 1);
 #endif
+        if (VAR == 2 && valid(c2)) {
+            issue(c2, jj, vna, vnb);
+            if (valid(c3)) load_idx(c3, jj);
+        }
         if (!SQ && more) commit(c1, vca, vcb, planes + (buf ^ 1) * 6 * kOvPlane);
 #ifdef MPGNN_STAMPS
         stamp_at(ra.stamps, nsl, 2);
@@ -6191,14 +6199,15 @@ static int32_t run_rowsum(const mpgnn_plan* p, RowSumArgs a, const int* pb, cons
 }
 
 static void launch_outer_bf3(dim3 grid, const OuterArgs& r_in, const OuterArgs& w, int ra_n, int n_all, bool vec,
-                             bool sq, hipStream_t st, bool sidx = false) {
+                             bool sq, hipStream_t st, int var = 0) {
     OuterArgs r = r_in;
 #ifdef MPGNN_STAMPS
     r.stamps = g_stamps_host;
 #endif
     if (vec)
         if (sq) hipLaunchKernelGGL(outer_bf3v_kernel_t<true>, grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
-        else if (sidx) hipLaunchKernelGGL((outer_bf3v_kernel_t<false, true>), grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
+        else if (var == 1) hipLaunchKernelGGL((outer_bf3v_kernel_t<false, 1>), grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
+        else if (var == 2) hipLaunchKernelGGL((outer_bf3v_kernel_t<false, 2>), grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
         else hipLaunchKernelGGL(outer_bf3v_kernel_t<false>, grid, dim3(kThreads), kOvLds, st, r, w, ra_n, n_all);
     else
         hipLaunchKernelGGL(outer_bf3_kernel, grid, dim3(kThreads), kOb3Lds, st, r, w, ra_n, n_all);
@@ -6716,7 +6725,10 @@ static int32_t set_switch(Options& o, int32_t option, int64_t value) {
         case MPGNN_OPT_OUTER_RANGES: o.outer_ranges = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_W_IL: o.gemm_w_il = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_W1: o.gemm_w1 = value != 0; return MPGNN_OK;
-        case MPGNN_OPT_OUTER_SIDX: o.outer_sidx = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_OUTER_VARIANT:
+            if (value < 0 || value > 2) return arg_error("MPGNN_OPT_OUTER_VARIANT must be 0, 1 or 2");
+            o.outer_variant = (int)value;
+            return MPGNN_OK;
         case MPGNN_OPT_GEMM_SWITCH_COST:
             if (value < 0 || value > 10000) return arg_error("MPGNN_OPT_GEMM_SWITCH_COST must be 0..10000 (percent of an item)");
             o.gemm_switch_cost = (int)value;
@@ -6743,7 +6755,7 @@ static bool get_switch(const Options& o, int32_t option, int64_t* value) {
         case MPGNN_OPT_OUTER_RANGES: *value = o.outer_ranges; return true;
         case MPGNN_OPT_GEMM_W_IL: *value = o.gemm_w_il; return true;
         case MPGNN_OPT_GEMM_W1: *value = o.gemm_w1; return true;
-        case MPGNN_OPT_OUTER_SIDX: *value = o.outer_sidx; return true;
+        case MPGNN_OPT_OUTER_VARIANT: *value = o.outer_variant; return true;
         case MPGNN_OPT_GEMM_SWITCH_COST: *value = o.gemm_switch_cost; return true;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = o.flat_wg_per_cu; return true;
         default: return false;
@@ -7805,7 +7817,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
                     rq.Pb = nullptr;
                     rq.dst_b = nullptr;
                 }
-                launch_outer_bf3(dim3(gx), rq, wq, rc.n, n_all, p->opt.outer_vec, p->opt.outer_sq, strm, p->opt.outer_sidx);
+                launch_outer_bf3(dim3(gx), rq, wq, rc.n, n_all, p->opt.outer_vec, p->opt.outer_sq, strm, p->opt.outer_variant);
                 if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel (quadrant) launch")) != MPGNN_OK) return st;
             }
     } else if (bf3) {
@@ -7814,7 +7826,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
         const int n_all = nch + rc.n;
         const int gx = std::max(1, std::min(n_all, cu_count() * 2));
         with_ranges(orr, n_all, gx);
-        launch_outer_bf3(dim3(gx), orr, ow, rc.n, n_all, p->opt.outer_vec, p->opt.outer_sq, strm, p->opt.outer_sidx);
+        launch_outer_bf3(dim3(gx), orr, ow, rc.n, n_all, p->opt.outer_vec, p->opt.outer_sq, strm, p->opt.outer_variant);
         if ((st = hip_check(hipGetLastError(), "outer_bf3_kernel launch")) != MPGNN_OK) return st;
     } else if (have_w && have_root && root_y == mt) {
         TimedLaunch tl(MPGNN_K_OUTER, strm);

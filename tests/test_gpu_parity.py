@@ -828,25 +828,26 @@ def test_k256_gemm_interleaved_commit_bit_identical(mode):
     assert res[0][0].abs().sum() > 0
 
 
-@pytest.mark.parametrize("opt", [35, 36])
-def test_w1_gemm_and_scalar_index_outer_bit_identical(opt):
+@pytest.mark.parametrize("opt,val", [(35, 1), (36, 1), (36, 2)])
+def test_w1_gemm_and_outer_variants_bit_identical(opt, val):
     """Round 6 variants, off by default, against the product kernels on one layer (forward, dgrad,
     every gradient) — bit for bit:
       35 MPGNN_OPT_GEMM_W1: rel_gemm_w1_kernel (one workgroup per CU, 64-row items: tile pairs of
          one relation, a relation's odd last tile alone, 64-node root items with a ragged last one,
          the next relation's weight slice prefetched) vs rel_gemm_bf3_kernel;
-      36 MPGNN_OPT_OUTER_SIDX: the weight gradient's row indices by scalar loads vs lane loads.
+      36 MPGNN_OPT_OUTER_VARIANT: the weight gradient's row indices by scalar loads (1), or the
+         next-next slice's rows issued after the MFMAs (2), vs the product order.
     A graph with relations of 1, odd and even 32-row tile counts and N % 64 != 0."""
     g = data.synthetic_graph(5003, 9, 12, feat_dim=128, seed=37)
     N, R = g.num_nodes, g.num_relations
-    gen = torch.Generator().manual_seed(opt)
+    gen = torch.Generator().manual_seed(opt + val)
     W = (torch.rand((R, 128, 128), generator=gen) - 0.5) * 0.1
     root = (torch.rand(128, 128, generator=gen) - 0.5) * 0.1
     bias = torch.rand(128, generator=gen) - 0.5
     gout = torch.randn(N, 128, generator=gen)
     plan = mpgnn_amd.GraphPlan(g.edge_index.to(DEV), g.edge_type.to(DEV), N)
     res = {}
-    for v in (0, 1):
+    for v in (0, val):
         plan.set_option(opt, v)
         xg = g.x.to(DEV).requires_grad_(True)
         Wg, rg, bg = (t.to(DEV).requires_grad_(True) for t in (W, root, bias))
@@ -855,7 +856,7 @@ def test_w1_gemm_and_scalar_index_outer_bit_identical(opt):
         torch.cuda.synchronize()
         res[v] = [out.detach(), xg.grad, Wg.grad, rg.grad, bg.grad]
     plan.set_option(opt, _lib_default(opt))
-    for k, a, b in zip(("out", "dx", "dW", "droot", "dbias"), res[1], res[0]):
+    for k, a, b in zip(("out", "dx", "dW", "droot", "dbias"), res[val], res[0]):
         assert torch.equal(a, b), k
     assert res[0][0].abs().sum() > 0 and res[0][2].abs().sum() > 0
 
