@@ -449,7 +449,9 @@ enum mpgnn_option {
     MPGNN_OPT_OUTER_VARIANT = 36 /* the bf16-split weight gradient (outer_bf3v_kernel_t) slice pipeline: 0 (default)
                                     the next-next slice's rows issued before this slice's MFMAs; 1 its row
                                     indices by scalar loads; 2 its rows issued after this slice's MFMAs; slabs
-                                    bit-identical */
+                                    bit-identical */,
+    MPGNN_OPT_FLAT_U = 37        /* gather-sum lists (means, combine, grad_x): rows in flight per wave, 16
+                                    (default), 8 or 32; sums bit-identical */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

@@ -6213,11 +6213,13 @@ static void launch_outer_bf3(dim3 grid, const OuterArgs& r_in, const OuterArgs& 
         hipLaunchKernelGGL(outer_bf3_kernel, grid, dim3(kThreads), kOb3Lds, st, r, w, ra_n, n_all);
 }
 template <int V, int T>
-static void launch_flat(const FlatArgs& a, int max_pieces, int wg_per_cu, hipStream_t st) {
+static void launch_flat(const FlatArgs& a, int max_pieces, int wg_per_cu, int u, hipStream_t st) {
     const int n_groups = a.g_hi - a.g_lo;
     const int n = wg_per_cu > 0 ? std::min(n_groups, cu_count() * wg_per_cu) : n_groups;
     const size_t lds = (size_t)max_pieces * a.F * sizeof(float);  // 0 when the list has no long row
-    hipLaunchKernelGGL((flat_rows_kernel<V, T>), dim3(n), dim3(kThreads), lds, st, a);
+    if (u == 32) hipLaunchKernelGGL((flat_rows_kernel<V, T, 32>), dim3(n), dim3(kThreads), lds, st, a);
+    else if (u == 8) hipLaunchKernelGGL((flat_rows_kernel<V, T, 8>), dim3(n), dim3(kThreads), lds, st, a);
+    else hipLaunchKernelGGL((flat_rows_kernel<V, T>), dim3(n), dim3(kThreads), lds, st, a);
 }
 
 template <int V, int T>
@@ -6379,6 +6381,7 @@ struct FlatRun {
     int relu;             // fused activation (unsharded forward combine)
     unsigned* arrive;     // mode 0: [nsplit] zeroed piece counters — split rows finished in the launch
     int wg_per_cu;        // the plan's MPGNN_OPT_FLAT_WG_PER_CU
+    int u = 16;           // the plan's MPGNN_OPT_FLAT_U: rows in flight per wave (8, 16, 32)
 };
 
 static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
@@ -6418,7 +6421,7 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
             a.split_ptr = f.fd->split_ptr;
             a.split_slot = f.fd->split_slot;
         }  // mode 1: the finalize adds extra + bias first
-        MPGNN_VT_DISPATCH(V, T, launch_flat, a, f.max_pieces, f.wg_per_cu, strm);
+        MPGNN_VT_DISPATCH(V, T, launch_flat, a, f.max_pieces, f.wg_per_cu, f.u, strm);
         int32_t st = hip_check(hipGetLastError(), "flat_rows_kernel launch");
         if (st != MPGNN_OK) return st;
     }
@@ -6460,6 +6463,7 @@ static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x
         // flat chunked list; chunks and splits of the relation range [d_lo, d_hi)
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
+        f.u = p->opt.flat_u;
         f.fd = &p->d.seg_f;
         f.max_pieces = p->seg_f.max_pieces;
         f.g_lo = p->seg_f.cut_group_ptr[s.d_lo];
@@ -6502,6 +6506,7 @@ static int32_t run_means_multi(const mpgnn_plan* p, const Selection& s, const fl
     if (!exact) {
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
+        f.u = p->opt.flat_u;
         f.fd = &p->d.segm_f;
         f.max_pieces = p->segm_f.max_pieces;
         f.g_lo = p->segm_f.cut_group_ptr[s.d_lo];
@@ -6725,6 +6730,10 @@ static int32_t set_switch(Options& o, int32_t option, int64_t value) {
         case MPGNN_OPT_OUTER_RANGES: o.outer_ranges = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_W_IL: o.gemm_w_il = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_W1: o.gemm_w1 = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_FLAT_U:
+            if (value != 8 && value != 16 && value != 32) return arg_error("MPGNN_OPT_FLAT_U must be 8, 16 or 32");
+            o.flat_u = (int)value;
+            return MPGNN_OK;
         case MPGNN_OPT_OUTER_VARIANT:
             if (value < 0 || value > 2) return arg_error("MPGNN_OPT_OUTER_VARIANT must be 0, 1 or 2");
             o.outer_variant = (int)value;
@@ -6756,6 +6765,7 @@ static bool get_switch(const Options& o, int32_t option, int64_t* value) {
         case MPGNN_OPT_GEMM_W_IL: *value = o.gemm_w_il; return true;
         case MPGNN_OPT_GEMM_W1: *value = o.gemm_w1; return true;
         case MPGNN_OPT_OUTER_VARIANT: *value = o.outer_variant; return true;
+        case MPGNN_OPT_FLAT_U: *value = o.flat_u; return true;
         case MPGNN_OPT_GEMM_SWITCH_COST: *value = o.gemm_switch_cost; return true;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = o.flat_wg_per_cu; return true;
         default: return false;
@@ -7102,6 +7112,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         }
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
+        f.u = p->opt.flat_u;
         f.fd = &p->d.rwx_f;
         f.max_pieces = p->rwx_f.max_pieces;
         f.g_lo = 0;
@@ -7130,6 +7141,7 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     if (mode == MPGNN_MODE_ALL && !exact) {
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
+        f.u = p->opt.flat_u;
         f.fd = &p->d.rw_f;
         f.max_pieces = p->rw_f.max_pieces;
         f.g_lo = 0;
@@ -7228,6 +7240,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         }
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
+        f.u = p->opt.flat_u;
         f.fd = &p->d.tx_f;
         f.max_pieces = p->tx_f.max_pieces;
         f.g_lo = 0;
@@ -7262,6 +7275,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
     } else if (mode == MPGNN_MODE_ALL && !exact) {
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
+        f.u = p->opt.flat_u;
         f.fd = &p->d.t_f;
         f.max_pieces = p->t_f.max_pieces;
         f.g_lo = 0;
