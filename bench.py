@@ -767,7 +767,7 @@ def bench_score_bags(args):
 def pmc_traffic(workload, mode, feat, kernel_prefix):
     """HBM bytes per launch of `kernel_prefix` from the committed PMC summary, or None."""
     rows = []
-    for rnd in ("r05", "r04", "r03", "r02"):  # the newest round's PMC summary first
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):  # the newest round's PMC summary first
         try:
             rows += json.load(open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic.json")))
         except (OSError, ValueError):

@@ -17,6 +17,7 @@ ap.add_argument("trace")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--layers", type=int, default=3)
 ap.add_argument("--json", default=None)
+ap.add_argument("--idle-us", type=float, default=40.0, help="GPU idle time that ends a run of steps")
 a = ap.parse_args()
 
 rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
@@ -42,10 +43,12 @@ while i + n <= len(seq):
         i += n
     else:
         i += 1
-# runs of consecutive steps
+# runs of consecutive steps, cut where the GPU idled > --idle-us between two steps (a host sync:
+# bench.py syncs after its pre-warm batches of 10, after the warm-up and after the timed region)
 runs, cur = [], [blocks[0]] if blocks else []
 for b in blocks[1:]:
-    if b == cur[-1] + n:
+    idle = (seq[b][1] - seq[cur[-1] + n - 1][2]) / 1e3
+    if b == cur[-1] + n and idle < a.idle_us:
         cur.append(b)
     else:
         runs.append(cur)
@@ -53,9 +56,9 @@ for b in blocks[1:]:
 if cur:
     runs.append(cur)
 runs = [r for r in runs if len(r) >= a.steps]
-# warm-up (>= 1 step, plan + warmup) then the timed block: the second run of >= steps steps is
-# the per-kernel pass; take the first run's last `steps` steps
-timed = runs[0][-a.steps:]
+# bench.py: plan + first step, pre-warm (runs of 10), warm-up, then the timed region = the first
+# run of >= --steps steps (the per-kernel event pass after it is the second)
+timed = runs[0][:a.steps]
 names = ["means L%d" % (k // 3) if k % 3 == 0 else ("gemm L%d" % (k // 3) if k % 3 == 1 else "combine L%d" % (k // 3))
          for k in range(n)]
 dur = {k: [] for k in range(n)}
