@@ -2136,6 +2136,7 @@ struct RelGemmW1 {
         const int i_beg = ld_uniform(a.wg_items, rng);
         const int i_end = ld_uniform(a.wg_items, rng + 1);
         if (i_beg >= i_end) return;
+        stamp_id();
 
         Item cur = item(a, i_beg, G);
         float4 va[WPT], vb[WPT];
@@ -2151,9 +2152,12 @@ struct RelGemmW1 {
             load_b_raw(cur.w, wave, lane, wf);
             issue_rows(a, tid, crow, vb);
             issue_rows(a, tid, r1, va);
+            stamp_pro(3);
             bf16x8 b0[NS][3];
             split_b(wf, b0);
+            stamp_pro(4);
             commit(tid, cur.nrows, vb, As);
+            stamp_pro(5);
             if constexpr (DGRAD) {
                 if (tid < ROWS) Sc[tid] = 1.0f / (float)c0;
             }
@@ -2177,6 +2181,7 @@ struct RelGemmW1 {
         float wf[NS][8];  // the next relation's slice, raw (loaded one item ahead of its first use)
         int buf = 0;
         auto step = [&](int i, float4 (&vc)[WPT], int& cntc, float4 (&vn)[WPT], int& cntn) {
+            stamp(i - i_beg, 0);
             const bool has_next = i + 1 < i_end;
             const Item nxt = has_next ? item(a, i + 1, G) : cur;
             {  // unconditional (past the range: the last item's rows again)
@@ -2251,6 +2256,7 @@ struct RelGemmW1 {
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
+            stamp(i - i_beg, 1);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 prev[0][r] = hi0[r] + lo0[r];
@@ -2267,8 +2273,13 @@ struct RelGemmW1 {
                 const int bytes = __builtin_amdgcn_readfirstlane(cur.nrows) * N * 4;
                 prev_rsrc = __builtin_amdgcn_make_buffer_rsrc(Yt, (short)0, bytes, 0x00020000);
             }
-            if (new_w) split_b(wf, b);
+            if (new_w) {
+                stamp(i - i_beg, 2);
+                split_b(wf, b);
+            }
+            stamp(i - i_beg, 3);
             __syncthreads();
+            stamp(i - i_beg, 4);
             cur = nxt;
             buf ^= 1;
         };
@@ -2282,6 +2293,7 @@ struct RelGemmW1 {
             for (int r = 0; r < 16; ++r)
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(prev[u][r]), prev_rsrc, col_b,
                                                       (32 * u + (r & 3) + 8 * (r >> 2)) * (N * 4), 16);
+        stamp_end();
     }
 };
 

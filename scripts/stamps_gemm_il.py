@@ -21,7 +21,11 @@ import argparse  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="fb15k237")
 ap.add_argument("--single", type=int, default=None, help="mode SINGLE over this relation")
+ap.add_argument("--opt", action="append", default=[], help="K=V process default before the plan is built "
+                "(35=1: rel_gemm_w1_kernel)")
 cli = ap.parse_args()
+for kv in cli.opt:
+    _lib.set_option(int(kv.split("=")[0]), int(kv.split("=")[1]))
 
 ITEMS, PH = 32, 8
 g = data.fb15k237_graph(feat_dim=128) if cli.workload == "fb15k237" else data.config_graph(cli.workload)
