@@ -106,7 +106,10 @@ def parse():
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed CPU repetitions (median), after 2 warm-ups")
     a = ap.parse_args()
     base = "C3" if a.workload.startswith("fb15k237") else a.workload
-    dflt = {"C3": (3, 128, 30, 40), "C2": (2, 128, 10, 20), "C5": (3, 256, 2, 8)}[base]
+    # loop epochs K: (t(6 + K) - t(6)) / K — the two calls' fixed costs (model build, capture,
+    # allocator) vary by a few ms, so K sets the noise: C3 K = 40 read 1.25 and 1.90 ms on one box
+    # (profiles/r06_bench_c3*.json), K = 120 holds ~150 ms of epochs against that
+    dflt = {"C3": (3, 128, 30, 120), "C2": (2, 128, 10, 40), "C5": (3, 256, 2, 8)}[base]
     a.layers = dflt[0] if a.layers is None else a.layers
     a.feat = dflt[1] if a.feat is None else a.feat
     a.epoch_steps = dflt[2] if a.epoch_steps is None else a.epoch_steps
