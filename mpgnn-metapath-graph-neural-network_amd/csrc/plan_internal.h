@@ -33,6 +33,7 @@ struct Options {
     bool gemm_w1 = false;         // MPGNN_OPT_GEMM_W1: one workgroup per CU, 64-row items (K = N = 128)
     int outer_variant = 0;        // MPGNN_OPT_OUTER_VARIANT: weight-gradient slice pipeline order (0, 1, 2)
     int flat_u = 16;              // MPGNN_OPT_FLAT_U: gather-sum rows in flight per wave
+    bool flat_pad = false;        // MPGNN_OPT_FLAT_PAD: gather-sum chunks fetched from padded slot tables
     bool gemm_cu_pairs = true;    // MPGNN_OPT_GEMM_CU_PAIRS: GEMM item ranges balanced per CU
     int gemm_switch_cost = 250;   // MPGNN_OPT_GEMM_SWITCH_COST: percent of an item per weight switch
     int flat_wg_per_cu = 0;       // MPGNN_OPT_FLAT_WG_PER_CU: persistent grid of flat_rows_kernel (0: off)
@@ -260,6 +261,9 @@ struct mpgnn_plan {
     mutable std::map<std::array<int64_t, 5>, GemmRanges> gemm_ranges;
     // outer_bf3v_kernel_t's per-workgroup chunk ranges (same ownership as gemm_ranges)
     mutable std::map<std::array<int64_t, 5>, GemmRanges> outer_ranges;
+    // flat_rows_kernel's padded slot tables per (list, value table) (rgcn_kernels.hip
+    // flat_pad_tables): one device block {desc, val, row}; host unused
+    mutable std::map<std::array<int64_t, 5>, GemmRanges> flat_pads;
 };
 
 namespace mpgnn {

@@ -3039,6 +3039,14 @@ struct FlatArgs {
     const int* row_split;   // split index per row
     const int* split_ptr;
     const int* split_slot;
+    // nullable (round 6, MPGNN_OPT_FLAT_PAD): the list's chunks re-laid per workgroup slot
+    // (4·group + wave): pad_desc[slot] = {n, info, long group, 0}, pad_val / pad_row[32·slot + q]
+    // = table / row_of of the chunk's position q — all at addresses the wave knows from its
+    // group and wave number, fetched by one round of vector loads instead of two dependent
+    // scalar hops (group → chunk range) and a vector hop (chunk → its positions)
+    const int4* pad_desc;
+    const int* pad_val;
+    const int* pad_row;
 };
 
 // The finishing step of a complete row: / cnt (IEEE), + bias on own rows, fused ReLU.
@@ -3115,14 +3123,23 @@ __device__ __forceinline__ void flat_split_arrive(const FlatArgs& a, int rr, flo
 // piece slots of a long group).  With a.arrive, a piece of a > kFlatLongPieces row is counted
 // after the loop (one piece per chunk) and its row finished by the wave that completes it.
 template <int V, int T, int U, bool GLOBAL>
+__device__ __forceinline__ void flat_chunk_body(const FlatArgs& a, int n, int info, int val, int row, int lane,
+                                                float* carry, const float (&bb)[T][V]);
+
+template <int V, int T, int U, bool GLOBAL>
 __device__ __forceinline__ void flat_chunk(const FlatArgs& a, int c, int lane, float* carry, const float (&bb)[T][V]) {
     const int p0 = ld_uniform(a.chunk_ptr, c);
     const int n = ld_uniform(a.chunk_ptr, c + 1) - p0;  // 1 .. kFlatChunk
     const int info = ld_uniform(a.chunk_info, c);
-    const int F = a.F;
     const int pq = p0 + min(lane, n - 1);
-    const int val = a.table[pq];
-    const int row = a.row_of[pq];
+    flat_chunk_body<V, T, U, GLOBAL>(a, n, info, a.table[pq], a.row_of[pq], lane, carry, bb);
+}
+
+// n positions (1 .. kFlatChunk), lane q < n holding position q's table value and output row
+template <int V, int T, int U, bool GLOBAL>
+__device__ __forceinline__ void flat_chunk_body(const FlatArgs& a, int n, int info, int val, int row, int lane,
+                                                float* carry, const float (&bb)[T][V]) {
+    const int F = a.F;
     bool keep = lane < n;
     const bool isx = val < 0;  // augmented lists: the row's trailing extra entry
     if (a.filter) keep = keep && (isx || (val >= a.flo && val < a.fhi));
@@ -3222,6 +3239,18 @@ __global__ __launch_bounds__(kThreads) void flat_rows_kernel(FlatArgs a) {
     // workgroup per group; every wave of a workgroup walks the same groups, so the long groups'
     // barriers line up
     for (int g = a.g_lo + (int)blockIdx.x; g < a.g_hi; g += (int)gridDim.x) {
+        if (a.pad_desc != nullptr) {  // one round of loads: the slot's descriptor and positions
+            const int slot = 4 * g + wave;
+            const int4 d = a.pad_desc[slot];
+            const int q = 32 * slot + (lane & 31);
+            const int val = a.pad_val[q], row = a.pad_row[q];
+            const int n = __builtin_amdgcn_readfirstlane(d.x);
+            if (__builtin_amdgcn_readfirstlane(d.z) == 0) {  // a normal group (uniform over the workgroup)
+                if (n > 0) flat_chunk_body<V, T, U, true>(a, n, __builtin_amdgcn_readfirstlane(d.y), val, row, lane,
+                                                          a.carry, bb);
+                continue;
+            }
+        }
         const int c0 = ld_uniform(a.group_ptr, g), c1 = ld_uniform(a.group_ptr, g + 1);
         const bool lng = ld_uniform(a.group_long, g) != 0;
         if (!lng) {
@@ -6394,7 +6423,77 @@ struct FlatRun {
     unsigned* arrive;     // mode 0: [nsplit] zeroed piece counters — split rows finished in the launch
     int wg_per_cu;        // the plan's MPGNN_OPT_FLAT_WG_PER_CU
     int u = 16;           // the plan's MPGNN_OPT_FLAT_U: rows in flight per wave (8, 16, 32)
+    int ngroups = 0;      // groups of the whole list (the padded slot tables cover them all)
+    const mpgnn_plan* plan = nullptr;  // non-null with MPGNN_OPT_FLAT_PAD: padded slot tables
 };
+
+// flat_rows_kernel's padded slot tables of one (list, value table) pair (FlatArgs::pad_desc):
+// one thread per (slot, position); a slot past its group's chunks, or of a long group, has n = 0
+__global__ __launch_bounds__(kThreads) void flat_pad_kernel(int64_t nslots, const int* __restrict__ group_ptr,
+                                                            const int* __restrict__ group_long,
+                                                            const int* __restrict__ chunk_ptr,
+                                                            const int* __restrict__ chunk_info,
+                                                            const int* __restrict__ table, const int* __restrict__ row_of,
+                                                            int4* desc, int* pval, int* prow) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t slot = t >> 5;
+    const int q = (int)(t & 31);
+    if (slot >= nslots) return;
+    const int g = (int)(slot >> 2), w = (int)(slot & 3);
+    const int lng = group_long[g] != 0;
+    const int c = group_ptr[g] + w;
+    int n = 0, info = 0, p0 = 0;
+    if (!lng && c < group_ptr[g + 1]) {
+        p0 = chunk_ptr[c];
+        n = chunk_ptr[c + 1] - p0;
+        info = chunk_info[c];
+    }
+    if (q == 0) desc[slot] = make_int4(n, info, lng, 0);
+    const int pq = p0 + min(q, max(n - 1, 0));  // flat_chunk's lane clamp
+    pval[t] = n > 0 ? table[pq] : 0;
+    prow[t] = n > 0 ? row_of[pq] : 0;
+}
+
+// Cached per plan and (list, table); made outside captures (false: the kernel's scalar path)
+static bool flat_pad_tables(const mpgnn_plan* p, const FlatDev* fd, int ngroups, const int* table, hipStream_t st,
+                            FlatArgs* a) {
+    if (ngroups <= 0 || table == nullptr) return false;
+    const std::array<int64_t, 5> key{(int64_t)(intptr_t)fd, (int64_t)(intptr_t)table, ngroups, 0, 0};
+    std::lock_guard<std::mutex> lk(p->bw_mu);
+    auto it = p->flat_pads.find(key);
+    const int64_t nslots = 4 * (int64_t)ngroups;
+    auto set = [&](char* base) {
+        a->pad_desc = reinterpret_cast<const int4*>(base);
+        a->pad_val = reinterpret_cast<const int*>(base + nslots * 16);
+        a->pad_row = reinterpret_cast<const int*>(base + nslots * 16 + nslots * 32 * 4);
+    };
+    if (it != p->flat_pads.end()) {
+        set(reinterpret_cast<char*>(it->second.dev));
+        return true;
+    }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+    mpgnn_plan::GemmRanges e;
+    const size_t bytes = (size_t)nslots * (16 + 2 * 32 * 4);
+    if (hipMalloc(reinterpret_cast<void**>(&e.dev), bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    char* base = reinterpret_cast<char*>(e.dev);
+    const int64_t nthr = nslots * 32;
+    hipLaunchKernelGGL(flat_pad_kernel, dim3((unsigned)((nthr + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
+                       nslots, fd->group_ptr, fd->group_long, fd->chunk_ptr, fd->chunk_info, table, fd->row_of,
+                       reinterpret_cast<int4*>(base), reinterpret_cast<int*>(base + nslots * 16),
+                       reinterpret_cast<int*>(base + nslots * 16 + nslots * 32 * 4));
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {  // published once complete
+        (void)hipGetLastError();
+        (void)hipFree(e.dev);
+        return false;
+    }
+    p->flat_pads[key] = e;
+    set(base);
+    return true;
+}
 
 static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
     int V, T;
@@ -6433,6 +6532,8 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
             a.split_ptr = f.fd->split_ptr;
             a.split_slot = f.fd->split_slot;
         }  // mode 1: the finalize adds extra + bias first
+        if (f.plan != nullptr && f.plan->opt.flat_pad && f.wg_per_cu == 0)
+            (void)flat_pad_tables(f.plan, f.fd, f.ngroups, f.table, strm, &a);
         MPGNN_VT_DISPATCH(V, T, launch_flat, a, f.max_pieces, f.wg_per_cu, f.u, strm);
         int32_t st = hip_check(hipGetLastError(), "flat_rows_kernel launch");
         if (st != MPGNN_OK) return st;
@@ -6476,8 +6577,10 @@ static int32_t run_means(const mpgnn_plan* p, const Selection& s, const float* x
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.u = p->opt.flat_u;
+        f.plan = p;
         f.fd = &p->d.seg_f;
         f.max_pieces = p->seg_f.max_pieces;
+        f.ngroups = p->seg_f.ngroups;
         f.g_lo = p->seg_f.cut_group_ptr[s.d_lo];
         f.g_hi = p->seg_f.cut_group_ptr[s.d_hi];
         f.k_lo = p->seg_f.cut_split_ptr[s.d_lo];
@@ -6519,8 +6622,10 @@ static int32_t run_means_multi(const mpgnn_plan* p, const Selection& s, const fl
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.u = p->opt.flat_u;
+        f.plan = p;
         f.fd = &p->d.segm_f;
         f.max_pieces = p->segm_f.max_pieces;
+        f.ngroups = p->segm_f.ngroups;
         f.g_lo = p->segm_f.cut_group_ptr[s.d_lo];
         f.g_hi = p->segm_f.cut_group_ptr[s.d_hi];
         f.k_lo = p->segm_f.cut_split_ptr[s.d_lo];
@@ -6742,6 +6847,7 @@ static int32_t set_switch(Options& o, int32_t option, int64_t value) {
         case MPGNN_OPT_OUTER_RANGES: o.outer_ranges = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_W_IL: o.gemm_w_il = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_W1: o.gemm_w1 = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_FLAT_PAD: o.flat_pad = value != 0; return MPGNN_OK;
         case MPGNN_OPT_FLAT_U:
             if (value != 8 && value != 16 && value != 32) return arg_error("MPGNN_OPT_FLAT_U must be 8, 16 or 32");
             o.flat_u = (int)value;
@@ -6778,6 +6884,7 @@ static bool get_switch(const Options& o, int32_t option, int64_t* value) {
         case MPGNN_OPT_GEMM_W1: *value = o.gemm_w1; return true;
         case MPGNN_OPT_OUTER_VARIANT: *value = o.outer_variant; return true;
         case MPGNN_OPT_FLAT_U: *value = o.flat_u; return true;
+        case MPGNN_OPT_FLAT_PAD: *value = o.flat_pad; return true;
         case MPGNN_OPT_GEMM_SWITCH_COST: *value = o.gemm_switch_cost; return true;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = o.flat_wg_per_cu; return true;
         default: return false;
@@ -7125,8 +7232,10 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.u = p->opt.flat_u;
+        f.plan = p;
         f.fd = &p->d.rwx_f;
         f.max_pieces = p->rwx_f.max_pieces;
+        f.ngroups = p->rwx_f.ngroups;
         f.g_lo = 0;
         f.g_hi = p->rwx_f.ngroups;
         f.k_lo = 0;
@@ -7154,8 +7263,10 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.u = p->opt.flat_u;
+        f.plan = p;
         f.fd = &p->d.rw_f;
         f.max_pieces = p->rw_f.max_pieces;
+        f.ngroups = p->rw_f.ngroups;
         f.g_lo = 0;
         f.g_hi = p->rw_f.ngroups;
         f.table = p->d.rw_seg;
@@ -7253,8 +7364,10 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.u = p->opt.flat_u;
+        f.plan = p;
         f.fd = &p->d.tx_f;
         f.max_pieces = p->tx_f.max_pieces;
+        f.ngroups = p->tx_f.ngroups;
         f.g_lo = 0;
         f.g_hi = p->tx_f.ngroups;
         f.k_lo = 0;
@@ -7288,8 +7401,10 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.u = p->opt.flat_u;
+        f.plan = p;
         f.fd = &p->d.t_f;
         f.max_pieces = p->t_f.max_pieces;
+        f.ngroups = p->t_f.ngroups;
         f.g_lo = 0;
         f.g_hi = p->t_f.ngroups;
         f.table = p->d.t_seg;

@@ -828,7 +828,7 @@ def test_k256_gemm_interleaved_commit_bit_identical(mode):
     assert res[0][0].abs().sum() > 0
 
 
-@pytest.mark.parametrize("opt,val", [(35, 1), (36, 1), (36, 2)])
+@pytest.mark.parametrize("opt,val", [(35, 1), (36, 1), (36, 2), (37, 32), (37, 8), (38, 1)])
 def test_w1_gemm_and_outer_variants_bit_identical(opt, val):
     """Round 6 variants, off by default, against the product kernels on one layer (forward, dgrad,
     every gradient) — bit for bit:
@@ -837,6 +837,10 @@ def test_w1_gemm_and_outer_variants_bit_identical(opt, val):
          the next relation's weight slice prefetched) vs rel_gemm_bf3_kernel;
       36 MPGNN_OPT_OUTER_VARIANT: the weight gradient's row indices by scalar loads (1), or the
          next-next slice's rows issued after the MFMAs (2), vs the product order.
+      37 MPGNN_OPT_FLAT_U: the gather-sum kernels with 32 / 8 rows in flight per wave (means,
+         combine, grad_x) vs 16;
+      38 MPGNN_OPT_FLAT_PAD: their chunks fetched from the padded per-slot tables vs the scalar
+         chunk-range hops.
     A graph with relations of 1, odd and even 32-row tile counts and N % 64 != 0."""
     g = data.synthetic_graph(5003, 9, 12, feat_dim=128, seed=37)
     N, R = g.num_nodes, g.num_relations
@@ -847,7 +851,8 @@ def test_w1_gemm_and_outer_variants_bit_identical(opt, val):
     gout = torch.randn(N, 128, generator=gen)
     plan = mpgnn_amd.GraphPlan(g.edge_index.to(DEV), g.edge_type.to(DEV), N)
     res = {}
-    for v in (0, val):
+    base = _lib_default(opt)  # the product setting (0, or 16 rows in flight for option 37)
+    for v in (base, val):
         plan.set_option(opt, v)
         xg = g.x.to(DEV).requires_grad_(True)
         Wg, rg, bg = (t.to(DEV).requires_grad_(True) for t in (W, root, bias))
@@ -856,9 +861,9 @@ def test_w1_gemm_and_outer_variants_bit_identical(opt, val):
         torch.cuda.synchronize()
         res[v] = [out.detach(), xg.grad, Wg.grad, rg.grad, bg.grad]
     plan.set_option(opt, _lib_default(opt))
-    for k, a, b in zip(("out", "dx", "dW", "droot", "dbias"), res[val], res[0]):
+    for k, a, b in zip(("out", "dx", "dW", "droot", "dbias"), res[val], res[base]):
         assert torch.equal(a, b), k
-    assert res[0][0].abs().sum() > 0 and res[0][2].abs().sum() > 0
+    assert res[base][0].abs().sum() > 0 and res[base][2].abs().sum() > 0
 
 
 def _lib_default(opt):
