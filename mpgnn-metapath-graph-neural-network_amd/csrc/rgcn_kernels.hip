@@ -7364,7 +7364,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.u = p->opt.flat_u;
-        f.plan = p;
+        // no padded slot tables here: the transposed lists are mostly long groups (measured +0.5 µs)
         f.fd = &p->d.tx_f;
         f.max_pieces = p->tx_f.max_pieces;
         f.ngroups = p->tx_f.ngroups;
@@ -7401,7 +7401,7 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         FlatRun f{};
         f.wg_per_cu = p->opt.flat_wg_per_cu;
         f.u = p->opt.flat_u;
-        f.plan = p;
+        // no padded slot tables here: the transposed lists are mostly long groups (measured +0.5 µs)
         f.fd = &p->d.t_f;
         f.max_pieces = p->t_f.max_pieces;
         f.ngroups = p->t_f.ngroups;
