@@ -784,6 +784,12 @@ def pmc_traffic(workload, mode, feat, kernel_prefix):
 
 def main():
     args = parse()
+    # A/B hook: library option defaults "K=V,K=V" (include/mpgnn_rgcn.h enum mpgnn_option), set
+    # before any plan exists; recorded in the line's config
+    ab_opts = os.environ.get("MPGNN_BENCH_SET_OPT", "")
+    for kv in filter(None, ab_opts.split(",")):
+        k, v = kv.split("=")
+        _lib.set_option(int(k), int(v))
     _lib.set_option(24, 1 if args.gemm == "bf3" else 0)  # MPGNN_OPT_GEMM_BF3
     _lib.set_option(25, args.bwd_fused)  # MPGNN_OPT_BWD_FUSED
     if args.chunk_rows is not None:
@@ -1189,7 +1195,8 @@ def main():
                        "graph": {"nodes": g.num_nodes, "relations": g.num_relations, "edges": g.num_edges,
                                  "edges_per_step": edges_per_step, "segments_layer1": S,
                                  "multi_edge_segments_layer1": Sm},
-                       "parallelism": par, "shard_side": side if sharded else None},
+                       "parallelism": par, "shard_side": side if sharded else None,
+                       "library_options": ab_opts or None},
             "graph_replay": graph,
             "epoch_ms": round(epoch_ms, 3) if epoch_ms is not None else None,
             "epoch_graph": epoch_graph,

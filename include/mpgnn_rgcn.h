@@ -456,7 +456,12 @@ enum mpgnn_option {
                                     group's chunk (descriptor, positions' values and rows) from per-slot padded
                                     tables built once per plan and list, in one round of vector loads (C3:
                                     means 18.5 -> 17.6 µs, combine 24.9 -> 24.2 µs); 0 the scalar chunk-range
-                                    hops; sums bit-identical */
+                                    hops; sums bit-identical */,
+    MPGNN_OPT_SINGLE_FOLD = 39   /* the fused mode-SINGLE layer (single_bf3_kernel, F_in in {64, 128}, F_out =
+                                    128): 1 computes the relation's multi-edge segment means inside the GEMM
+                                    launch (the means kernel's arithmetic: 32-edge pieces in order) instead of a
+                                    separate means launch; 0 the two launches; outputs and saved means
+                                    bit-identical */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };

@@ -2323,6 +2323,14 @@ struct SingleBf3Args {
     const float* H;       // compact means, row m - m_lo
     const int* node_map;  // [N]: s_src + 1 (x row), s_src (< 0: Hm row), 0 (no segment)
     int m_lo, m_rows, N;
+    // non-null (round 6, MPGNN_OPT_SINGLE_FOLD): the mean half computes a multi-edge segment's
+    // mean itself from the compact lists — Σ over 32-edge pieces (each summed in edge order from
+    // 0.0f) in piece order, / cnt: the means kernel's exact arithmetic — instead of reading H;
+    // H_out (nullable, training) receives those rows for the backward
+    const int* m_ptr;
+    const int* em_col;
+    const int* m_cnt;
+    float* H_out;
     const float* W;       // [K][128]
     const float* root;    // [K][128]
     const float* bias;    // nullable [128]
@@ -2355,6 +2363,40 @@ struct SingleBf3 {
     }
     // x rows (x half) or mean rows (mean half: x row, compact mean row, or zeros) of item it;
     // indices are clamped into the tables: a bad map cannot fault
+    // the fold of one multi-edge segment (global compact index mg) at float4 column c4: the
+    // segment means kernel's sums (32-edge pieces, each from 0.0f in edge order, added in piece
+    // order from 0.0f), then / cnt (IEEE); four edges' rows in flight
+    __device__ static __forceinline__ float4 fold_mean(const SingleBf3Args& a, int mg, int c4) {
+        const int e0 = a.m_ptr[mg], e1 = a.m_ptr[mg + 1];
+        const float d = (float)a.m_cnt[mg];
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int ps = e0; ps < e1; ps += 32) {
+            const int pe = min(ps + 32, e1);
+            float4 pc = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int e = ps; e < pe; e += 4) {
+                int src[4];
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) src[u] = a.em_col[min(e + u, pe - 1)];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    v[u] = *reinterpret_cast<const float4*>(a.x + (size_t)min(max(src[u], 0), a.N - 1) * K + c4);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (e + u < pe) {
+                        pc.x += v[u].x;
+                        pc.y += v[u].y;
+                        pc.z += v[u].z;
+                        pc.w += v[u].w;
+                    }
+            }
+            acc.x += pc.x;
+            acc.y += pc.y;
+            acc.z += pc.z;
+            acc.w += pc.w;
+        }
+        return make_float4(acc.x / d, acc.y / d, acc.z / d, acc.w / d);
+    }
     __device__ static __forceinline__ void issue(const SingleBf3Args& a, int it, bool mh, int t, Rows& q) {
 #pragma unroll
         for (int j = 0; j < WPT; ++j) {
@@ -2368,6 +2410,13 @@ struct SingleBf3 {
             } else {
                 const int m = q.mp[j];
                 zero = m == 0;
+                if (m < 0 && a.m_ptr != nullptr) {  // fold the multi-edge segment's mean here
+                    const int mg = -m - 1;
+                    q.v[j] = fold_mean(a, mg, c4);
+                    if (a.H_out != nullptr && it * 32 + e / W4 < a.N)
+                        *reinterpret_cast<float4*>(a.H_out + (size_t)(mg - a.m_lo) * K + c4) = q.v[j];
+                    continue;
+                }
                 base = m > 0 ? a.x + (size_t)min(m - 1, a.N - 1) * K
                              : a.H + (size_t)min(max(-m - 1 - a.m_lo, 0), max(a.m_rows - 1, 0)) * K;
                 if (zero) base = a.x;
@@ -6848,6 +6897,7 @@ static int32_t set_switch(Options& o, int32_t option, int64_t value) {
         case MPGNN_OPT_GEMM_W_IL: o.gemm_w_il = value != 0; return MPGNN_OK;
         case MPGNN_OPT_GEMM_W1: o.gemm_w1 = value != 0; return MPGNN_OK;
         case MPGNN_OPT_FLAT_PAD: o.flat_pad = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_SINGLE_FOLD: o.single_fold = value != 0; return MPGNN_OK;
         case MPGNN_OPT_FLAT_U:
             if (value != 8 && value != 16 && value != 32) return arg_error("MPGNN_OPT_FLAT_U must be 8, 16 or 32");
             o.flat_u = (int)value;
@@ -6885,6 +6935,7 @@ static bool get_switch(const Options& o, int32_t option, int64_t* value) {
         case MPGNN_OPT_OUTER_VARIANT: *value = o.outer_variant; return true;
         case MPGNN_OPT_FLAT_U: *value = o.flat_u; return true;
         case MPGNN_OPT_FLAT_PAD: *value = o.flat_pad; return true;
+        case MPGNN_OPT_SINGLE_FOLD: *value = o.single_fold; return true;
         case MPGNN_OPT_GEMM_SWITCH_COST: *value = o.gemm_switch_cost; return true;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = o.flat_wg_per_cu; return true;
         default: return false;
@@ -7130,7 +7181,12 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
             sa.relu = act == MPGNN_ACT_RELU;
             sa.out = out;
             const int n_gi = (int)((p->N + 31) / 32);
-            {
+            if (o.single_fold) {  // the means inside the layer's GEMM launch (no means launch)
+                sa.m_ptr = p->d.m_ptr;
+                sa.em_col = p->d.em_col;
+                sa.m_cnt = p->d.m_cnt;
+                sa.H_out = h_save;
+            } else {
                 TimedLaunch tl(MPGNN_K_MEAN, strm);
                 st = run_means_multi(p, s, x, F_in, H, reinterpret_cast<float*>(ws + w.pseg), exact, strm);
                 if (st != MPGNN_OK) return st;

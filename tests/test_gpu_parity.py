@@ -866,6 +866,44 @@ def test_w1_gemm_and_outer_variants_bit_identical(opt, val):
     assert res[base][0].abs().sum() > 0 and res[base][2].abs().sum() > 0
 
 
+@pytest.mark.parametrize("f_in", [128, 64])
+def test_single_fold_bit_identical(f_in):
+    """MPGNN_OPT_SINGLE_FOLD (39): the fused mode-SINGLE layer computing the relation's multi-edge
+    segment means inside its GEMM launch (32-edge pieces added in order, / cnt) against the means
+    launch + GEMM: forward and every gradient (dW reads the saved means the fold writes) bit for
+    bit, on a relation with hub segments of 33, 40 (two pieces) and 600 edges (> 16 pieces: the
+    means kernel's split rows) and a ragged last node tile."""
+    g = data.synthetic_graph(3001, 5, 12, feat_dim=f_in, seed=41)
+    rng = np.random.default_rng(5)
+    hubs = [(7, 600), (11, 40), (13, 33)]
+    n1 = np.concatenate([np.full(k, v) for v, k in hubs])
+    n2 = rng.integers(0, g.num_nodes, size=n1.size)
+    ei = torch.cat([g.edge_index, torch.from_numpy(np.stack([n1, n2]))], 1)
+    et = torch.cat([g.edge_type, torch.full((n1.size,), 2, dtype=torch.int64)])
+    N = g.num_nodes
+    gen = torch.Generator().manual_seed(f_in)
+    W = (torch.rand(f_in, 128, generator=gen) - 0.5) * 0.1
+    root = (torch.rand(f_in, 128, generator=gen) - 0.5) * 0.1
+    bias = torch.rand(128, generator=gen) - 0.5
+    gout = torch.randn(N, 128, generator=gen)
+    plan = mpgnn_amd.GraphPlan(ei.to(DEV), et.to(DEV), N)
+    res = {}
+    for v in (0, 1):
+        plan.set_option(39, v)
+        xg = g.x.to(DEV).requires_grad_(True)
+        Wg, rg, bg = (t.to(DEV).requires_grad_(True) for t in (W, root, bias))
+        out = rgcn_conv(xg, Wg, rg, bg, plan, MODE_SINGLE, relation=2, activation="relu")
+        out.backward(gout.to(DEV))
+        with torch.no_grad():
+            out_inf = rgcn_conv(g.x.to(DEV), Wg, rg, bg, plan, MODE_SINGLE, relation=2, activation="relu")
+        torch.cuda.synchronize()
+        res[v] = [out.detach(), out_inf, xg.grad, Wg.grad, rg.grad, bg.grad]
+    plan.set_option(39, _lib_default(39))
+    for k, a, b in zip(("out", "out no-grad", "dx", "dW", "droot", "dbias"), res[1], res[0]):
+        assert torch.equal(a, b), k
+    assert res[0][0].abs().sum() > 0 and res[0][3].abs().sum() > 0
+
+
 def _lib_default(opt):
     from mpgnn_amd import _lib
     return _lib.get_option(opt)
