@@ -20,7 +20,8 @@ import numpy as np
 import torch
 
 __all__ = ["shard_ranges", "edge_balanced_ranges", "rank_slice", "metapath_fanout", "best_metapaths",
-           "sharded_stack_forward", "ShardGradReducer", "gather_owned_rows", "group_ranges"]
+           "sharded_stack_forward", "sharded_stack_forwards", "ShardGradReducer", "gather_owned_rows",
+           "group_ranges"]
 
 
 def edge_balanced_ranges(gathered: np.ndarray | torch.Tensor, num_nodes: int, world: int) -> list[tuple[int, int]]:
@@ -298,33 +299,79 @@ def sharded_stack_forward(convs, x: torch.Tensor, edge_index: torch.Tensor, edge
     output is complete for its rows and zero elsewhere, every rank gathers from all rows, so each
     layer ends with an all-gather of the rows (same bytes as the reduce-scatter) and every
     per-rank pass — means, transform, combine — shrinks with the shard instead of only the edges."""
+    return sharded_stack_forwards(convs, x, edge_index, edge_type, ranges, group, steps=1, inflight=1,
+                                  activation=activation, shard_side=shard_side)[0]
+
+
+def _stack_pass(convs, x, edge_index, edge_type, ranges, group, activation, shard_side, outs, k):
+    """One pass of sharded_stack_forward as a generator: it yields right after issuing each
+    layer's collective asynchronously and waits for that collective only when resumed, so the
+    scheduler in sharded_stack_forwards can run another pass's layer meanwhile. Every tensor a
+    pending collective reads or writes stays referenced here until its wait."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     lo, hi = ranges[rank]
     idx, m = _padded_index(ranges, x.device)
     n = x.shape[0]
+    act = (lambda t: torch.relu(t)) if activation == "relu" else (lambda t: t)
     h = x
     if shard_side == "rows":
         for conv in convs:
             part = conv(h, edge_index, edge_type, shard=(lo, hi), group=None, shard_side="rows")
             slab = part.new_zeros(m, part.shape[1])
-            slab[:hi - lo] = torch.relu(part[lo:hi]) if activation == "relu" else part[lo:hi]
+            slab[:hi - lo] = act(part[lo:hi])
             full = part.new_empty(world * m, part.shape[1])
-            dist.all_gather_into_tensor(full, slab, group=group)
+            work = dist.all_gather_into_tensor(full, slab, group=group, async_op=True)
+            yield
+            work.wait()
             h = full.index_select(0, idx)
-        return h
+        outs[k] = h
+        return
     for conv in convs:
         part = conv(h, edge_index, edge_type, shard=(lo, hi), group=None)  # partial sums, all rows
         f = part.shape[1]
         pad = part.new_empty(world * m, f)
         pad.index_copy_(0, idx, part)
         mine = part.new_empty(m, f)
-        dist.reduce_scatter_tensor(mine, pad, group=group)
+        work = dist.reduce_scatter_tensor(mine, pad, group=group, async_op=True)
+        yield
+        work.wait()
         h = part.new_empty(n, f)  # only [lo, hi) is written: the only rows the next layer reads
-        h[lo:hi] = torch.relu(mine[:hi - lo]) if activation == "relu" else mine[:hi - lo]
+        h[lo:hi] = act(mine[:hi - lo])
     slab = h.new_zeros(m, h.shape[1])
     slab[:hi - lo] = h[lo:hi]
     full = h.new_empty(world * m, h.shape[1])
-    dist.all_gather_into_tensor(full, slab, group=group)
-    return full.index_select(0, idx)
+    work = dist.all_gather_into_tensor(full, slab, group=group, async_op=True)
+    yield
+    work.wait()
+    outs[k] = full.index_select(0, idx)
+
+
+def sharded_stack_forwards(convs, x: torch.Tensor, edge_index: torch.Tensor, edge_type: torch.Tensor,
+                           ranges: list[tuple[int, int]], group=None, steps: int = 1, inflight: int = 2,
+                           activation: str | None = "relu", shard_side: str = "gathered") -> list:
+    """``steps`` independent passes of ``sharded_stack_forward`` over the same input with up to
+    ``inflight`` of them in flight: a pass issues its layer's collective asynchronously and the
+    next pass computes its own layer while that collective runs (RCCL on its own HIP stream; the
+    compute stream waits for a collective only where the pass that needs its rows continues) —
+    the inference-serving overlap of communication with computation. Each pass performs exactly
+    the single-pass operations in the single-pass order: outputs bit-identical to
+    ``sharded_stack_forward`` (tests/test_distributed_gloo.py). Passes run round robin in the same
+    order on every rank, so the collectives match."""
+    from collections import deque
+    outs = [None] * steps
+    live = deque()
+    started = 0
+    while started < steps or live:
+        while len(live) < max(1, inflight) and started < steps:
+            live.append(_stack_pass(convs, x, edge_index, edge_type, ranges, group, activation, shard_side, outs,
+                                    started))
+            started += 1
+        gen = live.popleft()
+        try:
+            next(gen)
+            live.append(gen)
+        except StopIteration:
+            pass
+    return outs

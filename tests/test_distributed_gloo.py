@@ -346,7 +346,14 @@ def _stack_worker(rank, world, port, q, side="gathered"):
             ref64 = torch.relu(orc.rgcn_forward(ref64, g.edge_index, g.edge_type, W.double(), root.double(),
                                                 bias.double()))
         from tests._bars import passes
-        q.put((rank,) + passes(out, ref, ref64))
+        ok, msg = passes(out, ref, ref64)
+        # three passes with two in flight (collectives overlapped with the other pass's layer):
+        # bit-identical to the single pass
+        many = mpgnn_amd.distributed.sharded_stack_forwards(convs, g.x, g.edge_index, g.edge_type, ranges,
+                                                            steps=3, inflight=2, shard_side=side)
+        if not all(torch.equal(o, out) for o in many):
+            ok, msg = False, "pipelined passes differ from the single pass"
+        q.put((rank, ok, msg))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover
         import traceback
