@@ -3,7 +3,8 @@
 trace of `bench.py --epoch-steps 0 --loop-epochs 0` (every dispatch of the process).
 
 The steps are found as runs of the layer's launch pattern (means, GEMM, combine per layer); the
-timed region is the first block of --steps consecutive steps after the warm-up. Prints per-role
+timed region is the --steps steps right before bench.py's per-kernel HIP-event pass (whose steps
+show a gap of several us before every kernel). Prints per-role
 average duration, the average gap before each role, and the step time as the trace sees it
 (first start to last end over the block / steps).
 usage: python scripts/step_gaps.py <run_kernel_trace.csv> [--steps 20] [--json out.json]"""
@@ -17,6 +18,7 @@ ap.add_argument("trace")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--layers", type=int, default=3)
 ap.add_argument("--json", default=None)
+ap.add_argument("--event-gap-us", type=float, default=4.0, help="median kernel gap of an event-pass step")
 ap.add_argument("--idle-us", type=float, default=40.0, help="GPU idle time that ends a run of steps")
 a = ap.parse_args()
 
@@ -45,20 +47,32 @@ while i + n <= len(seq):
         i += 1
 # runs of consecutive steps, cut where the GPU idled > --idle-us between two steps (a host sync:
 # bench.py syncs after its pre-warm batches of 10, after the warm-up and after the timed region)
-runs, cur = [], [blocks[0]] if blocks else []
+runs, cur, after = [], ([blocks[0]] if blocks else []), []
 for b in blocks[1:]:
     idle = (seq[b][1] - seq[cur[-1] + n - 1][2]) / 1e3
     if b == cur[-1] + n and idle < a.idle_us:
         cur.append(b)
     else:
         runs.append(cur)
+        after.append(idle)
         cur = [b]
 if cur:
     runs.append(cur)
-runs = [r for r in runs if len(r) >= a.steps]
-# bench.py: plan + first step, pre-warm (runs of 10), warm-up, then the timed region = the first
-# run of >= --steps steps (the per-kernel event pass after it is the second)
-timed = runs[0][:a.steps]
+    after.append(None)
+# bench.py: plan + first step, pre-warm (batches of 10 with a host sync between them), warm-up,
+# the timed region, then the per-kernel event pass (--steps steps with a HIP event pair around
+# every kernel: each kernel then waits ~8 us behind its events). The timed region is the --steps
+# steps right before the first event-pass step (median gap between its kernels > --event-gap-us).
+def med_gap(b):
+    return st.median((seq[b + k][1] - seq[b + k - 1][2]) / 1e3 for k in range(1, n))
+
+
+ev = next((j for j, b in enumerate(blocks) if j >= a.steps and med_gap(b) > a.event_gap_us), None)
+if ev is None:
+    raise SystemExit("no per-kernel event pass found in the trace")
+timed = blocks[ev - a.steps:ev]
+if any(timed[j + 1] != timed[j] + n for j in range(len(timed) - 1)):
+    raise SystemExit("the steps before the event pass are not back to back")
 names = ["means L%d" % (k // 3) if k % 3 == 0 else ("gemm L%d" % (k // 3) if k % 3 == 1 else "combine L%d" % (k // 3))
          for k in range(n)]
 dur = {k: [] for k in range(n)}
