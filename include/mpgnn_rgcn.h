@@ -239,6 +239,28 @@ int32_t mpgnn_linear_fwd(const float* x, int64_t N, int32_t F, const float* weig
                          int32_t act, float* out, void* stream);
 int32_t mpgnn_linear_dgrad(const float* grad_out, int64_t N, int32_t O, const float* weight, int32_t F, float* grad_x,
                            void* stream);
+/* mpgnn_linear_dgrad with the ReLU backward of the layer that produced the head's input x [N,F]
+ * fused (grad_x = x <= 0 ? 0 : grad_out @ weight): Net.lin over the last conv's ReLU output. */
+int32_t mpgnn_linear_dgrad_relu_in(const float* grad_out, int64_t N, int32_t O, const float* weight, int32_t F,
+                                   const float* x, float* grad_x, void* stream);
+
+/* The loops' optimizer step (Adam(lr=0.01, weight_decay=5e-4), main.py:1119 / main_rgcn.py:454)
+ * over n <= 24 fp32 parameter tensors in ONE launch, replacing torch.optim.Adam(fused=True)'s
+ * _foreach_add_(steps, 1) + _fused_adam_ pair: for each tensor, step += 1 (float, device
+ * scalar), then ATen's fused update (L2 decay folded into the gradient, moments in double rounded
+ * to float, bias corrections 1 - beta^step in double; no amsgrad / maximize / grad scaling).
+ * Pointers 16-byte aligned (else MPGNN_ERR_UNSUPPORTED, nothing launched); `arrive`: a device
+ * int32 the caller zeroes once and keeps for the optimizer (the launch leaves it zero). */
+typedef struct mpgnn_adam_tensor {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    float* step;
+    int64_t numel;
+} mpgnn_adam_tensor;
+int32_t mpgnn_adam_step(const mpgnn_adam_tensor* tensors, int32_t n, double lr, double beta1, double beta2,
+                        double weight_decay, double eps, int32_t* arrive, void* stream);
 
 /* Bytes of scratch the fwd/bwd calls need (caller allocates, e.g. torch.empty(uint8)). */
 int32_t mpgnn_rgcn_workspace_bytes(const mpgnn_plan* plan, int32_t mode, int64_t relation,
@@ -309,6 +331,20 @@ int32_t mpgnn_rgcn_bwd_accumulate(const mpgnn_plan* plan, int32_t mode, int64_t 
                                   int64_t row_lo, int64_t row_hi,
                                   float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
                                   void* workspace, void* stream);
+
+/* mpgnn_rgcn_bwd (accumulate = 0) / mpgnn_rgcn_bwd_accumulate (1) for a layer whose input x is
+ * the ReLU output of the previous layer (Net, model.py:144-146: F.relu(conv(...)) feeding the
+ * next conv): grad_x is written with that ReLU's backward fused — grad_x[i] = x[i] <= 0 ? 0 :
+ * (the gradient w.r.t. x)[i] (threshold_backward's rule) — i.e. the gradient w.r.t. the previous
+ * layer's pre-activation output, so that layer's own ReLU backward launch is skipped. Used by
+ * Net's forward for its internal activations only (no caller sees the masked gradient). */
+int32_t mpgnn_rgcn_bwd_relu_in(const mpgnn_plan* plan, int32_t mode, int64_t relation,
+                               int32_t num_relations, const float* x, int32_t F_in,
+                               const float* weight, const float* root, int32_t F_out,
+                               const float* h_save, const float* grad_out,
+                               int64_t row_lo, int64_t row_hi,
+                               float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
+                               void* workspace, void* stream, int32_t accumulate);
 
 /* --- score function --------------------------------------------------------
  * The metapath-candidate score of the reference, OutputLayer.forward non-bag branch
@@ -461,12 +497,15 @@ enum mpgnn_option {
                                     128): 1 computes the relation's multi-edge segment means inside the GEMM
                                     launch (the means kernel's arithmetic: 32-edge pieces in order) instead of a
                                     separate means launch; 0 the two launches; outputs and saved means
-                                    bit-identical */
+                                    bit-identical */,
+    MPGNN_OPT_ADAM_CONTRACT = 40 /* process-wide: mpgnn_adam_step's double multiply-adds fused (1, default: the
+                                    contraction clang's default HIP flags give ATen's kernel) or each product
+                                    rounded (0); pinned bit-for-bit against torch by the GPU tests */
     /* ids 1, 2, 4, 6-10, 12-18, 21-23: round-1 profiling switches and measured-slower kernel variants,
        withdrawn in round 2; mpgnn_set_option refuses them with MPGNN_ERR_ARG */
 };
-/* Process defaults. The kernel switches (every option except TIMING_MASK, PLAN_THREADS and
- * CHUNK_ROWS) are PER PLAN: a plan copies the defaults when it is created and is changed only by
+/* Process defaults. The kernel switches (every option except TIMING_MASK, PLAN_THREADS,
+ * CHUNK_ROWS and ADAM_CONTRACT) are PER PLAN: a plan copies the defaults when it is created and is changed only by
  * mpgnn_plan_set_option, so no launch reads process-wide state; mpgnn_set_option of a switch
  * therefore affects plans created afterwards. TIMING_MASK (profiling) and PLAN_THREADS /
  * CHUNK_ROWS (plan build parameters, read when a plan is built) stay process-wide. */

@@ -56,6 +56,12 @@ class PlanInfo(ctypes.Structure):
     ]
 
 
+class AdamTensor(ctypes.Structure):
+    """mpgnn_adam_tensor of include/mpgnn_rgcn.h."""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("step", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+
 # (name, restype, argtypes) — exactly the symbols of include/mpgnn_rgcn.h
 _P = ctypes.c_void_p
 _I32, _I64 = ctypes.c_int32, ctypes.c_int64
@@ -87,11 +93,16 @@ SIGNATURES = [
                               _P, _P, _P, _P, _P, _P]),
     ("mpgnn_rgcn_bwd_accumulate", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _I32, _P, _P, _I64, _I64,
                                          _P, _P, _P, _P, _P, _P]),
+    ("mpgnn_rgcn_bwd_relu_in", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _I32, _P, _P, _I64, _I64,
+                                      _P, _P, _P, _P, _P, _P, _I32]),
     ("mpgnn_relu_bwd", _I32, [_P, _P, _I64, _P, _P]),
     ("mpgnn_linear_wgrad_workspace_bytes", _I32, [_I64, _I32, _I32, _PI64]),
     ("mpgnn_linear_wgrad", _I32, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P]),
     ("mpgnn_linear_fwd", _I32, [_P, _I64, _I32, _P, _I32, _P, _I32, _P, _P]),
     ("mpgnn_linear_dgrad", _I32, [_P, _I64, _I32, _P, _I32, _P, _P]),
+    ("mpgnn_linear_dgrad_relu_in", _I32, [_P, _I64, _I32, _P, _I32, _P, _P, _P]),
+    ("mpgnn_adam_step", _I32, [ctypes.POINTER(AdamTensor), _I32, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                ctypes.c_double, ctypes.c_double, _P, _P]),
     ("mpgnn_score_argmax", _I32, [_P, _I64, _P, _P, _P, _I64, _P, _P, _P, _P]),
     ("mpgnn_score_argmax_bwd", _I32, [_P, _I64, _P, _P, _P, _P, _P, _P, _P]),
     ("mpgnn_score_argmax_multi", _I32, [_P, _I64, _P, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -120,6 +131,7 @@ SIGNATURES = [
 KERNEL_KINDS = {"seg_fwd": 0, "row_fwd": 1, "seg_dgrad": 2, "row_dx": 3, "outer": 4, "reduce": 5, "mean": 6,
                 "piece": 7, "final": 8}
 OPT_EXACT_ORDER = 0
+OPT_ADAM_CONTRACT = 40
 ACT_NONE, ACT_RELU = 0, 1
 
 

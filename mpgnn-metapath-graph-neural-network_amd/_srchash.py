@@ -6,7 +6,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SOURCES = ("csrc/Makefile", "csrc/plan.cpp", "csrc/plan_internal.h", "csrc/io.cpp", "csrc/rgcn_kernels.hip",
-           "csrc/plan_device.hip", "csrc/score_kernels.hip", "../include/mpgnn_rgcn.h")
+           "csrc/plan_device.hip", "csrc/score_kernels.hip", "csrc/optim_kernels.hip", "../include/mpgnn_rgcn.h")
 STAMP = os.path.join(HERE, "libmpgnn_rgcn.so.srchash")
 
 

@@ -33,6 +33,9 @@
 
 namespace mpgnn {
 
+int adam_contract_get();  // optim_kernels.hip (MPGNN_OPT_ADAM_CONTRACT)
+void adam_contract_set(int v);
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kThreads = 256;  // 4 waves of 64
@@ -1053,6 +1056,8 @@ struct RelGemmArgs {
     int relu;             // CAT epilogue: fused ReLU
     const int* wg_items;  // nullable (rel_gemm_bf3_kernel): [G + 1] first item of each range
     int wg_cus;           // > 0 with wg_items: G = 2·wg_cus, ranges 2c and 2c+1 belong to one CU (below)
+    unsigned* zero;       // nullable (rel_gemm_bf3_kernel): zero_words words zeroed by the launch — the
+    int zero_words;       // next gather-sum's piece counters (dgrad -> grad_x), instead of a memset launch
 #ifdef MPGNN_STAMPS
     unsigned long long* stamps;
 #endif
@@ -2021,6 +2026,9 @@ struct RelGemmBf3 {
 template <int KB, bool DGRAD, bool IL = false>
 __global__ __launch_bounds__(kThreads, 2) void rel_gemm_bf3_kernel(RelGemmArgs a) {
     extern __shared__ __bf16 smem_bf[];
+    if (a.zero != nullptr)  // a few words, one store per thread at most (read by a later launch only)
+        for (int i = (int)(blockIdx.x * kThreads + threadIdx.x); i < a.zero_words; i += (int)(gridDim.x * kThreads))
+            a.zero[i] = 0u;
     if constexpr (IL) RelGemmBf3<KB, DGRAD>::run_il(a, smem_bf);
     else RelGemmBf3<KB, DGRAD>::run(a, smem_bf);
 }
@@ -3096,6 +3104,9 @@ struct FlatArgs {
     const int4* pad_desc;
     const int* pad_val;
     const int* pad_row;
+    // nullable (grad_x, round 6): the ReLU backward of the layer that produced this layer's input
+    // fused into the row finish — out = mask > 0 ? v : 0 with mask = that input (relu_bwd_f)
+    const float* mask;
 };
 
 // The finishing step of a complete row: / cnt (IEEE), + bias on own rows, fused ReLU.
@@ -3104,16 +3115,19 @@ __device__ __forceinline__ void flat_finish_store(const FlatArgs& a, int rr, flo
                                                   const float (&acc)[T][V], int lane) {
     const bool addb = a.bias != nullptr && rr >= a.lo && rr < a.hi;
     float* dst = a.out + (size_t)(rr - a.row_off) * a.F;
+    const bool msk = a.mask != nullptr;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const int col = (t * 64 + lane) * V;
         if (col < a.F) {
-            float o[V];
+            float o[V], mv[V];
+            if (msk) vload<V>(a.mask + (size_t)(rr - a.row_off) * a.F + col, mv);
 #pragma unroll
             for (int k = 0; k < V; ++k) {
                 o[k] = div ? acc[t][k] / d : acc[t][k];
                 if (addb) o[k] = o[k] + bb[t][k];
                 if (a.relu) o[k] = relu_f(o[k]);
+                if (msk) o[k] = relu_bwd_f(o[k], mv[k]);
             }
             vstore_sc1<V>(dst, col, o);
         }
@@ -3354,6 +3368,7 @@ struct FinalArgs {
     float* out;
     const float* dummy;    // any valid float row
     int relu;              // fused activation after the bias
+    const float* mask;     // nullable: FlatArgs::mask
 };
 
 // one wave, work index w (mode 0: split row k0 + w; mode 1: row r_lo + w)
@@ -3428,6 +3443,12 @@ __device__ __forceinline__ void finalize_row(const FinalArgs& a, int w, int lane
                 if (has_ex) o[q] = o[q] + ex[t][q];
                 if (has_b) o[q] = o[q] + bb[t][q];
                 if (a.relu) o[q] = relu_f(o[q]);
+            }
+            if (a.mask != nullptr) {
+                float mv[V];
+                vload<V>(a.mask + (size_t)(row - a.row_off) * F + col, mv);
+#pragma unroll
+                for (int q = 0; q < V; ++q) o[q] = relu_bwd_f(o[q], mv[q]);
             }
             vstore<V>(a.out + (size_t)(row - a.row_off) * F + col, o);
         }
@@ -5283,7 +5304,8 @@ __global__ __launch_bounds__(kThreads) void linear_small_fwd_kernel(const float*
 // grad of a Linear head's input: gx[i][f] = Σ_o g[i][o]·W[o][f] for O <= 8 (g @ W), float4 columns
 __global__ __launch_bounds__(kThreads) void linear_small_dgrad_kernel(const float* __restrict__ g, int N, int O,
                                                                       const float* __restrict__ W, int F,
-                                                                      float* __restrict__ gx) {
+                                                                      float* __restrict__ gx,
+                                                                      const float* __restrict__ mask) {
     const int F4 = F / 4;
     const int64_t total = (int64_t)N * F4;
     for (int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x; e < total; e += (int64_t)gridDim.x * kThreads) {
@@ -5296,6 +5318,11 @@ __global__ __launch_bounds__(kThreads) void linear_small_dgrad_kernel(const floa
             acc.y = fmaf(gv, wv.y, acc.y);
             acc.z = fmaf(gv, wv.z, acc.z);
             acc.w = fmaf(gv, wv.w, acc.w);
+        }
+        if (mask != nullptr) {  // the ReLU backward of the layer that produced the head's input, fused
+            const float4 m = *reinterpret_cast<const float4*>(mask + (size_t)i * F + f);
+            acc = make_float4(relu_bwd_f(acc.x, m.x), relu_bwd_f(acc.y, m.y), relu_bwd_f(acc.z, m.z),
+                              relu_bwd_f(acc.w, m.w));
         }
         *reinterpret_cast<float4*>(gx + (size_t)i * F + f) = acc;
     }
@@ -6009,7 +6036,9 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
                        int K, const float* W, const float* Wroot, int trans, int N, float* Y, float* Yroot,
                        int64_t row_lo, int64_t row_hi, float* H, float* Pseg, bool exact, int kind,
                        hipStream_t strm, const float* Hsrc = nullptr, const int* root_map = nullptr,
-                       const float* root_bias = nullptr, int root_relu = 0) {
+                       const float* root_bias = nullptr, int root_relu = 0, unsigned* zero = nullptr,
+                       int zero_words = 0, bool* zeroed = nullptr) {
+    if (zeroed != nullptr) *zeroed = false;
     const int m_lo = s.m_lo;
     const int n_rel = s.t_hi - s.t_lo;
     const int n_root = (Wroot != nullptr) ? (int)((row_hi - row_lo + kTileRows - 1) / kTileRows) : 0;
@@ -6083,6 +6112,11 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
             const bool pairs = p->opt.gemm_cu_pairs && G == cu_count() * 2 && cu_count() % 8 == 0;
             r.wg_items = gemm_ranges(p, r.t_lo, r.n_rel, r.n_root, G, pairs, strm);
             r.wg_cus = (pairs && r.wg_items != nullptr) ? cu_count() : 0;
+        }
+        if (zero != nullptr && zero_words > 0 && p->opt.gemm_bf3 && (K == 64 || K == 128) && r.node_map == nullptr) {
+            r.zero = zero;  // launch_rel_gemm takes rel_gemm_bf3_kernel for these shapes
+            r.zero_words = zero_words;
+            if (zeroed != nullptr) *zeroed = true;
         }
         TimedLaunch tl(kind, strm);
         launch_rel_gemm(r, K, gather_kind == 1, p->opt, strm);
@@ -6474,6 +6508,7 @@ struct FlatRun {
     int u = 16;           // the plan's MPGNN_OPT_FLAT_U: rows in flight per wave (8, 16, 32)
     int ngroups = 0;      // groups of the whole list (the padded slot tables cover them all)
     const mpgnn_plan* plan = nullptr;  // non-null with MPGNN_OPT_FLAT_PAD: padded slot tables
+    const float* mask = nullptr;       // FlatArgs::mask
 };
 
 // flat_rows_kernel's padded slot tables of one (list, value table) pair (FlatArgs::pad_desc):
@@ -6575,6 +6610,8 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
         a.out = f.out;
         a.carry = f.carry;
         a.relu = f.final_mode == 0 ? f.relu : 0;
+        // mode 0 finishes rows here; mode 1 leaves them to the finalize (which adds extra rows)
+        a.mask = f.final_mode == 0 ? f.mask : nullptr;
         if (f.final_mode == 0 && f.arrive != nullptr) {
             a.arrive = f.arrive;
             a.row_split = f.fd->row_split;
@@ -6609,6 +6646,7 @@ static int32_t run_flat(const FlatRun& f, hipStream_t strm) {
     b.out = f.out;
     b.dummy = f.out;
     b.relu = f.relu;
+    b.mask = f.mask;
     const int nrows = f.final_mode == 0 ? f.k_hi - f.k_lo : f.r_hi - f.r_lo;
     if (nrows <= 0 || (f.final_mode == 0 && f.arrive != nullptr && f.g_hi > f.g_lo)) return MPGNN_OK;
     TimedLaunch tl(MPGNN_K_FINAL, strm);
@@ -6796,21 +6834,40 @@ int32_t mpgnn_linear_fwd(const float* x, int64_t N, int32_t F, const float* weig
     return hip_check(hipGetLastError(), "linear_small_fwd_kernel launch");
 }
 
-int32_t mpgnn_linear_dgrad(const float* grad_out, int64_t N, int32_t O, const float* weight, int32_t F, float* grad_x,
-                           void* stream) {
+static int32_t linear_dgrad_impl(const float* grad_out, int64_t N, int32_t O, const float* weight, int32_t F,
+                                 float* grad_x, const float* mask, void* stream) {
     if (N < 0 || N > INT32_MAX || F <= 0 || O <= 0) return arg_error("mpgnn_linear_dgrad: bad N, F or O");
     const bool gemm = F == 128 && O == 128 && default_options().gemm_bf3;
     const bool small = O <= kLinSmallO && F % 4 == 0;
     if (!gemm && !small) return MPGNN_ERR_UNSUPPORTED;
     if (N == 0) return MPGNN_OK;
     if (!grad_out || !weight || !grad_x) return arg_error("mpgnn_linear_dgrad: NULL pointer");
-    if (((reinterpret_cast<uintptr_t>(grad_out) | reinterpret_cast<uintptr_t>(weight) | reinterpret_cast<uintptr_t>(grad_x)) & 15) != 0)
+    if (((reinterpret_cast<uintptr_t>(grad_out) | reinterpret_cast<uintptr_t>(weight) | reinterpret_cast<uintptr_t>(grad_x) |
+          reinterpret_cast<uintptr_t>(mask)) & 15) != 0)
         return arg_error("mpgnn_linear_dgrad: pointers must be 16-byte aligned");
     hipStream_t strm = static_cast<hipStream_t>(stream);
-    if (gemm) return linear_gemm128(grad_out, N, weight, false, grad_x, strm);
+    if (gemm) {
+        int32_t st = linear_gemm128(grad_out, N, weight, false, grad_x, strm);
+        if (st != MPGNN_OK || mask == nullptr) return st;
+        const int64_t n = N * F;
+        hipLaunchKernelGGL(relu_bwd_kernel, dim3((unsigned)std::min<int64_t>((n + kThreads - 1) / kThreads, 4096)),
+                           dim3(kThreads), 0, strm, grad_x, mask, n, grad_x, 1);
+        return hip_check(hipGetLastError(), "relu_bwd_kernel (linear dgrad mask) launch");
+    }
     hipLaunchKernelGGL(linear_small_dgrad_kernel, dim3(linear_grid(N * (F / 4))), dim3(kThreads), 0, strm, grad_out, (int)N, O,
-                       weight, F, grad_x);
+                       weight, F, grad_x, mask);
     return hip_check(hipGetLastError(), "linear_small_dgrad_kernel launch");
+}
+
+int32_t mpgnn_linear_dgrad(const float* grad_out, int64_t N, int32_t O, const float* weight, int32_t F, float* grad_x,
+                           void* stream) {
+    return linear_dgrad_impl(grad_out, N, O, weight, F, grad_x, nullptr, stream);
+}
+
+int32_t mpgnn_linear_dgrad_relu_in(const float* grad_out, int64_t N, int32_t O, const float* weight, int32_t F,
+                                   const float* x, float* grad_x, void* stream) {
+    if (N > 0 && x == nullptr) return arg_error("mpgnn_linear_dgrad_relu_in: NULL x");
+    return linear_dgrad_impl(grad_out, N, O, weight, F, grad_x, x, stream);
 }
 
 int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int32_t F, int32_t O, float* grad_weight,
@@ -6963,6 +7020,10 @@ int32_t mpgnn_set_option(int32_t option, int64_t value) {
                 return arg_error("MPGNN_OPT_CHUNK_ROWS must be 32..1024, a multiple of 32");
             g_chunk_rows = (int)value;
             return MPGNN_OK;
+        case MPGNN_OPT_ADAM_CONTRACT:
+            if (value != 0 && value != 1) return arg_error("MPGNN_OPT_ADAM_CONTRACT must be 0 or 1");
+            adam_contract_set((int)value);
+            return MPGNN_OK;
         default:
             return arg_error("unknown option " + std::to_string(option) +
                              " (measured-slower variants of round 1 were withdrawn: DESIGN.md §4)");
@@ -6983,6 +7044,7 @@ int32_t mpgnn_get_option(int32_t option, int64_t* value) {
         }
         case MPGNN_OPT_PLAN_THREADS: *value = g_plan_threads; return MPGNN_OK;
         case MPGNN_OPT_CHUNK_ROWS: *value = g_chunk_rows; return MPGNN_OK;
+        case MPGNN_OPT_ADAM_CONTRACT: *value = adam_contract_get(); return MPGNN_OK;
         default: return arg_error("unknown option " + std::to_string(option));
     }
 }
@@ -7394,10 +7456,17 @@ static int32_t rgcn_fwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
 // grad_x-style transposed gather: dx[j] = Σ_{edges (i, r, j) of the selection} G[seg] (+ Groot[j]
 // for own rows), over the flat / ragged / mode-SINGLE lists (used by mpgnn_rgcn_bwd and
 // mpgnn_rel_mean_bwd).
+// Where the piece counters of the augmented transposed list live in the carry region Pdx (F_in
+// floats per slot), 16-byte aligned; split_counter_bytes(p) of them.
+static unsigned* split_counters(const mpgnn_plan* p, float* Pdx, int F_in) {
+    return reinterpret_cast<unsigned*>(reinterpret_cast<char*>(Pdx) + align16((size_t)p->tx_f.nslots * F_in * sizeof(float)));
+}
+
 static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s, const float* G, const float* Groot,
                           int F_in, int64_t row_lo, int64_t row_hi, float* grad_x, float* Pdx, bool exact,
-                          hipStream_t strm) {
+                          hipStream_t strm, bool counters_zeroed = false, const float* mask = nullptr) {
     int32_t st = MPGNN_OK;
+    bool masked = mask == nullptr;  // the mask applied (fused into the flat list's row finish)
     RowSumArgs a{};
     a.N = (int)p->N;
     a.g.src = G;
@@ -7442,14 +7511,17 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         f.extra = Groot;
         f.lo = (int)row_lo;
         f.hi = (int)row_hi;
+        f.mask = mask;
+        masked = true;
         TimedLaunch tl(MPGNN_K_ROW_DX, strm);
         if (p->opt.flat_fuse_split && p->tx_f.nsplit > 0) {
             // piece counters behind the carry slots (ws_layout reserves them in the pdx region)
             // 16-byte aligned start and length: one fill launch (a ragged memset is two)
-            f.arrive = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(Pdx) +
-                                                   align16((size_t)p->tx_f.nslots * F_in * sizeof(float)));
-            st = hip_check(hipMemsetAsync(f.arrive, 0, split_counter_bytes(p), strm), "memset split counters");
-            if (st != MPGNN_OK) return st;
+            f.arrive = split_counters(p, Pdx, F_in);
+            if (!counters_zeroed) {  // else zeroed by the dgrad launch before this one (grad_x_part)
+                st = hip_check(hipMemsetAsync(f.arrive, 0, split_counter_bytes(p), strm), "memset split counters");
+                if (st != MPGNN_OK) return st;
+            }
         }
         st = run_flat(f, strm);
         if (st != MPGNN_OK) return st;
@@ -7522,6 +7594,13 @@ static int32_t run_grad_x(const mpgnn_plan* p, int32_t mode, const Selection& s,
         st = run_rowsum(p, a, pb, pe, k_lo, k_hi, Pdx, strm);
         if (st != MPGNN_OK) return st;
     }
+    if (!masked) {  // the other lists: the ReLU backward as one in-place pass after them
+        const int64_t n = (int64_t)p->N * F_in;
+        const int vec = ((reinterpret_cast<uintptr_t>(grad_x) | reinterpret_cast<uintptr_t>(mask)) & 15) == 0;
+        hipLaunchKernelGGL(relu_bwd_kernel, dim3((unsigned)std::min<int64_t>((n + kThreads - 1) / kThreads, 4096)),
+                           dim3(kThreads), 0, strm, grad_x, mask, n, grad_x, vec);
+        return hip_check(hipGetLastError(), "relu_bwd_kernel (grad_x mask) launch");
+    }
     return MPGNN_OK;
 }
 
@@ -7589,7 +7668,7 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
 static int32_t bwd_fused(const mpgnn_plan* p, int32_t mode, int32_t R, const float* x, const float* weight,
                          const float* root, const float* h_save, const float* grad_out, int64_t row_lo, int64_t row_hi,
                          float* grad_x, float* grad_weight, float* grad_root, float* grad_bias, const Selection& s,
-                         const WsLayout& w, char* ws, hipStream_t strm) {
+                         const WsLayout& w, char* ws, hipStream_t strm, const float* gx_mask) {
     const int n_rel = s.t32_hi - s.t32_lo;
     const int n_root = (int)((row_hi - row_lo + 31) / 32);
     const int n_items = n_rel + n_root;
@@ -7746,7 +7825,7 @@ static int32_t bwd_fused(const mpgnn_plan* p, int32_t mode, int32_t R, const flo
     }
     if (grad_x != nullptr)
         st = run_grad_x(p, mode, s, reinterpret_cast<float*>(ws + w.g), reinterpret_cast<float*>(ws + w.groot), 128,
-                        row_lo, row_hi, grad_x, reinterpret_cast<float*>(ws + w.pdx), false, strm);
+                        row_lo, row_hi, grad_x, reinterpret_cast<float*>(ws + w.pdx), false, strm, false, gx_mask);
     return st;
 }
 
@@ -7754,7 +7833,7 @@ static int32_t rgcn_bwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
                              int32_t F_in, const float* weight, const float* root, int32_t F_out,
                              const float* h_save, const float* grad_out, int64_t row_lo, int64_t row_hi,
                              float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
-                             void* workspace, void* stream, bool acc) {
+                             void* workspace, void* stream, bool acc, const float* gx_mask = nullptr) {
     int32_t st = check_common(p, F_in, F_out);
     if (st != MPGNN_OK) return st;
     Selection s;
@@ -7790,7 +7869,7 @@ static int32_t rgcn_bwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
         root != nullptr && grad_weight != nullptr && grad_root != nullptr && (h_save != nullptr || s.m_hi == s.m_lo) &&
         p->N <= INT32_MAX - 1) {
         st = bwd_fused(p, mode, R, x, weight, root, h_save, grad_out, row_lo, row_hi, want_x ? grad_x : nullptr,
-                       grad_weight, grad_root, grad_bias, s, w, ws, strm);
+                       grad_weight, grad_root, grad_bias, s, w, ws, strm, gx_mask);
         if (st != MPGNN_ERR_UNSUPPORTED) return st;
         st = MPGNN_OK;
     }
@@ -7798,11 +7877,18 @@ static int32_t rgcn_bwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     auto grad_x_part = [&](hipStream_t strm) -> int32_t {
         float* G = reinterpret_cast<float*>(ws + w.g);
         float* Groot = root ? reinterpret_cast<float*>(ws + w.groot) : nullptr;
+        float* Pdx = reinterpret_cast<float*>(ws + w.pdx);
+        // the augmented transposed list's piece counters (run_grad_x's first branch) are zeroed by
+        // the dgrad GEMM launch itself where it is rel_gemm_bf3_kernel: one memset launch less
+        const bool aug = mode == MPGNN_MODE_ALL && !exact && Groot != nullptr && row_lo == p->shard_lo &&
+                         row_hi == p->shard_hi && o.flat_fuse_split && p->tx_f.nsplit > 0;
+        bool zeroed = false;
         int32_t e = run_seg(p, mode, s, 1, grad_out, F_out, weight, root, 1, F_in, G, Groot, row_lo, row_hi, nullptr,
-                            nullptr, true, MPGNN_K_SEG_DGRAD, strm);
+                            nullptr, true, MPGNN_K_SEG_DGRAD, strm, nullptr, nullptr, nullptr, 0,
+                            aug ? split_counters(p, Pdx, F_in) : nullptr,
+                            aug ? (int)(split_counter_bytes(p) / sizeof(unsigned)) : 0, &zeroed);
         if (e != MPGNN_OK) return e;
-        return run_grad_x(p, mode, s, G, Groot, F_in, row_lo, row_hi, grad_x, reinterpret_cast<float*>(ws + w.pdx),
-                          exact, strm);
+        return run_grad_x(p, mode, s, G, Groot, F_in, row_lo, row_hi, grad_x, Pdx, exact, strm, zeroed, gx_mask);
     };
     // (the two halves on two streams — parameter gradients on a side stream forked from and
     // joined into the caller's — measured slower: C3 epoch 1.163 -> 1.207 ms; not kept)
@@ -7828,6 +7914,16 @@ int32_t mpgnn_rgcn_bwd_accumulate(const mpgnn_plan* p, int32_t mode, int64_t rel
                                   void* workspace, void* stream) {
     return rgcn_bwd_impl(p, mode, relation, R, x, F_in, weight, root, F_out, h_save, grad_out, row_lo, row_hi, grad_x,
                          grad_weight, grad_root, grad_bias, workspace, stream, true);
+}
+
+int32_t mpgnn_rgcn_bwd_relu_in(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
+                               int32_t F_in, const float* weight, const float* root, int32_t F_out,
+                               const float* h_save, const float* grad_out, int64_t row_lo, int64_t row_hi,
+                               float* grad_x, float* grad_weight, float* grad_root, float* grad_bias,
+                               void* workspace, void* stream, int32_t accumulate) {
+    if (grad_x != nullptr && x == nullptr) return arg_error("NULL x (the grad_x mask)");
+    return rgcn_bwd_impl(p, mode, relation, R, x, F_in, weight, root, F_out, h_save, grad_out, row_lo, row_hi, grad_x,
+                         grad_weight, grad_root, grad_bias, workspace, stream, accumulate != 0, x);
 }
 
 // the parameter gradients of mpgnn_rgcn_bwd (dW / droot / dbias outer products + slab reduce)

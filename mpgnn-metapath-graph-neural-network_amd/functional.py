@@ -19,6 +19,8 @@ from __future__ import annotations
 
 import ctypes
 
+import weakref
+
 import torch
 import torch.distributed as dist
 
@@ -164,6 +166,9 @@ class _RGCNConvFn(torch.autograd.Function):
     def forward(ctx, x, weight, root, bias, plan: GraphPlan, mode: int, relation: int,
                 num_relations: int, row_lo: int, row_hi: int, group, act: int, params_reduced: bool,
                 stash=None):
+        # x is a ReLU output internal to Net.forward (_relu_internal): the backward fuses that
+        # ReLU's backward into grad_x (mpgnn_rgcn_bwd_relu_in) and the producing layer skips its own
+        ctx.x_src = weakref.ref(x) if getattr(x, "_mpgnn_relu_internal", False) else None
         out, x, weight, root, h_save = _forward(x, weight, root, bias, plan, mode, relation, num_relations,
                                                 row_lo, row_hi, group, ctx.needs_input_grad[1], act)
         ctx.plan = plan
@@ -182,7 +187,8 @@ class _RGCNConvFn(torch.autograd.Function):
         x, weight, root, h_save, act_out = ctx.saved_tensors
         plan = ctx.plan
         grad_out = grad_out.contiguous()
-        if ctx.act == ACT_RELU:  # ReLU backward (threshold_backward): pass where the output > 0, one launch
+        if ctx.act == ACT_RELU and not premasked(grad_out, act_out):
+            # ReLU backward (threshold_backward): pass where the output > 0, one launch
             masked = torch.empty_like(act_out)
             check(lib.mpgnn_relu_bwd(grad_out.data_ptr(), act_out.data_ptr(), grad_out.numel(), masked.data_ptr(),
                                      _stream(x)), "mpgnn_relu_bwd")
@@ -193,8 +199,9 @@ class _RGCNConvFn(torch.autograd.Function):
         f_out = weight.shape[-1]
         nx, nw, nr, nb = ctx.needs_input_grad[:4]
         gx = torch.empty_like(x) if nx else None
+        mask_src = _mask_source(ctx) if nx and ctx.group is None else None
         if ctx.stash is not None and ctx.group is None and nw and nr and nb and root is not None and ctx.has_bias:
-            return _shared_backward(ctx, plan, x, weight, root, h_save, grad_out, gx)
+            return _shared_backward(ctx, plan, x, weight, root, h_save, grad_out, gx, mask_src)
         want = [nw, nr and root is not None, nb and ctx.has_bias]
         shapes = [weight.shape, root.shape if root is not None else None, (f_out,)]
         flat = None
@@ -210,10 +217,14 @@ class _RGCNConvFn(torch.autograd.Function):
                           for w, s in zip(want, shapes))
         ws = _workspace(plan.workspace_bytes(ctx.mode, ctx.relation, ctx.num_relations, f_in, f_out,
                                              *ctx.rows), x.device)
-        check(lib.mpgnn_rgcn_bwd(plan.handle, ctx.mode, int(ctx.relation), int(ctx.num_relations),
-                                 x.data_ptr(), f_in, weight.data_ptr(), _ptr(root), f_out, _ptr(h_save),
-                                 grad_out.data_ptr(), ctx.rows[0], ctx.rows[1], _ptr(gx), _ptr(gw),
-                                 _ptr(gr), _ptr(gb), ws.data_ptr(), _stream(x)), "mpgnn_rgcn_bwd")
+        args = (plan.handle, ctx.mode, int(ctx.relation), int(ctx.num_relations), x.data_ptr(), f_in,
+                weight.data_ptr(), _ptr(root), f_out, _ptr(h_save), grad_out.data_ptr(), ctx.rows[0], ctx.rows[1],
+                _ptr(gx), _ptr(gw), _ptr(gr), _ptr(gb), ws.data_ptr(), _stream(x))
+        if mask_src is not None:
+            check(lib.mpgnn_rgcn_bwd_relu_in(*args, 0), "mpgnn_rgcn_bwd_relu_in")
+            mark_premasked(gx, mask_src)
+        else:
+            check(lib.mpgnn_rgcn_bwd(*args), "mpgnn_rgcn_bwd")
         if ctx.group is not None:
             if gx is not None:
                 if plan.shard_side == "gathered":
@@ -227,7 +238,29 @@ class _RGCNConvFn(torch.autograd.Function):
         return gx, gw, gr, gb, None, None, None, None, None, None, None, None, None, None
 
 
-def _shared_backward(ctx, plan, x, weight, root, h_save, grad_out, gx):
+def _mask_source(ctx):
+    """The layer input whose producing ReLU the backward may fuse into grad_x: a tensor Net.forward
+    tagged internal, that nothing else observes (no tensor hook, no retain_grad)."""
+    src = ctx.x_src() if getattr(ctx, "x_src", None) is not None else None
+    if src is None or src.retains_grad or getattr(src, "_backward_hooks", None):
+        return None
+    return src
+
+
+def mark_premasked(g: torch.Tensor, src: torch.Tensor) -> None:
+    """g is the gradient w.r.t. ReLU output src with that ReLU's backward already applied."""
+    g._mpgnn_premasked = (src.data_ptr(), src._version, g._version)
+
+
+def premasked(grad_out: torch.Tensor, act_out: torch.Tensor) -> bool:
+    """grad_out came unchanged from a consumer that applied act_out's ReLU backward (the token
+    names act_out's storage and version and grad_out's own version: a gradient summed in place
+    with another consumer's afterwards no longer matches)."""
+    tok = getattr(grad_out, "_mpgnn_premasked", None)
+    return tok is not None and tok == (act_out.data_ptr(), act_out._version, grad_out._version)
+
+
+def _shared_backward(ctx, plan, x, weight, root, h_save, grad_out, gx, mask_src=None):
     """_RGCNConvFn.backward of one use of a shared layer (GradStash)."""
     stash, role = ctx.stash
     N, f_in = x.shape
@@ -236,22 +269,28 @@ def _shared_backward(ctx, plan, x, weight, root, h_save, grad_out, gx):
     args_head = (plan.handle, ctx.mode, int(ctx.relation), int(ctx.num_relations), x.data_ptr(), f_in,
                  weight.data_ptr(), root.data_ptr(), f_out, _ptr(h_save), grad_out.data_ptr(), ctx.rows[0],
                  ctx.rows[1], _ptr(gx))
+    def bwd(bufs, acc):
+        tail = (*(b.data_ptr() for b in bufs), ws.data_ptr(), _stream(x))
+        if mask_src is not None:
+            return lib.mpgnn_rgcn_bwd_relu_in(*args_head, *tail, 1 if acc else 0)
+        return (lib.mpgnn_rgcn_bwd_accumulate if acc else lib.mpgnn_rgcn_bwd)(*args_head, *tail)
+
     if role == "first" or stash.bufs is None:
         bufs = tuple(torch.empty(sh, dtype=torch.float32, device=x.device) for sh in (weight.shape, root.shape, (f_out,)))
-        check(lib.mpgnn_rgcn_bwd(*args_head, *(b.data_ptr() for b in bufs), ws.data_ptr(), _stream(x)),
-              "mpgnn_rgcn_bwd")
+        check(bwd(bufs, False), "mpgnn_rgcn_bwd")
         stash.bufs = bufs
     else:
         bufs = stash.bufs
-        st = lib.mpgnn_rgcn_bwd_accumulate(*args_head, *(b.data_ptr() for b in bufs), ws.data_ptr(), _stream(x))
+        st = bwd(bufs, True)
         if st == MPGNN_ERR_UNSUPPORTED:  # other widths / modes: fresh gradients, then autograd's add
             new = tuple(torch.empty_like(b) for b in bufs)
-            check(lib.mpgnn_rgcn_bwd(*args_head, *(b.data_ptr() for b in new), ws.data_ptr(), _stream(x)),
-                  "mpgnn_rgcn_bwd")
+            check(bwd(new, False), "mpgnn_rgcn_bwd")
             for b, n in zip(bufs, new):
                 b.add_(n)
         else:
             check(st, "mpgnn_rgcn_bwd_accumulate")
+    if mask_src is not None and gx is not None:
+        mark_premasked(gx, mask_src)
     none = (None,) * 10
     if role == "final":
         stash.bufs = None

@@ -104,16 +104,22 @@ def load_graph(link_file_path):
 # ---------------------------------------------------------------------------------------
 # loop (A11)
 # ---------------------------------------------------------------------------------------
+# MPGNN_HIP_ADAM=0: LeanAdam issues torch's _foreach_add_ + _fused_adam_ pair (A/B switch; same values)
+_HIP_ADAM = __import__("os").environ.get("MPGNN_HIP_ADAM", "1") != "0"
+
+
 class LeanAdam(torch.optim.Adam):
     """``torch.optim.Adam(fused=True)`` with a short host path for the loops' steady state.
 
     The fused optimizer's ``step`` costs ~80-110 µs of host time per call (group bookkeeping,
     checks, per-call regrouping of the tensors by device) and ``zero_grad`` ~30 µs — at C3 mode
     SINGLE, where the eager epoch is host-bound, that is a tenth of the epoch. Once the state
-    exists, this class issues exactly the calls torch's fused path makes for one device and
-    dtype — ``_foreach_add_`` of the step counters, then ``_fused_adam_`` with the same
+    exists, this class issues the step torch's fused path computes for one device and dtype —
+    on the GPU as ONE launch of the library's ``mpgnn_adam_step`` (step counters + ATen's fused
+    update arithmetic over a chip-filling grid; torch's pair of launches: ``_foreach_add_`` of
+    the step counters, ``_fused_adam_`` on ~120 blocks), else torch's two calls with the same
     arguments — so parameters and state are bit-identical to ``torch.optim.Adam`` (tests/
-    test_loop.py). Anything else (several groups or devices, amsgrad, maximize, a missing
+    test_loop.py, tests/test_gpu_parity.py). Anything else (several groups or devices, amsgrad, maximize, a missing
     gradient, a closure) goes through torch's own ``step``. Step hooks run as for any optimizer
     (torch wraps every optimizer class's ``step``)."""
 
@@ -164,11 +170,46 @@ class LeanAdam(torch.optim.Adam):
         lr = g["lr"]
         if torch.is_tensor(lr) and lr.device != params[0].device:
             return self._torch_step(closure)
+        if _HIP_ADAM and not torch.is_tensor(lr) and self._hip_step(lists, grads, g, float(lr), beta1, beta2):
+            return None
         torch._foreach_add_(steps, 1)
         torch._fused_adam_(params, grads, exp_avgs, exp_avg_sqs, [], steps, amsgrad=False, lr=lr,
                            beta1=float(beta1), beta2=float(beta2), weight_decay=g["weight_decay"], eps=g["eps"],
                            maximize=False, grad_scale=None, found_inf=None)
         return None
+
+    def _hip_step(self, lists, grads, g, lr, beta1, beta2) -> bool:
+        """The same step as mpgnn_adam_step: ONE launch (step counters + update) instead of torch's
+        two, over a grid that fills the chip (csrc/optim_kernels.hip). False (nothing launched):
+        not fp32 CUDA tensors, more than 24 tensors, or a pointer not 16-byte aligned."""
+        params, exp_avgs, exp_avg_sqs, steps = lists
+        p0 = params[0]
+        if not p0.is_cuda or p0.dtype != torch.float32 or len(params) > 24:
+            return False
+        from . import _lib
+        from .functional import _stream
+        hc = getattr(self, "_hip_cache", None)
+        if hc is None or hc[0] is not lists:
+            if any(not t.is_contiguous() or t.dtype != torch.float32 for t in (*params, *exp_avgs, *exp_avg_sqs)) or \
+                    any(s.dtype != torch.float32 or not s.is_cuda for s in steps):
+                return False
+            arr = (_lib.AdamTensor * len(params))()
+            for k, (p, m, v, s) in enumerate(zip(params, exp_avgs, exp_avg_sqs, steps)):
+                arr[k].param, arr[k].exp_avg, arr[k].exp_avg_sq = p.data_ptr(), m.data_ptr(), v.data_ptr()
+                arr[k].step, arr[k].numel = s.data_ptr(), p.numel()
+            arrive = torch.zeros(1, dtype=torch.int32, device=p0.device)
+            hc = self._hip_cache = (lists, arr, arrive)
+        _, arr, arrive = hc
+        for k, gr in enumerate(grads):
+            if gr.dtype != torch.float32 or not gr.is_contiguous() or gr.device != p0.device:
+                return False
+            arr[k].grad = gr.data_ptr()
+        st = _lib.lib.mpgnn_adam_step(arr, len(params), lr, float(beta1), float(beta2), float(g["weight_decay"]),
+                                      float(g["eps"]), arrive.data_ptr(), _stream(p0))
+        if st == _lib.MPGNN_ERR_UNSUPPORTED:
+            return False
+        _lib.check(st, "mpgnn_adam_step")
+        return True
 
     def zero_grad(self, set_to_none: bool = True):
         if not set_to_none or self._lean_lists() is None:

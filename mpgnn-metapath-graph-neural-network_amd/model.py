@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import torch
 import torch.nn as nn
@@ -45,6 +46,8 @@ class _SplitKLinear(torch.autograd.Function):
     def forward(ctx, x, weight, bias, relu=False):
         ctx.has_bias = bias is not None
         ctx.relu = relu
+        # x a ReLU output internal to Net.forward: its ReLU backward fused into grad_input
+        ctx.x_src = weakref.ref(x) if getattr(x, "_mpgnn_relu_internal", False) else None
         out = _head_fwd(x, weight, bias, relu)
         if out is None:  # other shapes: the library GEMM
             out = F.linear(x, weight, bias)
@@ -66,9 +69,13 @@ class _SplitKLinear(torch.autograd.Function):
                        "mpgnn_relu_bwd")
             g = masked
         if ctx.needs_input_grad[0]:
-            gx = _head_dgrad(g, weight)
+            from .functional import _mask_source, mark_premasked
+            src = _mask_source(ctx)
+            gx = _head_dgrad(g, weight, x if src is not None else None)
             if gx is None:
                 gx = g.mm(weight)
+            elif src is not None:
+                mark_premasked(gx, src)
         f, o = x.shape[1], g.shape[1]
         # the HIP pair is scalar-FMA work (N·F·O): for the heads with few outputs (O ≤ 32·256/F:
         # Net.lin, MPNetm.fc2) it beats the library's serial-K GEMM; F = O = 128 (MPNetm.fc1 of
@@ -142,16 +149,22 @@ def _head_fwd(x, weight, bias, relu):
     return out
 
 
-def _head_dgrad(g, weight):
-    """grad_out @ weight through mpgnn_linear_dgrad (F = O = 128, or O <= 8), else None."""
-    if g.dim() != 2 or weight.dim() != 2 or g.shape[1] != weight.shape[0] or not _aligned(g, weight):
+def _head_dgrad(g, weight, relu_in=None):
+    """grad_out @ weight through mpgnn_linear_dgrad (F = O = 128, or O <= 8), else None; with
+    ``relu_in`` (the head's input, a ReLU output) mpgnn_linear_dgrad_relu_in: that ReLU's backward
+    applied in the same launch."""
+    if g.dim() != 2 or weight.dim() != 2 or g.shape[1] != weight.shape[0] or not _aligned(g, weight, relu_in):
         return None
     from . import _lib
     from .functional import _stream
     n, o = g.shape
     f = weight.shape[1]
     gx = torch.empty(n, f, dtype=torch.float32, device=g.device)
-    st = _lib.lib.mpgnn_linear_dgrad(g.data_ptr(), n, o, weight.data_ptr(), f, gx.data_ptr(), _stream(g))
+    if relu_in is not None:
+        st = _lib.lib.mpgnn_linear_dgrad_relu_in(g.data_ptr(), n, o, weight.data_ptr(), f, relu_in.data_ptr(),
+                                                 gx.data_ptr(), _stream(g))
+    else:
+        st = _lib.lib.mpgnn_linear_dgrad(g.data_ptr(), n, o, weight.data_ptr(), f, gx.data_ptr(), _stream(g))
     if st == _lib.MPGNN_ERR_UNSUPPORTED:
         return None
     _lib.check(st, "mpgnn_linear_dgrad")
@@ -189,6 +202,13 @@ class _FastTrainToggle:
 
 # MPGNN_GRAD_STASH=0: Net's shared conv2 gradients summed by autograd (A/B switch; same values)
 _GRAD_STASH = os.environ.get("MPGNN_GRAD_STASH", "1") != "0"
+# MPGNN_RELU_FUSE=0: each of Net's ReLU backwards a launch of its own (A/B switch; same values)
+_RELU_FUSE = os.environ.get("MPGNN_RELU_FUSE", "1") != "0"
+
+
+def _forward_hooked(*mods) -> bool:
+    from torch.nn.modules import module as _m
+    return bool(_m._global_forward_hooks) or any(m._forward_hooks for m in mods)
 
 
 class Net(_FastTrainToggle, torch.nn.Module):
@@ -208,6 +228,12 @@ class Net(_FastTrainToggle, torch.nn.Module):
                 all(p.requires_grad for p in (self.conv2.weight, self.conv2.root, self.conv2.bias)):
             # conv2's gradients over its uses summed inside the backward kernels (GradStash)
             stash = GradStash()
+        # the activations between the layers (and into the head) are internal: nothing outside this
+        # forward can observe their gradients unless a forward hook hands them out — then each
+        # ReLU's backward stays a launch of its own instead of being fused into the consumer's
+        # input-gradient kernel (functional.premasked)
+        internal = shard is None and group is None and x.is_cuda and torch.is_grad_enabled() and _RELU_FUSE and \
+            not _forward_hooked(self.conv1, self.conv2, self.LinearLayer)
         for layer_index in range(0, self.metapath_length):
             conv = self.conv1 if layer_index == 0 else self.conv2
             kw = {}
@@ -216,6 +242,8 @@ class Net(_FastTrainToggle, torch.nn.Module):
             # F.relu(conv(...)) of model.py:144,146, fused into the layer's combine kernel
             x = conv(x, edge_index, edge_type, shard=shard, group=group, activation="relu", shard_side=shard_side,
                      **kw)
+            if internal:
+                x._mpgnn_relu_internal = True
         x = linear(self.LinearLayer, x)
         return F.log_softmax(x, dim=1)
 

@@ -1656,3 +1656,102 @@ def test_mode_single_streaming_combine_widths(f_in, f_out):
         r64 = act(0, orc.custom_rgcn_forward(g.x.double(), g.edge_index, g.edge_type, rel, W.double(), root.double(),
                                              bias.double()))
         rel_close(out, r32, what=f"single combine {f_in}x{f_out} rel {rel}", ref64=r64)
+
+
+def _adam_case(dev, contract_sizes=((37, 128, 128), (128, 128), (128,), (2, 128), (2,), (5, 3))):
+    g = torch.Generator().manual_seed(7)
+    return [torch.nn.Parameter(torch.randn(*s, generator=g).to(dev)) for s in contract_sizes]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("capturable", [False, True])
+def test_adam_step_bit_identical_to_torch(capturable):
+    """mpgnn_adam_step (LeanAdam's step on the GPU: step counters + ATen's fused update in one
+    launch, csrc/optim_kernels.hip) = torch.optim.Adam(fused=True) bit for bit — parameters,
+    exp_avg, exp_avg_sq, step — over 6 steps with fresh gradients, tensors whose sizes are and
+    are not multiples of 4. The default fma-contraction variant (MPGNN_OPT_ADAM_CONTRACT) is the
+    one that matches torch's build; the other is reported for the record."""
+    import ctypes
+    from mpgnn_amd import _lib, main
+    dev = torch.device("cuda", 0)
+    kw = dict(lr=0.01, weight_decay=5e-4, fused=True, capturable=capturable)
+    v0 = ctypes.c_int64()
+    _lib.check(_lib.lib.mpgnn_get_option(_lib.OPT_ADAM_CONTRACT, ctypes.byref(v0)), "get")
+    match = {}
+    try:
+        for contract in (int(v0.value), 1 - int(v0.value)):
+            _lib.check(_lib.lib.mpgnn_set_option(_lib.OPT_ADAM_CONTRACT, contract), "set")
+            pa, pb = _adam_case(dev), _adam_case(dev)
+            oa, ob = torch.optim.Adam(pa, **kw), main.LeanAdam(pb, **kw)
+            gg = torch.Generator().manual_seed(11)
+            for it in range(6):
+                grads = [torch.randn(p.shape, generator=gg).to(dev) * (10.0 ** (it - 3)) for p in pa]
+                for ps, o in ((pa, oa), (pb, ob)):
+                    for p, gr in zip(ps, grads):
+                        p.grad = gr.clone()
+                    o.step()
+                if it >= 1:
+                    assert getattr(ob, "_hip_cache", None) is not None, "the HIP step did not run"
+            torch.cuda.synchronize()
+            ok = all(torch.equal(p, q) and all(torch.equal(oa.state[p][k], ob.state[q][k])
+                                               for k in ("exp_avg", "exp_avg_sq", "step"))
+                     for p, q in zip(pa, pb))
+            match[contract] = ok
+    finally:
+        _lib.check(_lib.lib.mpgnn_set_option(_lib.OPT_ADAM_CONTRACT, int(v0.value)), "restore")
+    print(f"adam contraction variants bit-identical to torch: {match}")
+    assert match[int(v0.value)], match
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,hidden,classes", [("C1", 64, 5), ("fb15k237", 128, 2)])
+def test_net_relu_backward_fused_bit_identical(name, hidden, classes, monkeypatch):
+    """Net's ReLU backwards fused into the consumers' input-gradient kernels (grad_x of the next
+    conv: mpgnn_rgcn_bwd_relu_in, the head: mpgnn_linear_dgrad_relu_in) give every parameter
+    gradient bit for bit as the separate relu_bwd launches (MPGNN_RELU_FUSE=0), with no
+    relu_bwd launch left; a forward hook on a conv turns the fusion off (its output observable)."""
+    import mpgnn_amd.functional as fnl
+    from mpgnn_amd import _lib
+    from mpgnn_amd import model as mdl
+    g = data.config_graph(name)
+    F = g.x.shape[1]
+    torch.manual_seed(10)
+    net = mpgnn_amd.Net(F, hidden, g.num_relations, hidden, classes, 3).to(DEV)
+    gout = torch.randn(g.num_nodes, classes, generator=torch.Generator().manual_seed(3)).to(DEV)
+    x, ei, et = g.x.to(DEV), g.edge_index.to(DEV), g.edge_type.to(DEV)
+    calls = {}
+    real = _lib.lib
+
+    class _Count:
+        def __getattr__(self, k):
+            f = getattr(real, k)
+
+            def wrapped(*a):
+                calls[k] = calls.get(k, 0) + 1
+                return f(*a)
+            return wrapped
+    monkeypatch.setattr(fnl, "lib", _Count())
+    monkeypatch.setattr(_lib, "lib", _Count())
+
+    def grads(fuse, hook=False):
+        monkeypatch.setattr(mdl, "_RELU_FUSE", fuse)
+        calls.clear()
+        net.zero_grad(set_to_none=True)
+        h = net.conv2.register_forward_hook(lambda *_: None) if hook else None
+        out = net(x, ei, et)
+        if h is not None:
+            h.remove()
+        out.backward(gout)
+        torch.cuda.synchronize()
+        return {k: p.grad.clone() for k, p in net.named_parameters()}, dict(calls)
+
+    ref, c_ref = grads(False)
+    got, c_got = grads(True)
+    hooked, c_hook = grads(True, hook=True)
+    assert c_ref.get("mpgnn_relu_bwd", 0) == 3 and c_hook.get("mpgnn_relu_bwd", 0) == 3, (c_ref, c_hook)
+    assert c_got.get("mpgnn_relu_bwd", 0) == 0, c_got
+    # conv2's two uses (C1, F = 64: the accumulating call is refused, then a fresh one: three calls)
+    assert c_got.get("mpgnn_rgcn_bwd_relu_in", 0) >= 2 and c_got.get("mpgnn_linear_dgrad_relu_in", 0) == 1, c_got
+    for k in ref:
+        assert torch.equal(ref[k], got[k]), k
+        assert torch.equal(ref[k], hooked[k]), k
