@@ -1118,7 +1118,7 @@ def main():
             else:
                 netg = mpgnn_amd.Net(F, F, g.num_relations, F, 2, args.layers).to(dev)
             netg.load_state_dict(model.state_dict())
-            optg = torch.optim.Adam(netg.parameters(), lr=0.01, weight_decay=0.0005, fused=True, capturable=True)
+            optg = mpgnn_amd.main._adam_graphable(netg)  # LeanAdam: the HIP step, capturable
 
             def epoch_g():
                 netg.train()

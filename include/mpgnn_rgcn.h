@@ -227,6 +227,13 @@ int32_t mpgnn_nll_rows_fwd(const float* logp, int64_t rows, int32_t num_classes,
 int32_t mpgnn_nll_rows_bwd(const float* grad_loss, const float* total_weight, int64_t rows, int32_t num_classes,
                            const int64_t* row_idx, const int64_t* target, int64_t n, int64_t ignore_index,
                            float* grad_logp, void* stream);
+/* The same input gradient written WHOLE (zeros included: no fill launch before it), from the
+ * pairs grouped by row — row_perm[row_ptr[i] .. row_ptr[i+1]) = the positions j with
+ * row_idx[j] == i, ascending (int32 CSR over the rows, built once per list by the caller) —
+ * bit-identical to the zero fill + mpgnn_nll_rows_bwd. */
+int32_t mpgnn_nll_rows_bwd_dense(const float* grad_loss, const float* total_weight, int64_t rows, int32_t num_classes,
+                                 const int32_t* row_ptr, const int32_t* row_perm, const int64_t* target,
+                                 int64_t ignore_index, float* grad_logp, void* stream);
 
 /* Forward and input gradient of the wrappers' Linear heads (Net.lin model.py:147; MPNetm.fc1 /
  * fc2 model.py:224-226), replacing F.linear / grad_out @ weight (host-cheap single launches on the
@@ -239,6 +246,18 @@ int32_t mpgnn_linear_fwd(const float* x, int64_t N, int32_t F, const float* weig
                          int32_t act, float* out, void* stream);
 int32_t mpgnn_linear_dgrad(const float* grad_out, int64_t N, int32_t O, const float* weight, int32_t F, float* grad_x,
                            void* stream);
+/* Backward of out = log_softmax(x @ weightᵀ + bias) (mpgnn_linear_fwd with MPGNN_ACT_LOG_SOFTMAX;
+ * Net.lin + F.log_softmax, model.py:147-148) from grad_logp and the forward's logp [N,O]:
+ * dl = grad_logp - exp(logp) · Σ_o grad_logp[o] per row (log_softmax's backward), grad_x = dl @
+ * weight (nullable; relu_in [N,F] nullable: the ReLU backward of the layer that produced x fused,
+ * as mpgnn_linear_dgrad_relu_in), grad_weight = dlᵀ x, grad_bias = Σ_i dl (nullable): one pass
+ * over the rows + the ordered sum of its per-slice partials (deterministic). O <= 8, F <= 256
+ * (else MPGNN_ERR_UNSUPPORTED, nothing launched). Scratch: _workspace_bytes. */
+int32_t mpgnn_linear_logsoftmax_bwd_workspace_bytes(int64_t N, int32_t F, int32_t O, int64_t* bytes);
+int32_t mpgnn_linear_logsoftmax_bwd(const float* grad_logp, const float* logp, const float* x, int64_t N, int32_t F,
+                                    int32_t O, const float* weight, const float* relu_in, float* grad_x,
+                                    float* grad_weight, float* grad_bias, void* workspace, void* stream);
+
 /* mpgnn_linear_dgrad with the ReLU backward of the layer that produced the head's input x [N,F]
  * fused (grad_x = x <= 0 ? 0 : grad_out @ weight): Net.lin over the last conv's ReLU output. */
 int32_t mpgnn_linear_dgrad_relu_in(const float* grad_out, int64_t N, int32_t O, const float* weight, int32_t F,
@@ -291,7 +310,12 @@ int32_t mpgnn_rgcn_fwd(const mpgnn_plan* plan, int32_t mode, int64_t relation,
                        int32_t F_out, int64_t row_lo, int64_t row_hi, float* out,
                        float* h_save, void* workspace, void* stream);
 
-enum mpgnn_activation { MPGNN_ACT_NONE = 0, MPGNN_ACT_RELU = 1 };
+enum mpgnn_activation {
+    MPGNN_ACT_NONE = 0,
+    MPGNN_ACT_RELU = 1,
+    MPGNN_ACT_LOG_SOFTMAX = 2 /* mpgnn_linear_fwd with O <= 8 only: log_softmax over each row's O outputs
+                                 (Net's lin + F.log_softmax, model.py:147-148, in the head's launch) */
+};
 
 /* Layer forward with the caller's activation fused into the combine epilogue:
  *   out = act(Σ_r mean_r(x) @ W_r + x @ root + bias)

@@ -101,6 +101,8 @@ SIGNATURES = [
     ("mpgnn_linear_fwd", _I32, [_P, _I64, _I32, _P, _I32, _P, _I32, _P, _P]),
     ("mpgnn_linear_dgrad", _I32, [_P, _I64, _I32, _P, _I32, _P, _P]),
     ("mpgnn_linear_dgrad_relu_in", _I32, [_P, _I64, _I32, _P, _I32, _P, _P, _P]),
+    ("mpgnn_linear_logsoftmax_bwd_workspace_bytes", _I32, [_I64, _I32, _I32, _PI64]),
+    ("mpgnn_linear_logsoftmax_bwd", _I32, [_P, _P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
     ("mpgnn_adam_step", _I32, [ctypes.POINTER(AdamTensor), _I32, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                 ctypes.c_double, ctypes.c_double, _P, _P]),
     ("mpgnn_score_argmax", _I32, [_P, _I64, _P, _P, _P, _I64, _P, _P, _P, _P]),
@@ -111,6 +113,7 @@ SIGNATURES = [
     ("mpgnn_confusion_counts", _I32, [_P, _I64, _I32, _I32, _P, _P, _P, _P, _P]),
     ("mpgnn_nll_rows_fwd", _I32, [_P, _I64, _I32, _P, _P, _I64, _I64, _P, _P, _P]),
     ("mpgnn_nll_rows_bwd", _I32, [_P, _P, _I64, _I32, _P, _P, _I64, _I64, _P, _P]),
+    ("mpgnn_nll_rows_bwd_dense", _I32, [_P, _P, _I64, _I32, _P, _P, _P, _I64, _P, _P]),
     ("mpgnn_score_bag_argmax", _I32, [_P, _P, _I32, _P, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("mpgnn_score_bag_argmax_bwd", _I32, [_P, _I64, _P, _P, _P, _P, _P, _P, _I32, _I64, _P, _P, _P, _P, _P, _P,
                                           _P]),
@@ -132,7 +135,7 @@ KERNEL_KINDS = {"seg_fwd": 0, "row_fwd": 1, "seg_dgrad": 2, "row_dx": 3, "outer"
                 "piece": 7, "final": 8}
 OPT_EXACT_ORDER = 0
 OPT_ADAM_CONTRACT = 40
-ACT_NONE, ACT_RELU = 0, 1
+ACT_NONE, ACT_RELU, ACT_LOG_SOFTMAX = 0, 1, 2
 
 
 def _missing(name):

@@ -5294,10 +5294,126 @@ __global__ __launch_bounds__(kThreads) void linear_small_fwd_kernel(const float*
             for (int m = 8; m >= 1; m >>= 1) t += __shfl_xor(t, m);  // within the row's 16 lanes
             v = sub == o ? t : v;
         }
-        if (i < N && sub < O) {
-            const float r = (float)(v + b);
-            out[(size_t)i * O + sub] = act == MPGNN_ACT_RELU ? relu_f(r) : r;
+        float r = (float)(v + b);
+        if (act == MPGNN_ACT_LOG_SOFTMAX) {  // over the row's O logits (its 16 lanes; wave-uniform branch)
+            float mx = sub < O ? r : -INFINITY;
+#pragma unroll
+            for (int m = 8; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m));
+            float se = sub < O ? expf(r - mx) : 0.0f;
+#pragma unroll
+            for (int m = 8; m >= 1; m >>= 1) se += __shfl_xor(se, m);
+            r = (r - mx) - logf(se);
         }
+        if (i < N && sub < O) out[(size_t)i * O + sub] = act == MPGNN_ACT_RELU ? relu_f(r) : r;
+    }
+}
+
+// Backward of a narrow head followed by log_softmax (Net.lin + F.log_softmax, model.py:147-148):
+// per row i, dl = g_i - exp(logp_i) · Σ_o g_i[o] (log_softmax's backward), then in the same pass
+// grad_x[i] = dl @ W (ReLU mask of the head's input fused when given) and this workgroup's
+// partial of dW = dlᵀ x, db = Σ dl over its row slice (rows i ≡ grp mod G of the slice summed
+// in order per thread, the G groups in order through LDS): P[part][o][0..F]. The ordered sum of
+// the partials is linear_wgrad_sum_kernel's. One launch replaces log_softmax's backward, the
+// dgrad and the partial weight gradient.
+constexpr int kLsmO = 8;
+// OM: compiled bound on O (2: Net's two classes; 8). Thread layout: 4 consecutive columns per
+// thread (float4), F/4 threads per row, G = 256·4/F row groups per workgroup; rows i ≡ grp (mod G)
+// of the slice per thread, RB of them in flight together.
+template <int OM, int RB>
+__global__ __launch_bounds__(kThreads) void linear_lsm_bwd_kernel(const float* __restrict__ g,
+                                                                  const float* __restrict__ logp,
+                                                                  const float* __restrict__ x,
+                                                                  const float* __restrict__ mask, int N, int F, int O,
+                                                                  const float* __restrict__ W, float* __restrict__ gx,
+                                                                  int rows, float* __restrict__ P) {
+    __shared__ float red[(4 * kThreads + kThreads) * OM];  // [G][O][F + 1]: G·(F + 1) <= 1024 + 256 per output
+    const int tid = threadIdx.x;
+    const int F4 = F / 4;
+    const int G = kThreads / F4;
+    const int f = (tid % F4) * 4, grp = tid / F4;
+    const bool live = grp < G;
+    float4 w[OM], acc[OM];
+    float bacc[OM];
+#pragma unroll
+    for (int o = 0; o < OM; ++o) {
+        w[o] = (live && o < O) ? *reinterpret_cast<const float4*>(W + (size_t)o * F + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+        acc[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+        bacc[o] = 0.0f;
+    }
+    const int r0 = (int)blockIdx.x * rows, r1 = min(N, r0 + rows);
+    if (live) {
+        for (int i0 = r0 + grp; i0 < r1; i0 += G * RB) {
+            // the batch's operands first (one round trip per batch), rows past r1 clamped (unused)
+            float gi[RB][OM], lp[RB][OM];
+            float4 xv[RB], mv[RB];
+#pragma unroll
+            for (int u = 0; u < RB; ++u) {
+                const int i = min(i0 + u * G, r1 - 1);
+#pragma unroll
+                for (int o = 0; o < OM; ++o) {
+                    gi[u][o] = o < O ? g[(size_t)i * O + o] : 0.0f;
+                    lp[u][o] = o < O ? logp[(size_t)i * O + o] : 0.0f;
+                }
+                xv[u] = *reinterpret_cast<const float4*>(x + (size_t)i * F + f);
+                mv[u] = mask != nullptr ? *reinterpret_cast<const float4*>(mask + (size_t)i * F + f)
+                                        : make_float4(1.f, 1.f, 1.f, 1.f);
+            }
+#pragma unroll
+            for (int u = 0; u < RB; ++u) {
+                const int i = i0 + u * G;
+                if (i >= r1) break;
+                float S = 0.0f, dl[OM];
+#pragma unroll
+                for (int o = 0; o < OM; ++o)
+                    if (o < O) S += gi[u][o];
+#pragma unroll
+                for (int o = 0; o < OM; ++o) dl[o] = o < O ? gi[u][o] - expf(lp[u][o]) * S : 0.0f;
+                if (gx != nullptr) {
+                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int o = 0; o < OM; ++o)
+                        if (o < O) {
+                            v.x = fmaf(dl[o], w[o].x, v.x);
+                            v.y = fmaf(dl[o], w[o].y, v.y);
+                            v.z = fmaf(dl[o], w[o].z, v.z);
+                            v.w = fmaf(dl[o], w[o].w, v.w);
+                        }
+                    if (mask != nullptr)
+                        v = make_float4(relu_bwd_f(v.x, mv[u].x), relu_bwd_f(v.y, mv[u].y), relu_bwd_f(v.z, mv[u].z),
+                                        relu_bwd_f(v.w, mv[u].w));
+                    *reinterpret_cast<float4*>(gx + (size_t)i * F + f) = v;
+                }
+#pragma unroll
+                for (int o = 0; o < OM; ++o)
+                    if (o < O) {
+                        acc[o].x = fmaf(dl[o], xv[u].x, acc[o].x);
+                        acc[o].y = fmaf(dl[o], xv[u].y, acc[o].y);
+                        acc[o].z = fmaf(dl[o], xv[u].z, acc[o].z);
+                        acc[o].w = fmaf(dl[o], xv[u].w, acc[o].w);
+                        bacc[o] += dl[o];
+                    }
+            }
+        }
+    }
+    const int E = O * (F + 1);
+    if (live) {
+#pragma unroll
+        for (int o = 0; o < OM; ++o)
+            if (o < O) {
+                float* rp = red + grp * E + o * (F + 1) + f;
+                rp[0] = acc[o].x;
+                rp[1] = acc[o].y;
+                rp[2] = acc[o].z;
+                rp[3] = acc[o].w;
+                if (f == 0) red[grp * E + o * (F + 1) + F] = bacc[o];
+            }
+    }
+    __syncthreads();
+    float* Pp = P + (size_t)blockIdx.x * E;
+    for (int e = tid; e < E; e += kThreads) {
+        float t = red[e];
+        for (int q = 1; q < G; ++q) t += red[q * E + e];
+        Pp[e] = t;
     }
 }
 
@@ -6812,8 +6928,9 @@ static int32_t linear_gemm128(const float* A, int64_t N, const float* W, bool tr
 int32_t mpgnn_linear_fwd(const float* x, int64_t N, int32_t F, const float* weight, int32_t O, const float* bias,
                          int32_t act, float* out, void* stream) {
     if (N < 0 || N > INT32_MAX || F <= 0 || O <= 0) return arg_error("mpgnn_linear_fwd: bad N, F or O");
-    if (act != MPGNN_ACT_NONE && act != MPGNN_ACT_RELU) return arg_error("mpgnn_linear_fwd: bad act");
-    const bool gemm = F == 128 && O == 128 && default_options().gemm_bf3;
+    if (act != MPGNN_ACT_NONE && act != MPGNN_ACT_RELU && act != MPGNN_ACT_LOG_SOFTMAX)
+        return arg_error("mpgnn_linear_fwd: bad act");
+    const bool gemm = F == 128 && O == 128 && default_options().gemm_bf3 && act != MPGNN_ACT_LOG_SOFTMAX;
     const bool small = O <= kLinSmallO && F <= 256 && F % 4 == 0;
     if (!gemm && !small) return MPGNN_ERR_UNSUPPORTED;
     if (N == 0) return MPGNN_OK;
@@ -6868,6 +6985,49 @@ int32_t mpgnn_linear_dgrad_relu_in(const float* grad_out, int64_t N, int32_t O, 
                                    const float* x, float* grad_x, void* stream) {
     if (N > 0 && x == nullptr) return arg_error("mpgnn_linear_dgrad_relu_in: NULL x");
     return linear_dgrad_impl(grad_out, N, O, weight, F, grad_x, x, stream);
+}
+
+static int lsm_parts(int64_t N) { return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (N + 31) / 32)); }
+
+int32_t mpgnn_linear_logsoftmax_bwd_workspace_bytes(int64_t N, int32_t F, int32_t O, int64_t* bytes) {
+    if (!bytes) return arg_error("NULL bytes");
+    if (N < 0 || N > INT32_MAX || F <= 0 || O <= 0) return arg_error("bad N, F or O");
+    if (F > kThreads || F % 4 != 0 || O > kLsmO) return MPGNN_ERR_UNSUPPORTED;
+    *bytes = (int64_t)lsm_parts(N) * O * (F + 1) * (int64_t)sizeof(float);
+    return MPGNN_OK;
+}
+
+int32_t mpgnn_linear_logsoftmax_bwd(const float* grad_logp, const float* logp, const float* x, int64_t N, int32_t F,
+                                    int32_t O, const float* weight, const float* relu_in, float* grad_x,
+                                    float* grad_weight, float* grad_bias, void* workspace, void* stream) {
+    if (N < 0 || N > INT32_MAX || F <= 0 || O <= 0) return arg_error("bad N, F or O");
+    if (F > kThreads || F % 4 != 0 || O > kLsmO) return MPGNN_ERR_UNSUPPORTED;
+    if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(weight) | reinterpret_cast<uintptr_t>(relu_in) |
+          reinterpret_cast<uintptr_t>(grad_x)) & 15) != 0)
+        return arg_error("mpgnn_linear_logsoftmax_bwd: x, weight, relu_in, grad_x must be 16-byte aligned");
+    if (!grad_weight || !workspace || !weight || (N > 0 && (!x || !grad_logp || !logp)))
+        return arg_error("mpgnn_linear_logsoftmax_bwd: NULL pointer");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    if (N == 0) {
+        int32_t st = hip_check(hipMemsetAsync(grad_weight, 0, (size_t)O * F * sizeof(float), strm), "memset");
+        if (st == MPGNN_OK && grad_bias) st = hip_check(hipMemsetAsync(grad_bias, 0, (size_t)O * sizeof(float), strm), "memset");
+        return st;
+    }
+    const int parts = lsm_parts(N);
+    const int rows = (int)((N + parts - 1) / parts);
+    float* P = static_cast<float*>(workspace);
+    if (O <= 2)
+        hipLaunchKernelGGL((linear_lsm_bwd_kernel<2, 4>), dim3(parts), dim3(kThreads), 0, strm, grad_logp, logp, x,
+                           relu_in, (int)N, F, O, weight, grad_x, rows, P);
+    else
+        hipLaunchKernelGGL((linear_lsm_bwd_kernel<kLsmO, 4>), dim3(parts), dim3(kThreads), 0, strm, grad_logp, logp, x,
+                           relu_in, (int)N, F, O, weight, grad_x, rows, P);
+    int32_t st = hip_check(hipGetLastError(), "linear_lsm_bwd_kernel launch");
+    if (st != MPGNN_OK) return st;
+    const int elems = O * (F + 1);
+    hipLaunchKernelGGL(linear_wgrad_sum_kernel, dim3((elems + kWaves - 1) / kWaves), dim3(kThreads), 0, strm, P, parts, F,
+                       O, grad_weight, grad_bias);
+    return hip_check(hipGetLastError(), "linear_wgrad_sum_kernel launch");
 }
 
 int32_t mpgnn_linear_wgrad(const float* x, const float* grad_out, int64_t N, int32_t F, int32_t O, float* grad_weight,

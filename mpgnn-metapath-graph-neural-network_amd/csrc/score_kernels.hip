@@ -716,6 +716,44 @@ extern "C" int32_t mpgnn_nll_rows_fwd(const float* logp, int64_t rows, int32_t n
     return hip_status(hipGetLastError(), "nll_rows_fwd_kernel launch");
 }
 
+// The same gradient written whole (no zero fill before it): one thread per (row, class), the
+// row's positions j in row_idx from a CSR over the rows (row_ptr / row_perm, j ascending), its
+// kept pairs of this class added in sequence from 0 — the scatter's value bit for bit (equal
+// addends: every sequential order gives the same sum).
+__global__ __launch_bounds__(kScoreThreads) void nll_rows_bwd_dense_kernel(
+    const float* __restrict__ grad_loss, const float* __restrict__ total_weight, int64_t rows, int C,
+    const int* __restrict__ row_ptr, const int* __restrict__ row_perm, const int64_t* __restrict__ tgt,
+    int64_t ignore, float* __restrict__ grad) {
+    const int64_t e = (int64_t)blockIdx.x * kScoreThreads + threadIdx.x;
+    if (e >= rows * C) return;
+    const int64_t i = e / C;
+    const int c = (int)(e - i * C);
+    float v = 0.0f;
+    const int p1 = row_ptr[i + 1];
+    for (int p = row_ptr[i]; p < p1; ++p) {
+        const int64_t t = tgt[row_perm[p]];
+        if (t != ignore && t == c) v += -(grad_loss[0] / total_weight[0]);
+    }
+    grad[e] = v;
+}
+
+extern "C" int32_t mpgnn_nll_rows_bwd_dense(const float* grad_loss, const float* total_weight, int64_t rows,
+                                            int32_t num_classes, const int32_t* row_ptr, const int32_t* row_perm,
+                                            const int64_t* target, int64_t ignore_index, float* grad_logp,
+                                            void* stream) {
+    if (rows < 0 || num_classes <= 0 || rows * num_classes / kScoreThreads >= (int64_t)INT32_MAX)
+        return arg_fail("mpgnn_nll_rows_bwd_dense: bad sizes");
+    if (rows == 0) return MPGNN_OK;
+    if (!grad_loss || !total_weight || !row_ptr || !row_perm || !target || !grad_logp)
+        return arg_fail("mpgnn_nll_rows_bwd_dense: NULL argument");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    const int64_t total = rows * num_classes;
+    hipLaunchKernelGGL(nll_rows_bwd_dense_kernel, dim3((unsigned)((total + kScoreThreads - 1) / kScoreThreads)),
+                       dim3(kScoreThreads), 0, strm, grad_loss, total_weight, rows, (int)num_classes, row_ptr, row_perm,
+                       target, ignore_index, grad_logp);
+    return hip_status(hipGetLastError(), "nll_rows_bwd_dense_kernel launch");
+}
+
 extern "C" int32_t mpgnn_nll_rows_bwd(const float* grad_loss, const float* total_weight, int64_t rows,
                                       int32_t num_classes, const int64_t* row_idx, const int64_t* target, int64_t n,
                                       int64_t ignore_index, float* grad_logp, void* stream) {

@@ -115,9 +115,33 @@ def confusion_counts_rows(scores: torch.Tensor, lists) -> torch.Tensor:
     return out
 
 
+# (weakref to the row list, its _version, rows) -> (row_ptr, row_perm): the list grouped by row
+# (int32 CSR on the list's device), made once per list outside captures
+_ROW_CSR: list = []
+# MPGNN_NLL_DENSE=0: the zero fill + scatter backward (A/B switch; same values)
+_NLL_DENSE = __import__("os").environ.get("MPGNN_NLL_DENSE", "1") != "0"
+
+
+def _rows_csr(idx: torch.Tensor, rows: int):
+    for ri, vi, n, csr in _ROW_CSR:
+        if ri() is idx and vi == idx._version and n == rows:
+            return csr
+    if not _NLL_DENSE or torch.cuda.is_current_stream_capturing() or idx.numel() == 0 or idx.numel() >= 2 ** 31 or \
+            rows >= 2 ** 31:
+        return None
+    perm = torch.argsort(idx, stable=True)
+    ptr = torch.searchsorted(idx[perm], torch.arange(rows + 1, device=idx.device))
+    csr = (ptr.to(torch.int32).contiguous(), perm.to(torch.int32).contiguous())
+    _ROW_CSR.insert(0, (weakref.ref(idx), idx._version, rows, csr))
+    del _ROW_CSR[_NLL_OK_MAX:]
+    return csr
+
+
 class _NllRows(torch.autograd.Function):
-    """mpgnn_nll_rows_fwd / _bwd: the loss in one launch, its input gradient in a zero fill and
-    one scatter launch (torch: index_select, nll_loss and their backward, 7 launches)."""
+    """mpgnn_nll_rows_fwd / _bwd: the loss in one launch, its input gradient in one launch that
+    writes it whole from the list grouped by row (mpgnn_nll_rows_bwd_dense; without the grouping,
+    inside a capture that did not see the list before: a zero fill + one scatter launch) — torch:
+    index_select, nll_loss and their backward, 7 launches."""
 
     @staticmethod
     def forward(ctx, logp, idx, target):
@@ -130,6 +154,7 @@ class _NllRows(torch.autograd.Function):
                                                _stream(logp)), "mpgnn_nll_rows_fwd")
         ctx.lists = (idx, target, tw)
         ctx.shape = tuple(logp.shape)
+        ctx.csr = _rows_csr(idx, logp.shape[0])
         return loss
 
     @staticmethod
@@ -138,6 +163,13 @@ class _NllRows(torch.autograd.Function):
         from .functional import _stream
         idx, target, tw = ctx.lists
         g = g.contiguous()
+        if ctx.csr is not None:
+            grad = torch.empty(ctx.shape, dtype=torch.float32, device=g.device)
+            ptr, perm = ctx.csr
+            _lib.check(_lib.lib.mpgnn_nll_rows_bwd_dense(g.data_ptr(), tw.data_ptr(), ctx.shape[0], ctx.shape[1],
+                                                         ptr.data_ptr(), perm.data_ptr(), target.data_ptr(), -100,
+                                                         grad.data_ptr(), _stream(grad)), "mpgnn_nll_rows_bwd_dense")
+            return grad, None, None
         grad = torch.zeros(ctx.shape, dtype=torch.float32, device=g.device)
         _lib.check(_lib.lib.mpgnn_nll_rows_bwd(g.data_ptr(), tw.data_ptr(), ctx.shape[0], ctx.shape[1], idx.data_ptr(),
                                                target.data_ptr(), idx.numel(), -100, grad.data_ptr(), _stream(grad)),

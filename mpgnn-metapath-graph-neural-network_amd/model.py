@@ -171,6 +171,70 @@ def _head_dgrad(g, weight, relu_in=None):
     return gx
 
 
+class _HeadLogSoftmax(torch.autograd.Function):
+    """``F.log_softmax(layer(x), dim=1)`` for a narrow head (O <= 8 outputs, F <= 256: Net.lin,
+    model.py:147-148): the forward ONE launch (mpgnn_linear_fwd with MPGNN_ACT_LOG_SOFTMAX: the
+    float64-summed dots, then log_softmax over the row's outputs), the backward one pass
+    (mpgnn_linear_logsoftmax_bwd: log_softmax's backward, grad_input — with the ReLU backward of
+    an internal input fused, as _SplitKLinear — and the row-sliced weight / bias partials) + the
+    ordered partial sum: 2 + 2 launches where the separate ops take 2 + 4."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        from . import _lib
+        from .functional import _stream
+        ctx.x_src = weakref.ref(x) if getattr(x, "_mpgnn_relu_internal", False) else None
+        n, f = x.shape
+        o = weight.shape[0]
+        out = torch.empty(n, o, dtype=torch.float32, device=x.device)
+        _lib.check(_lib.lib.mpgnn_linear_fwd(x.data_ptr(), n, f, weight.data_ptr(), o,
+                                             bias.data_ptr() if bias is not None else None, _lib.ACT_LOG_SOFTMAX,
+                                             out.data_ptr(), _stream(x)), "mpgnn_linear_fwd (log_softmax)")
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import _lib
+        from .functional import _mask_source, _stream, _workspace, mark_premasked
+        x, weight, logp = ctx.saved_tensors
+        g = g.contiguous()
+        n, f = x.shape
+        o = weight.shape[0]
+        src = _mask_source(ctx) if ctx.needs_input_grad[0] else None
+        gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        gw = torch.empty(o, f, dtype=torch.float32, device=x.device)
+        gb = torch.empty(o, dtype=torch.float32, device=x.device) if ctx.has_bias else None
+        key = ("lsm", n, f, o)
+        nb = _WGRAD_WS.get(key)
+        if nb is None:
+            nbytes = ctypes.c_int64()
+            _lib.check(_lib.lib.mpgnn_linear_logsoftmax_bwd_workspace_bytes(n, f, o, ctypes.byref(nbytes)),
+                       "mpgnn_linear_logsoftmax_bwd_workspace_bytes")
+            nb = _WGRAD_WS[key] = int(nbytes.value)
+        ws = _workspace(nb, x.device)
+        _lib.check(_lib.lib.mpgnn_linear_logsoftmax_bwd(g.data_ptr(), logp.data_ptr(), x.data_ptr(), n, f, o,
+                                                        weight.data_ptr(), x.data_ptr() if src is not None else None,
+                                                        gx.data_ptr() if gx is not None else None, gw.data_ptr(),
+                                                        gb.data_ptr() if gb is not None else None, ws.data_ptr(),
+                                                        _stream(x)), "mpgnn_linear_logsoftmax_bwd")
+        if src is not None:
+            mark_premasked(gx, src)
+        return gx, gw if ctx.needs_input_grad[1] else None, gb if ctx.needs_input_grad[2] else None
+
+
+def head_log_softmax(layer: torch.nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    """``F.log_softmax(layer(x), dim=1)`` (Net's output, model.py:147-148): _HeadLogSoftmax for
+    fp32 CUDA inputs with O <= 8, F <= 256 (F % 4 == 0, 16-byte aligned), else the two ops."""
+    w, b = layer.weight, layer.bias
+    if (_HEAD_FUSE and x.dim() == 2 and x.is_cuda and x.is_contiguous() and w.dim() == 2 and w.shape[1] == x.shape[1]
+            and w.shape[0] <= 8 and x.shape[1] <= 256 and x.shape[1] % 4 == 0 and w.is_contiguous()
+            and (b is None or tuple(b.shape) == (w.shape[0],)) and _aligned(x, w, b)):
+        return _HeadLogSoftmax.apply(x, w, b)
+    return F.log_softmax(linear(layer, x), dim=1)
+
+
 def linear(layer: torch.nn.Linear, x: torch.Tensor, activation=None) -> torch.Tensor:
     """``layer(x)`` (``F.relu(layer(x))`` with ``activation='relu'``) with the heads' HIP forward /
     input gradient where covered and the split-K weight gradient above (same parameters)."""
@@ -204,6 +268,8 @@ class _FastTrainToggle:
 _GRAD_STASH = os.environ.get("MPGNN_GRAD_STASH", "1") != "0"
 # MPGNN_RELU_FUSE=0: each of Net's ReLU backwards a launch of its own (A/B switch; same values)
 _RELU_FUSE = os.environ.get("MPGNN_RELU_FUSE", "1") != "0"
+# MPGNN_HEAD_FUSE=0: Net's head as F.linear + F.log_softmax (A/B switch; rounding-level differences)
+_HEAD_FUSE = os.environ.get("MPGNN_HEAD_FUSE", "1") != "0"
 
 
 def _forward_hooked(*mods) -> bool:
@@ -244,8 +310,7 @@ class Net(_FastTrainToggle, torch.nn.Module):
                      **kw)
             if internal:
                 x._mpgnn_relu_internal = True
-        x = linear(self.LinearLayer, x)
-        return F.log_softmax(x, dim=1)
+        return head_log_softmax(self.LinearLayer, x)  # F.log_softmax(self.LinearLayer(x), dim=1)
 
 
 class MPNetm(_FastTrainToggle, torch.nn.Module):

@@ -1707,7 +1707,7 @@ def test_adam_step_bit_identical_to_torch(capturable):
 @pytest.mark.parametrize("name,hidden,classes", [("C1", 64, 5), ("fb15k237", 128, 2)])
 def test_net_relu_backward_fused_bit_identical(name, hidden, classes, monkeypatch):
     """Net's ReLU backwards fused into the consumers' input-gradient kernels (grad_x of the next
-    conv: mpgnn_rgcn_bwd_relu_in, the head: mpgnn_linear_dgrad_relu_in) give every parameter
+    conv: mpgnn_rgcn_bwd_relu_in, the head: mpgnn_linear_logsoftmax_bwd's relu_in) give every parameter
     gradient bit for bit as the separate relu_bwd launches (MPGNN_RELU_FUSE=0), with no
     relu_bwd launch left; a forward hook on a conv turns the fusion off (its output observable)."""
     import mpgnn_amd.functional as fnl
@@ -1751,7 +1751,41 @@ def test_net_relu_backward_fused_bit_identical(name, hidden, classes, monkeypatc
     assert c_ref.get("mpgnn_relu_bwd", 0) == 3 and c_hook.get("mpgnn_relu_bwd", 0) == 3, (c_ref, c_hook)
     assert c_got.get("mpgnn_relu_bwd", 0) == 0, c_got
     # conv2's two uses (C1, F = 64: the accumulating call is refused, then a fresh one: three calls)
-    assert c_got.get("mpgnn_rgcn_bwd_relu_in", 0) >= 2 and c_got.get("mpgnn_linear_dgrad_relu_in", 0) == 1, c_got
+    assert c_got.get("mpgnn_rgcn_bwd_relu_in", 0) >= 2, c_got
+    # the head (Net.lin + log_softmax, one fused backward) takes the last layer's ReLU mask
+    assert c_got.get("mpgnn_linear_logsoftmax_bwd", 0) == 1, c_got
     for k in ref:
         assert torch.equal(ref[k], got[k]), k
         assert torch.equal(ref[k], hooked[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,f,o,relu_in", [(14541, 128, 2, True), (1000, 64, 5, False), (37, 16, 8, True),
+                                           (300, 256, 3, False)])
+def test_head_log_softmax_vs_torch(n, f, o, relu_in):
+    """model.head_log_softmax (Net.lin + F.log_softmax, model.py:147-148: mpgnn_linear_fwd with
+    MPGNN_ACT_LOG_SOFTMAX, mpgnn_linear_logsoftmax_bwd) against torch's F.linear + F.log_softmax
+    in float64: the log-probabilities, grad_input (with the input's ReLU backward fused when the
+    input is tagged internal, against relu's autograd) and the weight / bias gradients, within
+    the suite's fp32 bars."""
+    from mpgnn_amd import model as mdl
+    gen = torch.Generator().manual_seed(n + f + o)
+    lin = torch.nn.Linear(f, o).to(DEV)
+    pre = torch.randn(n, f, generator=gen).to(DEV).requires_grad_(True)
+    x = torch.relu(pre) if relu_in else pre * 1.0
+    gout = torch.randn(n, o, generator=gen).to(DEV)
+    if relu_in:
+        x._mpgnn_relu_internal = True
+    out = mdl.head_log_softmax(lin, x)
+    out.backward(gout)
+    # float64 truth through torch's autograd
+    pre64 = pre.detach().double().requires_grad_(True)
+    w64 = lin.weight.detach().double().requires_grad_(True)
+    b64 = lin.bias.detach().double().requires_grad_(True)
+    x64 = torch.relu(pre64) if relu_in else pre64 * 1.0
+    ref = torch.nn.functional.log_softmax(torch.nn.functional.linear(x64, w64, b64), dim=1)
+    ref.backward(gout.double())
+    for what, got, want in (("logp", out, ref), ("grad_input", pre.grad, pre64.grad),
+                            ("grad_weight", lin.weight.grad, w64.grad), ("grad_bias", lin.bias.grad, b64.grad)):
+        err = normwise_err(got.double().cpu(), want.detach().cpu())
+        assert err <= 1e-5, (what, err)

@@ -98,7 +98,6 @@ def test_net_shared_conv2_grads_bit_identical_to_autograd_accumulation(kind, lay
     for li in range(layers):
         conv = net.conv1 if li == 0 else net.conv2
         h = conv(h, ei, et, activation="relu")
-    h = mpgnn_amd.model.linear(net.LinearLayer, h)
-    loss_of(torch.nn.functional.log_softmax(h, dim=1)).backward()
+    loss_of(mpgnn_amd.model.head_log_softmax(net.LinearLayer, h)).backward()  # Net's head, as Net runs it
     for n, p in net.named_parameters():
         assert torch.equal(got[n], p.grad), n
