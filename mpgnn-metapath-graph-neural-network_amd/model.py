@@ -272,9 +272,16 @@ _RELU_FUSE = os.environ.get("MPGNN_RELU_FUSE", "1") != "0"
 _HEAD_FUSE = os.environ.get("MPGNN_HEAD_FUSE", "1") != "0"
 
 
-def _forward_hooked(*mods) -> bool:
+def _hooked(*mods) -> bool:
+    """A forward hook (sees the activations) or a module backward hook (sees their gradients) on
+    any of mods, or a global one: Net's activations are then observable, not internal."""
     from torch.nn.modules import module as _m
-    return bool(_m._global_forward_hooks) or any(m._forward_hooks for m in mods)
+    glob = (_m._global_forward_hooks, getattr(_m, "_global_backward_hooks", None),
+            getattr(_m, "_global_backward_pre_hooks", None))
+    if any(g for g in glob):
+        return True
+    return any(m._forward_hooks or getattr(m, "_backward_hooks", None) or getattr(m, "_backward_pre_hooks", None)
+               for m in mods)
 
 
 class Net(_FastTrainToggle, torch.nn.Module):
@@ -295,11 +302,11 @@ class Net(_FastTrainToggle, torch.nn.Module):
             # conv2's gradients over its uses summed inside the backward kernels (GradStash)
             stash = GradStash()
         # the activations between the layers (and into the head) are internal: nothing outside this
-        # forward can observe their gradients unless a forward hook hands them out — then each
+        # forward can observe them or their gradients unless a module hook hands them out — then each
         # ReLU's backward stays a launch of its own instead of being fused into the consumer's
         # input-gradient kernel (functional.premasked)
         internal = shard is None and group is None and x.is_cuda and torch.is_grad_enabled() and _RELU_FUSE and \
-            not _forward_hooked(self.conv1, self.conv2, self.LinearLayer)
+            not _hooked(self.conv1, self.conv2, self.LinearLayer)
         for layer_index in range(0, self.metapath_length):
             conv = self.conv1 if layer_index == 0 else self.conv2
             kw = {}

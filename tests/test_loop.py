@@ -584,3 +584,27 @@ def test_lean_adam_bit_identical_to_torch_fused_adam(capturable):
 def test_loops_use_lean_adam_on_gpu_params_only():
     net = torch.nn.Linear(4, 2)
     assert type(main._adam(net)) is torch.optim.Adam  # CPU parameters: torch's (unfused) Adam
+
+
+def test_net_activations_internal_only_without_module_hooks():
+    """Net fuses its ReLU backwards into the consumers' input-gradient kernels only while its
+    activations are internal: a forward hook (sees them) or a module backward hook (sees their
+    gradients) on a conv or the head, or a global one, turns the fusion off (model._hooked)."""
+    from mpgnn_amd import model as mdl
+    net = mpgnn_amd.Net(8, 8, 3, 8, 2, 3)
+    mods = (net.conv1, net.conv2, net.LinearLayer)
+    assert not mdl._hooked(*mods)
+    for reg in (lambda m: m.register_forward_hook(lambda *_: None),
+                lambda m: m.register_full_backward_hook(lambda *_: None),
+                lambda m: m.register_full_backward_pre_hook(lambda *_: None)):
+        for m in mods:
+            h = reg(m)
+            assert mdl._hooked(*mods)
+            h.remove()
+            assert not mdl._hooked(*mods)
+    h = torch.nn.modules.module.register_module_full_backward_hook(lambda *_: None)
+    try:
+        assert mdl._hooked(*mods)
+    finally:
+        h.remove()
+    assert not mdl._hooked(*mods)
