@@ -361,5 +361,6 @@ class MPNetm(_FastTrainToggle, torch.nn.Module):
         # torch.cat of ONE embedding (a single metapath) is a copy of it: skipped, same values
         concatenated_embedding = embeddings[0] if len(embeddings) == 1 else torch.cat(embeddings, dim=1)
         h = linear(self.fc1, concatenated_embedding, activation="relu")  # F.relu(fc1(.)), model.py:225
-        h = linear(self.fc2, h)
-        return self.log_softmax(h)
+        if _hooked(self.fc2, self.log_softmax):
+            return self.log_softmax(linear(self.fc2, h))
+        return head_log_softmax(self.fc2, h)  # self.log_softmax(self.fc2(h)), model.py:226-227
