@@ -233,7 +233,18 @@ int32_t mpgnn_nll_rows_bwd(const float* grad_loss, const float* total_weight, in
  * bit-identical to the zero fill + mpgnn_nll_rows_bwd. */
 int32_t mpgnn_nll_rows_bwd_dense(const float* grad_loss, const float* total_weight, int64_t rows, int32_t num_classes,
                                  const int32_t* row_ptr, const int32_t* row_perm, const int64_t* target,
-                                 int64_t ignore_index, float* grad_logp, void* stream);
+                                 int64_t ignore_index, const float* class_weight, float* grad_logp, void* stream);
+/* The class-weighted loss of main_rgcn.py's training step (F.nll_loss(out[train_idx], train_y,
+ * weight=class_weight), main_rgcn.py:376-380): each kept pair weighted by class_weight[target]
+ * (float [num_classes], device; NULL: 1 — exactly the unweighted calls above), *total_weight =
+ * the sum of the kept pairs' weights, *loss = -(Σ w·logp) / *total_weight; the gradient
+ * -(w · (*grad_loss / *total_weight)) per pair. mpgnn_nll_rows_bwd_dense takes class_weight too. */
+int32_t mpgnn_nll_rows_fwd_weighted(const float* logp, int64_t rows, int32_t num_classes, const int64_t* row_idx,
+                                    const int64_t* target, int64_t n, int64_t ignore_index, const float* class_weight,
+                                    float* loss, float* total_weight, void* stream);
+int32_t mpgnn_nll_rows_bwd_weighted(const float* grad_loss, const float* total_weight, int64_t rows,
+                                    int32_t num_classes, const int64_t* row_idx, const int64_t* target, int64_t n,
+                                    int64_t ignore_index, const float* class_weight, float* grad_logp, void* stream);
 
 /* Forward and input gradient of the wrappers' Linear heads (Net.lin model.py:147; MPNetm.fc1 /
  * fc2 model.py:224-226), replacing F.linear / grad_out @ weight (host-cheap single launches on the

@@ -113,7 +113,9 @@ SIGNATURES = [
     ("mpgnn_confusion_counts", _I32, [_P, _I64, _I32, _I32, _P, _P, _P, _P, _P]),
     ("mpgnn_nll_rows_fwd", _I32, [_P, _I64, _I32, _P, _P, _I64, _I64, _P, _P, _P]),
     ("mpgnn_nll_rows_bwd", _I32, [_P, _P, _I64, _I32, _P, _P, _I64, _I64, _P, _P]),
-    ("mpgnn_nll_rows_bwd_dense", _I32, [_P, _P, _I64, _I32, _P, _P, _P, _I64, _P, _P]),
+    ("mpgnn_nll_rows_bwd_dense", _I32, [_P, _P, _I64, _I32, _P, _P, _P, _I64, _P, _P, _P]),
+    ("mpgnn_nll_rows_fwd_weighted", _I32, [_P, _I64, _I32, _P, _P, _I64, _I64, _P, _P, _P, _P]),
+    ("mpgnn_nll_rows_bwd_weighted", _I32, [_P, _P, _I64, _I32, _P, _P, _I64, _I64, _P, _P, _P]),
     ("mpgnn_score_bag_argmax", _I32, [_P, _P, _I32, _P, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("mpgnn_score_bag_argmax_bwd", _I32, [_P, _I64, _P, _P, _P, _P, _P, _P, _I32, _I64, _P, _P, _P, _P, _P, _P,
                                           _P]),

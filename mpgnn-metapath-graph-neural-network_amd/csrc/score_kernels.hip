@@ -430,6 +430,28 @@ struct ConfArgs {
     int64_t* out;                          // [n_lists][3][C]
 };
 
+// the predicted class of score row `row` (first maximum, a NaN wins: torch.argmax); C: none
+__device__ __forceinline__ int conf_pred(const ConfArgs& a, int64_t row) {
+    const int C = a.C;
+    if (row < 0 || row >= a.rows) return C;  // a row outside the score matrix predicts no class
+    const float* s = a.scores + row * (int64_t)C;
+    float bv = s[0];
+    int pc = 0;
+    for (int c = 1; c < C; ++c) {
+        const float v = s[c];
+        if (takes_over(bv, v)) {
+            bv = v;
+            pc = c;
+        }
+    }
+    return pc;
+}
+
+// One workgroup per list. C <= kConfRegC (the loops' 2 classes): each thread counts in registers,
+// the counts are summed by wave butterflies and one LDS add per wave and counter (integer sums:
+// any order, the same counts); wider C: LDS atomics per pair. Pairs in batches of kConfBatch per
+// thread (their list loads, then their score rows: two round trips per batch, not per pair).
+constexpr int kConfRegC = 8, kConfBatch = 8;  // 8192 pairs per pass: the loops' lists in one pass
 __global__ __launch_bounds__(kConfThreads) void confusion_counts_kernel(ConfArgs a) {
     extern __shared__ int conf_lds[];  // [3][C + 1]
     const int C = a.C, L = (int)blockIdx.x;
@@ -438,26 +460,54 @@ __global__ __launch_bounds__(kConfThreads) void confusion_counts_kernel(ConfArgs
     const int64_t* idx = a.idx[L];
     const int64_t* lab = a.labels[L];
     const int64_t n = a.n[L];
-    for (int64_t j = threadIdx.x; j < n; j += kConfThreads) {
-        const int64_t row = idx ? idx[j] : j;
-        int pc = C;  // a row outside the score matrix predicts no class
-        if (row >= 0 && row < a.rows) {
-            const float* s = a.scores + row * (int64_t)C;
-            float bv = s[0];
-            pc = 0;
-            for (int c = 1; c < C; ++c) {
-                const float v = s[c];
-                if (takes_over(bv, v)) {
-                    bv = v;
-                    pc = c;
+    const bool reg = C <= kConfRegC;
+    int cp[kConfRegC], cy[kConfRegC], cm[kConfRegC];
+#pragma unroll
+    for (int c = 0; c < kConfRegC; ++c) cp[c] = cy[c] = cm[c] = 0;
+    for (int64_t j0 = threadIdx.x; j0 < n; j0 += (int64_t)kConfBatch * kConfThreads) {
+        int64_t row[kConfBatch], y[kConfBatch];
+#pragma unroll
+        for (int u = 0; u < kConfBatch; ++u) {
+            const int64_t j = j0 + (int64_t)u * kConfThreads;
+            row[u] = j < n ? (idx ? idx[j] : j) : -1;
+            y[u] = j < n ? lab[j] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kConfBatch; ++u) {
+            if (j0 + (int64_t)u * kConfThreads >= n) break;
+            const int pc = conf_pred(a, row[u]);
+            const int yc = (y[u] >= 0 && y[u] < C) ? (int)y[u] : C;
+            if (reg) {
+#pragma unroll
+                for (int c = 0; c < kConfRegC; ++c) {
+                    cp[c] += pc == c;
+                    cy[c] += yc == c;
+                    cm[c] += (pc == yc && yc == c);
                 }
+            } else {
+                atomicAdd(&conf_lds[pc], 1);
+                atomicAdd(&conf_lds[(C + 1) + yc], 1);
+                atomicAdd(&conf_lds[2 * (C + 1) + (pc == yc ? yc : C)], 1);
             }
         }
-        const int64_t y = lab[j];
-        const int yc = (y >= 0 && y < C) ? (int)y : C;
-        atomicAdd(&conf_lds[pc], 1);
-        atomicAdd(&conf_lds[(C + 1) + yc], 1);
-        atomicAdd(&conf_lds[2 * (C + 1) + (pc == yc ? yc : C)], 1);
+    }
+    if (reg) {
+#pragma unroll
+        for (int c = 0; c < kConfRegC; ++c) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                cp[c] += __shfl_xor(cp[c], o);
+                cy[c] += __shfl_xor(cy[c], o);
+                cm[c] += __shfl_xor(cm[c], o);
+            }
+        }
+        if ((threadIdx.x & 63) == 0) {
+            for (int c = 0; c < C; ++c) {
+                atomicAdd(&conf_lds[c], cp[c]);
+                atomicAdd(&conf_lds[(C + 1) + c], cy[c]);
+                atomicAdd(&conf_lds[2 * (C + 1) + c], cm[c]);
+            }
+        }
     }
     __syncthreads();
     for (int k = threadIdx.x; k < 3 * C; k += kConfThreads)
@@ -476,13 +526,20 @@ __global__ __launch_bounds__(kConfThreads) void confusion_counts_kernel(ConfArgs
 // host validates the lists once, metrics.nll_loss_rows).
 // ---------------------------------------------------------------------------------------
 constexpr int kNllThreads = 1024;
+constexpr int kNllWClasses = 1024;
 
 __global__ __launch_bounds__(kNllThreads) void nll_rows_fwd_kernel(const float* __restrict__ logp, int64_t rows, int C,
                                                                    const int64_t* __restrict__ idx,
                                                                    const int64_t* __restrict__ tgt, int64_t n,
-                                                                   int64_t ignore, float* __restrict__ loss,
+                                                                   int64_t ignore, const float* __restrict__ cw,
+                                                                   float* __restrict__ loss,
                                                                    float* __restrict__ total_weight) {
     __shared__ float s_sum[kNllThreads / 64], s_w[kNllThreads / 64];
+    __shared__ float s_cw[kNllWClasses];  // the class weights (C <= kNllWClasses), read once
+    const bool lds_w = cw != nullptr && C <= kNllWClasses;
+    if (lds_w)
+        for (int k = threadIdx.x; k < C; k += kNllThreads) s_cw[k] = cw[k];
+    __syncthreads();
     // kNllBatch pairs per thread in flight: the list loads of a batch, then its matrix loads
     // (two memory round trips per batch instead of two per pair)
     constexpr int kNllBatch = 8;
@@ -504,8 +561,10 @@ __global__ __launch_bounds__(kNllThreads) void nll_rows_fwd_kernel(const float* 
 #pragma unroll
         for (int u = 0; u < kNllBatch; ++u)
             if (t[u] != ignore) {
-                sum += v[u];
-                w += 1.f;
+                // class weight of the pair (F.nll_loss(weight=...)); 1 without weights (1·v = v)
+                const float wt = (cw != nullptr && t[u] >= 0 && t[u] < C) ? (lds_w ? s_cw[t[u]] : cw[t[u]]) : 1.f;
+                sum += wt * v[u];
+                w += wt;
             }
     }
 #pragma unroll
@@ -534,13 +593,15 @@ __global__ __launch_bounds__(kScoreThreads) void nll_rows_bwd_kernel(const float
                                                                      const float* __restrict__ total_weight,
                                                                      int64_t rows, int C, const int64_t* __restrict__ idx,
                                                                      const int64_t* __restrict__ tgt, int64_t n,
-                                                                     int64_t ignore, float* __restrict__ grad) {
+                                                                     int64_t ignore, const float* __restrict__ cw,
+                                                                     float* __restrict__ grad) {
     const int64_t j = (int64_t)blockIdx.x * kScoreThreads + threadIdx.x;
     if (j >= n) return;
     const int64_t t = tgt[j];
     const int64_t r = idx[j];
     if (t == ignore || r < 0 || r >= rows || t < 0 || t >= C) return;
-    atomicAdd(grad + r * C + t, -(grad_loss[0] / total_weight[0]));  // equal addends: order-free
+    // equal addends per (row, class): order-free
+    atomicAdd(grad + r * C + t, -((cw != nullptr ? cw[t] : 1.f) * (grad_loss[0] / total_weight[0])));
 }
 
 }  // namespace
@@ -704,16 +765,24 @@ extern "C" int32_t mpgnn_confusion_counts(const float* scores, int64_t rows, int
     return hip_status(hipGetLastError(), "confusion_counts_kernel launch");
 }
 
+extern "C" int32_t mpgnn_nll_rows_fwd_weighted(const float* logp, int64_t rows, int32_t num_classes,
+                                               const int64_t* row_idx, const int64_t* target, int64_t n,
+                                               int64_t ignore_index, const float* class_weight, float* loss,
+                                               float* total_weight, void* stream) {
+    if (rows < 0 || num_classes <= 0 || n < 0) return arg_fail("mpgnn_nll_rows_fwd_weighted: bad sizes");
+    if (!loss || !total_weight || (n > 0 && (!logp || !row_idx || !target)))
+        return arg_fail("mpgnn_nll_rows_fwd_weighted: NULL argument");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(nll_rows_fwd_kernel, dim3(1), dim3(kNllThreads), 0, strm, logp, rows, (int)num_classes, row_idx,
+                       target, n, ignore_index, class_weight, loss, total_weight);
+    return hip_status(hipGetLastError(), "nll_rows_fwd_kernel launch");
+}
+
 extern "C" int32_t mpgnn_nll_rows_fwd(const float* logp, int64_t rows, int32_t num_classes, const int64_t* row_idx,
                                       const int64_t* target, int64_t n, int64_t ignore_index, float* loss,
                                       float* total_weight, void* stream) {
-    if (rows < 0 || num_classes <= 0 || n < 0) return arg_fail("mpgnn_nll_rows_fwd: bad sizes");
-    if (!loss || !total_weight || (n > 0 && (!logp || !row_idx || !target)))
-        return arg_fail("mpgnn_nll_rows_fwd: NULL argument");
-    hipStream_t strm = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(nll_rows_fwd_kernel, dim3(1), dim3(kNllThreads), 0, strm, logp, rows, (int)num_classes, row_idx,
-                       target, n, ignore_index, loss, total_weight);
-    return hip_status(hipGetLastError(), "nll_rows_fwd_kernel launch");
+    return mpgnn_nll_rows_fwd_weighted(logp, rows, num_classes, row_idx, target, n, ignore_index, nullptr, loss,
+                                       total_weight, stream);
 }
 
 // The same gradient written whole (no zero fill before it): one thread per (row, class), the
@@ -723,7 +792,7 @@ extern "C" int32_t mpgnn_nll_rows_fwd(const float* logp, int64_t rows, int32_t n
 __global__ __launch_bounds__(kScoreThreads) void nll_rows_bwd_dense_kernel(
     const float* __restrict__ grad_loss, const float* __restrict__ total_weight, int64_t rows, int C,
     const int* __restrict__ row_ptr, const int* __restrict__ row_perm, const int64_t* __restrict__ tgt,
-    int64_t ignore, float* __restrict__ grad) {
+    int64_t ignore, const float* __restrict__ cw, float* __restrict__ grad) {
     const int64_t e = (int64_t)blockIdx.x * kScoreThreads + threadIdx.x;
     if (e >= rows * C) return;
     const int64_t i = e / C;
@@ -732,15 +801,15 @@ __global__ __launch_bounds__(kScoreThreads) void nll_rows_bwd_dense_kernel(
     const int p1 = row_ptr[i + 1];
     for (int p = row_ptr[i]; p < p1; ++p) {
         const int64_t t = tgt[row_perm[p]];
-        if (t != ignore && t == c) v += -(grad_loss[0] / total_weight[0]);
+        if (t != ignore && t == c) v += -((cw != nullptr ? cw[c] : 1.f) * (grad_loss[0] / total_weight[0]));
     }
     grad[e] = v;
 }
 
 extern "C" int32_t mpgnn_nll_rows_bwd_dense(const float* grad_loss, const float* total_weight, int64_t rows,
                                             int32_t num_classes, const int32_t* row_ptr, const int32_t* row_perm,
-                                            const int64_t* target, int64_t ignore_index, float* grad_logp,
-                                            void* stream) {
+                                            const int64_t* target, int64_t ignore_index, const float* class_weight,
+                                            float* grad_logp, void* stream) {
     if (rows < 0 || num_classes <= 0 || rows * num_classes / kScoreThreads >= (int64_t)INT32_MAX)
         return arg_fail("mpgnn_nll_rows_bwd_dense: bad sizes");
     if (rows == 0) return MPGNN_OK;
@@ -750,21 +819,29 @@ extern "C" int32_t mpgnn_nll_rows_bwd_dense(const float* grad_loss, const float*
     const int64_t total = rows * num_classes;
     hipLaunchKernelGGL(nll_rows_bwd_dense_kernel, dim3((unsigned)((total + kScoreThreads - 1) / kScoreThreads)),
                        dim3(kScoreThreads), 0, strm, grad_loss, total_weight, rows, (int)num_classes, row_ptr, row_perm,
-                       target, ignore_index, grad_logp);
+                       target, ignore_index, class_weight, grad_logp);
     return hip_status(hipGetLastError(), "nll_rows_bwd_dense_kernel launch");
+}
+
+extern "C" int32_t mpgnn_nll_rows_bwd_weighted(const float* grad_loss, const float* total_weight, int64_t rows,
+                                               int32_t num_classes, const int64_t* row_idx, const int64_t* target,
+                                               int64_t n, int64_t ignore_index, const float* class_weight,
+                                               float* grad_logp, void* stream) {
+    if (rows < 0 || num_classes <= 0 || n < 0 || n / kScoreThreads >= (int64_t)INT32_MAX)
+        return arg_fail("mpgnn_nll_rows_bwd_weighted: bad sizes");
+    if (n == 0) return MPGNN_OK;
+    if (!grad_loss || !total_weight || !row_idx || !target || !grad_logp)
+        return arg_fail("mpgnn_nll_rows_bwd_weighted: NULL argument");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    const unsigned grid = (unsigned)((n + kScoreThreads - 1) / kScoreThreads);
+    hipLaunchKernelGGL(nll_rows_bwd_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, grad_loss, total_weight, rows,
+                       (int)num_classes, row_idx, target, n, ignore_index, class_weight, grad_logp);
+    return hip_status(hipGetLastError(), "nll_rows_bwd_kernel launch");
 }
 
 extern "C" int32_t mpgnn_nll_rows_bwd(const float* grad_loss, const float* total_weight, int64_t rows,
                                       int32_t num_classes, const int64_t* row_idx, const int64_t* target, int64_t n,
                                       int64_t ignore_index, float* grad_logp, void* stream) {
-    if (rows < 0 || num_classes <= 0 || n < 0 || n / kScoreThreads >= (int64_t)INT32_MAX)
-        return arg_fail("mpgnn_nll_rows_bwd: bad sizes");
-    if (n == 0) return MPGNN_OK;
-    if (!grad_loss || !total_weight || !row_idx || !target || !grad_logp)
-        return arg_fail("mpgnn_nll_rows_bwd: NULL argument");
-    hipStream_t strm = static_cast<hipStream_t>(stream);
-    const unsigned grid = (unsigned)((n + kScoreThreads - 1) / kScoreThreads);
-    hipLaunchKernelGGL(nll_rows_bwd_kernel, dim3(grid), dim3(kScoreThreads), 0, strm, grad_loss, total_weight, rows,
-                       (int)num_classes, row_idx, target, n, ignore_index, grad_logp);
-    return hip_status(hipGetLastError(), "nll_rows_bwd_kernel launch");
+    return mpgnn_nll_rows_bwd_weighted(grad_loss, total_weight, rows, num_classes, row_idx, target, n, ignore_index,
+                                       nullptr, grad_logp, stream);
 }

@@ -43,7 +43,8 @@ def _train_step(model, optimizer, data):
     out = _forward(model, data)
     weights = class_weight_balanced(data.train_y)
     weights_tensor = class_weight_tensor(data.train_y, out.device)
-    loss = F.nll_loss(take_rows(out, data.train_idx).squeeze(-1), data.train_y, weight=weights_tensor)
+    # F.nll_loss(out[train_idx], train_y, weight=weights_tensor): one launch each way on the GPU
+    loss = nll_loss_rows(out, data.train_idx, data.train_y, weight=weights_tensor)
     loss.backward()
     optimizer.step()
     return loss.detach(), weights

@@ -144,15 +144,16 @@ class _NllRows(torch.autograd.Function):
     index_select, nll_loss and their backward, 7 launches."""
 
     @staticmethod
-    def forward(ctx, logp, idx, target):
+    def forward(ctx, logp, idx, target, weight=None):
         from . import _lib
         from .functional import _stream
         loss = torch.empty((), dtype=torch.float32, device=logp.device)
         tw = torch.empty((), dtype=torch.float32, device=logp.device)
-        _lib.check(_lib.lib.mpgnn_nll_rows_fwd(logp.data_ptr(), logp.shape[0], logp.shape[1], idx.data_ptr(),
-                                               target.data_ptr(), idx.numel(), -100, loss.data_ptr(), tw.data_ptr(),
-                                               _stream(logp)), "mpgnn_nll_rows_fwd")
-        ctx.lists = (idx, target, tw)
+        wp = weight.data_ptr() if weight is not None else None
+        _lib.check(_lib.lib.mpgnn_nll_rows_fwd_weighted(logp.data_ptr(), logp.shape[0], logp.shape[1], idx.data_ptr(),
+                                                        target.data_ptr(), idx.numel(), -100, wp, loss.data_ptr(),
+                                                        tw.data_ptr(), _stream(logp)), "mpgnn_nll_rows_fwd")
+        ctx.lists = (idx, target, tw, weight)
         ctx.shape = tuple(logp.shape)
         ctx.csr = _rows_csr(idx, logp.shape[0])
         return loss
@@ -161,20 +162,21 @@ class _NllRows(torch.autograd.Function):
     def backward(ctx, g):
         from . import _lib
         from .functional import _stream
-        idx, target, tw = ctx.lists
+        idx, target, tw, weight = ctx.lists
+        wp = weight.data_ptr() if weight is not None else None
         g = g.contiguous()
         if ctx.csr is not None:
             grad = torch.empty(ctx.shape, dtype=torch.float32, device=g.device)
             ptr, perm = ctx.csr
             _lib.check(_lib.lib.mpgnn_nll_rows_bwd_dense(g.data_ptr(), tw.data_ptr(), ctx.shape[0], ctx.shape[1],
-                                                         ptr.data_ptr(), perm.data_ptr(), target.data_ptr(), -100,
+                                                         ptr.data_ptr(), perm.data_ptr(), target.data_ptr(), -100, wp,
                                                          grad.data_ptr(), _stream(grad)), "mpgnn_nll_rows_bwd_dense")
-            return grad, None, None
+            return grad, None, None, None
         grad = torch.zeros(ctx.shape, dtype=torch.float32, device=g.device)
-        _lib.check(_lib.lib.mpgnn_nll_rows_bwd(g.data_ptr(), tw.data_ptr(), ctx.shape[0], ctx.shape[1], idx.data_ptr(),
-                                               target.data_ptr(), idx.numel(), -100, grad.data_ptr(), _stream(grad)),
-                   "mpgnn_nll_rows_bwd")
-        return grad, None, None
+        _lib.check(_lib.lib.mpgnn_nll_rows_bwd_weighted(g.data_ptr(), tw.data_ptr(), ctx.shape[0], ctx.shape[1],
+                                                        idx.data_ptr(), target.data_ptr(), idx.numel(), -100, wp,
+                                                        grad.data_ptr(), _stream(grad)), "mpgnn_nll_rows_bwd")
+        return grad, None, None, None
 
 
 # the (row list, target list) pairs last checked in range, by OBJECT (weakrefs) and _version, with
@@ -198,9 +200,10 @@ def _nll_lists_valid(idx: torch.Tensor, target: torch.Tensor, rows: int, c: int)
     return ok
 
 
-def nll_loss_rows(logp: torch.Tensor, idx, target: torch.Tensor) -> torch.Tensor:
-    """``F.nll_loss(logp[idx].squeeze(-1), target)`` — the loops' loss (main.py:1065, 1088,
-    1106, main_rgcn.py:402, 422; mean over the listed rows, ignore_index -100, no class weights). On the GPU
+def nll_loss_rows(logp: torch.Tensor, idx, target: torch.Tensor, weight=None) -> torch.Tensor:
+    """``F.nll_loss(logp[idx].squeeze(-1), target, weight=weight)`` — the loops' losses (main.py:1065,
+    1088, 1106, main_rgcn.py:402, 422 unweighted; main_rgcn.py:376-380's training step with the
+    balanced class weights); mean over the listed rows, ignore_index -100. On the GPU
     (float32 [rows, C >= 2] log-probabilities, 1-D int64 row and target lists on the same device,
     lists checked in range once) ``mpgnn_nll_rows_fwd`` / ``_bwd``: the same loss up to the
     summation order (a few ulp), the same input gradient bit for bit (tests/test_loop.py).
@@ -210,12 +213,15 @@ def nll_loss_rows(logp: torch.Tensor, idx, target: torch.Tensor) -> torch.Tensor
             and torch.is_tensor(idx) and idx.dim() == 1 and idx.dtype == torch.int64 and idx.device == logp.device
             and torch.is_tensor(target) and target.dim() == 1 and target.dtype == torch.int64
             and target.device == logp.device and target.numel() == idx.numel()
+            and (weight is None or (torch.is_tensor(weight) and weight.dtype == torch.float32
+                                    and weight.device == logp.device and tuple(weight.shape) == (logp.shape[1],)))
             and _nll_lists_valid(idx, target, logp.shape[0], logp.shape[1]))
     if fast:
-        return _NllRows.apply(logp.contiguous(), idx.contiguous(), target.contiguous())
+        return _NllRows.apply(logp.contiguous(), idx.contiguous(), target.contiguous(),
+                              weight.contiguous() if weight is not None else None)
     rows = logp.index_select(0, idx.to(logp.device)) if torch.is_tensor(idx) and idx.dim() == 1 and idx.dtype in (
         torch.int64, torch.int32) else logp[idx]
-    return torch.nn.functional.nll_loss(rows.squeeze(-1), target)
+    return torch.nn.functional.nll_loss(rows.squeeze(-1), target, weight=weight)
 
 
 def _num_cols(t: torch.Tensor) -> int:

@@ -275,6 +275,32 @@ def test_nll_loss_rows_kernel_vs_torch(seed, rows, c, n, dup, ignore):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed,rows,c,n,dup,ignore", [(0, 14541, 2, 4847, False, False), (1, 3000, 5, 2500, True, True),
+                                                      (4, 5000, 40, 4000, True, False)])
+def test_nll_loss_rows_class_weighted_vs_torch(seed, rows, c, n, dup, ignore):
+    """metrics.nll_loss_rows(..., weight=w) on the GPU (mpgnn_nll_rows_fwd_weighted and the dense
+    / scatter backward with class weights) against F.nll_loss(..., weight=w) — main_rgcn.py's
+    training loss (main_rgcn.py:376-380): the loss within the summation-order bar, the gradient
+    of the softmax input within 1e-6 of its largest entry (torch's per-pair value is -(w·(g /
+    total_weight)) too; repeated rows are summed in another order)."""
+    h, idx, y = _nll_case(seed, rows, c, n, dup, ignore)
+    dev = torch.device("cuda", 0)
+    w = (torch.rand(c, generator=torch.Generator().manual_seed(seed + 7)) + 0.25).to(dev)
+    hd, idx_d, y_d = h.to(dev), idx.to(dev), y.to(dev)
+    ha = hd.clone().requires_grad_(True)
+    hb = hd.clone().requires_grad_(True)
+    la = metrics.nll_loss_rows(torch.log_softmax(ha, 1), idx_d, y_d, weight=w)
+    assert la.grad_fn is not None and "NllRows" in type(la.grad_fn).__name__
+    lb = torch.nn.functional.nll_loss(torch.log_softmax(hb, 1).index_select(0, idx_d), y_d, weight=w)
+    la.backward()
+    lb.backward()
+    assert torch.allclose(la, lb, rtol=1e-6 * max(1.0, n ** 0.5), atol=0), (float(la), float(lb))
+    # repeated rows: torch sums their addends through index_add's atomics, the kernel in row order
+    scale = float(hb.grad.abs().max())
+    assert torch.allclose(ha.grad, hb.grad, rtol=1e-6, atol=1e-6 * scale), float((ha.grad - hb.grad).abs().max())
+
+
+@pytest.mark.gpu
 def test_nll_loss_rows_out_of_range_lists_take_torchs_path():
     """A row or target outside the matrix fails the one-time list check (the call then runs
     torch's ops, which raise torch's error, instead of the kernels); ignore_index passes."""
