@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Kernels of one training epoch from a rocprofv3 kernel trace of `bench.py` (its eager epoch
-leg): the window between two consecutive optimizer (fused Adam) launches in the middle of the
-run, per kernel name: launches, total and average µs, share of the epoch's kernel time, plus the
+leg): the window between the last two optimizer launches (the graph replays' steady state; or,
+--window middle, two in the middle of the run), per kernel name: launches, total and average µs, share of the epoch's kernel time, plus the
 epoch's span and its idle time between kernels.
 usage: python scripts/epoch_kernels.py <run_kernel_trace.csv> [--json out.json]"""
 import argparse
@@ -12,12 +12,15 @@ from collections import defaultdict
 ap = argparse.ArgumentParser()
 ap.add_argument("trace")
 ap.add_argument("--json", default=None)
+ap.add_argument("--window", choices=["last", "middle"], default="last")
 a = ap.parse_args()
 rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
 adam = [i for i, r in enumerate(rows) if "adam" in r["Kernel_Name"].lower()]
 if len(adam) < 3:
     raise SystemExit("fewer than 3 Adam launches in the trace")
-k = len(adam) // 2
+# the last complete window: bench.py's epoch leg ends with the HIP-graph replays (steady state,
+# no host gaps, no one-time setup launches)
+k = len(adam) - 1 if a.window == "last" else len(adam) // 2
 lo, hi = adam[k - 1] + 1, adam[k] + 1  # kernels after one Adam up to and including the next
 win = rows[lo:hi]
 by = defaultdict(lambda: [0, 0.0])
