@@ -190,6 +190,13 @@ int32_t mpgnn_rel_mean_bwd(const mpgnn_plan* plan, int32_t mode, int64_t relatio
  * Net) and of the ReLU after each metapath layer (model.py:213-215). */
 int32_t mpgnn_relu_bwd(const float* grad_out, const float* act_out, int64_t n, float* dst, void* stream);
 
+/* Dropout's backward with the ReLU backward of the layer before it fused (MPNetm: F.relu(conv)
+ * then Dropout(0.6), model.py:211-215): dst[i] = act_out[i] <= 0 ? 0 : grad_out[i] · mask[i] · scale
+ * (torch's native_dropout_backward arithmetic, then threshold_backward's rule; act_out NULL: the
+ * dropout backward alone). mask: the forward's keep mask (bool bytes), scale = 1 / (1 - p). */
+int32_t mpgnn_dropout_relu_bwd(const float* grad_out, const uint8_t* mask, const float* act_out, float scale, int64_t n,
+                               float* dst, void* stream);
+
 /* Weight / bias gradient of the wrappers' Linear heads over all N node rows (Net.lin,
  * model.py:147; MPNetm.fc1/fc2, model.py:224-226): grad_weight[o][f] = Σ_i grad_out[i][o]·x[i][f],
  * grad_bias[o] = Σ_i grad_out[i][o] (nullable), row-sliced partials summed in a fixed order

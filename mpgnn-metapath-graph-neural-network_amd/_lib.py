@@ -96,6 +96,7 @@ SIGNATURES = [
     ("mpgnn_rgcn_bwd_relu_in", _I32, [_P, _I32, _I64, _I32, _P, _I32, _P, _P, _I32, _P, _P, _I64, _I64,
                                       _P, _P, _P, _P, _P, _P, _I32]),
     ("mpgnn_relu_bwd", _I32, [_P, _P, _I64, _P, _P]),
+    ("mpgnn_dropout_relu_bwd", _I32, [_P, _P, _P, ctypes.c_float, _I64, _P, _P]),
     ("mpgnn_linear_wgrad_workspace_bytes", _I32, [_I64, _I32, _I32, _PI64]),
     ("mpgnn_linear_wgrad", _I32, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P]),
     ("mpgnn_linear_fwd", _I32, [_P, _I64, _I32, _P, _I32, _P, _I32, _P, _P]),

@@ -5250,6 +5250,21 @@ __global__ __launch_bounds__(kThreads) void relu_bwd_kernel(const float* g, cons
     for (int64_t k = i; k < n; k += stride) d[k] = relu_bwd_f(g[k], y[k]);
 }
 
+// Dropout's backward (torch's masked_scale: grad · mask · scale) and the ReLU backward of the
+// layer whose output the dropout took (MPNetm: F.relu(conv) then Dropout(0.6), model.py:211-215)
+// in one pass: dst = relu_bwd(g · (float)mask · scale, act) — masked_scale's arithmetic, then
+// threshold_backward's rule.
+__global__ __launch_bounds__(kThreads) void dropout_relu_bwd_kernel(const float* __restrict__ g,
+                                                                    const unsigned char* __restrict__ mask,
+                                                                    const float* __restrict__ act, float scale,
+                                                                    int64_t n, float* __restrict__ d) {
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    for (int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x; k < n; k += stride) {
+        const float v = (g[k] * (float)mask[k]) * scale;
+        d[k] = act != nullptr ? relu_bwd_f(v, act[k]) : v;
+    }
+}
+
 // The wrappers' Linear heads with few outputs (model.py:147 Net.lin, :226 MPNetm.fc2):
 // out[i][o] = act(Σ_f x[i][f]·W[o][f] + b[o]) for O <= 8, F <= 256 (F % 4 == 0). Four rows per
 // wave, 16 lanes per row: lane s of a row holds columns 4s + 64k (k < F/64, rounded up). The
@@ -6974,6 +6989,17 @@ static int32_t linear_dgrad_impl(const float* grad_out, int64_t N, int32_t O, co
     hipLaunchKernelGGL(linear_small_dgrad_kernel, dim3(linear_grid(N * (F / 4))), dim3(kThreads), 0, strm, grad_out, (int)N, O,
                        weight, F, grad_x, mask);
     return hip_check(hipGetLastError(), "linear_small_dgrad_kernel launch");
+}
+
+int32_t mpgnn_dropout_relu_bwd(const float* grad_out, const uint8_t* mask, const float* act_out, float scale, int64_t n,
+                               float* dst, void* stream) {
+    if (n < 0) return arg_error("mpgnn_dropout_relu_bwd: bad n");
+    if (n == 0) return MPGNN_OK;
+    if (!grad_out || !mask || !dst) return arg_error("mpgnn_dropout_relu_bwd: NULL pointer");
+    hipStream_t strm = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(dropout_relu_bwd_kernel, dim3((unsigned)std::min<int64_t>((n + kThreads - 1) / kThreads, 8192)),
+                       dim3(kThreads), 0, strm, grad_out, mask, act_out, scale, n, dst);
+    return hip_check(hipGetLastError(), "dropout_relu_bwd_kernel launch");
 }
 
 int32_t mpgnn_linear_dgrad(const float* grad_out, int64_t N, int32_t O, const float* weight, int32_t F, float* grad_x,

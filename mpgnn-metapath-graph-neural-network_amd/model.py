@@ -61,7 +61,8 @@ class _SplitKLinear(torch.autograd.Function):
         x, weight, out = ctx.saved_tensors
         gx = gw = gb = None
         g = g.contiguous()
-        if ctx.relu:  # ReLU fused into the forward: threshold_backward, one launch
+        from .functional import premasked
+        if ctx.relu and not premasked(g, out):  # ReLU fused into the forward: threshold_backward, one launch
             from . import _lib
             from .functional import _stream
             masked = torch.empty_like(out)
@@ -224,6 +225,47 @@ class _HeadLogSoftmax(torch.autograd.Function):
         return gx, gw if ctx.needs_input_grad[1] else None, gb if ctx.needs_input_grad[2] else None
 
 
+class _DropoutRelu(torch.autograd.Function):
+    """``F.dropout(x, p, training=True)`` of a ReLU output internal to MPNetm.forward (model.py:
+    211-215): the forward is torch's own fused dropout (``torch.native_dropout``: the kernel and
+    random stream F.dropout uses on the GPU), the backward ONE launch (mpgnn_dropout_relu_bwd:
+    dropout's masked scale with the ReLU backward of x's layer applied, which then skips its own
+    launch) instead of two."""
+
+    @staticmethod
+    def forward(ctx, x, p):
+        out, mask = torch.native_dropout(x, p, True)
+        ctx.scale = 1.0 / (1.0 - p)
+        ctx.x_src = weakref.ref(x)
+        ctx.save_for_backward(mask, x)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import _lib
+        from .functional import _mask_source, _stream, mark_premasked
+        mask, x = ctx.saved_tensors
+        g = g.contiguous()
+        src = _mask_source(ctx)
+        gx = torch.empty_like(g)
+        _lib.check(_lib.lib.mpgnn_dropout_relu_bwd(g.data_ptr(), mask.data_ptr(),
+                                                   x.data_ptr() if src is not None else None, ctx.scale, g.numel(),
+                                                   gx.data_ptr(), _stream(g)), "mpgnn_dropout_relu_bwd")
+        if src is not None:
+            mark_premasked(gx, src)
+        return gx, None
+
+
+def dropout_after_relu(module: torch.nn.Dropout, x: torch.Tensor, internal: bool) -> torch.Tensor:
+    """``module(x)`` for x = F.relu(conv(...)): _DropoutRelu when x is internal (training, CUDA,
+    0 < p < 1, contiguous fp32), else the module itself."""
+    if (internal and module.training and not module.inplace and 0.0 < module.p < 1.0 and x.is_cuda
+            and x.dtype == torch.float32 and x.is_contiguous() and x.numel() > 0):
+        x._mpgnn_relu_internal = True
+        return _DropoutRelu.apply(x, float(module.p))
+    return module(x)
+
+
 def head_log_softmax(layer: torch.nn.Linear, x: torch.Tensor) -> torch.Tensor:
     """``F.log_softmax(layer(x), dim=1)`` (Net's output, model.py:147-148): _HeadLogSoftmax for
     fp32 CUDA inputs with O <= 8, F <= 256 (F % 4 == 0, 16-byte aligned), else the two ops."""
@@ -345,6 +387,12 @@ class MPNetm(_FastTrainToggle, torch.nn.Module):
         self.dropout2 = nn.Dropout(0.6)
 
     def forward(self, x, edge_index, edge_type):
+        # the ReLU outputs (after each conv and fc1) are internal to this forward unless a module
+        # hook observes them: their ReLU backwards then fuse into the consumer's backward (the
+        # dropout's, the head's; functional.premasked)
+        internal = x.is_cuda and torch.is_grad_enabled() and _RELU_FUSE and not _hooked(
+            self.fc1, self.fc2, self.log_softmax, self.dropout, self.dropout2,
+            *(c for convs in self.layers_list for c in convs))
         embeddings = []
         for i in range(0, len(self.metapaths)):
             for layer_index in range(0, len(self.metapaths[i])):
@@ -353,14 +401,16 @@ class MPNetm(_FastTrainToggle, torch.nn.Module):
                 # F.relu(conv(...)) of model.py:211,214, fused into the layer's output kernel
                 if layer_index == 0:
                     h = conv(layer_index, rel, x, edge_index, edge_type, activation="relu")
-                    h = self.dropout(h)
+                    h = dropout_after_relu(self.dropout, h, internal)
                 else:
                     h = conv(layer_index, rel, h, edge_index, edge_type, activation="relu")
-                    h = self.dropout2(h)
+                    h = dropout_after_relu(self.dropout2, h, internal)
             embeddings.append(h)
         # torch.cat of ONE embedding (a single metapath) is a copy of it: skipped, same values
         concatenated_embedding = embeddings[0] if len(embeddings) == 1 else torch.cat(embeddings, dim=1)
         h = linear(self.fc1, concatenated_embedding, activation="relu")  # F.relu(fc1(.)), model.py:225
         if _hooked(self.fc2, self.log_softmax):
             return self.log_softmax(linear(self.fc2, h))
+        if internal:
+            h._mpgnn_relu_internal = True
         return head_log_softmax(self.fc2, h)  # self.log_softmax(self.fc2(h)), model.py:226-227

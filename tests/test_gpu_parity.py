@@ -1789,3 +1789,56 @@ def test_head_log_softmax_vs_torch(n, f, o, relu_in):
                             ("grad_weight", lin.weight.grad, w64.grad), ("grad_bias", lin.bias.grad, b64.grad)):
         err = normwise_err(got.double().cpu(), want.detach().cpu())
         assert err <= 1e-5, (what, err)
+
+
+@pytest.mark.gpu
+def test_mpnetm_dropout_relu_backward_fused_bit_identical(monkeypatch):
+    """MPNetm in training mode (Dropout(0.6) after each metapath layer's ReLU, model.py:211-215):
+    with the ReLU outputs internal, each dropout's backward and the ReLU backward of the layer
+    before it run as ONE launch (mpgnn_dropout_relu_bwd) and fc1's ReLU backward fuses into the
+    head's (no relu_bwd launch left); the forward draws the same dropout masks (torch's own
+    native_dropout, the kernel and random stream F.dropout uses) — every parameter gradient bit
+    for bit as MPGNN_RELU_FUSE=0 under the same seed; a forward hook turns it off."""
+    from mpgnn_amd import _lib
+    from mpgnn_amd import model as mdl
+    import mpgnn_amd.functional as fnl
+    g = data.synthetic_graph(3000, 4, 12, feat_dim=64, seed=9)
+    ei, et, x = g.edge_index.to(DEV), g.edge_type.to(DEV), g.x.to(DEV)
+    y = torch.randint(0, 2, (g.num_nodes,), generator=torch.Generator().manual_seed(1)).to(DEV)
+    torch.manual_seed(30)
+    net = mpgnn_amd.MPNetm(64, 128, 4, 128, 2, 1, [[3, 1, 0]]).to(DEV).train()
+    calls = {}
+    real = _lib.lib
+
+    class _Count:
+        def __getattr__(self, k):
+            f = getattr(real, k)
+
+            def wrapped(*a):
+                calls[k] = calls.get(k, 0) + 1
+                return f(*a)
+            return wrapped
+    monkeypatch.setattr(fnl, "lib", _Count())
+    monkeypatch.setattr(_lib, "lib", _Count())
+
+    def grads(fuse, hook=False):
+        monkeypatch.setattr(mdl, "_RELU_FUSE", fuse)
+        calls.clear()
+        net.zero_grad(set_to_none=True)
+        h = net.fc1.register_forward_hook(lambda *_: None) if hook else None
+        torch.manual_seed(123)  # the same dropout masks in every run
+        out = net(x, ei, et)
+        if h is not None:
+            h.remove()
+        torch.nn.functional.nll_loss(out, y).backward()
+        torch.cuda.synchronize()
+        return {k: p.grad.clone() for k, p in net.named_parameters()}, dict(calls)
+
+    ref, c_ref = grads(False)
+    got, c_got = grads(True)
+    hooked, c_hook = grads(True, hook=True)
+    assert c_ref.get("mpgnn_relu_bwd", 0) == 4 and c_hook.get("mpgnn_relu_bwd", 0) == 4, (c_ref, c_hook)
+    assert c_got.get("mpgnn_relu_bwd", 0) == 0 and c_got.get("mpgnn_dropout_relu_bwd", 0) == 3, c_got
+    for k in ref:
+        assert torch.equal(ref[k], got[k]), k
+        assert torch.equal(ref[k], hooked[k]), k
