@@ -540,6 +540,10 @@ enum mpgnn_option {
                                     launch (the means kernel's arithmetic: 32-edge pieces in order) instead of a
                                     separate means launch; 0 the two launches; outputs and saved means
                                     bit-identical */,
+    MPGNN_OPT_BWD_SIDE_REDUCE = 41 /* mpgnn_rgcn_bwd (not accumulating): 1 runs the weight gradient's outer
+                                    products first, then its ordered slab sum on a library side stream beside the
+                                    dgrad GEMM and grad_x, joined before the call returns; 0 (default) all in
+                                    stream order; gradients bit-identical */,
     MPGNN_OPT_ADAM_CONTRACT = 40 /* process-wide: mpgnn_adam_step's double multiply-adds fused (1, default: the
                                     contraction clang's default HIP flags give ATen's kernel) or each product
                                     rounded (0); pinned bit-for-bit against torch by the GPU tests */

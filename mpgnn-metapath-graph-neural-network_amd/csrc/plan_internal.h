@@ -35,6 +35,7 @@ struct Options {
     int flat_u = 16;              // MPGNN_OPT_FLAT_U: gather-sum rows in flight per wave
     bool flat_pad = true;         // MPGNN_OPT_FLAT_PAD: forward gather-sum chunks from padded slot tables
     bool single_fold = false;     // MPGNN_OPT_SINGLE_FOLD: mode-SINGLE means folded into single_bf3_kernel
+    bool side_reduce = false;     // MPGNN_OPT_BWD_SIDE_REDUCE: the weight gradient's slab sum on a side stream
     bool gemm_cu_pairs = true;    // MPGNN_OPT_GEMM_CU_PAIRS: GEMM item ranges balanced per CU
     int gemm_switch_cost = 250;   // MPGNN_OPT_GEMM_SWITCH_COST: percent of an item per weight switch
     int flat_wg_per_cu = 0;       // MPGNN_OPT_FLAT_WG_PER_CU: persistent grid of flat_rows_kernel (0: off)

@@ -7141,6 +7141,7 @@ static int32_t set_switch(Options& o, int32_t option, int64_t value) {
         case MPGNN_OPT_GEMM_W1: o.gemm_w1 = value != 0; return MPGNN_OK;
         case MPGNN_OPT_FLAT_PAD: o.flat_pad = value != 0; return MPGNN_OK;
         case MPGNN_OPT_SINGLE_FOLD: o.single_fold = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_BWD_SIDE_REDUCE: o.side_reduce = value != 0; return MPGNN_OK;
         case MPGNN_OPT_FLAT_U:
             if (value != 8 && value != 16 && value != 32) return arg_error("MPGNN_OPT_FLAT_U must be 8, 16 or 32");
             o.flat_u = (int)value;
@@ -7179,6 +7180,7 @@ static bool get_switch(const Options& o, int32_t option, int64_t* value) {
         case MPGNN_OPT_FLAT_U: *value = o.flat_u; return true;
         case MPGNN_OPT_FLAT_PAD: *value = o.flat_pad; return true;
         case MPGNN_OPT_SINGLE_FOLD: *value = o.single_fold; return true;
+        case MPGNN_OPT_BWD_SIDE_REDUCE: *value = o.side_reduce; return true;
         case MPGNN_OPT_GEMM_SWITCH_COST: *value = o.gemm_switch_cost; return true;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = o.flat_wg_per_cu; return true;
         default: return false;
@@ -7845,7 +7847,8 @@ int32_t mpgnn_rel_mean_bwd(const mpgnn_plan* p, int32_t mode, int64_t relation, 
 static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const float* x, int32_t F_in, int32_t F_out,
                           const float* h_save, const float* grad_out, float* grad_weight, float* grad_root,
                           float* grad_bias, const Selection& s, const WsLayout& w, const RootChunks& rc, char* ws,
-                          hipStream_t strm, bool acc);
+                          hipStream_t strm, bool acc, hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr,
+                          hipEvent_t ev_join = nullptr, bool* forked = nullptr);
 
 
 // The backward at F_in = F_out = 128 through bwd_bf3_kernel (dgrad + dW / droot / dbias in one
@@ -8015,6 +8018,41 @@ static int32_t bwd_fused(const mpgnn_plan* p, int32_t mode, int32_t R, const flo
     return st;
 }
 
+// A side stream of the current device for this host thread, with a fork / join event pair, made
+// once (outside captures: false there until made). Per thread, so concurrent callers never share
+// events.
+static bool side_stream(hipStream_t* side, hipEvent_t* ev_fork, hipEvent_t* ev_join, hipStream_t strm) {
+    struct Side {
+        hipStream_t s = nullptr;
+        hipEvent_t a = nullptr, b = nullptr;
+    };
+    thread_local std::array<Side, 64> sides{};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        (void)hipGetLastError();
+        return false;
+    }
+    Side& e = sides[dev];
+    if (e.s == nullptr) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(strm, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e.a, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.b, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            e = Side{};
+            return false;
+        }
+    }
+    *side = e.s;
+    *ev_fork = e.a;
+    *ev_join = e.b;
+    return true;
+}
+
 static int32_t rgcn_bwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation, int32_t R, const float* x,
                              int32_t F_in, const float* weight, const float* root, int32_t F_out,
                              const float* h_save, const float* grad_out, int64_t row_lo, int64_t row_hi,
@@ -8078,6 +8116,25 @@ static int32_t rgcn_bwd_impl(const mpgnn_plan* p, int32_t mode, int64_t relation
     };
     // (the two halves on two streams — parameter gradients on a side stream forked from and
     // joined into the caller's — measured slower: C3 epoch 1.163 -> 1.207 ms; not kept)
+    // MPGNN_OPT_BWD_SIDE_REDUCE: the weight gradient's outer products first, then its ordered
+    // slab sum (HBM-bound, ~40 VGPRs) on a side stream beside the dgrad GEMM (MFMA-bound, 464 of a
+    // SIMD's 512 VGPRs) and grad_x, joined before this call returns
+    if (o.side_reduce && want_x && want_p && !acc) {
+        hipStream_t side = nullptr;
+        hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+        if (side_stream(&side, &ev_fork, &ev_join, strm)) {
+            bool forked = false;
+            st = bwd_params(p, mode, R, x, F_in, F_out, h_save, grad_out, grad_weight, grad_root, grad_bias, s, w, rc, ws,
+                            strm, acc, side, ev_fork, ev_join, &forked);
+            if (st != MPGNN_OK) return st;
+            st = grad_x_part(strm);
+            if (forked) {
+                const int32_t sj = hip_check(hipStreamWaitEvent(strm, ev_join, 0), "join side reduce");
+                if (st == MPGNN_OK) st = sj;
+            }
+            return st;
+        }
+    }
     if (want_x && (st = grad_x_part(strm)) != MPGNN_OK) return st;
     if (want_p) st = bwd_params(p, mode, R, x, F_in, F_out, h_save, grad_out, grad_weight, grad_root, grad_bias, s, w,
                                 rc, ws, strm, acc);
@@ -8116,8 +8173,10 @@ int32_t mpgnn_rgcn_bwd_relu_in(const mpgnn_plan* p, int32_t mode, int64_t relati
 static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const float* x, int32_t F_in, int32_t F_out,
                           const float* h_save, const float* grad_out, float* grad_weight, float* grad_root,
                           float* grad_bias, const Selection& s, const WsLayout& w, const RootChunks& rc, char* ws,
-                          hipStream_t strm, bool acc) {
+                          hipStream_t strm, bool acc, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join,
+                          bool* forked) {
     int32_t st = MPGNN_OK;
+    if (forked != nullptr) *forked = false;
     const size_t wsize = (size_t)F_in * F_out;
     const bool exact = p->opt.exact_order;
     const int mt = (F_in + kColTile - 1) / kColTile;
@@ -8347,10 +8406,24 @@ static int32_t bwd_params(const mpgnn_plan* p, int32_t mode, int32_t R, const fl
             gx[k] = reduces[k].gx;
             ey = std::max(ey, reduces[k].ey);
         }
-        TimedLaunch tl(MPGNN_K_REDUCE, strm);
-        hipLaunchKernelGGL(reduce_slabs3_kernel, dim3(gx[0] + gx[1] + gx[2] + zl.n, ey), dim3(kThreads), 0, strm, r3[0],
-                           r3[1], r3[2], gx[0], gx[1], gx[2], zl);
-        return hip_check(hipGetLastError(), "reduce_slabs3_kernel launch");
+        // MPGNN_OPT_BWD_SIDE_REDUCE: the ordered slab sum on a side stream forked here (the caller
+        // runs grad_x's launches meanwhile and joins on ev_join)
+        hipStream_t rs = strm;
+        if (side != nullptr && ev_fork != nullptr && ev_join != nullptr &&
+            hipEventRecord(ev_fork, strm) == hipSuccess && hipStreamWaitEvent(side, ev_fork, 0) == hipSuccess)
+            rs = side;
+        (void)hipGetLastError();
+        {
+            TimedLaunch tl(MPGNN_K_REDUCE, rs);
+            hipLaunchKernelGGL(reduce_slabs3_kernel, dim3(gx[0] + gx[1] + gx[2] + zl.n, ey), dim3(kThreads), 0, rs,
+                               r3[0], r3[1], r3[2], gx[0], gx[1], gx[2], zl);
+            if ((st = hip_check(hipGetLastError(), "reduce_slabs3_kernel launch")) != MPGNN_OK) return st;
+        }
+        if (rs != strm) {
+            if ((st = hip_check(hipEventRecord(ev_join, rs), "side reduce event")) != MPGNN_OK) return st;
+            if (forked != nullptr) *forked = true;
+        }
+        return MPGNN_OK;
     }
 }
 

@@ -828,8 +828,9 @@ def test_k256_gemm_interleaved_commit_bit_identical(mode):
     assert res[0][0].abs().sum() > 0
 
 
-@pytest.mark.parametrize("opt,val", [(35, 1), (36, 1), (36, 2), (37, 32), (37, 8), (38, 1)])
-def test_w1_gemm_and_outer_variants_bit_identical(opt, val):
+@pytest.mark.parametrize("opt,val,graph", [(35, 1, "syn"), (36, 1, "syn"), (36, 2, "syn"), (37, 32, "syn"),
+                                           (37, 8, "syn"), (38, 1, "syn"), (41, 1, "syn"), (41, 1, "fb15k237")])
+def test_w1_gemm_and_outer_variants_bit_identical(opt, val, graph):
     """Round 6 variants, off by default, against the product kernels on one layer (forward, dgrad,
     every gradient) — bit for bit:
       35 MPGNN_OPT_GEMM_W1: rel_gemm_w1_kernel (one workgroup per CU, 64-row items: tile pairs of
@@ -840,9 +841,11 @@ def test_w1_gemm_and_outer_variants_bit_identical(opt, val):
       37 MPGNN_OPT_FLAT_U: the gather-sum kernels with 32 / 8 rows in flight per wave (means,
          combine, grad_x) vs 16;
       38 MPGNN_OPT_FLAT_PAD: their chunks fetched from the padded per-slot tables vs the scalar
-         chunk-range hops.
-    A graph with relations of 1, odd and even 32-row tile counts and N % 64 != 0."""
-    g = data.synthetic_graph(5003, 9, 12, feat_dim=128, seed=37)
+         chunk-range hops;
+      41 MPGNN_OPT_BWD_SIDE_REDUCE: the weight gradient's slab sum on a side stream beside dgrad and
+         grad_x (C3 takes that path: more items than the one-launch backward's four per CU).
+    A graph with relations of 1, odd and even 32-row tile counts and N % 64 != 0, and C3."""
+    g = data.synthetic_graph(5003, 9, 12, feat_dim=128, seed=37) if graph == "syn" else data.config_graph(graph)
     N, R = g.num_nodes, g.num_relations
     gen = torch.Generator().manual_seed(opt + val)
     W = (torch.rand((R, 128, 128), generator=gen) - 0.5) * 0.1
