@@ -544,6 +544,11 @@ enum mpgnn_option {
                                     products first, then its ordered slab sum on a library side stream beside the
                                     dgrad GEMM and grad_x, joined before the call returns; 0 (default) all in
                                     stream order; gradients bit-identical */,
+    MPGNN_OPT_GEMM_FIRST = 42    /* the bf16-split GEMM at K = 128, mode ALL: 1 (default) reads each workgroup's
+                                    range and its first three items' gathered row numbers from a per-range record
+                                    built once per plan (one round trip, not range -> tiles -> row-index hops; C3
+                                    forward GEMM 45.1-45.2 -> 44.75-44.9 us, alternated 3x); 0 the hops; outputs
+                                    bit-identical */,
     MPGNN_OPT_ADAM_CONTRACT = 40 /* process-wide: mpgnn_adam_step's double multiply-adds fused (1, default: the
                                     contraction clang's default HIP flags give ATen's kernel) or each product
                                     rounded (0); pinned bit-for-bit against torch by the GPU tests */

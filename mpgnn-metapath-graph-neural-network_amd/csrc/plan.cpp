@@ -719,7 +719,7 @@ int32_t mpgnn_plan_destroy(mpgnn_plan* p) {
         free_device_plan(p);
         if (p->d.rel_node_map) (void)hipFree(p->d.rel_node_map);
         for (auto& kv : p->bw_slabs) (void)hipFree(kv.second.dev);
-        for (auto* m : {&p->gemm_ranges, &p->outer_ranges, &p->flat_pads})
+        for (auto* m : {&p->gemm_ranges, &p->outer_ranges, &p->flat_pads, &p->gemm_first})
             for (auto& kv : *m) {
                 (void)hipFree(kv.second.dev);
                 (void)hipHostFree(kv.second.host);

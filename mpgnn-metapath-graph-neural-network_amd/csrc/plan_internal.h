@@ -36,6 +36,7 @@ struct Options {
     bool flat_pad = true;         // MPGNN_OPT_FLAT_PAD: forward gather-sum chunks from padded slot tables
     bool single_fold = false;     // MPGNN_OPT_SINGLE_FOLD: mode-SINGLE means folded into single_bf3_kernel
     bool side_reduce = false;     // MPGNN_OPT_BWD_SIDE_REDUCE: the weight gradient's slab sum on a side stream
+    bool gemm_first = true;       // MPGNN_OPT_GEMM_FIRST: the bf16-split GEMM's prologue from per-range records
     bool gemm_cu_pairs = true;    // MPGNN_OPT_GEMM_CU_PAIRS: GEMM item ranges balanced per CU
     int gemm_switch_cost = 250;   // MPGNN_OPT_GEMM_SWITCH_COST: percent of an item per weight switch
     int flat_wg_per_cu = 0;       // MPGNN_OPT_FLAT_WG_PER_CU: persistent grid of flat_rows_kernel (0: off)
@@ -261,6 +262,8 @@ struct mpgnn_plan {
         int* host = nullptr;  // pinned
     };
     mutable std::map<std::array<int64_t, 5>, GemmRanges> gemm_ranges;
+    // rel_gemm_bf3_kernel's per-range prologue records (RelGemmArgs::first; device only)
+    mutable std::map<std::array<int64_t, 5>, GemmRanges> gemm_first;
     // outer_bf3v_kernel_t's per-workgroup chunk ranges (same ownership as gemm_ranges)
     mutable std::map<std::array<int64_t, 5>, GemmRanges> outer_ranges;
     // flat_rows_kernel's padded slot tables per (list, value table) (rgcn_kernels.hip

@@ -1028,6 +1028,8 @@ __device__ __forceinline__ void tile_gemm_body(const TileGemmArgs& a, float* sme
 // Output rows leave straight from the accumulators: each accumulator register is two 128-B
 // row segments (C/D layout: col = lane & 31, row = (r & 3) + 8(r >> 2) + 4(lane >> 5)).
 // ----------------------------------------------------------------------------------------
+constexpr int kFirstRec = 8 + 6 * 32;  // ints per item range of RelGemmArgs::first
+
 struct RelGemmArgs {
     const int* t_begin;   // 32-row relation tiles (segments)
     const int* t_end;
@@ -1058,6 +1060,12 @@ struct RelGemmArgs {
     int wg_cus;           // > 0 with wg_items: G = 2·wg_cus, ranges 2c and 2c+1 belong to one CU (below)
     unsigned* zero;       // nullable (rel_gemm_bf3_kernel): zero_words words zeroed by the launch — the
     int zero_words;       // next gather-sum's piece counters (dgrad -> grad_x), instead of a memset launch
+    // nullable (rel_gemm_bf3_kernel, K = 128, MPGNN_OPT_GEMM_FIRST): per item range (kFirstRec ints)
+    // {i_beg, i_end, weight index of item i_beg (-1 root), its r0, its nrows, 0, 0, 0, then the
+    // gathered row numbers of items i_beg .. i_beg + 2 (clamped to the range) [3][32] and their
+    // dgrad counts [3][32]}: the prologue reads them in one round instead of range -> tiles ->
+    // s_src / s_row hops
+    const int* first;
 #ifdef MPGNN_STAMPS
     unsigned long long* stamps;
 #endif
@@ -1749,8 +1757,9 @@ struct RelGemmBf3 {
         const int G = (int)gridDim.x;
         const int g = (int)blockIdx.x & 7, q = G >> 3, rem = G & 7;
         const int rng = a.wg_cus > 0 ? wg_pair_range((int)blockIdx.x, a.wg_cus) : g * q + min(g, rem) + ((int)blockIdx.x >> 3);
-        const int i_beg = a.wg_items ? ld_uniform(a.wg_items, rng) : (int)((long long)rng * n_items / G);
-        const int i_end = a.wg_items ? ld_uniform(a.wg_items, rng + 1) : (int)((long long)(rng + 1) * n_items / G);
+        const int* rec = a.first != nullptr ? a.first + (size_t)rng * kFirstRec : nullptr;
+        const int i_beg = rec ? ld_uniform(rec, 0) : a.wg_items ? ld_uniform(a.wg_items, rng) : (int)((long long)rng * n_items / G);
+        const int i_end = rec ? ld_uniform(rec, 1) : a.wg_items ? ld_uniform(a.wg_items, rng + 1) : (int)((long long)(rng + 1) * n_items / G);
         if (i_beg >= i_end) return;
         stamp_id();
 
@@ -1773,16 +1782,36 @@ struct RelGemmBf3 {
             }
         }
         auto get_item = [&](int i) { return i - i_beg < 64 ? Base::item_at(a, tab, i - i_beg) : Base::item(a, i); };
-        Item cur = get_item(i_beg);
+        Item cur;
         float4 va[WPT], vb[WPT];
         int cnta = 1, cntb = 1, zm = 0;
         int nrow[WPT];
         int ncnt = 1;
         int crow[WPT], c0;
         int r1[WPT];
-        Base::gather_idx(a, cur, tid, crow, c0);
-        Base::gather_idx(a, get_item(min(i_beg + 1, i_end - 1)), tid, r1, cnta);
-        Base::gather_idx(a, get_item(min(i_beg + 2, i_end - 1)), tid, nrow, ncnt);
+        if (rec != nullptr) {  // the first three items' row numbers from the range's record (one round)
+            const int wr = ld_uniform(rec, 2);
+            cur.r0 = ld_uniform(rec, 3);
+            cur.nrows = ld_uniform(rec, 4);
+            cur.root = wr < 0;
+            cur.w = cur.root ? a.Wroot : a.W + (size_t)wr * K * N;
+            constexpr int W4 = K / 4;
+#pragma unroll
+            for (int j = 0; j < WPT; ++j) {
+                const int q = (tid + j * kThreads) / W4;
+                crow[j] = rec[8 + q];
+                r1[j] = rec[8 + 32 + q];
+                nrow[j] = rec[8 + 64 + q];
+            }
+            c0 = DGRAD ? rec[8 + 96 + (tid & 31)] : 1;
+            cnta = DGRAD ? rec[8 + 128 + (tid & 31)] : 1;
+            ncnt = DGRAD ? rec[8 + 160 + (tid & 31)] : 1;
+        } else {
+            cur = get_item(i_beg);
+            Base::gather_idx(a, cur, tid, crow, c0);
+            Base::gather_idx(a, get_item(min(i_beg + 1, i_end - 1)), tid, r1, cnta);
+            Base::gather_idx(a, get_item(min(i_beg + 2, i_end - 1)), tid, nrow, ncnt);
+        }
         float wf[NS][8];
         load_b_raw(cur.w, wave, lane, wf);
         Base::issue_rows(a, tid, crow, vb, zm);
@@ -5742,6 +5771,80 @@ static void launch_rel_gemm_bf3w(const RelGemmArgs& a, bool il, hipStream_t st) 
 // dependent s_rel load. Cached per plan; made outside captures (nullptr: the kernel's equal split
 // and s_rel lookups). Uploaded on the caller's stream from a pinned buffer the plan keeps and
 // published in the cache only after that stream has drained the copy (once per key).
+// RelGemmArgs::first from the item ranges: one workgroup per range, thread t < 96 the row number
+// of item k = t / 32 (clamped to the range), position q = t % 32 — gather_idx's values — thread
+// 96 + t its dgrad count
+__global__ __launch_bounds__(kThreads) void gemm_first_kernel(const int* __restrict__ ranges, int G, int n_rel,
+                                                              int t_lo, const int* __restrict__ t_begin,
+                                                              const int* __restrict__ t_end,
+                                                              const int* __restrict__ map, const int* __restrict__ cnt,
+                                                              int row_lo, int row_hi, int* __restrict__ rec) {
+    const int rng = (int)blockIdx.x, t = threadIdx.x;
+    const int i_beg = ranges[rng], i_end = ranges[rng + 1];
+    int* r = rec + (size_t)rng * kFirstRec;
+    if (i_beg >= i_end) {
+        if (t == 0) r[0] = r[1] = i_beg;
+        return;
+    }
+    auto tile = [&](int i, int& r0, int& nrows) {
+        if (i < n_rel) {
+            r0 = t_begin[t_lo + i];
+            nrows = t_end[t_lo + i] - r0;
+        } else {
+            r0 = row_lo + (i - n_rel) * 32;
+            nrows = min(32, row_hi - r0);
+        }
+    };
+    if (t == 0) {
+        int r0, nrows;
+        tile(i_beg, r0, nrows);
+        r[0] = i_beg;
+        r[1] = i_end;
+        r[2] = i_beg < n_rel ? ranges[G + 1 + i_beg] : -1;
+        r[3] = r0;
+        r[4] = nrows;
+        r[5] = r[6] = r[7] = 0;
+    }
+    if (t < 192) {
+        const int k = (t % 96) / 32, q = t % 32;
+        const int i = min(i_beg + k, i_end - 1);
+        int r0, nrows;
+        tile(i, r0, nrows);
+        const int row = r0 + min(q, nrows - 1);
+        if (t < 96) r[8 + t] = i < n_rel ? map[row] : row;
+        else r[8 + t] = (i < n_rel && cnt != nullptr) ? cnt[row] : 1;
+    }
+}
+
+static const int* gemm_ranges(const mpgnn_plan* p, int t_lo, int n_rel, int n_root, int G, bool pairs,
+                              hipStream_t st);
+
+// Cached per plan, ranges table and direction (made outside captures; nullptr: the kernel's hops)
+static const int* gemm_first(const mpgnn_plan* p, const int* ranges, int G, const RelGemmArgs& r, bool dgrad,
+                             hipStream_t st) {
+    if (ranges == nullptr || G <= 0) return nullptr;
+    const std::array<int64_t, 5> key{(int64_t)(intptr_t)ranges, G, dgrad ? 1 : 0, r.row_lo, r.row_hi};
+    std::lock_guard<std::mutex> lk(p->bw_mu);
+    auto it = p->gemm_first.find(key);
+    if (it != p->gemm_first.end()) return it->second.dev;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    mpgnn_plan::GemmRanges e;
+    if (hipMalloc(reinterpret_cast<void**>(&e.dev), (size_t)G * kFirstRec * sizeof(int)) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    hipLaunchKernelGGL(gemm_first_kernel, dim3(G), dim3(kThreads), 0, st, ranges, G, r.n_rel, r.t_lo, r.t_begin,
+                       r.t_end, dgrad ? r.s_row : r.s_src, dgrad ? r.s_cnt : nullptr, r.row_lo, r.row_hi, e.dev);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {  // published once complete
+        (void)hipGetLastError();
+        (void)hipFree(e.dev);
+        return nullptr;
+    }
+    p->gemm_first[key] = e;
+    return e.dev;
+}
+
 static const int* gemm_ranges(const mpgnn_plan* p, int t_lo, int n_rel, int n_root, int G, bool pairs,
                               hipStream_t st) {
     const int cost = p->opt.gemm_switch_cost;
@@ -6243,6 +6346,8 @@ static int32_t run_seg(const mpgnn_plan* p, int32_t mode, const Selection& s, in
             const bool pairs = p->opt.gemm_cu_pairs && G == cu_count() * 2 && cu_count() % 8 == 0;
             r.wg_items = gemm_ranges(p, r.t_lo, r.n_rel, r.n_root, G, pairs, strm);
             r.wg_cus = (pairs && r.wg_items != nullptr) ? cu_count() : 0;
+            if (p->opt.gemm_first && K == 128 && p->opt.gemm_il && r.wg_items != nullptr && r.w_per_rel)
+                r.first = gemm_first(p, r.wg_items, G, r, gather_kind == 1, strm);
         }
         if (zero != nullptr && zero_words > 0 && p->opt.gemm_bf3 && (K == 64 || K == 128) && r.node_map == nullptr) {
             r.zero = zero;  // launch_rel_gemm takes rel_gemm_bf3_kernel for these shapes
@@ -7142,6 +7247,7 @@ static int32_t set_switch(Options& o, int32_t option, int64_t value) {
         case MPGNN_OPT_FLAT_PAD: o.flat_pad = value != 0; return MPGNN_OK;
         case MPGNN_OPT_SINGLE_FOLD: o.single_fold = value != 0; return MPGNN_OK;
         case MPGNN_OPT_BWD_SIDE_REDUCE: o.side_reduce = value != 0; return MPGNN_OK;
+        case MPGNN_OPT_GEMM_FIRST: o.gemm_first = value != 0; return MPGNN_OK;
         case MPGNN_OPT_FLAT_U:
             if (value != 8 && value != 16 && value != 32) return arg_error("MPGNN_OPT_FLAT_U must be 8, 16 or 32");
             o.flat_u = (int)value;
@@ -7181,6 +7287,7 @@ static bool get_switch(const Options& o, int32_t option, int64_t* value) {
         case MPGNN_OPT_FLAT_PAD: *value = o.flat_pad; return true;
         case MPGNN_OPT_SINGLE_FOLD: *value = o.single_fold; return true;
         case MPGNN_OPT_BWD_SIDE_REDUCE: *value = o.side_reduce; return true;
+        case MPGNN_OPT_GEMM_FIRST: *value = o.gemm_first; return true;
         case MPGNN_OPT_GEMM_SWITCH_COST: *value = o.gemm_switch_cost; return true;
         case MPGNN_OPT_FLAT_WG_PER_CU: *value = o.flat_wg_per_cu; return true;
         default: return false;

@@ -829,7 +829,8 @@ def test_k256_gemm_interleaved_commit_bit_identical(mode):
 
 
 @pytest.mark.parametrize("opt,val,graph", [(35, 1, "syn"), (36, 1, "syn"), (36, 2, "syn"), (37, 32, "syn"),
-                                           (37, 8, "syn"), (38, 1, "syn"), (41, 1, "syn"), (41, 1, "fb15k237")])
+                                           (37, 8, "syn"), (38, 1, "syn"), (41, 1, "syn"), (41, 1, "fb15k237"),
+                                           (42, 0, "syn"), (42, 0, "fb15k237")])
 def test_w1_gemm_and_outer_variants_bit_identical(opt, val, graph):
     """Round 6 variants, off by default, against the product kernels on one layer (forward, dgrad,
     every gradient) — bit for bit:
@@ -843,7 +844,9 @@ def test_w1_gemm_and_outer_variants_bit_identical(opt, val, graph):
       38 MPGNN_OPT_FLAT_PAD: their chunks fetched from the padded per-slot tables vs the scalar
          chunk-range hops;
       41 MPGNN_OPT_BWD_SIDE_REDUCE: the weight gradient's slab sum on a side stream beside dgrad and
-         grad_x (C3 takes that path: more items than the one-launch backward's four per CU).
+         grad_x (C3 takes that path: more items than the one-launch backward's four per CU);
+      42 MPGNN_OPT_GEMM_FIRST (on by default; the test turns it off): the GEMM prologue's range and
+         first rows from per-range records vs the range -> tiles -> row-index hops.
     A graph with relations of 1, odd and even 32-row tile counts and N % 64 != 0, and C3."""
     g = data.synthetic_graph(5003, 9, 12, feat_dim=128, seed=37) if graph == "syn" else data.config_graph(graph)
     N, R = g.num_nodes, g.num_relations
