@@ -158,3 +158,39 @@ def test_product_path_fails_loudly_on_cpu_tensors():
     c2 = mpgnn_amd.CustomRGCNConv(128, 64, 1, flow="target_to_source")
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         c2(0, 1, g.x, g.edge_index, g.edge_type)
+
+
+def test_round6_entry_points_check_arguments_before_launching():
+    """The round-6 entry points refuse bad arguments and unsupported shapes before any launch
+    (host-side checks only: callable without a GPU)."""
+    from mpgnn_amd import _lib
+    from mpgnn_amd._lib import lib
+    # mpgnn_adam_step: at most 24 tensors, 16-byte aligned pointers, n >= 0, NULL arrays refused
+    arr = (_lib.AdamTensor * 25)()
+    assert lib.mpgnn_adam_step(arr, 25, 0.01, 0.9, 0.999, 5e-4, 1e-8, ctypes.c_void_p(64), None) == \
+        _lib.MPGNN_ERR_UNSUPPORTED
+    assert lib.mpgnn_adam_step(arr, -1, 0.01, 0.9, 0.999, 5e-4, 1e-8, ctypes.c_void_p(64), None) == _lib.MPGNN_ERR_ARG
+    assert lib.mpgnn_adam_step(None, 1, 0.01, 0.9, 0.999, 5e-4, 1e-8, ctypes.c_void_p(64), None) == _lib.MPGNN_ERR_ARG
+    assert lib.mpgnn_adam_step(arr, 0, 0.01, 0.9, 0.999, 5e-4, 1e-8, None, None) == _lib.MPGNN_OK
+    one = (_lib.AdamTensor * 1)()
+    one[0].param, one[0].grad, one[0].exp_avg, one[0].exp_avg_sq, one[0].step = 4096 + 4, 4096, 4096, 4096, 4096
+    one[0].numel = 8
+    assert lib.mpgnn_adam_step(one, 1, 0.01, 0.9, 0.999, 5e-4, 1e-8, ctypes.c_void_p(64), None) == \
+        _lib.MPGNN_ERR_UNSUPPORTED  # a misaligned parameter: nothing launched
+    # the fused log-softmax head: O <= 8, F <= 256, F % 4 == 0
+    nb = ctypes.c_int64()
+    assert lib.mpgnn_linear_logsoftmax_bwd_workspace_bytes(100, 128, 9, ctypes.byref(nb)) == _lib.MPGNN_ERR_UNSUPPORTED
+    assert lib.mpgnn_linear_logsoftmax_bwd_workspace_bytes(100, 260, 2, ctypes.byref(nb)) == _lib.MPGNN_ERR_UNSUPPORTED
+    assert lib.mpgnn_linear_logsoftmax_bwd_workspace_bytes(100, 126, 2, ctypes.byref(nb)) == _lib.MPGNN_ERR_UNSUPPORTED
+    assert lib.mpgnn_linear_logsoftmax_bwd_workspace_bytes(100, 128, 2, ctypes.byref(nb)) == _lib.MPGNN_OK
+    assert nb.value == 4 * 2 * 129 * 4  # 4 row slices of 32 rows, [O][F + 1] floats each
+    # empty inputs are no-ops; negative sizes refused
+    assert lib.mpgnn_dropout_relu_bwd(None, None, None, ctypes.c_float(2.5), 0, None, None) == _lib.MPGNN_OK
+    assert lib.mpgnn_dropout_relu_bwd(None, None, None, ctypes.c_float(2.5), -1, None, None) == _lib.MPGNN_ERR_ARG
+    assert lib.mpgnn_nll_rows_bwd_dense(None, None, 0, 2, None, None, None, -100, None, None, None) == _lib.MPGNN_OK
+    assert lib.mpgnn_nll_rows_fwd_weighted(None, 10, 2, None, None, -1, -100, None, None, None, None) == \
+        _lib.MPGNN_ERR_ARG
+    # the process-wide contraction switch round-trips and refuses other values
+    v = ctypes.c_int64()
+    assert lib.mpgnn_get_option(_lib.OPT_ADAM_CONTRACT, ctypes.byref(v)) == _lib.MPGNN_OK and v.value == 1
+    assert lib.mpgnn_set_option(_lib.OPT_ADAM_CONTRACT, 2) == _lib.MPGNN_ERR_ARG
