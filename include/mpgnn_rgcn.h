@@ -500,8 +500,9 @@ enum mpgnn_option {
                                     (outer_bf3v_kernel); 0: 4-B column gathers (outer_bf3_kernel) */
     MPGNN_OPT_GEMM_SWITCH_COST = 29 /* the bf16-split GEMM's workgroup item ranges (K = 64, 128): 0 = equal item
                                     counts; c > 0 = ranges balanced by items + (c / 100) per weight run, each
-                                    run paying an exposed weight-slice load (default 250: the round-5 A/B with
-                                    per-CU ranges, forward 47.4 -> 45.3 us against 85; outputs bit-identical) */,
+                                    run paying an exposed weight-slice load (default 150: the round-6 re-sweep
+                                    with the prologue records, C3 forward 43.1-43.3 us at 120-150 against
+                                    44.0-44.4 at 250, 45.7 at 400; round 5 chose 250; outputs bit-identical) */,
     MPGNN_OPT_GEMM_IL = 30       /* 1 (default): the bf16-split GEMM (K = 64, 128) commits the next item's tile in
                                     parts scheduled among the MFMAs of the current item's k-steps; 0: the
                                     round-4 skeleton (whole tile in one k-step); outputs bit-identical */,

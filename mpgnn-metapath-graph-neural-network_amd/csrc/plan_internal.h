@@ -38,7 +38,7 @@ struct Options {
     bool side_reduce = false;     // MPGNN_OPT_BWD_SIDE_REDUCE: the weight gradient's slab sum on a side stream
     bool gemm_first = true;       // MPGNN_OPT_GEMM_FIRST: the bf16-split GEMM's prologue from per-range records
     bool gemm_cu_pairs = true;    // MPGNN_OPT_GEMM_CU_PAIRS: GEMM item ranges balanced per CU
-    int gemm_switch_cost = 250;   // MPGNN_OPT_GEMM_SWITCH_COST: percent of an item per weight switch
+    int gemm_switch_cost = 150;  // MPGNN_OPT_GEMM_SWITCH_COST: range balance, items + c/100 per weight run (round 6 re-sweep)
     int flat_wg_per_cu = 0;       // MPGNN_OPT_FLAT_WG_PER_CU: persistent grid of flat_rows_kernel (0: off)
 };
 // a copy of the process defaults (rgcn_kernels.hip)

@@ -91,11 +91,12 @@ def test_round4_switches_default_on_and_round_trip():
     """The round-4 / round-5 A/B switches (header enum mpgnn_option): the shipped values are the measured
     winners — hub rows finished in the gather launch (27), the 16-B-gather weight gradient (28),
     one workgroup per gather-list group (26 = 0), GEMM item ranges balanced with a weight switch
-    priced at 2.5 items (29 = 250), the interleaved GEMM item skeleton (30) and per-CU item ranges (31)
+    priced at 1.5 items (29 = 150: re-swept in round 6 with the prologue records; 250 before), the
+    interleaved GEMM item skeleton (30) and per-CU item ranges (31)
     — and each round-trips through set / get."""
     from mpgnn_amd import _lib
     lib = _lib.lib
-    shipped = {26: 0, 27: 1, 28: 1, 29: 250, 30: 1, 31: 1, 32: 0, 33: 1, 34: 1}
+    shipped = {26: 0, 27: 1, 28: 1, 29: 150, 30: 1, 31: 1, 32: 0, 33: 1, 34: 1}
     for opt, v in shipped.items():
         assert _lib.get_option(opt) == v, (opt, _lib.get_option(opt))
     try:
