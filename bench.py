@@ -1029,7 +1029,7 @@ def main():
                     "algorithmic": dom["algorithmic"],
                     "note": "dominant kernel of the forward layer by the per-kernel HIP-event pass (events on the "
                             "launch stream, one pair per launch; the headline timed region has none); traffic = "
-                            "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/r05_pmc_traffic.json; older rounds for kernels not re-profiled)"}
+                            "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/r06_pmc_traffic.json; older rounds for kernels not re-profiled)"}
         # SURVEY 8d whole-step HBM roofline of the aggregation (kept beside the kernel roofline)
     b_edge = 4 * F + 4
     hbm_roofline = {"bound": "hbm", "bytes_per_edge": b_edge,
